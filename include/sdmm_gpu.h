@@ -1,0 +1,175 @@
+/*
+ * sdmm_gpu.h -- C ABI of the MI355X-native SDMM path-guiding hot path.
+ *
+ * This is the drop-in boundary the Mitsuba `sdmm` integrator plugin calls in
+ * place of the (absent) sdmm-lib submodule.  Every entry point names the
+ * reference interface it replaces (paths relative to anadodik/sdmm-mitsuba):
+ *
+ *   sdmm_create / sdmm_destroy    SDMMContext construction
+ *                                 (mitsuba/src/integrators/sdmm/sdmm_proc.h:92-93)
+ *   sdmm_init_hemisphere          sdmm::initialize  (volpath_sdmm.cpp:132-138);
+ *                                 math: jmm uniformHemisphereInit
+ *                                 (dmm/jmm/mixture_model_init.h:79-242)
+ *   sdmm_em_step                  sdmm::em_step     (volpath_sdmm.cpp:220, :304)
+ *                                 + sdmm::prepare   (volpath_sdmm.cpp:237, :307);
+ *                                 math: jmm StepwiseTangentEM::optimize
+ *                                 (dmm/jmm/opt/stepwise_tangent.h:597-1053)
+ *   sdmm_estep_stats/sdmm_mstep   the same EM step split around the
+ *                                 sufficient-statistics all-reduce (multi-GPU)
+ *   sdmm_responsibilities         MixtureModel::posteriorAndLog over a batch
+ *                                 (dmm/jmm/mixture_model.h:146-192)
+ *   sdmm_guide_batch              sdmm::create_conditional + conditional.sample
+ *                                 + posterior/hsum_nested (sdmm_proc.cpp:368,
+ *                                 :411-421, :539-545); math: jmm
+ *                                 MixtureModel::conditional/sample/pdf
+ *                                 (mixture_model.h:235-304, :72-75, :113-121)
+ *   sdmm_pdf_batch                pdfSurface's gmmPdf (sdmm_proc.cpp:510-590)
+ *   sdmm_get_params/set_params    sdmm::save_json / load_json
+ *                                 (volpath_sdmm.cpp:121-130; bsdfs/diffuse.cpp:101-114)
+ *
+ * Conventions: plain C types only; every function returns SDMM_OK (0) or a
+ * negative SDMM_E* code and sets a thread-local message (sdmm_last_error).
+ * No C++ exception crosses the ABI.  Pointers documented "device" must be
+ * HBM-resident allocations on the handle's device; "host" pointers are
+ * ordinary memory, read-only during the call.  A handle is re-entrant
+ * against other handles; calls on one handle must be serialised by the
+ * caller.  Work is enqueued on the handle's HIP stream (sdmm_set_stream);
+ * functions that return data to host memory synchronise that stream.
+ */
+#ifndef SDMM_GPU_H
+#define SDMM_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDMM_ABI_VERSION 1
+
+enum {
+    SDMM_OK = 0,
+    SDMM_E_INVALID = -1,   /* bad argument / unsupported K */
+    SDMM_E_HIP = -2,       /* HIP runtime error */
+    SDMM_E_STATE = -3,     /* handle not initialised */
+    SDMM_E_NOMEM = -4
+};
+
+typedef struct sdmm_mix sdmm_mix;
+
+/* StepwiseTangentEM constructor arguments (stepwise_tangent.h:221-252). */
+typedef struct {
+    float alpha;              /* 0.9   stepwise exponent */
+    float bprior[5];          /* 1e-5  diagonal covariance prior (overwritten by init) */
+    float ni_prior_minus_one; /* 6e-5  weight prior */
+    double epsilon;           /* 1e-100 depth-prior diagonal (as float: 0) */
+    int decrease_prior;       /* 1 */
+} sdmm_em_params;
+
+/* SoA sample batch, one plane per field (Samples<6,float>, samples.h:32-46). */
+typedef struct {
+    const float* x[6];          /* normalised position (3) + unit direction (3) */
+    const float* w;             /* weight */
+    const float* hpdf;          /* heuristic pdf, may be NULL */
+    const uint8_t* is_diffuse;  /* heuristic flag, may be NULL */
+    int64_t n;
+} sdmm_samples;
+
+/* Fill p with the reference defaults. */
+void sdmm_em_params_default(sdmm_em_params* p);
+
+/* Create a K-component mixture (1 <= K <= 512) on HIP device `device`. */
+int sdmm_create(int K, const sdmm_em_params* params, int device, sdmm_mix** out);
+void sdmm_destroy(sdmm_mix* m);
+int sdmm_num_components(const sdmm_mix* m);
+int sdmm_set_stream(sdmm_mix* m, void* hip_stream);   /* NULL: the handle's own stream */
+void* sdmm_get_stream(const sdmm_mix* m);
+int sdmm_synchronize(sdmm_mix* m);
+
+/* uniformHemisphereInit with given seed positions/normals (host, n_pos*3 each);
+ * K must equal 8 * n_pos.  depth_prior / min_spatial_distance in normalised
+ * scene units; seed drives the PCG32 direction jitter. */
+int sdmm_init_hemisphere(sdmm_mix* m, const float* positions, const float* normals, int n_pos,
+                         float depth_prior, float min_spatial_distance, uint64_t seed);
+
+/* Host-only variant (no device, no handle): writes the initial component
+ * parameters, for data generators and tests.  Arrays sized K=8*n_pos. */
+int sdmm_hemisphere_init_host(const float* positions, const float* normals, int n_pos,
+                              float depth_prior, float min_spatial_distance, uint64_t seed,
+                              float* weights /*K*/, float* means /*K*6*/, float* covs /*K*25*/,
+                              float* bpriors /*K*25*/, float* bdepth /*K*9*/);
+
+/* One stepwise EM iteration (`iterations` times) over device-resident samples. */
+int sdmm_em_step(sdmm_mix* m, const sdmm_samples* device_samples, int iterations);
+/* Same with host-resident samples (staged through the handle's buffers). */
+int sdmm_em_step_host(sdmm_mix* m, const sdmm_samples* host_samples, int iterations);
+
+/* Split-phase EM step for sample-sharded multi-GPU runs:
+ *   sdmm_estep_stats  writes this shard's fp64 sufficient statistics,
+ *                     layout [H, weightSum, W(K), M(5K), C_lower(15K)],
+ *                     sdmm_stats_len(K) doubles, into `stats` (device);
+ *   (caller all-reduces `stats` with a SUM over ranks, e.g. ncclAllReduce)
+ *   sdmm_mstep        consumes the global statistics; n_total = global sample
+ *                     count (samples.size() of the reference).              */
+size_t sdmm_stats_len(int K);
+int sdmm_estep_stats(sdmm_mix* m, const sdmm_samples* device_samples, double* stats);
+int sdmm_mstep(sdmm_mix* m, const double* stats, int64_t n_total);
+
+/* Posterior (responsibility) of every sample: resp[n*K + k], device, fp32. */
+int sdmm_responsibilities(sdmm_mix* m, const sdmm_samples* device_samples, float* resp);
+
+/* Guided bounce for nq queries (device SoA planes):
+ *   c[3]   normalised condition position     u[3]  uniforms (cdf, Box-Muller)
+ *   d[3]   sampled world direction (out)     pdf   conditional mixture pdf at d
+ *   comp   joint component index used (-1: no valid conditional -> BSDF only) */
+int sdmm_guide_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], const float* const u[3],
+                     float* const d[3], float* pdf, int32_t* comp);
+/* gmmPdf of given directions d (device SoA). */
+int sdmm_pdf_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], const float* const d[3],
+                   float* pdf);
+/* lower_bound + tie walk of utils.h:104-115 on a caller CDF (device). */
+int sdmm_sample_discrete_cdf(const sdmm_mix* m, const float* cdf, int n, const float* u, int64_t nq,
+                             int32_t* out);
+
+/* Export the mixture (host outputs, any may be NULL): the canonical MVTN
+ * parameters plus every derived array, in the oracle's or_mixture layout. */
+typedef struct {
+    float* weights;    /* K */
+    float* cdf;        /* K */
+    float* mean;       /* K*6 */
+    float* cov;        /* K*25 */
+    float* to;         /* K*9 */
+    float* cholL;      /* K*25 */
+    float* cholLInv;   /* K*25 */
+    float* detInv;     /* K */
+    float* muPremult;  /* K*6 */
+    float* condCov;    /* K*4 */
+    float* margL;      /* K*9 */
+    float* margDetInv; /* K */
+    float* condL;      /* K*4 */
+    float* condLInv;   /* K*4 */
+    float* condDetInv; /* K */
+    int32_t* valid;    /* K */
+    float* normalization; /* 1 */
+} sdmm_params_out;
+int sdmm_get_params(const sdmm_mix* m, const sdmm_params_out* out);
+/* Replace the mixture by (weights, means, covs) host arrays; runs MVTN::set. */
+int sdmm_set_params(sdmm_mix* m, const float* weights, const float* means, const float* covs);
+
+/* Stepwise state export/import (checkpointing, tests).  Host buffers:
+ * scalars[9] = {heuristicTotalWeight, sgH, normalization, iterationsRun,
+ * alpha, niPriorMinusOne, decreasePrior, trainingCutoff, lastStatus};
+ * T[K], sgW[K], sgM[5K], sgC[25K] (double); bpriors[25K], bdepth[9K] (float). */
+int sdmm_get_state(const sdmm_mix* m, double* scalars, double* T, double* sgW, double* sgM,
+                   double* sgC, float* bpriors, float* bdepth);
+int sdmm_set_state(sdmm_mix* m, const double* scalars, const double* T, const double* sgW,
+                   const double* sgM, const double* sgC, const float* bpriors, const float* bdepth);
+
+const char* sdmm_last_error(void);
+int sdmm_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SDMM_GPU_H */

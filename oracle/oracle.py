@@ -1,0 +1,299 @@
+"""CPU ORACLE wrapper (test infrastructure only).
+
+ctypes binding of oracle/_build/liboracle.so, the plain-C restatement of the
+jmm stepwise tangent-space EM and guided sampling (see sdmm_oracle.h for the
+reference file:line map).  Only tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py may import this module; the product path never
+does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "_build" / "liboracle.so"
+
+_f = C.POINTER(C.c_float)
+_d = C.POINTER(C.c_double)
+_i = C.POINTER(C.c_int)
+
+
+class _Mixture(C.Structure):
+    _fields_ = [
+        ("K", C.c_int), ("heuristicWeight", C.c_float), ("normalization", C.c_float),
+        ("weights", _f), ("cdf", _f), ("mean", _f), ("cov", _f), ("to", _f),
+        ("cholL", _f), ("cholLInv", _f), ("detInv", _f), ("muPremult", _f),
+        ("condCov", _f), ("margL", _f), ("margDetInv", _f), ("condL", _f),
+        ("condLInv", _f), ("condDetInv", _f), ("valid", _i),
+    ]
+
+
+class _EmState(C.Structure):
+    _fields_ = [
+        ("K", C.c_int), ("iterationsRun", C.c_int), ("decreasePrior", C.c_int),
+        ("trainingCutoff", C.c_int), ("alpha", C.c_double), ("niPriorMinusOne", C.c_double),
+        ("heuristicTotalWeight", C.c_double), ("sgH", C.c_double),
+        ("totalWeight", _d), ("sgW", _d), ("sgM", _d), ("sgC", _d),
+        ("bPriors", _f), ("bDepth", _f),
+    ]
+
+
+class _Samples(C.Structure):
+    _fields_ = [
+        ("n", C.c_int64), ("x", _f * 6), ("w", _f), ("hpdf", _f),
+        ("isDiffuse", C.POINTER(C.c_uint8)),
+    ]
+
+
+def build() -> Path:
+    """Compile the oracle with its committed Makefile (gcc)."""
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            build()
+        L = C.CDLL(str(LIB_PATH))
+        L.or_pcg32_next_float.restype = C.c_float
+        L.or_pcg32_next_uint.restype = C.c_uint32
+        L.or_sinc_pi.restype = C.c_float
+        L.or_sinc_pi.argtypes = [C.c_float]
+        L.or_mvtn_pdf_and_log.restype = C.c_float
+        L.or_marginal_pdf.restype = C.c_float
+        L.or_conditional_pdf.restype = C.c_float
+        L.or_uniform_hemisphere_init.argtypes = [
+            C.c_void_p, C.c_void_p, _f, _f, C.c_int, C.c_float, C.c_float, C.c_uint64, C.c_int]
+        L.or_em_state_init.argtypes = [C.c_void_p, C.c_int, C.c_double, _d, C.c_double,
+                                       C.c_double, C.c_int]
+        L.or_mstep_f32.argtypes = [C.c_void_p, C.c_void_p, _d, C.c_int64]
+        L.or_mstep_f64.argtypes = [C.c_void_p, C.c_void_p, _d, C.c_int64]
+        L.or_guide_batch.argtypes = [C.c_void_p, C.c_int64, _f, _f, _f, _f,
+                                     C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        L.or_pdf_batch.argtypes = [C.c_void_p, C.c_int64, _f, _f, _f]
+        L.or_sample_discrete_cdf.argtypes = [_f, C.c_int, C.c_float]
+        L.or_is_positive_definite_f64.argtypes = [_d, C.c_int]
+        L.or_is_positive_definite_f32.argtypes = [_f, C.c_int]
+        L.or_ts_log.argtypes = [_f, _f, _f, _f]
+        L.or_ts_exp.argtypes = [_f, _f, _f, _f]
+        L.or_coordinates.argtypes = [_f, _f]
+        L.or_component_set.argtypes = [C.c_void_p, C.c_int, _d, _d, C.c_int]
+        _lib = L
+    return _lib
+
+
+def _fp(a):
+    return a.ctypes.data_as(_f)
+
+
+def _dp(a):
+    return a.ctypes.data_as(_d)
+
+
+MIX_FIELDS = {
+    "weights": 1, "cdf": 1, "mean": 6, "cov": 25, "to": 9, "cholL": 25, "cholLInv": 25,
+    "detInv": 1, "muPremult": 6, "condCov": 4, "margL": 9, "margDetInv": 1, "condL": 4,
+    "condLInv": 4, "condDetInv": 1,
+}
+
+
+class Mixture:
+    """jmm::MixtureModel<6,K,3,float,...> held in numpy arrays."""
+
+    def __init__(self, K: int):
+        self.K = K
+        self.arr = {k: np.zeros(K * w, np.float32) for k, w in MIX_FIELDS.items()}
+        self.valid = np.zeros(K, np.int32)
+        self.s = _Mixture()
+        self.s.K = K
+        self.s.heuristicWeight = 0.5
+        self.s.normalization = 1.0
+        for k, a in self.arr.items():
+            setattr(self.s, k, _fp(a))
+        self.s.valid = self.valid.ctypes.data_as(_i)
+
+    @property
+    def ptr(self):
+        return C.byref(self.s)
+
+    def __getattr__(self, name):
+        if name in MIX_FIELDS:
+            w = MIX_FIELDS[name]
+            a = self.__dict__["arr"][name]
+            return a if w == 1 else a.reshape(self.K, -1)
+        raise AttributeError(name)
+
+    def set_component(self, k, mean6, cov25, mode=1):
+        m = np.ascontiguousarray(mean6, np.float64)
+        c = np.ascontiguousarray(np.asarray(cov25, np.float64).reshape(25))
+        return lib().or_component_set(self.ptr, k, _dp(m), _dp(c), mode)
+
+    def configure(self):
+        return lib().or_mixture_configure(self.ptr)
+
+    def copy_params_from(self, params: dict):
+        """Load exported derived params (dict of arrays named like MIX_FIELDS)."""
+        for k in MIX_FIELDS:
+            if k in params:
+                self.arr[k][:] = np.asarray(params[k], np.float32).reshape(-1)
+        if "normalization" in params:
+            self.s.normalization = float(params["normalization"])
+        self.valid[:] = 1
+
+
+class EmState:
+    def __init__(self, K, alpha=0.9, bprior=1e-5, ni=6e-5, epsilon=1e-100, decrease_prior=True):
+        self.K = K
+        self.d = {"totalWeight": np.zeros(K), "sgW": np.zeros(K), "sgM": np.zeros(K * 5),
+                  "sgC": np.zeros(K * 25)}
+        self.bPriors = np.zeros(K * 25, np.float32)
+        self.bDepth = np.zeros(K * 9, np.float32)
+        self.s = _EmState()
+        for k, a in self.d.items():
+            setattr(self.s, k, _dp(a))
+        self.s.bPriors = _fp(self.bPriors)
+        self.s.bDepth = _fp(self.bDepth)
+        bp = np.full(5, bprior, np.float64)
+        lib().or_em_state_init(C.byref(self.s), K, alpha, _dp(bp), ni, epsilon, int(decrease_prior))
+
+    @property
+    def ptr(self):
+        return C.byref(self.s)
+
+
+class Samples:
+    def __init__(self, x: np.ndarray, w: np.ndarray, hpdf=None, is_diffuse=None):
+        self.x = [np.ascontiguousarray(x[i], np.float32) for i in range(6)]
+        self.w = np.ascontiguousarray(w, np.float32)
+        self.hpdf = None if hpdf is None else np.ascontiguousarray(hpdf, np.float32)
+        self.isd = None if is_diffuse is None else np.ascontiguousarray(is_diffuse, np.uint8)
+        self.s = _Samples()
+        self.s.n = len(self.w)
+        for i in range(6):
+            self.s.x[i] = _fp(self.x[i])
+        self.s.w = _fp(self.w)
+        self.s.hpdf = _fp(self.hpdf) if self.hpdf is not None else _f()
+        self.s.isDiffuse = (self.isd.ctypes.data_as(C.POINTER(C.c_uint8))
+                            if self.isd is not None else C.POINTER(C.c_uint8)())
+
+    @property
+    def ptr(self):
+        return C.byref(self.s)
+
+
+def hemisphere_init(K_positions, positions, normals, depth_prior, min_dist, seed, mode=1,
+                    with_state=True, **em_kw):
+    K = K_positions * 8
+    m = Mixture(K)
+    st = EmState(K, **em_kw) if with_state else None
+    pos = np.ascontiguousarray(positions, np.float32).reshape(-1)
+    nrm = np.ascontiguousarray(normals, np.float32).reshape(-1)
+    lib().or_uniform_hemisphere_init(m.ptr, st.ptr if st else None, _fp(pos), _fp(nrm),
+                                     K_positions, depth_prior, min_dist, seed, mode)
+    return m, st
+
+
+def stats_len(K):
+    return 2 + 31 * K
+
+
+def calculate_stats(m: Mixture, s: Samples, accurate=True):
+    out = np.zeros(stats_len(m.K))
+    f = lib().or_calculate_stats_f64 if accurate else lib().or_calculate_stats_f32
+    f(m.ptr, s.ptr, _dp(out))
+    return out
+
+
+def mstep(m: Mixture, st: EmState, stats: np.ndarray, n_samples: int, accurate=True):
+    f = lib().or_mstep_f64 if accurate else lib().or_mstep_f32
+    st_ = np.ascontiguousarray(stats, np.float64)
+    return f(m.ptr, st.ptr, _dp(st_), n_samples)
+
+
+def optimize(m: Mixture, st: EmState, s: Samples, accurate=True):
+    f = lib().or_optimize_f64 if accurate else lib().or_optimize_f32
+    return f(m.ptr, st.ptr, s.ptr)
+
+
+def responsibilities(m: Mixture, s: Samples):
+    out = np.zeros((s.s.n, m.K), np.float32)
+    lib().or_responsibilities(m.ptr, s.ptr, _fp(out))
+    return out
+
+
+def guide_batch(m: Mixture, c: np.ndarray, u: np.ndarray):
+    c = np.ascontiguousarray(c, np.float32)
+    u = np.ascontiguousarray(u, np.float32)
+    nq = c.shape[0]
+    d = np.zeros((nq, 3), np.float32)
+    pdf = np.zeros(nq, np.float32)
+    comp = np.zeros(nq, np.int32)
+    slot = np.zeros(nq, np.int32)
+    I32 = C.POINTER(C.c_int32)
+    lib().or_guide_batch(m.ptr, nq, _fp(c), _fp(u), _fp(d), _fp(pdf),
+                         comp.ctypes.data_as(I32), slot.ctypes.data_as(I32))
+    return d, pdf, comp, slot
+
+
+def pdf_batch(m: Mixture, c: np.ndarray, d: np.ndarray):
+    c = np.ascontiguousarray(c, np.float32)
+    d = np.ascontiguousarray(d, np.float32)
+    out = np.zeros(c.shape[0], np.float32)
+    lib().or_pdf_batch(m.ptr, c.shape[0], _fp(c), _fp(d), _fp(out))
+    return out
+
+
+def sample_discrete_cdf(cdf, u):
+    cdf = np.ascontiguousarray(cdf, np.float32)
+    return lib().or_sample_discrete_cdf(_fp(cdf), len(cdf), float(u))
+
+
+def is_pd(A, single=False):
+    if single:
+        a = np.ascontiguousarray(A, np.float32)
+        return bool(lib().or_is_positive_definite_f32(_fp(a), a.shape[0]))
+    a = np.ascontiguousarray(A, np.float64)
+    return bool(lib().or_is_positive_definite_f64(_dp(a), a.shape[0]))
+
+
+def ts_log(to, emb):
+    to = np.ascontiguousarray(to, np.float32).reshape(9)
+    emb = np.ascontiguousarray(emb, np.float32).reshape(6)
+    t = np.zeros(5, np.float32)
+    j = np.zeros(1, np.float32)
+    ok = lib().or_ts_log(_fp(to), _fp(emb), _fp(t), _fp(j))
+    return ok, t, float(j[0])
+
+
+def ts_exp(to, tangent):
+    to = np.ascontiguousarray(to, np.float32).reshape(9)
+    t = np.ascontiguousarray(tangent, np.float32).reshape(5)
+    e = np.zeros(6, np.float32)
+    j = np.zeros(1, np.float32)
+    ok = lib().or_ts_exp(_fp(to), _fp(t), _fp(e), _fp(j))
+    return ok, e, float(j[0])
+
+
+def coordinates(n):
+    n = np.ascontiguousarray(n, np.float32)
+    to = np.zeros(9, np.float32)
+    lib().or_coordinates(_fp(n), _fp(to))
+    return to.reshape(3, 3)
+
+
+def pcg32_floats(seed, n, seq=0xda3e39cb94b95bdb):
+    class R(C.Structure):
+        _fields_ = [("state", C.c_uint64), ("inc", C.c_uint64)]
+    r = R()
+    lib().or_pcg32_seed(C.byref(r), C.c_uint64(seed), C.c_uint64(seq))
+    return np.array([lib().or_pcg32_next_float(C.byref(r)) for _ in range(n)], np.float32)

@@ -1,0 +1,336 @@
+"""sdmm-mitsuba_amd -- MI355X-native SDMM path-guiding hot path.
+
+Python binding (ctypes) of the C ABI in include/sdmm_gpu.h, used by the tests
+and bench.py.  It mirrors the reference's jmm interface names (MixtureModel /
+StepwiseTangentEM::optimize / posteriorAndLog / conditional+sample+pdf):
+
+    mix = SDMM(K=128)                       # jmm::MixtureModel + StepwiseTangentEM
+    mix.init_hemisphere(pos, nrm, ...)      # uniformHemisphereInit
+    mix.optimize(samples)                   # StepwiseTangentEM::optimize (one EM step)
+    mix.posterior(samples, out)             # posteriorAndLog over a batch
+    d, pdf, comp = mix.guide(c, u)          # conditional + sample + pdf per query
+
+Device buffers are torch tensors on the HIP device (torch is only the memory
+and stream plumbing).  There is no CPU fallback: if lib/libsdmm_amd.so is
+missing or the device is absent, every call fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = PKG_DIR / "lib" / "libsdmm_amd.so"
+REPO = PKG_DIR.parent
+
+
+class SDMMError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def build(arch: str = "gfx950", jobs: int = 4) -> Path:
+    import subprocess
+    subprocess.run(["make", "-s", f"-j{jobs}", "-C", str(PKG_DIR), f"ARCH={arch}"], check=True)
+    return LIB_PATH
+
+
+class _Samples(C.Structure):
+    _fields_ = [("x", C.c_void_p * 6), ("w", C.c_void_p), ("hpdf", C.c_void_p),
+                ("is_diffuse", C.c_void_p), ("n", C.c_int64)]
+
+
+class _EmParams(C.Structure):
+    _fields_ = [("alpha", C.c_float), ("bprior", C.c_float * 5), ("ni_prior_minus_one", C.c_float),
+                ("epsilon", C.c_double), ("decrease_prior", C.c_int)]
+
+
+PARAM_FIELDS = [("weights", 1), ("cdf", 1), ("mean", 6), ("cov", 25), ("to", 9), ("cholL", 25),
+                ("cholLInv", 25), ("detInv", 1), ("muPremult", 6), ("condCov", 4), ("margL", 9),
+                ("margDetInv", 1), ("condL", 4), ("condLInv", 4), ("condDetInv", 1)]
+
+
+class _ParamsOut(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n, _ in PARAM_FIELDS] + [("valid", C.c_void_p),
+                                                              ("normalization", C.c_void_p)]
+
+
+def lib():
+    """Load lib/libsdmm_amd.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise SDMMError(f"{LIB_PATH} not found: run `make -C {PKG_DIR}` (or __graft_entry__.build())")
+        # torch (the memory/stream plumbing) and this library share one HIP
+        # runtime (same SONAME); let torch initialise it before our code object
+        # registers, otherwise torch's later device discovery fails.
+        try:
+            import torch
+            torch.cuda.is_available()
+        except ImportError:
+            pass
+        L = C.CDLL(str(LIB_PATH))
+        L.sdmm_last_error.restype = C.c_char_p
+        L.sdmm_stats_len.restype = C.c_size_t
+        L.sdmm_stats_len.argtypes = [C.c_int]
+        L.sdmm_get_stream.restype = C.c_void_p
+        L.sdmm_get_stream.argtypes = [C.c_void_p]
+        L.sdmm_create.argtypes = [C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
+        L.sdmm_destroy.argtypes = [C.c_void_p]
+        L.sdmm_set_stream.argtypes = [C.c_void_p, C.c_void_p]
+        L.sdmm_synchronize.argtypes = [C.c_void_p]
+        L.sdmm_init_hemisphere.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_float,
+                                           C.c_float, C.c_uint64]
+        L.sdmm_hemisphere_init_host.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_float, C.c_float,
+                                                C.c_uint64] + [C.c_void_p] * 5
+        L.sdmm_em_step.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        L.sdmm_em_step_host.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        L.sdmm_estep_stats.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.sdmm_mstep.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.sdmm_responsibilities.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.sdmm_guide_batch.argtypes = [C.c_void_p, C.c_int64, C.c_void_p * 3, C.c_void_p * 3,
+                                       C.c_void_p * 3, C.c_void_p, C.c_void_p]
+        L.sdmm_pdf_batch.argtypes = [C.c_void_p, C.c_int64, C.c_void_p * 3, C.c_void_p * 3, C.c_void_p]
+        L.sdmm_sample_discrete_cdf.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int64,
+                                               C.c_void_p]
+        L.sdmm_get_params.argtypes = [C.c_void_p, C.c_void_p]
+        L.sdmm_set_params.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.sdmm_get_state.argtypes = [C.c_void_p] + [C.c_void_p] * 7
+        L.sdmm_set_state.argtypes = [C.c_void_p] + [C.c_void_p] * 7
+        L.sdmm_em_params_default.argtypes = [C.c_void_p]
+        _lib = L
+    return _lib
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise SDMMError(f"sdmm error {rc}: {lib().sdmm_last_error().decode()}")
+
+
+def stats_len(K: int) -> int:
+    return 2 + 21 * K
+
+
+EXPORTED_SYMBOLS = [
+    "sdmm_em_params_default", "sdmm_create", "sdmm_destroy", "sdmm_num_components",
+    "sdmm_set_stream", "sdmm_get_stream", "sdmm_synchronize", "sdmm_init_hemisphere",
+    "sdmm_hemisphere_init_host", "sdmm_em_step", "sdmm_em_step_host", "sdmm_stats_len",
+    "sdmm_estep_stats", "sdmm_mstep", "sdmm_responsibilities", "sdmm_guide_batch", "sdmm_pdf_batch",
+    "sdmm_sample_discrete_cdf", "sdmm_get_params", "sdmm_set_params", "sdmm_get_state",
+    "sdmm_set_state", "sdmm_last_error", "sdmm_abi_version",
+]
+
+
+def hemisphere_init_host(positions, normals, depth_prior, min_dist, seed):
+    """uniformHemisphereInit on the host (no device needed): initial params."""
+    pos = np.ascontiguousarray(positions, np.float32).reshape(-1, 3)
+    nrm = np.ascontiguousarray(normals, np.float32).reshape(-1, 3)
+    n_pos = pos.shape[0]
+    K = 8 * n_pos
+    out = {"weights": np.zeros(K, np.float32), "mean": np.zeros((K, 6), np.float32),
+           "cov": np.zeros((K, 5, 5), np.float32), "bpriors": np.zeros((K, 5, 5), np.float32),
+           "bdepth": np.zeros((K, 3, 3), np.float32)}
+    _check(lib().sdmm_hemisphere_init_host(pos.ctypes.data, nrm.ctypes.data, n_pos, depth_prior,
+                                           min_dist, seed, out["weights"].ctypes.data,
+                                           out["mean"].ctypes.data, out["cov"].ctypes.data,
+                                           out["bpriors"].ctypes.data, out["bdepth"].ctypes.data))
+    return out
+
+
+class DeviceSamples:
+    """SoA sample planes resident in HBM (torch tensors on the HIP device)."""
+
+    def __init__(self, x, w, hpdf=None, is_diffuse=None):
+        import torch
+        self.x = [t.contiguous() for t in x]
+        self.w = w.contiguous()
+        self.hpdf = None if hpdf is None else hpdf.contiguous()
+        self.is_diffuse = None if is_diffuse is None else is_diffuse.to(torch.uint8).contiguous()
+        assert len(self.x) == 6
+        for t in self.x + [self.w]:
+            assert t.dtype == torch.float32 and t.is_cuda, "sample planes must be fp32 device tensors"
+        self.n = int(self.w.numel())
+        self.s = _Samples()
+        for i in range(6):
+            self.s.x[i] = self.x[i].data_ptr()
+        self.s.w = self.w.data_ptr()
+        self.s.hpdf = self.hpdf.data_ptr() if self.hpdf is not None else None
+        self.s.is_diffuse = self.is_diffuse.data_ptr() if self.is_diffuse is not None else None
+        self.s.n = self.n
+
+    @classmethod
+    def from_numpy(cls, x, w, hpdf=None, is_diffuse=None, device="cuda"):
+        import torch
+        xt = [torch.from_numpy(np.ascontiguousarray(x[i], np.float32)).to(device) for i in range(6)]
+        wt = torch.from_numpy(np.ascontiguousarray(w, np.float32)).to(device)
+        ht = None if hpdf is None else torch.from_numpy(np.ascontiguousarray(hpdf, np.float32)).to(device)
+        dt = None if is_diffuse is None else torch.from_numpy(np.ascontiguousarray(is_diffuse, np.uint8)).to(device)
+        return cls(xt, wt, ht, dt)
+
+    def shard(self, rank: int, world: int) -> "DeviceSamples":
+        """Contiguous sample range of `rank` (SURVEY 8e partitioning)."""
+        per = (self.n + world - 1) // world
+        a, b = min(self.n, rank * per), min(self.n, (rank + 1) * per)
+        sl = lambda t: None if t is None else t[a:b]
+        return DeviceSamples([t[a:b] for t in self.x], self.w[a:b], sl(self.hpdf), sl(self.is_diffuse))
+
+    @property
+    def ptr(self):
+        return C.byref(self.s)
+
+
+class SDMM:
+    """One K-component SDMM + its stepwise EM state, resident on one GPU."""
+
+    def __init__(self, K: int, device: int = 0, alpha=0.9, bprior=1e-5, ni_prior_minus_one=6e-5,
+                 epsilon=1e-100, decrease_prior=True, stream=None):
+        self.K = K
+        p = _EmParams()
+        p.alpha = alpha
+        for i in range(5):
+            p.bprior[i] = bprior
+        p.ni_prior_minus_one = ni_prior_minus_one
+        p.epsilon = epsilon
+        p.decrease_prior = int(decrease_prior)
+        h = C.c_void_p()
+        _check(lib().sdmm_create(K, C.byref(p), device, C.byref(h)))
+        self.h = h
+        # Enqueue on the caller's stream so work is ordered with the torch ops
+        # that allocate, fill and read the buffers (default: torch's current
+        # stream; the C ABI's own default is a private non-blocking stream).
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream() if torch.cuda.is_available() else None
+        if stream is not None:
+            self.set_stream(stream)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().sdmm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- streams ---------------------------------------------------------
+    def set_stream(self, stream):
+        """stream: a torch.cuda.Stream, a raw hipStream_t int, or None."""
+        ptr = getattr(stream, "cuda_stream", stream)
+        _check(lib().sdmm_set_stream(self.h, ptr))
+
+    @property
+    def stream_ptr(self) -> int:
+        return lib().sdmm_get_stream(self.h) or 0
+
+    def synchronize(self):
+        _check(lib().sdmm_synchronize(self.h))
+
+    # ---- init / params ---------------------------------------------------
+    def init_hemisphere(self, positions, normals, depth_prior, min_spatial_distance, seed):
+        pos = np.ascontiguousarray(positions, np.float32).reshape(-1, 3)
+        nrm = np.ascontiguousarray(normals, np.float32).reshape(-1, 3)
+        _check(lib().sdmm_init_hemisphere(self.h, pos.ctypes.data, nrm.ctypes.data, pos.shape[0],
+                                          depth_prior, min_spatial_distance, seed))
+
+    def set_params(self, weights, means, covs):
+        w = np.ascontiguousarray(weights, np.float32)
+        m = np.ascontiguousarray(means, np.float32)
+        c = np.ascontiguousarray(covs, np.float32)
+        _check(lib().sdmm_set_params(self.h, w.ctypes.data, m.ctypes.data, c.ctypes.data))
+
+    def get_params(self) -> dict:
+        K = self.K
+        arrs = {n: np.zeros(K * w, np.float32) for n, w in PARAM_FIELDS}
+        valid = np.zeros(K, np.int32)
+        norm = np.zeros(1, np.float32)
+        o = _ParamsOut()
+        for n, _ in PARAM_FIELDS:
+            setattr(o, n, arrs[n].ctypes.data)
+        o.valid = valid.ctypes.data
+        o.normalization = norm.ctypes.data
+        _check(lib().sdmm_get_params(self.h, C.byref(o)))
+        out = {n: (a if w == 1 else a.reshape(K, w)) for (n, w), a in zip(PARAM_FIELDS, arrs.values())}
+        out["valid"] = valid
+        out["normalization"] = float(norm[0])
+        return out
+
+    def get_state(self) -> dict:
+        K = self.K
+        st = {"scalars": np.zeros(9), "T": np.zeros(K), "sgW": np.zeros(K), "sgM": np.zeros(5 * K),
+              "sgC": np.zeros(25 * K), "bpriors": np.zeros(25 * K, np.float32),
+              "bdepth": np.zeros(9 * K, np.float32)}
+        _check(lib().sdmm_get_state(self.h, *[st[k].ctypes.data for k in
+                                              ("scalars", "T", "sgW", "sgM", "sgC", "bpriors", "bdepth")]))
+        return st
+
+    def set_state(self, st: dict):
+        keys = ("scalars", "T", "sgW", "sgM", "sgC", "bpriors", "bdepth")
+        arrs = []
+        for k in keys:
+            dt = np.float32 if k in ("bpriors", "bdepth") else np.float64
+            arrs.append(np.ascontiguousarray(st[k], dt))
+        _check(lib().sdmm_set_state(self.h, *[a.ctypes.data for a in arrs]))
+
+    # ---- EM --------------------------------------------------------------
+    def optimize(self, samples: DeviceSamples, iterations: int = 1):
+        """StepwiseTangentEM::optimize: `iterations` EM steps (enqueued, async)."""
+        _check(lib().sdmm_em_step(self.h, samples.ptr, iterations))
+
+    em_step = optimize
+
+    def estep_stats(self, samples: DeviceSamples, stats):
+        """Shard statistics into `stats` (fp64 device tensor of stats_len(K))."""
+        assert stats.numel() >= stats_len(self.K) and stats.is_cuda
+        _check(lib().sdmm_estep_stats(self.h, samples.ptr, stats.data_ptr()))
+
+    def mstep(self, stats, n_total: int):
+        _check(lib().sdmm_mstep(self.h, stats.data_ptr(), n_total))
+
+    def posterior(self, samples: DeviceSamples, resp):
+        """posteriorAndLog for every sample into resp (fp32 [N, K] device tensor)."""
+        assert resp.numel() >= samples.n * self.K and resp.is_cuda
+        _check(lib().sdmm_responsibilities(self.h, samples.ptr, resp.data_ptr()))
+
+    responsibilities = posterior
+
+    # ---- guiding ---------------------------------------------------------
+    def guide(self, c, u, out=None):
+        """conditional(c) -> sample(u) -> pdf: c, u are 3 device planes each."""
+        import torch
+        nq = c[0].numel()
+        if out is None:
+            dev = c[0].device
+            out = ([torch.empty(nq, device=dev) for _ in range(3)], torch.empty(nq, device=dev),
+                   torch.empty(nq, device=dev, dtype=torch.int32))
+        d, pdf, comp = out
+        cc = (C.c_void_p * 3)(*[t.data_ptr() for t in c])
+        uu = (C.c_void_p * 3)(*[t.data_ptr() for t in u])
+        dd = (C.c_void_p * 3)(*[t.data_ptr() for t in d])
+        _check(lib().sdmm_guide_batch(self.h, nq, cc, uu, dd, pdf.data_ptr(), comp.data_ptr()))
+        return d, pdf, comp
+
+    def pdf(self, c, d, out=None):
+        import torch
+        nq = c[0].numel()
+        if out is None:
+            out = torch.empty(nq, device=c[0].device)
+        cc = (C.c_void_p * 3)(*[t.data_ptr() for t in c])
+        dd = (C.c_void_p * 3)(*[t.data_ptr() for t in d])
+        _check(lib().sdmm_pdf_batch(self.h, nq, cc, dd, out.data_ptr()))
+        return out
+
+    def sample_discrete_cdf(self, cdf, u, out=None):
+        import torch
+        if out is None:
+            out = torch.empty(u.numel(), device=u.device, dtype=torch.int32)
+        _check(lib().sdmm_sample_discrete_cdf(self.h, cdf.data_ptr(), cdf.numel(), u.data_ptr(),
+                                              u.numel(), out.data_ptr()))
+        return out

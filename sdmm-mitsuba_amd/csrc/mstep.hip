@@ -1,0 +1,400 @@
+// mstep.hip -- stepwise blend, MAP M-step and component set-up on gfx950.
+//
+// Replaces (per EM iteration, all on the device, no host round trip):
+//   stepwise blend      stepwise_tangent.h:685-743
+//   MAP M-step          stepwise_tangent.h:745-980  (priors, exp of the mean in
+//                       the old frame, PD test, stats re-centring)
+//   normalisation/CDF   stepwise_tangent.h:992-1035, utils.h:64-102
+//   MVTN::set           multivariate_tangent_normal.cpp:16-65 (+ conditioning
+//                       mvtn.h:386-408, marginal mvtn.h:446-454)
+// The M-step is O(K * 5^3): one thread per component, fp64 throughout (the
+// "accurate" oracle mode), component parameters rounded to float at the end.
+// FMA contraction is off so the fp64 op order equals oracle/sdmm_oracle.c's.
+#include "sdmm_device.h"
+
+#pragma clang fp contract(off)
+
+namespace sdmm {
+
+__device__ static void coordinates_d(const double n[3], double to[9]) {
+    // Coordinates (utils.h:32-48)
+    double sign = copysign(1.0, n[2]);
+    const double a = -1.0 / (sign + n[2]);
+    const double b = n[0] * n[1] * a;
+    to[0] = 1.0 + sign * n[0] * n[0] * a; to[1] = sign * b; to[2] = -sign * n[0];
+    to[3] = b; to[4] = sign + n[1] * n[1] * a; to[5] = -n[1];
+    to[6] = n[0]; to[7] = n[1]; to[8] = n[2];
+}
+
+__device__ static double sinc_pi_d(double x) {
+    // boost::math::sinc_pi
+    const double taylor_0_bound = 2.220446049250313e-16;
+    const double taylor_2_bound = sqrt(taylor_0_bound);
+    const double taylor_n_bound = sqrt(taylor_2_bound);
+    double ax = fabs(x);
+    if (ax >= taylor_n_bound) return sin(x) / x;
+    double result = 1.0;
+    if (ax >= taylor_0_bound) {
+        double x2 = x * x;
+        result -= x2 / 6.0;
+        if (ax >= taylor_2_bound) result += (x2 * x2) / 120.0;
+    }
+    return result;
+}
+
+// Eigen LLT<Lower>, unblocked (reads the lower triangle of row-major A).
+template <int N>
+__device__ static bool llt_d(const double* A, double* L) {
+    for (int i = 0; i < N * N; ++i) L[i] = 0.0;
+    for (int i = 0; i < N; ++i)
+        for (int j = 0; j <= i; ++j) L[i * N + j] = A[i * N + j];
+    for (int k = 0; k < N; ++k) {
+        double x = L[k * N + k];
+        for (int j = 0; j < k; ++j) x -= L[k * N + j] * L[k * N + j];
+        if (!(x > 0.0)) return false;
+        x = sqrt(x);
+        L[k * N + k] = x;
+        for (int i = k + 1; i < N; ++i) {
+            double v = L[i * N + k];
+            for (int j = 0; j < k; ++j) v -= L[i * N + j] * L[k * N + j];
+            L[i * N + k] = v / x;
+        }
+    }
+    return true;
+}
+
+template <int N>
+__device__ static void tri_inv_d(const double* L, double* Li) {
+    for (int i = 0; i < N * N; ++i) Li[i] = 0.0;
+    for (int c = 0; c < N; ++c)
+        for (int i = c; i < N; ++i) {
+            double v = (i == c) ? 1.0 : 0.0;
+            for (int j = c; j < i; ++j) v -= L[i * N + j] * Li[j * N + c];
+            Li[i * N + c] = v / L[i * N + i];
+        }
+}
+
+__device__ static void inv3_d(const double* m, double* r) {
+    // Eigen compute_inverse_size3 (adjugate / det)
+    double c00 = m[4] * m[8] - m[5] * m[7];
+    double c10 = m[7] * m[2] - m[8] * m[1];
+    double c20 = m[1] * m[5] - m[2] * m[4];
+    double det = c00 * m[0] + c10 * m[3] + c20 * m[6];
+    double invdet = 1.0 / det;
+    r[0] = c00 * invdet; r[1] = c10 * invdet; r[2] = c20 * invdet;
+    r[3] = (m[5] * m[6] - m[3] * m[8]) * invdet;
+    r[4] = (m[8] * m[0] - m[6] * m[2]) * invdet;
+    r[5] = (m[2] * m[3] - m[0] * m[5]) * invdet;
+    r[6] = (m[3] * m[7] - m[4] * m[6]) * invdet;
+    r[7] = (m[6] * m[1] - m[7] * m[0]) * invdet;
+    r[8] = (m[0] * m[4] - m[1] * m[3]) * invdet;
+}
+
+// MVTN::set(mean, cov) in fp64, results rounded to float (oracle mode 1).
+__device__ static void set_component(int k, const double* mean, const double* cov, const CanonDev& C) {
+    float fm[6];
+    for (int i = 0; i < 6; ++i) { fm[i] = (float)mean[i]; C.mean[6 * k + i] = fm[i]; }
+    for (int i = 0; i < 25; ++i) C.cov[25 * k + i] = (float)cov[i];
+    double md[3] = {(double)fm[3], (double)fm[4], (double)fm[5]};
+    double tod[9];
+    coordinates_d(md, tod);
+    for (int i = 0; i < 9; ++i) C.to[9 * k + i] = (float)tod[i];
+    double AA[9], AB[6], BA[6], BB[4], AAi[9], P[6], S[4];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) AA[3 * i + j] = cov[5 * i + j];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 2; ++j) AB[2 * i + j] = cov[5 * i + 3 + j];
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 3; ++j) BA[3 * i + j] = cov[5 * (3 + i) + j];
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 2; ++j) BB[2 * i + j] = cov[5 * (3 + i) + 3 + j];
+    inv3_d(AA, AAi);
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double v = 0.0;
+            for (int l = 0; l < 3; ++l) v += BA[3 * i + l] * AAi[3 * l + j];
+            P[3 * i + j] = v;
+        }
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 2; ++j) {
+            double v = 0.0;
+            for (int l = 0; l < 3; ++l) v += P[3 * i + l] * AB[2 * l + j];
+            S[2 * i + j] = BB[2 * i + j] - v;
+        }
+    for (int i = 0; i < 6; ++i) C.muPremult[6 * k + i] = (float)P[i];
+    for (int i = 0; i < 4; ++i) C.condCov[4 * k + i] = (float)S[i];
+    double L[25], Li[25];
+    int ok = 1;
+    if (llt_d<5>(cov, L)) {
+        tri_inv_d<5>(L, Li);
+        double det = 1.0;
+        for (int i = 0; i < 5; ++i) det *= L[6 * i];
+        for (int i = 0; i < 25; ++i) {
+            C.cholL[25 * k + i] = (float)L[i];
+            C.cholLInv[25 * k + i] = (float)Li[i];
+        }
+        C.detInv[k] = (float)(1.0 / det);
+    } else {
+        ok = 0;
+    }
+    double A3[9], L3[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) A3[3 * i + j] = cov[5 * i + j];
+    if (llt_d<3>(A3, L3)) {
+        for (int i = 0; i < 9; ++i) C.margL[9 * k + i] = (float)L3[i];
+        C.margDetInv[k] = (float)(1.0 / (L3[0] * L3[4] * L3[8]));
+    }
+    double L2[4];
+    if (llt_d<2>(S, L2)) {
+        double det2 = L2[0] * L2[3];
+        C.condL[4 * k + 0] = (float)L2[0]; C.condL[4 * k + 1] = 0.0f;
+        C.condL[4 * k + 2] = (float)L2[2]; C.condL[4 * k + 3] = (float)L2[3];
+        C.condLInv[4 * k + 0] = (float)(L2[3] / det2);
+        C.condLInv[4 * k + 1] = 0.0f;
+        C.condLInv[4 * k + 2] = (float)(-L2[2] / det2);
+        C.condLInv[4 * k + 3] = (float)(L2[0] / det2);
+        C.condDetInv[k] = (float)(1.0 / det2);
+    }
+    C.valid[k] = ok;
+}
+
+// Packed E-step and guide records of component k (k < Kp; k >= K is padding).
+__device__ static void pack_component(int k, int K, int Kp, const CanonDev& C, float* ep, float* gp,
+                                      float norm5) {
+    float e[EP_FIELDS];
+    float g[GP_FIELDS];
+    for (int f = 0; f < EP_FIELDS; ++f) e[f] = 0.0f;
+    for (int f = 0; f < GP_FIELDS; ++f) g[f] = 0.0f;
+    if (k < K) {
+        const float w = C.weights[k];
+        const float* mu = C.mean + 6 * k;
+        const float* Li = C.cholLInv + 25 * k;
+        const float* to = C.to + 9 * k;
+        e[EP_MU0] = mu[0]; e[EP_MU1] = mu[1]; e[EP_MU2] = mu[2];
+        const int lidx[15] = {0, 5, 6, 10, 11, 12, 15, 16, 17, 18, 20, 21, 22, 23, 24};
+        for (int i = 0; i < 15; ++i) e[EP_L00 + i] = Li[lidx[i]];
+        for (int i = 0; i < 9; ++i) e[EP_R00 + i] = to[i];
+        e[EP_DI] = C.detInv[k];
+        e[EP_PI] = C.valid[k] ? w : 0.0f;
+        g[GP_W] = w;
+        g[GP_MU0] = mu[0]; g[GP_MU1] = mu[1]; g[GP_MU2] = mu[2];
+        const float* ML = C.margL + 9 * k;
+        g[GP_ML00] = ML[0]; g[GP_ML10] = ML[3]; g[GP_ML11] = ML[4];
+        g[GP_ML20] = ML[6]; g[GP_ML21] = ML[7]; g[GP_ML22] = ML[8];
+        g[GP_MDI] = C.margDetInv[k];
+        for (int i = 0; i < 6; ++i) g[GP_P00 + i] = C.muPremult[6 * k + i];
+        for (int i = 0; i < 9; ++i) g[GP_T00 + i] = to[i];
+        g[GP_CL00] = C.condL[4 * k + 0]; g[GP_CL10] = C.condL[4 * k + 2]; g[GP_CL11] = C.condL[4 * k + 3];
+        for (int i = 0; i < 4; ++i) g[GP_CI00 + i] = C.condLInv[4 * k + i];
+        g[GP_CDI] = C.condDetInv[k];
+    }
+    for (int f = 0; f < EP_FIELDS; ++f) ep[f * Kp + k] = e[f];
+    for (int f = 0; f < GP_FIELDS; ++f) gp[f * Kp + k] = g[f];
+}
+
+// createCdf(false) then configure()'s createCdf(true) (float, sequential);
+// executed by one thread.
+__device__ static void weights_cdf(float* w, float* cdf, int K, bool first_partial) {
+    if (first_partial) {
+        float acc = 0.0f;
+        for (int k = 0; k < K; ++k) { acc += w[k]; cdf[k] = acc; }
+    }
+    float sum = 0.0f;
+    for (int k = 0; k < K; ++k) sum += w[k];
+    if (sum == 0.0f) return;
+    for (int k = 0; k < K; ++k) w[k] = w[k] / sum;
+    float acc = 0.0f;
+    for (int k = 0; k < K; ++k) { acc += w[k]; cdf[k] = acc; }
+}
+
+// ---------------------------------------------------------------------------
+// set() for all components from (mean, cov) given in fp64, then configure().
+__global__ void __launch_bounds__(512)
+set_all_kernel(int K, int Kp, const double* __restrict__ mean, const double* __restrict__ cov,
+               CanonDev C, float* ep, float* gp, float norm5) {
+    const int k = threadIdx.x;
+    if (k < K) set_component(k, mean + 6 * k, cov + 25 * k, C);
+    __syncthreads();
+    if (k == 0) weights_cdf(C.weights, C.cdf, K, false);
+    __syncthreads();
+    for (int kk = k; kk < Kp; kk += blockDim.x) pack_component(kk, K, Kp, C, ep, gp, norm5);
+}
+
+// Re-derive the packed records only (after sdmm_set_params of weights).
+__global__ void __launch_bounds__(512)
+pack_all_kernel(int K, int Kp, CanonDev C, float* ep, float* gp, float norm5) {
+    for (int kk = threadIdx.x; kk < Kp; kk += blockDim.x) pack_component(kk, K, Kp, C, ep, gp, norm5);
+}
+
+// ---------------------------------------------------------------------------
+// One stepwise M-step from the compact fp64 stats [H, wsum, W, M, Clow].
+__global__ void __launch_bounds__(512)
+mstep_kernel(int K, int Kp, const double* __restrict__ stats, int64_t nSamples, CanonDev C,
+             EmStateDev S, float* ep, float* gp, float norm5) {
+    __shared__ double sh[16];
+    extern __shared__ double newW[];
+    const int t = threadIdx.x;
+    if (t == 0) {
+        const double weightSum = stats[1];
+        sh[0] = (weightSum == 0.0) ? 0.0 : 1.0;
+        if (weightSum != 0.0) {
+            const int it = (int)S.scalars[SC_IT];
+            const double alpha = S.scalars[SC_ALPHA];
+            const double learningRate = (double)0.2f;
+            const double eta = pow(learningRate * (double)it + 1.0, -alpha);
+            double hTW = S.scalars[SC_HTW];
+            hTW *= (1.0 - eta);
+            hTW += eta * weightSum;
+            S.scalars[SC_HTW] = hTW;
+            double gH = S.scalars[SC_SGH] * (1.0 - eta);
+            gH = eta * stats[0] + gH;
+            S.scalars[SC_SGH] = gH;
+            const double norm = (double)(float)S.scalars[SC_NORM];
+            S.scalars[SC_NORM] = (double)(float)((1.0 - eta) * norm + eta * weightSum / (double)nSamples);
+            const int cutoff = (int)S.scalars[SC_CUT];
+            const int cut = (cutoff < it) ? cutoff : it;
+            const double invGlobal = 1.0 / pow(3.0, (double)cut);
+            const double invMix = 1.0 / pow(2.0, (double)cut);
+            sh[1] = eta;
+            sh[2] = weightSum;
+            sh[3] = 1.0 / hTW;
+            sh[4] = invGlobal;
+            sh[5] = invMix;
+        }
+        S.scalars[SC_STATUS] = sh[0];
+    }
+    __syncthreads();
+    if (sh[0] == 0.0) return;  // optimize() returns early when weightSum == 0
+    const double eta = sh[1], weightSum = sh[2], invTotalWeight = sh[3];
+    const double invGlobal = sh[4], invMix = sh[5];
+    const double ni = S.scalars[SC_NI];
+    const bool decreasePrior = S.scalars[SC_DECP] != 0.0;
+
+    for (int k = t; k < K; k += blockDim.x) {
+        double T = S.T[k];
+        T *= (1.0 - eta);
+        T += eta * weightSum;
+        S.T[k] = T;
+        // statsGlobal *= (1 - eta); stats.sumProductInto(statsGlobal, eta)
+        const double oneMinus = 1.0 - eta;
+        double gW = S.sgW[k] * oneMinus;
+        gW = eta * stats[2 + k] + gW;
+        double gM[5], gC[25];
+        for (int i = 0; i < 5; ++i) {
+            double v = S.sgM[5 * k + i] * oneMinus;
+            gM[i] = eta * stats[2 + K + 5 * k + i] + v;
+        }
+        for (int i = 0; i < 5; ++i)
+            for (int j = 0; j < 5; ++j) {
+                const int a = i > j ? i : j, b = i > j ? j : i;
+                const double sc = stats[2 + 6 * K + 15 * k + a * (a + 1) / 2 + b];
+                double v = S.sgC[25 * k + 5 * i + j] * oneMinus;
+                gC[5 * i + j] = eta * sc + v;
+            }
+        // statsGlobalNormalized
+        const double nW = gW * invTotalWeight;
+        double nM[5], nC[25];
+        for (int i = 0; i < 5; ++i) nM[i] = gM[i] * invTotalWeight;
+        for (int i = 0; i < 25; ++i) nC[i] = gC[i] * invTotalWeight;
+
+        double decNi = ni;
+        double decA = 100.0 / (double)K;
+        double decB[25];
+        for (int i = 0; i < 25; ++i) decB[i] = decA * (double)S.bPriors[25 * k + i];
+        if (decreasePrior) {
+            for (int i = 0; i < 25; ++i) decB[i] = decB[i] * invMix;
+            decA = decA * invMix;
+            decNi = ni * invGlobal;
+        }
+        const double invW = 1.0 / nW;
+        const double invMatNorm = 1.0 / (0.05 * decA + nW);
+        double w_new;
+        if (C.weights[k] == 0.0f) {
+            w_new = 0.0;                       // dead stays dead (:785)
+        } else if (!isfinite(invW)) {
+            w_new = decNi + nW;                // weak component (:791)
+        } else {
+            w_new = decNi + nW;
+            double mean5[5], cov[25];
+            for (int i = 0; i < 5; ++i) mean5[i] = nM[i] * invW;
+            for (int i = 0; i < 5; ++i)
+                for (int j = 0; j < 5; ++j) cov[5 * i + j] = nC[5 * i + j] - nM[i] * mean5[j];
+            for (int i = 0; i < 25; ++i) cov[i] += decB[i];
+            for (int i = 0; i < 25; ++i) cov[i] *= invMatNorm;
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) cov[5 * i + j] += (double)S.bDepth[9 * k + 3 * i + j];
+            // exp of the new tangent mean in the OLD frame (:845-852)
+            double to[9], emb[6];
+            for (int i = 0; i < 9; ++i) to[i] = (double)C.to[9 * k + i];
+            {
+                const double t0 = mean5[3], t1 = mean5[4];
+                const double length = sqrt(t0 * t0 + t1 * t1);
+                if (length >= kPi) {
+                    for (int i = 0; i < 6; ++i) emb[i] = 0.0;
+                } else {
+                    const double sc = sinc_pi_d(length);
+                    const double rel0 = t0 * sc, rel1 = t1 * sc, rel2 = cos(length);
+                    emb[0] = mean5[0]; emb[1] = mean5[1]; emb[2] = mean5[2];
+                    emb[3] = to[0] * rel0 + to[3] * rel1 + to[6] * rel2;
+                    emb[4] = to[1] * rel0 + to[4] * rel1 + to[7] * rel2;
+                    emb[5] = to[2] * rel0 + to[5] * rel1 + to[8] * rel2;
+                }
+            }
+            double Ltmp[25];
+            if (!llt_d<5>(cov, Ltmp)) {
+                w_new = 0.0;                   // non-PD: kill (:945-960)
+            } else {
+                set_component(k, emb, cov, C);
+                for (int i = 0; i < 5; ++i)
+                    for (int j = 0; j < 5; ++j) nC[5 * i + j] -= nM[i] * mean5[j];
+                const double condStat[5] = {nM[0], nM[1], nM[2], 0.0, 0.0};
+                const double condNew[5] = {mean5[0], mean5[1], mean5[2], 0.0, 0.0};
+                for (int i = 0; i < 5; ++i)
+                    for (int j = 0; j < 5; ++j) nC[5 * i + j] += condStat[i] * condNew[j];
+                for (int i = 0; i < 25; ++i) gC[i] = nC[i] * T;
+                gM[3] = 0.0;
+                gM[4] = 0.0;
+            }
+        }
+        newW[k] = w_new;
+        S.sgW[k] = gW;
+        for (int i = 0; i < 5; ++i) S.sgM[5 * k + i] = gM[i];
+        for (int i = 0; i < 25; ++i) S.sgC[25 * k + i] = gC[i];
+    }
+    __syncthreads();
+    if (t == 0) {
+        double sum = 0.0;
+        for (int k = 0; k < K; ++k) sum += newW[k];
+        if (sum != 0.0)
+            for (int k = 0; k < K; ++k) newW[k] = newW[k] / sum;
+        for (int k = 0; k < K; ++k) C.weights[k] = (float)newW[k];
+        weights_cdf(C.weights, C.cdf, K, true);
+        S.scalars[SC_IT] = S.scalars[SC_IT] + 1.0;
+    }
+    __syncthreads();
+    for (int kk = t; kk < Kp; kk += blockDim.x) pack_component(kk, K, Kp, C, ep, gp, norm5);
+}
+
+// ---------------------------------------------------------------------------
+hipError_t launch_set_all(int K, int Kp, const double* mean, const double* cov, const CanonDev& C,
+                          float* ep, float* gp, float norm5, hipStream_t st) {
+    const int threads = Kp < 64 ? 64 : (Kp > 512 ? 512 : Kp);
+    hipLaunchKernelGGL(set_all_kernel, dim3(1), dim3(threads), 0, st, K, Kp, mean, cov, C, ep, gp, norm5);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_all(int K, int Kp, const CanonDev& C, float* ep, float* gp, float norm5,
+                           hipStream_t st) {
+    hipLaunchKernelGGL(pack_all_kernel, dim3(1), dim3(256), 0, st, K, Kp, C, ep, gp, norm5);
+    return hipGetLastError();
+}
+
+hipError_t launch_mstep(int K, int Kp, const double* stats, int64_t nSamples, const CanonDev& C,
+                        const EmStateDev& S, float* ep, float* gp, float norm5, hipStream_t st) {
+    const int threads = Kp < 64 ? 64 : (Kp > 512 ? 512 : Kp);
+    hipLaunchKernelGGL(mstep_kernel, dim3(1), dim3(threads), sizeof(double) * (size_t)K, st, K, Kp,
+                       stats, nSamples, C, S, ep, gp, norm5);
+    return hipGetLastError();
+}
+
+}  // namespace sdmm

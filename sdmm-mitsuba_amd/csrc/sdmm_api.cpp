@@ -1,0 +1,602 @@
+// sdmm_api.cpp -- host runtime behind include/sdmm_gpu.h.
+//
+// Owns one mixture + its stepwise EM state on one GPU and sequences the
+// kernels of estep.hip / mstep.hip / guide.hip on the handle's HIP stream.
+// The reference counterpart is the per-leaf SDMMContext of the sdmm plugin
+// (sdmm_proc.h:92-93) driving sdmm-lib's em_step / create_conditional.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/sdmm_gpu.h"
+#include "sdmm_device.h"
+
+#pragma clang fp contract(off)
+
+namespace sdmm {
+hipError_t launch_estep_resp(int cpl, int lps, const float* ep, int Kp, int K, const SamplesDev& s,
+                             int64_t n, int64_t chunk, float* resp, hipStream_t st);
+hipError_t launch_estep_stats(int cpl, int lps, const float* ep, int Kp, int K, const SamplesDev& s,
+                              int64_t n, int64_t chunk, int blocks, int wpb, float* partials,
+                              int pstride, hipStream_t st);
+hipError_t launch_reduce_partials(const float* partials, int rows, int pstride, int Kp, int K,
+                                  double* stats, hipStream_t st);
+hipError_t launch_set_all(int K, int Kp, const double* mean, const double* cov, const CanonDev& C,
+                          float* ep, float* gp, float norm5, hipStream_t st);
+hipError_t launch_pack_all(int K, int Kp, const CanonDev& C, float* ep, float* gp, float norm5,
+                           hipStream_t st);
+hipError_t launch_mstep(int K, int Kp, const double* stats, int64_t nSamples, const CanonDev& C,
+                        const EmStateDev& S, float* ep, float* gp, float norm5, hipStream_t st);
+hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float* const c[3],
+                        const float* const u[3], float* const d[3], float* pdf, int32_t* comp,
+                        float norm2, float norm3, hipStream_t st);
+hipError_t launch_guide_pdf(const float* gp, int Kp, int K, int64_t nq, const float* const c[3],
+                            const float* const d[3], float* pdf, float norm2, float norm3,
+                            hipStream_t st);
+hipError_t launch_sample_cdf(const float* cdf, int n, const float* u, int64_t nq, int32_t* out,
+                             hipStream_t st);
+}  // namespace sdmm
+
+using namespace sdmm;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(SDMM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
+    } while (0)
+
+// (float) pow((double)(float)INV_SQRT_TWO_PI, d) -- mvtn.h:351-352
+float norm_const(int d) {
+    return (float)std::pow((double)(float)0.39894228040143267793994605993438186847585863116492, (double)d);
+}
+
+// --------------------------------------------------------------------------
+// PCG32 + uniformHemisphereInit on the host (O(K), runs once per mixture).
+struct Pcg32 {
+    uint64_t state, inc;
+    void seed(uint64_t initstate, uint64_t initseq) {
+        state = 0u;
+        inc = (initseq << 1u) | 1u;
+        next_uint();
+        state += initstate;
+        next_uint();
+    }
+    uint32_t next_uint() {
+        uint64_t old = state;
+        state = old * 0x5851f42d4c957f2dULL + inc;
+        uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = (uint32_t)(old >> 59u);
+        return (xs >> rot) | (xs << ((~rot + 1u) & 31));
+    }
+    float next_float() {
+        union { uint32_t u; float f; } x;
+        x.u = (next_uint() >> 9) | 0x3f800000u;
+        return x.f - 1.0f;
+    }
+};
+
+void coordinates_f(const float n[3], float to[9]) {
+    float sign = std::copysign(1.0f, n[2]);
+    const float a = -1.0f / (sign + n[2]);
+    const float b = n[0] * n[1] * a;
+    to[0] = 1.0f + sign * n[0] * n[0] * a; to[1] = sign * b; to[2] = -sign * n[0];
+    to[3] = b; to[4] = sign + n[1] * n[1] * a; to[5] = -n[1];
+    to[6] = n[0]; to[7] = n[1]; to[8] = n[2];
+}
+
+float fl_cos(float x) { return (float)std::cos((double)x); }
+float fl_sin(float x) { return (float)std::sin((double)x); }
+
+// mixture_model_init.h:79-242 (kMeansPlusPlus == false branch).
+void hemisphere_init(const float* positions, const float* normals, int nPositions, float depthPrior,
+                     float minDist, uint64_t seed, float* weights, float* means, float* covs,
+                     float* bpriors, float* bdepth) {
+    const double PI = 3.14159265358979323846;
+    Pcg32 rng;
+    rng.seed(seed, 0xda3e39cb94b95bdbULL);
+    const float maxRadiusSqr = (float)10.644640675668422;  // chi2(6).quantile(0.9)
+    const float widthVarSqr = (float)(0.5 * (double)minDist * (double)minDist / (double)maxRadiusSqr);
+    const float depthVarSqr = depthPrior * depthPrior / maxRadiusSqr;
+    const float nThetas = 2.0f, nPhis = 4.0f;
+    const float directionalInit = 1.0f / (nThetas * nPhis);
+    const int K = nPositions * 8;
+    int k = 0;
+    for (int pi = 0; pi < nPositions; ++pi) {
+        const float* p = positions + 3 * pi;
+        const float* n = normals + 3 * pi;
+        float to[9];
+        coordinates_f(n, to);
+        const float* s = to;
+        const float* t = to + 3;
+        float cov[25] = {0};
+        for (int i = 0; i < 5; ++i) cov[6 * i] = 1.0f;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                cov[5 * i + j] = (s[i] * s[j] * widthVarSqr + t[i] * t[j] * widthVarSqr) +
+                                 n[i] * n[j] * depthVarSqr;
+        const float dcov = (float)(2.0 * PI * (double)directionalInit);
+        cov[18] = dcov; cov[24] = dcov; cov[19] = 0.0f; cov[23] = 0.0f;
+        float bPrior[25] = {0};
+        for (int i = 0; i < 5; ++i) bPrior[6 * i] = 1.0f;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                bPrior[5 * i + j] = s[i] * s[j] * 1e-4f + t[i] * t[j] * 1e-4f + n[i] * n[j] * 1e-4f;
+        bPrior[18] = 1e-5f; bPrior[24] = 1e-5f;
+        float theta = 0.0f;
+        for (int ti = 0; ti < (int)nThetas; ++ti) {
+            float rn = (float)(((double)rng.next_float() - 0.5) * 2e-1);
+            theta = (float)((double)theta + (0.5 * PI / (double)(nThetas + 1.0f) + (double)rn));
+            const float cosTheta = fl_cos(theta);
+            const float sinTheta = std::sqrt(1.0f - cosTheta * cosTheta);
+            float phi = 0.0f;
+            for (int fi = 0; fi < (int)nPhis; ++fi) {
+                rn = (float)(((double)rng.next_float() - 0.5) * 1e-1);
+                phi = (float)((double)phi + (2.0 * PI / (double)nPhis + (double)rn));
+                const float sinPhi = fl_sin(phi), cosPhi = fl_cos(phi);
+                const float dl0 = sinTheta * cosPhi, dl1 = sinTheta * sinPhi, dl2 = cosTheta;
+                float* mean = means + 6 * k;
+                for (int i = 0; i < 3; ++i) mean[i] = p[i];
+                for (int i = 0; i < 3; ++i) mean[3 + i] = (s[i] * dl0 + t[i] * dl1) + n[i] * dl2;
+                std::memcpy(covs + 25 * k, cov, sizeof(cov));
+                weights[k] = 1.0f / (float)K;
+                std::memcpy(bpriors + 25 * k, bPrior, sizeof(bPrior));
+                for (int i = 0; i < 3; ++i)
+                    for (int j = 0; j < 3; ++j) bdepth[9 * k + 3 * i + j] = n[i] * n[j] * 1e-6f;
+                ++k;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+// ==========================================================================
+struct sdmm_mix {
+    int K = 0, Kp = 0, cpl = 1, lps = 64;
+    int device = 0;
+    int cus = 256;
+    hipStream_t stream = nullptr;
+    hipStream_t own_stream = nullptr;
+    sdmm_em_params params{};
+    float norm2 = 0, norm3 = 0, norm5 = 0;
+    bool initialised = false;
+
+    // device memory
+    void* block = nullptr;       // canonical + state + packed records
+    CanonDev C{};
+    EmStateDev S{};
+    float* ep = nullptr;
+    float* gp = nullptr;
+    double* stats = nullptr;     // compact stats (2 + 21K)
+    double* tmp_mean = nullptr;  // K*6 (set_params / init)
+    double* tmp_cov = nullptr;   // K*25
+    float* partials = nullptr;
+    int partial_rows = 0;
+    int pstride = 0;
+    // staging for host-resident samples
+    void* staging = nullptr;
+    size_t staging_bytes = 0;
+};
+
+namespace {
+
+int choose_layout(int K, int& cpl, int& lps) {
+    if (K <= 16) { lps = 16; cpl = 1; }
+    else if (K <= 32) { lps = 32; cpl = 1; }
+    else if (K <= 64) { lps = 64; cpl = 1; }
+    else if (K <= 128) { lps = 64; cpl = 2; }
+    else if (K <= 256) { lps = 64; cpl = 4; }
+    else if (K <= 512) { lps = 64; cpl = 8; }
+    else return -1;
+    return 0;
+}
+
+// Work split of an E-step launch: contiguous chunk of samples per wave.
+struct Split {
+    int64_t chunk;
+    int blocks;
+    int wpb;
+};
+
+Split split_for(const sdmm_mix* m, int64_t n) {
+    const int spw = 64 / m->lps;
+    const int64_t target_waves = (int64_t)m->cus * 8;
+    int64_t chunk = (n + target_waves - 1) / target_waves;
+    if (chunk < 4 * spw) chunk = 4 * spw;
+    chunk = ((chunk + spw - 1) / spw) * spw;
+    const int wpb = 4;
+    int64_t waves = (n + chunk - 1) / chunk;
+    int64_t blocks = (waves + wpb - 1) / wpb;
+    if (blocks < 1) blocks = 1;
+    return Split{chunk, (int)blocks, wpb};
+}
+
+SamplesDev to_dev(const sdmm_samples* s) {
+    SamplesDev d;
+    for (int i = 0; i < 6; ++i) d.x[i] = s->x[i];
+    d.w = s->w;
+    d.hpdf = s->hpdf;
+    d.isDiffuse = s->is_diffuse;
+    return d;
+}
+
+int check_samples(const sdmm_samples* s) {
+    if (!s) return fail(SDMM_E_INVALID, "samples is NULL");
+    if (s->n < 0) return fail(SDMM_E_INVALID, "negative sample count");
+    if (s->n == 0) return SDMM_OK;
+    for (int i = 0; i < 6; ++i)
+        if (!s->x[i]) return fail(SDMM_E_INVALID, "sample plane x[i] is NULL");
+    if (!s->w) return fail(SDMM_E_INVALID, "weight plane is NULL");
+    return SDMM_OK;
+}
+
+int ensure_partials(sdmm_mix* m, int rows) {
+    if (rows <= m->partial_rows) return SDMM_OK;
+    if (m->partials) HIP_TRY(hipFree(m->partials));
+    m->partials = nullptr;
+    int cap = rows < 1024 ? 1024 : rows;
+    HIP_TRY(hipMalloc(&m->partials, sizeof(float) * (size_t)cap * m->pstride));
+    m->partial_rows = cap;
+    return SDMM_OK;
+}
+
+int run_estep_stats(sdmm_mix* m, const sdmm_samples* s, double* stats_out) {
+    const Split sp = split_for(m, s->n);
+    int r = ensure_partials(m, sp.blocks);
+    if (r) return r;
+    SamplesDev d = to_dev(s);
+    HIP_TRY(launch_estep_stats(m->cpl, m->lps, m->ep, m->Kp, m->K, d, s->n, sp.chunk, sp.blocks, sp.wpb,
+                               m->partials, m->pstride, m->stream));
+    HIP_TRY(launch_reduce_partials(m->partials, sp.blocks, m->pstride, m->Kp, m->K, stats_out, m->stream));
+    return SDMM_OK;
+}
+
+}  // namespace
+
+// ==========================================================================
+extern "C" {
+
+const char* sdmm_last_error(void) { return g_err.c_str(); }
+int sdmm_abi_version(void) { return SDMM_ABI_VERSION; }
+
+void sdmm_em_params_default(sdmm_em_params* p) {
+    if (!p) return;
+    p->alpha = 0.9f;
+    for (int i = 0; i < 5; ++i) p->bprior[i] = 1e-5f;
+    p->ni_prior_minus_one = 6e-5f;
+    p->epsilon = 1e-100;
+    p->decrease_prior = 1;
+}
+
+size_t sdmm_stats_len(int K) { return 2 + (size_t)ST_FIELDS * (size_t)K; }
+
+int sdmm_create(int K, const sdmm_em_params* params, int device, sdmm_mix** out) {
+    if (!out) return fail(SDMM_E_INVALID, "out is NULL");
+    *out = nullptr;
+    int cpl, lps;
+    if (K < 1 || choose_layout(K, cpl, lps)) return fail(SDMM_E_INVALID, "K must be in [1, 512]");
+    sdmm_mix* m = new (std::nothrow) sdmm_mix();
+    if (!m) return fail(SDMM_E_NOMEM, "out of host memory");
+    m->K = K;
+    m->cpl = cpl;
+    m->lps = lps;
+    m->Kp = cpl * lps;
+    m->device = device;
+    if (params) m->params = *params; else sdmm_em_params_default(&m->params);
+    m->norm2 = norm_const(2);
+    m->norm3 = norm_const(3);
+    m->norm5 = norm_const(5);
+    m->pstride = ((ST_FIELDS * m->Kp + 2 + 3) / 4) * 4;
+
+    auto cleanup = [&](int code) { sdmm_destroy(m); return code; };
+    if (hipSetDevice(device) != hipSuccess) return cleanup(fail(SDMM_E_HIP, "hipSetDevice failed"));
+    (void)hipDeviceGetAttribute(&m->cus, hipDeviceAttributeMultiprocessorCount, device);
+    if (m->cus <= 0) m->cus = 256;
+    if (hipStreamCreateWithFlags(&m->own_stream, hipStreamNonBlocking) != hipSuccess)
+        return cleanup(fail(SDMM_E_HIP, "hipStreamCreate failed"));
+    m->stream = m->own_stream;
+
+    // one allocation for every fixed-size array (all 16-byte aligned)
+    const size_t Kc = (size_t)K;
+    const size_t f_canon = Kc * (1 + 1 + 6 + 25 + 9 + 25 + 25 + 1 + 6 + 4 + 9 + 1 + 4 + 4 + 1);
+    struct Piece { void** p; size_t bytes; };
+    std::vector<Piece> pieces;
+    float *w, *cdf, *mean, *cov, *to, *cl, *cli, *di, *mp, *cc, *ml, *mdi, *cdl, *cdli, *cdi;
+    int* valid;
+    double *sc, *T, *sgW, *sgM, *sgC;
+    float *bp, *bd;
+    auto add = [&](void* pp, size_t bytes) { pieces.push_back({(void**)pp, (bytes + 15) / 16 * 16}); };
+    add(&w, 4 * Kc); add(&cdf, 4 * Kc); add(&mean, 24 * Kc); add(&cov, 100 * Kc); add(&to, 36 * Kc);
+    add(&cl, 100 * Kc); add(&cli, 100 * Kc); add(&di, 4 * Kc); add(&mp, 24 * Kc); add(&cc, 16 * Kc);
+    add(&ml, 36 * Kc); add(&mdi, 4 * Kc); add(&cdl, 16 * Kc); add(&cdli, 16 * Kc); add(&cdi, 4 * Kc);
+    add(&valid, 4 * Kc);
+    add(&sc, 8 * SC_COUNT); add(&T, 8 * Kc); add(&sgW, 8 * Kc); add(&sgM, 40 * Kc); add(&sgC, 200 * Kc);
+    add(&bp, 100 * Kc); add(&bd, 36 * Kc);
+    add(&m->ep, 4 * (size_t)EP_FIELDS * m->Kp); add(&m->gp, 4 * (size_t)GP_FIELDS * m->Kp);
+    add(&m->stats, 8 * sdmm_stats_len(K));
+    add(&m->tmp_mean, 48 * Kc); add(&m->tmp_cov, 200 * Kc);
+    (void)f_canon;
+    size_t total = 0;
+    for (auto& pc : pieces) total += pc.bytes;
+    if (hipMalloc(&m->block, total) != hipSuccess) return cleanup(fail(SDMM_E_HIP, "hipMalloc failed"));
+    if (hipMemset(m->block, 0, total) != hipSuccess) return cleanup(fail(SDMM_E_HIP, "hipMemset failed"));
+    char* base = (char*)m->block;
+    for (auto& pc : pieces) { *pc.p = base; base += pc.bytes; }
+    m->C = CanonDev{w, cdf, mean, cov, to, cl, cli, di, mp, cc, ml, mdi, cdl, cdli, cdi, valid};
+    m->S = EmStateDev{sc, T, sgW, sgM, sgC, bp, bd};
+
+    // StepwiseTangentEM constructor state (stepwise_tangent.h:221-252)
+    double scal[SC_COUNT] = {0};
+    scal[SC_HTW] = 0.0;
+    scal[SC_SGH] = 0.0;
+    scal[SC_NORM] = 1.0;
+    scal[SC_IT] = 0.0;
+    scal[SC_ALPHA] = (double)m->params.alpha;
+    scal[SC_NI] = (double)m->params.ni_prior_minus_one;
+    scal[SC_DECP] = m->params.decrease_prior ? 1.0 : 0.0;
+    scal[SC_CUT] = 32.0;
+    std::vector<float> bpr(25 * Kc, 0.0f), bde(9 * Kc, 0.0f);
+    const float eps = (float)m->params.epsilon;
+    for (size_t k = 0; k < Kc; ++k) {
+        for (int i = 0; i < 5; ++i) bpr[25 * k + 6 * i] = m->params.bprior[i];
+        for (int i = 0; i < 3; ++i) bde[9 * k + 4 * i] = eps;
+    }
+    if (hipMemcpy(sc, scal, sizeof(scal), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(bp, bpr.data(), 100 * Kc, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(bd, bde.data(), 36 * Kc, hipMemcpyHostToDevice) != hipSuccess)
+        return cleanup(fail(SDMM_E_HIP, "hipMemcpy of the initial state failed"));
+    // packed records: every component dead until init/set_params
+    if (launch_pack_all(K, m->Kp, m->C, m->ep, m->gp, m->norm5, m->stream) != hipSuccess)
+        return cleanup(fail(SDMM_E_HIP, "pack kernel launch failed"));
+    if (hipStreamSynchronize(m->stream) != hipSuccess)
+        return cleanup(fail(SDMM_E_HIP, "hipStreamSynchronize failed"));
+    *out = m;
+    return SDMM_OK;
+}
+
+void sdmm_destroy(sdmm_mix* m) {
+    if (!m) return;
+    (void)hipSetDevice(m->device);
+    if (m->own_stream) (void)hipStreamSynchronize(m->own_stream);
+    if (m->stream && m->stream != m->own_stream) (void)hipStreamSynchronize(m->stream);
+    if (m->block) (void)hipFree(m->block);
+    if (m->partials) (void)hipFree(m->partials);
+    if (m->staging) (void)hipFree(m->staging);
+    if (m->own_stream) (void)hipStreamDestroy(m->own_stream);
+    delete m;
+}
+
+int sdmm_num_components(const sdmm_mix* m) { return m ? m->K : 0; }
+
+int sdmm_set_stream(sdmm_mix* m, void* hip_stream) {
+    if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
+    m->stream = hip_stream ? (hipStream_t)hip_stream : m->own_stream;
+    return SDMM_OK;
+}
+
+void* sdmm_get_stream(const sdmm_mix* m) { return m ? (void*)m->stream : nullptr; }
+
+int sdmm_synchronize(sdmm_mix* m) {
+    if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
+    HIP_TRY(hipStreamSynchronize(m->stream));
+    return SDMM_OK;
+}
+
+int sdmm_hemisphere_init_host(const float* positions, const float* normals, int n_pos, float depth_prior,
+                              float min_spatial_distance, uint64_t seed, float* weights, float* means,
+                              float* covs, float* bpriors, float* bdepth) {
+    if (!positions || !normals || n_pos <= 0 || !weights || !means || !covs || !bpriors || !bdepth)
+        return fail(SDMM_E_INVALID, "invalid argument to sdmm_hemisphere_init_host");
+    hemisphere_init(positions, normals, n_pos, depth_prior, min_spatial_distance, seed, weights, means,
+                    covs, bpriors, bdepth);
+    return SDMM_OK;
+}
+
+static int upload_and_set(sdmm_mix* m, const float* weights, const float* means, const float* covs) {
+    const size_t K = (size_t)m->K;
+    std::vector<double> md(6 * K), cd(25 * K);
+    for (size_t i = 0; i < 6 * K; ++i) md[i] = (double)means[i];
+    for (size_t i = 0; i < 25 * K; ++i) cd[i] = (double)covs[i];
+    HIP_TRY(hipMemcpyAsync(m->tmp_mean, md.data(), 8 * 6 * K, hipMemcpyHostToDevice, m->stream));
+    HIP_TRY(hipMemcpyAsync(m->tmp_cov, cd.data(), 8 * 25 * K, hipMemcpyHostToDevice, m->stream));
+    HIP_TRY(hipMemcpyAsync(m->C.weights, weights, 4 * K, hipMemcpyHostToDevice, m->stream));
+    HIP_TRY(launch_set_all(m->K, m->Kp, m->tmp_mean, m->tmp_cov, m->C, m->ep, m->gp, m->norm5, m->stream));
+    HIP_TRY(hipStreamSynchronize(m->stream));  // host vectors go out of scope
+    m->initialised = true;
+    return SDMM_OK;
+}
+
+int sdmm_init_hemisphere(sdmm_mix* m, const float* positions, const float* normals, int n_pos,
+                         float depth_prior, float min_spatial_distance, uint64_t seed) {
+    if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
+    if (n_pos * 8 != m->K) return fail(SDMM_E_INVALID, "K must equal 8 * n_pos");
+    const size_t K = (size_t)m->K;
+    std::vector<float> w(K), mean(6 * K), cov(25 * K), bp(25 * K), bd(9 * K);
+    int r = sdmm_hemisphere_init_host(positions, normals, n_pos, depth_prior, min_spatial_distance, seed,
+                                      w.data(), mean.data(), cov.data(), bp.data(), bd.data());
+    if (r) return r;
+    HIP_TRY(hipMemcpyAsync(m->S.bPriors, bp.data(), 4 * 25 * K, hipMemcpyHostToDevice, m->stream));
+    HIP_TRY(hipMemcpyAsync(m->S.bDepth, bd.data(), 4 * 9 * K, hipMemcpyHostToDevice, m->stream));
+    return upload_and_set(m, w.data(), mean.data(), cov.data());
+}
+
+int sdmm_set_params(sdmm_mix* m, const float* weights, const float* means, const float* covs) {
+    if (!m || !weights || !means || !covs) return fail(SDMM_E_INVALID, "invalid argument");
+    return upload_and_set(m, weights, means, covs);
+}
+
+int sdmm_estep_stats(sdmm_mix* m, const sdmm_samples* s, double* stats) {
+    if (!m || !stats) return fail(SDMM_E_INVALID, "invalid argument");
+    if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
+    int r = check_samples(s);
+    if (r) return r;
+    if (s->n == 0) {
+        HIP_TRY(hipMemsetAsync(stats, 0, 8 * sdmm_stats_len(m->K), m->stream));
+        return SDMM_OK;
+    }
+    return run_estep_stats(m, s, stats);
+}
+
+int sdmm_mstep(sdmm_mix* m, const double* stats, int64_t n_total) {
+    if (!m || !stats) return fail(SDMM_E_INVALID, "invalid argument");
+    if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
+    HIP_TRY(launch_mstep(m->K, m->Kp, stats, n_total, m->C, m->S, m->ep, m->gp, m->norm5, m->stream));
+    return SDMM_OK;
+}
+
+int sdmm_em_step(sdmm_mix* m, const sdmm_samples* s, int iterations) {
+    if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
+    if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
+    int r = check_samples(s);
+    if (r) return r;
+    if (s->n == 0) return SDMM_OK;  // weightSum == 0: optimize() returns early
+    for (int it = 0; it < iterations; ++it) {
+        r = run_estep_stats(m, s, m->stats);
+        if (r) return r;
+        HIP_TRY(launch_mstep(m->K, m->Kp, m->stats, s->n, m->C, m->S, m->ep, m->gp, m->norm5, m->stream));
+    }
+    return SDMM_OK;
+}
+
+int sdmm_em_step_host(sdmm_mix* m, const sdmm_samples* s, int iterations) {
+    if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
+    int r = check_samples(s);
+    if (r) return r;
+    if (s->n == 0) return SDMM_OK;
+    const size_t n = (size_t)s->n;
+    const size_t need = n * (7 * 4 + 4 + 1) + 64;
+    if (need > m->staging_bytes) {
+        if (m->staging) HIP_TRY(hipFree(m->staging));
+        m->staging = nullptr;
+        HIP_TRY(hipMalloc(&m->staging, need));
+        m->staging_bytes = need;
+    }
+    float* f = (float*)m->staging;
+    sdmm_samples d{};
+    for (int i = 0; i < 6; ++i) {
+        HIP_TRY(hipMemcpyAsync(f + i * n, s->x[i], 4 * n, hipMemcpyHostToDevice, m->stream));
+        d.x[i] = f + i * n;
+    }
+    HIP_TRY(hipMemcpyAsync(f + 6 * n, s->w, 4 * n, hipMemcpyHostToDevice, m->stream));
+    d.w = f + 6 * n;
+    if (s->hpdf) {
+        HIP_TRY(hipMemcpyAsync(f + 7 * n, s->hpdf, 4 * n, hipMemcpyHostToDevice, m->stream));
+        d.hpdf = f + 7 * n;
+    }
+    if (s->is_diffuse) {
+        HIP_TRY(hipMemcpyAsync(f + 8 * n, s->is_diffuse, n, hipMemcpyHostToDevice, m->stream));
+        d.is_diffuse = (const uint8_t*)(f + 8 * n);
+    }
+    d.n = s->n;
+    r = sdmm_em_step(m, &d, iterations);
+    if (r) return r;
+    HIP_TRY(hipStreamSynchronize(m->stream));  // the host planes may be reused on return
+    return SDMM_OK;
+}
+
+int sdmm_responsibilities(sdmm_mix* m, const sdmm_samples* s, float* resp) {
+    if (!m || !resp) return fail(SDMM_E_INVALID, "invalid argument");
+    if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
+    int r = check_samples(s);
+    if (r) return r;
+    if (s->n == 0) return SDMM_OK;
+    const Split sp = split_for(m, s->n);
+    HIP_TRY(launch_estep_resp(m->cpl, m->lps, m->ep, m->Kp, m->K, to_dev(s), s->n, sp.chunk, resp,
+                              m->stream));
+    return SDMM_OK;
+}
+
+int sdmm_guide_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], const float* const u[3],
+                     float* const d[3], float* pdf, int32_t* comp) {
+    if (!m || !c || !u || !d || !pdf || !comp) return fail(SDMM_E_INVALID, "invalid argument");
+    if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
+    HIP_TRY(launch_guide(m->gp, m->Kp, m->K, nq, c, u, d, pdf, comp, m->norm2, m->norm3, m->stream));
+    return SDMM_OK;
+}
+
+int sdmm_pdf_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], const float* const d[3],
+                   float* pdf) {
+    if (!m || !c || !d || !pdf) return fail(SDMM_E_INVALID, "invalid argument");
+    if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
+    HIP_TRY(launch_guide_pdf(m->gp, m->Kp, m->K, nq, c, d, pdf, m->norm2, m->norm3, m->stream));
+    return SDMM_OK;
+}
+
+int sdmm_sample_discrete_cdf(const sdmm_mix* m, const float* cdf, int n, const float* u, int64_t nq,
+                             int32_t* out) {
+    if (!m || !cdf || n <= 0 || !u || !out) return fail(SDMM_E_INVALID, "invalid argument");
+    HIP_TRY(launch_sample_cdf(cdf, n, u, nq, out, m->stream));
+    return SDMM_OK;
+}
+
+int sdmm_get_params(const sdmm_mix* m, const sdmm_params_out* o) {
+    if (!m || !o) return fail(SDMM_E_INVALID, "invalid argument");
+    const size_t K = (size_t)m->K;
+    hipStream_t st = m->stream;
+    struct Item { void* dst; const void* src; size_t bytes; };
+    const Item items[] = {
+        {o->weights, m->C.weights, 4 * K}, {o->cdf, m->C.cdf, 4 * K}, {o->mean, m->C.mean, 24 * K},
+        {o->cov, m->C.cov, 100 * K}, {o->to, m->C.to, 36 * K}, {o->cholL, m->C.cholL, 100 * K},
+        {o->cholLInv, m->C.cholLInv, 100 * K}, {o->detInv, m->C.detInv, 4 * K},
+        {o->muPremult, m->C.muPremult, 24 * K}, {o->condCov, m->C.condCov, 16 * K},
+        {o->margL, m->C.margL, 36 * K}, {o->margDetInv, m->C.margDetInv, 4 * K},
+        {o->condL, m->C.condL, 16 * K}, {o->condLInv, m->C.condLInv, 16 * K},
+        {o->condDetInv, m->C.condDetInv, 4 * K}, {o->valid, m->C.valid, 4 * K},
+    };
+    for (const Item& it : items)
+        if (it.dst) HIP_TRY(hipMemcpyAsync(it.dst, it.src, it.bytes, hipMemcpyDeviceToHost, st));
+    double sc[SC_COUNT];
+    HIP_TRY(hipMemcpyAsync(sc, m->S.scalars, sizeof(sc), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (o->normalization) *o->normalization = (float)sc[SC_NORM];
+    return SDMM_OK;
+}
+
+int sdmm_get_state(const sdmm_mix* m, double* scalars, double* T, double* sgW, double* sgM, double* sgC,
+                   float* bpriors, float* bdepth) {
+    if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
+    const size_t K = (size_t)m->K;
+    hipStream_t st = m->stream;
+    if (scalars) HIP_TRY(hipMemcpyAsync(scalars, m->S.scalars, 8 * SC_COUNT, hipMemcpyDeviceToHost, st));
+    if (T) HIP_TRY(hipMemcpyAsync(T, m->S.T, 8 * K, hipMemcpyDeviceToHost, st));
+    if (sgW) HIP_TRY(hipMemcpyAsync(sgW, m->S.sgW, 8 * K, hipMemcpyDeviceToHost, st));
+    if (sgM) HIP_TRY(hipMemcpyAsync(sgM, m->S.sgM, 40 * K, hipMemcpyDeviceToHost, st));
+    if (sgC) HIP_TRY(hipMemcpyAsync(sgC, m->S.sgC, 200 * K, hipMemcpyDeviceToHost, st));
+    if (bpriors) HIP_TRY(hipMemcpyAsync(bpriors, m->S.bPriors, 100 * K, hipMemcpyDeviceToHost, st));
+    if (bdepth) HIP_TRY(hipMemcpyAsync(bdepth, m->S.bDepth, 36 * K, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return SDMM_OK;
+}
+
+int sdmm_set_state(sdmm_mix* m, const double* scalars, const double* T, const double* sgW, const double* sgM,
+                   const double* sgC, const float* bpriors, const float* bdepth) {
+    if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
+    const size_t K = (size_t)m->K;
+    hipStream_t st = m->stream;
+    if (scalars) HIP_TRY(hipMemcpyAsync(m->S.scalars, scalars, 8 * SC_COUNT, hipMemcpyHostToDevice, st));
+    if (T) HIP_TRY(hipMemcpyAsync(m->S.T, T, 8 * K, hipMemcpyHostToDevice, st));
+    if (sgW) HIP_TRY(hipMemcpyAsync(m->S.sgW, sgW, 8 * K, hipMemcpyHostToDevice, st));
+    if (sgM) HIP_TRY(hipMemcpyAsync(m->S.sgM, sgM, 40 * K, hipMemcpyHostToDevice, st));
+    if (sgC) HIP_TRY(hipMemcpyAsync(m->S.sgC, sgC, 200 * K, hipMemcpyHostToDevice, st));
+    if (bpriors) HIP_TRY(hipMemcpyAsync(m->S.bPriors, bpriors, 100 * K, hipMemcpyHostToDevice, st));
+    if (bdepth) HIP_TRY(hipMemcpyAsync(m->S.bDepth, bdepth, 36 * K, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return SDMM_OK;
+}
+
+}  // extern "C"

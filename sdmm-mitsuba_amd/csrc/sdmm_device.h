@@ -1,0 +1,141 @@
+// sdmm_device.h -- device-side layouts and helpers shared by the gfx950 kernels.
+//
+// HBM layouts (all SoA so a wave's 64 lanes touch consecutive addresses):
+//   samples      x0..x5, w, [hpdf], [isDiffuse]  one plane per field, N each
+//   E-step param ep[f * Kp + k], f < EP_FIELDS    (component k on lane k / CPL)
+//   guide param  gp[f * Kp + k], f < GP_FIELDS
+//   stats        compact double [H, wsum, W(K), M(5K), Clow(15K)]  (2 + 21K)
+//   partials     float [G][PSTRIDE], one row per E-step workgroup
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sdmm {
+
+// ---- E-step component record (per component k, SoA over k) -----------------
+// mu_p (3) | L^{-1} lower 5x5 row-major (15) | to rows 0..2 (9) | detInv | pi
+// (pi = 0 for dead/padded components).  The pdf is evaluated in the
+// reference's factor order NORM5*exp(-q/2) -> *detInv*J -> *pi so that, with
+// the kernel in FTZ/DAZ mode, underflow flushes where the reference's
+// flushDenormals=true build flushes (volpath_sdmm.cpp:88-90).
+enum : int {
+    EP_MU0 = 0, EP_MU1, EP_MU2,
+    EP_L00, EP_L10, EP_L11, EP_L20, EP_L21, EP_L22,
+    EP_L30, EP_L31, EP_L32, EP_L33,
+    EP_L40, EP_L41, EP_L42, EP_L43, EP_L44,
+    EP_R00, EP_R01, EP_R02, EP_R10, EP_R11, EP_R12, EP_R20, EP_R21, EP_R22,
+    EP_DI, EP_PI,
+    EP_FIELDS
+};
+
+// ---- guide record (per joint component) -------------------------------------
+enum : int {
+    GP_W = 0,                            // mixture weight pi_k
+    GP_MU0, GP_MU1, GP_MU2,              // spatial mean (marginal mean)
+    GP_ML00, GP_ML10, GP_ML11, GP_ML20, GP_ML21, GP_ML22,  // marginal LLT lower
+    GP_MDI,                              // marginal detInv
+    GP_P00, GP_P01, GP_P02, GP_P10, GP_P11, GP_P12,        // muPremult 2x3
+    GP_T00, GP_T01, GP_T02, GP_T10, GP_T11, GP_T12, GP_T20, GP_T21, GP_T22, // to
+    GP_CL00, GP_CL10, GP_CL11,           // conditional LLT (2x2 lower)
+    GP_CI00, GP_CI01, GP_CI10, GP_CI11,  // conditional L^{-1}
+    GP_CDI,                              // conditional detInv
+    GP_FIELDS
+};
+
+// Per-component sufficient statistics accumulated by the E-step.
+enum : int {
+    ST_W = 0, ST_M0, ST_M1, ST_M2, ST_M3, ST_M4,
+    ST_C00, ST_C10, ST_C11, ST_C20, ST_C21, ST_C22,
+    ST_C30, ST_C31, ST_C32, ST_C33, ST_C40, ST_C41, ST_C42, ST_C43, ST_C44,
+    ST_FIELDS  // 21
+};
+
+// Canonical per-component arrays (same names/widths as the oracle's or_mixture,
+// oracle/sdmm_oracle.h) kept on the device for export and the M-step.
+struct CanonDev {
+    float* weights;    // K
+    float* cdf;        // K
+    float* mean;       // K*6
+    float* cov;        // K*25
+    float* to;         // K*9
+    float* cholL;      // K*25
+    float* cholLInv;   // K*25
+    float* detInv;     // K
+    float* muPremult;  // K*6
+    float* condCov;    // K*4
+    float* margL;      // K*9
+    float* margDetInv; // K
+    float* condL;      // K*4
+    float* condLInv;   // K*4
+    float* condDetInv; // K
+    int* valid;        // K
+};
+
+// Stepwise EM state (stepwise_tangent.h:181-210), device resident, fp64.
+struct EmStateDev {
+    double* scalars;   // [0]=heuristicTotalWeight [1]=sgH [2]=normalization
+                       // [3]=iterationsRun [4]=alpha [5]=niPriorMinusOne
+                       // [6]=decreasePrior [7]=trainingCutoff [8]=last status
+    double* T;         // K   totalWeightForMixture
+    double* sgW;       // K
+    double* sgM;       // K*5
+    double* sgC;       // K*25 (full, the reference keeps full 5x5)
+    float* bPriors;    // K*25
+    float* bDepth;     // K*9
+};
+
+enum : int {
+    SC_HTW = 0, SC_SGH, SC_NORM, SC_IT, SC_ALPHA, SC_NI, SC_DECP, SC_CUT, SC_STATUS, SC_COUNT
+};
+
+struct SamplesDev {
+    const float* x[6];
+    const float* w;
+    const float* hpdf;          // nullable
+    const uint8_t* isDiffuse;   // nullable
+};
+
+constexpr float kHeuristicWeight = 0.5f;     // mixture_model.h:398
+constexpr double kPi = 3.14159265358979323846;
+
+// Constant address space: uniform loads from it become scalar (SMEM) loads.
+typedef const float __attribute__((address_space(4)))* cfloat_p;
+typedef const uint8_t __attribute__((address_space(4)))* cu8_p;
+
+// ---- wave-level helpers (wave64) -------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ float dpp(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+        0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over aligned groups of G lanes (G in {16, 32, 64}); every lane of the
+// group receives the group sum.  quad_perm/mirror DPP reduce within rows of
+// 16 lanes; rows are then combined through v_readlane (SGPR) reads.  (The
+// gfx950 permlane16/32 swaps would save two instructions, but ROCm 7.2 folds
+// swap(x, x) into x + x, so they are not used.)
+template <int G>
+__device__ __forceinline__ float group_sum(float x) {
+    x += dpp<0xB1>(x);   // quad_perm [1,0,3,2]  (xor 1)
+    x += dpp<0x4E>(x);   // quad_perm [2,3,0,1]  (xor 2)
+    x += dpp<0x141>(x);  // row_half_mirror      (pairs within 8)
+    x += dpp<0x140>(x);  // row_mirror           (pairs within 16)
+    if constexpr (G == 64) {
+        const int xi = __builtin_bit_cast(int, x);
+        const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(xi, 0));
+        const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(xi, 16));
+        const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(xi, 32));
+        const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(xi, 48));
+        x = (r0 + r1) + (r2 + r3);
+    } else if constexpr (G == 32) {
+        const int xi = __builtin_bit_cast(int, x);
+        const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(xi, 0));
+        const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(xi, 16));
+        const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(xi, 32));
+        const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(xi, 48));
+        x = ((threadIdx.x & 63) < 32) ? (r0 + r1) : (r2 + r3);
+    }
+    return x;
+}
+
+}  // namespace sdmm

@@ -1,0 +1,60 @@
+"""Test configuration: markers, package loading and shared fixtures.
+
+`-m "not gpu"` tests run on CPU (oracle KATs, golden fixtures, C-ABI symbol
+table, host logic, gloo world_size-2 sharding).  `-m gpu` tests are the parity
+tests proper: they call the HIP library through the C ABI and compare it with
+the CPU oracle (oracle/) on the same seeded inputs.
+"""
+import importlib.util
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+if str(ROOT) not in sys.path:
+    sys.path.insert(0, str(ROOT))
+
+
+def load_pkg():
+    name = "sdmm_mitsuba_amd"
+    if name in sys.modules:
+        return sys.modules[name]
+    pkg_dir = ROOT / "sdmm-mitsuba_amd"
+    spec = importlib.util.spec_from_file_location(name, pkg_dir / "__init__.py",
+                                                  submodule_search_locations=[str(pkg_dir)])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) and the built HIP library")
+
+
+@pytest.fixture(scope="session")
+def pkg():
+    return load_pkg()
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from oracle import oracle as o
+    o.build()
+    return o
+
+
+@pytest.fixture(scope="session")
+def synth(pkg):
+    import importlib
+    return importlib.import_module("sdmm_mitsuba_amd.synth")
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda:0")

@@ -1,0 +1,298 @@
+"""GPU parity tests: the HIP path (through the C ABI) vs the CPU oracle.
+
+Tolerances (stated here, see DESIGN.md "Parity"):
+  * responsibilities: judged against an fp64 evaluation of the same float
+    parameters: max |gpu - exact| <= 4 * max |oracle_fp32 - exact| + 1e-5 (both
+    fp32 paths carry the rounding of q, the squared Mahalanobis distance, which
+    for far samples (q ~ 1e3..1e5) is ~q*6e-8 in the exponent), and
+    |gpu - oracle| <= 2e-5 on samples the mixture explains (max posterior of
+    the fp64 evaluation found at q < 100);
+  * sufficient statistics: relative 2e-5 of each statistic's scale;
+  * mixture parameters after EM iterations (north star): weights, means and
+    covariances within 1e-4 relative (covariances scaled by sqrt(S_ii S_jj));
+  * guided sampling: component indices BIT-EXACT; directions 1e-5, pdf 1e-4 rel.
+"""
+import numpy as np
+import pytest
+
+from helpers import posterior_f64
+
+pytestmark = pytest.mark.gpu
+
+RTOL_PARAMS = 1e-4
+
+
+def _check_resp(got, ref, params, x):
+    """got: GPU, ref: fp32 oracle, exact: fp64 of the same parameters."""
+    exact = posterior_f64(params, x)
+    live = ref.sum(1) > 0
+    # FTZ boundary: rows whose every component underflows in one path only
+    mism = live != (got.sum(1) > 0)
+    assert mism.mean() <= 2e-3, f"{mism.sum()} rows live in only one path"
+    both = live & ~mism
+    eg = np.abs(got[both] - exact[both]).max(initial=0.0)
+    eo = np.abs(ref[both] - exact[both]).max(initial=0.0)
+    assert eg <= 4 * eo + 1e-5, f"gpu err {eg} vs oracle-fp32 err {eo}"
+    np.testing.assert_allclose(got[both].sum(1), 1.0, atol=1e-5)
+    return eg, eo
+
+
+def _setup(pkg, oracle, synth, K, N, heuristic=False, guards=True, mode=1):
+    import torch
+    b = synth.em_batch(N, 128, heuristic=heuristic, guards=guards)
+    pos, nrm = synth.model_seed_points(b, max(K, 8))
+    n_pos = K // 8
+    pos, nrm = pos[:n_pos], nrm[:n_pos]
+    mix = pkg.SDMM(K)
+    mix.init_hemisphere(pos, nrm, synth.DEPTH_PRIOR, synth.SPATIAL_DISTANCE, synth.SEED_MODEL)
+    om, ost = oracle.hemisphere_init(n_pos, pos, nrm, synth.DEPTH_PRIOR, synth.SPATIAL_DISTANCE,
+                                     synth.SEED_MODEL, mode=mode)
+    ds = pkg.DeviceSamples.from_numpy(b["x"], b["w"], b["hpdf"], b["is_diffuse"])
+    os_ = oracle.Samples(b["x"], b["w"], b["hpdf"], b["is_diffuse"])
+    return b, mix, om, ost, ds, os_
+
+
+def _cov_close(a, b, rtol):
+    a = a.reshape(-1, 5, 5).astype(np.float64)
+    b = b.reshape(-1, 5, 5).astype(np.float64)
+    d = np.sqrt(np.abs(np.einsum("kii->ki", b)))
+    scale = d[:, :, None] * d[:, None, :]
+    err = np.abs(a - b) / np.maximum(scale, 1e-30)
+    return float(err.max())
+
+
+def _full_stats(compact, K):
+    """compact [H, ws, W, M, Clow] -> oracle layout [H, ws, W, M, C(25)]."""
+    H, ws = compact[0], compact[1]
+    W = compact[2:2 + K]
+    M = compact[2 + K:2 + 6 * K]
+    Cl = compact[2 + 6 * K:].reshape(K, 15)
+    C = np.zeros((K, 5, 5))
+    e = 0
+    for i in range(5):
+        for j in range(i + 1):
+            C[:, i, j] = Cl[:, e]
+            C[:, j, i] = Cl[:, e]
+            e += 1
+    return np.concatenate([[H, ws], W, M, C.reshape(-1)])
+
+
+@pytest.mark.parametrize("K", [16, 32, 64, 128, 256])
+def test_init_params_match_oracle(pkg, oracle, synth, gpu, K):
+    b, mix, om, ost, ds, os_ = _setup(pkg, oracle, synth, K, 256)
+    p = mix.get_params()
+    for name in ("weights", "cdf", "mean", "cov", "to", "cholL", "cholLInv", "detInv", "muPremult",
+                 "condCov", "margL", "margDetInv", "condL", "condLInv", "condDetInv"):
+        np.testing.assert_allclose(p[name], getattr(om, name), rtol=2e-6, atol=1e-7, err_msg=name)
+    assert (p["valid"] == 1).all()
+
+
+@pytest.mark.parametrize("K,N", [(16, 4099), (32, 2048), (64, 3000), (128, 4096), (256, 1500), (512, 700)])
+def test_responsibilities_match_oracle(pkg, oracle, synth, gpu, K, N):
+    import torch
+    b, mix, om, ost, ds, os_ = _setup(pkg, oracle, synth, K, N)
+    resp = torch.full((N, K), -1.0, device=gpu)
+    mix.posterior(ds, resp)
+    torch.cuda.synchronize()
+    got = resp.cpu().numpy()
+    ref = oracle.responsibilities(om, os_)
+    assert np.isfinite(got).all()
+    _check_resp(got, ref, mix.get_params(), b["x"])
+
+
+@pytest.mark.parametrize("heuristic", [False, True])
+def test_responsibilities_heuristic(pkg, oracle, synth, gpu, heuristic):
+    import torch
+    K, N = 128, 2048
+    b, mix, om, ost, ds, os_ = _setup(pkg, oracle, synth, K, N, heuristic=heuristic)
+    resp = torch.empty((N, K), device=gpu)
+    mix.posterior(ds, resp)
+    got = resp.cpu().numpy()
+    ref = oracle.responsibilities(om, os_)
+    if not heuristic:
+        _check_resp(got, ref, mix.get_params(), b["x"])
+    else:
+        live = ref.sum(1) > 0
+        assert np.abs(got[live] - ref[live]).max() <= 1e-3
+        # sum_k posterior = (1-h) S / ((1-h) S + h hpdf) on diffuse samples
+        np.testing.assert_allclose(got.sum(1)[live], ref.sum(1)[live], atol=1e-5)
+
+
+@pytest.mark.parametrize("K,N,heuristic", [(16, 5000, False), (128, 8192, False), (128, 4096, True),
+                                           (256, 3000, False), (512, 1024, False), (32, 999, True)])
+def test_stats_match_oracle(pkg, oracle, synth, gpu, K, N, heuristic):
+    import torch
+    b, mix, om, ost, ds, os_ = _setup(pkg, oracle, synth, K, N, heuristic=heuristic)
+    st = torch.zeros(pkg.stats_len(K), dtype=torch.float64, device=gpu)
+    mix.estep_stats(ds, st)
+    got = _full_stats(st.cpu().numpy(), K)
+    ref = oracle.calculate_stats(om, os_, accurate=True)
+    # weightSum counts finite weights only; H and W, M, C relative to their scale
+    np.testing.assert_allclose(got[1], ref[1], rtol=1e-6)
+    np.testing.assert_allclose(got[0], ref[0], rtol=2e-5, atol=1e-6 * abs(ref[1]))
+    W, Wr = got[2:2 + K], ref[2:2 + K]
+    np.testing.assert_allclose(W, Wr, rtol=2e-5, atol=1e-6 * ref[1])
+    M, Mr = got[2 + K:2 + 6 * K].reshape(K, 5), ref[2 + K:2 + 6 * K].reshape(K, 5)
+    np.testing.assert_allclose(M, Mr, rtol=2e-5, atol=2e-6 * ref[1])
+    Cg, Cr = got[2 + 6 * K:].reshape(K, 25), ref[2 + 6 * K:].reshape(K, 25)
+    np.testing.assert_allclose(Cg, Cr, rtol=2e-5, atol=2e-6 * ref[1])
+
+
+@pytest.mark.parametrize("K,N,iters,heuristic", [(128, 16384, 5, False), (16, 8192, 6, True),
+                                                 (256, 6000, 3, False)])
+def test_em_matches_oracle(pkg, oracle, synth, gpu, K, N, iters, heuristic):
+    """StepwiseTangentEM::optimize x iters: params within 1e-4 of the oracle."""
+    b, mix, om, ost, ds, os_ = _setup(pkg, oracle, synth, K, N, heuristic=heuristic)
+    for _ in range(iters):
+        mix.optimize(ds)
+        assert oracle.optimize(om, ost, os_, accurate=True) == 1
+    p = mix.get_params()
+    st = mix.get_state()
+    assert int(st["scalars"][3]) == iters
+    np.testing.assert_allclose(p["weights"], om.weights, rtol=RTOL_PARAMS, atol=1e-7)
+    np.testing.assert_allclose(p["mean"], om.mean, rtol=RTOL_PARAMS, atol=RTOL_PARAMS)
+    assert _cov_close(p["cov"], om.cov, RTOL_PARAMS) <= RTOL_PARAMS
+    np.testing.assert_allclose(p["normalization"], om.s.normalization, rtol=1e-5)
+    np.testing.assert_array_equal(p["weights"] > 0, om.weights > 0)
+
+
+def test_em_faithful_oracle_within_reference_noise(pkg, oracle, synth, gpu):
+    """Against the fp32 'faithful' oracle the agreement is the reference's own
+    fp32 noise (~1e-4 relative); reported, looser bound."""
+    K, N = 128, 16384
+    b, mix, om, ost, ds, os_ = _setup(pkg, oracle, synth, K, N, mode=0)
+    for _ in range(3):
+        mix.optimize(ds)
+        oracle.optimize(om, ost, os_, accurate=False)
+    p = mix.get_params()
+    np.testing.assert_allclose(p["weights"], om.weights, rtol=2e-3, atol=1e-6)
+    assert _cov_close(p["cov"], om.cov, 1e-2) <= 1e-2
+
+
+def test_em_split_phase_equals_fused(pkg, oracle, synth, gpu):
+    """estep_stats + mstep (the multi-GPU path) == em_step."""
+    import torch
+    K, N = 128, 8192
+    b, mix, om, ost, ds, os_ = _setup(pkg, oracle, synth, K, N)
+    mix2 = pkg.SDMM(K)
+    pos, nrm = synth.model_seed_points(b, K)
+    mix2.init_hemisphere(pos, nrm, synth.DEPTH_PRIOR, synth.SPATIAL_DISTANCE, synth.SEED_MODEL)
+    st = torch.zeros(pkg.stats_len(K), dtype=torch.float64, device=gpu)
+    for _ in range(3):
+        mix.optimize(ds)
+        # two shards summed on the device == one batch
+        s0, s1 = ds.shard(0, 2), ds.shard(1, 2)
+        a = torch.zeros_like(st)
+        mix2.estep_stats(s0, st)
+        a += st
+        mix2.synchronize()
+        mix2.estep_stats(s1, st)
+        mix2.synchronize()
+        a += st
+        mix2.mstep(a, N)
+    p, q = mix.get_params(), mix2.get_params()
+    np.testing.assert_allclose(q["weights"], p["weights"], rtol=1e-5, atol=1e-8)
+    assert _cov_close(q["cov"], p["cov"], 1e-5) <= 1e-5
+
+
+def test_em_guards(pkg, oracle, synth, gpu):
+    """weightSum == 0 -> optimize() is a no-op; empty batches are no-ops."""
+    import torch
+    K, N = 64, 1024
+    b, mix, om, ost, ds, os_ = _setup(pkg, oracle, synth, K, N)
+    before = mix.get_params()
+    zero = pkg.DeviceSamples(ds.x, torch.zeros_like(ds.w))
+    mix.optimize(zero)
+    nan = pkg.DeviceSamples(ds.x, torch.full_like(ds.w, float("nan")))
+    mix.optimize(nan)
+    empty = pkg.DeviceSamples([t[:0] for t in ds.x], ds.w[:0])
+    mix.optimize(empty)
+    after = mix.get_params()
+    np.testing.assert_array_equal(before["weights"], after["weights"])
+    np.testing.assert_array_equal(before["cov"], after["cov"])
+    assert int(mix.get_state()["scalars"][3]) == 0
+
+
+def test_zero_direction_samples(pkg, oracle, synth, gpu):
+    """d == 0 fails the log map (pdf 0, posterior all zero), like the oracle."""
+    import torch
+    K, N = 128, 512
+    b, mix, om, ost, ds, os_ = _setup(pkg, oracle, synth, K, N)
+    x = [t.clone() for t in ds.x]
+    for i in (3, 4, 5):
+        x[i][::7] = 0.0
+    d2 = pkg.DeviceSamples(x, ds.w)
+    resp = torch.empty((N, K), device=gpu)
+    mix.posterior(d2, resp)
+    got = resp.cpu().numpy()
+    xs = np.stack([t.cpu().numpy() for t in x])
+    ref = oracle.responsibilities(om, oracle.Samples(xs, b["w"]))
+    _check_resp(got, ref, mix.get_params(), xs)
+    assert (got[::7] == 0).all()
+
+
+def _em_model(pkg, oracle, synth, K, N, iters):
+    b, mix, om, ost, ds, os_ = _setup(pkg, oracle, synth, K, N)
+    for _ in range(iters):
+        mix.optimize(ds)
+    p = mix.get_params()
+    m = oracle.Mixture(K)
+    m.copy_params_from(p)
+    m.valid[:] = p["valid"]
+    return b, mix, m
+
+
+@pytest.mark.parametrize("K,iters", [(16, 3), (128, 4), (256, 2)])
+def test_guide_indices_bit_exact(pkg, oracle, synth, gpu, K, iters):
+    import torch
+    b, mix, om = _em_model(pkg, oracle, synth, K, 8192, iters)
+    nq = 4096
+    c, u = synth.sample_queries_near(b, nq // 2)
+    c2, u2 = synth.queries(nq // 2)
+    c = np.concatenate([c, c2], 1)
+    u = np.concatenate([u, u2], 1)
+    ct = [torch.from_numpy(c[i].copy()).to(gpu) for i in range(3)]
+    ut = [torch.from_numpy(u[i].copy()).to(gpu) for i in range(3)]
+    d, pdf, comp = mix.guide(ct, ut)
+    torch.cuda.synchronize()
+    dg = np.stack([t.cpu().numpy() for t in d], 1)
+    pg, cg = pdf.cpu().numpy(), comp.cpu().numpy()
+    dr, pr, cr, sr = oracle.guide_batch(om, c.T, u.T)
+    np.testing.assert_array_equal(cg, cr)            # bit-exact component selection
+    np.testing.assert_allclose(dg, dr, atol=1e-5)
+    np.testing.assert_allclose(pg, pr, rtol=1e-4, atol=1e-7)
+    # the sampled directions are unit vectors and the pdf is positive there
+    ok = cr >= 0
+    np.testing.assert_allclose(np.linalg.norm(dg[ok], axis=1), 1.0, atol=1e-5)
+
+
+def test_pdf_batch_matches_oracle(pkg, oracle, synth, gpu):
+    import torch
+    K = 128
+    b, mix, om = _em_model(pkg, oracle, synth, K, 8192, 3)
+    c, u = synth.sample_queries_near(b, 2048)
+    rng = np.random.default_rng(7)
+    d = rng.normal(size=(3, 2048)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=0, keepdims=True)
+    ct = [torch.from_numpy(c[i].copy()).to(gpu) for i in range(3)]
+    dt = [torch.from_numpy(d[i].copy()).to(gpu) for i in range(3)]
+    got = mix.pdf(ct, dt).cpu().numpy()
+    ref = oracle.pdf_batch(om, c.T, d.T)
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-7)
+
+
+def test_sample_discrete_cdf_bit_exact(pkg, oracle, gpu):
+    import torch
+    mix = pkg.SDMM(16)
+    rng = np.random.default_rng(3)
+    for n in (1, 2, 7, 64, 513):
+        w = rng.random(n).astype(np.float32)
+        w[rng.random(n) < 0.3] = 0.0                       # ties in the CDF
+        if w.sum() == 0:
+            w[0] = 1
+        cdf = np.cumsum(w / w.sum(), dtype=np.float32)
+        u = np.concatenate([rng.random(997).astype(np.float32), cdf, np.nextafter(cdf, 2),
+                            np.float32([0.0, 0.99999994, 1.0])]).astype(np.float32)
+        got = mix.sample_discrete_cdf(torch.from_numpy(cdf).to(gpu), torch.from_numpy(u).to(gpu))
+        ref = np.array([oracle.sample_discrete_cdf(cdf, x) for x in u])
+        np.testing.assert_array_equal(got.cpu().numpy(), ref)
