@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""Benchmark: EM samples/sec (N x K responsibilities) at K=128, N=2^20.
+
+Headline step (BASELINE.json `metric`, configs[1]): one responsibility E-step
+(MixtureModel::posteriorAndLog for every sample, mixture_model.h:146-192 --
+the N x K hot loop of StepwiseTangentEM, stepwise_tangent.h:270-353) over a
+synthetic batch of N = 2^20 samples against a K = 128 mixture that has been
+through 5 warm EM iterations.  Inputs (SoA fp32 planes) are resident in HBM
+before timing; the N x K fp32 responsibilities are written to HBM.
+
+Multi-GPU (torchrun, one process per GPU): the N samples are sharded
+contiguously across ranks (strong scaling, no data-path collective for the
+E-step); warm EM iterations all-reduce the fp64 sufficient statistics with
+RCCL before each M-step.  value = N / max-over-ranks step time.
+
+Also reported (same JSON line): the full EM step (E-step + statistics +
+all-reduce + M-step), guided queries/sec (conditional + sample + pdf, Q = 2^20,
+replicas), the roofline of the dominant kernel (HIP events on the kernel's
+stream) and the CPU baseline (the C oracle on the host cores, bounded sample).
+"""
+import argparse
+import importlib.util
+import json
+import os
+import sys
+import threading
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+PKG_DIR = ROOT / "sdmm-mitsuba_amd"
+HBM_PEAK = 8.0e12            # B/s, MI355X spec (MI355X_MICROARCH.md)
+FP32_PEAK = 157.3e12         # FLOP/s vector fp32 spec
+
+
+def load_pkg():
+    name = "sdmm_mitsuba_amd"
+    if name in sys.modules:
+        return sys.modules[name]
+    spec = importlib.util.spec_from_file_location(name, PKG_DIR / "__init__.py",
+                                                  submodule_search_locations=[str(PKG_DIR)])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(batch, K, pos, nrm, synth, n_sample, threads):
+    """The CPU oracle (faithful fp32 restatement of jmm) on the host cores.
+    Measures the same responsibility E-step on a bounded sample."""
+    sys.path.insert(0, str(ROOT))
+    from oracle import oracle as orc
+    orc.build()
+    m, _ = orc.hemisphere_init(K // 8, pos, nrm, synth.DEPTH_PRIOR, synth.SPATIAL_DISTANCE,
+                               synth.SEED_MODEL, mode=0)
+    x, w = batch["x"][:, :n_sample], batch["w"][:n_sample]
+
+    def run(nthreads, n_sample):
+        per = (n_sample + nthreads - 1) // nthreads
+        shards = []
+        for t in range(nthreads):
+            a, b = t * per, min(n_sample, (t + 1) * per)
+            shards.append(orc.Samples(x[:, a:b], w[a:b]))
+        outs = [None] * nthreads
+
+        def work(t):
+            outs[t] = orc.responsibilities(m, shards[t])
+        ths = [threading.Thread(target=work, args=(t,)) for t in range(nthreads)]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        return time.perf_counter() - t0
+
+    tn = run(threads, n_sample)
+    n1 = min(n_sample, 1 << 18)
+    t1 = run(1, n1)
+    return {"value": n_sample / tn, "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"{n_sample} of the {batch['w'].shape[0]} samples x K={K}, oracle "
+                      f"or_responsibilities (faithful fp32 jmm restatement), {threads} host threads, "
+                      f"sample-sharded", "seconds": tn,
+            "single_thread": {"value": n1 / t1, "cores": 1, "sample": f"{n1} samples", "seconds": t1}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--K", type=int, default=128)
+    ap.add_argument("--N", type=int, default=1 << 20)
+    ap.add_argument("--Q", type=int, default=1 << 20)
+    ap.add_argument("--em-warm", type=int, default=5)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="headline E-step only (profiling)")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 20)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    pkg = load_pkg()
+    synth = importlib.import_module("sdmm_mitsuba_amd.synth")
+    K, N = args.K, args.N
+
+    t0 = time.perf_counter()
+    batch = synth.em_batch(N, 128)
+    pos, nrm = synth.model_seed_points(batch, K)
+    log(f"[bench] rank {rank}/{world}: synthetic batch N={N} in {time.perf_counter() - t0:.1f}s")
+    full = pkg.DeviceSamples.from_numpy(batch["x"], batch["w"], batch["hpdf"], batch["is_diffuse"],
+                                        device=dev)
+    shard = full.shard(rank, world) if world > 1 else full
+    n_local = shard.n
+
+    stream = torch.cuda.current_stream(dev)
+    mix = pkg.SDMM(K, device=dev.index, stream=stream)
+    mix.init_hemisphere(pos, nrm, synth.DEPTH_PRIOR, synth.SPATIAL_DISTANCE, synth.SEED_MODEL)
+    stats = torch.zeros(pkg.stats_len(K), dtype=torch.float64, device=dev)
+
+    def em_step():
+        if world > 1:
+            mix.estep_stats(shard, stats)
+            dist.all_reduce(stats)                 # RCCL sum of sufficient statistics
+            mix.mstep(stats, N)
+        else:
+            mix.optimize(shard)
+
+    for _ in range(args.em_warm):                  # 5 warm EM iterations
+        em_step()
+    torch.cuda.synchronize()
+
+    resp = torch.empty((n_local, K), dtype=torch.float32, device=dev)
+
+    def estep():
+        mix.posterior(shard, resp)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def timed(fn, steps, events=True):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * steps)] if events else None
+        barrier()
+        t = time.perf_counter()
+        for i in range(steps):
+            if events:
+                ev[2 * i].record(stream)
+            fn()
+            if events:
+                ev[2 * i + 1].record(stream)
+        barrier()
+        wall = time.perf_counter() - t
+        wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
+        kern = None
+        if events:
+            torch.cuda.synchronize()
+            kern = float(np.mean([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(steps)])) * 1e-3
+        return float(wall_t.item()), kern
+
+    # ---- headline: responsibility E-step --------------------------------
+    for _ in range(args.warmup):
+        estep()
+    wall, kern = timed(estep, args.steps)
+    ms_per_step = wall / args.steps * 1e3
+    value = N / (wall / args.steps)
+    bytes_per_launch = n_local * (28 + 4 * K)
+    flops_per_launch = n_local * K * 66.0
+    achieved = bytes_per_launch / kern
+    log(f"[bench] E-step: {ms_per_step:.3f} ms/step wall, kernel {kern * 1e6:.1f} us, "
+        f"{achieved / 1e12:.2f} TB/s")
+
+    out = {
+        "metric": "EM samples/sec (NxK resp) at K=128, N=2^20",
+        "value": value,
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (BASELINE.md 2: 2^20 samples from a K=128 uniformHemisphereInit "
+                "generator, LogNormal weights with 0.1% zero / 0.01% non-finite; model after 5 EM steps)",
+        "config": {"workload": "responsibility E-step, synthetic 5D sample batch (configs[1])",
+                   "K": K, "N": N, "global_batch": N, "samples_per_gpu": n_local,
+                   "parallelism": f"sample-sharded x{world}", "layout": "SoA fp32 in, [N][K] fp32 out"},
+        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK, "traffic": None,
+                     "kernel": "estep_resp_kernel<CPL=2,LPS=64>",
+                     "bytes_per_launch": bytes_per_launch, "kernel_us": kern * 1e6,
+                     "fp32_frac": flops_per_launch / kern / FP32_PEAK},
+    }
+    pmc = ROOT / "profiles" / "round1_pmc_estep.json"
+    if pmc.exists() and world == 1:
+        try:
+            pm = json.loads(pmc.read_text())
+            if pm.get("K") == K and pm.get("N") == N:
+                out["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            pass
+
+    if not args.no_extra:
+        # ---- full EM step (E-step stats + reduce + [all-reduce] + M-step) ----
+        em_wall, _ = timed(em_step, max(5, args.steps // 2), events=False)
+        em_steps = max(5, args.steps // 2)
+        out["em_step"] = {"samples_per_s": N / (em_wall / em_steps), "ms_per_step": em_wall / em_steps * 1e3}
+        # ---- fused stats kernel alone (per rank) ----
+        st_wall, st_kern = timed(lambda: mix.estep_stats(shard, stats), args.steps)
+        out["estep_stats"] = {"ms_per_step": st_wall / args.steps * 1e3, "samples_per_s": N / (st_wall / args.steps)}
+        # ---- guided queries (replicas: each rank serves Q/world queries) ----
+        q_local = args.Q // world
+        c, u = synth.sample_queries_near(batch, q_local, seed=synth.SEED_QUERIES + rank)
+        ct = [torch.from_numpy(c[i].copy()).to(dev) for i in range(3)]
+        ut = [torch.from_numpy(u[i].copy()).to(dev) for i in range(3)]
+        gout = ([torch.empty(q_local, device=dev) for _ in range(3)], torch.empty(q_local, device=dev),
+                torch.empty(q_local, device=dev, dtype=torch.int32))
+        mix.guide(ct, ut, gout)
+        g_steps = max(3, args.steps // 4)
+        g_wall, g_kern = timed(lambda: mix.guide(ct, ut, gout), g_steps)
+        out["guide"] = {"queries_per_s": q_local * world / (g_wall / g_steps), "Q": q_local * world,
+                        "ms_per_step": g_wall / g_steps * 1e3, "bytes_per_query": 48,
+                        "kernel_us": g_kern * 1e6}
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            out["cpu_baseline"] = cpu_baseline(batch, K, pos, nrm, synth, min(args.cpu_sample, N),
+                                               args.cpu_threads)
+        except Exception as e:  # the baseline is reported, never required
+            out["cpu_baseline"] = {"value": None, "error": repr(e)}
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

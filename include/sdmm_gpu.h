@@ -83,7 +83,10 @@ void sdmm_em_params_default(sdmm_em_params* p);
 int sdmm_create(int K, const sdmm_em_params* params, int device, sdmm_mix** out);
 void sdmm_destroy(sdmm_mix* m);
 int sdmm_num_components(const sdmm_mix* m);
-int sdmm_set_stream(sdmm_mix* m, void* hip_stream);   /* NULL: the handle's own stream */
+/* Work is enqueued on this hipStream_t, taken literally (NULL = the HIP null
+ * stream).  A new handle starts on its own non-blocking stream, whose value
+ * sdmm_get_stream returns before any sdmm_set_stream call. */
+int sdmm_set_stream(sdmm_mix* m, void* hip_stream);
 void* sdmm_get_stream(const sdmm_mix* m);
 int sdmm_synchronize(sdmm_mix* m);
 

@@ -78,6 +78,7 @@ def lib():
                                        C.c_double, C.c_int]
         L.or_mstep_f32.argtypes = [C.c_void_p, C.c_void_p, _d, C.c_int64]
         L.or_mstep_f64.argtypes = [C.c_void_p, C.c_void_p, _d, C.c_int64]
+        L.or_mstep_x64.argtypes = [C.c_void_p, C.c_void_p, _d, C.c_int64]
         L.or_guide_batch.argtypes = [C.c_void_p, C.c_int64, _f, _f, _f, _f,
                                      C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         L.or_pdf_batch.argtypes = [C.c_void_p, C.c_int64, _f, _f, _f]
@@ -207,22 +208,27 @@ def stats_len(K):
     return 2 + 31 * K
 
 
+_SFX = {"faithful": "f32", "accurate": "f64", "exact": "x64", True: "f64", False: "f32"}
+
+
+def _mode(accurate):
+    """accurate: True/False (accurate/faithful) or 'faithful'|'accurate'|'exact'."""
+    return _SFX[accurate]
+
+
 def calculate_stats(m: Mixture, s: Samples, accurate=True):
     out = np.zeros(stats_len(m.K))
-    f = lib().or_calculate_stats_f64 if accurate else lib().or_calculate_stats_f32
-    f(m.ptr, s.ptr, _dp(out))
+    getattr(lib(), "or_calculate_stats_" + _mode(accurate))(m.ptr, s.ptr, _dp(out))
     return out
 
 
 def mstep(m: Mixture, st: EmState, stats: np.ndarray, n_samples: int, accurate=True):
-    f = lib().or_mstep_f64 if accurate else lib().or_mstep_f32
     st_ = np.ascontiguousarray(stats, np.float64)
-    return f(m.ptr, st.ptr, _dp(st_), n_samples)
+    return getattr(lib(), "or_mstep_" + _mode(accurate))(m.ptr, st.ptr, _dp(st_), n_samples)
 
 
 def optimize(m: Mixture, st: EmState, s: Samples, accurate=True):
-    f = lib().or_optimize_f64 if accurate else lib().or_optimize_f32
-    return f(m.ptr, st.ptr, s.ptr)
+    return getattr(lib(), "or_optimize_" + _mode(accurate))(m.ptr, st.ptr, s.ptr)
 
 
 def responsibilities(m: Mixture, s: Samples):

@@ -509,21 +509,73 @@ void or_responsibilities(const or_mixture* m, const or_samples* s, float* out) {
 }
 
 /* ------------------------------------------------------------------------ */
-/* EM, instantiated twice (faithful float / accurate double).                */
+/* "exact" E-step term: w_k * pdf_k(x) of mvtn.h:350-365 evaluated in double
+ * from the float parameters, flushing where the reference's fp32 FTZ build
+ * flushes (NORM*exp -> *detInv*J -> *w_k); tangent spatial part = p.        */
+static double ftz_d(double v) { return (fabs(v) < (double)1.17549435082228750797e-38F) ? 0.0 : v; }
+
+static double posterior_term_exact(const or_mixture* m, int k, const float xf[6], double tangent[5]) {
+    const float* mf = m->mean + 6 * k;
+    const float* tof = m->to + 9 * k;
+    const double d0 = xf[3], d1 = xf[4], d2 = xf[5];
+    for (int i = 0; i < 5; ++i) tangent[i] = 0.0;
+    if (d0 == 0.0 && d1 == 0.0 && d2 == 0.0) return 0.0;
+    const double r0 = (double)tof[0] * d0 + (double)tof[1] * d1 + (double)tof[2] * d2;
+    const double r1 = (double)tof[3] * d0 + (double)tof[4] * d1 + (double)tof[5] * d2;
+    double c = (double)tof[6] * d0 + (double)tof[7] * d1 + (double)tof[8] * d2;
+    if (c <= -1.0) return 0.0;
+    c = (c < 1.0) ? c : 1.0;
+    const double angle = acos(c);
+    const double sn = sqrt(1.0 - c * c);
+    const double a = (sn < 1e-3) ? 1.0 : angle / sn;
+    double t[5] = {(double)xf[0] - (double)mf[0], (double)xf[1] - (double)mf[1],
+                   (double)xf[2] - (double)mf[2], r0 * a, r1 * a};
+    const float* Li = m->cholLInv + 25 * k;
+    double q = 0.0;
+    for (int i = 0; i < 5; ++i) {
+        double u = 0.0;
+        for (int j = 0; j < 5; ++j) u += (double)Li[5 * i + j] * t[j];
+        q += u * u;
+    }
+    static float NORM5 = -1.0f;
+    if (NORM5 < 0.0f) NORM5 = norm_const(5);
+    const double p1 = ftz_d((double)NORM5 * exp(-0.5 * q));
+    const double p2 = ftz_d(p1 * ftz_d((double)m->detInv[k] * a));
+    tangent[0] = xf[0]; tangent[1] = xf[1]; tangent[2] = xf[2];
+    tangent[3] = t[3]; tangent[4] = t[4];
+    return ftz_d((double)m->weights[k] * p2);
+}
+
+/* EM, instantiated three times: faithful (float), accurate (float per-pair
+ * math, double accumulation and M-step), exact (double per-pair math too). */
 #define ACC float
 #define ACC_IS_FLOAT 1
+#define EXACT_E 0
 #define FN(x) x##_f32
 #include "sdmm_oracle_em.inc"
 #undef ACC
 #undef ACC_IS_FLOAT
+#undef EXACT_E
 #undef FN
 
 #define ACC double
 #define ACC_IS_FLOAT 0
+#define EXACT_E 0
 #define FN(x) x##_f64
 #include "sdmm_oracle_em.inc"
 #undef ACC
 #undef ACC_IS_FLOAT
+#undef EXACT_E
+#undef FN
+
+#define ACC double
+#define ACC_IS_FLOAT 0
+#define EXACT_E 1
+#define FN(x) x##_x64
+#include "sdmm_oracle_em.inc"
+#undef ACC
+#undef ACC_IS_FLOAT
+#undef EXACT_E
 #undef FN
 
 void or_em_state_init(or_em_state* st, int K, double alpha, const double bPrior5[5],

@@ -126,6 +126,12 @@ EXPORTED_SYMBOLS = [
 ]
 
 
+def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
+    """[a, b) of the contiguous sample shard owned by `rank` of `world`."""
+    per = (n + world - 1) // world
+    return min(n, rank * per), min(n, (rank + 1) * per)
+
+
 def hemisphere_init_host(positions, normals, depth_prior, min_dist, seed):
     """uniformHemisphereInit on the host (no device needed): initial params."""
     pos = np.ascontiguousarray(positions, np.float32).reshape(-1, 3)
@@ -174,8 +180,7 @@ class DeviceSamples:
 
     def shard(self, rank: int, world: int) -> "DeviceSamples":
         """Contiguous sample range of `rank` (SURVEY 8e partitioning)."""
-        per = (self.n + world - 1) // world
-        a, b = min(self.n, rank * per), min(self.n, (rank + 1) * per)
+        a, b = shard_range(self.n, rank, world)
         sl = lambda t: None if t is None else t[a:b]
         return DeviceSamples([t[a:b] for t in self.x], self.w[a:b], sl(self.hpdf), sl(self.is_diffuse))
 
@@ -205,8 +210,9 @@ class SDMM:
         # stream; the C ABI's own default is a private non-blocking stream).
         if stream is None:
             import torch
-            stream = torch.cuda.current_stream() if torch.cuda.is_available() else None
-        if stream is not None:
+            if torch.cuda.is_available():
+                self.set_stream(torch.cuda.current_stream())
+        else:
             self.set_stream(stream)
 
     def close(self):
@@ -224,7 +230,7 @@ class SDMM:
     def set_stream(self, stream):
         """stream: a torch.cuda.Stream, a raw hipStream_t int, or None."""
         ptr = getattr(stream, "cuda_stream", stream)
-        _check(lib().sdmm_set_stream(self.h, ptr))
+        _check(lib().sdmm_set_stream(self.h, C.c_void_p(ptr or 0)))
 
     @property
     def stream_ptr(self) -> int:

@@ -221,35 +221,40 @@ estep_stats_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, in
         const float w = use ? sv.w : 0.0f;
         const float hpost = (fin && sv.diffuse) ? kHeuristicWeight * sv.h * inv : 0.0f;
         accH = fmaf(w, hpost, accH);
-        const float p0 = sv.x0, p1 = sv.x1, p2 = sv.x2;
-        const float pp00 = p0 * p0, pp10 = p1 * p0, pp11 = p1 * p1;
-        const float pp20 = p2 * p0, pp21 = p2 * p1, pp22 = p2 * p2;
+        // Spatial statistics are accumulated centred on the component's mean
+        // position (tp = p - mu_k, already formed by pair_pdf) and un-centred in
+        // fp64 by finalize_stats_kernel: the M-step's C/W - mu mu^T then does
+        // not amplify fp32 accumulation error by |p|^2 / sigma^2.
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const float gam = q[c] * gsc;
             // posterior < 1e-10 is skipped (:312); unused samples have w == 0
             const float v = (gam < 1e-10f || !use) ? 0.0f : w * gam;
+            const float tp0 = sv.x0 - P.v[c][EP_MU0];
+            const float tp1 = sv.x1 - P.v[c][EP_MU1];
+            const float tp2 = sv.x2 - P.v[c][EP_MU2];
             float* A = acc[c];
             A[ST_W] += v;
-            A[ST_M0] = fmaf(v, p0, A[ST_M0]);
-            A[ST_M1] = fmaf(v, p1, A[ST_M1]);
-            A[ST_M2] = fmaf(v, p2, A[ST_M2]);
+            const float v0 = v * tp0, v1 = v * tp1, v2 = v * tp2;
+            A[ST_M0] += v0;
+            A[ST_M1] += v1;
+            A[ST_M2] += v2;
             const float v3 = v * ta[c], v4 = v * tb[c];
             A[ST_M3] += v3;
             A[ST_M4] += v4;
-            A[ST_C00] = fmaf(v, pp00, A[ST_C00]);
-            A[ST_C10] = fmaf(v, pp10, A[ST_C10]);
-            A[ST_C11] = fmaf(v, pp11, A[ST_C11]);
-            A[ST_C20] = fmaf(v, pp20, A[ST_C20]);
-            A[ST_C21] = fmaf(v, pp21, A[ST_C21]);
-            A[ST_C22] = fmaf(v, pp22, A[ST_C22]);
-            A[ST_C30] = fmaf(v3, p0, A[ST_C30]);
-            A[ST_C31] = fmaf(v3, p1, A[ST_C31]);
-            A[ST_C32] = fmaf(v3, p2, A[ST_C32]);
+            A[ST_C00] = fmaf(v0, tp0, A[ST_C00]);
+            A[ST_C10] = fmaf(v1, tp0, A[ST_C10]);
+            A[ST_C11] = fmaf(v1, tp1, A[ST_C11]);
+            A[ST_C20] = fmaf(v2, tp0, A[ST_C20]);
+            A[ST_C21] = fmaf(v2, tp1, A[ST_C21]);
+            A[ST_C22] = fmaf(v2, tp2, A[ST_C22]);
+            A[ST_C30] = fmaf(v3, tp0, A[ST_C30]);
+            A[ST_C31] = fmaf(v3, tp1, A[ST_C31]);
+            A[ST_C32] = fmaf(v3, tp2, A[ST_C32]);
             A[ST_C33] = fmaf(v3, ta[c], A[ST_C33]);
-            A[ST_C40] = fmaf(v4, p0, A[ST_C40]);
-            A[ST_C41] = fmaf(v4, p1, A[ST_C41]);
-            A[ST_C42] = fmaf(v4, p2, A[ST_C42]);
+            A[ST_C40] = fmaf(v4, tp0, A[ST_C40]);
+            A[ST_C41] = fmaf(v4, tp1, A[ST_C41]);
+            A[ST_C42] = fmaf(v4, tp2, A[ST_C42]);
             A[ST_C43] = fmaf(v4, ta[c], A[ST_C43]);
             A[ST_C44] = fmaf(v4, tb[c], A[ST_C44]);
         }
@@ -340,6 +345,33 @@ reduce_partials_kernel(const float* __restrict__ partials, int rows, int pstride
     }
 }
 
+// Un-centre the spatial statistics of component k (fp64, in place):
+//   M_p = M'_p + W mu,  C_pp = C'_pp + M'_p mu^T + mu M'_p^T + W mu mu^T,
+//   C_tp = C'_tp + M_t mu^T   (mu = the float mean the E-step subtracted).
+__global__ void finalize_stats_kernel(const float* __restrict__ ep, int Kp, int K,
+                                      double* __restrict__ stats) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= K) return;
+    double* W = stats + 2 + k;
+    double* M = stats + 2 + K + 5 * k;
+    double* C = stats + 2 + 6 * K + 15 * k;   // lower triangle, row-major
+    const double mu[3] = {(double)ep[EP_MU0 * Kp + k], (double)ep[EP_MU1 * Kp + k],
+                          (double)ep[EP_MU2 * Kp + k]};
+    const double w = *W;
+    const double mp[3] = {M[0], M[1], M[2]};
+    // C_pp (entries 0..5: (0,0) (1,0) (1,1) (2,0) (2,1) (2,2))
+    int e = 0;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j <= i; ++j, ++e)
+            C[e] += mp[i] * mu[j] + mu[i] * mp[j] + w * mu[i] * mu[j];
+    // C_tp: rows 3, 4 (entries 6..8 and 10..12)
+    for (int j = 0; j < 3; ++j) {
+        C[6 + j] += M[3] * mu[j];
+        C[10 + j] += M[4] * mu[j];
+    }
+    for (int i = 0; i < 3; ++i) M[i] = mp[i] + w * mu[i];
+}
+
 // ---------------------------------------------------------------------------
 // host-side launch helpers (called from sdmm_api.cpp)
 template <int CPL, int LPS>
@@ -398,11 +430,16 @@ hipError_t launch_estep_stats(int cpl, int lps, const float* ep, int Kp, int K, 
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_reduce_partials(const float* partials, int rows, int pstride, int Kp, int K,
+hipError_t launch_reduce_partials(const float* partials, int rows, int pstride, const float* ep_for_finalize,
+                                  int Kp, int K,
                                   double* stats, hipStream_t st) {
     const int ncols = 2 + ST_FIELDS * K;
     hipLaunchKernelGGL(reduce_partials_kernel, dim3((ncols + 63) / 64), dim3(1024), 0, st,
                        partials, rows, pstride, Kp, K, stats);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(finalize_stats_kernel, dim3((K + 255) / 256), dim3(256), 0, st, ep_for_finalize,
+                       Kp, K, stats);
     return hipGetLastError();
 }
 

@@ -24,7 +24,8 @@ hipError_t launch_estep_resp(int cpl, int lps, const float* ep, int Kp, int K, c
 hipError_t launch_estep_stats(int cpl, int lps, const float* ep, int Kp, int K, const SamplesDev& s,
                               int64_t n, int64_t chunk, int blocks, int wpb, float* partials,
                               int pstride, hipStream_t st);
-hipError_t launch_reduce_partials(const float* partials, int rows, int pstride, int Kp, int K,
+hipError_t launch_reduce_partials(const float* partials, int rows, int pstride, const float* ep_for_finalize,
+                                  int Kp, int K,
                                   double* stats, hipStream_t st);
 hipError_t launch_set_all(int K, int Kp, const double* mean, const double* cov, const CanonDev& C,
                           float* ep, float* gp, float norm5, hipStream_t st);
@@ -262,7 +263,8 @@ int run_estep_stats(sdmm_mix* m, const sdmm_samples* s, double* stats_out) {
     SamplesDev d = to_dev(s);
     HIP_TRY(launch_estep_stats(m->cpl, m->lps, m->ep, m->Kp, m->K, d, s->n, sp.chunk, sp.blocks, sp.wpb,
                                m->partials, m->pstride, m->stream));
-    HIP_TRY(launch_reduce_partials(m->partials, sp.blocks, m->pstride, m->Kp, m->K, stats_out, m->stream));
+    HIP_TRY(launch_reduce_partials(m->partials, sp.blocks, m->pstride, m->ep, m->Kp, m->K, stats_out,
+                                   m->stream));
     return SDMM_OK;
 }
 
@@ -385,7 +387,7 @@ int sdmm_num_components(const sdmm_mix* m) { return m ? m->K : 0; }
 
 int sdmm_set_stream(sdmm_mix* m, void* hip_stream) {
     if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
-    m->stream = hip_stream ? (hipStream_t)hip_stream : m->own_stream;
+    m->stream = (hipStream_t)hip_stream;  // taken literally: NULL is the HIP null stream
     return SDMM_OK;
 }
 

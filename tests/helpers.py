@@ -2,6 +2,20 @@
 import numpy as np
 
 NORM5 = float(np.float32(np.float32(0.3989422804014327) ** 5))
+FLT_MIN = float(np.finfo(np.float32).tiny)
+
+
+def _ftz(a):
+    """Flush the values an fp32 FTZ/DAZ evaluation would flush (the plugin's
+    flushDenormals=true, volpath_sdmm.cpp:88-90)."""
+    return np.where(np.abs(a) < FLT_MIN, 0.0, a)
+
+
+def _pdf_ftz(q, di, a, w):
+    """pi_k * NORM5 * exp(-q/2) * detInv * J with the fp32 flush points."""
+    p1 = _ftz(NORM5 * np.exp(-0.5 * q))
+    p2 = _ftz(p1 * _ftz(di * a))
+    return _ftz(w * p2)
 
 
 def posterior_f64(mix_params: dict, x: np.ndarray) -> np.ndarray:
@@ -24,10 +38,69 @@ def posterior_f64(mix_params: dict, x: np.ndarray) -> np.ndarray:
     tau = np.concatenate([p[:, None, :] - mean[None, :, :3], (r[..., :2] * a[..., None])], -1)
     u = np.einsum("kij,nkj->nki", Li, tau)
     q = (u * u).sum(-1)
-    pdf = NORM5 * np.exp(-0.5 * q) * di[None] * a
-    pdf[bad] = 0
-    post = w[None] * pdf
+    post = _pdf_ftz(q, di[None], a, w[None])
+    post[bad] = 0
     S = post.sum(1, keepdims=True)
     with np.errstate(invalid="ignore", divide="ignore"):
         out = np.where(S > 0, post / S, 0.0)
     return out
+
+
+def estep_f64(mix_params: dict, x, w, hpdf=None, is_diffuse=None, h=0.5, chunk=2048):
+    """calculateStats + sumWeights (stepwise_tangent.h:270-353, :462-475) in
+    float64 from the float mixture parameters.  Returns the oracle stats
+    layout [H, weightSum, W(K), M(5K), C(25K)]."""
+    wt = np.asarray(mix_params["weights"], np.float64)
+    mean = np.asarray(mix_params["mean"], np.float64).reshape(-1, 6)
+    to = np.asarray(mix_params["to"], np.float64).reshape(-1, 3, 3)
+    Li = np.asarray(mix_params["cholLInv"], np.float64).reshape(-1, 5, 5)
+    di = np.asarray(mix_params["detInv"], np.float64)
+    K = wt.shape[0]
+    x = np.asarray(x, np.float64)
+    w = np.asarray(w, np.float64)
+    N = w.shape[0]
+    hp = np.zeros(N) if hpdf is None else np.asarray(hpdf, np.float64)
+    isd = np.zeros(N, bool) if is_diffuse is None else np.asarray(is_diffuse) != 0
+    fin = np.isfinite(w)
+    wsum = w[fin].sum()
+    H = 0.0
+    W = np.zeros(K)
+    M = np.zeros((K, 5))
+    C = np.zeros((K, 5, 5))
+    for a in range(0, N, chunk):
+        sl = slice(a, min(N, a + chunk))
+        ww = w[sl]
+        use = np.isfinite(ww) & (ww != 0)
+        p, d = x[0:3, sl].T, x[3:6, sl].T
+        r = np.einsum("kij,nj->nki", to, d)
+        c = r[..., 2]
+        bad = (c <= -1) | (np.abs(d).sum(1) == 0)[:, None]
+        cc = np.minimum(c, 1.0)
+        th = np.arccos(np.clip(cc, -1, 1))
+        s = np.sqrt(np.maximum(1 - cc * cc, 0))
+        aa = np.where(s < 1e-3, 1.0, th / np.where(s > 0, s, 1))
+        tdir = r[..., :2] * aa[..., None]
+        tau_rel = np.concatenate([p[:, None, :] - mean[None, :, :3], tdir], -1)
+        u = np.einsum("kij,nkj->nki", Li, tau_rel)
+        q = (u * u).sum(-1)
+        post = _pdf_ftz(q, di[None], aa, wt[None])
+        post[bad] = 0
+        S = post.sum(1)
+        dd = isd[sl]
+        S2 = np.where(dd, (1 - h) * S + h * hp[sl], S)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            inv = 1.0 / S2
+        ok = np.isfinite(inv)
+        g = np.where(ok, np.where(dd, inv * (1 - h), inv), 0.0)
+        gam = post * g[:, None]
+        with np.errstate(invalid="ignore"):
+            hpost = np.where(ok & dd, h * hp[sl] * inv, 0.0)
+        H += (np.where(use, ww, 0) * hpost).sum()
+        with np.errstate(invalid="ignore"):
+            v = np.where((gam >= 1e-10) & use[:, None], ww[:, None] * gam, 0.0)
+        tau = np.concatenate([np.broadcast_to(p[:, None, :], tdir.shape[:2] + (3,)), tdir], -1)
+        tau = np.where(bad[..., None], 0.0, tau)
+        W += v.sum(0)
+        M += np.einsum("nk,nki->ki", v, tau)
+        C += np.einsum("nk,nki,nkj->kij", v, tau, tau)
+    return np.concatenate([[H, wsum], W, M.reshape(-1), C.reshape(-1)])

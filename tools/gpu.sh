@@ -1,0 +1,17 @@
+#!/bin/bash
+# Run a command on the GPU box via gpurun; retry only when the infrastructure
+# (not our command) failed: box not prepared / no slot (status transient, rc 3).
+# Usage: tools/gpu.sh TIMEOUT 'command'
+T=$1; shift
+for attempt in 1 2 3 4; do
+  rm -f gpurun_out/.last_call.json
+  /usr/local/graft/bin/gpurun --timeout "$T" -- "$@" > /tmp/gpurun_last.out 2>&1
+  rc=$?
+  st=$(python3 -c "import json;print(json.load(open('gpurun_out/.last_call.json'))['status'])" 2>/dev/null)
+  if [ "$st" = "transient" ] || [ $rc -eq 3 ]; then
+    echo "[gpu.sh] transient infrastructure failure (attempt $attempt), retrying in 30s"; sleep 30; continue
+  fi
+  tail -3 /tmp/gpurun_last.out
+  exit $rc
+done
+echo "[gpu.sh] giving up after repeated transient failures"; exit 3
