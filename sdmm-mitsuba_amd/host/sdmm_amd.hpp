@@ -1,0 +1,160 @@
+// sdmm_amd.hpp -- C++ host-side mirror of the guiding interface the Mitsuba
+// `sdmm` integrator plugin uses, layered over the C ABI (include/sdmm_gpu.h).
+//
+// The plugin (mitsuba/src/integrators/sdmm/volpath_sdmm.cpp, sdmm_proc.cpp)
+// drives sdmm-lib through a handful of free functions on per-leaf contexts:
+//   sdmm::initialize(sdmm, em, data, rng, n_spatial, dist)  volpath_sdmm.cpp:135
+//   sdmm::em_step(sdmm, em, training_data)                  volpath_sdmm.cpp:220,304
+//   sdmm::prepare(conditioner, sdmm)                        volpath_sdmm.cpp:237,307
+//   sdmm::create_conditional(conditioner, cond, conditional) sdmm_proc.cpp:368
+//   conditional.sample(rng, embedded, inv_jacobian, tangent) sdmm_proc.cpp:411-421
+//   posterior + hsum_nested -> gmmPdf                        sdmm_proc.cpp:539-545
+//   context.data.push_back(point6, normal3, weight)          sdmm_proc.cpp:894-902
+// This header offers the same verbs with the same argument meaning, but the
+// per-bounce calls are batched: a Mitsuba worker appends its bounce queries to
+// a GuidingBatch and the whole wavefront is answered by one kernel launch.
+// Errors surface as sdmm_amd::Error (the C ABI itself never throws).
+#pragma once
+
+#include <cstdint>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/sdmm_gpu.h"
+
+namespace sdmm_amd {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& what) : std::runtime_error(what), code(c) {}
+};
+
+inline void check(int rc, const char* where) {
+    if (rc != SDMM_OK) throw Error(rc, std::string(where) + ": " + sdmm_last_error());
+}
+
+// jmm::Samples / sdmm::Data: SoA training data, appended from many render
+// threads (push_back_synchronized, samples.h:250-256), handed to em_step.
+class TrainingData {
+public:
+    void reserve(size_t n) {
+        for (auto& p : x_) p.reserve(n);
+        w_.reserve(n);
+        nrm_.reserve(3 * n);
+    }
+    // point = (normalised position, unit direction), normal, weight.
+    // Zero weights are dropped like Samples::push_back (samples.h:281-283).
+    bool push_back(const float point[6], const float normal[3], float weight) {
+        if (weight == 0.0f) return false;
+        std::lock_guard<std::mutex> lock(mutex_);
+        for (int i = 0; i < 6; ++i) x_[i].push_back(point[i]);
+        w_.push_back(weight);
+        nrm_.insert(nrm_.end(), normal, normal + 3);
+        return true;
+    }
+    size_t size() const { return w_.size(); }
+    void clear() {
+        for (auto& p : x_) p.clear();
+        w_.clear();
+        nrm_.clear();
+    }
+    sdmm_samples view() const {
+        sdmm_samples s{};
+        for (int i = 0; i < 6; ++i) s.x[i] = x_[i].data();
+        s.w = w_.data();
+        s.hpdf = nullptr;
+        s.is_diffuse = nullptr;
+        s.n = (int64_t)w_.size();
+        return s;
+    }
+    const float* normals() const { return nrm_.data(); }
+    const std::vector<float>& plane(int i) const { return x_[i]; }
+
+private:
+    std::vector<float> x_[6];
+    std::vector<float> w_;
+    std::vector<float> nrm_;
+    std::mutex mutex_;
+};
+
+// One spatio-directional mixture + its stepwise EM state on one GPU
+// (jmm::MixtureModel<6,K,3,...> + StepwiseTangentEM, i.e. sdmm::SDMM + sdmm::EM).
+class Mixture {
+public:
+    explicit Mixture(int K, int device = 0, const sdmm_em_params* params = nullptr) {
+        check(sdmm_create(K, params, device, &h_), "sdmm_create");
+    }
+    ~Mixture() { sdmm_destroy(h_); }
+    Mixture(const Mixture&) = delete;
+    Mixture& operator=(const Mixture&) = delete;
+
+    int components() const { return sdmm_num_components(h_); }
+    sdmm_mix* handle() { return h_; }
+    void set_stream(void* hip_stream) { check(sdmm_set_stream(h_, hip_stream), "sdmm_set_stream"); }
+    void synchronize() { check(sdmm_synchronize(h_), "sdmm_synchronize"); }
+
+    // sdmm::initialize: seed positions = the first K/8 training points
+    // (uniformHemisphereInit, mixture_model_init.h:139-141).
+    void initialize(const TrainingData& data, float depth_prior, float spatial_distance, uint64_t seed) {
+        const int n_pos = components() / 8;
+        if ((int64_t)data.size() < n_pos) throw Error(SDMM_E_INVALID, "initialize: too few samples");
+        std::vector<float> pos(3 * n_pos);
+        for (int i = 0; i < n_pos; ++i)
+            for (int d = 0; d < 3; ++d) pos[3 * i + d] = data.plane(d)[i];
+        check(sdmm_init_hemisphere(h_, pos.data(), data.normals(), n_pos, depth_prior, spatial_distance, seed),
+              "sdmm_init_hemisphere");
+    }
+
+    // sdmm::em_step + sdmm::prepare on host-resident training data.
+    void em_step(const TrainingData& data, int iterations = 1) {
+        sdmm_samples s = data.view();
+        check(sdmm_em_step_host(h_, &s, iterations), "sdmm_em_step_host");
+    }
+    // ... or on device-resident SoA planes (no PCIe copy).
+    void em_step_device(const sdmm_samples& device_samples, int iterations = 1) {
+        check(sdmm_em_step(h_, &device_samples, iterations), "sdmm_em_step");
+    }
+
+    // sdmm::save_json counterpart: export the canonical parameters.
+    void params(std::vector<float>& weights, std::vector<float>& means, std::vector<float>& covs) const {
+        const int K = sdmm_num_components(h_);
+        weights.resize(K);
+        means.resize(6 * K);
+        covs.resize(25 * K);
+        sdmm_params_out o{};
+        o.weights = weights.data();
+        o.mean = means.data();
+        o.cov = covs.data();
+        check(sdmm_get_params(h_, &o), "sdmm_get_params");
+    }
+
+private:
+    sdmm_mix* h_ = nullptr;
+};
+
+// A wavefront of guided-bounce queries against one mixture: the batched form
+// of create_conditional + sample + posterior/hsum (sdmm_proc.cpp:368-545).
+// Device SoA planes; capacity fixed at construction.
+struct GuidingBatch {
+    const float* c[3];   // condition (normalised position), device
+    const float* u[3];   // uniforms: component choice, Box-Muller u1, u2, device
+    float* d[3];         // sampled direction, device
+    float* pdf;          // conditional mixture pdf at d (gmmPdf), device
+    int32_t* comp;       // joint component used, -1 = invalid conditional, device
+    int64_t n;
+};
+
+inline void sample_guided(const Mixture& m, const GuidingBatch& q) {
+    check(sdmm_guide_batch(const_cast<Mixture&>(m).handle(), q.n, q.c, q.u, q.d, q.pdf, q.comp),
+          "sdmm_guide_batch");
+}
+
+// pdfSurface's mixing of BSDF and guiding densities (sdmm_proc.cpp:587-589):
+// pdf = h * bsdfPdf + (1 - h) * gmmPdf, h = 0.5 (0.3 with product sampling).
+inline float mixed_pdf(float heuristicConditionalWeight, float bsdfPdf, float gmmPdf) {
+    return heuristicConditionalWeight * bsdfPdf + (1.0f - heuristicConditionalWeight) * gmmPdf;
+}
+
+}  // namespace sdmm_amd

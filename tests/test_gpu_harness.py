@@ -1,0 +1,61 @@
+"""GPU: the C++ mirror header (sdmm-mitsuba_amd/host/sdmm_amd.hpp) driven in
+the plugin's pattern -- per-leaf mixtures on concurrent host threads, host
+training data staged through sdmm_em_step_host -- gives bitwise the same
+mixtures as the device-resident Python path, and both match the oracle."""
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _build(tmp_path):
+    exe = tmp_path / "plugin_harness"
+    lib = ROOT / "sdmm-mitsuba_amd" / "lib"
+    subprocess.run(["g++", "-O2", "-std=c++17", f"-I{ROOT / 'sdmm-mitsuba_amd' / 'host'}",
+                    f"-I{ROOT / 'include'}", str(ROOT / "tests" / "cpp" / "plugin_harness.cpp"),
+                    f"-L{lib}", "-lsdmm_amd", f"-Wl,-rpath,{lib}", "-pthread", "-o", str(exe)],
+                   check=True)
+    return exe
+
+
+def test_plugin_pattern_harness(pkg, oracle, synth, gpu, tmp_path):
+    import torch
+    K, L, N = 16, 4, 4 * 3000
+    b = synth.em_batch(N, 128)
+    w = b["w"].copy()
+    with open(tmp_path / "in.bin", "wb") as f:
+        np.array([N], np.int64).tofile(f)
+        np.array([K, L], np.int32).tofile(f)
+        b["x"].astype(np.float32).tofile(f)
+        w.astype(np.float32).tofile(f)
+        b["normals"].astype(np.float32).tofile(f)
+    exe = _build(tmp_path)
+    subprocess.run([str(exe), str(tmp_path / "in.bin"), str(tmp_path / "out.bin")], check=True, timeout=120)
+    out = np.fromfile(tmp_path / "out.bin", np.float32).reshape(L, -1)
+    for l in range(L):
+        a, e = N * l // L, N * (l + 1) // L
+        # TrainingData::push_back drops zero weights (samples.h:281-283)
+        keep = w[a:e] != 0
+        x = b["x"][:, a:e][:, keep]
+        ww = w[a:e][keep]
+        nrm = b["normals"][a:e][keep]
+        mix = pkg.SDMM(K)
+        mix.init_hemisphere(x[0:3, :K // 8].T, nrm[:K // 8], 0.01, 0.1, 0x1A17 + l)
+        ds = pkg.DeviceSamples.from_numpy(x, ww)
+        for _ in range(4):
+            mix.optimize(ds)
+        p = mix.get_params()
+        got = out[l]
+        np.testing.assert_array_equal(got[:K], p["weights"])
+        np.testing.assert_array_equal(got[K:7 * K].reshape(K, 6), p["mean"])
+        np.testing.assert_array_equal(got[7 * K:].reshape(K, 25), p["cov"])
+        # and the oracle (exact E-step) agrees to the EM tolerance
+        m, st = oracle.hemisphere_init(K // 8, x[0:3, :K // 8].T, nrm[:K // 8], 0.01, 0.1, 0x1A17 + l)
+        s = oracle.Samples(x, ww)
+        for _ in range(4):
+            oracle.optimize(m, st, s, accurate="exact")
+        np.testing.assert_allclose(p["weights"], m.weights, rtol=2e-4, atol=1e-7)
