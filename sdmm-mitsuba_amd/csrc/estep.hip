@@ -28,13 +28,34 @@ namespace sdmm {
 // log2(NORMALIZATION) of mvtn.h:351-352, NORMALIZATION = (float)pow(0.39894228f, 5)
 constexpr float kLog2Norm5 = -6.628740082514092f;
 
-// theta / sin(theta) for cos(theta) = c, with the reference's quirk
+// theta / sin(theta) for cos(theta) = c in [-1, 1], with the reference's quirk
 // `(sinAngle < 1e-3) ? 1 : angle / sinAngle` (mvtn.h:163-164).
+//
+// The reference computes acos and sqrt separately (~40 VALU ops with the
+// libm-grade acosf and the IEEE sqrt expansion).  Here, with u = (1-|c|)/2,
+//   acos(|c|) = 2 asin(sqrt(u)),  sin(acos|c|) = 2 sqrt(u) sqrt(1-u),
+// so theta'/sin(theta') = g(u) / sqrt(1-u) with g(u) = asin(sqrt u)/sqrt u,
+// a smooth function on [0, 1/2] fitted by a degree-7 minimax-style polynomial
+// (max rel. error 8.8e-8, tools/fit_angle_over_sin.py).  For c < 0,
+// theta = pi - theta' gives (pi - theta')/s = pi/s - theta'/s.  Overall
+// <= 4e-7 relative (3 ulp) against the exact value; the fp32 acos/sqrt path
+// of the reference is itself 1.8e-7 from exact.  ~16 VALU + 2 v_rsq.
 __device__ __forceinline__ float angle_over_sin(float c) {
-    float s = __builtin_sqrtf(fmaf(-c, c, 1.0f));
-    float th = acosf(c);
-    float a = th * __builtin_amdgcn_rcpf(s);
-    return (s < 1e-3f) ? 1.0f : a;
+    const float ac = __builtin_fabsf(c);
+    const float u = fmaf(-0.5f, ac, 0.5f);
+    float g = 0.1111316829919815f;
+    g = fmaf(g, u, -0.09260322898626328f);
+    g = fmaf(g, u, 0.07724328339099884f);
+    g = fmaf(g, u, 0.01616133376955986f);
+    g = fmaf(g, u, 0.04657839611172676f);
+    g = fmaf(g, u, 0.07487323880195618f);
+    g = fmaf(g, u, 0.1666697859764099f);
+    g = fmaf(g, u, 1.0f);
+    const float fpos = g * __builtin_amdgcn_rsqf(fmaf(0.5f, ac, 0.5f));
+    const float s2 = fmaf(-c, c, 1.0f);
+    const float fneg = fmaf(3.14159265358979f, __builtin_amdgcn_rsqf(s2), -fpos);
+    const float f = (c < 0.0f) ? fneg : fpos;
+    return (s2 < 1e-6f) ? 1.0f : f;
 }
 
 template <int CPL>
@@ -87,7 +108,16 @@ __device__ __forceinline__ SampleVals load_sample(const SamplesDev& s, int64_t i
         v.x3 = ((cfloat_p)s.x[3])[i]; v.x4 = ((cfloat_p)s.x[4])[i]; v.x5 = ((cfloat_p)s.x[5])[i];
         v.w = ((cfloat_p)s.w)[i];
         v.h = s.hpdf ? ((cfloat_p)s.hpdf)[i] : 0.0f;
-        v.diffuse = s.isDiffuse ? (((cu8_p)s.isDiffuse)[i] != 0) : false;
+        // gfx950 SMEM has no byte load: fetch the aligned dword holding byte i
+        // as a scalar load and extract it (a plain u8 load would become a
+        // per-sample VMEM load + vmcnt(0) stall).
+        if (s.isDiffuse) {
+            const uintptr_t a = (uintptr_t)(s.isDiffuse + i);
+            const unsigned word = *(const __attribute__((address_space(4))) unsigned*)(a & ~(uintptr_t)3);
+            v.diffuse = ((word >> ((a & 3) * 8)) & 0xffu) != 0;
+        } else {
+            v.diffuse = false;
+        }
     } else {
         v.x0 = s.x[0][i]; v.x1 = s.x[1][i]; v.x2 = s.x[2][i];
         v.x3 = s.x[3][i]; v.x4 = s.x[4][i]; v.x5 = s.x[5][i];
