@@ -7,20 +7,25 @@
 // (multivariate_tangent_normal.h:146-177, :350-365).
 //
 // Work mapping (MI355X-first, not the reference's sample-outer loop):
-//   * a wave owns ALL K components: lane j of a lane group holds components
-//     j*CPL .. j*CPL+CPL-1 with their 28 parameters in VGPRs for the whole
-//     kernel (loaded once, coalesced, from the SoA record ep[f*Kp + k]);
-//   * the wave walks a contiguous chunk of samples; with LPS == 64 lanes per
-//     sample the sample is wave-uniform and is fetched with scalar (SMEM)
-//     loads through the constant address space -- no VGPRs, no LDS;
-//   * the posterior normaliser sum_k pi_k pdf_k is a DPP + permlane-swap
-//     group reduction (group_sum), one per sample;
+//   * a group of LPS lanes owns ALL K components: lane j holds components
+//     j*CPL .. j*CPL+CPL-1 (CPL even) with their 29 parameters in VGPRs for
+//     the whole kernel (loaded once, coalesced, from the SoA record
+//     ep[f*Kp + k]);
+//   * a lane evaluates its components two at a time with packed fp32
+//     (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 on float2), halving the
+//     VALU issue of the pair math; the sample operands are SGPR broadcasts;
+//   * with LPS == 64 the sample is wave-uniform and is fetched with scalar
+//     (SMEM) loads through the constant address space, one sample ahead of
+//     its use (software pipelined) -- no VGPRs, no LDS, no VMEM;
+//   * the posterior normaliser sum_k pi_k pdf_k is a DPP row reduction plus
+//     v_readlane across rows (group_sum), one per sample;
 //   * STATS: each lane accumulates the 21 sufficient statistics of its own
 //     components in registers over the whole chunk (no cross-lane traffic in
 //     the loop), then the workgroup folds its waves through LDS in a fixed
 //     order and writes one fp32 partial row; reduce_partials sums rows in fp64.
 //   * RESP: the normalised responsibilities are stored row-major [N][K]; a
-//     wave writes one contiguous K*4-byte row per sample (CPL*4 B per lane).
+//     group writes one contiguous K*4-byte row per sample (CPL*4 B per lane,
+//     non-temporal vector stores).
 #include "sdmm_device.h"
 
 namespace sdmm {
@@ -28,76 +33,95 @@ namespace sdmm {
 // log2(NORMALIZATION) of mvtn.h:351-352, NORMALIZATION = (float)pow(0.39894228f, 5)
 constexpr float kLog2Norm5 = -6.628740082514092f;
 
+// ---- float / float2 arithmetic -------------------------------------------
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef f2 V;   // two components per packed operation
+
+__device__ __forceinline__ V sp(float x) { return (V)(x); }
+__device__ __forceinline__ V vfma(V a, V b, V c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ V vrsq(V x) { return V{__builtin_amdgcn_rsqf(x.x), __builtin_amdgcn_rsqf(x.y)}; }
+__device__ __forceinline__ V vexp2(V x) { return V{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)}; }
+__device__ __forceinline__ V vabs(V x) { return __builtin_elementwise_abs(x); }
+
 // theta / sin(theta) for cos(theta) = c in [-1, 1], with the reference's quirk
 // `(sinAngle < 1e-3) ? 1 : angle / sinAngle` (mvtn.h:163-164).
 //
 // The reference computes acos and sqrt separately (~40 VALU ops with the
-// libm-grade acosf and the IEEE sqrt expansion).  Here, with u = (1-|c|)/2,
-//   acos(|c|) = 2 asin(sqrt(u)),  sin(acos|c|) = 2 sqrt(u) sqrt(1-u),
-// so theta'/sin(theta') = g(u) / sqrt(1-u) with g(u) = asin(sqrt u)/sqrt u,
-// a smooth function on [0, 1/2] fitted by a degree-7 minimax-style polynomial
-// (max rel. error 8.8e-8, tools/fit_angle_over_sin.py).  For c < 0,
-// theta = pi - theta' gives (pi - theta')/s = pi/s - theta'/s.  Overall
-// <= 4e-7 relative (3 ulp) against the exact value; the fp32 acos/sqrt path
-// of the reference is itself 1.8e-7 from exact.  ~16 VALU + 2 v_rsq.
-__device__ __forceinline__ float angle_over_sin(float c) {
-    const float ac = __builtin_fabsf(c);
-    const float u = fmaf(-0.5f, ac, 0.5f);
-    float g = 0.1111316829919815f;
-    g = fmaf(g, u, -0.09260322898626328f);
-    g = fmaf(g, u, 0.07724328339099884f);
-    g = fmaf(g, u, 0.01616133376955986f);
-    g = fmaf(g, u, 0.04657839611172676f);
-    g = fmaf(g, u, 0.07487323880195618f);
-    g = fmaf(g, u, 0.1666697859764099f);
-    g = fmaf(g, u, 1.0f);
-    const float fpos = g * __builtin_amdgcn_rsqf(fmaf(0.5f, ac, 0.5f));
-    const float s2 = fmaf(-c, c, 1.0f);
-    const float fneg = fmaf(3.14159265358979f, __builtin_amdgcn_rsqf(s2), -fpos);
-    const float f = (c < 0.0f) ? fneg : fpos;
-    return (s2 < 1e-6f) ? 1.0f : f;
+// libm-grade acosf and the IEEE sqrt expansion).  For c >= 0, with
+// u = (1-c)/2, theta/sin(theta) = asin(sqrt u) / (sqrt u sqrt(1-u)) =: h(u) is
+// analytic on [0, 1/2] and is a degree-9 polynomial here (8.5e-8 rel.,
+// tools/fit_angle_over_sin.py).  For c < 0, theta = pi - theta' with
+// theta' = acos|c| gives pi / sin(theta) - h(u).  Overall <= 2.9e-7 relative
+// against float64; the reference's own fp32 acos/sqrt form is 1.8e-7 from it.
+// Cost: 9 FMA + one v_rsq per component.
+__device__ __forceinline__ V angle_over_sin(V c) {
+    const V u = vfma(sp(-0.5f), vabs(c), sp(0.5f));
+    V h = sp(5.659248352050781f);
+    h = vfma(h, u, sp(-8.219043731689453f));
+    h = vfma(h, u, sp(6.410147190093994f));
+    h = vfma(h, u, sp(-2.090447187423706f));
+    h = vfma(h, u, sp(0.9454659819602966f));
+    h = vfma(h, u, sp(0.32539111375808716f));
+    h = vfma(h, u, sp(0.46356001496315f));
+    h = vfma(h, u, sp(0.533078670501709f));
+    h = vfma(h, u, sp(0.666670560836792f));
+    h = vfma(h, u, sp(1.0f));
+    const V s2 = vfma(-c, c, sp(1.0f));
+    const V fneg = vfma(sp(3.14159265358979f), vrsq(s2), -h);
+    const V f = (c < sp(0.0f)) ? fneg : h;
+    return (s2 < sp(1e-6f)) ? sp(1.0f) : f;
 }
 
-template <int CPL>
-struct Params {
-    float v[CPL][EP_FIELDS];
-};
-
-// pi_k * pdf_k(x) (unnormalised posterior) and the directional tangent of the
-// sample in component k's frame.  p: sample position, d: sample direction.
+// pi_k * pdf_k(x) (unnormalised posterior) of two components and the
+// directional tangent of the sample in their frames.  p: sample position,
+// d: sample direction.  cfail: -1 for a valid sample, +inf when d == 0
+// (log map fails for d == 0 or c <= -1, mvtn.h:152-159: pdf = 0).
+// q = |L^-1 t|^2 with t = (p - mu, a R0.d, a R1.d), a = theta/sin(theta);
+// pdf = NORM5 exp(-q/2) * detInv * a (mvtn.h:350-365), times pi_k.
 template <bool WANT_T>
-__device__ __forceinline__ float pair_pdf(const float* __restrict__ P, float p0, float p1, float p2,
-                                          float d0, float d1, float d2, bool dvalid, float& t0,
-                                          float& t1) {
-    const float tp0 = p0 - P[EP_MU0], tp1 = p1 - P[EP_MU1], tp2 = p2 - P[EP_MU2];
-    const float r0 = fmaf(P[EP_R02], d2, fmaf(P[EP_R01], d1, P[EP_R00] * d0));
-    const float r1 = fmaf(P[EP_R12], d2, fmaf(P[EP_R11], d1, P[EP_R10] * d0));
-    const float c = fmaf(P[EP_R22], d2, fmaf(P[EP_R21], d1, P[EP_R20] * d0));
-    const bool ok = dvalid && (c > -1.0f);   // log map fails for d == 0 or c <= -1 (mvtn.h:152-159)
-    const float cc = (c < 1.0f) ? c : 1.0f;
-    const float a = angle_over_sin(cc);
-    const float ta = r0 * a, tb = r1 * a;
-    const float u0 = P[EP_L00] * tp0;
-    const float u1 = fmaf(P[EP_L11], tp1, P[EP_L10] * tp0);
-    const float u2 = fmaf(P[EP_L22], tp2, fmaf(P[EP_L21], tp1, P[EP_L20] * tp0));
-    const float u3 = fmaf(P[EP_L33], ta, fmaf(P[EP_L32], tp2, fmaf(P[EP_L31], tp1, P[EP_L30] * tp0)));
-    const float u4 = fmaf(P[EP_L44], tb, fmaf(P[EP_L43], ta,
-                     fmaf(P[EP_L42], tp2, fmaf(P[EP_L41], tp1, P[EP_L40] * tp0))));
-    const float q = fmaf(u4, u4, fmaf(u3, u3, fmaf(u2, u2, fmaf(u1, u1, u0 * u0))));
-    // NORM5 * exp(-q/2) as one v_exp_f32: 2^(q * -log2(e)/2 + log2(NORM5))
-    const float e = __builtin_amdgcn_exp2f(fmaf(q, -0.72134752044448170368f, kLog2Norm5));
-    const float pdf = e * (P[EP_DI] * a);     // pdf *= m_detInv * jacobian (mvtn.h:361)
+__device__ __forceinline__ V pair_pdf(const V* __restrict__ P, float p0, float p1, float p2,
+                                      float d0, float d1, float d2, float cfail, V& t0, V& t1) {
+    const V tp0 = p0 - P[EP_MU0], tp1 = p1 - P[EP_MU1], tp2 = p2 - P[EP_MU2];
+    const V c = vfma(P[EP_R22], sp(d2), vfma(P[EP_R21], sp(d1), P[EP_R20] * d0));
+    const V a = angle_over_sin(__builtin_elementwise_min(c, sp(1.0f)));
+    const V u0 = P[EP_L00] * tp0;
+    const V u1 = vfma(P[EP_L11], tp1, P[EP_L10] * tp0);
+    const V u2 = vfma(P[EP_L22], tp2, vfma(P[EP_L21], tp1, P[EP_L20] * tp0));
+    const V s3 = vfma(P[EP_L32], tp2, vfma(P[EP_L31], tp1, P[EP_L30] * tp0));
+    const V s4 = vfma(P[EP_L42], tp2, vfma(P[EP_L41], tp1, P[EP_L40] * tp0));
+    V u3, u4;
     if constexpr (WANT_T) {
-        t0 = ok ? ta : 0.0f;
-        t1 = ok ? tb : 0.0f;
+        // the statistics need the tangent vector itself
+        const V r0 = vfma(P[EP_R02], sp(d2), vfma(P[EP_R01], sp(d1), P[EP_R00] * d0));
+        const V r1 = vfma(P[EP_R12], sp(d2), vfma(P[EP_R11], sp(d1), P[EP_R10] * d0));
+        const V ta = r0 * a, tb = r1 * a;
+        u3 = vfma(P[EP_L33], ta, s3);
+        u4 = vfma(P[EP_L44], tb, vfma(P[EP_L43], ta, s4));
+        const auto okt = c > sp(cfail);
+        t0 = okt ? ta : sp(0.0f);
+        t1 = okt ? tb : sp(0.0f);
+    } else {
+        // folded: L33 a R0.d = a (A.d), L43 a R0.d + L44 a R1.d = a (B.d)
+        const V ad = vfma(P[EP_A2], sp(d2), vfma(P[EP_A1], sp(d1), P[EP_A0] * d0));
+        const V bd = vfma(P[EP_B2], sp(d2), vfma(P[EP_B1], sp(d1), P[EP_B0] * d0));
+        u3 = vfma(a, ad, s3);
+        u4 = vfma(a, bd, s4);
     }
-    return ok ? P[EP_PI] * pdf : 0.0f;        // m_weights[k] * pdf (mixture_model.h:164)
+    const V q = vfma(u4, u4, vfma(u3, u3, vfma(u2, u2, vfma(u1, u1, u0 * u0))));
+    // NORM5 * exp(-q/2) as one v_exp_f32: 2^(q * -log2(e)/2 + log2(NORM5))
+    const V e = vexp2(vfma(q, sp(-0.72134752044448170368f), sp(kLog2Norm5)));
+    const V pdf = e * (P[EP_DIPI] * a);   // * detInv * jacobian * pi_k (mvtn.h:361, mixture_model.h:164)
+    return (c > sp(cfail)) ? pdf : sp(0.0f);
 }
 
 struct SampleVals {
     float x0, x1, x2, x3, x4, x5, w, h;
     bool diffuse;
-    __device__ bool dvalid() const { return !(x3 == 0.0f && x4 == 0.0f && x5 == 0.0f); }
+    // c > cfail selects valid log maps; d == 0 fails for every component
+    __device__ float cfail() const {
+        return (x3 == 0.0f && x4 == 0.0f && x5 == 0.0f) ? __builtin_inff() : -1.0f;
+    }
 };
 
 template <int LPS>
@@ -128,6 +152,35 @@ __device__ __forceinline__ SampleVals load_sample(const SamplesDev& s, int64_t i
     return v;
 }
 
+// Posterior normalisation of one sample (mixture_model.h:170-191):
+// S' = (1-h) S + h hpdf for diffuse samples, gamma_k = q_k / S' (x (1-h)),
+// gamma_h = h hpdf / S'; everything zero when 1/S' is not finite.
+struct Norm {
+    float gsc;     // gamma_k = q_k * gsc
+    float hpost;   // gamma_h
+    bool fin;      // 1/S' finite
+};
+template <int LPS>
+__device__ __forceinline__ Norm normalise(float local, const SampleVals& sv) {
+    const float S = group_sum<LPS>(local);
+    const float S2 = sv.diffuse ? fmaf(1.0f - kHeuristicWeight, S, kHeuristicWeight * sv.h) : S;
+    const float inv = __builtin_amdgcn_rcpf(S2);
+    Norm n;
+    n.fin = __builtin_isfinite(inv);
+    n.gsc = n.fin ? (sv.diffuse ? inv * (1.0f - kHeuristicWeight) : inv) : 0.0f;
+    n.hpost = (n.fin && sv.diffuse) ? kHeuristicWeight * sv.h * inv : 0.0f;
+    return n;
+}
+
+template <int CPL>
+__device__ __forceinline__ void load_params(const float* __restrict__ ep, int Kp, int kbase,
+                                            V (&P)[CPL / 2][EP_FIELDS]) {
+#pragma unroll
+    for (int c = 0; c < CPL / 2; ++c)
+#pragma unroll
+        for (int f = 0; f < EP_FIELDS; ++f) P[c][f] = *(const V*)(ep + f * Kp + kbase + 2 * c);
+}
+
 // ---------------------------------------------------------------------------
 // Responsibility E-step: resp[n*K + k] = posterior_k(x_n) exactly as
 // posteriorAndLog returns it (zeros when 1/sum is not finite).
@@ -135,7 +188,9 @@ template <int CPL, int LPS>
 __global__ void __launch_bounds__(256)
 estep_resp_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, int64_t n,
                   int64_t chunk, float* __restrict__ resp) {
+    static_assert(CPL % 2 == 0, "components are processed in packed pairs");
     constexpr int SPW = 64 / LPS;
+    constexpr int NP = CPL / 2;
     const int lane = threadIdx.x & 63;
     const int g = lane / LPS;
     const int j = lane % LPS;
@@ -146,52 +201,50 @@ estep_resp_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, int
     if (s0 >= n) return;
     const int64_t s1 = (s0 + chunk < n) ? s0 + chunk : n;
 
-    Params<CPL> P;
-#pragma unroll
-    for (int c = 0; c < CPL; ++c)
-#pragma unroll
-        for (int f = 0; f < EP_FIELDS; ++f) P.v[c][f] = ep[f * Kp + j * CPL + c];
-
     const int kbase = j * CPL;
+    V P[NP][EP_FIELDS];
+    load_params<CPL>(ep, Kp, kbase, P);
+
     const bool full = ((kbase + CPL) <= K) && (K % CPL == 0);  // aligned vector row store
+    SampleVals nxt = load_sample<LPS>(s, (s0 + g < s1) ? s0 + g : s1 - 1);
     for (int64_t base = s0; base < s1; base += SPW) {
         const int64_t i = base + g;
         const bool in = i < s1;
-        const SampleVals sv = load_sample<LPS>(s, in ? i : s0);
-        const bool dv = sv.dvalid();
-        float q[CPL];
-        float local = 0.0f;
+        const SampleVals sv = nxt;
+        const int64_t inx = i + SPW;
+        nxt = load_sample<LPS>(s, (inx < s1) ? inx : s1 - 1);   // prefetch the next sample
+        const float cf = sv.cfail();
+        V q[NP];
+        V acc = sp(0.0f);
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-            float t0, t1;
-            q[c] = pair_pdf<false>(P.v[c], sv.x0, sv.x1, sv.x2, sv.x3, sv.x4, sv.x5, dv, t0, t1);
-            local += q[c];
+        for (int c = 0; c < NP; ++c) {
+            V t0, t1;
+            q[c] = pair_pdf<false>(P[c], sv.x0, sv.x1, sv.x2, sv.x3, sv.x4, sv.x5, cf, t0, t1);
+            acc += q[c];
         }
-        const float S = group_sum<LPS>(local);
-        const float S2 = sv.diffuse ? ((1.0f - kHeuristicWeight) * S + kHeuristicWeight * sv.h) : S;
-        const float inv = 1.0f / S2;
-        const float gsc = __builtin_isfinite(inv) ? (sv.diffuse ? inv * (1.0f - kHeuristicWeight) : inv)
-                                                  : 0.0f;
+        const Norm nm = normalise<LPS>(acc.x + acc.y, sv);
         if (!in) continue;
         float* row = resp + i * (int64_t)K + kbase;
-        if constexpr (CPL == 4) {
-            if (full) {
-                typedef float f4 __attribute__((ext_vector_type(4)));
-                f4 o = {q[0] * gsc, q[1] * gsc, q[2] * gsc, q[3] * gsc};
-                __builtin_nontemporal_store(o, (f4*)row);
-                continue;
+        V o[NP];
+#pragma unroll
+        for (int c = 0; c < NP; ++c) o[c] = nm.fin ? q[c] * nm.gsc : sp(0.0f);
+        if (full) {
+            if constexpr (NP == 1) {
+                __builtin_nontemporal_store(o[0], (V*)row);
+            } else {
+#pragma unroll
+                for (int c = 0; c < NP; c += 2) {
+                    const f4 o4 = {o[c].x, o[c].y, o[c + 1].x, o[c + 1].y};
+                    __builtin_nontemporal_store(o4, (f4*)(row + 2 * c));
+                }
             }
-        } else if constexpr (CPL == 2) {
-            if (full) {
-                typedef float f2 __attribute__((ext_vector_type(2)));
-                f2 o = {q[0] * gsc, q[1] * gsc};
-                __builtin_nontemporal_store(o, (f2*)row);
-                continue;
+        } else {
+#pragma unroll
+            for (int c = 0; c < NP; ++c) {
+                if (kbase + 2 * c < K) __builtin_nontemporal_store(o[c].x, row + 2 * c);
+                if (kbase + 2 * c + 1 < K) __builtin_nontemporal_store(o[c].y, row + 2 * c + 1);
             }
         }
-#pragma unroll
-        for (int c = 0; c < CPL; ++c)
-            if (kbase + c < K) __builtin_nontemporal_store(q[c] * gsc, row + c);
     }
 }
 
@@ -202,7 +255,9 @@ template <int CPL, int LPS>
 __global__ void __launch_bounds__(256)
 estep_stats_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, int64_t n,
                    int64_t chunk, float* __restrict__ partials, int pstride) {
+    static_assert(CPL % 2 == 0, "components are processed in packed pairs");
     constexpr int SPW = 64 / LPS;
+    constexpr int NP = CPL / 2;
     extern __shared__ __attribute__((aligned(16))) float red[];
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -213,80 +268,78 @@ estep_stats_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, in
     const int64_t s0 = wave * chunk;
     const int64_t s1 = (s0 + chunk < n) ? s0 + chunk : n;  // s1 <= s0: no samples
 
-    Params<CPL> P;
-#pragma unroll
-    for (int c = 0; c < CPL; ++c)
-#pragma unroll
-        for (int f = 0; f < EP_FIELDS; ++f) P.v[c][f] = ep[f * Kp + j * CPL + c];
+    const int kbase = j * CPL;
+    V P[NP][EP_FIELDS];
+    load_params<CPL>(ep, Kp, kbase, P);
 
-    float acc[CPL][ST_FIELDS];
+    V acc[NP][ST_FIELDS];
 #pragma unroll
-    for (int c = 0; c < CPL; ++c)
+    for (int c = 0; c < NP; ++c)
 #pragma unroll
-        for (int f = 0; f < ST_FIELDS; ++f) acc[c][f] = 0.0f;
+        for (int f = 0; f < ST_FIELDS; ++f) acc[c][f] = sp(0.0f);
     float accH = 0.0f, accWs = 0.0f;
 
+    SampleVals nxt = load_sample<LPS>(s, (s0 + g < s1) ? s0 + g : (s1 > s0 ? s1 - 1 : 0));
     for (int64_t base = s0; base < s1; base += SPW) {
         const int64_t i = base + g;
         const bool in = i < s1;
-        const SampleVals sv = load_sample<LPS>(s, in ? i : s0);
+        const SampleVals sv = nxt;
+        const int64_t inx = i + SPW;
+        nxt = load_sample<LPS>(s, (inx < s1) ? inx : s1 - 1);   // prefetch the next sample
         const bool finite_w = __builtin_isfinite(sv.w);
         // sumWeights counts every finite weight (stepwise_tangent.h:462-475)
         accWs += (in && finite_w) ? sv.w : 0.0f;
         // calculateStats skips non-finite and zero weights (:288-293)
         const bool use = in && finite_w && (sv.w != 0.0f);
-        const bool dv = sv.dvalid();
-        float q[CPL], ta[CPL], tb[CPL];
-        float local = 0.0f;
+        const float cf = sv.cfail();
+        V q[NP], ta[NP], tb[NP];
+        V qs = sp(0.0f);
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-            q[c] = pair_pdf<true>(P.v[c], sv.x0, sv.x1, sv.x2, sv.x3, sv.x4, sv.x5, dv, ta[c], tb[c]);
-            local += q[c];
+        for (int c = 0; c < NP; ++c) {
+            q[c] = pair_pdf<true>(P[c], sv.x0, sv.x1, sv.x2, sv.x3, sv.x4, sv.x5, cf, ta[c], tb[c]);
+            qs += q[c];
         }
-        const float S = group_sum<LPS>(local);
-        const float S2 = sv.diffuse ? ((1.0f - kHeuristicWeight) * S + kHeuristicWeight * sv.h) : S;
-        const float inv = 1.0f / S2;
-        const bool fin = __builtin_isfinite(inv);
-        const float gsc = fin ? (sv.diffuse ? inv * (1.0f - kHeuristicWeight) : inv) : 0.0f;
+        const Norm nm = normalise<LPS>(qs.x + qs.y, sv);
         const float w = use ? sv.w : 0.0f;
-        const float hpost = (fin && sv.diffuse) ? kHeuristicWeight * sv.h * inv : 0.0f;
-        accH = fmaf(w, hpost, accH);
+        accH = fmaf(w, nm.hpost, accH);
+        // posterior < 1e-10 is skipped (:312).  With thr = +inf when 1/S' is not
+        // finite (posterior set to zero, mixture_model.h:182-191) nothing passes.
+        const float thr = nm.fin ? 1e-10f : __builtin_inff();
         // Spatial statistics are accumulated centred on the component's mean
-        // position (tp = p - mu_k, already formed by pair_pdf) and un-centred in
-        // fp64 by finalize_stats_kernel: the M-step's C/W - mu mu^T then does
-        // not amplify fp32 accumulation error by |p|^2 / sigma^2.
+        // position (tp = p - mu_k) and un-centred in fp64 by
+        // finalize_stats_kernel: the M-step's C/W - mu mu^T then does not
+        // amplify fp32 accumulation error by |p|^2 / sigma^2.
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-            const float gam = q[c] * gsc;
-            // posterior < 1e-10 is skipped (:312); unused samples have w == 0
-            const float v = (gam < 1e-10f || !use) ? 0.0f : w * gam;
-            const float tp0 = sv.x0 - P.v[c][EP_MU0];
-            const float tp1 = sv.x1 - P.v[c][EP_MU1];
-            const float tp2 = sv.x2 - P.v[c][EP_MU2];
-            float* A = acc[c];
+        for (int c = 0; c < NP; ++c) {
+            const V gam = q[c] * nm.gsc;
+            const V v = (gam >= sp(thr)) ? gam * w : sp(0.0f);   // unused samples have w == 0
+            const V tp0 = sv.x0 - P[c][EP_MU0];
+            const V tp1 = sv.x1 - P[c][EP_MU1];
+            const V tp2 = sv.x2 - P[c][EP_MU2];
+            V* A = acc[c];
             A[ST_W] += v;
-            const float v0 = v * tp0, v1 = v * tp1, v2 = v * tp2;
+            const V v0 = v * tp0, v1 = v * tp1, v2 = v * tp2;
             A[ST_M0] += v0;
             A[ST_M1] += v1;
             A[ST_M2] += v2;
-            const float v3 = v * ta[c], v4 = v * tb[c];
+            const V v3 = v * ta[c], v4 = v * tb[c];
             A[ST_M3] += v3;
             A[ST_M4] += v4;
-            A[ST_C00] = fmaf(v0, tp0, A[ST_C00]);
-            A[ST_C10] = fmaf(v1, tp0, A[ST_C10]);
-            A[ST_C11] = fmaf(v1, tp1, A[ST_C11]);
-            A[ST_C20] = fmaf(v2, tp0, A[ST_C20]);
-            A[ST_C21] = fmaf(v2, tp1, A[ST_C21]);
-            A[ST_C22] = fmaf(v2, tp2, A[ST_C22]);
-            A[ST_C30] = fmaf(v3, tp0, A[ST_C30]);
-            A[ST_C31] = fmaf(v3, tp1, A[ST_C31]);
-            A[ST_C32] = fmaf(v3, tp2, A[ST_C32]);
-            A[ST_C33] = fmaf(v3, ta[c], A[ST_C33]);
-            A[ST_C40] = fmaf(v4, tp0, A[ST_C40]);
-            A[ST_C41] = fmaf(v4, tp1, A[ST_C41]);
-            A[ST_C42] = fmaf(v4, tp2, A[ST_C42]);
-            A[ST_C43] = fmaf(v4, ta[c], A[ST_C43]);
-            A[ST_C44] = fmaf(v4, tb[c], A[ST_C44]);
+            A[ST_C00] = vfma(v0, tp0, A[ST_C00]);
+            A[ST_C10] = vfma(v1, tp0, A[ST_C10]);
+            A[ST_C11] = vfma(v1, tp1, A[ST_C11]);
+            A[ST_C20] = vfma(v2, tp0, A[ST_C20]);
+            A[ST_C21] = vfma(v2, tp1, A[ST_C21]);
+            A[ST_C22] = vfma(v2, tp2, A[ST_C22]);
+            A[ST_C30] = vfma(v3, tp0, A[ST_C30]);
+            A[ST_C31] = vfma(v3, tp1, A[ST_C31]);
+            A[ST_C32] = vfma(v3, tp2, A[ST_C32]);
+            A[ST_C33] = vfma(v3, ta[c], A[ST_C33]);
+            A[ST_C40] = vfma(v4, tp0, A[ST_C40]);
+            A[ST_C41] = vfma(v4, tp1, A[ST_C41]);
+            A[ST_C42] = vfma(v4, tp2, A[ST_C42]);
+            A[ST_C43] = vfma(v4, ta[c], A[ST_C43]);
+            A[ST_C44] = vfma(v4, tb[c], A[ST_C44]);
         }
     }
 
@@ -295,9 +348,12 @@ estep_stats_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, in
 #pragma unroll
         for (int off = LPS; off < 64; off <<= 1) {
 #pragma unroll
-            for (int c = 0; c < CPL; ++c)
+            for (int c = 0; c < NP; ++c)
 #pragma unroll
-                for (int f = 0; f < ST_FIELDS; ++f) acc[c][f] += __shfl_xor(acc[c][f], off);
+                for (int f = 0; f < ST_FIELDS; ++f) {
+                    acc[c][f].x += __shfl_xor(acc[c][f].x, off);
+                    acc[c][f].y += __shfl_xor(acc[c][f].y, off);
+                }
         }
     }
     // H and wsum are group-uniform: keep one copy per group, then sum groups
@@ -314,11 +370,11 @@ estep_stats_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, in
     for (int w = 0; w < nw; ++w) {
         if (wid == w && g == 0) {
 #pragma unroll
-            for (int c = 0; c < CPL; ++c)
+            for (int c = 0; c < NP; ++c)
 #pragma unroll
                 for (int f = 0; f < ST_FIELDS; ++f) {
-                    const int idx = f * Kp + j * CPL + c;
-                    red[idx] = (w == 0) ? acc[c][f] : red[idx] + acc[c][f];
+                    V* dst = (V*)&red[f * Kp + kbase + 2 * c];
+                    *dst = (w == 0) ? acc[c][f] : *dst + acc[c][f];
                 }
             if (lane == 0) {
                 red[ST_FIELDS * Kp] = (w == 0) ? accH : red[ST_FIELDS * Kp] + accH;
@@ -425,38 +481,26 @@ static hipError_t launch_stats_t(const float* ep, int Kp, int K, const SamplesDe
     return hipGetLastError();
 }
 
+// Layouts (choose_layout in sdmm_api.cpp): CPL = 2 with LPS in {8, 16, 32, 64}
+// for K <= 128, then LPS = 64 with CPL in {4, 8}.
+#define SDMM_LAYOUTS(X) X(2, 8) X(2, 16) X(2, 32) X(2, 64) X(4, 64) X(8, 64)
+
 hipError_t launch_estep_resp(int cpl, int lps, const float* ep, int Kp, int K, const SamplesDev& s,
                              int64_t n, int64_t chunk, float* resp, hipStream_t st) {
-    if (lps == 64) {
-        switch (cpl) {
-            case 1: return launch_resp_t<1, 64>(ep, Kp, K, s, n, chunk, resp, st);
-            case 2: return launch_resp_t<2, 64>(ep, Kp, K, s, n, chunk, resp, st);
-            case 4: return launch_resp_t<4, 64>(ep, Kp, K, s, n, chunk, resp, st);
-            case 8: return launch_resp_t<8, 64>(ep, Kp, K, s, n, chunk, resp, st);
-        }
-    } else if (lps == 32 && cpl == 1) {
-        return launch_resp_t<1, 32>(ep, Kp, K, s, n, chunk, resp, st);
-    } else if (lps == 16 && cpl == 1) {
-        return launch_resp_t<1, 16>(ep, Kp, K, s, n, chunk, resp, st);
-    }
+#define X(C, L) if (cpl == C && lps == L) return launch_resp_t<C, L>(ep, Kp, K, s, n, chunk, resp, st);
+    SDMM_LAYOUTS(X)
+#undef X
     return hipErrorInvalidValue;
 }
 
 hipError_t launch_estep_stats(int cpl, int lps, const float* ep, int Kp, int K, const SamplesDev& s,
                               int64_t n, int64_t chunk, int blocks, int wpb, float* partials,
                               int pstride, hipStream_t st) {
-    if (lps == 64) {
-        switch (cpl) {
-            case 1: return launch_stats_t<1, 64>(ep, Kp, K, s, n, chunk, blocks, wpb, partials, pstride, st);
-            case 2: return launch_stats_t<2, 64>(ep, Kp, K, s, n, chunk, blocks, wpb, partials, pstride, st);
-            case 4: return launch_stats_t<4, 64>(ep, Kp, K, s, n, chunk, blocks, wpb, partials, pstride, st);
-            case 8: return launch_stats_t<8, 64>(ep, Kp, K, s, n, chunk, blocks, wpb, partials, pstride, st);
-        }
-    } else if (lps == 32 && cpl == 1) {
-        return launch_stats_t<1, 32>(ep, Kp, K, s, n, chunk, blocks, wpb, partials, pstride, st);
-    } else if (lps == 16 && cpl == 1) {
-        return launch_stats_t<1, 16>(ep, Kp, K, s, n, chunk, blocks, wpb, partials, pstride, st);
-    }
+#define X(C, L)                                                                                    \
+    if (cpl == C && lps == L)                                                                      \
+        return launch_stats_t<C, L>(ep, Kp, K, s, n, chunk, blocks, wpb, partials, pstride, st);
+    SDMM_LAYOUTS(X)
+#undef X
     return hipErrorInvalidValue;
 }
 

@@ -176,6 +176,11 @@ __device__ static void pack_component(int k, int K, int Kp, const CanonDev& C, f
         for (int i = 0; i < 9; ++i) e[EP_R00 + i] = to[i];
         e[EP_DI] = C.detInv[k];
         e[EP_PI] = C.valid[k] ? w : 0.0f;
+        for (int i = 0; i < 3; ++i) {
+            e[EP_A0 + i] = Li[18] * to[i];
+            e[EP_B0 + i] = Li[23] * to[i] + Li[24] * to[3 + i];
+        }
+        e[EP_DIPI] = e[EP_DI] * e[EP_PI];
         g[GP_W] = w;
         g[GP_MU0] = mu[0]; g[GP_MU1] = mu[1]; g[GP_MU2] = mu[2];
         const float* ML = C.margL + 9 * k;

@@ -197,9 +197,10 @@ struct sdmm_mix {
 namespace {
 
 int choose_layout(int K, int& cpl, int& lps) {
-    if (K <= 16) { lps = 16; cpl = 1; }
-    else if (K <= 32) { lps = 32; cpl = 1; }
-    else if (K <= 64) { lps = 64; cpl = 1; }
+    // components are evaluated in packed pairs: CPL is always even
+    if (K <= 16) { lps = 8; cpl = 2; }
+    else if (K <= 32) { lps = 16; cpl = 2; }
+    else if (K <= 64) { lps = 32; cpl = 2; }
     else if (K <= 128) { lps = 64; cpl = 2; }
     else if (K <= 256) { lps = 64; cpl = 4; }
     else if (K <= 512) { lps = 64; cpl = 8; }

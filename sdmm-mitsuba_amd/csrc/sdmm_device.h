@@ -25,6 +25,11 @@ enum : int {
     EP_L40, EP_L41, EP_L42, EP_L43, EP_L44,
     EP_R00, EP_R01, EP_R02, EP_R10, EP_R11, EP_R12, EP_R20, EP_R21, EP_R22,
     EP_DI, EP_PI,
+    // folded forms for the responsibility kernel (no tangent vector needed):
+    //   u3 = L30 tp0 + L31 tp1 + L32 tp2 + a (A . d),  A = L33 R0
+    //   u4 = L40 tp0 + L41 tp1 + L42 tp2 + a (B . d),  B = L43 R0 + L44 R1
+    //   pi pdf = NORM5 exp(-q/2) * a * (detInv pi)
+    EP_A0, EP_A1, EP_A2, EP_B0, EP_B1, EP_B2, EP_DIPI,
     EP_FIELDS
 };
 
@@ -109,7 +114,7 @@ __device__ __forceinline__ float dpp(float x) {
         0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
 }
 
-// Sum over aligned groups of G lanes (G in {16, 32, 64}); every lane of the
+// Sum over aligned groups of G lanes (G in {8, 16, 32, 64}); every lane of the
 // group receives the group sum.  quad_perm/mirror DPP reduce within rows of
 // 16 lanes; rows are then combined through v_readlane (SGPR) reads.  (The
 // gfx950 permlane16/32 swaps would save two instructions, but ROCm 7.2 folds
@@ -119,6 +124,7 @@ __device__ __forceinline__ float group_sum(float x) {
     x += dpp<0xB1>(x);   // quad_perm [1,0,3,2]  (xor 1)
     x += dpp<0x4E>(x);   // quad_perm [2,3,0,1]  (xor 2)
     x += dpp<0x141>(x);  // row_half_mirror      (pairs within 8)
+    if constexpr (G == 8) return x;
     x += dpp<0x140>(x);  // row_mirror           (pairs within 16)
     if constexpr (G == 64) {
         const int xi = __builtin_bit_cast(int, x);
