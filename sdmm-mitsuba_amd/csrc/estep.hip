@@ -504,6 +504,25 @@ hipError_t launch_estep_stats(int cpl, int lps, const float* ep, int Kp, int K, 
     return hipErrorInvalidValue;
 }
 
+// Resident workgroups (of 256 threads) per CU for the layout's kernels: the
+// E-step launches exactly one chip-full of waves, each walking a contiguous
+// chunk, so the loop's dependent packed-FMA chains are covered by as many
+// waves per SIMD as the register budget allows.
+hipError_t estep_occupancy(int cpl, int lps, int Kp, int* resp_blocks, int* stats_blocks) {
+    const size_t lds = sizeof(float) * (size_t)(ST_FIELDS * Kp + 2);
+#define X(C, L)                                                                                    \
+    if (cpl == C && lps == L) {                                                                    \
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(                               \
+            resp_blocks, reinterpret_cast<const void*>(&estep_resp_kernel<C, L>), 256, 0);         \
+        if (e != hipSuccess) return e;                                                             \
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(                                       \
+            stats_blocks, reinterpret_cast<const void*>(&estep_stats_kernel<C, L>), 256, lds);     \
+    }
+    SDMM_LAYOUTS(X)
+#undef X
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_reduce_partials(const float* partials, int rows, int pstride, const float* ep_for_finalize,
                                   int Kp, int K,
                                   double* stats, hipStream_t st) {

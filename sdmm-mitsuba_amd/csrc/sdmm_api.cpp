@@ -24,6 +24,7 @@ hipError_t launch_estep_resp(int cpl, int lps, const float* ep, int Kp, int K, c
 hipError_t launch_estep_stats(int cpl, int lps, const float* ep, int Kp, int K, const SamplesDev& s,
                               int64_t n, int64_t chunk, int blocks, int wpb, float* partials,
                               int pstride, hipStream_t st);
+hipError_t estep_occupancy(int cpl, int lps, int Kp, int* resp_blocks, int* stats_blocks);
 hipError_t launch_reduce_partials(const float* partials, int rows, int pstride, const float* ep_for_finalize,
                                   int Kp, int K,
                                   double* stats, hipStream_t st);
@@ -171,6 +172,7 @@ struct sdmm_mix {
     int K = 0, Kp = 0, cpl = 1, lps = 64;
     int device = 0;
     int cus = 256;
+    int resp_blocks = 2, stats_blocks = 2;   // resident 256-thread WGs per CU
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
     sdmm_em_params params{};
@@ -215,9 +217,9 @@ struct Split {
     int wpb;
 };
 
-Split split_for(const sdmm_mix* m, int64_t n) {
+Split split_for(const sdmm_mix* m, int64_t n, int blocks_per_cu) {
     const int spw = 64 / m->lps;
-    const int64_t target_waves = (int64_t)m->cus * 8;
+    const int64_t target_waves = (int64_t)m->cus * 4 * (blocks_per_cu > 0 ? blocks_per_cu : 2);
     int64_t chunk = (n + target_waves - 1) / target_waves;
     if (chunk < 4 * spw) chunk = 4 * spw;
     chunk = ((chunk + spw - 1) / spw) * spw;
@@ -258,7 +260,7 @@ int ensure_partials(sdmm_mix* m, int rows) {
 }
 
 int run_estep_stats(sdmm_mix* m, const sdmm_samples* s, double* stats_out) {
-    const Split sp = split_for(m, s->n);
+    const Split sp = split_for(m, s->n, m->stats_blocks);
     int r = ensure_partials(m, sp.blocks);
     if (r) return r;
     SamplesDev d = to_dev(s);
@@ -310,6 +312,8 @@ int sdmm_create(int K, const sdmm_em_params* params, int device, sdmm_mix** out)
     if (hipSetDevice(device) != hipSuccess) return cleanup(fail(SDMM_E_HIP, "hipSetDevice failed"));
     (void)hipDeviceGetAttribute(&m->cus, hipDeviceAttributeMultiprocessorCount, device);
     if (m->cus <= 0) m->cus = 256;
+    if (estep_occupancy(m->cpl, m->lps, m->Kp, &m->resp_blocks, &m->stats_blocks) != hipSuccess)
+        return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
     if (hipStreamCreateWithFlags(&m->own_stream, hipStreamNonBlocking) != hipSuccess)
         return cleanup(fail(SDMM_E_HIP, "hipStreamCreate failed"));
     m->stream = m->own_stream;
@@ -518,7 +522,7 @@ int sdmm_responsibilities(sdmm_mix* m, const sdmm_samples* s, float* resp) {
     int r = check_samples(s);
     if (r) return r;
     if (s->n == 0) return SDMM_OK;
-    const Split sp = split_for(m, s->n);
+    const Split sp = split_for(m, s->n, m->resp_blocks);
     HIP_TRY(launch_estep_resp(m->cpl, m->lps, m->ep, m->Kp, m->K, to_dev(s), s->n, sp.chunk, resp,
                               m->stream));
     return SDMM_OK;

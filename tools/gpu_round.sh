@@ -13,11 +13,15 @@ timeout -k 10 500 python -m pytest tests -m gpu -q -rf "$@" > "$OUT/pytest_gpu_$
 rc=$?; echo "pytest rc=$rc" | tee -a "$OUT/pytest_gpu_$TAG.log"; tail -5 "$OUT/pytest_gpu_$TAG.log"
 ok $rc || exit $rc
 
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_$TAG.log" 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -3 "$OUT/smoke_$TAG.log"
+ok $rc || exit $rc
+
 timeout -k 10 300 python bench.py > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err"
 rc=$?; echo "bench rc=$rc"; cat "$OUT/bench_$TAG.json"
 [ $rc -eq 0 ] || { tail -20 "$OUT/bench_$TAG.err"; exit $rc; }
 
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof_$TAG" -o run \
-    -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu --steps 10 --warmup 3 > "$GRAFT_REPO_ROOT/$OUT/prof_$TAG.log" 2>&1
+    --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu --steps 10 --warmup 3 > "$GRAFT_REPO_ROOT/$OUT/prof_$TAG.log" 2>&1
 rc=$?; echo "rocprof rc=$rc"
 exit $rc
