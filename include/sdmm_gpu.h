@@ -83,6 +83,9 @@ void sdmm_em_params_default(sdmm_em_params* p);
 int sdmm_create(int K, const sdmm_em_params* params, int device, sdmm_mix** out);
 void sdmm_destroy(sdmm_mix* m);
 int sdmm_num_components(const sdmm_mix* m);
+/* Diagnostics: E-step kernel layouts (components per lane, lanes per sample)
+ * of the responsibility and statistics kernels.  Any pointer may be NULL. */
+int sdmm_layout(const sdmm_mix* m, int* resp_cpl, int* resp_lps, int* stats_cpl, int* stats_lps);
 /* Work is enqueued on this hipStream_t, taken literally (NULL = the HIP null
  * stream).  A new handle starts on its own non-blocking stream, whose value
  * sdmm_get_stream returns before any sdmm_set_stream call. */

@@ -14,9 +14,10 @@
 //   * a lane evaluates its components two at a time with packed fp32
 //     (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 on float2), halving the
 //     VALU issue of the pair math; the sample operands are SGPR broadcasts;
-//   * with LPS == 64 the sample is wave-uniform and is fetched with scalar
-//     (SMEM) loads through the constant address space, one sample ahead of
-//     its use (software pipelined) -- no VGPRs, no LDS, no VMEM;
+//   * samples are staged in blocks of 64 (one coalesced vector load per plane,
+//     a block ahead of use) and broadcast to the lanes per sample (with
+//     LPS == 64 by v_readlane into SGPRs: the pair math reads them as scalar
+//     operands);
 //   * the posterior normaliser sum_k pi_k pdf_k is a DPP row reduction plus
 //     v_readlane across rows (group_sum), one per sample;
 //   * STATS: each lane accumulates the 21 sufficient statistics of its own
@@ -124,32 +125,99 @@ struct SampleVals {
     }
 };
 
+// Sample staging.  The wave walks its chunk in blocks of 64 consecutive
+// samples: lane j loads sample base + j of every plane with one coalesced
+// vector load (256 B per plane), one block ahead of use, and the per-sample
+// values are broadcast from the block registers (v_readlane into SGPRs for
+// LPS == 64, ds_bpermute for smaller groups).  Scalar (SMEM) loads per sample
+// left the waves parked on HBM latency every 16 samples (one 64-B scalar line).
+struct SampleBlock {
+    float x0, x1, x2, x3, x4, x5, w, h;
+    int diff;
+};
+
+__device__ __forceinline__ SampleBlock load_block(const SamplesDev& s, int64_t base, int64_t s1, int lane) {
+    const int64_t i = (base + lane < s1) ? base + lane : s1 - 1;
+    SampleBlock b;
+    b.x0 = __builtin_nontemporal_load(s.x[0] + i);
+    b.x1 = __builtin_nontemporal_load(s.x[1] + i);
+    b.x2 = __builtin_nontemporal_load(s.x[2] + i);
+    b.x3 = __builtin_nontemporal_load(s.x[3] + i);
+    b.x4 = __builtin_nontemporal_load(s.x[4] + i);
+    b.x5 = __builtin_nontemporal_load(s.x[5] + i);
+    b.w = __builtin_nontemporal_load(s.w + i);
+    // optional planes: always issue the load (from a valid plane when absent)
+    // so the number of loads in flight is static and the compiler's vmcnt
+    // waits before each block stay partial
+    const float* hp = s.hpdf ? s.hpdf : s.x[0];
+    const uint8_t* dp = s.isDiffuse ? s.isDiffuse : (const uint8_t*)s.x[0];
+    // (raw values: take_sample applies "absent -> 0" after the broadcast, so
+    // nothing consumes the loaded registers before the block is used)
+    b.h = __builtin_nontemporal_load(hp + i);
+    // the flag byte travels inside its aligned dword (a u8 load's zero
+    // extension would be re-applied right after the load, forcing the wait);
+    // the dword never leaves the 4-byte word that holds byte i
+    b.diff = *(const __attribute__((address_space(1))) int*)((uintptr_t)(dp + i) & ~(uintptr_t)3);
+    return b;
+}
+
 template <int LPS>
-__device__ __forceinline__ SampleVals load_sample(const SamplesDev& s, int64_t i) {
+__device__ __forceinline__ float bcast(float v, int src) {
+    if constexpr (LPS == 64)
+        return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
+    else
+        return __shfl(v, src);
+}
+
+// sample t + g of the block (t: wave-uniform offset, g: this lane's group)
+template <int LPS>
+__device__ __forceinline__ SampleVals take_sample(const SampleBlock& b, int t, int g, bool has_h,
+                                                  bool has_d, uintptr_t dpos) {
+    const int src = (LPS == 64) ? t : t + g;
     SampleVals v;
-    if constexpr (LPS == 64) {
-        v.x0 = ((cfloat_p)s.x[0])[i]; v.x1 = ((cfloat_p)s.x[1])[i]; v.x2 = ((cfloat_p)s.x[2])[i];
-        v.x3 = ((cfloat_p)s.x[3])[i]; v.x4 = ((cfloat_p)s.x[4])[i]; v.x5 = ((cfloat_p)s.x[5])[i];
-        v.w = ((cfloat_p)s.w)[i];
-        v.h = s.hpdf ? ((cfloat_p)s.hpdf)[i] : 0.0f;
-        // gfx950 SMEM has no byte load: fetch the aligned dword holding byte i
-        // as a scalar load and extract it (a plain u8 load would become a
-        // per-sample VMEM load + vmcnt(0) stall).
-        if (s.isDiffuse) {
-            const uintptr_t a = (uintptr_t)(s.isDiffuse + i);
-            const unsigned word = *(const __attribute__((address_space(4))) unsigned*)(a & ~(uintptr_t)3);
-            v.diffuse = ((word >> ((a & 3) * 8)) & 0xffu) != 0;
-        } else {
-            v.diffuse = false;
-        }
-    } else {
-        v.x0 = s.x[0][i]; v.x1 = s.x[1][i]; v.x2 = s.x[2][i];
-        v.x3 = s.x[3][i]; v.x4 = s.x[4][i]; v.x5 = s.x[5][i];
-        v.w = s.w[i];
-        v.h = s.hpdf ? s.hpdf[i] : 0.0f;
-        v.diffuse = s.isDiffuse ? (s.isDiffuse[i] != 0) : false;
-    }
+    v.x0 = bcast<LPS>(b.x0, src); v.x1 = bcast<LPS>(b.x1, src); v.x2 = bcast<LPS>(b.x2, src);
+    v.x3 = bcast<LPS>(b.x3, src); v.x4 = bcast<LPS>(b.x4, src); v.x5 = bcast<LPS>(b.x5, src);
+    v.w = bcast<LPS>(b.w, src);
+    v.h = has_h ? bcast<LPS>(b.h, src) : 0.0f;
+    int word;
+    if constexpr (LPS == 64)
+        word = __builtin_amdgcn_readlane(b.diff, src);
+    else
+        word = __shfl(b.diff, src);
+    v.diffuse = has_d && ((word >> (8 * (int)(dpos & 3))) & 0xff) != 0;
     return v;
+}
+
+// Walk samples [s0, s1) of this wave: body(sample, index, in_range) for each
+// group's sample.  Two block buffers, each reloaded right after the block it
+// holds has been consumed, so the loads of block b+1 fly during block b and
+// no register copy (which would force an early vmcnt wait) is needed.
+template <int LPS, class F>
+__device__ __forceinline__ void run_block(const SampleBlock& b, int64_t blk, int64_t s1, int g,
+                                          const SamplesDev& s, F& body) {
+    constexpr int SPW = 64 / LPS;
+    const int cnt = (s1 - blk < 64) ? (int)(s1 - blk) : 64;
+    const bool has_h = s.hpdf != nullptr, has_d = s.isDiffuse != nullptr;
+    for (int t = 0; t < cnt; t += SPW) {
+        // block lane t+g held sample blk+t+g (clamped to s1-1 past the end)
+        int64_t si = blk + t + g;
+        si = (si < s1) ? si : s1 - 1;
+        const SampleVals sv = take_sample<LPS>(b, t, g, has_h, has_d, (uintptr_t)(s.isDiffuse + si));
+        body(sv, blk + t + g, t + g < cnt);
+    }
+}
+
+template <int LPS, class F>
+__device__ __forceinline__ void walk_samples(const SamplesDev& s, int64_t s0, int64_t s1, int lane, int g,
+                                             F&& body) {
+    if (s0 >= s1) return;
+    SampleBlock A = load_block(s, s0, s1, lane);
+    for (int64_t blk = s0; blk < s1; blk += 128) {
+        const SampleBlock B = load_block(s, blk + 64, s1, lane);   // clamped past the end
+        run_block<LPS>(A, blk, s1, g, s, body);
+        A = load_block(s, blk + 128, s1, lane);
+        if (blk + 64 < s1) run_block<LPS>(B, blk + 64, s1, g, s, body);
+    }
 }
 
 // Posterior normalisation of one sample (mixture_model.h:170-191):
@@ -206,13 +274,8 @@ estep_resp_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, int
     load_params<CPL>(ep, Kp, kbase, P);
 
     const bool full = ((kbase + CPL) <= K) && (K % CPL == 0);  // aligned vector row store
-    SampleVals nxt = load_sample<LPS>(s, (s0 + g < s1) ? s0 + g : s1 - 1);
-    for (int64_t base = s0; base < s1; base += SPW) {
-        const int64_t i = base + g;
-        const bool in = i < s1;
-        const SampleVals sv = nxt;
-        const int64_t inx = i + SPW;
-        nxt = load_sample<LPS>(s, (inx < s1) ? inx : s1 - 1);   // prefetch the next sample
+    walk_samples<LPS>(s, s0, s1, lane, g, [&](const SampleVals& sv, int64_t i, bool in)
+                                              __attribute__((always_inline)) {
         const float cf = sv.cfail();
         V q[NP];
         V acc = sp(0.0f);
@@ -223,7 +286,7 @@ estep_resp_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, int
             acc += q[c];
         }
         const Norm nm = normalise<LPS>(acc.x + acc.y, sv);
-        if (!in) continue;
+        if (!in) return;
         float* row = resp + i * (int64_t)K + kbase;
         V o[NP];
 #pragma unroll
@@ -245,7 +308,7 @@ estep_resp_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, int
                 if (kbase + 2 * c + 1 < K) __builtin_nontemporal_store(o[c].y, row + 2 * c + 1);
             }
         }
-    }
+    });
 }
 
 // ---------------------------------------------------------------------------
@@ -279,13 +342,8 @@ estep_stats_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, in
         for (int f = 0; f < ST_FIELDS; ++f) acc[c][f] = sp(0.0f);
     float accH = 0.0f, accWs = 0.0f;
 
-    SampleVals nxt = load_sample<LPS>(s, (s0 + g < s1) ? s0 + g : (s1 > s0 ? s1 - 1 : 0));
-    for (int64_t base = s0; base < s1; base += SPW) {
-        const int64_t i = base + g;
-        const bool in = i < s1;
-        const SampleVals sv = nxt;
-        const int64_t inx = i + SPW;
-        nxt = load_sample<LPS>(s, (inx < s1) ? inx : s1 - 1);   // prefetch the next sample
+    walk_samples<LPS>(s, s0, s1, lane, g, [&](const SampleVals& sv, int64_t, bool in)
+                                              __attribute__((always_inline)) {
         const bool finite_w = __builtin_isfinite(sv.w);
         // sumWeights counts every finite weight (stepwise_tangent.h:462-475)
         accWs += (in && finite_w) ? sv.w : 0.0f;
@@ -341,7 +399,7 @@ estep_stats_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, in
             A[ST_C43] = vfma(v4, ta[c], A[ST_C43]);
             A[ST_C44] = vfma(v4, tb[c], A[ST_C44]);
         }
-    }
+    });
 
     // fold the lane groups of this wave holding the same components
     if constexpr (SPW > 1) {
@@ -483,7 +541,7 @@ static hipError_t launch_stats_t(const float* ep, int Kp, int K, const SamplesDe
 
 // Layouts (choose_layout in sdmm_api.cpp): CPL = 2 with LPS in {8, 16, 32, 64}
 // for K <= 128, then LPS = 64 with CPL in {4, 8}.
-#define SDMM_LAYOUTS(X) X(2, 8) X(2, 16) X(2, 32) X(2, 64) X(4, 64) X(8, 64)
+#define SDMM_LAYOUTS(X) X(2, 8) X(2, 16) X(2, 32) X(2, 64) X(4, 32) X(4, 64) X(8, 64)
 
 hipError_t launch_estep_resp(int cpl, int lps, const float* ep, int Kp, int K, const SamplesDev& s,
                              int64_t n, int64_t chunk, float* resp, hipStream_t st) {

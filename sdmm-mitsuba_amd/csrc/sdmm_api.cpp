@@ -169,7 +169,8 @@ void hemisphere_init(const float* positions, const float* normals, int nPosition
 
 // ==========================================================================
 struct sdmm_mix {
-    int K = 0, Kp = 0, cpl = 1, lps = 64;
+    int K = 0, Kp = 0, cpl = 1, lps = 64;   // statistics E-step layout
+    int rcpl = 2, rlps = 64;                 // responsibility E-step layout (same Kp)
     int device = 0;
     int cus = 256;
     int resp_blocks = 2, stats_blocks = 2;   // resident 256-thread WGs per CU
@@ -217,8 +218,8 @@ struct Split {
     int wpb;
 };
 
-Split split_for(const sdmm_mix* m, int64_t n, int blocks_per_cu) {
-    const int spw = 64 / m->lps;
+Split split_for(const sdmm_mix* m, int64_t n, int lps, int blocks_per_cu) {
+    const int spw = 64 / lps;
     const int64_t target_waves = (int64_t)m->cus * 4 * (blocks_per_cu > 0 ? blocks_per_cu : 2);
     int64_t chunk = (n + target_waves - 1) / target_waves;
     if (chunk < 4 * spw) chunk = 4 * spw;
@@ -260,7 +261,7 @@ int ensure_partials(sdmm_mix* m, int rows) {
 }
 
 int run_estep_stats(sdmm_mix* m, const sdmm_samples* s, double* stats_out) {
-    const Split sp = split_for(m, s->n, m->stats_blocks);
+    const Split sp = split_for(m, s->n, m->lps, m->stats_blocks);
     int r = ensure_partials(m, sp.blocks);
     if (r) return r;
     SamplesDev d = to_dev(s);
@@ -312,7 +313,15 @@ int sdmm_create(int K, const sdmm_em_params* params, int device, sdmm_mix** out)
     if (hipSetDevice(device) != hipSuccess) return cleanup(fail(SDMM_E_HIP, "hipSetDevice failed"));
     (void)hipDeviceGetAttribute(&m->cus, hipDeviceAttributeMultiprocessorCount, device);
     if (m->cus <= 0) m->cus = 256;
-    if (estep_occupancy(m->cpl, m->lps, m->Kp, &m->resp_blocks, &m->stats_blocks) != hipSuccess)
+    // responsibilities: for 64 < K <= 128, 4 components per lane and 2 samples
+    // per wave halve the per-sample reduction/normalisation overhead per pair
+    // and give each lane two independent packed chains (same Kp = 128)
+    m->rcpl = cpl;
+    m->rlps = lps;
+    if (K > 64 && K <= 128) { m->rcpl = 4; m->rlps = 32; }
+    int unused = 0;
+    if (estep_occupancy(m->rcpl, m->rlps, m->Kp, &m->resp_blocks, &unused) != hipSuccess ||
+        estep_occupancy(m->cpl, m->lps, m->Kp, &unused, &m->stats_blocks) != hipSuccess)
         return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
     if (hipStreamCreateWithFlags(&m->own_stream, hipStreamNonBlocking) != hipSuccess)
         return cleanup(fail(SDMM_E_HIP, "hipStreamCreate failed"));
@@ -389,6 +398,15 @@ void sdmm_destroy(sdmm_mix* m) {
 }
 
 int sdmm_num_components(const sdmm_mix* m) { return m ? m->K : 0; }
+
+int sdmm_layout(const sdmm_mix* m, int* resp_cpl, int* resp_lps, int* stats_cpl, int* stats_lps) {
+    if (!m) return fail(SDMM_E_INVALID, "null handle");
+    if (resp_cpl) *resp_cpl = m->rcpl;
+    if (resp_lps) *resp_lps = m->rlps;
+    if (stats_cpl) *stats_cpl = m->cpl;
+    if (stats_lps) *stats_lps = m->lps;
+    return SDMM_OK;
+}
 
 int sdmm_set_stream(sdmm_mix* m, void* hip_stream) {
     if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
@@ -522,8 +540,8 @@ int sdmm_responsibilities(sdmm_mix* m, const sdmm_samples* s, float* resp) {
     int r = check_samples(s);
     if (r) return r;
     if (s->n == 0) return SDMM_OK;
-    const Split sp = split_for(m, s->n, m->resp_blocks);
-    HIP_TRY(launch_estep_resp(m->cpl, m->lps, m->ep, m->Kp, m->K, to_dev(s), s->n, sp.chunk, resp,
+    const Split sp = split_for(m, s->n, m->rlps, m->resp_blocks);
+    HIP_TRY(launch_estep_resp(m->rcpl, m->rlps, m->ep, m->Kp, m->K, to_dev(s), s->n, sp.chunk, resp,
                               m->stream));
     return SDMM_OK;
 }
