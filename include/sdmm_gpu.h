@@ -86,6 +86,11 @@ int sdmm_num_components(const sdmm_mix* m);
 /* Diagnostics: E-step kernel layouts (components per lane, lanes per sample)
  * of the responsibility and statistics kernels.  Any pointer may be NULL. */
 int sdmm_layout(const sdmm_mix* m, int* resp_cpl, int* resp_lps, int* stats_cpl, int* stats_lps);
+/* Guided queries keep a per-query list of at most `cap` candidate components
+ * (default and maximum 40); queries that do not fit take the full-K path.
+ * Results are identical for every cap; 0 sends every query down the full-K
+ * path (a testing knob). */
+int sdmm_set_guide_capacity(sdmm_mix* m, int cap);
 /* Work is enqueued on this hipStream_t, taken literally (NULL = the HIP null
  * stream).  A new handle starts on its own non-blocking stream, whose value
  * sdmm_get_stream returns before any sdmm_set_stream call. */

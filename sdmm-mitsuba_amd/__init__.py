@@ -83,6 +83,7 @@ def lib():
         L.sdmm_create.argtypes = [C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
         L.sdmm_destroy.argtypes = [C.c_void_p]
         L.sdmm_layout.argtypes = [C.c_void_p] + [C.POINTER(C.c_int)] * 4
+        L.sdmm_set_guide_capacity.argtypes = [C.c_void_p, C.c_int]
         L.sdmm_set_stream.argtypes = [C.c_void_p, C.c_void_p]
         L.sdmm_synchronize.argtypes = [C.c_void_p]
         L.sdmm_init_hemisphere.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_float,
@@ -119,6 +120,7 @@ def stats_len(K: int) -> int:
 
 EXPORTED_SYMBOLS = [
     "sdmm_em_params_default", "sdmm_create", "sdmm_destroy", "sdmm_num_components", "sdmm_layout",
+    "sdmm_set_guide_capacity",
     "sdmm_set_stream", "sdmm_get_stream", "sdmm_synchronize", "sdmm_init_hemisphere",
     "sdmm_hemisphere_init_host", "sdmm_em_step", "sdmm_em_step_host", "sdmm_stats_len",
     "sdmm_estep_stats", "sdmm_mstep", "sdmm_responsibilities", "sdmm_guide_batch", "sdmm_pdf_batch",
@@ -285,6 +287,10 @@ class SDMM:
             dt = np.float32 if k in ("bpriors", "bdepth") else np.float64
             arrs.append(np.ascontiguousarray(st[k], dt))
         _check(lib().sdmm_set_state(self.h, *[a.ctypes.data for a in arrs]))
+
+    def set_guide_capacity(self, cap: int):
+        """Per-query candidate-list capacity of the guided-query kernel (0..40)."""
+        _check(lib().sdmm_set_guide_capacity(self.h, cap))
 
     def layout(self) -> dict:
         """E-step kernel layouts: (components per lane, lanes per sample)."""

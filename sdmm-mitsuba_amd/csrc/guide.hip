@@ -125,29 +125,226 @@ __device__ __forceinline__ float cond_component_pdf(const float* gp, int Kp, int
     p *= gp_ld(gp, Kp, GP_CDI, k) * a;
     return p;
 }
+// validity of joint component k's conditional at c (cond_mean_dir's
+// TangentSpace::exp check, same float operations) without the sin/cos
+__device__ __forceinline__ bool cond_valid(const float* gp, int Kp, int k, const float c[3]) {
+    float d0 = c[0] - gp_ld(gp, Kp, GP_MU0, k);
+    float d1 = c[1] - gp_ld(gp, Kp, GP_MU1, k);
+    float d2 = c[2] - gp_ld(gp, Kp, GP_MU2, k);
+    float t0 = gp_ld(gp, Kp, GP_P00, k) * d0 + gp_ld(gp, Kp, GP_P01, k) * d1 + gp_ld(gp, Kp, GP_P02, k) * d2;
+    float t1 = gp_ld(gp, Kp, GP_P10, k) * d0 + gp_ld(gp, Kp, GP_P11, k) * d1 + gp_ld(gp, Kp, GP_P12, k) * d2;
+    float length = sqrtf(t0 * t0 + t1 * t1);
+    return !((double)length >= kPi);
+}
 
-// Shared per-query conditional construction.  Returns lastIdx (0 if the
-// conditional is invalid); fills the LDS slot list.  wl: [K][T] weights whose
-// sign bit marks "taken"; sl: [K][T] slot -> component.
-struct CondInfo {
-    int lastIdx;
-    float invSum;   // 1/sum if finite else 1 (no scaling)
-    bool scaled;
-    float sum2;
+// ---------------------------------------------------------------------------
+// The part of a query after the kept (sorted, cut-off) prefix is known:
+// normalisation, sampleDiscreteCdf, Box-Muller + exp map, and the conditional
+// mixture pdf (mixture_model.h:286-303, :72-75, :113-121; utils.h:64-115;
+// mvtn.h:321-339, :367-381).  Slots supplies slot i -> (component, raw
+// weight, valid); weights of invalid conditionals count as 0 (oracle
+// convention, oracle/sdmm_oracle.c or_conditional_create).
+struct QueryOut {
+    float d[3];
+    float pdf;
+    int comp;
 };
 
-__device__ __forceinline__ CondInfo build_conditional(const float* gp, int Kp, int K, const float c[3],
-                                                      float* wl, int* sl, int T, int tid, float norm3) {
+template <class Slots>
+__device__ __forceinline__ QueryOut finish_query(const float* gp, int Kp, const float c[3], const float u[3],
+                                                 int lastIdx, float accum, const Slots& S,
+                                                 const float* dir_in, GuideConsts gc) {
+    QueryOut o{{0.0f, 0.0f, 0.0f}, 0.0f, -1};
+    // sum of the kept weights (std::accumulate) == accum (same values, same order)
+    const float invSum = 1.0f / accum;
+    const bool scaled = __builtin_isfinite(invSum);
+    float sum2 = 0.0f;
+    for (int i = 0; i < lastIdx; ++i) {
+        float wi = S.valid(i) ? S.weight(i) : 0.0f;
+        if (scaled) wi = wi * invSum;
+        sum2 += wi;
+    }
+    if (lastIdx == 0 || sum2 == 0.0f) return o;   // createCdf(true) fails: BSDF only
+    auto slot_w = [&](int i) {
+        float wi = S.valid(i) ? S.weight(i) : 0.0f;
+        if (scaled) wi = wi * invSum;
+        return wi / sum2;
+    };
+    float dir[3];
+    if (!dir_in) {
+        // sampleDiscreteCdf: lower_bound == first slot with cdf >= u, else tie walk
+        float cdf = 0.0f, prev = 0.0f;
+        int slot = -1, runStart = 0;
+        for (int i = 0; i < lastIdx; ++i) {
+            cdf += slot_w(i);
+            if (i == 0 || cdf != prev) runStart = i;
+            prev = cdf;
+            if (cdf >= u[0]) { slot = i; break; }
+        }
+        if (slot < 0) slot = runStart;
+        const int ksel = S.comp(slot);
+        float esel[3];
+        cond_mean_dir(gp, Kp, ksel, c, esel);
+        // MVTN::sample of the conditional component (Box-Muller, L z, exp map)
+        const float radius = sqrtf(-2.0f * fl_log(1.0f - u[1]));
+        const float theta = (float)(2.0 * kPi * (double)u[2]);
+        const double res0 = sin((double)theta), res1 = cos((double)theta);
+        const float z0 = radius * (float)res0, z1 = radius * (float)res1;
+        const float L00 = gp_ld(gp, Kp, GP_CL00, ksel), L10 = gp_ld(gp, Kp, GP_CL10, ksel);
+        const float L11 = gp_ld(gp, Kp, GP_CL11, ksel);
+        const float v0 = L00 * z0 + 0.0f * z1;
+        const float v1 = L10 * z0 + L11 * z1;
+        float tof[9];
+        coordinates_f(esel, tof);
+        ts_exp_dir(tof, v0, v1, dir);
+        o.comp = ksel;
+    } else {
+        dir[0] = dir_in[0]; dir[1] = dir_in[1]; dir[2] = dir_in[2];
+    }
+    // MixtureModel::pdf over the conditional (the gmmPdf of pdfSurface)
+    float acc = 0.0f;
+    for (int i = 0; i < lastIdx; ++i) {
+        const float f = slot_w(i);
+        if (f == 0.0f) continue;
+        const int k = S.comp(i);
+        float e[3];
+        cond_mean_dir(gp, Kp, k, c, e);
+        acc += f * cond_component_pdf(gp, Kp, k, e, dir, gc.norm2);
+    }
+    o.d[0] = dir[0]; o.d[1] = dir[1]; o.d[2] = dir[2];
+    o.pdf = acc;
+    return o;
+}
+
+// ---------------------------------------------------------------------------
+// Fast path: per-query candidate list.
+//
+// Pass 1 forms totalMass exactly as the reference (sequential float sum in
+// component order, mixture_model.h:248-261).  No component with weight
+// w < tau = (totalMass - cutoff) / K * 0.999 can be in the kept prefix: all
+// of them together hold less than totalMass - cutoff, so the sorted
+// accumulation reaches the cutoff before the first of them (the 0.999 covers
+// the float rounding of the sums, |error| <= K eps << 1e-3).  Pass 2
+// recomputes the weights and keeps those >= tau in an LDS list sorted
+// (weight desc, index asc) -- the order of the reference's std::sort with
+// ties broken towards the lower index -- together with the validity of their
+// conditionals.  The cutoff walk then runs over that list.  A query falls back
+// to the full-K path (guide_fallback_kernel) when totalMass is not finite,
+// the list overflows, or the list runs out before the cutoff (only possible
+// when invalid conditionals zero out kept weights).  With K = 128 the list
+// holds a median of ~10 and a 99th percentile of ~34 entries.
+constexpr int kGuideCap = 40;
+
+struct CandSlots {
+    const float* cw;
+    const unsigned short* ck;
+    int T, tid;
+    __device__ float weight(int i) const { return cw[i * T + tid]; }
+    __device__ int comp(int i) const { return ck[i * T + tid] & 0x7fff; }
+    __device__ bool valid(int i) const { return (ck[i * T + tid] >> 15) != 0; }
+};
+
+// returns lastIdx >= 0, or -1: needs the full-K fallback
+__device__ __forceinline__ int build_candidates(const float* gp, int Kp, int K, const float c[3], float* cw,
+                                                unsigned short* ck, int T, int tid, float norm3, int cap,
+                                                float& accum) {
+    float total = 0.0f;
+    for (int k = 0; k < K; ++k) total += gp_ld(gp, Kp, GP_W, k) * marginal_pdf(gp, Kp, k, c, norm3);
+    if (!__builtin_isfinite(total)) return -1;
+    const float cutoff = (float)(0.99 * (double)total);
+    const double tau = ((double)total - (double)cutoff) / (double)K * 0.999;
+    int cnt = 0;
+    bool over = false;
+    for (int k = 0; k < K; ++k) {
+        const float w = gp_ld(gp, Kp, GP_W, k) * marginal_pdf(gp, Kp, k, c, norm3);
+        if (!((double)w >= tau)) continue;
+        if (cnt == cap) { over = true; continue; }
+        const unsigned short key = (unsigned short)(k | (cond_valid(gp, Kp, k, c) ? 0x8000 : 0));
+        // stable insertion (descending): equal weights keep index order
+        int pos = cnt;
+        while (pos > 0 && cw[(pos - 1) * T + tid] < w) {
+            cw[pos * T + tid] = cw[(pos - 1) * T + tid];
+            ck[pos * T + tid] = ck[(pos - 1) * T + tid];
+            --pos;
+        }
+        cw[pos * T + tid] = w;
+        ck[pos * T + tid] = key;
+        ++cnt;
+    }
+    if (over) return -1;
+    accum = 0.0f;
+    for (int i = 0; i < cnt; ++i) {
+        const float wi = (ck[i * T + tid] >> 15) ? cw[i * T + tid] : 0.0f;
+        accum += wi;
+        if (accum >= cutoff) return i + 1;
+    }
+    // cutoff never reached inside the list: exact only if the list is all of K
+    return (cnt == K) ? K : -1;
+}
+
+template <bool PDF_ONLY>
+__global__ void __launch_bounds__(64)
+guide_cand_kernel(const float* __restrict__ gp, int Kp, int K, int64_t nq, const float* __restrict__ c0,
+                  const float* __restrict__ c1, const float* __restrict__ c2, const float* __restrict__ u0,
+                  const float* __restrict__ u1, const float* __restrict__ u2, const float* __restrict__ e0,
+                  const float* __restrict__ e1, const float* __restrict__ e2, float* __restrict__ d0,
+                  float* __restrict__ d1, float* __restrict__ d2, float* __restrict__ pdf,
+                  int32_t* __restrict__ comp, GuideConsts gc, int cap, int* __restrict__ fb_count,
+                  int32_t* __restrict__ fb_list) {
+    __shared__ float cw[kGuideCap * 64];
+    __shared__ unsigned short ck[kGuideCap * 64];
+    const int T = 64;
+    const int tid = threadIdx.x;
+    const int64_t q = (int64_t)blockIdx.x * T + tid;
+    if (q >= nq) return;
+    const float c[3] = {c0[q], c1[q], c2[q]};
+    float accum = 0.0f;
+    const int lastIdx = build_candidates(gp, Kp, K, c, cw, ck, T, tid, gc.norm3, cap, accum);
+    if (lastIdx < 0) {
+        fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
+        return;
+    }
+    const CandSlots S{cw, ck, T, tid};
+    if constexpr (PDF_ONLY) {
+        const float dir[3] = {e0[q], e1[q], e2[q]};
+        const QueryOut o = finish_query(gp, Kp, c, nullptr, lastIdx, accum, S, dir, gc);
+        pdf[q] = o.pdf;
+    } else {
+        const float u[3] = {u0[q], u1[q], u2[q]};
+        const QueryOut o = finish_query(gp, Kp, c, u, lastIdx, accum, S, nullptr, gc);
+        d0[q] = o.d[0]; d1[q] = o.d[1]; d2[q] = o.d[2];
+        pdf[q] = o.pdf;
+        comp[q] = o.comp;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Fallback: the full-K conditional of one query.  The per-query marginal
+// weights live in LDS laid out [k][thread] (conflict-free); the sort is an
+// incremental selection that stops at the 0.99-mass cutoff.
+struct FullSlots {
+    const float* gp;
+    int Kp;
+    const float* c;
+    const float* wl;
+    const int* sl;
+    int T, tid;
+    __device__ int comp(int i) const { return sl[i * T + tid]; }
+    __device__ float weight(int i) const { return -wl[comp(i) * T + tid]; }
+    __device__ bool valid(int i) const { return cond_valid(gp, Kp, comp(i), c); }
+};
+
+__device__ __forceinline__ int build_full(const float* gp, int Kp, int K, const float c[3], float* wl, int* sl,
+                                          int T, int tid, float norm3, float& accum) {
     float total = 0.0f;
     for (int k = 0; k < K; ++k) {
-        const float mp = marginal_pdf(gp, Kp, k, c, norm3);
-        const float wk = gp_ld(gp, Kp, GP_W, k) * mp;
+        const float wk = gp_ld(gp, Kp, GP_W, k) * marginal_pdf(gp, Kp, k, c, norm3);
         wl[k * T + tid] = wk;
         total += wk;
     }
     const float cutoff = (float)(0.99 * (double)total);
-    float accum = 0.0f;
-    int lastIdx = K;
+    accum = 0.0f;
+    int lastIdx = K;   // the reference leaves it uninitialised if never reached
     for (int i = 0; i < K; ++i) {
         int best = -1;
         float bw = 0.0f;
@@ -159,136 +356,44 @@ __device__ __forceinline__ CondInfo build_conditional(const float* gp, int Kp, i
         if (best < 0) { lastIdx = i; break; }
         wl[best * T + tid] = -bw;
         sl[i * T + tid] = best;
-        float e[3];
-        float wi = bw;
-        if (!cond_mean_dir(gp, Kp, best, c, e)) wi = 0.0f;  // oracle convention
-        accum += wi;
+        accum += cond_valid(gp, Kp, best, c) ? bw : 0.0f;
         if (accum >= cutoff) { lastIdx = i + 1; break; }
     }
-    CondInfo ci;
-    ci.lastIdx = lastIdx;
-    // sum of the kept weights (std::accumulate) == accum (same values, same order)
-    const float invSum = 1.0f / accum;
-    ci.scaled = __builtin_isfinite(invSum);
-    ci.invSum = invSum;
-    float sum2 = 0.0f;
-    for (int i = 0; i < lastIdx; ++i) {
-        const int k = sl[i * T + tid];
-        float wi = -wl[k * T + tid];
-        float e[3];
-        if (!cond_mean_dir(gp, Kp, k, c, e)) wi = 0.0f;
-        if (ci.scaled) wi = wi * invSum;
-        sum2 += wi;
-    }
-    ci.sum2 = sum2;
-    return ci;
+    return lastIdx;
 }
 
-// normalised conditional weight of slot i (createCdf(true) after the 1/sum scale)
-__device__ __forceinline__ float slot_weight(const float* gp, int Kp, const float c[3], const CondInfo& ci,
-                                             const float* wl, const int* sl, int T, int tid, int i,
-                                             int& k, float e[3]) {
-    k = sl[i * T + tid];
-    float wi = -wl[k * T + tid];
-    if (!cond_mean_dir(gp, Kp, k, c, e)) wi = 0.0f;
-    if (ci.scaled) wi = wi * ci.invSum;
-    return wi / ci.sum2;
-}
-
+template <bool PDF_ONLY>
 __global__ void __launch_bounds__(64)
-guide_kernel(const float* __restrict__ gp, int Kp, int K, int64_t nq, const float* __restrict__ c0,
-             const float* __restrict__ c1, const float* __restrict__ c2, const float* __restrict__ u0,
-             const float* __restrict__ u1, const float* __restrict__ u2, float* __restrict__ d0,
-             float* __restrict__ d1, float* __restrict__ d2, float* __restrict__ pdf,
-             int32_t* __restrict__ comp, GuideConsts gc) {
+guide_fallback_kernel(const float* __restrict__ gp, int Kp, int K, const float* __restrict__ c0,
+                      const float* __restrict__ c1, const float* __restrict__ c2, const float* __restrict__ u0,
+                      const float* __restrict__ u1, const float* __restrict__ u2, const float* __restrict__ e0,
+                      const float* __restrict__ e1, const float* __restrict__ e2, float* __restrict__ d0,
+                      float* __restrict__ d1, float* __restrict__ d2, float* __restrict__ pdf,
+                      int32_t* __restrict__ comp, GuideConsts gc, const int* __restrict__ fb_count,
+                      const int32_t* __restrict__ fb_list) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int T = blockDim.x;
     const int tid = threadIdx.x;
     float* wl = lds;
     int* sl = (int*)(lds + (size_t)K * T);
-    const int64_t q = (int64_t)blockIdx.x * T + tid;
-    if (q >= nq) return;
-    const float c[3] = {c0[q], c1[q], c2[q]};
-    const float u[3] = {u0[q], u1[q], u2[q]};
-    const CondInfo ci = build_conditional(gp, Kp, K, c, wl, sl, T, tid, gc.norm3);
-    if (ci.lastIdx == 0 || ci.sum2 == 0.0f) {
-        d0[q] = 0.0f; d1[q] = 0.0f; d2[q] = 0.0f; pdf[q] = 0.0f; comp[q] = -1;
-        return;
+    const int count = *fb_count;
+    for (int idx = blockIdx.x * T + tid; idx < count; idx += gridDim.x * T) {
+        const int64_t q = fb_list[idx];
+        const float c[3] = {c0[q], c1[q], c2[q]};
+        float accum = 0.0f;
+        const int lastIdx = build_full(gp, Kp, K, c, wl, sl, T, tid, gc.norm3, accum);
+        const FullSlots S{gp, Kp, c, wl, sl, T, tid};
+        if constexpr (PDF_ONLY) {
+            const float dir[3] = {e0[q], e1[q], e2[q]};
+            pdf[q] = finish_query(gp, Kp, c, nullptr, lastIdx, accum, S, dir, gc).pdf;
+        } else {
+            const float u[3] = {u0[q], u1[q], u2[q]};
+            const QueryOut o = finish_query(gp, Kp, c, u, lastIdx, accum, S, nullptr, gc);
+            d0[q] = o.d[0]; d1[q] = o.d[1]; d2[q] = o.d[2];
+            pdf[q] = o.pdf;
+            comp[q] = o.comp;
+        }
     }
-    // sampleDiscreteCdf: lower_bound == first slot with cdf >= u, else tie walk
-    float cdf = 0.0f, prev = 0.0f;
-    int slot = -1, runStart = 0;
-    int ksel = -1;
-    float esel[3] = {0.0f, 0.0f, 0.0f};
-    for (int i = 0; i < ci.lastIdx; ++i) {
-        int k;
-        float e[3];
-        const float f = slot_weight(gp, Kp, c, ci, wl, sl, T, tid, i, k, e);
-        cdf += f;
-        if (i == 0 || cdf != prev) runStart = i;
-        prev = cdf;
-        if (cdf >= u[0]) { slot = i; ksel = k; esel[0] = e[0]; esel[1] = e[1]; esel[2] = e[2]; break; }
-    }
-    if (slot < 0) {
-        slot = runStart;
-        float e[3];
-        int k;
-        slot_weight(gp, Kp, c, ci, wl, sl, T, tid, slot, k, e);
-        ksel = k; esel[0] = e[0]; esel[1] = e[1]; esel[2] = e[2];
-    }
-    // MVTN::sample of the conditional component (Box-Muller, L z, exp map)
-    const float radius = sqrtf(-2.0f * fl_log(1.0f - u[1]));
-    const float theta = (float)(2.0 * kPi * (double)u[2]);
-    const double res0 = sin((double)theta), res1 = cos((double)theta);
-    const float z0 = radius * (float)res0, z1 = radius * (float)res1;
-    const float L00 = gp_ld(gp, Kp, GP_CL00, ksel), L10 = gp_ld(gp, Kp, GP_CL10, ksel);
-    const float L11 = gp_ld(gp, Kp, GP_CL11, ksel);
-    const float v0 = L00 * z0 + 0.0f * z1;
-    const float v1 = L10 * z0 + L11 * z1;
-    float tof[9];
-    coordinates_f(esel, tof);
-    float dir[3];
-    ts_exp_dir(tof, v0, v1, dir);
-    // MixtureModel::pdf over the conditional (the gmmPdf of pdfSurface)
-    float acc = 0.0f;
-    for (int i = 0; i < ci.lastIdx; ++i) {
-        int k;
-        float e[3];
-        const float f = slot_weight(gp, Kp, c, ci, wl, sl, T, tid, i, k, e);
-        if (f == 0.0f) continue;
-        acc += f * cond_component_pdf(gp, Kp, k, e, dir, gc.norm2);
-    }
-    d0[q] = dir[0]; d1[q] = dir[1]; d2[q] = dir[2];
-    pdf[q] = acc;
-    comp[q] = ksel;
-}
-
-// gmmPdf of a given direction (BSDF-sampled bounce): conditional + pdf.
-__global__ void __launch_bounds__(64)
-guide_pdf_kernel(const float* __restrict__ gp, int Kp, int K, int64_t nq, const float* __restrict__ c0,
-                 const float* __restrict__ c1, const float* __restrict__ c2, const float* __restrict__ e0,
-                 const float* __restrict__ e1, const float* __restrict__ e2, float* __restrict__ pdf,
-                 GuideConsts gc) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int T = blockDim.x;
-    const int tid = threadIdx.x;
-    float* wl = lds;
-    int* sl = (int*)(lds + (size_t)K * T);
-    const int64_t q = (int64_t)blockIdx.x * T + tid;
-    if (q >= nq) return;
-    const float c[3] = {c0[q], c1[q], c2[q]};
-    const float dir[3] = {e0[q], e1[q], e2[q]};
-    const CondInfo ci = build_conditional(gp, Kp, K, c, wl, sl, T, tid, gc.norm3);
-    if (ci.lastIdx == 0 || ci.sum2 == 0.0f) { pdf[q] = 0.0f; return; }
-    float acc = 0.0f;
-    for (int i = 0; i < ci.lastIdx; ++i) {
-        int k;
-        float e[3];
-        const float f = slot_weight(gp, Kp, c, ci, wl, sl, T, tid, i, k, e);
-        if (f == 0.0f) continue;
-        acc += f * cond_component_pdf(gp, Kp, k, e, dir, gc.norm2);
-    }
-    pdf[q] = acc;
 }
 
 // lower_bound + tie walk on caller-provided CDFs (the bit-exact index KAT).
@@ -310,33 +415,49 @@ __global__ void sample_cdf_kernel(const float* __restrict__ cdf, int n, const fl
     out[q] = lo;
 }
 
-static int guide_threads() { return 64; }
-
+// Candidate pass over all queries, then the fallback queries (listed by the
+// candidate kernel) through the full-K path; both on stream st.
+// fb_count: one device int, fb_list: nq device ints (scratch).
 hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float* const c[3],
-                        const float* const u[3], float* const d[3], float* pdf, int32_t* comp,
-                        float norm2, float norm3, hipStream_t st) {
+                        const float* const u[3], const float* const dgiven[3], float* const d[3], float* pdf,
+                        int32_t* comp, float norm2, float norm3, int cap, int* fb_count, int32_t* fb_list,
+                        int cus, hipStream_t st) {
     if (nq <= 0) return hipSuccess;
-    const int T = guide_threads();
-    const size_t lds = (size_t)K * T * (sizeof(float) + sizeof(int));
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    cap = (cap < 0) ? 0 : (cap > kGuideCap ? kGuideCap : cap);
+    if (nq > INT32_MAX) return hipErrorInvalidValue;
+    const int T = 64;
+    const size_t lds_fb = (size_t)K * T * (sizeof(float) + sizeof(int));
+    if (lds_fb > 160 * 1024) return hipErrorInvalidValue;
     GuideConsts gc{norm2, norm3};
+    hipError_t e = hipMemsetAsync(fb_count, 0, sizeof(int), st);
+    if (e != hipSuccess) return e;
     const int64_t blocks = (nq + T - 1) / T;
-    hipLaunchKernelGGL(guide_kernel, dim3((unsigned)blocks), dim3(T), lds, st, gp, Kp, K, nq, c[0], c[1],
-                       c[2], u[0], u[1], u[2], d[0], d[1], d[2], pdf, comp, gc);
-    return hipGetLastError();
-}
-
-hipError_t launch_guide_pdf(const float* gp, int Kp, int K, int64_t nq, const float* const c[3],
-                            const float* const d[3], float* pdf, float norm2, float norm3,
-                            hipStream_t st) {
-    if (nq <= 0) return hipSuccess;
-    const int T = guide_threads();
-    const size_t lds = (size_t)K * T * (sizeof(float) + sizeof(int));
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
-    GuideConsts gc{norm2, norm3};
-    const int64_t blocks = (nq + T - 1) / T;
-    hipLaunchKernelGGL(guide_pdf_kernel, dim3((unsigned)blocks), dim3(T), lds, st, gp, Kp, K, nq, c[0],
-                       c[1], c[2], d[0], d[1], d[2], pdf, gc);
+    const int fb_blocks = cus * 2;
+    const bool pdf_only = dgiven != nullptr;
+    const float* g0 = pdf_only ? dgiven[0] : nullptr;
+    const float* g1 = pdf_only ? dgiven[1] : nullptr;
+    const float* g2 = pdf_only ? dgiven[2] : nullptr;
+    const float* v0 = pdf_only ? nullptr : u[0];
+    const float* v1 = pdf_only ? nullptr : u[1];
+    const float* v2 = pdf_only ? nullptr : u[2];
+    float* o0 = pdf_only ? nullptr : d[0];
+    float* o1 = pdf_only ? nullptr : d[1];
+    float* o2 = pdf_only ? nullptr : d[2];
+    if (pdf_only) {
+        hipLaunchKernelGGL(guide_cand_kernel<true>, dim3((unsigned)blocks), dim3(T), 0, st, gp, Kp, K, nq, c[0],
+                           c[1], c[2], v0, v1, v2, g0, g1, g2, o0, o1, o2, pdf, comp, gc, cap, fb_count, fb_list);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(guide_fallback_kernel<true>, dim3(fb_blocks), dim3(T), lds_fb, st, gp, Kp, K, c[0],
+                           c[1], c[2], v0, v1, v2, g0, g1, g2, o0, o1, o2, pdf, comp, gc, fb_count, fb_list);
+    } else {
+        hipLaunchKernelGGL(guide_cand_kernel<false>, dim3((unsigned)blocks), dim3(T), 0, st, gp, Kp, K, nq, c[0],
+                           c[1], c[2], v0, v1, v2, g0, g1, g2, o0, o1, o2, pdf, comp, gc, cap, fb_count, fb_list);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(guide_fallback_kernel<false>, dim3(fb_blocks), dim3(T), lds_fb, st, gp, Kp, K, c[0],
+                           c[1], c[2], v0, v1, v2, g0, g1, g2, o0, o1, o2, pdf, comp, gc, fb_count, fb_list);
+    }
     return hipGetLastError();
 }
 

@@ -35,11 +35,10 @@ hipError_t launch_pack_all(int K, int Kp, const CanonDev& C, float* ep, float* g
 hipError_t launch_mstep(int K, int Kp, const double* stats, int64_t nSamples, const CanonDev& C,
                         const EmStateDev& S, float* ep, float* gp, float norm5, hipStream_t st);
 hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float* const c[3],
-                        const float* const u[3], float* const d[3], float* pdf, int32_t* comp,
-                        float norm2, float norm3, hipStream_t st);
-hipError_t launch_guide_pdf(const float* gp, int Kp, int K, int64_t nq, const float* const c[3],
-                            const float* const d[3], float* pdf, float norm2, float norm3,
-                            hipStream_t st);
+                        const float* const u[3], const float* const dgiven[3], float* const d[3], float* pdf,
+                        int32_t* comp, float norm2, float norm3, int cap, int* fb_count, int32_t* fb_list,
+                        int cus, hipStream_t st);
+constexpr int kGuideCapMax = 40;
 hipError_t launch_sample_cdf(const float* cdf, int n, const float* u, int64_t nq, int32_t* out,
                              hipStream_t st);
 }  // namespace sdmm
@@ -174,6 +173,10 @@ struct sdmm_mix {
     int device = 0;
     int cus = 256;
     int resp_blocks = 2, stats_blocks = 2;   // resident 256-thread WGs per CU
+    // guided-query scratch: fallback counter + list of fallback query indices
+    int guide_cap = kGuideCapMax;   // candidate-list capacity (sdmm_set_guide_capacity)
+    mutable int* guide_fb = nullptr;
+    mutable int64_t guide_fb_cap = 0;
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
     sdmm_em_params params{};
@@ -257,6 +260,22 @@ int ensure_partials(sdmm_mix* m, int rows) {
     int cap = rows < 1024 ? 1024 : rows;
     HIP_TRY(hipMalloc(&m->partials, sizeof(float) * (size_t)cap * m->pstride));
     m->partial_rows = cap;
+    return SDMM_OK;
+}
+
+// [count, list...] of fallback guided queries; grows on demand (stream-ordered
+// free is not needed: the previous buffer is only released after a sync)
+int ensure_guide_scratch(const sdmm_mix* m, int64_t nq) {
+    if (nq + 1 <= m->guide_fb_cap) return SDMM_OK;
+    if (m->guide_fb) {
+        HIP_TRY(hipStreamSynchronize(m->stream));
+        HIP_TRY(hipFree(m->guide_fb));
+        m->guide_fb = nullptr;
+        m->guide_fb_cap = 0;
+    }
+    const int64_t cap = (nq + 1 < (1 << 20)) ? (1 << 20) : nq + 1;
+    HIP_TRY(hipMalloc(&m->guide_fb, sizeof(int) * (size_t)cap));
+    m->guide_fb_cap = cap;
     return SDMM_OK;
 }
 
@@ -392,12 +411,20 @@ void sdmm_destroy(sdmm_mix* m) {
     if (m->stream && m->stream != m->own_stream) (void)hipStreamSynchronize(m->stream);
     if (m->block) (void)hipFree(m->block);
     if (m->partials) (void)hipFree(m->partials);
+    if (m->guide_fb) (void)hipFree(m->guide_fb);
     if (m->staging) (void)hipFree(m->staging);
     if (m->own_stream) (void)hipStreamDestroy(m->own_stream);
     delete m;
 }
 
 int sdmm_num_components(const sdmm_mix* m) { return m ? m->K : 0; }
+
+int sdmm_set_guide_capacity(sdmm_mix* m, int cap) {
+    if (!m) return fail(SDMM_E_INVALID, "null handle");
+    if (cap < 0 || cap > kGuideCapMax) return fail(SDMM_E_INVALID, "guide capacity must be in [0, 40]");
+    m->guide_cap = cap;
+    return SDMM_OK;
+}
 
 int sdmm_layout(const sdmm_mix* m, int* resp_cpl, int* resp_lps, int* stats_cpl, int* stats_lps) {
     if (!m) return fail(SDMM_E_INVALID, "null handle");
@@ -550,7 +577,11 @@ int sdmm_guide_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], con
                      float* const d[3], float* pdf, int32_t* comp) {
     if (!m || !c || !u || !d || !pdf || !comp) return fail(SDMM_E_INVALID, "invalid argument");
     if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
-    HIP_TRY(launch_guide(m->gp, m->Kp, m->K, nq, c, u, d, pdf, comp, m->norm2, m->norm3, m->stream));
+    if (nq <= 0) return SDMM_OK;
+    int r = ensure_guide_scratch(m, nq);
+    if (r) return r;
+    HIP_TRY(launch_guide(m->gp, m->Kp, m->K, nq, c, u, nullptr, d, pdf, comp, m->norm2, m->norm3,
+                         m->guide_cap, m->guide_fb, m->guide_fb + 1, m->cus, m->stream));
     return SDMM_OK;
 }
 
@@ -558,7 +589,11 @@ int sdmm_pdf_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], const
                    float* pdf) {
     if (!m || !c || !d || !pdf) return fail(SDMM_E_INVALID, "invalid argument");
     if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
-    HIP_TRY(launch_guide_pdf(m->gp, m->Kp, m->K, nq, c, d, pdf, m->norm2, m->norm3, m->stream));
+    if (nq <= 0) return SDMM_OK;
+    int r = ensure_guide_scratch(m, nq);
+    if (r) return r;
+    HIP_TRY(launch_guide(m->gp, m->Kp, m->K, nq, c, nullptr, d, nullptr, pdf, nullptr, m->norm2, m->norm3,
+                         m->guide_cap, m->guide_fb, m->guide_fb + 1, m->cus, m->stream));
     return SDMM_OK;
 }
 

@@ -54,6 +54,10 @@ def test_invalid_arguments_are_reported_not_raised(pkg):
     assert lib.sdmm_create(0, None, 0, C.byref(h)) == -1         # K out of range
     assert lib.sdmm_create(513, None, 0, C.byref(h)) == -1
     assert not h.value
+    # null handles are reported, never dereferenced
+    assert lib.sdmm_set_guide_capacity(None, 8) == -1
+    ci = C.c_int()
+    assert lib.sdmm_layout(None, C.byref(ci), None, None, None) == -1
 
 
 def test_python_binding_fails_loudly_without_library(pkg, tmp_path, monkeypatch):

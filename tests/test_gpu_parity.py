@@ -274,10 +274,15 @@ def _em_model(pkg, oracle, synth, K, N, iters):
     return b, mix, m
 
 
-@pytest.mark.parametrize("K,iters", [(16, 3), (128, 4), (256, 2)])
-def test_guide_indices_bit_exact(pkg, oracle, synth, gpu, K, iters):
+@pytest.mark.parametrize("K,iters,cap", [(16, 3, 40), (128, 4, 40), (128, 4, 4), (128, 4, 0),
+                                         (256, 2, 40)])
+def test_guide_indices_bit_exact(pkg, oracle, synth, gpu, K, iters, cap):
+    """Guided bounces vs the oracle.  cap: per-query candidate-list capacity;
+    4 sends most K=128 queries and 0 sends all of them down the full-K
+    fallback path, which must give the same bits."""
     import torch
     b, mix, om = _em_model(pkg, oracle, synth, K, 8192, iters)
+    mix.set_guide_capacity(cap)
     nq = 4096
     c, u = synth.sample_queries_near(b, nq // 2)
     c2, u2 = synth.queries(nq // 2)
@@ -298,10 +303,12 @@ def test_guide_indices_bit_exact(pkg, oracle, synth, gpu, K, iters):
     np.testing.assert_allclose(np.linalg.norm(dg[ok], axis=1), 1.0, atol=1e-5)
 
 
-def test_pdf_batch_matches_oracle(pkg, oracle, synth, gpu):
+@pytest.mark.parametrize("cap", [40, 0])
+def test_pdf_batch_matches_oracle(pkg, oracle, synth, gpu, cap):
     import torch
     K = 128
     b, mix, om = _em_model(pkg, oracle, synth, K, 8192, 3)
+    mix.set_guide_capacity(cap)
     c, u = synth.sample_queries_near(b, 2048)
     rng = np.random.default_rng(7)
     d = rng.normal(size=(3, 2048)).astype(np.float32)
