@@ -208,7 +208,7 @@ def main():
                    "parallelism": f"sample-sharded x{world}", "layout": "SoA fp32 in, [N][K] fp32 out"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK, "traffic": None,
-                     "kernel": "estep_resp_kernel<CPL=%d,LPS=%d>" % mix.layout()["resp"],
+                     "kernel": mix.kernel_name("resp"),
                      "bytes_per_launch": bytes_per_launch, "kernel_us": kern * 1e6,
                      "fp32_frac": flops_per_launch / kern / FP32_PEAK},
     }

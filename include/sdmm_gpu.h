@@ -86,6 +86,9 @@ int sdmm_num_components(const sdmm_mix* m);
 /* Diagnostics: E-step kernel layouts (components per lane, lanes per sample)
  * of the responsibility and statistics kernels.  Any pointer may be NULL. */
 int sdmm_layout(const sdmm_mix* m, int* resp_cpl, int* resp_lps, int* stats_cpl, int* stats_lps);
+/* Diagnostics: name of the kernel the handle launches for the responsibility
+ * (which = 0) or statistics (which = 1) E-step; "" for a NULL handle. */
+const char* sdmm_kernel_name(const sdmm_mix* m, int which);
 /* Guided queries keep a per-query list of at most `cap` candidate components
  * (default and maximum 40); queries that do not fit take the full-K path.
  * Results are identical for every cap; 0 sends every query down the full-K

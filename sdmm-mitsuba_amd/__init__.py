@@ -83,6 +83,8 @@ def lib():
         L.sdmm_create.argtypes = [C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
         L.sdmm_destroy.argtypes = [C.c_void_p]
         L.sdmm_layout.argtypes = [C.c_void_p] + [C.POINTER(C.c_int)] * 4
+        L.sdmm_kernel_name.argtypes = [C.c_void_p, C.c_int]
+        L.sdmm_kernel_name.restype = C.c_char_p
         L.sdmm_set_guide_capacity.argtypes = [C.c_void_p, C.c_int]
         L.sdmm_set_stream.argtypes = [C.c_void_p, C.c_void_p]
         L.sdmm_synchronize.argtypes = [C.c_void_p]
@@ -120,6 +122,7 @@ def stats_len(K: int) -> int:
 
 EXPORTED_SYMBOLS = [
     "sdmm_em_params_default", "sdmm_create", "sdmm_destroy", "sdmm_num_components", "sdmm_layout",
+    "sdmm_kernel_name",
     "sdmm_set_guide_capacity",
     "sdmm_set_stream", "sdmm_get_stream", "sdmm_synchronize", "sdmm_init_hemisphere",
     "sdmm_hemisphere_init_host", "sdmm_em_step", "sdmm_em_step_host", "sdmm_stats_len",
@@ -297,6 +300,10 @@ class SDMM:
         v = [C.c_int() for _ in range(4)]
         _check(lib().sdmm_layout(self.h, *[C.byref(x) for x in v]))
         return {"resp": (v[0].value, v[1].value), "stats": (v[2].value, v[3].value)}
+
+    def kernel_name(self, which: str = "resp") -> str:
+        """Name of the E-step kernel the handle launches ("resp" or "stats")."""
+        return lib().sdmm_kernel_name(self.h, 0 if which == "resp" else 1).decode()
 
     # ---- EM --------------------------------------------------------------
     def optimize(self, samples: DeviceSamples, iterations: int = 1):

@@ -312,6 +312,202 @@ estep_resp_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, int
 }
 
 // ---------------------------------------------------------------------------
+// Tiled responsibility E-step for 64 < K <= 128 (one packed component pair per
+// lane, the wave holds all K components).
+//
+// The per-sample overheads of estep_resp_kernel (sample broadcast, a full
+// wave reduction and the normalisation for every sample) are ~30 % of its
+// VALU issue.  Here:
+//   * the wave stages 64 samples in its own LDS slot (lane = sample, one
+//     coalesced load per plane, a block ahead) and every lane reads a sample
+//     with two broadcast ds_read_b128 (LDS pipe, no VALU);
+//   * samples are taken in tiles of kTile = 16: each lane keeps its 16
+//     unnormalised pairs q in registers and the 16 per-lane partial sums are
+//     reduced across the wave in ONE transposed butterfly (each step halves the
+//     values per lane), ~4 VALU per sample;
+//   * the lane that ends up holding sample t's sum normalises it and hands the
+//     scale back through LDS (one broadcast read per 4 samples);
+//   * the pair math is pair_pdf<false> with a degree-7 angle polynomial, the
+//     reference's rare angle cases folded into one select, and d == 0 handled
+//     once per sample in the normalisation.
+constexpr int kTile = 16;
+
+// theta/sin(theta) of two components, the reference's quirks included
+// (mvtn.h:157-164): with s2 = 1 - c^2,
+//   s2 >= 1e-6:  h(u) for c >= 0, pi/sqrt(s2) - h(u) for c < 0 (theta = pi -
+//                theta'), h a degree-7 fit (5.5e-7 relative on [0, 1/2],
+//                tools/fit_angle_over_sin.py);
+//   s2 <  1e-6:  1 (sin < 1e-3; also c > 1 by rounding, clamped to 1), or 0
+//                when c <= -1 (the log map fails: pdf = 0).
+// The last case is clamp(2^30 (c + 1)) -- one packed FMA with the clamp bit.
+__device__ __forceinline__ V angle_over_sin_fast(V c) {
+    const V s2 = vfma(-c, c, sp(1.0f));
+    const V u = V{fmaf(-0.5f, fabsf(c.x), 0.5f), fmaf(-0.5f, fabsf(c.y), 0.5f)};
+    V h = sp(3.3755881786346436f);
+    h = vfma(h, u, sp(-3.17423415184021f));
+    h = vfma(h, u, sp(2.1241207122802734f));
+    h = vfma(h, u, sp(-0.04515757039189339f));
+    h = vfma(h, u, sp(0.5178175568580627f));
+    h = vfma(h, u, sp(0.5294308066368103f));
+    h = vfma(h, u, sp(0.6667603850364685f));
+    h = vfma(h, u, sp(0.9999996423721313f));
+    const V fneg = vfma(sp(3.14159265358979f), vrsq(s2), -h);
+    V one;
+    const V big = sp(1073741824.0f);
+    asm("v_pk_fma_f32 %0, %1, %2, %2 clamp" : "=v"(one) : "v"(c), "s"(big));
+    const V f = V{c.x < 0.0f ? fneg.x : h.x, c.y < 0.0f ? fneg.y : h.y};
+    return V{s2.x < 1e-6f ? one.x : f.x, s2.y < 1e-6f ? one.y : f.y};
+}
+
+// pi_k pdf_k of a component pair (the folded form of pair_pdf<false>; d == 0
+// is handled per sample by the caller).
+__device__ __forceinline__ V pair_q_fast(const V* __restrict__ P, float p0, float p1, float p2, float d0,
+                                         float d1, float d2) {
+    const V tp0 = p0 - P[EP_MU0], tp1 = p1 - P[EP_MU1], tp2 = p2 - P[EP_MU2];
+    const V c = vfma(P[EP_R22], sp(d2), vfma(P[EP_R21], sp(d1), P[EP_R20] * d0));
+    const V a = angle_over_sin_fast(c);
+    const V u0 = P[EP_L00] * tp0;
+    const V u1 = vfma(P[EP_L11], tp1, P[EP_L10] * tp0);
+    const V u2 = vfma(P[EP_L22], tp2, vfma(P[EP_L21], tp1, P[EP_L20] * tp0));
+    const V s3 = vfma(P[EP_L32], tp2, vfma(P[EP_L31], tp1, P[EP_L30] * tp0));
+    const V s4 = vfma(P[EP_L42], tp2, vfma(P[EP_L41], tp1, P[EP_L40] * tp0));
+    const V ad = vfma(P[EP_A2], sp(d2), vfma(P[EP_A1], sp(d1), P[EP_A0] * d0));
+    const V bd = vfma(P[EP_B2], sp(d2), vfma(P[EP_B1], sp(d1), P[EP_B0] * d0));
+    const V u3 = vfma(a, ad, s3);
+    const V u4 = vfma(a, bd, s4);
+    const V q = vfma(u4, u4, vfma(u3, u3, vfma(u2, u2, vfma(u1, u1, u0 * u0))));
+    const V e = vexp2(vfma(q, sp(-0.72134752044448170368f), sp(kLog2Norm5)));
+    return e * (P[EP_DIPI] * a);
+}
+
+// lane ^ 4 within each row of 16 (row_shl:4 on banks 0 and 2, row_shr:4 on
+// banks 1 and 3: a disabled bank keeps the `old` operand)
+__device__ __forceinline__ float xor4(float x) {
+    const int xi = __builtin_bit_cast(int, x);
+    int t = __builtin_amdgcn_update_dpp(xi, xi, 0x104, 0xF, 0x5, false);
+    t = __builtin_amdgcn_update_dpp(t, xi, 0x114, 0xF, 0xA, false);
+    return __builtin_bit_cast(float, t);
+}
+
+// Transposed butterfly over the wave: v[16] per lane in, out: the wave-wide
+// sum of v[lane & 15] (every row of 16 lanes holds all 16 sums).  Step s
+// pairs lane L with L ^ 2^s; L keeps the half of its values whose index bit
+// equals its lane bit and receives the partner's copy of the same half.
+__device__ __forceinline__ float transpose_sum16(const float (&v)[kTile], int lane) {
+    const bool b0 = lane & 1, b1 = lane & 2, b2 = lane & 4, b3 = lane & 8;
+    float a[8], b[4], c[2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const float keep = b0 ? v[2 * i + 1] : v[2 * i];
+        const float send = b0 ? v[2 * i] : v[2 * i + 1];
+        a[i] = keep + dpp<0xB1>(send);   // quad_perm [1,0,3,2]: lane ^ 1
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float keep = b1 ? a[2 * i + 1] : a[2 * i];
+        const float send = b1 ? a[2 * i] : a[2 * i + 1];
+        b[i] = keep + dpp<0x4E>(send);   // quad_perm [2,3,0,1]: lane ^ 2
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const float keep = b2 ? b[2 * i + 1] : b[2 * i];
+        const float send = b2 ? b[2 * i] : b[2 * i + 1];
+        c[i] = keep + xor4(send);
+    }
+    const float keep = b3 ? c[1] : c[0];
+    const float send = b3 ? c[0] : c[1];
+    float x = keep + dpp<0x128>(send);  // row_ror:8: lane ^ 8
+    x += __shfl_xor(x, 16);
+    x += __shfl_xor(x, 32);
+    return x;
+}
+
+template <int WPB>
+__global__ void __launch_bounds__(64 * WPB, 4)
+estep_resp_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, int64_t n,
+                       int64_t chunk, float* __restrict__ resp) {
+    // per wave: the staged sample block (x0 x1 x2 x3 | x4 x5 hpdf diffuse) and
+    // the tile's normalisation scales
+    __shared__ float4 sblk[WPB][64][2];
+    __shared__ float sg[WPB][kTile];
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t wave = (int64_t)blockIdx.x * WPB + wid;
+    const int64_t s0 = wave * chunk;
+    if (s0 >= n) return;
+    const int64_t s1 = (s0 + chunk < n) ? s0 + chunk : n;
+
+    const int kbase = 2 * lane;
+    V P[EP_FIELDS];
+#pragma unroll
+    for (int f = 0; f < EP_FIELDS; ++f) P[f] = *(const V*)(ep + f * Kp + kbase);
+    const bool full = (kbase + 2 <= K);
+    const bool has_h = s.hpdf != nullptr, has_d = s.isDiffuse != nullptr;
+    float4 (*blk_lds)[2] = sblk[wid];
+    float* g_lds = sg[wid];
+
+    SampleBlock A = load_block(s, s0, s1, lane);
+    for (int64_t blk = s0; blk < s1; blk += 64) {
+        {
+            // stage the block (lane = sample); the flag byte comes out of its dword
+            const int64_t si = (blk + lane < s1) ? blk + lane : s1 - 1;
+            const int sh = 8 * (int)((uintptr_t)(s.isDiffuse + si) & 3);
+            const bool dif = has_d && ((A.diff >> sh) & 0xff) != 0;
+            blk_lds[lane][0] = float4{A.x0, A.x1, A.x2, A.x3};
+            blk_lds[lane][1] = float4{A.x4, A.x5, has_h ? A.h : 0.0f, dif ? 1.0f : 0.0f};
+        }
+        A = load_block(s, blk + 64, s1, lane);   // next block in flight (clamped past the end)
+        const int cnt = (s1 - blk < 64) ? (int)(s1 - blk) : 64;
+        for (int tb = 0; tb < cnt; tb += kTile) {
+            V q[kTile];
+#pragma unroll
+            for (int t = 0; t < kTile; ++t) {
+                const float4 a = blk_lds[tb + t][0];
+                const float4 b = blk_lds[tb + t][1];
+                q[t] = pair_q_fast(P, a.x, a.y, a.z, a.w, b.x, b.y);
+                // keep the scheduler from hoisting every sample's LDS reads
+                // (and their registers) to the top of the tile
+                if (t % 2 == 1) __builtin_amdgcn_sched_barrier(0);
+            }
+            float ps[kTile];
+#pragma unroll
+            for (int t = 0; t < kTile; ++t) ps[t] = q[t].x + q[t].y;
+            const float S = transpose_sum16(ps, lane);
+            // posterior normalisation of sample tb + (lane & 15) (mixture_model.h:170-191);
+            // d == 0 fails every log map (mvtn.h:152-154): all pdfs 0, 1/S' not finite
+            {
+                const int t = tb + (lane & 15);
+                const float4 a = blk_lds[t][0];
+                const float4 b = blk_lds[t][1];
+                const bool dzero = (a.w == 0.0f && b.x == 0.0f && b.y == 0.0f);
+                const bool dif = b.w != 0.0f;
+                const float S2 = dif ? fmaf(1.0f - kHeuristicWeight, S, kHeuristicWeight * b.z) : S;
+                const float inv = __builtin_amdgcn_rcpf(S2);
+                const bool fin = __builtin_isfinite(inv) && !dzero;
+                const float g = fin ? (dif ? inv * (1.0f - kHeuristicWeight) : inv) : 0.0f;
+                if (lane < kTile) g_lds[lane] = g;
+            }
+            // a non-finite sum means a non-finite q (NaN input): zero by select
+            const bool bad = __builtin_amdgcn_ballot_w64(!__builtin_isfinite(S)) != 0;
+            const int tcnt = (cnt - tb < kTile) ? cnt - tb : kTile;
+#pragma unroll
+            for (int t = 0; t < kTile; ++t) {
+                if (t >= tcnt) break;
+                const float g = g_lds[t];
+                V o = q[t] * g;
+                if (bad) o = (g != 0.0f) ? o : sp(0.0f);
+                float* row = resp + (blk + tb + t) * (int64_t)K + kbase;
+                if (full) {
+                    __builtin_nontemporal_store(o, (V*)row);
+                } else {
+                    if (kbase < K) __builtin_nontemporal_store(o.x, row);
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Fused E-step + sufficient statistics (calculateStats + sumWeights).
 // partial row layout: [f*Kp + k] for f < ST_FIELDS, then [21Kp] = H, [21Kp+1] = wsum.
 template <int CPL, int LPS>
@@ -549,6 +745,24 @@ hipError_t launch_estep_resp(int cpl, int lps, const float* ep, int Kp, int K, c
     SDMM_LAYOUTS(X)
 #undef X
     return hipErrorInvalidValue;
+}
+
+// Tiled responsibility kernel (64 < K <= 128, Kp == 128): chunk is a multiple
+// of 64 samples per wave.
+hipError_t launch_estep_resp_tile(const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
+                                  int64_t chunk, float* resp, hipStream_t st) {
+    if (Kp != 128 || K <= 64 || K > 128) return hipErrorInvalidValue;
+    constexpr int wpb = 4;
+    const int64_t waves = (n + chunk - 1) / chunk;
+    const int64_t blocks = (waves + wpb - 1) / wpb;
+    hipLaunchKernelGGL(estep_resp_tile_kernel<wpb>, dim3((unsigned)blocks), dim3(64 * wpb), 0, st, ep, Kp,
+                       K, s, n, chunk, resp);
+    return hipGetLastError();
+}
+
+hipError_t estep_resp_tile_occupancy(int* blocks_per_cu) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        blocks_per_cu, reinterpret_cast<const void*>(&estep_resp_tile_kernel<4>), 256, 0);
 }
 
 hipError_t launch_estep_stats(int cpl, int lps, const float* ep, int Kp, int K, const SamplesDev& s,

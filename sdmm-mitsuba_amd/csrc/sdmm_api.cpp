@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -25,6 +26,9 @@ hipError_t launch_estep_stats(int cpl, int lps, const float* ep, int Kp, int K, 
                               int64_t n, int64_t chunk, int blocks, int wpb, float* partials,
                               int pstride, hipStream_t st);
 hipError_t estep_occupancy(int cpl, int lps, int Kp, int* resp_blocks, int* stats_blocks);
+hipError_t launch_estep_resp_tile(const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
+                                  int64_t chunk, float* resp, hipStream_t st);
+hipError_t estep_resp_tile_occupancy(int* blocks_per_cu);
 hipError_t launch_reduce_partials(const float* partials, int rows, int pstride, const float* ep_for_finalize,
                                   int Kp, int K,
                                   double* stats, hipStream_t st);
@@ -170,6 +174,7 @@ void hemisphere_init(const float* positions, const float* normals, int nPosition
 struct sdmm_mix {
     int K = 0, Kp = 0, cpl = 1, lps = 64;   // statistics E-step layout
     int rcpl = 2, rlps = 64;                 // responsibility E-step layout (same Kp)
+    int rtile = 0;                           // 1: estep_resp_tile_kernel (64 < K <= 128)
     int device = 0;
     int cus = 256;
     int resp_blocks = 2, stats_blocks = 2;   // resident 256-thread WGs per CU
@@ -338,9 +343,19 @@ int sdmm_create(int K, const sdmm_em_params* params, int device, sdmm_mix** out)
     m->rcpl = cpl;
     m->rlps = lps;
     if (K > 64 && K <= 128) { m->rcpl = 4; m->rlps = 32; }
+    // 64 < K <= 128: the tiled kernel (one packed pair per lane, 16-sample
+    // tiles, transposed normaliser reduction); SDMM_RESP_KERNEL=legacy keeps
+    // estep_resp_kernel<4,32> (A/B measurements)
+    {
+        const char* ev = std::getenv("SDMM_RESP_KERNEL");
+        const bool legacy = ev && std::strcmp(ev, "legacy") == 0;
+        if (K > 64 && K <= 128 && !legacy) { m->rtile = 1; m->rcpl = 2; m->rlps = 64; }
+    }
     int unused = 0;
     if (estep_occupancy(m->rcpl, m->rlps, m->Kp, &m->resp_blocks, &unused) != hipSuccess ||
         estep_occupancy(m->cpl, m->lps, m->Kp, &unused, &m->stats_blocks) != hipSuccess)
+        return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
+    if (m->rtile && estep_resp_tile_occupancy(&m->resp_blocks) != hipSuccess)
         return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
     if (hipStreamCreateWithFlags(&m->own_stream, hipStreamNonBlocking) != hipSuccess)
         return cleanup(fail(SDMM_E_HIP, "hipStreamCreate failed"));
@@ -433,6 +448,18 @@ int sdmm_layout(const sdmm_mix* m, int* resp_cpl, int* resp_lps, int* stats_cpl,
     if (stats_cpl) *stats_cpl = m->cpl;
     if (stats_lps) *stats_lps = m->lps;
     return SDMM_OK;
+}
+
+const char* sdmm_kernel_name(const sdmm_mix* m, int which) {
+    if (!m) return "";
+    static thread_local char buf[64];
+    if (which == 0) {
+        if (m->rtile) return "estep_resp_tile_kernel<4>";
+        std::snprintf(buf, sizeof buf, "estep_resp_kernel<%d,%d>", m->rcpl, m->rlps);
+        return buf;
+    }
+    std::snprintf(buf, sizeof buf, "estep_stats_kernel<%d,%d>", m->cpl, m->lps);
+    return buf;
 }
 
 int sdmm_set_stream(sdmm_mix* m, void* hip_stream) {
@@ -567,6 +594,16 @@ int sdmm_responsibilities(sdmm_mix* m, const sdmm_samples* s, float* resp) {
     int r = check_samples(s);
     if (r) return r;
     if (s->n == 0) return SDMM_OK;
+    if (m->rtile) {
+        // chunks of whole 64-sample blocks; ~3 rounds of resident waves so the
+        // tail of the launch stays short
+        const int64_t resident = (int64_t)m->cus * 4 * (m->resp_blocks > 0 ? m->resp_blocks : 1);
+        int64_t chunk = (s->n + 3 * resident - 1) / (3 * resident);
+        chunk = ((chunk + 63) / 64) * 64;
+        if (chunk < 128) chunk = 128;
+        HIP_TRY(launch_estep_resp_tile(m->ep, m->Kp, m->K, to_dev(s), s->n, chunk, resp, m->stream));
+        return SDMM_OK;
+    }
     const Split sp = split_for(m, s->n, m->rlps, m->resp_blocks);
     HIP_TRY(launch_estep_resp(m->rcpl, m->rlps, m->ep, m->Kp, m->K, to_dev(s), s->n, sp.chunk, resp,
                               m->stream));

@@ -87,7 +87,8 @@ def test_init_params_match_oracle(pkg, oracle, synth, gpu, K):
     assert (p["valid"] == 1).all()
 
 
-@pytest.mark.parametrize("K,N", [(16, 4099), (32, 2048), (64, 3000), (128, 4096), (256, 1500), (512, 700)])
+@pytest.mark.parametrize("K,N", [(16, 4099), (32, 2048), (64, 3000), (128, 4096), (128, 1001), (72, 777),
+                                 (120, 2050), (256, 1500), (512, 700)])
 def test_responsibilities_match_oracle(pkg, oracle, synth, gpu, K, N):
     import torch
     b, mix, om, ost, ds, os_ = _setup(pkg, oracle, synth, K, N)
@@ -261,6 +262,45 @@ def test_zero_direction_samples(pkg, oracle, synth, gpu):
     ref = oracle.responsibilities(om, oracle.Samples(xs, b["w"]))
     _check_resp(got, ref, mix.get_params(), xs)
     assert (got[::7] == 0).all()
+
+
+@pytest.mark.parametrize("K", [128, 72])
+def test_rare_angle_cases(pkg, oracle, synth, gpu, K):
+    """Directions at the reference's angle quirks (mvtn.h:157-164): exactly on
+    a component's mean direction (sin < 1e-3 -> J = 1), exactly antipodal
+    (cos <= -1: the log map fails, pdf 0) and within 1e-3 rad of antipodal
+    (sin < 1e-3 with cos < 0: J = 1 again), plus NaN samples (posterior all
+    zero) -- against the oracle, on the tiled kernel's exact fast path."""
+    import torch
+    N = 999
+    b, mix, om, ost, ds, os_ = _setup(pkg, oracle, synth, K, N)
+    x = b["x"].copy()
+    mu = mix.get_params()["mean"][:, 3:6].astype(np.float64)
+    rng = np.random.default_rng(7)
+    for i in range(0, N, 5):
+        k = rng.integers(K)
+        d = mu[k] / np.linalg.norm(mu[k])
+        mode = (i // 5) % 4
+        if mode == 1:
+            d = -d
+        elif mode == 2:
+            t = np.cross(d, [0.0, 0.0, 1.0] if abs(d[2]) < 0.9 else [1.0, 0.0, 0.0])
+            t /= np.linalg.norm(t)
+            d = -np.cos(4e-4) * d + np.sin(4e-4) * t
+        elif mode == 3:
+            d = mu[k]                      # the stored float mean itself
+        x[3:6, i] = d.astype(np.float32)
+    x[:, 1::97] = np.nan
+    xt = [torch.from_numpy(x[i].copy()).to(gpu) for i in range(6)]
+    d2 = pkg.DeviceSamples(xt, ds.w)
+    resp = torch.empty((N, K), device=gpu)
+    mix.posterior(d2, resp)
+    got = resp.cpu().numpy()
+    ref = oracle.responsibilities(om, oracle.Samples(x, b["w"]))
+    assert (got[1::97] == 0).all() and (ref[1::97] == 0).all()
+    keep = np.ones(N, bool)
+    keep[1::97] = False
+    _check_resp(got[keep], ref[keep], mix.get_params(), x[:, keep])
 
 
 def _em_model(pkg, oracle, synth, K, N, iters):
