@@ -422,8 +422,8 @@ __device__ __forceinline__ float transpose_sum16(const float (&v)[kTile], int la
     return x;
 }
 
-template <int WPB>
-__global__ void __launch_bounds__(64 * WPB, 4)
+template <int WPB, int SB>
+__global__ void __launch_bounds__(64 * WPB, (SB <= 2 ? 4 : 3))
 estep_resp_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, int64_t n,
                        int64_t chunk, float* __restrict__ resp) {
     // per wave: the staged sample block (x0 x1 x2 x3 | x4 x5 hpdf diffuse) and
@@ -467,7 +467,7 @@ estep_resp_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s
                 q[t] = pair_q_fast(P, a.x, a.y, a.z, a.w, b.x, b.y);
                 // keep the scheduler from hoisting every sample's LDS reads
                 // (and their registers) to the top of the tile
-                if (t % 2 == 1) __builtin_amdgcn_sched_barrier(0);
+                if (t % SB == SB - 1) __builtin_amdgcn_sched_barrier(0);
             }
             float ps[kTile];
 #pragma unroll
@@ -749,20 +749,26 @@ hipError_t launch_estep_resp(int cpl, int lps, const float* ep, int Kp, int K, c
 
 // Tiled responsibility kernel (64 < K <= 128, Kp == 128): chunk is a multiple
 // of 64 samples per wave.
-hipError_t launch_estep_resp_tile(const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
+hipError_t launch_estep_resp_tile(int variant, const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
                                   int64_t chunk, float* resp, hipStream_t st) {
     if (Kp != 128 || K <= 64 || K > 128) return hipErrorInvalidValue;
     constexpr int wpb = 4;
     const int64_t waves = (n + chunk - 1) / chunk;
     const int64_t blocks = (waves + wpb - 1) / wpb;
-    hipLaunchKernelGGL(estep_resp_tile_kernel<wpb>, dim3((unsigned)blocks), dim3(64 * wpb), 0, st, ep, Kp,
-                       K, s, n, chunk, resp);
+#define L(SB) hipLaunchKernelGGL((estep_resp_tile_kernel<wpb, SB>), dim3((unsigned)blocks), dim3(64 * wpb), 0, \
+                                 st, ep, Kp, K, s, n, chunk, resp)
+    if (variant == 1) L(4);
+    else if (variant == 2) L(16);
+    else L(2);
+#undef L
     return hipGetLastError();
 }
 
-hipError_t estep_resp_tile_occupancy(int* blocks_per_cu) {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        blocks_per_cu, reinterpret_cast<const void*>(&estep_resp_tile_kernel<4>), 256, 0);
+hipError_t estep_resp_tile_occupancy(int variant, int* blocks_per_cu) {
+    const void* f = variant == 1 ? reinterpret_cast<const void*>(&estep_resp_tile_kernel<4, 4>)
+                  : variant == 2 ? reinterpret_cast<const void*>(&estep_resp_tile_kernel<4, 16>)
+                                 : reinterpret_cast<const void*>(&estep_resp_tile_kernel<4, 2>);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, 256, 0);
 }
 
 hipError_t launch_estep_stats(int cpl, int lps, const float* ep, int Kp, int K, const SamplesDev& s,

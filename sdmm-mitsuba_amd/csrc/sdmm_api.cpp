@@ -26,9 +26,9 @@ hipError_t launch_estep_stats(int cpl, int lps, const float* ep, int Kp, int K, 
                               int64_t n, int64_t chunk, int blocks, int wpb, float* partials,
                               int pstride, hipStream_t st);
 hipError_t estep_occupancy(int cpl, int lps, int Kp, int* resp_blocks, int* stats_blocks);
-hipError_t launch_estep_resp_tile(const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
+hipError_t launch_estep_resp_tile(int variant, const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
                                   int64_t chunk, float* resp, hipStream_t st);
-hipError_t estep_resp_tile_occupancy(int* blocks_per_cu);
+hipError_t estep_resp_tile_occupancy(int variant, int* blocks_per_cu);
 hipError_t launch_reduce_partials(const float* partials, int rows, int pstride, const float* ep_for_finalize,
                                   int Kp, int K,
                                   double* stats, hipStream_t st);
@@ -175,6 +175,7 @@ struct sdmm_mix {
     int K = 0, Kp = 0, cpl = 1, lps = 64;   // statistics E-step layout
     int rcpl = 2, rlps = 64;                 // responsibility E-step layout (same Kp)
     int rtile = 0;                           // 1: estep_resp_tile_kernel (64 < K <= 128)
+    int rvariant = 0;                        // tile kernel scheduling variant (SDMM_RESP_VARIANT)
     int device = 0;
     int cus = 256;
     int resp_blocks = 2, stats_blocks = 2;   // resident 256-thread WGs per CU
@@ -350,12 +351,14 @@ int sdmm_create(int K, const sdmm_em_params* params, int device, sdmm_mix** out)
         const char* ev = std::getenv("SDMM_RESP_KERNEL");
         const bool legacy = ev && std::strcmp(ev, "legacy") == 0;
         if (K > 64 && K <= 128 && !legacy) { m->rtile = 1; m->rcpl = 2; m->rlps = 64; }
+        const char* vv = std::getenv("SDMM_RESP_VARIANT");
+        if (vv) m->rvariant = std::atoi(vv);
     }
     int unused = 0;
     if (estep_occupancy(m->rcpl, m->rlps, m->Kp, &m->resp_blocks, &unused) != hipSuccess ||
         estep_occupancy(m->cpl, m->lps, m->Kp, &unused, &m->stats_blocks) != hipSuccess)
         return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
-    if (m->rtile && estep_resp_tile_occupancy(&m->resp_blocks) != hipSuccess)
+    if (m->rtile && estep_resp_tile_occupancy(m->rvariant, &m->resp_blocks) != hipSuccess)
         return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
     if (hipStreamCreateWithFlags(&m->own_stream, hipStreamNonBlocking) != hipSuccess)
         return cleanup(fail(SDMM_E_HIP, "hipStreamCreate failed"));
@@ -454,7 +457,10 @@ const char* sdmm_kernel_name(const sdmm_mix* m, int which) {
     if (!m) return "";
     static thread_local char buf[64];
     if (which == 0) {
-        if (m->rtile) return "estep_resp_tile_kernel<4>";
+        if (m->rtile) {
+            std::snprintf(buf, sizeof buf, "estep_resp_tile_kernel<4,%d>", m->rvariant == 1 ? 4 : m->rvariant == 2 ? 16 : 2);
+            return buf;
+        }
         std::snprintf(buf, sizeof buf, "estep_resp_kernel<%d,%d>", m->rcpl, m->rlps);
         return buf;
     }
@@ -601,7 +607,7 @@ int sdmm_responsibilities(sdmm_mix* m, const sdmm_samples* s, float* resp) {
         int64_t chunk = (s->n + 3 * resident - 1) / (3 * resident);
         chunk = ((chunk + 63) / 64) * 64;
         if (chunk < 128) chunk = 128;
-        HIP_TRY(launch_estep_resp_tile(m->ep, m->Kp, m->K, to_dev(s), s->n, chunk, resp, m->stream));
+        HIP_TRY(launch_estep_resp_tile(m->rvariant, m->ep, m->Kp, m->K, to_dev(s), s->n, chunk, resp, m->stream));
         return SDMM_OK;
     }
     const Split sp = split_for(m, s->n, m->rlps, m->resp_blocks);
