@@ -642,6 +642,201 @@ estep_stats_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, in
 }
 
 // ---------------------------------------------------------------------------
+// Tiled fused E-step + statistics for 64 < K <= 128 (one packed pair per
+// lane), the estep_resp_tile_kernel scheme applied to calculateStats
+// (stepwise_tangent.h:270-353): tiles of kStatTile = 4 samples keep q and the
+// directional tangent (ta, tb) of the lane's pair in registers, the
+// normaliser comes from a transposed butterfly, and the lane holding sample t
+// publishes {gamma scale, weight, threshold} through LDS for the accumulation.
+
+constexpr int kStatTile = 4;
+
+// pi_k pdf_k and the directional tangent (mvtn.h:146-177 with the quirks of
+// angle_over_sin_fast: a = 0 when the log map fails, so ta = tb = 0 then).
+__device__ __forceinline__ V pair_qt_fast(const V* __restrict__ P, float p0, float p1, float p2, float d0,
+                                          float d1, float d2, V& ta, V& tb) {
+    const V tp0 = p0 - P[EP_MU0], tp1 = p1 - P[EP_MU1], tp2 = p2 - P[EP_MU2];
+    const V c = vfma(P[EP_R22], sp(d2), vfma(P[EP_R21], sp(d1), P[EP_R20] * d0));
+    const V a = angle_over_sin_fast(c);
+    const V r0 = vfma(P[EP_R02], sp(d2), vfma(P[EP_R01], sp(d1), P[EP_R00] * d0));
+    const V r1 = vfma(P[EP_R12], sp(d2), vfma(P[EP_R11], sp(d1), P[EP_R10] * d0));
+    ta = r0 * a;
+    tb = r1 * a;
+    const V u0 = P[EP_L00] * tp0;
+    const V u1 = vfma(P[EP_L11], tp1, P[EP_L10] * tp0);
+    const V u2 = vfma(P[EP_L22], tp2, vfma(P[EP_L21], tp1, P[EP_L20] * tp0));
+    const V s3 = vfma(P[EP_L32], tp2, vfma(P[EP_L31], tp1, P[EP_L30] * tp0));
+    const V s4 = vfma(P[EP_L42], tp2, vfma(P[EP_L41], tp1, P[EP_L40] * tp0));
+    const V u3 = vfma(P[EP_L33], ta, s3);
+    const V u4 = vfma(P[EP_L44], tb, vfma(P[EP_L43], ta, s4));
+    const V q = vfma(u4, u4, vfma(u3, u3, vfma(u2, u2, vfma(u1, u1, u0 * u0))));
+    const V e = vexp2(vfma(q, sp(-0.72134752044448170368f), sp(kLog2Norm5)));
+    return e * (P[EP_DIPI] * a);
+}
+
+// Transposed butterfly for 4 values: out = wave-wide sum of v[lane & 3].
+__device__ __forceinline__ float transpose_sum4(const float (&v)[kStatTile], int lane) {
+    const bool b0 = lane & 1, b1 = lane & 2;
+    float a[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const float keep = b0 ? v[2 * i + 1] : v[2 * i];
+        const float send = b0 ? v[2 * i] : v[2 * i + 1];
+        a[i] = keep + dpp<0xB1>(send);
+    }
+    const float keep = b1 ? a[1] : a[0];
+    const float send = b1 ? a[0] : a[1];
+    float x = keep + dpp<0x4E>(send);
+    x += xor4(x);
+    x += dpp<0x128>(x);   // lane ^ 8
+    x += __shfl_xor(x, 16);
+    x += __shfl_xor(x, 32);
+    return x;
+}
+
+template <int WPB, int OCC>
+__global__ void __launch_bounds__(64 * WPB, OCC)
+estep_stats_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, int64_t n,
+                        int64_t chunk, float* __restrict__ partials, int pstride) {
+    __shared__ float4 sblk[WPB][64][2];      // x0 x1 x2 x3 | x4 x5 hpdf diffuse
+    __shared__ float sw[WPB][64];            // weight
+    __shared__ float4 sg[WPB][kStatTile];    // {gamma scale, weight, threshold, -}
+    extern __shared__ __attribute__((aligned(16))) float red[];
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t wave = (int64_t)blockIdx.x * WPB + wid;
+    const int64_t s0 = wave * chunk;
+    const int64_t s1 = (s0 + chunk < n) ? s0 + chunk : n;   // s1 <= s0: no samples
+
+    const int kbase = 2 * lane;
+    V P[EP_FIELDS];
+#pragma unroll
+    for (int f = 0; f < EP_FIELDS; ++f) P[f] = *(const V*)(ep + f * Kp + kbase);
+    V acc[ST_FIELDS];
+#pragma unroll
+    for (int f = 0; f < ST_FIELDS; ++f) acc[f] = sp(0.0f);
+    float accH = 0.0f, accWs = 0.0f;   // lanes < kStatTile: their samples' H and sumWeights terms
+    const bool has_h = s.hpdf != nullptr, has_d = s.isDiffuse != nullptr;
+    float4 (*blk_lds)[2] = sblk[wid];
+    float* w_lds = sw[wid];
+    float4* g_lds = sg[wid];
+
+    if (s0 < s1) {
+        SampleBlock A = load_block(s, s0, s1, lane);
+        for (int64_t blk = s0; blk < s1; blk += 64) {
+            {
+                const int64_t si = (blk + lane < s1) ? blk + lane : s1 - 1;
+                const int sh = 8 * (int)((uintptr_t)(s.isDiffuse + si) & 3);
+                const bool dif = has_d && ((A.diff >> sh) & 0xff) != 0;
+                blk_lds[lane][0] = float4{A.x0, A.x1, A.x2, A.x3};
+                blk_lds[lane][1] = float4{A.x4, A.x5, has_h ? A.h : 0.0f, dif ? 1.0f : 0.0f};
+                w_lds[lane] = A.w;
+            }
+            A = load_block(s, blk + 64, s1, lane);
+            const int cnt = (s1 - blk < 64) ? (int)(s1 - blk) : 64;
+            for (int tb = 0; tb < cnt; tb += kStatTile) {
+                V q[kStatTile], ta[kStatTile], tb2[kStatTile];
+#pragma unroll
+                for (int t = 0; t < kStatTile; ++t) {
+                    const float4 a = blk_lds[tb + t][0];
+                    const float4 b = blk_lds[tb + t][1];
+                    q[t] = pair_qt_fast(P, a.x, a.y, a.z, a.w, b.x, b.y, ta[t], tb2[t]);
+                }
+                float ps[kStatTile];
+#pragma unroll
+                for (int t = 0; t < kStatTile; ++t) ps[t] = q[t].x + q[t].y;
+                const float S = transpose_sum4(ps, lane);
+                {
+                    // posteriorAndLog normalisation (mixture_model.h:170-191) and the
+                    // weight guards of calculateStats / sumWeights (:288-293, :462-475)
+                    // for sample tb + (lane & 3); d == 0: every pdf is 0 (mvtn.h:152-154)
+                    const int t = tb + (lane & 3);
+                    const bool in = t < cnt;
+                    const float4 a = blk_lds[t][0];
+                    const float4 b = blk_lds[t][1];
+                    const float w = w_lds[t];
+                    const bool dzero = (a.w == 0.0f && b.x == 0.0f && b.y == 0.0f);
+                    const bool dif = b.w != 0.0f;
+                    const float Se = dzero ? 0.0f : S;
+                    const float S2 = dif ? fmaf(1.0f - kHeuristicWeight, Se, kHeuristicWeight * b.z) : Se;
+                    const float inv = __builtin_amdgcn_rcpf(S2);
+                    const bool fin = __builtin_isfinite(inv);
+                    const bool finite_w = __builtin_isfinite(w);
+                    const bool use = in && finite_w && w != 0.0f;
+                    const float g = (fin && !dzero) ? (dif ? inv * (1.0f - kHeuristicWeight) : inv) : 0.0f;
+                    const float hpost = (fin && dif) ? kHeuristicWeight * b.z * inv : 0.0f;
+                    const float weff = use ? w : 0.0f;
+                    if (lane < kStatTile) {
+                        accWs += (in && finite_w) ? w : 0.0f;
+                        accH = fmaf(weff, hpost, accH);
+                        // gamma < 1e-10 is skipped (:312); nothing passes when 1/S' is
+                        // not finite (posterior zeroed, mixture_model.h:182-191)
+                        g_lds[lane] = float4{g, weff, (fin && !dzero) ? 1e-10f : __builtin_inff(), 0.0f};
+                    }
+                }
+#pragma unroll
+                for (int t = 0; t < kStatTile; ++t) {
+                    const float4 gw = g_lds[t];
+                    const float4 a = blk_lds[tb + t][0];
+                    const V gam = q[t] * gw.x;
+                    const V v = V{gam.x >= gw.z ? gam.x : 0.0f, gam.y >= gw.z ? gam.y : 0.0f} * gw.y;
+                    const V tp0 = a.x - P[EP_MU0];
+                    const V tp1 = a.y - P[EP_MU1];
+                    const V tp2 = a.z - P[EP_MU2];
+                    acc[ST_W] += v;
+                    const V v0 = v * tp0, v1 = v * tp1, v2 = v * tp2;
+                    acc[ST_M0] += v0;
+                    acc[ST_M1] += v1;
+                    acc[ST_M2] += v2;
+                    const V v3 = v * ta[t], v4 = v * tb2[t];
+                    acc[ST_M3] += v3;
+                    acc[ST_M4] += v4;
+                    acc[ST_C00] = vfma(v0, tp0, acc[ST_C00]);
+                    acc[ST_C10] = vfma(v1, tp0, acc[ST_C10]);
+                    acc[ST_C11] = vfma(v1, tp1, acc[ST_C11]);
+                    acc[ST_C20] = vfma(v2, tp0, acc[ST_C20]);
+                    acc[ST_C21] = vfma(v2, tp1, acc[ST_C21]);
+                    acc[ST_C22] = vfma(v2, tp2, acc[ST_C22]);
+                    acc[ST_C30] = vfma(v3, tp0, acc[ST_C30]);
+                    acc[ST_C31] = vfma(v3, tp1, acc[ST_C31]);
+                    acc[ST_C32] = vfma(v3, tp2, acc[ST_C32]);
+                    acc[ST_C33] = vfma(v3, ta[t], acc[ST_C33]);
+                    acc[ST_C40] = vfma(v4, tp0, acc[ST_C40]);
+                    acc[ST_C41] = vfma(v4, tp1, acc[ST_C41]);
+                    acc[ST_C42] = vfma(v4, tp2, acc[ST_C42]);
+                    acc[ST_C43] = vfma(v4, ta[t], acc[ST_C43]);
+                    acc[ST_C44] = vfma(v4, tb2[t], acc[ST_C44]);
+                }
+            }
+        }
+    }
+    // H and sumWeights live in lanes 0..3: sum them over the wave
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        accH += __shfl_xor(accH, off);
+        accWs += __shfl_xor(accWs, off);
+    }
+    // fold the workgroup's waves in a fixed order through LDS
+    const int rowlen = ST_FIELDS * Kp + 2;
+    for (int w = 0; w < WPB; ++w) {
+        if (wid == w) {
+#pragma unroll
+            for (int f = 0; f < ST_FIELDS; ++f) {
+                V* dst = (V*)&red[f * Kp + kbase];
+                *dst = (w == 0) ? acc[f] : *dst + acc[f];
+            }
+            if (lane == 0) {
+                red[ST_FIELDS * Kp] = (w == 0) ? accH : red[ST_FIELDS * Kp] + accH;
+                red[ST_FIELDS * Kp + 1] = (w == 0) ? accWs : red[ST_FIELDS * Kp + 1] + accWs;
+            }
+        }
+        __syncthreads();
+    }
+    float* out = partials + (int64_t)blockIdx.x * pstride;
+    for (int idx = threadIdx.x; idx < rowlen; idx += blockDim.x) out[idx] = red[idx];
+}
+
+// ---------------------------------------------------------------------------
 // Deterministic fp64 reduction of the partial rows into the compact stats
 // vector [H, wsum, W(K), M(5K), Clow(15K)].  One workgroup per 64 output
 // columns; its 16 waves split the rows, then combine in a fixed order.
@@ -769,6 +964,28 @@ hipError_t estep_resp_tile_occupancy(int variant, int* blocks_per_cu) {
                   : variant == 2 ? reinterpret_cast<const void*>(&estep_resp_tile_kernel<4, 16>)
                                  : reinterpret_cast<const void*>(&estep_resp_tile_kernel<4, 2>);
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, 256, 0);
+}
+
+// Tiled statistics kernel (64 < K <= 128, Kp == 128): `blocks` workgroups of 4
+// waves, chunk a multiple of 64 samples per wave; one partial row per block.
+hipError_t launch_estep_stats_tile(int variant, const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
+                                   int64_t chunk, int blocks, float* partials, int pstride, hipStream_t st) {
+    if (Kp != 128 || K <= 64 || K > 128) return hipErrorInvalidValue;
+    const size_t lds = sizeof(float) * (size_t)(ST_FIELDS * Kp + 2);
+    if (variant == 1)
+        hipLaunchKernelGGL((estep_stats_tile_kernel<4, 3>), dim3(blocks), dim3(256), lds, st, ep, Kp, K, s, n,
+                           chunk, partials, pstride);
+    else
+        hipLaunchKernelGGL((estep_stats_tile_kernel<4, 2>), dim3(blocks), dim3(256), lds, st, ep, Kp, K, s, n,
+                           chunk, partials, pstride);
+    return hipGetLastError();
+}
+
+hipError_t estep_stats_tile_occupancy(int variant, int Kp, int* blocks_per_cu) {
+    const size_t lds = sizeof(float) * (size_t)(ST_FIELDS * Kp + 2);
+    const void* f = variant == 1 ? reinterpret_cast<const void*>(&estep_stats_tile_kernel<4, 3>)
+                                 : reinterpret_cast<const void*>(&estep_stats_tile_kernel<4, 2>);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, 256, lds);
 }
 
 hipError_t launch_estep_stats(int cpl, int lps, const float* ep, int Kp, int K, const SamplesDev& s,

@@ -29,6 +29,9 @@ hipError_t estep_occupancy(int cpl, int lps, int Kp, int* resp_blocks, int* stat
 hipError_t launch_estep_resp_tile(int variant, const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
                                   int64_t chunk, float* resp, hipStream_t st);
 hipError_t estep_resp_tile_occupancy(int variant, int* blocks_per_cu);
+hipError_t launch_estep_stats_tile(int variant, const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
+                                   int64_t chunk, int blocks, float* partials, int pstride, hipStream_t st);
+hipError_t estep_stats_tile_occupancy(int variant, int Kp, int* blocks_per_cu);
 hipError_t launch_reduce_partials(const float* partials, int rows, int pstride, const float* ep_for_finalize,
                                   int Kp, int K,
                                   double* stats, hipStream_t st);
@@ -176,6 +179,8 @@ struct sdmm_mix {
     int rcpl = 2, rlps = 64;                 // responsibility E-step layout (same Kp)
     int rtile = 0;                           // 1: estep_resp_tile_kernel (64 < K <= 128)
     int rvariant = 0;                        // tile kernel scheduling variant (SDMM_RESP_VARIANT)
+    int stile = 0;                           // 1: estep_stats_tile_kernel (64 < K <= 128)
+    int svariant = 0;                        // its occupancy variant (SDMM_STATS_VARIANT)
     int device = 0;
     int cus = 256;
     int resp_blocks = 2, stats_blocks = 2;   // resident 256-thread WGs per CU
@@ -286,10 +291,26 @@ int ensure_guide_scratch(const sdmm_mix* m, int64_t nq) {
 }
 
 int run_estep_stats(sdmm_mix* m, const sdmm_samples* s, double* stats_out) {
+    SamplesDev d = to_dev(s);
+    if (m->stile) {
+        // one round of resident waves, each a whole number of 64-sample blocks
+        const int64_t resident = (int64_t)m->cus * 4 * (m->stats_blocks > 0 ? m->stats_blocks : 1);
+        int64_t chunk = (s->n + resident - 1) / resident;
+        chunk = ((chunk + 63) / 64) * 64;
+        if (chunk < 64) chunk = 64;
+        const int64_t waves = (s->n + chunk - 1) / chunk;
+        const int blocks = (int)((waves + 3) / 4 > 0 ? (waves + 3) / 4 : 1);
+        int r = ensure_partials(m, blocks);
+        if (r) return r;
+        HIP_TRY(launch_estep_stats_tile(m->svariant, m->ep, m->Kp, m->K, d, s->n, chunk, blocks, m->partials,
+                                        m->pstride, m->stream));
+        HIP_TRY(launch_reduce_partials(m->partials, blocks, m->pstride, m->ep, m->Kp, m->K, stats_out,
+                                       m->stream));
+        return SDMM_OK;
+    }
     const Split sp = split_for(m, s->n, m->lps, m->stats_blocks);
     int r = ensure_partials(m, sp.blocks);
     if (r) return r;
-    SamplesDev d = to_dev(s);
     HIP_TRY(launch_estep_stats(m->cpl, m->lps, m->ep, m->Kp, m->K, d, s->n, sp.chunk, sp.blocks, sp.wpb,
                                m->partials, m->pstride, m->stream));
     HIP_TRY(launch_reduce_partials(m->partials, sp.blocks, m->pstride, m->ep, m->Kp, m->K, stats_out,
@@ -353,12 +374,18 @@ int sdmm_create(int K, const sdmm_em_params* params, int device, sdmm_mix** out)
         if (K > 64 && K <= 128 && !legacy) { m->rtile = 1; m->rcpl = 2; m->rlps = 64; }
         const char* vv = std::getenv("SDMM_RESP_VARIANT");
         if (vv) m->rvariant = std::atoi(vv);
+        const char* sv = std::getenv("SDMM_STATS_KERNEL");
+        if (K > 64 && K <= 128 && !(sv && std::strcmp(sv, "legacy") == 0)) m->stile = 1;
+        const char* svv = std::getenv("SDMM_STATS_VARIANT");
+        if (svv) m->svariant = std::atoi(svv);
     }
     int unused = 0;
     if (estep_occupancy(m->rcpl, m->rlps, m->Kp, &m->resp_blocks, &unused) != hipSuccess ||
         estep_occupancy(m->cpl, m->lps, m->Kp, &unused, &m->stats_blocks) != hipSuccess)
         return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
     if (m->rtile && estep_resp_tile_occupancy(m->rvariant, &m->resp_blocks) != hipSuccess)
+        return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
+    if (m->stile && estep_stats_tile_occupancy(m->svariant, m->Kp, &m->stats_blocks) != hipSuccess)
         return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
     if (hipStreamCreateWithFlags(&m->own_stream, hipStreamNonBlocking) != hipSuccess)
         return cleanup(fail(SDMM_E_HIP, "hipStreamCreate failed"));
@@ -464,7 +491,10 @@ const char* sdmm_kernel_name(const sdmm_mix* m, int which) {
         std::snprintf(buf, sizeof buf, "estep_resp_kernel<%d,%d>", m->rcpl, m->rlps);
         return buf;
     }
-    std::snprintf(buf, sizeof buf, "estep_stats_kernel<%d,%d>", m->cpl, m->lps);
+    if (m->stile)
+        std::snprintf(buf, sizeof buf, "estep_stats_tile_kernel<4,%d>", m->svariant == 1 ? 3 : 2);
+    else
+        std::snprintf(buf, sizeof buf, "estep_stats_kernel<%d,%d>", m->cpl, m->lps);
     return buf;
 }
 
