@@ -838,73 +838,82 @@ estep_stats_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
 
 // ---------------------------------------------------------------------------
 // Deterministic fp64 reduction of the partial rows into the compact stats
-// vector [H, wsum, W(K), M(5K), Clow(15K)].  One workgroup per 64 output
-// columns; its 16 waves split the rows, then combine in a fixed order.
-__global__ void __launch_bounds__(1024)
-reduce_partials_kernel(const float* __restrict__ partials, int rows, int pstride, int Kp, int K,
-                       double* __restrict__ stats) {
-    __shared__ double buf[16][64];
+// vector [H, wsum, W(K), M(5K), Clow(15K)], in two launches so the whole chip
+// takes part: stage 1 = (64-column block) x (row slice) workgroups, each
+// summing its slice in a fixed order into slice[s][col]; stage 2 (inside
+// finalize_stats_kernel) sums the kReduceSlices slices of each column in order.
+constexpr int kReduceSlices = 16;
+
+__device__ __forceinline__ int partial_col(int o, int Kp, int K) {
+    if (o == 0) return ST_FIELDS * Kp;
+    if (o == 1) return ST_FIELDS * Kp + 1;
+    const int r = o - 2;
+    if (r < K) return ST_W * Kp + r;
+    if (r < 6 * K) { const int q = r - K; return (ST_M0 + q % 5) * Kp + q / 5; }
+    const int q = r - 6 * K;
+    return (ST_C00 + q % 15) * Kp + q / 15;
+}
+
+__global__ void __launch_bounds__(256)
+reduce_partials_slices_kernel(const float* __restrict__ partials, int rows, int pstride, int Kp, int K,
+                              double* __restrict__ slices) {
+    __shared__ double buf[4][64];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const int ncols = 2 + ST_FIELDS * K;
     const int o = blockIdx.x * 64 + lane;
-    int col = -1;
-    if (o < ncols) {
-        if (o == 0) col = ST_FIELDS * Kp;
-        else if (o == 1) col = ST_FIELDS * Kp + 1;
-        else {
-            const int r = o - 2;
-            if (r < K) col = ST_W * Kp + r;
-            else if (r < 6 * K) { const int q = r - K; col = (ST_M0 + q % 5) * Kp + q / 5; }
-            else { const int q = r - 6 * K; col = (ST_C00 + q % 15) * Kp + q / 15; }
-        }
-    }
+    const int sl = blockIdx.y;
+    const int r0 = (int)((int64_t)rows * sl / kReduceSlices);
+    const int r1 = (int)((int64_t)rows * (sl + 1) / kReduceSlices);
     double sum = 0.0;
-    if (col >= 0) {
-        int r = wid;
-        for (; r + 48 < rows; r += 64) {
-            const float a = partials[(int64_t)r * pstride + col];
-            const float b = partials[(int64_t)(r + 16) * pstride + col];
-            const float c = partials[(int64_t)(r + 32) * pstride + col];
-            const float d = partials[(int64_t)(r + 48) * pstride + col];
-            sum += (double)a; sum += (double)b; sum += (double)c; sum += (double)d;
-        }
-        for (; r < rows; r += 16) sum += (double)partials[(int64_t)r * pstride + col];
+    if (o < ncols) {
+        const int col = partial_col(o, Kp, K);
+        for (int r = r0 + wid; r < r1; r += 4) sum += (double)partials[(int64_t)r * pstride + col];
     }
     buf[wid][lane] = sum;
     __syncthreads();
-    if (wid == 0 && o < ncols) {
-        double t = 0.0;
-        for (int w = 0; w < 16; ++w) t += buf[w][lane];
-        stats[o] = t;
-    }
+    if (wid == 0 && o < ncols)
+        slices[(int64_t)sl * ncols + o] = ((buf[0][lane] + buf[1][lane]) + buf[2][lane]) + buf[3][lane];
 }
 
-// Un-centre the spatial statistics of component k (fp64, in place):
+
+// Sum the row slices of component k's columns, then un-centre its spatial
+// statistics (fp64):
 //   M_p = M'_p + W mu,  C_pp = C'_pp + M'_p mu^T + mu M'_p^T + W mu mu^T,
 //   C_tp = C'_tp + M_t mu^T   (mu = the float mean the E-step subtracted).
 __global__ void finalize_stats_kernel(const float* __restrict__ ep, int Kp, int K,
-                                      double* __restrict__ stats) {
+                                      const double* __restrict__ slices, double* __restrict__ stats) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ncols = 2 + ST_FIELDS * K;
+    // stage 2 of the reduction: the slices of each column, in slice order
+    auto col = [&](int o) {
+        double t = 0.0;
+#pragma unroll
+        for (int sl = 0; sl < kReduceSlices; ++sl) t += slices[(int64_t)sl * ncols + o];
+        return t;
+    };
+    if (k == 0) { stats[0] = col(0); stats[1] = col(1); }
     if (k >= K) return;
-    double* W = stats + 2 + k;
-    double* M = stats + 2 + K + 5 * k;
-    double* C = stats + 2 + 6 * K + 15 * k;   // lower triangle, row-major
     const double mu[3] = {(double)ep[EP_MU0 * Kp + k], (double)ep[EP_MU1 * Kp + k],
                           (double)ep[EP_MU2 * Kp + k]};
-    const double w = *W;
-    const double mp[3] = {M[0], M[1], M[2]};
+    const double w = col(2 + k);
+    double M[5], C[15];   // C: lower triangle, row-major
+    for (int i = 0; i < 5; ++i) M[i] = col(2 + K + 5 * k + i);
+    for (int i = 0; i < 15; ++i) C[i] = col(2 + 6 * K + 15 * k + i);
     // C_pp (entries 0..5: (0,0) (1,0) (1,1) (2,0) (2,1) (2,2))
     int e = 0;
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j <= i; ++j, ++e)
-            C[e] += mp[i] * mu[j] + mu[i] * mp[j] + w * mu[i] * mu[j];
+            C[e] += M[i] * mu[j] + mu[i] * M[j] + w * mu[i] * mu[j];
     // C_tp: rows 3, 4 (entries 6..8 and 10..12)
     for (int j = 0; j < 3; ++j) {
         C[6 + j] += M[3] * mu[j];
         C[10 + j] += M[4] * mu[j];
     }
-    for (int i = 0; i < 3; ++i) M[i] = mp[i] + w * mu[i];
+    for (int i = 0; i < 3; ++i) M[i] = M[i] + w * mu[i];
+    stats[2 + k] = w;
+    for (int i = 0; i < 5; ++i) stats[2 + K + 5 * k + i] = M[i];
+    for (int i = 0; i < 15; ++i) stats[2 + 6 * K + 15 * k + i] = C[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -1019,15 +1028,14 @@ hipError_t estep_occupancy(int cpl, int lps, int Kp, int* resp_blocks, int* stat
 }
 
 hipError_t launch_reduce_partials(const float* partials, int rows, int pstride, const float* ep_for_finalize,
-                                  int Kp, int K,
-                                  double* stats, hipStream_t st) {
+                                  int Kp, int K, double* stats, double* scratch, hipStream_t st) {
     const int ncols = 2 + ST_FIELDS * K;
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3((ncols + 63) / 64), dim3(1024), 0, st,
-                       partials, rows, pstride, Kp, K, stats);
+    hipLaunchKernelGGL(reduce_partials_slices_kernel, dim3((ncols + 63) / 64, kReduceSlices), dim3(256), 0, st,
+                       partials, rows, pstride, Kp, K, scratch);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(finalize_stats_kernel, dim3((K + 255) / 256), dim3(256), 0, st, ep_for_finalize,
-                       Kp, K, stats);
+    hipLaunchKernelGGL(finalize_stats_kernel, dim3((K + 63) / 64), dim3(64), 0, st, ep_for_finalize, Kp, K,
+                       scratch, stats);
     return hipGetLastError();
 }
 

@@ -13,10 +13,17 @@
 //
 // One thread per query.  The per-query marginal weights live in LDS laid out
 // [k][thread] (conflict-free); the sort is an incremental selection that stops
-// at the 0.99-mass cutoff, so only the kept prefix is ever ordered.  Every
-// floating-point step follows oracle/sdmm_oracle.c operation for operation
-// (no FMA contraction, double-precision transcendentals rounded to float, IEEE
-// division/sqrt), which makes the selected component index bit-identical.
+// at the 0.99-mass cutoff, so only the kept prefix is ever ordered.
+//
+// Precision split.  Everything the selected component index depends on -- the
+// marginal weights, the validity of each conditional, the normalisation and
+// the CDF -- follows oracle/sdmm_oracle.c operation for operation (no FMA
+// contraction, the double-precision exp of mvtn.h:359 rounded to float, IEEE
+// division/sqrt), which makes the index bit-identical.  A marginal weight whose
+// exponent argument puts NORM3 exp(-q/2) below FLT_MIN is exactly 0 under the
+// plugin's FTZ (volpath_sdmm.cpp:88-90) and skips the double exp.  The sampled
+// direction and the mixture pdf (tolerances 1e-5 / 1e-4) use the float
+// transcendentals.
 #include "sdmm_device.h"
 
 #pragma clang fp contract(off)
@@ -28,13 +35,12 @@ struct GuideConsts {
 };
 
 __device__ __forceinline__ float gp_ld(const float* gp, int Kp, int f, int k) {
-    return ((cfloat_p)gp)[f * Kp + k];
+    return ((cfloat_p)gp)[k * GP_STRIDE + f];   // AoS record (sdmm_device.h)
 }
 
-__device__ __forceinline__ float fl_acos(float x) { return (float)acos((double)x); }
-__device__ __forceinline__ float fl_cos(float x) { return (float)cos((double)x); }
-__device__ __forceinline__ float fl_sin(float x) { return (float)sin((double)x); }
-__device__ __forceinline__ float fl_log(float x) { return (float)log((double)x); }
+// q above this gives NORM3 exp(-q/2) < 2^-126: the float weight flushes to 0
+// (2 (126 ln 2 + ln NORM3) = 169.16, with margin)
+constexpr float kMarginalZeroQ = 170.0f;
 
 __device__ __forceinline__ void coordinates_f(const float n[3], float to[9]) {
     float sign = copysignf(1.0f, n[2]);
@@ -50,7 +56,7 @@ __device__ __forceinline__ float sinc_pi_f(float x) {
     const float taylor_2_bound = 3.4526698300124393e-04f;  // sqrtf(eps)
     const float taylor_n_bound = 1.8581361171917516e-02f;  // sqrtf(sqrtf(eps))
     float ax = fabsf(x);
-    if (ax >= taylor_n_bound) return fl_sin(x) / x;
+    if (ax >= taylor_n_bound) return sinf(x) / x;
     float result = 1.0f;
     if (ax >= taylor_0_bound) {
         float x2 = x * x;
@@ -65,16 +71,16 @@ __device__ __forceinline__ bool ts_exp_dir(const float to[9], float t0, float t1
     float length = sqrtf(t0 * t0 + t1 * t1);
     if ((double)length >= kPi) { e[0] = e[1] = e[2] = 0.0f; return false; }
     float s = sinc_pi_f(length);
-    float rel0 = t0 * s, rel1 = t1 * s, rel2 = fl_cos(length);
+    float rel0 = t0 * s, rel1 = t1 * s, rel2 = cosf(length);
     e[0] = to[0] * rel0 + to[3] * rel1 + to[6] * rel2;
     e[1] = to[1] * rel0 + to[4] * rel1 + to[7] * rel2;
     e[2] = to[2] * rel0 + to[5] * rel1 + to[8] * rel2;
     return true;
 }
 
-// MVN<3,3>::pdf with the forward substitution of LLT::matrixL().solve.
-__device__ __forceinline__ float marginal_pdf(const float* gp, int Kp, int k, const float c[3],
-                                              float norm3) {
+// MVN<3,3>::pdf with the forward substitution of LLT::matrixL().solve:
+// marginal_q is the squared Mahalanobis distance, marginal_pdf_q the pdf.
+__device__ __forceinline__ float marginal_q(const float* gp, int Kp, int k, const float c[3]) {
     float r0 = c[0] - gp_ld(gp, Kp, GP_MU0, k);
     float r1 = c[1] - gp_ld(gp, Kp, GP_MU1, k);
     float r2 = c[2] - gp_ld(gp, Kp, GP_MU2, k);
@@ -84,9 +90,15 @@ __device__ __forceinline__ float marginal_pdf(const float* gp, int Kp, int k, co
     float s1 = r1 / gp_ld(gp, Kp, GP_ML11, k);
     r2 = r2 - s1 * gp_ld(gp, Kp, GP_ML21, k);
     float s2 = r2 / gp_ld(gp, Kp, GP_ML22, k);
-    float q = s0 * s0 + s1 * s1 + s2 * s2;
+    return s0 * s0 + s1 * s1 + s2 * s2;
+}
+__device__ __forceinline__ float marginal_pdf_q(const float* gp, int Kp, int k, float q, float norm3) {
+    if (q > kMarginalZeroQ) return 0.0f;   // flushes to 0 in the reference (FTZ)
     float pdf = (float)((double)norm3 * exp(-0.5 * (double)q));
     return pdf * gp_ld(gp, Kp, GP_MDI, k);
+}
+__device__ __forceinline__ float marginal_pdf(const float* gp, int Kp, int k, const float c[3], float norm3) {
+    return marginal_pdf_q(gp, Kp, k, marginal_q(gp, Kp, k, c), norm3);
 }
 
 // MVTN::conditional: mean direction of joint component k's conditional at c.
@@ -114,14 +126,14 @@ __device__ __forceinline__ float cond_component_pdf(const float* gp, int Kp, int
     float cth = to[6] * d[0] + to[7] * d[1] + to[8] * d[2];
     if (cth <= -1.0f) return 0.0f;
     cth = (cth < 1.0f) ? cth : 1.0f;
-    float angle = fl_acos(cth);
+    float angle = acosf(cth);
     float s = sqrtf(1.0f - cth * cth);
     float a = ((double)s < 1e-3) ? 1.0f : (angle / s);
     float t0 = r0 * a, t1 = r1 * a;
     float s0 = gp_ld(gp, Kp, GP_CI00, k) * t0 + gp_ld(gp, Kp, GP_CI01, k) * t1;
     float s1 = gp_ld(gp, Kp, GP_CI10, k) * t0 + gp_ld(gp, Kp, GP_CI11, k) * t1;
     float q = s0 * s0 + s1 * s1;
-    float p = (float)((double)norm2 * exp(-0.5 * (double)q));
+    float p = norm2 * expf(-0.5f * q);
     p *= gp_ld(gp, Kp, GP_CDI, k) * a;
     return p;
 }
@@ -186,10 +198,11 @@ __device__ __forceinline__ QueryOut finish_query(const float* gp, int Kp, const 
         float esel[3];
         cond_mean_dir(gp, Kp, ksel, c, esel);
         // MVTN::sample of the conditional component (Box-Muller, L z, exp map)
-        const float radius = sqrtf(-2.0f * fl_log(1.0f - u[1]));
+        const float radius = sqrtf(-2.0f * logf(1.0f - u[1]));
         const float theta = (float)(2.0 * kPi * (double)u[2]);
-        const double res0 = sin((double)theta), res1 = cos((double)theta);
-        const float z0 = radius * (float)res0, z1 = radius * (float)res1;
+        float res0, res1;
+        sincosf(theta, &res0, &res1);
+        const float z0 = radius * res0, z1 = radius * res1;
         const float L00 = gp_ld(gp, Kp, GP_CL00, ksel), L10 = gp_ld(gp, Kp, GP_CL10, ksel);
         const float L11 = gp_ld(gp, Kp, GP_CL11, ksel);
         const float v0 = L00 * z0 + 0.0f * z1;
@@ -256,7 +269,13 @@ __device__ __forceinline__ int build_candidates(const float* gp, int Kp, int K, 
     int cnt = 0;
     bool over = false;
     for (int k = 0; k < K; ++k) {
-        const float w = gp_ld(gp, Kp, GP_W, k) * marginal_pdf(gp, Kp, k, c, norm3);
+        // pre-screen with the float exp (relative error ~1e-6): a weight more than
+        // 1e-3 below tau cannot reach it, and skips the double exp
+        const float q = marginal_q(gp, Kp, k, c);
+        const float pik = gp_ld(gp, Kp, GP_W, k);
+        const float wfast = pik * gp_ld(gp, Kp, GP_MDI, k) * norm3 * __expf(-0.5f * q);
+        if ((double)wfast * 1.001 < tau) continue;
+        const float w = pik * marginal_pdf_q(gp, Kp, k, q, norm3);
         if (!((double)w >= tau)) continue;
         if (cnt == cap) { over = true; continue; }
         const unsigned short key = (unsigned short)(k | (cond_valid(gp, Kp, k, c) ? 0x8000 : 0));

@@ -194,7 +194,7 @@ __device__ static void pack_component(int k, int K, int Kp, const CanonDev& C, f
         g[GP_CDI] = C.condDetInv[k];
     }
     for (int f = 0; f < EP_FIELDS; ++f) ep[f * Kp + k] = e[f];
-    for (int f = 0; f < GP_FIELDS; ++f) gp[f * Kp + k] = g[f];
+    for (int f = 0; f < GP_FIELDS; ++f) gp[k * GP_STRIDE + f] = g[f];
 }
 
 // createCdf(false) then configure()'s createCdf(true) (float, sequential);
@@ -235,9 +235,16 @@ pack_all_kernel(int K, int Kp, CanonDev C, float* ep, float* gp, float norm5) {
 // One stepwise M-step from the compact fp64 stats [H, wsum, W, M, Clow].
 __global__ void __launch_bounds__(512)
 mstep_kernel(int K, int Kp, const double* __restrict__ stats, int64_t nSamples, CanonDev C,
-             EmStateDev S, float* ep, float* gp, float norm5) {
+             EmStateDev S, float* ep, float* gp, float norm5, double* __restrict__ wmean,
+             double* __restrict__ wcov) {
+    // Two phases so the fp64 register footprint of the M-step and of MVTN::set
+    // never overlap (one phase alone fits the VGPR file, both spilled):
+    //   1. blend, MAP update, PD test, stats re-centring; the accepted (mean,
+    //      cov) go to wmean/wcov (K*6, K*25 doubles) and setk[k] = 1;
+    //   2. set_component for the accepted components.
     __shared__ double sh[16];
     extern __shared__ double newW[];
+    int* setk = (int*)(newW + K);
     const int t = threadIdx.x;
     if (t == 0) {
         const double weightSum = stats[1];
@@ -275,6 +282,7 @@ mstep_kernel(int K, int Kp, const double* __restrict__ stats, int64_t nSamples, 
     const double ni = S.scalars[SC_NI];
     const bool decreasePrior = S.scalars[SC_DECP] != 0.0;
 
+    for (int k = t; k < K; k += blockDim.x) setk[k] = 0;
     for (int k = t; k < K; k += blockDim.x) {
         double T = S.T[k];
         T *= (1.0 - eta);
@@ -349,7 +357,9 @@ mstep_kernel(int K, int Kp, const double* __restrict__ stats, int64_t nSamples, 
             if (!llt_d<5>(cov, Ltmp)) {
                 w_new = 0.0;                   // non-PD: kill (:945-960)
             } else {
-                set_component(k, emb, cov, C);
+                for (int i = 0; i < 6; ++i) wmean[6 * k + i] = emb[i];
+                for (int i = 0; i < 25; ++i) wcov[25 * k + i] = cov[i];
+                setk[k] = 1;
                 for (int i = 0; i < 5; ++i)
                     for (int j = 0; j < 5; ++j) nC[5 * i + j] -= nM[i] * mean5[j];
                 const double condStat[5] = {nM[0], nM[1], nM[2], 0.0, 0.0};
@@ -366,6 +376,9 @@ mstep_kernel(int K, int Kp, const double* __restrict__ stats, int64_t nSamples, 
         for (int i = 0; i < 5; ++i) S.sgM[5 * k + i] = gM[i];
         for (int i = 0; i < 25; ++i) S.sgC[25 * k + i] = gC[i];
     }
+    __syncthreads();
+    for (int k = t; k < K; k += blockDim.x)
+        if (setk[k]) set_component(k, wmean + 6 * k, wcov + 25 * k, C);
     __syncthreads();
     if (t == 0) {
         double sum = 0.0;
@@ -395,10 +408,11 @@ hipError_t launch_pack_all(int K, int Kp, const CanonDev& C, float* ep, float* g
 }
 
 hipError_t launch_mstep(int K, int Kp, const double* stats, int64_t nSamples, const CanonDev& C,
-                        const EmStateDev& S, float* ep, float* gp, float norm5, hipStream_t st) {
+                        const EmStateDev& S, float* ep, float* gp, float norm5, double* wmean, double* wcov,
+                        hipStream_t st) {
     const int threads = Kp < 64 ? 64 : (Kp > 512 ? 512 : Kp);
-    hipLaunchKernelGGL(mstep_kernel, dim3(1), dim3(threads), sizeof(double) * (size_t)K, st, K, Kp,
-                       stats, nSamples, C, S, ep, gp, norm5);
+    hipLaunchKernelGGL(mstep_kernel, dim3(1), dim3(threads), (sizeof(double) + sizeof(int)) * (size_t)K, st, K,
+                       Kp, stats, nSamples, C, S, ep, gp, norm5, wmean, wcov);
     return hipGetLastError();
 }
 

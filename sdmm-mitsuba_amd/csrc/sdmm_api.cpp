@@ -33,14 +33,14 @@ hipError_t launch_estep_stats_tile(int variant, const float* ep, int Kp, int K, 
                                    int64_t chunk, int blocks, float* partials, int pstride, hipStream_t st);
 hipError_t estep_stats_tile_occupancy(int variant, int Kp, int* blocks_per_cu);
 hipError_t launch_reduce_partials(const float* partials, int rows, int pstride, const float* ep_for_finalize,
-                                  int Kp, int K,
-                                  double* stats, hipStream_t st);
+                                  int Kp, int K, double* stats, double* scratch, hipStream_t st);
 hipError_t launch_set_all(int K, int Kp, const double* mean, const double* cov, const CanonDev& C,
                           float* ep, float* gp, float norm5, hipStream_t st);
 hipError_t launch_pack_all(int K, int Kp, const CanonDev& C, float* ep, float* gp, float norm5,
                            hipStream_t st);
 hipError_t launch_mstep(int K, int Kp, const double* stats, int64_t nSamples, const CanonDev& C,
-                        const EmStateDev& S, float* ep, float* gp, float norm5, hipStream_t st);
+                        const EmStateDev& S, float* ep, float* gp, float norm5, double* wmean, double* wcov,
+                        hipStream_t st);
 hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float* const c[3],
                         const float* const u[3], const float* const dgiven[3], float* const d[3], float* pdf,
                         int32_t* comp, float norm2, float norm3, int cap, int* fb_count, int32_t* fb_list,
@@ -201,6 +201,7 @@ struct sdmm_mix {
     float* ep = nullptr;
     float* gp = nullptr;
     double* stats = nullptr;     // compact stats (2 + 21K)
+    double* rscratch = nullptr;  // 16 x (2 + 21K) fp64 row-slice sums of the stats reduction
     double* tmp_mean = nullptr;  // K*6 (set_params / init)
     double* tmp_cov = nullptr;   // K*25
     float* partials = nullptr;
@@ -305,7 +306,7 @@ int run_estep_stats(sdmm_mix* m, const sdmm_samples* s, double* stats_out) {
         HIP_TRY(launch_estep_stats_tile(m->svariant, m->ep, m->Kp, m->K, d, s->n, chunk, blocks, m->partials,
                                         m->pstride, m->stream));
         HIP_TRY(launch_reduce_partials(m->partials, blocks, m->pstride, m->ep, m->Kp, m->K, stats_out,
-                                       m->stream));
+                                       m->rscratch, m->stream));
         return SDMM_OK;
     }
     const Split sp = split_for(m, s->n, m->lps, m->stats_blocks);
@@ -314,7 +315,7 @@ int run_estep_stats(sdmm_mix* m, const sdmm_samples* s, double* stats_out) {
     HIP_TRY(launch_estep_stats(m->cpl, m->lps, m->ep, m->Kp, m->K, d, s->n, sp.chunk, sp.blocks, sp.wpb,
                                m->partials, m->pstride, m->stream));
     HIP_TRY(launch_reduce_partials(m->partials, sp.blocks, m->pstride, m->ep, m->Kp, m->K, stats_out,
-                                   m->stream));
+                                   m->rscratch, m->stream));
     return SDMM_OK;
 }
 
@@ -407,8 +408,9 @@ int sdmm_create(int K, const sdmm_em_params* params, int device, sdmm_mix** out)
     add(&valid, 4 * Kc);
     add(&sc, 8 * SC_COUNT); add(&T, 8 * Kc); add(&sgW, 8 * Kc); add(&sgM, 40 * Kc); add(&sgC, 200 * Kc);
     add(&bp, 100 * Kc); add(&bd, 36 * Kc);
-    add(&m->ep, 4 * (size_t)EP_FIELDS * m->Kp); add(&m->gp, 4 * (size_t)GP_FIELDS * m->Kp);
+    add(&m->ep, 4 * (size_t)EP_FIELDS * m->Kp); add(&m->gp, 4 * (size_t)GP_STRIDE * m->Kp);
     add(&m->stats, 8 * sdmm_stats_len(K));
+    add(&m->rscratch, 8 * 16 * sdmm_stats_len(K));
     add(&m->tmp_mean, 48 * Kc); add(&m->tmp_cov, 200 * Kc);
     (void)f_canon;
     size_t total = 0;
@@ -570,7 +572,8 @@ int sdmm_estep_stats(sdmm_mix* m, const sdmm_samples* s, double* stats) {
 int sdmm_mstep(sdmm_mix* m, const double* stats, int64_t n_total) {
     if (!m || !stats) return fail(SDMM_E_INVALID, "invalid argument");
     if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
-    HIP_TRY(launch_mstep(m->K, m->Kp, stats, n_total, m->C, m->S, m->ep, m->gp, m->norm5, m->stream));
+    HIP_TRY(launch_mstep(m->K, m->Kp, stats, n_total, m->C, m->S, m->ep, m->gp, m->norm5, m->tmp_mean,
+                         m->tmp_cov, m->stream));
     return SDMM_OK;
 }
 
@@ -583,7 +586,8 @@ int sdmm_em_step(sdmm_mix* m, const sdmm_samples* s, int iterations) {
     for (int it = 0; it < iterations; ++it) {
         r = run_estep_stats(m, s, m->stats);
         if (r) return r;
-        HIP_TRY(launch_mstep(m->K, m->Kp, m->stats, s->n, m->C, m->S, m->ep, m->gp, m->norm5, m->stream));
+        HIP_TRY(launch_mstep(m->K, m->Kp, m->stats, s->n, m->C, m->S, m->ep, m->gp, m->norm5, m->tmp_mean,
+                             m->tmp_cov, m->stream));
     }
     return SDMM_OK;
 }

@@ -3,7 +3,7 @@
 // HBM layouts (all SoA so a wave's 64 lanes touch consecutive addresses):
 //   samples      x0..x5, w, [hpdf], [isDiffuse]  one plane per field, N each
 //   E-step param ep[f * Kp + k], f < EP_FIELDS    (component k on lane k / CPL)
-//   guide param  gp[f * Kp + k], f < GP_FIELDS
+//   guide param  gp[k * GP_STRIDE + f], f < GP_FIELDS (AoS, see below)
 //   stats        compact double [H, wsum, W(K), M(5K), Clow(15K)]  (2 + 21K)
 //   partials     float [G][PSTRIDE], one row per E-step workgroup
 #pragma once
@@ -46,6 +46,11 @@ enum : int {
     GP_CDI,                              // conditional detInv
     GP_FIELDS
 };
+// The guide record is AoS, gp[k * GP_STRIDE + f]: a query thread walks the
+// components in order with wave-uniform k, so one component's fields come in
+// a few wide scalar loads (s_load_dwordx8/x16) instead of one load per field.
+constexpr int GP_STRIDE = 36;
+static_assert(GP_FIELDS <= GP_STRIDE, "guide record stride");
 
 // Per-component sufficient statistics accumulated by the E-step.
 enum : int {
