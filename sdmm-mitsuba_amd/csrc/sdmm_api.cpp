@@ -29,6 +29,10 @@ hipError_t estep_occupancy(int cpl, int lps, int Kp, int* resp_blocks, int* stat
 hipError_t launch_estep_resp_tile(int variant, const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
                                   int64_t chunk, float* resp, hipStream_t st);
 hipError_t estep_resp_tile_occupancy(int variant, int* blocks_per_cu);
+hipError_t launch_estep_resp_mfma(int variant, const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
+                                  int64_t chunk, float* resp, hipStream_t st);
+hipError_t estep_resp_mfma_occupancy(int variant, int Kp, int* blocks_per_cu);
+const char* estep_resp_mfma_name(int variant, int Kp);
 hipError_t launch_estep_stats_tile(int variant, const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
                                    int64_t chunk, int blocks, float* partials, int pstride, hipStream_t st);
 hipError_t estep_stats_tile_occupancy(int variant, int Kp, int* blocks_per_cu);
@@ -178,6 +182,7 @@ struct sdmm_mix {
     int K = 0, Kp = 0, cpl = 1, lps = 64;   // statistics E-step layout
     int rcpl = 2, rlps = 64;                 // responsibility E-step layout (same Kp)
     int rtile = 0;                           // 1: estep_resp_tile_kernel (64 < K <= 128)
+                                             // 2: estep_resp_mfma_kernel (every K)
     int rvariant = 0;                        // tile kernel scheduling variant (SDMM_RESP_VARIANT)
     int stile = 0;                           // 1: estep_stats_tile_kernel (64 < K <= 128)
     int svariant = 0;                        // its occupancy variant (SDMM_STATS_VARIANT)
@@ -372,7 +377,12 @@ int sdmm_create(int K, const sdmm_em_params* params, int device, sdmm_mix** out)
     {
         const char* ev = std::getenv("SDMM_RESP_KERNEL");
         const bool legacy = ev && std::strcmp(ev, "legacy") == 0;
-        if (K > 64 && K <= 128 && !legacy) { m->rtile = 1; m->rcpl = 2; m->rlps = 64; }
+        const bool mfma = ev && std::strcmp(ev, "mfma") == 0;
+        if (K > 64 && K <= 128 && !legacy && !mfma) { m->rtile = 1; m->rcpl = 2; m->rlps = 64; }
+        // SDMM_RESP_KERNEL=mfma: the linear forms on the f32 matrix cores
+        // (estep_mfma.hip); measured slower on gfx950 (no VALU/MFMA co-execution
+        // for f32 MFMA), kept as a tested alternative
+        if (mfma) m->rtile = 2;
         const char* vv = std::getenv("SDMM_RESP_VARIANT");
         if (vv) m->rvariant = std::atoi(vv);
         const char* sv = std::getenv("SDMM_STATS_KERNEL");
@@ -384,7 +394,9 @@ int sdmm_create(int K, const sdmm_em_params* params, int device, sdmm_mix** out)
     if (estep_occupancy(m->rcpl, m->rlps, m->Kp, &m->resp_blocks, &unused) != hipSuccess ||
         estep_occupancy(m->cpl, m->lps, m->Kp, &unused, &m->stats_blocks) != hipSuccess)
         return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
-    if (m->rtile && estep_resp_tile_occupancy(m->rvariant, &m->resp_blocks) != hipSuccess)
+    if (m->rtile == 2 && estep_resp_mfma_occupancy(m->rvariant, m->Kp, &m->resp_blocks) != hipSuccess)
+        return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
+    if (m->rtile == 1 && estep_resp_tile_occupancy(m->rvariant, &m->resp_blocks) != hipSuccess)
         return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
     if (m->stile && estep_stats_tile_occupancy(m->svariant, m->Kp, &m->stats_blocks) != hipSuccess)
         return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
@@ -486,7 +498,10 @@ const char* sdmm_kernel_name(const sdmm_mix* m, int which) {
     if (!m) return "";
     static thread_local char buf[64];
     if (which == 0) {
-        if (m->rtile) {
+        if (m->rtile == 2) {
+            std::snprintf(buf, sizeof buf, "%s", estep_resp_mfma_name(m->rvariant, m->Kp));
+            return buf;
+        } else if (m->rtile) {
             std::snprintf(buf, sizeof buf, "estep_resp_tile_kernel<4,%d>", m->rvariant == 1 ? 4 : m->rvariant == 2 ? 16 : 2);
             return buf;
         }
@@ -634,6 +649,15 @@ int sdmm_responsibilities(sdmm_mix* m, const sdmm_samples* s, float* resp) {
     int r = check_samples(s);
     if (r) return r;
     if (s->n == 0) return SDMM_OK;
+    if (m->rtile == 2) {
+        // chunks of whole 16-sample tiles, ~3 rounds of resident waves
+        const int64_t resident = (int64_t)m->cus * 4 * (m->resp_blocks > 0 ? m->resp_blocks : 1);
+        int64_t chunk = (s->n + 3 * resident - 1) / (3 * resident);
+        chunk = ((chunk + 15) / 16) * 16;
+        if (chunk < 64) chunk = 64;
+        HIP_TRY(launch_estep_resp_mfma(m->rvariant, m->ep, m->Kp, m->K, to_dev(s), s->n, chunk, resp, m->stream));
+        return SDMM_OK;
+    }
     if (m->rtile) {
         // chunks of whole 64-sample blocks; ~3 rounds of resident waves so the
         // tail of the launch stays short

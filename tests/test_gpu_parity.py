@@ -375,3 +375,27 @@ def test_sample_discrete_cdf_bit_exact(pkg, oracle, gpu):
         got = mix.sample_discrete_cdf(torch.from_numpy(cdf).to(gpu), torch.from_numpy(u).to(gpu))
         ref = np.array([oracle.sample_discrete_cdf(cdf, x) for x in u])
         np.testing.assert_array_equal(got.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("kernel,K", [("mfma", 128), ("mfma", 72), ("mfma", 16), ("mfma", 256), ("mfma", 512),
+                                      ("tile", 128), ("legacy", 128), ("legacy", 256)])
+def test_responsibilities_fitted_each_kernel(pkg, oracle, synth, gpu, monkeypatch, kernel, K):
+    """Every responsibility kernel (SDMM_RESP_KERNEL) on a FITTED mixture (4 EM
+    iterations: tight covariances, large L^-1) against the fp32 oracle and the
+    fp64 evaluation of the same float parameters.  The MFMA kernel evaluates
+    L^-1 (p - mu) as L^-1 (p - o) - L^-1 (mu - o) (o = 0.5): the bound of
+    _check_resp (4x the fp32 oracle's own error + 1e-5) holds for it too."""
+    import torch
+    monkeypatch.setenv("SDMM_RESP_KERNEL", kernel)
+    N = 3001
+    b, mix, m = _em_model(pkg, oracle, synth, K, N, 4)
+    name = mix.kernel_name("resp")
+    assert {"mfma": "mfma", "tile": "tile", "legacy": "estep_resp_kernel"}[kernel] in name, name
+    ds = pkg.DeviceSamples.from_numpy(b["x"], b["w"], b["hpdf"], b["is_diffuse"])
+    resp = torch.full((N, K), -1.0, device=gpu)
+    mix.posterior(ds, resp)
+    torch.cuda.synchronize()
+    got = resp.cpu().numpy()
+    ref = oracle.responsibilities(m, oracle.Samples(b["x"], b["w"]))
+    assert np.isfinite(got).all()
+    _check_resp(got, ref, mix.get_params(), b["x"])

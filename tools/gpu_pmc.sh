@@ -11,10 +11,10 @@ export TMPDIR=/tmp
 cd /tmp || exit 1
 timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || { echo "counter listing failed"; exit 1; }
 i=0
-for group in "FETCH_SIZE" "WRITE_SIZE" \
-             "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" \
-             "SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_INSTS_LDS" \
-             "GRBM_GUI_ACTIVE GRBM_COUNT"; do
+# PMC_GROUPS (optional): counter groups separated by ';' replace the default passes
+GROUPS_DEFAULT="FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU;SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_INSTS_LDS;SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES SQ_ACTIVE_INST_MISC;GRBM_GUI_ACTIVE GRBM_COUNT"
+IFS=';' read -r -a GROUP_LIST <<< "${PMC_GROUPS:-$GROUPS_DEFAULT}"
+for group in "${GROUP_LIST[@]}"; do
   i=$((i + 1))
   timeout -k 10 240 rocprofv3 --pmc $group --output-format csv -d "$OUT/p$i" -o run \
       -- python3 "$GRAFT_REPO_ROOT/tools/prof_kernels.py" "$@" > "$OUT/p$i.log" 2>&1
