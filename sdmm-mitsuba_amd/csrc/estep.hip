@@ -380,6 +380,48 @@ __device__ __forceinline__ V pair_q_fast(const V* __restrict__ P, float p0, floa
     return e * (P[EP_DIPI] * a);
 }
 
+// theta/sin(theta) without the sin < 1e-3 quirks (mvtn.h:157-164): h(u) for
+// c >= 0 (h is within 1.7e-7 of the reference's exact 1 when sin < 1e-3), and
+// pi/sqrt(1 - c^2) - h(u) for c < 0.  Tiles where some c < -0.9999995 (the
+// quirk: J = 1, or a failed log map at c <= -1) are redone with
+// angle_over_sin_fast by the caller.  u = (1 - |c|)/2 in plain VOP3 fmas with
+// the |.| source modifier (packed ops have no abs).
+__device__ __forceinline__ V angle_over_sin_main(V c) {
+    const V s2 = vfma(-c, c, sp(1.0f));
+    const V u = V{fmaf(-0.5f, fabsf(c.x), 0.5f), fmaf(-0.5f, fabsf(c.y), 0.5f)};
+    V h = vfma(sp(3.3755881786346436f), u, sp(-3.17423415184021f));
+    h = vfma(h, u, sp(2.1241207122802734f));
+    h = vfma(h, u, sp(-0.04515757039189339f));
+    h = vfma(h, u, sp(0.5178175568580627f));
+    h = vfma(h, u, sp(0.5294308066368103f));
+    h = vfma(h, u, sp(0.6667603850364685f));
+    h = vfma(h, u, sp(0.9999996423721313f));
+    const V fneg = vfma(sp(3.14159265358979f), vrsq(s2), -h);
+    return V{c.x < 0.0f ? fneg.x : h.x, c.y < 0.0f ? fneg.y : h.y};
+}
+
+// pi_k pdf_k of a component pair for the responsibility tiles: origin-shifted
+// spatial rows (p0..p2 are p - kOrigin; EP_NC* fold -L (mu - kOrigin)), folded
+// directional rows, and the main-path angle (RARE selects the quirk path).
+template <bool RARE>
+__device__ __forceinline__ V pair_q_tile(const V* __restrict__ P, float p0, float p1, float p2, float d0,
+                                         float d1, float d2) {
+    const V c = vfma(P[EP_R22], sp(d2), vfma(P[EP_R21], sp(d1), P[EP_R20] * d0));
+    const V a = RARE ? angle_over_sin_fast(c) : angle_over_sin_main(c);
+    const V u0 = vfma(P[EP_L00], sp(p0), P[EP_NC0]);
+    const V u1 = vfma(P[EP_L11], sp(p1), vfma(P[EP_L10], sp(p0), P[EP_NC1]));
+    const V u2 = vfma(P[EP_L22], sp(p2), vfma(P[EP_L21], sp(p1), vfma(P[EP_L20], sp(p0), P[EP_NC2])));
+    const V s3 = vfma(P[EP_L32], sp(p2), vfma(P[EP_L31], sp(p1), vfma(P[EP_L30], sp(p0), P[EP_NC3])));
+    const V s4 = vfma(P[EP_L42], sp(p2), vfma(P[EP_L41], sp(p1), vfma(P[EP_L40], sp(p0), P[EP_NC4])));
+    const V ad = vfma(P[EP_A2], sp(d2), vfma(P[EP_A1], sp(d1), P[EP_A0] * d0));
+    const V bd = vfma(P[EP_B2], sp(d2), vfma(P[EP_B1], sp(d1), P[EP_B0] * d0));
+    const V u3 = vfma(a, ad, s3);
+    const V u4 = vfma(a, bd, s4);
+    const V q = vfma(u4, u4, vfma(u3, u3, vfma(u2, u2, vfma(u1, u1, u0 * u0))));
+    const V e = vexp2(vfma(q, sp(-0.72134752044448170368f), sp(kLog2Norm5)));
+    return e * (P[EP_DIPI] * a);
+}
+
 // lane ^ 4 within each row of 16 (row_shl:4 on banks 0 and 2, row_shr:4 on
 // banks 1 and 3: a disabled bank keeps the `old` operand)
 __device__ __forceinline__ float xor4(float x) {
@@ -422,14 +464,51 @@ __device__ __forceinline__ float transpose_sum16(const float (&v)[kTile], int la
     return x;
 }
 
-template <int WPB, int SB>
-__global__ void __launch_bounds__(64 * WPB, (SB <= 2 ? 4 : 3))
+// lane ^ M within the wave (DPP inside rows of 16, ds_bpermute across rows)
+template <int M>
+__device__ __forceinline__ float lane_xor(float x) {
+    if constexpr (M == 1) return dpp<0xB1>(x);        // quad_perm [1,0,3,2]
+    else if constexpr (M == 2) return dpp<0x4E>(x);   // quad_perm [2,3,0,1]
+    else if constexpr (M == 4) return xor4(x);
+    else if constexpr (M == 8) return dpp<0x128>(x);  // row_ror:8
+    else return __shfl_xor(x, M);
+}
+
+// transposed butterfly, generic KT (power of two <= 16): out = the wave-wide
+// sum of v[lane & (KT-1)]
+template <int KT, int S = 0>
+__device__ __forceinline__ float transpose_sum_step(const float* v, int lane) {
+    constexpr int M = 1 << S;
+    if constexpr (KT == 1) {
+        float x = v[0];
+        if constexpr (M <= 1) x += lane_xor<1>(x);
+        if constexpr (M <= 2) x += lane_xor<2>(x);
+        if constexpr (M <= 4) x += lane_xor<4>(x);
+        if constexpr (M <= 8) x += lane_xor<8>(x);
+        if constexpr (M <= 16) x += lane_xor<16>(x);
+        x += lane_xor<32>(x);
+        return x;
+    } else {
+        const bool bit = lane & M;
+        float nxt[KT / 2];
+#pragma unroll
+        for (int i = 0; i < KT / 2; ++i) {
+            const float keep = bit ? v[2 * i + 1] : v[2 * i];
+            const float send = bit ? v[2 * i] : v[2 * i + 1];
+            nxt[i] = keep + lane_xor<M>(send);
+        }
+        return transpose_sum_step<KT / 2, S + 1>(nxt, lane);
+    }
+}
+
+template <int WPB, int SB, int KT, int OCC>
+__global__ void __launch_bounds__(64 * WPB, OCC)
 estep_resp_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, int64_t n,
                        int64_t chunk, float* __restrict__ resp) {
     // per wave: the staged sample block (x0 x1 x2 x3 | x4 x5 hpdf diffuse) and
     // the tile's normalisation scales
     __shared__ float4 sblk[WPB][64][2];
-    __shared__ float sg[WPB][kTile];
+    __shared__ float sg[WPB][KT];
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t wave = (int64_t)blockIdx.x * WPB + wid;
@@ -453,30 +532,57 @@ estep_resp_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s
             const int64_t si = (blk + lane < s1) ? blk + lane : s1 - 1;
             const int sh = 8 * (int)((uintptr_t)(s.isDiffuse + si) & 3);
             const bool dif = has_d && ((A.diff >> sh) & 0xff) != 0;
-            blk_lds[lane][0] = float4{A.x0, A.x1, A.x2, A.x3};
+            // positions relative to kOrigin (the EP_NC* rows fold -L (mu - kOrigin))
+            blk_lds[lane][0] = float4{A.x0 - kOrigin, A.x1 - kOrigin, A.x2 - kOrigin, A.x3};
             blk_lds[lane][1] = float4{A.x4, A.x5, has_h ? A.h : 0.0f, dif ? 1.0f : 0.0f};
         }
         A = load_block(s, blk + 64, s1, lane);   // next block in flight (clamped past the end)
         const int cnt = (s1 - blk < 64) ? (int)(s1 - blk) : 64;
-        for (int tb = 0; tb < cnt; tb += kTile) {
-            V q[kTile];
+        for (int tb = 0; tb < cnt; tb += KT) {
+            V q[KT];
+            // rare-angle detector: c < -0.9999995 <=> its bits, unsigned, exceed
+            // those of -0.9999995f (integer max, no NaN canonicalisation)
+            uint32_t cbits = 0;
 #pragma unroll
-            for (int t = 0; t < kTile; ++t) {
+            for (int t = 0; t < KT; ++t) {
                 const float4 a = blk_lds[tb + t][0];
                 const float4 b = blk_lds[tb + t][1];
-                q[t] = pair_q_fast(P, a.x, a.y, a.z, a.w, b.x, b.y);
+                q[t] = pair_q_tile<false>(P, a.x, a.y, a.z, a.w, b.x, b.y);
+                const V c = vfma(P[EP_R22], sp(b.y), vfma(P[EP_R21], sp(b.x), P[EP_R20] * a.w));
+                cbits = __builtin_elementwise_max(cbits, __builtin_elementwise_max(__builtin_bit_cast(uint32_t, c.x),
+                                                                                   __builtin_bit_cast(uint32_t, c.y)));
                 // keep the scheduler from hoisting every sample's LDS reads
                 // (and their registers) to the top of the tile
                 if (t % SB == SB - 1) __builtin_amdgcn_sched_barrier(0);
             }
-            float ps[kTile];
+            {
+                // rare angle case in the tile (c < -0.9999995 somewhere): redo it
+                // with the reference's quirks.  The test also reads the fast
+                // path's values (a NaN -- NaN input -- takes the redo too,
+                // harmlessly) so that the fast path is not sunk below the branch.
+                V qs = q[0];
 #pragma unroll
-            for (int t = 0; t < kTile; ++t) ps[t] = q[t].x + q[t].y;
-            const float S = transpose_sum16(ps, lane);
-            // posterior normalisation of sample tb + (lane & 15) (mixture_model.h:170-191);
+                for (int t = 1; t < KT; ++t) qs += q[t];
+                const bool odd = cbits > __builtin_bit_cast(uint32_t, -0.9999995f) || !(qs.x + qs.y >= 0.0f);
+                if (__builtin_amdgcn_ballot_w64(odd) != 0) {
+#pragma unroll 1
+                    for (int t = 0; t < KT; ++t) {
+                        const float4 a = blk_lds[tb + t][0];
+                        const float4 b = blk_lds[tb + t][1];
+                        const V qt = pair_q_tile<true>(P, a.x, a.y, a.z, a.w, b.x, b.y);
+#pragma unroll
+                        for (int u = 0; u < KT; ++u) q[u] = (u == t) ? qt : q[u];
+                    }
+                }
+            }
+            float ps[KT];
+#pragma unroll
+            for (int t = 0; t < KT; ++t) ps[t] = q[t].x + q[t].y;
+            const float S = transpose_sum_step<KT>(ps, lane);
+            // posterior normalisation of sample tb + (lane & (KT - 1)) (mixture_model.h:170-191);
             // d == 0 fails every log map (mvtn.h:152-154): all pdfs 0, 1/S' not finite
             {
-                const int t = tb + (lane & 15);
+                const int t = tb + (lane & (KT - 1));
                 const float4 a = blk_lds[t][0];
                 const float4 b = blk_lds[t][1];
                 const bool dzero = (a.w == 0.0f && b.x == 0.0f && b.y == 0.0f);
@@ -485,13 +591,13 @@ estep_resp_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s
                 const float inv = __builtin_amdgcn_rcpf(S2);
                 const bool fin = __builtin_isfinite(inv) && !dzero;
                 const float g = fin ? (dif ? inv * (1.0f - kHeuristicWeight) : inv) : 0.0f;
-                if (lane < kTile) g_lds[lane] = g;
+                if (lane < KT) g_lds[lane] = g;
             }
             // a non-finite sum means a non-finite q (NaN input): zero by select
             const bool bad = __builtin_amdgcn_ballot_w64(!__builtin_isfinite(S)) != 0;
-            const int tcnt = (cnt - tb < kTile) ? cnt - tb : kTile;
+            const int tcnt = (cnt - tb < KT) ? cnt - tb : KT;
 #pragma unroll
-            for (int t = 0; t < kTile; ++t) {
+            for (int t = 0; t < KT; ++t) {
                 if (t >= tcnt) break;
                 const float g = g_lds[t];
                 V o = q[t] * g;
@@ -653,11 +759,12 @@ constexpr int kStatTile = 4;
 
 // pi_k pdf_k and the directional tangent (mvtn.h:146-177 with the quirks of
 // angle_over_sin_fast: a = 0 when the log map fails, so ta = tb = 0 then).
+template <bool RARE>
 __device__ __forceinline__ V pair_qt_fast(const V* __restrict__ P, float p0, float p1, float p2, float d0,
                                           float d1, float d2, V& ta, V& tb) {
     const V tp0 = p0 - P[EP_MU0], tp1 = p1 - P[EP_MU1], tp2 = p2 - P[EP_MU2];
     const V c = vfma(P[EP_R22], sp(d2), vfma(P[EP_R21], sp(d1), P[EP_R20] * d0));
-    const V a = angle_over_sin_fast(c);
+    const V a = RARE ? angle_over_sin_fast(c) : angle_over_sin_main(c);
     const V r0 = vfma(P[EP_R02], sp(d2), vfma(P[EP_R01], sp(d1), P[EP_R00] * d0));
     const V r1 = vfma(P[EP_R12], sp(d2), vfma(P[EP_R11], sp(d1), P[EP_R10] * d0));
     ta = r0 * a;
@@ -736,11 +843,37 @@ estep_stats_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
             const int cnt = (s1 - blk < 64) ? (int)(s1 - blk) : 64;
             for (int tb = 0; tb < cnt; tb += kStatTile) {
                 V q[kStatTile], ta[kStatTile], tb2[kStatTile];
+                uint32_t cbits = 0;   // rare-angle detector (see estep_resp_tile_kernel)
 #pragma unroll
                 for (int t = 0; t < kStatTile; ++t) {
                     const float4 a = blk_lds[tb + t][0];
                     const float4 b = blk_lds[tb + t][1];
-                    q[t] = pair_qt_fast(P, a.x, a.y, a.z, a.w, b.x, b.y, ta[t], tb2[t]);
+                    q[t] = pair_qt_fast<false>(P, a.x, a.y, a.z, a.w, b.x, b.y, ta[t], tb2[t]);
+                    const V c = vfma(P[EP_R22], sp(b.y), vfma(P[EP_R21], sp(b.x), P[EP_R20] * a.w));
+                    cbits = __builtin_elementwise_max(
+                        cbits, __builtin_elementwise_max(__builtin_bit_cast(uint32_t, c.x), __builtin_bit_cast(uint32_t, c.y)));
+                }
+                {
+                    // c < -0.9999995 somewhere in the tile: redo it with the
+                    // reference's angle quirks (a NaN sum takes the redo too)
+                    const V qs = (q[0] + q[1]) + (q[2] + q[3]);
+                    const bool odd = cbits > __builtin_bit_cast(uint32_t, -0.9999995f) || !(qs.x + qs.y >= 0.0f);
+                    if (__builtin_amdgcn_ballot_w64(odd) != 0) {
+                        // (a loop, so that the compiler does not speculate it)
+#pragma unroll 1
+                        for (int t = 0; t < kStatTile; ++t) {
+                            const float4 a = blk_lds[tb + t][0];
+                            const float4 b = blk_lds[tb + t][1];
+                            V ta1, tb1;
+                            const V q1 = pair_qt_fast<true>(P, a.x, a.y, a.z, a.w, b.x, b.y, ta1, tb1);
+#pragma unroll
+                            for (int u = 0; u < kStatTile; ++u) {
+                                q[u] = (u == t) ? q1 : q[u];
+                                ta[u] = (u == t) ? ta1 : ta[u];
+                                tb2[u] = (u == t) ? tb1 : tb2[u];
+                            }
+                        }
+                    }
                 }
                 float ps[kStatTile];
 #pragma unroll
@@ -953,26 +1086,42 @@ hipError_t launch_estep_resp(int cpl, int lps, const float* ep, int Kp, int K, c
 
 // Tiled responsibility kernel (64 < K <= 128, Kp == 128): chunk is a multiple
 // of 64 samples per wave.
+// Variants (SDMM_RESP_VARIANT): {SB, KT, waves per SIMD}.
+#define SDMM_TILE_VARIANTS(X) X(0, 2, 16, 4) X(1, 2, 8, 4) X(2, 2, 16, 3) X(3, 4, 16, 3) X(4, 2, 8, 3)
+
 hipError_t launch_estep_resp_tile(int variant, const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
                                   int64_t chunk, float* resp, hipStream_t st) {
     if (Kp != 128 || K <= 64 || K > 128) return hipErrorInvalidValue;
     constexpr int wpb = 4;
     const int64_t waves = (n + chunk - 1) / chunk;
     const int64_t blocks = (waves + wpb - 1) / wpb;
-#define L(SB) hipLaunchKernelGGL((estep_resp_tile_kernel<wpb, SB>), dim3((unsigned)blocks), dim3(64 * wpb), 0, \
-                                 st, ep, Kp, K, s, n, chunk, resp)
-    if (variant == 1) L(4);
-    else if (variant == 2) L(16);
-    else L(2);
-#undef L
-    return hipGetLastError();
+#define X(V, SB, KT, OCC)                                                                           \
+    if (variant == V) {                                                                            \
+        hipLaunchKernelGGL((estep_resp_tile_kernel<wpb, SB, KT, OCC>), dim3((unsigned)blocks), dim3(64 * wpb), 0, \
+                           st, ep, Kp, K, s, n, chunk, resp);                                     \
+        return hipGetLastError();                                                                  \
+    }
+    SDMM_TILE_VARIANTS(X)
+#undef X
+    return hipErrorInvalidValue;
 }
 
 hipError_t estep_resp_tile_occupancy(int variant, int* blocks_per_cu) {
-    const void* f = variant == 1 ? reinterpret_cast<const void*>(&estep_resp_tile_kernel<4, 4>)
-                  : variant == 2 ? reinterpret_cast<const void*>(&estep_resp_tile_kernel<4, 16>)
-                                 : reinterpret_cast<const void*>(&estep_resp_tile_kernel<4, 2>);
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, 256, 0);
+#define X(V, SB, KT, OCC)                                                                           \
+    if (variant == V)                                                                              \
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(                                       \
+            blocks_per_cu, reinterpret_cast<const void*>(&estep_resp_tile_kernel<4, SB, KT, OCC>), 256, 0);
+    SDMM_TILE_VARIANTS(X)
+#undef X
+    return hipErrorInvalidValue;
+}
+
+const char* estep_resp_tile_name(int variant) {
+#define X(V, SB, KT, OCC) \
+    if (variant == V) return "estep_resp_tile_kernel<4," #SB "," #KT "," #OCC ">";
+    SDMM_TILE_VARIANTS(X)
+#undef X
+    return "estep_resp_tile_kernel<?>";
 }
 
 // Tiled statistics kernel (64 < K <= 128, Kp == 128): `blocks` workgroups of 4

@@ -42,7 +42,6 @@ namespace {
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 constexpr float kLog2Norm5M = -6.628740082514092f;   // log2((float)pow(0.39894228f, 5)), mvtn.h:351-352
-constexpr float kOrigin = 0.5f;
 
 
 template <int CTRL>

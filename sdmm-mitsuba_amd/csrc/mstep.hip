@@ -181,6 +181,14 @@ __device__ static void pack_component(int k, int K, int Kp, const CanonDev& C, f
             e[EP_B0 + i] = Li[23] * to[i] + Li[24] * to[3 + i];
         }
         e[EP_DIPI] = e[EP_DI] * e[EP_PI];
+        for (int m = 0; m < 5; ++m) {
+            const int row = m * (m + 1) / 2;          // packed lower-triangle row of L^-1
+            const int jn = m < 3 ? m + 1 : 3;
+            double acc = 0.0;
+            for (int j = 0; j < jn; ++j)
+                acc += (double)e[EP_L00 + row + j] * ((double)mu[j] - (double)kOrigin);
+            e[EP_NC0 + m] = (float)(-acc);
+        }
         g[GP_W] = w;
         g[GP_MU0] = mu[0]; g[GP_MU1] = mu[1]; g[GP_MU2] = mu[2];
         const float* ML = C.margL + 9 * k;

@@ -29,6 +29,7 @@ hipError_t estep_occupancy(int cpl, int lps, int Kp, int* resp_blocks, int* stat
 hipError_t launch_estep_resp_tile(int variant, const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
                                   int64_t chunk, float* resp, hipStream_t st);
 hipError_t estep_resp_tile_occupancy(int variant, int* blocks_per_cu);
+const char* estep_resp_tile_name(int variant);
 hipError_t launch_estep_resp_mfma(int variant, const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
                                   int64_t chunk, float* resp, hipStream_t st);
 hipError_t estep_resp_mfma_occupancy(int variant, int Kp, int* blocks_per_cu);
@@ -183,7 +184,7 @@ struct sdmm_mix {
     int rcpl = 2, rlps = 64;                 // responsibility E-step layout (same Kp)
     int rtile = 0;                           // 1: estep_resp_tile_kernel (64 < K <= 128)
                                              // 2: estep_resp_mfma_kernel (every K)
-    int rvariant = 0;                        // tile kernel scheduling variant (SDMM_RESP_VARIANT)
+    int rvariant = 4;                        // tile kernel variant (SDMM_RESP_VARIANT): KT=8, 3 waves/SIMD
     int stile = 0;                           // 1: estep_stats_tile_kernel (64 < K <= 128)
     int svariant = 0;                        // its occupancy variant (SDMM_STATS_VARIANT)
     int device = 0;
@@ -502,7 +503,7 @@ const char* sdmm_kernel_name(const sdmm_mix* m, int which) {
             std::snprintf(buf, sizeof buf, "%s", estep_resp_mfma_name(m->rvariant, m->Kp));
             return buf;
         } else if (m->rtile) {
-            std::snprintf(buf, sizeof buf, "estep_resp_tile_kernel<4,%d>", m->rvariant == 1 ? 4 : m->rvariant == 2 ? 16 : 2);
+            std::snprintf(buf, sizeof buf, "%s", estep_resp_tile_name(m->rvariant));
             return buf;
         }
         std::snprintf(buf, sizeof buf, "estep_resp_kernel<%d,%d>", m->rcpl, m->rlps);

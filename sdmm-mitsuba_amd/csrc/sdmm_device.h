@@ -30,8 +30,14 @@ enum : int {
     //   u4 = L40 tp0 + L41 tp1 + L42 tp2 + a (B . d),  B = L43 R0 + L44 R1
     //   pi pdf = NORM5 exp(-q/2) * a * (detInv pi)
     EP_A0, EP_A1, EP_A2, EP_B0, EP_B1, EP_B2, EP_DIPI,
+    // origin-shifted spatial rows for the responsibility kernel:
+    //   u_m = sum_j L_mj (p_j - o) + NC_m,  NC_m = -sum_j L_mj (mu_j - o)  (fp64 -> f32)
+    // with o = kOrigin (the centre of the normalised scene box), so the
+    // subtraction p - mu costs nothing per pair
+    EP_NC0, EP_NC1, EP_NC2, EP_NC3, EP_NC4,
     EP_FIELDS
 };
+constexpr float kOrigin = 0.5f;
 
 // ---- guide record (per joint component) -------------------------------------
 enum : int {
