@@ -89,6 +89,45 @@ def cpu_baseline(batch, K, pos, nrm, synth, n_sample, threads):
             "single_thread": {"value": n1 / t1, "cores": 1, "sample": f"{n1} samples", "seconds": t1}}
 
 
+def leaf_em_bench(pkg, synth, batch, n_local, shard, dev, stream, args, timed, world,
+                  K=16, leaf_samples=4096):
+    """One batched EM step over n_local / leaf_samples leaves of K components
+    (sdmm_em_step_batched), against the same leaves stepped one call each."""
+    n_leaves = n_local // leaf_samples
+    seg = np.arange(n_leaves + 1, dtype=np.int64) * leaf_samples
+    x = np.stack([t.cpu().numpy() for t in shard.x])
+    nrm = np.ascontiguousarray(x[3:6].T)    # seed "normals": any unit vectors (directions)
+    n_pos = K // 8
+
+    def make():
+        mixes = []
+        for i in range(n_leaves):
+            a = int(seg[i])
+            m = pkg.SDMM(K, device=dev.index, stream=stream)
+            m.init_hemisphere(x[0:3, a:a + n_pos].T.copy(), nrm[a:a + n_pos].copy(), synth.DEPTH_PRIOR,
+                              synth.SPATIAL_DISTANCE, synth.SEED_MODEL + i)
+            mixes.append(m)
+        return mixes
+
+    mixes = make()
+    leaves = [pkg.DeviceSamples([t[int(seg[i]):int(seg[i + 1])] for t in shard.x],
+                                shard.w[int(seg[i]):int(seg[i + 1])]) for i in range(n_leaves)]
+    pkg.em_step_batched(mixes, shard, seg, 1)          # warm-up (tables, partial rows)
+    steps = max(3, args.steps // 4)
+    b_wall, b_kern = timed(lambda: pkg.em_step_batched(mixes, shard, seg, 1), steps)
+
+    def sequential():
+        for m, leaf in zip(mixes, leaves):
+            m.optimize(leaf)
+    sequential()
+    s_wall, _ = timed(sequential, 2, events=False)
+    n_all = n_leaves * leaf_samples * world
+    return {"samples_per_s": n_all / (b_wall / steps), "ms_per_step": b_wall / steps * 1e3,
+            "device_ms_per_step": b_kern * 1e3, "leaves": n_leaves * world, "K": K,
+            "samples_per_leaf": leaf_samples, "scaling": "weak (leaves sharded, no exchange)",
+            "sequential_per_leaf_calls_ms": s_wall / 2 * 1e3}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -157,15 +196,19 @@ def main():
         torch.cuda.synchronize()
 
     def timed(fn, steps, events=True):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * steps)] if events else None
+        """Wall time of `steps` calls (barrier + synchronize on both sides, max
+        over ranks) and, with events, the average device time per call from ONE
+        pair of HIP events on the kernels' stream around the whole run (per-call
+        event pairs would add their own marker cost to every launch)."""
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if events else None
         barrier()
         t = time.perf_counter()
-        for i in range(steps):
-            if events:
-                ev[2 * i].record(stream)
+        if events:
+            ev[0].record(stream)
+        for _ in range(steps):
             fn()
-            if events:
-                ev[2 * i + 1].record(stream)
+        if events:
+            ev[1].record(stream)
         barrier()
         wall = time.perf_counter() - t
         wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
@@ -174,7 +217,7 @@ def main():
         kern = None
         if events:
             torch.cuda.synchronize()
-            kern = float(np.mean([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(steps)])) * 1e-3
+            kern = ev[0].elapsed_time(ev[1]) * 1e-3 / steps
         return float(wall_t.item()), kern
 
     # ---- headline: responsibility E-step --------------------------------
@@ -212,11 +255,14 @@ def main():
                      "bytes_per_launch": bytes_per_launch, "kernel_us": kern * 1e6,
                      "fp32_frac": flops_per_launch / kern / FP32_PEAK},
     }
+    # HBM traffic per launch from the committed rocprofv3 PMC summary of THIS
+    # kernel (tools/gpu_pmc.sh + tools/pmc_summary.py), if it matches
     pmc = ROOT / "profiles" / "round1_pmc_estep.json"
     if pmc.exists() and world == 1:
         try:
             pm = json.loads(pmc.read_text())
-            if pm.get("K") == K and pm.get("N") == N:
+            same = pm.get("kernel", "").replace(" ", "") == mix.kernel_name("resp").replace(" ", "")
+            if pm.get("K") == K and pm.get("N") == N and same:
                 out["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
         except Exception:
             pass
@@ -242,6 +288,10 @@ def main():
         out["guide"] = {"queries_per_s": q_local * world / (g_wall / g_steps), "Q": q_local * world,
                         "ms_per_step": g_wall / g_steps * 1e3, "bytes_per_query": 48,
                         "kernel_us": g_kern * 1e6}
+        # ---- batched per-leaf EM: the plugin's tree leaves,
+        # each its own K=16 mixture over its own samples (volpath_sdmm.cpp:287-311);
+        # leaves shard across ranks with no exchange (weak scaling per rank) ----
+        out["leaf_em"] = leaf_em_bench(pkg, synth, batch, n_local, shard, dev, stream, args, timed, world)
 
     if rank == 0 and world == 1 and not args.no_cpu:
         try:

@@ -14,6 +14,10 @@
  *                                 + sdmm::prepare   (volpath_sdmm.cpp:237, :307);
  *                                 math: jmm StepwiseTangentEM::optimize
  *                                 (dmm/jmm/opt/stepwise_tangent.h:597-1053)
+ *   sdmm_em_step_batched          the plugin's per-leaf optimisation loop: one
+ *                                 sdmm::em_step per tree leaf, run on a thread
+ *                                 pool (volpath_sdmm.cpp:244-312, leaf filter
+ *                                 :140-149), as ONE batched device launch
  *   sdmm_estep_stats/sdmm_mstep   the same EM step split around the
  *                                 sufficient-statistics all-reduce (multi-GPU)
  *   sdmm_responsibilities         MixtureModel::posteriorAndLog over a batch
@@ -118,6 +122,18 @@ int sdmm_hemisphere_init_host(const float* positions, const float* normals, int 
 int sdmm_em_step(sdmm_mix* m, const sdmm_samples* device_samples, int iterations);
 /* Same with host-resident samples (staged through the handle's buffers). */
 int sdmm_em_step_host(sdmm_mix* m, const sdmm_samples* host_samples, int iterations);
+
+/* Batched per-leaf EM (the spatial tree's leaves, each its own mixture):
+ * mixes[i] takes one stepwise EM iteration (`iterations` times) over samples
+ * [seg[i], seg[i+1]) of the device planes `device_samples` (the leaves' data
+ * stored back to back).  seg: host, n_mix + 1 non-decreasing offsets within
+ * [0, device_samples->n]; a leaf with no samples is left unchanged (like
+ * sdmm_em_step with n = 0).  All handles must share K and the device and be
+ * distinct; the work runs on mixes[0]'s stream (the other handles' streams
+ * are synchronised on entry and wait for the batch on exit).  Results are
+ * bitwise those of sdmm_em_step(mixes[i], leaf i) called one by one. */
+int sdmm_em_step_batched(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* device_samples,
+                         const int64_t* seg, int iterations);
 
 /* Split-phase EM step for sample-sharded multi-GPU runs:
  *   sdmm_estep_stats  writes this shard's fp64 sufficient statistics,

@@ -125,11 +125,26 @@ EXPORTED_SYMBOLS = [
     "sdmm_kernel_name",
     "sdmm_set_guide_capacity",
     "sdmm_set_stream", "sdmm_get_stream", "sdmm_synchronize", "sdmm_init_hemisphere",
-    "sdmm_hemisphere_init_host", "sdmm_em_step", "sdmm_em_step_host", "sdmm_stats_len",
+    "sdmm_hemisphere_init_host", "sdmm_em_step", "sdmm_em_step_host", "sdmm_em_step_batched",
+    "sdmm_stats_len",
     "sdmm_estep_stats", "sdmm_mstep", "sdmm_responsibilities", "sdmm_guide_batch", "sdmm_pdf_batch",
     "sdmm_sample_discrete_cdf", "sdmm_get_params", "sdmm_set_params", "sdmm_get_state",
     "sdmm_set_state", "sdmm_last_error", "sdmm_abi_version",
 ]
+
+
+def em_step_batched(mixes, samples, seg, iterations: int = 1):
+    """Per-leaf EM of the plugin's optimisation loop (volpath_sdmm.cpp:287-311)
+    as one batched launch: mixes[i] takes `iterations` EM steps over samples
+    [seg[i], seg[i+1]) of `samples` (a DeviceSamples with the leaves stored
+    back to back).  Bitwise the same as mixes[i].optimize(leaf i) one by one.
+    Runs on mixes[0]'s stream."""
+    seg = np.ascontiguousarray(seg, np.int64)
+    n = len(mixes)
+    assert seg.shape == (n + 1,), "seg needs len(mixes) + 1 offsets"
+    hs = (C.c_void_p * max(n, 1))(*[m.h for m in mixes])
+    _check(lib().sdmm_em_step_batched(hs, n, samples.ptr, seg.ctypes.data_as(C.POINTER(C.c_int64)),
+                                      iterations))
 
 
 def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:

@@ -613,13 +613,37 @@ estep_resp_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s
     }
 }
 
+// Batched launches (sdmm_em_step_batched): workgroup b runs block items[b].y
+// of leaf items[b].x, i.e. exactly the workgroup of the single-mixture launch
+// over that leaf's samples, and writes its partial row at the leaf's rows.
+__device__ __forceinline__ SamplesDev shift_samples(SamplesDev s, int64_t s0) {
+    for (int i = 0; i < 6; ++i) s.x[i] += s0;
+    s.w += s0;
+    if (s.hpdf) s.hpdf += s0;
+    if (s.isDiffuse) s.isDiffuse += s0;
+    return s;
+}
+
 // ---------------------------------------------------------------------------
 // Fused E-step + sufficient statistics (calculateStats + sumWeights).
 // partial row layout: [f*Kp + k] for f < ST_FIELDS, then [21Kp] = H, [21Kp+1] = wsum.
 template <int CPL, int LPS>
 __global__ void __launch_bounds__(256)
 estep_stats_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, int64_t n,
-                   int64_t chunk, float* __restrict__ partials, int pstride) {
+                   int64_t chunk, float* __restrict__ partials, int pstride,
+                   const LeafDesc* __restrict__ leaves, const int2* __restrict__ items) {
+    int64_t bid = blockIdx.x;
+    float* prow = partials + bid * pstride;
+    if (leaves) {
+        const int2 it = items[blockIdx.x];
+        const LeafDesc& L = leaves[it.x];
+        ep = L.ep;
+        s = shift_samples(s, L.s0);
+        n = L.n;
+        chunk = L.chunk;
+        bid = it.y;
+        prow = partials + (int64_t)(L.row0 + it.y) * pstride;
+    }
     static_assert(CPL % 2 == 0, "components are processed in packed pairs");
     constexpr int SPW = 64 / LPS;
     constexpr int NP = CPL / 2;
@@ -629,7 +653,7 @@ estep_stats_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, in
     const int nw = blockDim.x >> 6;
     const int g = lane / LPS;
     const int j = lane % LPS;
-    const int64_t wave = (int64_t)blockIdx.x * nw + wid;
+    const int64_t wave = bid * nw + wid;
     const int64_t s0 = wave * chunk;
     const int64_t s1 = (s0 + chunk < n) ? s0 + chunk : n;  // s1 <= s0: no samples
 
@@ -743,8 +767,7 @@ estep_stats_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, in
         }
         __syncthreads();
     }
-    float* out = partials + (int64_t)blockIdx.x * pstride;
-    for (int idx = threadIdx.x; idx < rowlen; idx += blockDim.x) out[idx] = red[idx];
+    for (int idx = threadIdx.x; idx < rowlen; idx += blockDim.x) prow[idx] = red[idx];
 }
 
 // ---------------------------------------------------------------------------
@@ -804,14 +827,27 @@ __device__ __forceinline__ float transpose_sum4(const float (&v)[kStatTile], int
 template <int WPB, int OCC>
 __global__ void __launch_bounds__(64 * WPB, OCC)
 estep_stats_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, int64_t n,
-                        int64_t chunk, float* __restrict__ partials, int pstride) {
+                        int64_t chunk, float* __restrict__ partials, int pstride,
+                        const LeafDesc* __restrict__ leaves, const int2* __restrict__ items) {
+    int64_t bid = blockIdx.x;
+    float* prow = partials + bid * pstride;
+    if (leaves) {
+        const int2 it = items[blockIdx.x];
+        const LeafDesc& L = leaves[it.x];
+        ep = L.ep;
+        s = shift_samples(s, L.s0);
+        n = L.n;
+        chunk = L.chunk;
+        bid = it.y;
+        prow = partials + (int64_t)(L.row0 + it.y) * pstride;
+    }
     __shared__ float4 sblk[WPB][64][2];      // x0 x1 x2 x3 | x4 x5 hpdf diffuse
     __shared__ float sw[WPB][64];            // weight
     __shared__ float4 sg[WPB][kStatTile];    // {gamma scale, weight, threshold, -}
     extern __shared__ __attribute__((aligned(16))) float red[];
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t wave = (int64_t)blockIdx.x * WPB + wid;
+    const int64_t wave = bid * WPB + wid;
     const int64_t s0 = wave * chunk;
     const int64_t s1 = (s0 + chunk < n) ? s0 + chunk : n;   // s1 <= s0: no samples
 
@@ -965,8 +1001,7 @@ estep_stats_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
         }
         __syncthreads();
     }
-    float* out = partials + (int64_t)blockIdx.x * pstride;
-    for (int idx = threadIdx.x; idx < rowlen; idx += blockDim.x) out[idx] = red[idx];
+    for (int idx = threadIdx.x; idx < rowlen; idx += blockDim.x) prow[idx] = red[idx];
 }
 
 // ---------------------------------------------------------------------------
@@ -1049,6 +1084,67 @@ __global__ void finalize_stats_kernel(const float* __restrict__ ep, int Kp, int 
     for (int i = 0; i < 15; ++i) stats[2 + 6 * K + 15 * k + i] = C[i];
 }
 
+// Batched reduction + finalisation: thread (leaf blockIdx.y, component k)
+// reproduces, operation for operation, reduce_partials_slices_kernel (slices
+// of the leaf's rows, four row-interleaved fp64 partials per slice combined as
+// ((b0 + b1) + b2) + b3) followed by finalize_stats_kernel (slices summed in
+// order, then the un-centring), so a batched leaf's stats are bitwise those of
+// its single-mixture E-step.
+__device__ __forceinline__ double batched_col(const float* __restrict__ partials, int pstride, int row0, int rows,
+                                              int col) {
+    double t = 0.0;
+    for (int sl = 0; sl < kReduceSlices; ++sl) {
+        const int r0 = (int)((int64_t)rows * sl / kReduceSlices);
+        const int r1 = (int)((int64_t)rows * (sl + 1) / kReduceSlices);
+        double b[4];
+        for (int w = 0; w < 4; ++w) {
+            double sum = 0.0;
+            for (int r = r0 + w; r < r1; r += 4) sum += (double)partials[(int64_t)(row0 + r) * pstride + col];
+            b[w] = sum;
+        }
+        t += ((b[0] + b[1]) + b[2]) + b[3];
+    }
+    return t;
+}
+
+__global__ void __launch_bounds__(64)
+reduce_finalize_batched_kernel(const float* __restrict__ partials, int pstride, int Kp, int K,
+                               const LeafDesc* __restrict__ leaves) {
+    const LeafDesc& L = leaves[blockIdx.y];
+    if (L.n <= 0) return;
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    double* stats = L.stats;
+    auto col = [&](int o) { return batched_col(partials, pstride, L.row0, L.rows, partial_col(o, Kp, K)); };
+    if (k == 0) { stats[0] = col(0); stats[1] = col(1); }
+    if (k >= K) return;
+    const float* ep = L.ep;
+    const double mu[3] = {(double)ep[EP_MU0 * Kp + k], (double)ep[EP_MU1 * Kp + k], (double)ep[EP_MU2 * Kp + k]};
+    const double w = col(2 + k);
+    double M[5], C[15];
+    for (int i = 0; i < 5; ++i) M[i] = col(2 + K + 5 * k + i);
+    for (int i = 0; i < 15; ++i) C[i] = col(2 + 6 * K + 15 * k + i);
+    int e = 0;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j <= i; ++j, ++e)
+            C[e] += M[i] * mu[j] + mu[i] * M[j] + w * mu[i] * mu[j];
+    for (int j = 0; j < 3; ++j) {
+        C[6 + j] += M[3] * mu[j];
+        C[10 + j] += M[4] * mu[j];
+    }
+    for (int i = 0; i < 3; ++i) M[i] = M[i] + w * mu[i];
+    stats[2 + k] = w;
+    for (int i = 0; i < 5; ++i) stats[2 + K + 5 * k + i] = M[i];
+    for (int i = 0; i < 15; ++i) stats[2 + 6 * K + 15 * k + i] = C[i];
+}
+
+hipError_t launch_reduce_finalize_batched(const float* partials, int pstride, int Kp, int K,
+                                          const LeafDesc* leaves, int n_leaves, hipStream_t st) {
+    if (n_leaves <= 0) return hipSuccess;
+    hipLaunchKernelGGL(reduce_finalize_batched_kernel, dim3((K + 63) / 64, n_leaves), dim3(64), 0, st, partials,
+                       pstride, Kp, K, leaves);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // host-side launch helpers (called from sdmm_api.cpp)
 template <int CPL, int LPS>
@@ -1065,10 +1161,10 @@ static hipError_t launch_resp_t(const float* ep, int Kp, int K, const SamplesDev
 template <int CPL, int LPS>
 static hipError_t launch_stats_t(const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
                                  int64_t chunk, int blocks, int wpb, float* partials, int pstride,
-                                 hipStream_t st) {
+                                 hipStream_t st, const LeafDesc* leaves, const int2* items) {
     const size_t lds = sizeof(float) * (size_t)(ST_FIELDS * Kp + 2);
     hipLaunchKernelGGL((estep_stats_kernel<CPL, LPS>), dim3(blocks), dim3(64 * wpb), lds, st,
-                       ep, Kp, K, s, n, chunk, partials, pstride);
+                       ep, Kp, K, s, n, chunk, partials, pstride, leaves, items);
     return hipGetLastError();
 }
 
@@ -1127,15 +1223,16 @@ const char* estep_resp_tile_name(int variant) {
 // Tiled statistics kernel (64 < K <= 128, Kp == 128): `blocks` workgroups of 4
 // waves, chunk a multiple of 64 samples per wave; one partial row per block.
 hipError_t launch_estep_stats_tile(int variant, const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
-                                   int64_t chunk, int blocks, float* partials, int pstride, hipStream_t st) {
+                                   int64_t chunk, int blocks, float* partials, int pstride, hipStream_t st,
+                                   const LeafDesc* leaves, const int2* items) {
     if (Kp != 128 || K <= 64 || K > 128) return hipErrorInvalidValue;
     const size_t lds = sizeof(float) * (size_t)(ST_FIELDS * Kp + 2);
     if (variant == 1)
         hipLaunchKernelGGL((estep_stats_tile_kernel<4, 3>), dim3(blocks), dim3(256), lds, st, ep, Kp, K, s, n,
-                           chunk, partials, pstride);
+                           chunk, partials, pstride, leaves, items);
     else
         hipLaunchKernelGGL((estep_stats_tile_kernel<4, 2>), dim3(blocks), dim3(256), lds, st, ep, Kp, K, s, n,
-                           chunk, partials, pstride);
+                           chunk, partials, pstride, leaves, items);
     return hipGetLastError();
 }
 
@@ -1148,10 +1245,10 @@ hipError_t estep_stats_tile_occupancy(int variant, int Kp, int* blocks_per_cu) {
 
 hipError_t launch_estep_stats(int cpl, int lps, const float* ep, int Kp, int K, const SamplesDev& s,
                               int64_t n, int64_t chunk, int blocks, int wpb, float* partials,
-                              int pstride, hipStream_t st) {
+                              int pstride, hipStream_t st, const LeafDesc* leaves, const int2* items) {
 #define X(C, L)                                                                                    \
     if (cpl == C && lps == L)                                                                      \
-        return launch_stats_t<C, L>(ep, Kp, K, s, n, chunk, blocks, wpb, partials, pstride, st);
+        return launch_stats_t<C, L>(ep, Kp, K, s, n, chunk, blocks, wpb, partials, pstride, st, leaves, items);
     SDMM_LAYOUTS(X)
 #undef X
     return hipErrorInvalidValue;

@@ -241,10 +241,9 @@ pack_all_kernel(int K, int Kp, CanonDev C, float* ep, float* gp, float norm5) {
 
 // ---------------------------------------------------------------------------
 // One stepwise M-step from the compact fp64 stats [H, wsum, W, M, Clow].
-__global__ void __launch_bounds__(512)
-mstep_kernel(int K, int Kp, const double* __restrict__ stats, int64_t nSamples, CanonDev C,
-             EmStateDev S, float* ep, float* gp, float norm5, double* __restrict__ wmean,
-             double* __restrict__ wcov) {
+__device__ __forceinline__ void mstep_body(int K, int Kp, const double* __restrict__ stats, int64_t nSamples,
+                                           CanonDev C, EmStateDev S, float* ep, float* gp, float norm5,
+                                           double* __restrict__ wmean, double* __restrict__ wcov) {
     // Two phases so the fp64 register footprint of the M-step and of MVTN::set
     // never overlap (one phase alone fits the VGPR file, both spilled):
     //   1. blend, MAP update, PD test, stats re-centring; the accepted (mean,
@@ -401,6 +400,21 @@ mstep_kernel(int K, int Kp, const double* __restrict__ stats, int64_t nSamples, 
     for (int kk = t; kk < Kp; kk += blockDim.x) pack_component(kk, K, Kp, C, ep, gp, norm5);
 }
 
+__global__ void __launch_bounds__(512)
+mstep_kernel(int K, int Kp, const double* __restrict__ stats, int64_t nSamples, CanonDev C,
+             EmStateDev S, float* ep, float* gp, float norm5, double* __restrict__ wmean,
+             double* __restrict__ wcov) {
+    mstep_body(K, Kp, stats, nSamples, C, S, ep, gp, norm5, wmean, wcov);
+}
+
+// Batched M-step: workgroup b updates mixture b of the table (per-leaf EM).
+__global__ void __launch_bounds__(512)
+mstep_batched_kernel(int K, int Kp, const MixDesc* __restrict__ mixes, float norm5) {
+    const MixDesc& d = mixes[blockIdx.x];
+    if (d.n <= 0) return;   // no samples: optimize() returns early (weightSum == 0)
+    mstep_body(K, Kp, d.stats, d.n, d.C, d.S, d.ep, d.gp, norm5, d.wmean, d.wcov);
+}
+
 // ---------------------------------------------------------------------------
 hipError_t launch_set_all(int K, int Kp, const double* mean, const double* cov, const CanonDev& C,
                           float* ep, float* gp, float norm5, hipStream_t st) {
@@ -421,6 +435,14 @@ hipError_t launch_mstep(int K, int Kp, const double* stats, int64_t nSamples, co
     const int threads = Kp < 64 ? 64 : (Kp > 512 ? 512 : Kp);
     hipLaunchKernelGGL(mstep_kernel, dim3(1), dim3(threads), (sizeof(double) + sizeof(int)) * (size_t)K, st, K,
                        Kp, stats, nSamples, C, S, ep, gp, norm5, wmean, wcov);
+    return hipGetLastError();
+}
+
+hipError_t launch_mstep_batched(int K, int Kp, const MixDesc* mixes, int n_mix, float norm5, hipStream_t st) {
+    if (n_mix <= 0) return hipSuccess;
+    const int threads = Kp < 64 ? 64 : (Kp > 512 ? 512 : Kp);
+    hipLaunchKernelGGL(mstep_batched_kernel, dim3(n_mix), dim3(threads), (sizeof(double) + sizeof(int)) * (size_t)K,
+                       st, K, Kp, mixes, norm5);
     return hipGetLastError();
 }
 

@@ -13,6 +13,7 @@
 #include <new>
 #include <string>
 #include <vector>
+#include <algorithm>
 
 #include "../../include/sdmm_gpu.h"
 #include "sdmm_device.h"
@@ -24,7 +25,11 @@ hipError_t launch_estep_resp(int cpl, int lps, const float* ep, int Kp, int K, c
                              int64_t n, int64_t chunk, float* resp, hipStream_t st);
 hipError_t launch_estep_stats(int cpl, int lps, const float* ep, int Kp, int K, const SamplesDev& s,
                               int64_t n, int64_t chunk, int blocks, int wpb, float* partials,
-                              int pstride, hipStream_t st);
+                              int pstride, hipStream_t st, const LeafDesc* leaves = nullptr,
+                              const int2* items = nullptr);
+hipError_t launch_reduce_finalize_batched(const float* partials, int pstride, int Kp, int K,
+                                          const LeafDesc* leaves, int n_leaves, hipStream_t st);
+hipError_t launch_mstep_batched(int K, int Kp, const MixDesc* mixes, int n_mix, float norm5, hipStream_t st);
 hipError_t estep_occupancy(int cpl, int lps, int Kp, int* resp_blocks, int* stats_blocks);
 hipError_t launch_estep_resp_tile(int variant, const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
                                   int64_t chunk, float* resp, hipStream_t st);
@@ -35,7 +40,8 @@ hipError_t launch_estep_resp_mfma(int variant, const float* ep, int Kp, int K, c
 hipError_t estep_resp_mfma_occupancy(int variant, int Kp, int* blocks_per_cu);
 const char* estep_resp_mfma_name(int variant, int Kp);
 hipError_t launch_estep_stats_tile(int variant, const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
-                                   int64_t chunk, int blocks, float* partials, int pstride, hipStream_t st);
+                                   int64_t chunk, int blocks, float* partials, int pstride, hipStream_t st,
+                                   const LeafDesc* leaves = nullptr, const int2* items = nullptr);
 hipError_t estep_stats_tile_occupancy(int variant, int Kp, int* blocks_per_cu);
 hipError_t launch_reduce_partials(const float* partials, int rows, int pstride, const float* ep_for_finalize,
                                   int Kp, int K, double* stats, double* scratch, hipStream_t st);
@@ -216,6 +222,12 @@ struct sdmm_mix {
     // staging for host-resident samples
     void* staging = nullptr;
     size_t staging_bytes = 0;
+    // batched per-leaf EM tables (this handle as mixes[0]): device + pinned host
+    void* batch_dev = nullptr;
+    void* batch_host = nullptr;
+    size_t batch_bytes = 0;
+    hipEvent_t batch_copied = nullptr;   // the last table upload has completed
+    hipEvent_t batch_done = nullptr;     // the last batch's kernels have completed
 };
 
 namespace {
@@ -297,31 +309,43 @@ int ensure_guide_scratch(const sdmm_mix* m, int64_t nq) {
     return SDMM_OK;
 }
 
-int run_estep_stats(sdmm_mix* m, const sdmm_samples* s, double* stats_out) {
-    SamplesDev d = to_dev(s);
+// Work split of m's statistics E-step over n samples (the same for a
+// single-mixture call and for that mixture as a leaf of a batched call).
+struct StatsPlan {
+    int64_t chunk;
+    int blocks;
+};
+StatsPlan stats_plan(const sdmm_mix* m, int64_t n) {
     if (m->stile) {
         // one round of resident waves, each a whole number of 64-sample blocks
         const int64_t resident = (int64_t)m->cus * 4 * (m->stats_blocks > 0 ? m->stats_blocks : 1);
-        int64_t chunk = (s->n + resident - 1) / resident;
+        int64_t chunk = (n + resident - 1) / resident;
         chunk = ((chunk + 63) / 64) * 64;
         if (chunk < 64) chunk = 64;
-        const int64_t waves = (s->n + chunk - 1) / chunk;
-        const int blocks = (int)((waves + 3) / 4 > 0 ? (waves + 3) / 4 : 1);
-        int r = ensure_partials(m, blocks);
-        if (r) return r;
-        HIP_TRY(launch_estep_stats_tile(m->svariant, m->ep, m->Kp, m->K, d, s->n, chunk, blocks, m->partials,
-                                        m->pstride, m->stream));
-        HIP_TRY(launch_reduce_partials(m->partials, blocks, m->pstride, m->ep, m->Kp, m->K, stats_out,
-                                       m->rscratch, m->stream));
-        return SDMM_OK;
+        const int64_t waves = (n + chunk - 1) / chunk;
+        return StatsPlan{chunk, (int)((waves + 3) / 4 > 0 ? (waves + 3) / 4 : 1)};
     }
-    const Split sp = split_for(m, s->n, m->lps, m->stats_blocks);
-    int r = ensure_partials(m, sp.blocks);
+    const Split sp = split_for(m, n, m->lps, m->stats_blocks);
+    return StatsPlan{sp.chunk, sp.blocks};
+}
+
+hipError_t launch_stats_kernel(const sdmm_mix* m, const SamplesDev& d, int64_t n, const StatsPlan& p, int blocks,
+                               float* partials, hipStream_t st, const LeafDesc* leaves, const int2* items) {
+    if (m->stile)
+        return launch_estep_stats_tile(m->svariant, m->ep, m->Kp, m->K, d, n, p.chunk, blocks, partials, m->pstride,
+                                       st, leaves, items);
+    return launch_estep_stats(m->cpl, m->lps, m->ep, m->Kp, m->K, d, n, p.chunk, blocks, 4, partials, m->pstride,
+                              st, leaves, items);
+}
+
+int run_estep_stats(sdmm_mix* m, const sdmm_samples* s, double* stats_out) {
+    SamplesDev d = to_dev(s);
+    const StatsPlan p = stats_plan(m, s->n);
+    int r = ensure_partials(m, p.blocks);
     if (r) return r;
-    HIP_TRY(launch_estep_stats(m->cpl, m->lps, m->ep, m->Kp, m->K, d, s->n, sp.chunk, sp.blocks, sp.wpb,
-                               m->partials, m->pstride, m->stream));
-    HIP_TRY(launch_reduce_partials(m->partials, sp.blocks, m->pstride, m->ep, m->Kp, m->K, stats_out,
-                                   m->rscratch, m->stream));
+    HIP_TRY(launch_stats_kernel(m, d, s->n, p, p.blocks, m->partials, m->stream, nullptr, nullptr));
+    HIP_TRY(launch_reduce_partials(m->partials, p.blocks, m->pstride, m->ep, m->Kp, m->K, stats_out, m->rscratch,
+                                   m->stream));
     return SDMM_OK;
 }
 
@@ -473,6 +497,10 @@ void sdmm_destroy(sdmm_mix* m) {
     if (m->partials) (void)hipFree(m->partials);
     if (m->guide_fb) (void)hipFree(m->guide_fb);
     if (m->staging) (void)hipFree(m->staging);
+    if (m->batch_dev) (void)hipFree(m->batch_dev);
+    if (m->batch_host) (void)hipHostFree(m->batch_host);
+    if (m->batch_copied) (void)hipEventDestroy(m->batch_copied);
+    if (m->batch_done) (void)hipEventDestroy(m->batch_done);
     if (m->own_stream) (void)hipStreamDestroy(m->own_stream);
     delete m;
 }
@@ -605,6 +633,97 @@ int sdmm_em_step(sdmm_mix* m, const sdmm_samples* s, int iterations) {
         HIP_TRY(launch_mstep(m->K, m->Kp, m->stats, s->n, m->C, m->S, m->ep, m->gp, m->norm5, m->tmp_mean,
                              m->tmp_cov, m->stream));
     }
+    return SDMM_OK;
+}
+
+int sdmm_em_step_batched(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* s, const int64_t* seg,
+                         int iterations) {
+    if (n_mix < 0 || (n_mix > 0 && (!mixes || !seg))) return fail(SDMM_E_INVALID, "invalid argument");
+    if (n_mix == 0) return SDMM_OK;
+    int r = check_samples(s);
+    if (r) return r;
+    sdmm_mix* m0 = mixes[0];
+    if (!m0) return fail(SDMM_E_INVALID, "mixes[0] is NULL");
+    if (seg[0] < 0 || seg[n_mix] > s->n) return fail(SDMM_E_INVALID, "segment offsets outside the sample batch");
+    std::vector<const sdmm_mix*> seen;
+    seen.reserve((size_t)n_mix);
+    for (int i = 0; i < n_mix; ++i) {
+        const sdmm_mix* m = mixes[i];
+        if (!m) return fail(SDMM_E_INVALID, "NULL handle in mixes");
+        if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
+        if (m->K != m0->K || m->device != m0->device)
+            return fail(SDMM_E_INVALID, "batched mixtures must share K and the device");
+        if (seg[i + 1] < seg[i]) return fail(SDMM_E_INVALID, "segment offsets must be non-decreasing");
+        seen.push_back(m);
+    }
+    std::sort(seen.begin(), seen.end());
+    if (std::adjacent_find(seen.begin(), seen.end()) != seen.end())
+        return fail(SDMM_E_INVALID, "a handle appears twice in mixes");
+    if (iterations <= 0 || seg[n_mix] == seg[0]) return SDMM_OK;
+    HIP_TRY(hipSetDevice(m0->device));
+    const hipStream_t st = m0->stream;
+    for (int i = 1; i < n_mix; ++i)
+        if (mixes[i]->stream != st) HIP_TRY(hipStreamSynchronize(mixes[i]->stream));
+
+    // tables: leaves, M-step operands, (leaf, block) work items
+    std::vector<StatsPlan> plans((size_t)n_mix);
+    int64_t rows = 0;
+    for (int i = 0; i < n_mix; ++i) {
+        const int64_t n = seg[i + 1] - seg[i];
+        plans[(size_t)i] = n > 0 ? stats_plan(mixes[i], n) : StatsPlan{0, 0};
+        rows += plans[(size_t)i].blocks;
+    }
+    if (rows > (int64_t)1 << 30) return fail(SDMM_E_INVALID, "batch too large");
+    const size_t off_mix = ((sizeof(LeafDesc) * (size_t)n_mix + 255) / 256) * 256;
+    const size_t off_items = off_mix + ((sizeof(MixDesc) * (size_t)n_mix + 255) / 256) * 256;
+    const size_t need = off_items + sizeof(int2) * (size_t)rows;
+    if (!m0->batch_copied) {
+        HIP_TRY(hipEventCreateWithFlags(&m0->batch_copied, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&m0->batch_done, hipEventDisableTiming));
+    }
+    HIP_TRY(hipEventSynchronize(m0->batch_copied));   // the pinned tables are free again
+    if (need > m0->batch_bytes) {
+        HIP_TRY(hipStreamSynchronize(st));
+        if (m0->batch_dev) HIP_TRY(hipFree(m0->batch_dev));
+        if (m0->batch_host) HIP_TRY(hipHostFree(m0->batch_host));
+        m0->batch_dev = m0->batch_host = nullptr;
+        m0->batch_bytes = 0;
+        const size_t cap = need < (1u << 16) ? (1u << 16) : need + need / 2;
+        HIP_TRY(hipMalloc(&m0->batch_dev, cap));
+        HIP_TRY(hipHostMalloc(&m0->batch_host, cap, hipHostMallocDefault));
+        m0->batch_bytes = cap;
+    }
+    r = ensure_partials(m0, (int)(rows > 0 ? rows : 1));
+    if (r) return r;
+    char* hb = (char*)m0->batch_host;
+    char* db = (char*)m0->batch_dev;
+    LeafDesc* leaves = (LeafDesc*)hb;
+    MixDesc* mixd = (MixDesc*)(hb + off_mix);
+    int2* items = (int2*)(hb + off_items);
+    int row = 0;
+    for (int i = 0; i < n_mix; ++i) {
+        sdmm_mix* m = mixes[i];
+        const int64_t n = seg[i + 1] - seg[i];
+        leaves[i] = LeafDesc{m->ep, m->stats, seg[i], n, plans[(size_t)i].chunk, row, plans[(size_t)i].blocks};
+        mixd[i] = MixDesc{m->C, m->S, m->ep, m->gp, m->stats, m->tmp_mean, m->tmp_cov, n};
+        for (int b = 0; b < plans[(size_t)i].blocks; ++b) items[row + b] = int2{i, b};
+        row += plans[(size_t)i].blocks;
+    }
+    HIP_TRY(hipMemcpyAsync(db, hb, need, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipEventRecord(m0->batch_copied, st));
+    const LeafDesc* dleaves = (const LeafDesc*)db;
+    const MixDesc* dmix = (const MixDesc*)(db + off_mix);
+    const int2* ditems = (const int2*)(db + off_items);
+    const SamplesDev d = to_dev(s);
+    for (int it = 0; it < iterations; ++it) {
+        if (rows > 0)
+            HIP_TRY(launch_stats_kernel(m0, d, 0, StatsPlan{0, 0}, (int)rows, m0->partials, st, dleaves, ditems));
+        HIP_TRY(launch_reduce_finalize_batched(m0->partials, m0->pstride, m0->Kp, m0->K, dleaves, n_mix, st));
+        HIP_TRY(launch_mstep_batched(m0->K, m0->Kp, dmix, n_mix, m0->norm5, st));
+    }
+    HIP_TRY(hipEventRecord(m0->batch_done, st));
+    for (int i = 1; i < n_mix; ++i)
+        if (mixes[i]->stream != st) HIP_TRY(hipStreamWaitEvent(mixes[i]->stream, m0->batch_done, 0));
     return SDMM_OK;
 }
 

@@ -111,6 +111,30 @@ struct SamplesDev {
     const uint8_t* isDiffuse;   // nullable
 };
 
+// ---- batched per-leaf EM (sdmm_em_step_batched) ------------------------------
+// One leaf of the plugin's spatial tree = one mixture with its own contiguous
+// sample range of the batch planes (volpath_sdmm.cpp:287-311 runs em_step per
+// leaf).  The E-step of leaf i is the single-mixture launch (same chunking,
+// same partial rows) relocated to rows [row0, row0 + rows) of a shared buffer.
+struct LeafDesc {
+    const float* ep;   // E-step record of the leaf's mixture
+    double* stats;     // its compact stats [H, wsum, W, M, Clow]
+    int64_t s0, n;     // samples [s0, s0 + n) of the batch planes
+    int64_t chunk;     // samples per wave (the single-mixture split)
+    int row0, rows;    // its partial rows
+};
+// M-step operands of one mixture (mstep_batched_kernel: one workgroup each)
+struct MixDesc {
+    CanonDev C;
+    EmStateDev S;
+    float* ep;
+    float* gp;
+    const double* stats;
+    double* wmean;
+    double* wcov;
+    int64_t n;
+};
+
 constexpr float kHeuristicWeight = 0.5f;     // mixture_model.h:398
 constexpr double kPi = 3.14159265358979323846;
 
