@@ -78,18 +78,37 @@ __device__ __forceinline__ bool ts_exp_dir(const float to[9], float t0, float t1
     return true;
 }
 
+// IEEE float division x / d as (float)((double)x * RN64(1 / d)), bit for bit.
+// Why exact: write x / d = (A / B) 2^e with A, B < 2^24 integer significands.
+// A float rounding midpoint near it is N / 2^s with N odd of 25 bits; then
+// A / B - N / 2^s = (A 2^s - N B) / (B 2^s) with a NONZERO integer numerator
+// (N odd and > A cannot divide A 2^s), so the exact quotient is at least
+// 2^-49 / |A/B| ~ 2^-50 (relative) away from every midpoint, while the double
+// product is within 2^-52 of it (two roundings to 53 bits).  Rounding the
+// product to float therefore lands on the same float as rounding the exact
+// quotient; exact quotients stay exact.  (The usual "double rounding is
+// innocuous for >= 2p + 2 bits" argument, applied to a reciprocal product.)
+// Replaces the ~11-instruction v_div_scale/fmas/fixup expansion and its two
+// s_setreg denormal-mode switches per division.
+__device__ __forceinline__ float div_exact(float x, const float* gp, int f, int k) {
+    const uint32_t lo = __builtin_bit_cast(uint32_t, ((cfloat_p)gp)[k * GP_STRIDE + f]);
+    const uint32_t hi = __builtin_bit_cast(uint32_t, ((cfloat_p)gp)[k * GP_STRIDE + f + 1]);
+    const double r = __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
+    return (float)((double)x * r);
+}
+
 // MVN<3,3>::pdf with the forward substitution of LLT::matrixL().solve:
 // marginal_q is the squared Mahalanobis distance, marginal_pdf_q the pdf.
 __device__ __forceinline__ float marginal_q(const float* gp, int Kp, int k, const float c[3]) {
     float r0 = c[0] - gp_ld(gp, Kp, GP_MU0, k);
     float r1 = c[1] - gp_ld(gp, Kp, GP_MU1, k);
     float r2 = c[2] - gp_ld(gp, Kp, GP_MU2, k);
-    float s0 = r0 / gp_ld(gp, Kp, GP_ML00, k);
+    float s0 = div_exact(r0, gp, GP_RML00, k);   // r0 / ML00
     r1 = r1 - s0 * gp_ld(gp, Kp, GP_ML10, k);
     r2 = r2 - s0 * gp_ld(gp, Kp, GP_ML20, k);
-    float s1 = r1 / gp_ld(gp, Kp, GP_ML11, k);
+    float s1 = div_exact(r1, gp, GP_RML11, k);   // r1 / ML11
     r2 = r2 - s1 * gp_ld(gp, Kp, GP_ML21, k);
-    float s2 = r2 / gp_ld(gp, Kp, GP_ML22, k);
+    float s2 = div_exact(r2, gp, GP_RML22, k);   // r2 / ML22
     return s0 * s0 + s1 * s1 + s2 * s2;
 }
 __device__ __forceinline__ float marginal_pdf_q(const float* gp, int Kp, int k, float q, float norm3) {
@@ -257,29 +276,43 @@ struct CandSlots {
     __device__ bool valid(int i) const { return (ck[i * T + tid] >> 15) != 0; }
 };
 
-// returns lastIdx >= 0, or -1: needs the full-K fallback
+// returns lastIdx >= 0, or -1: needs the full-K fallback.
+//
+// ONE pass over the components: it forms totalMass exactly as the reference
+// (sequential float sum in component order, mixture_model.h:248-261) and, in
+// the same loop, keeps every LIVE component (weight > 0) in the LDS list
+// sorted (weight desc, index asc) by stable insertion, at most `cap` of them.
+// When the list is full a newcomer either displaces the last entry or is
+// dropped; `dropped` is the largest weight ever dropped.  Once totalMass (hence
+// tau) is known, the candidates are the list prefix with w >= tau -- the same
+// sequence the two-pass form built, provided no dropped weight reaches tau
+// (else: fallback).  tau > 0 whenever totalMass > 0, so a weight of exactly 0
+// (all components with q > kMarginalZeroQ, most of K) can never be a candidate
+// and never enters the list.  Validity of the conditionals is only evaluated
+// for the candidates.
 __device__ __forceinline__ int build_candidates(const float* gp, int Kp, int K, const float c[3], float* cw,
                                                 unsigned short* ck, int T, int tid, float norm3, int cap,
                                                 float& accum) {
     float total = 0.0f;
-    for (int k = 0; k < K; ++k) total += gp_ld(gp, Kp, GP_W, k) * marginal_pdf(gp, Kp, k, c, norm3);
-    if (!__builtin_isfinite(total)) return -1;
-    const float cutoff = (float)(0.99 * (double)total);
-    const double tau = ((double)total - (double)cutoff) / (double)K * 0.999;
+    float dropped = 0.0f;
     int cnt = 0;
-    bool over = false;
     for (int k = 0; k < K; ++k) {
-        // pre-screen with the float exp (relative error ~1e-6): a weight more than
-        // 1e-3 below tau cannot reach it, and skips the double exp
-        const float q = marginal_q(gp, Kp, k, c);
-        const float pik = gp_ld(gp, Kp, GP_W, k);
-        const float wfast = pik * gp_ld(gp, Kp, GP_MDI, k) * norm3 * __expf(-0.5f * q);
-        if ((double)wfast * 1.001 < tau) continue;
-        const float w = pik * marginal_pdf_q(gp, Kp, k, q, norm3);
-        if (!((double)w >= tau)) continue;
-        if (cnt == cap) { over = true; continue; }
-        const unsigned short key = (unsigned short)(k | (cond_valid(gp, Kp, k, c) ? 0x8000 : 0));
-        // stable insertion (descending): equal weights keep index order
+        const float w = gp_ld(gp, Kp, GP_W, k) * marginal_pdf_q(gp, Kp, k, marginal_q(gp, Kp, k, c), norm3);
+        total += w;
+        // the float sum of non-negative terms never decreases, so the final
+        // tau >= (0.01 total - ulp) 0.999 / K > 0.009 total_so_far / K: a weight
+        // below that is neither a candidate nor a dropped weight that matters
+        if (!(w > 0.0f) || (double)w < 0.009 * (double)total / (double)K) continue;
+        if (cnt == cap) {
+            // full: w joins only if it sorts before the last entry (ties keep
+            // the lower index, which arrived first)
+            if (cap == 0 || !(w > cw[(cap - 1) * T + tid])) {
+                dropped = fmaxf(dropped, w);
+                continue;
+            }
+            dropped = fmaxf(dropped, cw[(cap - 1) * T + tid]);
+            --cnt;
+        }
         int pos = cnt;
         while (pos > 0 && cw[(pos - 1) * T + tid] < w) {
             cw[pos * T + tid] = cw[(pos - 1) * T + tid];
@@ -287,18 +320,25 @@ __device__ __forceinline__ int build_candidates(const float* gp, int Kp, int K, 
             --pos;
         }
         cw[pos * T + tid] = w;
-        ck[pos * T + tid] = key;
+        ck[pos * T + tid] = (unsigned short)k;
         ++cnt;
     }
-    if (over) return -1;
+    if (!__builtin_isfinite(total)) return -1;
+    const float cutoff = (float)(0.99 * (double)total);
+    const double tau = ((double)total - (double)cutoff) / (double)K * 0.999;
+    if (!(tau > 0.0) || (double)dropped >= tau) return -1;
+    int ncand = 0;
+    while (ncand < cnt && (double)cw[ncand * T + tid] >= tau) ++ncand;
     accum = 0.0f;
-    for (int i = 0; i < cnt; ++i) {
-        const float wi = (ck[i * T + tid] >> 15) ? cw[i * T + tid] : 0.0f;
-        accum += wi;
+    for (int i = 0; i < ncand; ++i) {
+        const int k = ck[i * T + tid];
+        const bool ok = cond_valid(gp, Kp, k, c);
+        ck[i * T + tid] = (unsigned short)(k | (ok ? 0x8000 : 0));
+        accum += ok ? cw[i * T + tid] : 0.0f;
         if (accum >= cutoff) return i + 1;
     }
-    // cutoff never reached inside the list: exact only if the list is all of K
-    return (cnt == K) ? K : -1;
+    // cutoff never reached inside the candidates: exact only if they are all of K
+    return (ncand == K) ? K : -1;
 }
 
 template <bool PDF_ONLY>

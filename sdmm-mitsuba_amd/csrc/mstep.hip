@@ -200,6 +200,13 @@ __device__ static void pack_component(int k, int K, int Kp, const CanonDev& C, f
         g[GP_CL00] = C.condL[4 * k + 0]; g[GP_CL10] = C.condL[4 * k + 2]; g[GP_CL11] = C.condL[4 * k + 3];
         for (int i = 0; i < 4; ++i) g[GP_CI00 + i] = C.condLInv[4 * k + i];
         g[GP_CDI] = C.condDetInv[k];
+        const int rml[3] = {GP_RML00, GP_RML11, GP_RML22};
+        const float mld[3] = {g[GP_ML00], g[GP_ML11], g[GP_ML22]};
+        for (int i = 0; i < 3; ++i) {
+            const uint64_t bits = __builtin_bit_cast(uint64_t, 1.0 / (double)mld[i]);
+            g[rml[i]] = __builtin_bit_cast(float, (uint32_t)bits);
+            g[rml[i] + 1] = __builtin_bit_cast(float, (uint32_t)(bits >> 32));
+        }
     }
     for (int f = 0; f < EP_FIELDS; ++f) ep[f * Kp + k] = e[f];
     for (int f = 0; f < GP_FIELDS; ++f) gp[k * GP_STRIDE + f] = g[f];

@@ -50,12 +50,16 @@ enum : int {
     GP_CL00, GP_CL10, GP_CL11,           // conditional LLT (2x2 lower)
     GP_CI00, GP_CI01, GP_CI10, GP_CI11,  // conditional L^{-1}
     GP_CDI,                              // conditional detInv
-    GP_FIELDS
+    // RN64(1 / ML_ii) as doubles (two float slots each, 8-byte aligned): the
+    // float division r / ML_ii of the marginal's triangular solve is exactly
+    // (float)((double) r * RN64(1 / ML_ii)) -- see div_exact in guide.hip
+    GP_RML00 = 34, GP_RML11 = 36, GP_RML22 = 38,
+    GP_FIELDS = 40
 };
 // The guide record is AoS, gp[k * GP_STRIDE + f]: a query thread walks the
 // components in order with wave-uniform k, so one component's fields come in
 // a few wide scalar loads (s_load_dwordx8/x16) instead of one load per field.
-constexpr int GP_STRIDE = 36;
+constexpr int GP_STRIDE = 40;
 static_assert(GP_FIELDS <= GP_STRIDE, "guide record stride");
 
 // Per-component sufficient statistics accumulated by the E-step.

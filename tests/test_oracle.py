@@ -267,3 +267,23 @@ def test_pd_check(oracle):
     S = np.eye(5)
     S[0, 4] = 100.0
     assert oracle.is_pd(S)
+
+
+def test_float_division_by_double_reciprocal_is_exact():
+    """The guide kernel's div_exact (guide.hip): IEEE float x / d equals
+    (float)((double)x * RN64(1 / d)) -- checked here on 4M pairs, including
+    divisors whose significands are all ones / powers of two and quotients that
+    are exact, near overflow of the significand, or tiny."""
+    rng = np.random.default_rng(11)
+    n = 1 << 22
+    x = (rng.standard_normal(n) * np.exp(rng.uniform(-20, 20, n))).astype(np.float32)
+    d = np.abs(rng.standard_normal(n) * np.exp(rng.uniform(-10, 10, n))).astype(np.float32) + np.float32(1e-30)
+    special = np.array([1.0, 2.0, 0.5, np.nextafter(np.float32(2), np.float32(0)), np.float32(1.9999999),
+                        np.float32(3.0), np.float32(0.1), np.float32(7.0)], np.float32)
+    d[:special.size * 1000] = np.repeat(special, 1000)
+    x[:4000] = (d[:4000] * np.float32(3)).astype(np.float32)          # exact quotients
+    with np.errstate(over="ignore", under="ignore"):
+        ref = x / d
+        got = (x.astype(np.float64) * (1.0 / d.astype(np.float64))).astype(np.float32)
+    ok = np.isfinite(ref) & (np.abs(ref) >= np.finfo(np.float32).tiny)
+    np.testing.assert_array_equal(got[ok], ref[ok])
