@@ -134,6 +134,10 @@ int sdmm_em_step_host(sdmm_mix* m, const sdmm_samples* host_samples, int iterati
  * bitwise those of sdmm_em_step(mixes[i], leaf i) called one by one. */
 int sdmm_em_step_batched(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* device_samples,
                          const int64_t* seg, int iterations);
+/* Same with host-resident planes (staged through mixes[0]'s buffers; returns
+ * after the batch, so the host planes may be reused). */
+int sdmm_em_step_batched_host(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* host_samples,
+                              const int64_t* seg, int iterations);
 
 /* Split-phase EM step for sample-sharded multi-GPU runs:
  *   sdmm_estep_stats  writes this shard's fp64 sufficient statistics,

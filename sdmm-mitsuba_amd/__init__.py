@@ -126,6 +126,7 @@ EXPORTED_SYMBOLS = [
     "sdmm_set_guide_capacity",
     "sdmm_set_stream", "sdmm_get_stream", "sdmm_synchronize", "sdmm_init_hemisphere",
     "sdmm_hemisphere_init_host", "sdmm_em_step", "sdmm_em_step_host", "sdmm_em_step_batched",
+    "sdmm_em_step_batched_host",
     "sdmm_stats_len",
     "sdmm_estep_stats", "sdmm_mstep", "sdmm_responsibilities", "sdmm_guide_batch", "sdmm_pdf_batch",
     "sdmm_sample_discrete_cdf", "sdmm_get_params", "sdmm_set_params", "sdmm_get_state",

@@ -727,6 +727,55 @@ int sdmm_em_step_batched(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* 
     return SDMM_OK;
 }
 
+// Stage host sample planes into m's staging buffer (device SoA view in *d).
+static int stage_host_samples(sdmm_mix* m, const sdmm_samples* s, sdmm_samples* d) {
+    const size_t n = (size_t)s->n;
+    const size_t need = n * (7 * 4 + 4 + 1) + 64;
+    if (need > m->staging_bytes) {
+        HIP_TRY(hipStreamSynchronize(m->stream));
+        if (m->staging) HIP_TRY(hipFree(m->staging));
+        m->staging = nullptr;
+        HIP_TRY(hipMalloc(&m->staging, need));
+        m->staging_bytes = need;
+    }
+    float* f = (float*)m->staging;
+    *d = sdmm_samples{};
+    for (int i = 0; i < 6; ++i) {
+        HIP_TRY(hipMemcpyAsync(f + i * n, s->x[i], 4 * n, hipMemcpyHostToDevice, m->stream));
+        d->x[i] = f + i * n;
+    }
+    HIP_TRY(hipMemcpyAsync(f + 6 * n, s->w, 4 * n, hipMemcpyHostToDevice, m->stream));
+    d->w = f + 6 * n;
+    if (s->hpdf) {
+        HIP_TRY(hipMemcpyAsync(f + 7 * n, s->hpdf, 4 * n, hipMemcpyHostToDevice, m->stream));
+        d->hpdf = f + 7 * n;
+    }
+    if (s->is_diffuse) {
+        HIP_TRY(hipMemcpyAsync(f + 8 * n, s->is_diffuse, n, hipMemcpyHostToDevice, m->stream));
+        d->is_diffuse = (const uint8_t*)(f + 8 * n);
+    }
+    d->n = s->n;
+    return SDMM_OK;
+}
+
+int sdmm_em_step_batched_host(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* s, const int64_t* seg,
+                              int iterations) {
+    if (n_mix < 0 || (n_mix > 0 && (!mixes || !mixes[0]))) return fail(SDMM_E_INVALID, "invalid argument");
+    if (n_mix == 0) return SDMM_OK;
+    int r = check_samples(s);
+    if (r) return r;
+    if (s->n == 0) return sdmm_em_step_batched(mixes, n_mix, s, seg, iterations);
+    sdmm_mix* m0 = mixes[0];
+    HIP_TRY(hipSetDevice(m0->device));
+    sdmm_samples d;
+    r = stage_host_samples(m0, s, &d);
+    if (r) return r;
+    r = sdmm_em_step_batched(mixes, n_mix, &d, seg, iterations);
+    if (r) return r;
+    HIP_TRY(hipStreamSynchronize(m0->stream));  // the host planes may be reused on return
+    return SDMM_OK;
+}
+
 int sdmm_em_step_host(sdmm_mix* m, const sdmm_samples* s, int iterations) {
     if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
     int r = check_samples(s);

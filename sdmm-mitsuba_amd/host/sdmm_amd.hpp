@@ -70,6 +70,7 @@ public:
         return s;
     }
     const float* normals() const { return nrm_.data(); }
+    const float* weights() const { return w_.data(); }
     const std::vector<float>& plane(int i) const { return x_[i]; }
 
 private:
@@ -133,6 +134,43 @@ public:
 private:
     sdmm_mix* h_ = nullptr;
 };
+
+// The plugin's per-leaf optimisation loop (volpath_sdmm.cpp:287-311: one
+// sdmm::em_step per tree leaf on a tev::ThreadPool) as one batched launch:
+// leaves[i] takes `iterations` EM steps over samples [seg[i], seg[i+1]) of the
+// device planes `device_samples` (the leaves' training data back to back).
+// Bitwise the same as leaves[i]->em_step_device(leaf i) one by one.
+inline void em_step_leaves(const std::vector<Mixture*>& leaves, const sdmm_samples& device_samples,
+                           const std::vector<int64_t>& seg, int iterations = 1) {
+    if (seg.size() != leaves.size() + 1) throw Error(SDMM_E_INVALID, "em_step_leaves: seg needs leaves + 1 offsets");
+    std::vector<sdmm_mix*> h(leaves.size());
+    for (size_t i = 0; i < leaves.size(); ++i) h[i] = leaves[i]->handle();
+    check(sdmm_em_step_batched(h.data(), (int)h.size(), &device_samples, seg.data(), iterations),
+          "sdmm_em_step_batched");
+}
+// ... on host-resident training data: the leaves' TrainingData concatenated.
+inline void em_step_leaves(const std::vector<Mixture*>& leaves, const std::vector<const TrainingData*>& data,
+                           int iterations = 1) {
+    if (data.size() != leaves.size()) throw Error(SDMM_E_INVALID, "em_step_leaves: one TrainingData per leaf");
+    std::vector<int64_t> seg(leaves.size() + 1, 0);
+    for (size_t i = 0; i < data.size(); ++i) seg[i + 1] = seg[i] + data[i]->size();
+    const int64_t n = seg.back();
+    std::vector<float> planes[7];
+    for (auto& p : planes) p.resize((size_t)n);
+    for (size_t i = 0; i < data.size(); ++i)
+        for (int d = 0; d < 7; ++d) {
+            const float* src = d < 6 ? data[i]->plane(d).data() : data[i]->weights();
+            std::copy(src, src + data[i]->size(), planes[d].begin() + seg[i]);
+        }
+    sdmm_samples s{};
+    for (int d = 0; d < 6; ++d) s.x[d] = planes[d].data();
+    s.w = planes[6].data();
+    s.n = n;
+    std::vector<sdmm_mix*> h(leaves.size());
+    for (size_t i = 0; i < leaves.size(); ++i) h[i] = leaves[i]->handle();
+    check(sdmm_em_step_batched_host(h.data(), (int)h.size(), &s, seg.data(), iterations),
+          "sdmm_em_step_batched_host");
+}
 
 // A wavefront of guided-bounce queries against one mixture: the batched form
 // of create_conditional + sample + posterior/hsum (sdmm_proc.cpp:368-545).

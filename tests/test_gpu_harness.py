@@ -66,3 +66,25 @@ def test_plugin_pattern_harness(pkg, oracle, synth, gpu, tmp_path):
         rel = lambda a: float(np.max(np.abs(a - ex) / np.maximum(np.abs(ex), 1e-7)))
         assert rel(p["weights"]) <= max(1e-4, 2 * rel(runs["accurate"])), (rel(p["weights"]),
                                                                            rel(runs["accurate"]))
+
+
+def test_plugin_pattern_batched_equals_threaded(pkg, synth, gpu, tmp_path):
+    """The harness in batched mode (one sdmm_em_step_batched_host per plugin
+    call over all leaves, sdmm_amd::em_step_leaves) gives bitwise the same
+    per-leaf mixtures as the thread-per-leaf sdmm_em_step_host pattern."""
+    K, L, N = 16, 6, 6 * 2500
+    b = synth.em_batch(N, 128)
+    with open(tmp_path / "in.bin", "wb") as f:
+        np.array([N], np.int64).tofile(f)
+        np.array([K, L], np.int32).tofile(f)
+        b["x"].astype(np.float32).tofile(f)
+        b["w"].astype(np.float32).tofile(f)
+        b["normals"].astype(np.float32).tofile(f)
+    exe = _build(tmp_path)
+    subprocess.run([str(exe), str(tmp_path / "in.bin"), str(tmp_path / "threads.bin")], check=True, timeout=120)
+    subprocess.run([str(exe), str(tmp_path / "in.bin"), str(tmp_path / "batched.bin"), "batched"], check=True,
+                   timeout=120)
+    a = np.fromfile(tmp_path / "threads.bin", np.float32)
+    c = np.fromfile(tmp_path / "batched.bin", np.float32)
+    assert a.size == L * K * 32
+    np.testing.assert_array_equal(a, c)
