@@ -98,6 +98,11 @@ const char* sdmm_kernel_name(const sdmm_mix* m, int which);
  * Results are identical for every cap; 0 sends every query down the full-K
  * path (a testing knob). */
 int sdmm_set_guide_capacity(sdmm_mix* m, int cap);
+/* coherent != 0 (default): guided batches of >= 16384 queries are served in
+ * Morton order of their condition position (a device radix sort of the
+ * batch), so the queries of a wave touch the same components.  Outputs are
+ * written at each query's own index and are identical either way. */
+int sdmm_set_guide_order(sdmm_mix* m, int coherent);
 /* Work is enqueued on this hipStream_t, taken literally (NULL = the HIP null
  * stream).  A new handle starts on its own non-blocking stream, whose value
  * sdmm_get_stream returns before any sdmm_set_stream call. */

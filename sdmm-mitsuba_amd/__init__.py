@@ -123,7 +123,7 @@ def stats_len(K: int) -> int:
 EXPORTED_SYMBOLS = [
     "sdmm_em_params_default", "sdmm_create", "sdmm_destroy", "sdmm_num_components", "sdmm_layout",
     "sdmm_kernel_name",
-    "sdmm_set_guide_capacity",
+    "sdmm_set_guide_capacity", "sdmm_set_guide_order",
     "sdmm_set_stream", "sdmm_get_stream", "sdmm_synchronize", "sdmm_init_hemisphere",
     "sdmm_hemisphere_init_host", "sdmm_em_step", "sdmm_em_step_host", "sdmm_em_step_batched",
     "sdmm_em_step_batched_host",
@@ -310,6 +310,10 @@ class SDMM:
     def set_guide_capacity(self, cap: int):
         """Per-query candidate-list capacity of the guided-query kernel (0..40)."""
         _check(lib().sdmm_set_guide_capacity(self.h, cap))
+
+    def set_guide_order(self, coherent: bool):
+        """Serve large guided batches in Morton order of c (default) or as given."""
+        _check(lib().sdmm_set_guide_order(self.h, 1 if coherent else 0))
 
     def layout(self) -> dict:
         """E-step kernel layouts: (components per lane, lanes per sample)."""

@@ -52,10 +52,11 @@ hipError_t launch_pack_all(int K, int Kp, const CanonDev& C, float* ep, float* g
 hipError_t launch_mstep(int K, int Kp, const double* stats, int64_t nSamples, const CanonDev& C,
                         const EmStateDev& S, float* ep, float* gp, float norm5, double* wmean, double* wcov,
                         hipStream_t st);
+size_t guide_sort_temp_bytes(int n);
 hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float* const c[3],
                         const float* const u[3], const float* const dgiven[3], float* const d[3], float* pdf,
                         int32_t* comp, float norm2, float norm3, int cap, int* fb_count, int32_t* fb_list,
-                        int cus, hipStream_t st);
+                        int cus, hipStream_t st, const GuideSortScratch* sort);
 constexpr int kGuideCapMax = 40;
 hipError_t launch_sample_cdf(const float* cdf, int n, const float* u, int64_t nq, int32_t* out,
                              hipStream_t st);
@@ -200,6 +201,8 @@ struct sdmm_mix {
     int guide_cap = kGuideCapMax;   // candidate-list capacity (sdmm_set_guide_capacity)
     mutable int* guide_fb = nullptr;
     mutable int64_t guide_fb_cap = 0;
+    mutable GuideSortScratch guide_sort{};
+    int guide_order = 1;            // 1: serve large batches in Morton order of c (sdmm_set_guide_order)
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
     sdmm_em_params params{};
@@ -293,8 +296,10 @@ int ensure_partials(sdmm_mix* m, int rows) {
     return SDMM_OK;
 }
 
-// [count, list...] of fallback guided queries; grows on demand (stream-ordered
-// free is not needed: the previous buffer is only released after a sync)
+// Guided-batch scratch, one allocation grown on demand: [count, fallback
+// list...] (cap + 1 ints), then the coherent-order buffers (2 x cap keys,
+// 2 x cap indices, the radix sort's temporary storage).  The previous buffer
+// is only released after a stream sync.
 int ensure_guide_scratch(const sdmm_mix* m, int64_t nq) {
     if (nq + 1 <= m->guide_fb_cap) return SDMM_OK;
     if (m->guide_fb) {
@@ -304,9 +309,25 @@ int ensure_guide_scratch(const sdmm_mix* m, int64_t nq) {
         m->guide_fb_cap = 0;
     }
     const int64_t cap = (nq + 1 < (1 << 20)) ? (1 << 20) : nq + 1;
-    HIP_TRY(hipMalloc(&m->guide_fb, sizeof(int) * (size_t)cap));
+    const size_t a = ((sizeof(int) * (size_t)cap + 255) / 256) * 256;
+    const size_t kb = ((sizeof(uint32_t) * (size_t)cap + 255) / 256) * 256;
+    const size_t tb = guide_sort_temp_bytes((int)(cap > INT32_MAX ? INT32_MAX : cap));
+    char* base = nullptr;
+    HIP_TRY(hipMalloc((void**)&base, a + 4 * kb + tb + 256));
+    m->guide_fb = (int*)base;
+    m->guide_sort.keys[0] = (uint32_t*)(base + a);
+    m->guide_sort.keys[1] = (uint32_t*)(base + a + kb);
+    m->guide_sort.idx[0] = (int32_t*)(base + a + 2 * kb);
+    m->guide_sort.idx[1] = (int32_t*)(base + a + 3 * kb);
+    m->guide_sort.temp = base + a + 4 * kb;
+    m->guide_sort.temp_bytes = tb;
     m->guide_fb_cap = cap;
     return SDMM_OK;
+}
+
+// coherent order for batches large enough to fill the chip several times
+const GuideSortScratch* guide_order(const sdmm_mix* m, int64_t nq) {
+    return (m->guide_order && nq >= (1 << 14)) ? &m->guide_sort : nullptr;
 }
 
 // Work split of m's statistics E-step over n samples (the same for a
@@ -506,6 +527,12 @@ void sdmm_destroy(sdmm_mix* m) {
 }
 
 int sdmm_num_components(const sdmm_mix* m) { return m ? m->K : 0; }
+
+int sdmm_set_guide_order(sdmm_mix* m, int coherent) {
+    if (!m) return fail(SDMM_E_INVALID, "null handle");
+    m->guide_order = coherent ? 1 : 0;
+    return SDMM_OK;
+}
 
 int sdmm_set_guide_capacity(sdmm_mix* m, int cap) {
     if (!m) return fail(SDMM_E_INVALID, "null handle");
@@ -851,7 +878,7 @@ int sdmm_guide_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], con
     int r = ensure_guide_scratch(m, nq);
     if (r) return r;
     HIP_TRY(launch_guide(m->gp, m->Kp, m->K, nq, c, u, nullptr, d, pdf, comp, m->norm2, m->norm3,
-                         m->guide_cap, m->guide_fb, m->guide_fb + 1, m->cus, m->stream));
+                         m->guide_cap, m->guide_fb, m->guide_fb + 1, m->cus, m->stream, guide_order(m, nq)));
     return SDMM_OK;
 }
 
@@ -863,7 +890,7 @@ int sdmm_pdf_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], const
     int r = ensure_guide_scratch(m, nq);
     if (r) return r;
     HIP_TRY(launch_guide(m->gp, m->Kp, m->K, nq, c, nullptr, d, nullptr, pdf, nullptr, m->norm2, m->norm3,
-                         m->guide_cap, m->guide_fb, m->guide_fb + 1, m->cus, m->stream));
+                         m->guide_cap, m->guide_fb, m->guide_fb + 1, m->cus, m->stream, guide_order(m, nq)));
     return SDMM_OK;
 }
 

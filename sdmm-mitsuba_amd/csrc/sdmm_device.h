@@ -139,6 +139,14 @@ struct MixDesc {
     int64_t n;
 };
 
+// scratch of the coherent (Morton) ordering of a guided batch
+struct GuideSortScratch {
+    uint32_t* keys[2];
+    int32_t* idx[2];
+    void* temp;
+    size_t temp_bytes;
+};
+
 constexpr float kHeuristicWeight = 0.5f;     // mixture_model.h:398
 constexpr double kPi = 3.14159265358979323846;
 

@@ -399,3 +399,33 @@ def test_responsibilities_fitted_each_kernel(pkg, oracle, synth, gpu, monkeypatc
     ref = oracle.responsibilities(m, oracle.Samples(b["x"], b["w"]))
     assert np.isfinite(got).all()
     _check_resp(got, ref, mix.get_params(), b["x"])
+
+
+@pytest.mark.parametrize("K", [128, 16])
+def test_guide_coherent_order_identical(pkg, oracle, synth, gpu, K):
+    """Large batches are served in Morton order of c (sdmm_set_guide_order):
+    every output equals the as-given order bit for bit, and the indices stay
+    bit-exact with the oracle."""
+    import torch
+    b, mix, om = _em_model(pkg, oracle, synth, K, 8192, 3)
+    nq = 40000                                   # above the 16384 threshold
+    c, u = synth.sample_queries_near(b, nq // 2)
+    c2, u2 = synth.queries(nq - nq // 2, seed=5)
+    c = np.concatenate([c, c2], 1)
+    u = np.concatenate([u, u2], 1)
+    c[:, 7] = np.nan                             # a NaN condition takes the fallback in either order
+    ct = [torch.from_numpy(c[i].copy()).to(gpu) for i in range(3)]
+    ut = [torch.from_numpy(u[i].copy()).to(gpu) for i in range(3)]
+    outs = []
+    for coherent in (True, False):
+        mix.set_guide_order(coherent)
+        d, pdf, comp = mix.guide(ct, ut)
+        torch.cuda.synchronize()
+        outs.append((np.stack([t.cpu().numpy() for t in d]), pdf.cpu().numpy(), comp.cpu().numpy()))
+    for a, bb in zip(outs[0], outs[1]):
+        np.testing.assert_array_equal(a, bb)
+    # (query 7 excluded: with a NaN condition the reference's lastIdx is
+    # uninitialised -- mixture_model.h:262-284, SURVEY appendix A item 9)
+    sub = np.r_[0:7, 8:6000]
+    dr, pr, cr, sr = oracle.guide_batch(om, c[:, sub].T, u[:, sub].T)
+    np.testing.assert_array_equal(outs[0][2][sub], cr)
