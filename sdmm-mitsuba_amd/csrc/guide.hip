@@ -343,7 +343,9 @@ __device__ __forceinline__ int build_candidates(const float* gp, int Kp, int K, 
     return (ncand == K) ? K : -1;
 }
 
-template <bool PDF_ONLY>
+// LDS list capacity LCAP (24 or 40): the lists are 6 B per entry per thread,
+// so the capacity sets the workgroups per CU (LDS-limited occupancy).
+template <bool PDF_ONLY, int LCAP>
 __global__ void __launch_bounds__(64)
 guide_cand_kernel(const float* __restrict__ gp, int Kp, int K, int64_t nq, const float* __restrict__ c0,
                   const float* __restrict__ c1, const float* __restrict__ c2, const float* __restrict__ u0,
@@ -352,8 +354,8 @@ guide_cand_kernel(const float* __restrict__ gp, int Kp, int K, int64_t nq, const
                   float* __restrict__ d1, float* __restrict__ d2, float* __restrict__ pdf,
                   int32_t* __restrict__ comp, GuideConsts gc, int cap, int* __restrict__ fb_count,
                   int32_t* __restrict__ fb_list, const int32_t* __restrict__ perm) {
-    __shared__ float cw[kGuideCap * 64];
-    __shared__ unsigned short ck[kGuideCap * 64];
+    __shared__ float cw[LCAP * 64];
+    __shared__ unsigned short ck[LCAP * 64];
     const int T = 64;
     const int tid = threadIdx.x;
     const int64_t t = (int64_t)blockIdx.x * T + tid;
@@ -564,15 +566,27 @@ hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float*
     float* o1 = pdf_only ? nullptr : d[1];
     float* o2 = pdf_only ? nullptr : d[2];
     if (pdf_only) {
-        hipLaunchKernelGGL(guide_cand_kernel<true>, dim3((unsigned)blocks), dim3(T), 0, st, gp, Kp, K, nq, c[0],
-                           c[1], c[2], v0, v1, v2, g0, g1, g2, o0, o1, o2, pdf, comp, gc, cap, fb_count, fb_list, perm);
+        if (cap <= 24)
+            hipLaunchKernelGGL((guide_cand_kernel<true, 24>), dim3((unsigned)blocks), dim3(T), 0, st, gp, Kp, K, nq,
+                               c[0], c[1], c[2], v0, v1, v2, g0, g1, g2, o0, o1, o2, pdf, comp, gc, cap, fb_count,
+                               fb_list, perm);
+        else
+            hipLaunchKernelGGL((guide_cand_kernel<true, kGuideCap>), dim3((unsigned)blocks), dim3(T), 0, st, gp, Kp,
+                               K, nq, c[0], c[1], c[2], v0, v1, v2, g0, g1, g2, o0, o1, o2, pdf, comp, gc, cap,
+                               fb_count, fb_list, perm);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(guide_fallback_kernel<true>, dim3(fb_blocks), dim3(T), lds_fb, st, gp, Kp, K, c[0],
                            c[1], c[2], v0, v1, v2, g0, g1, g2, o0, o1, o2, pdf, comp, gc, fb_count, fb_list);
     } else {
-        hipLaunchKernelGGL(guide_cand_kernel<false>, dim3((unsigned)blocks), dim3(T), 0, st, gp, Kp, K, nq, c[0],
-                           c[1], c[2], v0, v1, v2, g0, g1, g2, o0, o1, o2, pdf, comp, gc, cap, fb_count, fb_list, perm);
+        if (cap <= 24)
+            hipLaunchKernelGGL((guide_cand_kernel<false, 24>), dim3((unsigned)blocks), dim3(T), 0, st, gp, Kp, K, nq,
+                               c[0], c[1], c[2], v0, v1, v2, g0, g1, g2, o0, o1, o2, pdf, comp, gc, cap, fb_count,
+                               fb_list, perm);
+        else
+            hipLaunchKernelGGL((guide_cand_kernel<false, kGuideCap>), dim3((unsigned)blocks), dim3(T), 0, st, gp,
+                               Kp, K, nq, c[0], c[1], c[2], v0, v1, v2, g0, g1, g2, o0, o1, o2, pdf, comp, gc, cap,
+                               fb_count, fb_list, perm);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(guide_fallback_kernel<false>, dim3(fb_blocks), dim3(T), lds_fb, st, gp, Kp, K, c[0],
