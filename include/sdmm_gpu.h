@@ -205,6 +205,36 @@ int sdmm_get_state(const sdmm_mix* m, double* scalars, double* T, double* sgW, d
 int sdmm_set_state(sdmm_mix* m, const double* scalars, const double* T, const double* sgW,
                    const double* sgM, const double* sgC, const float* bpriors, const float* bdepth);
 
+/* Spatial tree (the plugin's accelerator: sdmm-lib DMMSTree, sdmm_proc.h:91,
+ * absent; restated from jmm SNTree, dmm/jmm/sntree.h:93-299, spatial part).
+ * Node ids are the reference's m_nodes indices; child 0 is the upper part of
+ * a split.  Construction is host work (as in the reference); find and route
+ * run on the device, on the tree's own stream.
+ *   sdmm_stree_create          root = the AABB enlarged to a cube (:101-106)
+ *   sdmm_stree_split_to_depth  split_to_depth (:195-233), volpath_sdmm.cpp:358
+ *   sdmm_stree_split           split(threshold) (:235-283) on HOST position
+ *                              planes p[3] (n points), volpath_sdmm.cpp:161,226
+ *   sdmm_stree_find            STree.find(key) (sdmm_proc.cpp:351, :931, :958)
+ *                              for n DEVICE points -> node id or -1 (outside)
+ *   sdmm_stree_route           device samples -> device planes `out` (same n,
+ *                              same optional planes) in leaf-contiguous order,
+ *                              stable within a leaf; seg (host, num_nodes + 1):
+ *                              node v's samples are [seg[v], seg[v+1]), points
+ *                              outside the tree follow seg[num_nodes].  `seg`
+ *                              with the leaves' mixtures feeds
+ *                              sdmm_em_step_batched directly. Synchronous. */
+typedef struct sdmm_stree sdmm_stree;
+int sdmm_stree_create(const float aabb_min[3], const float aabb_max[3], int device, sdmm_stree** out);
+void sdmm_stree_destroy(sdmm_stree* t);
+int sdmm_stree_split_to_depth(sdmm_stree* t, int max_depth);
+int sdmm_stree_split(sdmm_stree* t, const float* const p[3], int64_t n, int threshold);
+int sdmm_stree_num_nodes(const sdmm_stree* t);
+/* aabb[6 * i] = min(3), max(3); child[2 * i] = children (-1, -1 for a leaf);
+ * axis[i]: split axis.  Any output may be NULL. */
+int sdmm_stree_get_nodes(const sdmm_stree* t, float* aabb, int32_t* child, int32_t* axis);
+int sdmm_stree_find(sdmm_stree* t, int64_t n, const float* const p[3], int32_t* node_out);
+int sdmm_stree_route(sdmm_stree* t, const sdmm_samples* device_samples, const sdmm_samples* out, int64_t* seg);
+
 const char* sdmm_last_error(void);
 int sdmm_abi_version(void);
 

@@ -303,3 +303,36 @@ def pcg32_floats(seed, n, seq=0xda3e39cb94b95bdb):
     r = R()
     lib().or_pcg32_seed(C.byref(r), C.c_uint64(seed), C.c_uint64(seq))
     return np.array([lib().or_pcg32_next_float(C.byref(r)) for _ in range(n)], np.float32)
+
+
+def stree_build(aabb_min, aabb_max, depth, p, threshold, cap=1 << 16):
+    """jmm SNTree (spatial part) restated in C: returns (aabb[n,6], child[n,2], axis[n])."""
+    p = [np.ascontiguousarray(x, np.float32) for x in p]
+    n = p[0].shape[0]
+    mn = np.zeros(3 * cap, np.float32)
+    mx = np.zeros(3 * cap, np.float32)
+    ax = np.zeros(cap, np.int32)
+    ch = np.zeros(2 * cap, np.int32)
+    lo = np.ascontiguousarray(aabb_min, np.float32)
+    hi = np.ascontiguousarray(aabb_max, np.float32)
+    f = lib().or_stree_build
+    f.restype = C.c_int
+    cnt = f(_fp(lo), _fp(hi), C.c_int(depth), _fp(p[0]), _fp(p[1]), _fp(p[2]), C.c_int64(n),
+            C.c_int(threshold), C.c_int(cap), _fp(mn), _fp(mx), ax.ctypes.data_as(C.c_void_p),
+            ch.ctypes.data_as(C.c_void_p))
+    assert cnt > 0, "oracle tree capacity exceeded"
+    aabb = np.concatenate([mn[:3 * cnt].reshape(-1, 3), mx[:3 * cnt].reshape(-1, 3)], 1)
+    return aabb, ch[:2 * cnt].reshape(-1, 2).copy(), ax[:cnt].copy()
+
+
+def stree_find(aabb, child, pts):
+    """SNTreeNode::find for points (n, 3) on a tree from stree_build."""
+    mn = np.ascontiguousarray(aabb[:, :3].reshape(-1), np.float32)
+    mx = np.ascontiguousarray(aabb[:, 3:].reshape(-1), np.float32)
+    ch = np.ascontiguousarray(child.reshape(-1), np.int32)
+    f = lib().or_stree_find
+    f.restype = C.c_int
+    out = np.empty(len(pts), np.int32)
+    for i, q in enumerate(np.ascontiguousarray(pts, np.float32)):
+        out[i] = f(_fp(mn), _fp(mx), ch.ctypes.data_as(C.c_void_p), _fp(q))
+    return out

@@ -131,6 +131,8 @@ EXPORTED_SYMBOLS = [
     "sdmm_estep_stats", "sdmm_mstep", "sdmm_responsibilities", "sdmm_guide_batch", "sdmm_pdf_batch",
     "sdmm_sample_discrete_cdf", "sdmm_get_params", "sdmm_set_params", "sdmm_get_state",
     "sdmm_set_state", "sdmm_last_error", "sdmm_abi_version",
+    "sdmm_stree_create", "sdmm_stree_destroy", "sdmm_stree_split_to_depth", "sdmm_stree_split",
+    "sdmm_stree_num_nodes", "sdmm_stree_get_nodes", "sdmm_stree_find", "sdmm_stree_route",
 ]
 
 
@@ -380,3 +382,66 @@ class SDMM:
         _check(lib().sdmm_sample_discrete_cdf(self.h, cdf.data_ptr(), cdf.numel(), u.data_ptr(),
                                               u.numel(), out.data_ptr()))
         return out
+
+
+class STree:
+    """The guiding accelerator's spatial tree (jmm SNTree spatial part,
+    sntree.h:93-299; the plugin's sdmm-lib DMMSTree is absent).  Built on the
+    host; find / route run on the device (sdmm_stree_* in include/sdmm_gpu.h)."""
+
+    def __init__(self, aabb_min, aabb_max, device: int = 0):
+        lo = np.ascontiguousarray(aabb_min, np.float32)
+        hi = np.ascontiguousarray(aabb_max, np.float32)
+        h = C.c_void_p()
+        _check(lib().sdmm_stree_create(lo.ctypes.data_as(C.c_void_p), hi.ctypes.data_as(C.c_void_p),
+                                       C.c_int(device), C.byref(h)))
+        self.h = h
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.sdmm_stree_destroy(self.h)
+            self.h = None
+
+    def split_to_depth(self, depth: int):
+        _check(lib().sdmm_stree_split_to_depth(self.h, C.c_int(depth)))
+
+    def split(self, positions, threshold: int):
+        """split(threshold) over host positions (3, n)."""
+        p = [np.ascontiguousarray(positions[i], np.float32) for i in range(3)]
+        arr = (C.c_void_p * 3)(*[x.ctypes.data for x in p])
+        _check(lib().sdmm_stree_split(self.h, arr, C.c_int64(p[0].shape[0]), C.c_int(threshold)))
+
+    @property
+    def num_nodes(self) -> int:
+        return int(lib().sdmm_stree_num_nodes(self.h))
+
+    def nodes(self):
+        n = self.num_nodes
+        aabb = np.zeros((n, 6), np.float32)
+        child = np.zeros((n, 2), np.int32)
+        axis = np.zeros(n, np.int32)
+        _check(lib().sdmm_stree_get_nodes(self.h, aabb.ctypes.data_as(C.c_void_p),
+                                          child.ctypes.data_as(C.c_void_p), axis.ctypes.data_as(C.c_void_p)))
+        return aabb, child, axis
+
+    def find(self, p, out=None):
+        """Node id per device point (3 device planes) -> int32 device tensor (-1: outside)."""
+        import torch
+        n = p[0].numel()
+        if out is None:
+            out = torch.empty(n, dtype=torch.int32, device=p[0].device)
+        arr = (C.c_void_p * 3)(*[t.data_ptr() for t in p])
+        _check(lib().sdmm_stree_find(self.h, C.c_int64(n), arr, C.c_void_p(out.data_ptr())))
+        return out
+
+    def route(self, samples: "DeviceSamples"):
+        """Leaf-contiguous copy of `samples` and seg (num_nodes + 1 offsets)."""
+        import torch
+        x = [torch.empty_like(t) for t in samples.x]
+        w = torch.empty_like(samples.w)
+        hp = None if samples.hpdf is None else torch.empty_like(samples.hpdf)
+        dd = None if samples.is_diffuse is None else torch.empty_like(samples.is_diffuse)
+        out = DeviceSamples(x, w, hp, dd)
+        seg = np.zeros(self.num_nodes + 1, np.int64)
+        _check(lib().sdmm_stree_route(self.h, samples.ptr, out.ptr, seg.ctypes.data_as(C.c_void_p)))
+        return out, seg

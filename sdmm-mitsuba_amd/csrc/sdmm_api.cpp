@@ -53,6 +53,13 @@ hipError_t launch_mstep(int K, int Kp, const double* stats, int64_t nSamples, co
                         const EmStateDev& S, float* ep, float* gp, float norm5, double* wmean, double* wcov,
                         hipStream_t st);
 size_t guide_sort_temp_bytes(int n);
+hipError_t launch_stree_find(const void* nodes, int64_t n, const float* p0, const float* p1, const float* p2,
+                             int32_t* out, hipStream_t st);
+size_t stree_route_temp_bytes(int n, int key_bits);
+hipError_t launch_stree_route(const void* nodes, int num_nodes, int key_bits, const SamplesDev& in, int n,
+                              uint32_t* keys0, uint32_t* keys1, int32_t* idx0, int32_t* idx1, void* temp,
+                              size_t temp_bytes, int64_t* seg_dev, float* const out_x[6], float* out_w,
+                              float* out_h, uint8_t* out_d, hipStream_t st);
 hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float* const c[3],
                         const float* const u[3], const float* const dgiven[3], float* const d[3], float* pdf,
                         int32_t* comp, float norm2, float norm3, int cap, int* fb_count, int32_t* fb_list,
@@ -953,6 +960,303 @@ int sdmm_set_state(sdmm_mix* m, const double* scalars, const double* T, const do
     if (bpriors) HIP_TRY(hipMemcpyAsync(m->S.bPriors, bpriors, 100 * K, hipMemcpyHostToDevice, st));
     if (bdepth) HIP_TRY(hipMemcpyAsync(m->S.bDepth, bdepth, 36 * K, hipMemcpyHostToDevice, st));
     HIP_TRY(hipStreamSynchronize(st));
+    return SDMM_OK;
+}
+
+}  // extern "C"
+
+// ==========================================================================
+// Spatial tree: jmm SNTree (mitsuba/src/integrators/dmm/jmm/sntree.h:93-299),
+// spatial part.  The plugin's accelerator is sdmm-lib's DMMSTree
+// (sdmm_proc.h:91), absent from the snapshot; SNTree is its readable
+// counterpart.  Construction runs on the host, as in the reference (it is a
+// once-per-iteration, data-dependent recursion); find() and the routing of a
+// sample batch into leaf-contiguous order run on the device.
+//
+// Restated behaviour (file:line of sntree.h):
+//   * the root box is the given AABB enlarged to a cube (:101-106);
+//   * split_to_depth(d) (:195-233): midpoint splits along the node's axis,
+//     children take axis (a + 1) % 3, "depth" advances after the z split;
+//   * split(threshold) (:235-283): a leaf holding more than `threshold`
+//     samples splits at the sample mean along its max-variance axis
+//     (getSplitLocation :141-170, strict > so ties keep the lower axis);
+//     each child receives the parent's samples its box contains (inclusive
+//     on both sides: a sample on the plane goes to both, :174-192), and the
+//     children are split recursively, child 0 first;
+//   * child 0 is the UPPER part (min[axis] += s * diag), child 1 the lower
+//     (max[axis] -= (1 - s) * diag) (createChildNode :172-186);
+//   * nodes are appended in creation order, so node ids are the reference's
+//     m_nodes indices.
+// Deviations (documented): the mean/variance are summed in double
+// (jmm: float Eigen sums, order unspecified); a split that would not separate
+// the samples (zero variance: the reference recurses forever) is skipped;
+// the per-normal NGridNode cells are not modelled (one value per leaf).
+struct STNodeHost {
+    float mn[3], mx[3];
+    int axis = 0;
+    int child[2] = {-1, -1};
+};
+
+struct sdmm_stree {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::vector<STNodeHost> nodes;
+    void* dnodes = nullptr;
+    size_t dnodes_cap = 0;
+    bool dirty = true;
+    void* scratch = nullptr;
+    size_t scratch_bytes = 0;
+};
+
+namespace {
+
+bool st_contains(const STNodeHost& n, const float p[3]) {
+    return n.mn[0] <= p[0] && p[0] <= n.mx[0] && n.mn[1] <= p[1] && p[1] <= n.mx[1] && n.mn[2] <= p[2] &&
+           p[2] <= n.mx[2];
+}
+
+STNodeHost st_child(const STNodeHost& parent, int child_i, float split) {
+    STNodeHost c;
+    const int axis = parent.axis;
+    c.axis = (axis + 1) % 3;
+    for (int i = 0; i < 3; ++i) { c.mn[i] = parent.mn[i]; c.mx[i] = parent.mx[i]; }
+    const float diag = parent.mx[axis] - parent.mn[axis];
+    if (child_i == 0) {
+        const float d = split * diag;
+        c.mn[axis] = parent.mn[axis] + d;
+    } else {
+        const float d = (1.0f - split) * diag;
+        c.mx[axis] = parent.mx[axis] - d;
+    }
+    return c;
+}
+
+void st_split_depth(sdmm_stree* t, int node, int depth, int max_depth) {
+    const int next = (t->nodes[node].axis == 2) ? depth + 1 : depth;
+    if (t->nodes[node].child[0] >= 0) {
+        for (int c = 0; c < 2; ++c) st_split_depth(t, t->nodes[node].child[c], next, max_depth);
+        return;
+    }
+    if (depth < max_depth) {
+        for (int c = 0; c < 2; ++c) {
+            STNodeHost ch = st_child(t->nodes[node], c, 0.5f);
+            t->nodes[node].child[c] = (int)t->nodes.size();
+            t->nodes.push_back(ch);
+        }
+        for (int c = 0; c < 2; ++c) st_split_depth(t, t->nodes[node].child[c], next, max_depth);
+    }
+}
+
+// samples: indices into the position planes px/py/pz owned by node
+void st_split_recurse(sdmm_stree* t, int node, std::vector<int64_t>& idx, const float* px, const float* py,
+                      const float* pz, int threshold) {
+    if (t->nodes[node].child[0] >= 0) return;   // (inner nodes are routed by the caller)
+    const int64_t n = (int64_t)idx.size();
+    if (n <= threshold) return;
+    double mean[3] = {0, 0, 0}, sq[3] = {0, 0, 0};
+    for (int64_t i : idx) {
+        const double p[3] = {px[i], py[i], pz[i]};
+        for (int a = 0; a < 3; ++a) { mean[a] += p[a]; sq[a] += p[a] * p[a]; }
+    }
+    float m[3], var[3];
+    for (int a = 0; a < 3; ++a) {
+        const double mu = mean[a] / (double)n;
+        m[a] = (float)mu;
+        var[a] = (float)(sq[a] / (double)n - mu * mu);
+    }
+    int ax = 0;
+    for (int a = 0; a < 3; ++a)
+        if (var[a] > var[ax]) ax = a;
+    const STNodeHost& nd = t->nodes[node];
+    const float split = (m[ax] - nd.mn[ax]) / (nd.mx[ax] - nd.mn[ax]);
+    if (!(split > 0.0f && split < 1.0f)) return;   // degenerate (zero variance / outside)
+    STNodeHost parent = nd;
+    parent.axis = ax;
+    STNodeHost ch[2] = {st_child(parent, 0, split), st_child(parent, 1, split)};
+    std::vector<int64_t> sub[2];
+    for (int c = 0; c < 2; ++c) {
+        for (int64_t i : idx) {
+            const float p[3] = {px[i], py[i], pz[i]};
+            if (st_contains(ch[c], p)) sub[c].push_back(i);
+        }
+        if ((int64_t)sub[c].size() == n) return;   // would not separate the samples
+    }
+    t->nodes[node].axis = ax;
+    for (int c = 0; c < 2; ++c) {
+        t->nodes[node].child[c] = (int)t->nodes.size();
+        t->nodes.push_back(ch[c]);
+    }
+    idx.clear();
+    idx.shrink_to_fit();
+    for (int c = 0; c < 2; ++c)
+        st_split_recurse(t, t->nodes[node].child[c], sub[c], px, py, pz, threshold);
+}
+
+int st_find_host(const sdmm_stree* t, const float p[3]) {
+    if (!st_contains(t->nodes[0], p)) return -1;
+    int id = 0;
+    while (t->nodes[id].child[0] >= 0) {
+        const int c0 = t->nodes[id].child[0], c1 = t->nodes[id].child[1];
+        if (st_contains(t->nodes[c0], p)) id = c0;
+        else if (st_contains(t->nodes[c1], p)) id = c1;
+        else return -1;
+    }
+    return id;
+}
+
+int st_upload(sdmm_stree* t) {
+    if (!t->stream) HIP_TRY(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
+    if (!t->dirty) return SDMM_OK;
+    const size_t bytes = 32 * t->nodes.size();
+    if (bytes > t->dnodes_cap) {
+        HIP_TRY(hipStreamSynchronize(t->stream));
+        if (t->dnodes) HIP_TRY(hipFree(t->dnodes));
+        t->dnodes = nullptr;
+        const size_t cap = bytes * 2 > 4096 ? bytes * 2 : 4096;
+        HIP_TRY(hipMalloc(&t->dnodes, cap));
+        t->dnodes_cap = cap;
+    }
+    std::vector<float> rec(8 * t->nodes.size());
+    for (size_t i = 0; i < t->nodes.size(); ++i) {
+        const STNodeHost& n = t->nodes[i];
+        for (int a = 0; a < 3; ++a) { rec[8 * i + a] = n.mn[a]; rec[8 * i + 3 + a] = n.mx[a]; }
+        int c0 = n.child[0], c1 = n.child[1];
+        std::memcpy(&rec[8 * i + 6], &c0, 4);
+        std::memcpy(&rec[8 * i + 7], &c1, 4);
+    }
+    HIP_TRY(hipMemcpyAsync(t->dnodes, rec.data(), bytes, hipMemcpyHostToDevice, t->stream));
+    HIP_TRY(hipStreamSynchronize(t->stream));   // rec is a host temporary
+    t->dirty = false;
+    return SDMM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sdmm_stree_create(const float aabb_min[3], const float aabb_max[3], int device, sdmm_stree** out) {
+    if (!out || !aabb_min || !aabb_max) return fail(SDMM_E_INVALID, "invalid argument");
+    *out = nullptr;
+    float size = 0.0f;
+    for (int a = 0; a < 3; ++a) {
+        if (!(aabb_max[a] >= aabb_min[a])) return fail(SDMM_E_INVALID, "empty AABB");
+        size = std::max(size, aabb_max[a] - aabb_min[a]);
+    }
+    sdmm_stree* t = new (std::nothrow) sdmm_stree();
+    if (!t) return fail(SDMM_E_NOMEM, "out of host memory");
+    t->device = device;
+    STNodeHost root;
+    for (int a = 0; a < 3; ++a) { root.mn[a] = aabb_min[a]; root.mx[a] = aabb_min[a] + size; }   // cube (:101-106)
+    t->nodes.push_back(root);
+    *out = t;   // (the device stream is created on first device use: building needs no GPU)
+    return SDMM_OK;
+}
+
+void sdmm_stree_destroy(sdmm_stree* t) {
+    if (!t) return;
+    (void)hipSetDevice(t->device);
+    if (t->stream) (void)hipStreamSynchronize(t->stream);
+    if (t->dnodes) (void)hipFree(t->dnodes);
+    if (t->scratch) (void)hipFree(t->scratch);
+    if (t->stream) (void)hipStreamDestroy(t->stream);
+    delete t;
+}
+
+int sdmm_stree_split_to_depth(sdmm_stree* t, int max_depth) {
+    if (!t || max_depth < 0 || max_depth > 8) return fail(SDMM_E_INVALID, "max_depth must be in [0, 8]");
+    st_split_depth(t, 0, 0, max_depth);
+    t->dirty = true;
+    return SDMM_OK;
+}
+
+int sdmm_stree_split(sdmm_stree* t, const float* const p[3], int64_t n, int threshold) {
+    if (!t || (n > 0 && (!p || !p[0] || !p[1] || !p[2])) || n < 0 || threshold < 1)
+        return fail(SDMM_E_INVALID, "invalid argument");
+    // leaf assignment of the given samples (find), then the recursive split
+    std::vector<std::vector<int64_t>> per(t->nodes.size());
+    for (int64_t i = 0; i < n; ++i) {
+        const float q[3] = {p[0][i], p[1][i], p[2][i]};
+        const int id = st_find_host(t, q);
+        if (id >= 0) per[(size_t)id].push_back(i);
+    }
+    const size_t n0 = t->nodes.size();
+    for (size_t id = 0; id < n0; ++id)
+        if (t->nodes[id].child[0] < 0) st_split_recurse(t, (int)id, per[id], p[0], p[1], p[2], threshold);
+    t->dirty = true;
+    return SDMM_OK;
+}
+
+int sdmm_stree_num_nodes(const sdmm_stree* t) { return t ? (int)t->nodes.size() : 0; }
+
+int sdmm_stree_get_nodes(const sdmm_stree* t, float* aabb, int32_t* child, int32_t* axis) {
+    if (!t) return fail(SDMM_E_INVALID, "null tree");
+    for (size_t i = 0; i < t->nodes.size(); ++i) {
+        const STNodeHost& n = t->nodes[i];
+        if (aabb)
+            for (int a = 0; a < 3; ++a) { aabb[6 * i + a] = n.mn[a]; aabb[6 * i + 3 + a] = n.mx[a]; }
+        if (child) { child[2 * i] = n.child[0]; child[2 * i + 1] = n.child[1]; }
+        if (axis) axis[i] = n.axis;
+    }
+    return SDMM_OK;
+}
+
+int sdmm_stree_find(sdmm_stree* t, int64_t n, const float* const p[3], int32_t* node_out) {
+    if (!t || n < 0 || (n > 0 && (!p || !node_out))) return fail(SDMM_E_INVALID, "invalid argument");
+    if (n == 0) return SDMM_OK;
+    HIP_TRY(hipSetDevice(t->device));
+    int r = st_upload(t);
+    if (r) return r;
+    HIP_TRY(launch_stree_find(t->dnodes, n, p[0], p[1], p[2], node_out, t->stream));
+    return SDMM_OK;
+}
+
+int sdmm_stree_route(sdmm_stree* t, const sdmm_samples* in, const sdmm_samples* out, int64_t* seg) {
+    if (!t || !in || !out || !seg) return fail(SDMM_E_INVALID, "invalid argument");
+    int r = check_samples(in);
+    if (r) return r;
+    const int64_t n = in->n;
+    const int nn = (int)t->nodes.size();
+    if (n > INT32_MAX) return fail(SDMM_E_INVALID, "route: at most 2^31 - 1 samples");
+    for (int i = 0; i < 6; ++i)
+        if (n > 0 && !out->x[i]) return fail(SDMM_E_INVALID, "route: output plane missing");
+    if (n > 0 && !out->w) return fail(SDMM_E_INVALID, "route: output weight plane missing");
+    if ((in->hpdf != nullptr) != (out->hpdf != nullptr) ||
+        (in->is_diffuse != nullptr) != (out->is_diffuse != nullptr))
+        return fail(SDMM_E_INVALID, "route: optional planes must match");
+    if (n == 0) {
+        for (int v = 0; v <= nn; ++v) seg[v] = 0;
+        return SDMM_OK;
+    }
+    HIP_TRY(hipSetDevice(t->device));
+    r = st_upload(t);
+    if (r) return r;
+    int key_bits = 1;
+    while ((1 << key_bits) <= nn) ++key_bits;             // keys 0..nn
+    const size_t kb = ((sizeof(uint32_t) * (size_t)n + 255) / 256) * 256;
+    const size_t sb = ((sizeof(int64_t) * (size_t)(nn + 2) + 255) / 256) * 256;
+    const size_t tb = stree_route_temp_bytes((int)n, key_bits);
+    const size_t need = 4 * kb + sb + tb + 256;
+    if (need > t->scratch_bytes) {
+        HIP_TRY(hipStreamSynchronize(t->stream));
+        if (t->scratch) HIP_TRY(hipFree(t->scratch));
+        t->scratch = nullptr;
+        HIP_TRY(hipMalloc(&t->scratch, need));
+        t->scratch_bytes = need;
+    }
+    char* b = (char*)t->scratch;
+    uint32_t* k0 = (uint32_t*)b;
+    uint32_t* k1 = (uint32_t*)(b + kb);
+    int32_t* i0 = (int32_t*)(b + 2 * kb);
+    int32_t* i1 = (int32_t*)(b + 3 * kb);
+    int64_t* sdev = (int64_t*)(b + 4 * kb);
+    void* temp = b + 4 * kb + sb;
+    float* ox[6];
+    for (int i = 0; i < 6; ++i) ox[i] = const_cast<float*>(out->x[i]);
+    HIP_TRY(launch_stree_route(t->dnodes, nn, key_bits, to_dev(in), (int)n, k0, k1, i0, i1, temp, tb, sdev, ox,
+                               const_cast<float*>(out->w), const_cast<float*>(out->hpdf),
+                               const_cast<uint8_t*>(out->is_diffuse), t->stream));
+    HIP_TRY(hipMemcpyAsync(seg, sdev, sizeof(int64_t) * (size_t)(nn + 1), hipMemcpyDeviceToHost, t->stream));
+    HIP_TRY(hipStreamSynchronize(t->stream));
     return SDMM_OK;
 }
 

@@ -1,0 +1,117 @@
+"""Spatial tree (jmm SNTree restatement, sntree.h:93-299): the library's
+host-built tree against the C oracle's (CPU, bitwise), device find / route
+against the oracle's find (GPU, bit-exact node ids), and the routed batch
+driving the per-leaf EM (GPU)."""
+import numpy as np
+import pytest
+
+
+def _points(synth, n, seed=4):
+    b = synth.em_batch(n, 128)
+    return b, b["x"][0:3].copy()
+
+
+@pytest.mark.parametrize("depth,threshold", [(0, 4000), (1, 3000), (2, 20000), (3, 50000)])
+def test_tree_matches_oracle(pkg, oracle, synth, depth, threshold):
+    """split_to_depth + split(threshold) -> identical node arrays (ids, boxes,
+    children, axes) from the library and from the oracle."""
+    b, p = _points(synth, 60000)
+    lo, hi = np.float32([0.0, 0.0, 0.0]), np.float32([1.0, 0.95, 0.9])
+    t = pkg.STree(lo, hi)
+    t.split_to_depth(depth)
+    t.split(p, threshold)
+    aabb, child, axis = t.nodes()
+    oa, oc, ox = oracle.stree_build(lo, hi, depth, p, threshold)
+    np.testing.assert_array_equal(child, oc)
+    np.testing.assert_array_equal(aabb, oa)
+    np.testing.assert_array_equal(axis, ox)
+    leaves = child[:, 0] < 0
+    assert leaves.sum() == (len(child) + 1) // 2
+    # root is the cube over the AABB (SNTree ctor)
+    np.testing.assert_array_equal(aabb[0], np.float32([0, 0, 0, 1, 1, 1]))
+    # children of a data split: child 0 is the upper part along the split axis
+    inner = np.nonzero(~leaves)[0]
+    for i in inner[:50]:
+        a = axis[i]
+        c0, c1 = child[i]
+        assert aabb[c0, a] >= aabb[c1, a] and aabb[c0, 3 + a] == aabb[i, 3 + a]
+    # every leaf holds <= threshold points unless it could not be split
+    ids = oracle.stree_find(aabb, child, p.T[:5000])
+    assert (ids >= 0).all() and leaves[ids].all()
+
+
+@pytest.mark.gpu
+def test_device_find_and_route(pkg, oracle, synth, gpu):
+    import torch
+    b, p = _points(synth, 200000)
+    lo, hi = np.float32([0, 0, 0]), np.float32([1, 1, 1])
+    t = pkg.STree(lo, hi)
+    t.split_to_depth(2)
+    t.split(p, 6000)
+    aabb, child, axis = t.nodes()
+    # queries: samples, exact split-plane coordinates, box corners, outside points, NaN
+    rng = np.random.default_rng(3)
+    q = p[:, :20000].copy()
+    inner = np.nonzero(child[:, 0] >= 0)[0]
+    for j, i in enumerate(inner[:2000]):
+        c0 = child[i, 0]
+        q[axis[i], j] = aabb[c0, axis[i]]                  # on the plane: child 0 (upper) wins
+    q[:, 2000:2008] = np.float32([[0, 1, 0, 1, 0, 1, 0, 1], [0, 0, 1, 1, 0, 0, 1, 1], [0, 0, 0, 0, 1, 1, 1, 1]])
+    q[:, 2008:2100] = rng.uniform(-0.5, 1.5, size=(3, 92)).astype(np.float32)
+    q[0, 2100] = np.nan
+    qt = [torch.from_numpy(q[i].copy()).to(gpu) for i in range(3)]
+    got = t.find(qt).cpu().numpy()
+    ref = oracle.stree_find(aabb, child, q.T)
+    np.testing.assert_array_equal(got, ref)
+    # route: leaf-contiguous, stable inside a leaf, seg = per-node counts
+    ds = pkg.DeviceSamples.from_numpy(b["x"], b["w"], b["hpdf"], b["is_diffuse"])
+    out, seg = t.route(ds)
+    torch.cuda.synchronize()
+    ids = oracle.stree_find(aabb, child, p.T)
+    order = np.argsort(np.where(ids < 0, len(child), ids), kind="stable")
+    for i in range(6):
+        np.testing.assert_array_equal(out.x[i].cpu().numpy(), b["x"][i][order])
+    np.testing.assert_array_equal(out.w.cpu().numpy(), b["w"][order])
+    counts = np.bincount(ids[ids >= 0], minlength=len(child))
+    np.testing.assert_array_equal(np.diff(seg), counts)
+
+
+@pytest.mark.gpu
+def test_routed_leaves_batched_em(pkg, synth, gpu):
+    """route -> one mixture per tree node -> ONE sdmm_em_step_batched over the
+    routed planes with the route's own seg equals each node's own em_step
+    (inner nodes own no samples and stay untouched): the plugin's optimise
+    loop over the tree (volpath_sdmm.cpp:287-311)."""
+    import torch
+    b, p = _points(synth, 60000)
+    t = pkg.STree(np.float32([0, 0, 0]), np.float32([1, 1, 1]))
+    t.split_to_depth(1)
+    t.split(p, 8000)
+    ds = pkg.DeviceSamples.from_numpy(b["x"], b["w"])
+    out, seg = t.route(ds)
+    nn = len(seg) - 1
+    K = 16
+    xs = np.stack([x.cpu().numpy() for x in out.x])
+
+    def mixes():
+        ms = []
+        for v in range(nn):
+            a = int(seg[v]) if seg[v + 1] - seg[v] >= 2 else 0
+            m = pkg.SDMM(K)
+            m.init_hemisphere(xs[0:3, a:a + 2].T.copy(), xs[3:6, a:a + 2].T.copy(), synth.DEPTH_PRIOR,
+                              synth.SPATIAL_DISTANCE, 7 + v)
+            ms.append(m)
+        return ms
+    A, B = mixes(), mixes()
+    inside = pkg.DeviceSamples([x[:int(seg[nn])] for x in out.x], out.w[:int(seg[nn])])
+    pkg.em_step_batched(A, inside, seg, 1)
+    for m, v in zip(B, range(nn)):
+        a, e = int(seg[v]), int(seg[v + 1])
+        if e > a:
+            m.optimize(pkg.DeviceSamples([x[a:e] for x in out.x], out.w[a:e]))
+    torch.cuda.synchronize()
+    assert (np.diff(seg) > 0).sum() >= 8
+    for ma, mb in zip(A, B):
+        pa, pb = ma.get_params(), mb.get_params()
+        for k in ("weights", "mean", "cov"):
+            np.testing.assert_array_equal(pa[k], pb[k])
