@@ -234,6 +234,31 @@ int sdmm_stree_num_nodes(const sdmm_stree* t);
 int sdmm_stree_get_nodes(const sdmm_stree* t, float* aabb, int32_t* child, int32_t* axis);
 int sdmm_stree_find(sdmm_stree* t, int64_t n, const float* const p[3], int32_t* node_out);
 int sdmm_stree_route(sdmm_stree* t, const sdmm_samples* device_samples, const sdmm_samples* out, int64_t* seg);
+/* The tree's HIP stream (NULL: its own non-blocking stream).  Put the leaf
+ * mixtures and the tree on one stream to order EM steps before wavefronts. */
+int sdmm_stree_set_stream(sdmm_stree* t, void* hip_stream);
+void* sdmm_stree_get_stream(const sdmm_stree* t);
+
+/* Guided wavefront over the tree's leaves -- SDMMRenderer::sampleSurface for
+ * a batch of bounces (sdmm_proc.cpp:309-421): per query, node =
+ * STree.find(c) (:314), that node's mixture node_mix[node] (host array of
+ * sdmm_stree_num_nodes handles; NULL or uninitialised = no trained context,
+ * and a query outside the tree: BSDF only, :316-323), then conditional /
+ * sample / pdf exactly as sdmm_guide_batch against that mixture (outputs
+ * bitwise equal to it; comp -1 and pdf 0 when there is no valid conditional).
+ * node_out (nullable): node id per query (-1 outside).  Runs on the tree's
+ * stream; the mixtures must have no pending work on other streams.
+ * node_mix NULL: use the table bound by sdmm_stree_bind_mixtures (the
+ * plugin binds once per training iteration, after the per-leaf EM; the
+ * table re-uploads only when a handle/K changes).
+ *   sdmm_pdf_wavefront   pdfSurface's gmmPdf of given directions d
+ *                        (sdmm_proc.cpp:510-590) per query's own leaf. */
+int sdmm_stree_bind_mixtures(sdmm_stree* t, const sdmm_mix* const* node_mix);
+int sdmm_guide_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
+                         const float* const u[3], float* const d[3], float* pdf, int32_t* comp,
+                         int32_t* node_out);
+int sdmm_pdf_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
+                       const float* const d[3], float* pdf);
 
 const char* sdmm_last_error(void);
 int sdmm_abi_version(void);

@@ -107,6 +107,14 @@ def lib():
         L.sdmm_get_state.argtypes = [C.c_void_p] + [C.c_void_p] * 7
         L.sdmm_set_state.argtypes = [C.c_void_p] + [C.c_void_p] * 7
         L.sdmm_em_params_default.argtypes = [C.c_void_p]
+        L.sdmm_stree_set_stream.argtypes = [C.c_void_p, C.c_void_p]
+        L.sdmm_stree_get_stream.restype = C.c_void_p
+        L.sdmm_stree_get_stream.argtypes = [C.c_void_p]
+        L.sdmm_guide_wavefront.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p * 3, C.c_void_p * 3,
+                                           C.c_void_p * 3, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.sdmm_stree_bind_mixtures.argtypes = [C.c_void_p, C.c_void_p]
+        L.sdmm_pdf_wavefront.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p * 3, C.c_void_p * 3,
+                                         C.c_void_p]
         _lib = L
     return _lib
 
@@ -133,6 +141,8 @@ EXPORTED_SYMBOLS = [
     "sdmm_set_state", "sdmm_last_error", "sdmm_abi_version",
     "sdmm_stree_create", "sdmm_stree_destroy", "sdmm_stree_split_to_depth", "sdmm_stree_split",
     "sdmm_stree_num_nodes", "sdmm_stree_get_nodes", "sdmm_stree_find", "sdmm_stree_route",
+    "sdmm_stree_set_stream", "sdmm_stree_get_stream", "sdmm_guide_wavefront", "sdmm_pdf_wavefront",
+    "sdmm_stree_bind_mixtures",
 ]
 
 
@@ -445,3 +455,50 @@ class STree:
         seg = np.zeros(self.num_nodes + 1, np.int64)
         _check(lib().sdmm_stree_route(self.h, samples.ptr, out.ptr, seg.ctypes.data_as(C.c_void_p)))
         return out, seg
+
+    # ---- guided wavefront over the leaves (sampleSurface, sdmm_proc.cpp:309-421)
+    def _node_table(self, node_mix):
+        if node_mix is None:
+            return None                            # the bound table
+        if len(node_mix) != self.num_nodes:
+            raise ValueError(f"node_mix needs one entry per node ({self.num_nodes}), got {len(node_mix)}")
+        return (C.c_void_p * len(node_mix))(*[(m.h.value if m is not None else None) for m in node_mix])
+
+    def bind(self, node_mix):
+        """Bind one mixture per node (None: no trained mixture) for
+        guide/pdf calls made with node_mix=None."""
+        _check(lib().sdmm_stree_bind_mixtures(self.h, self._node_table(node_mix)))
+
+    def set_stream(self, stream):
+        """Run on `stream` (a torch.cuda.Stream, a raw hipStream_t int, or None for the tree's own)."""
+        ptr = None if stream is None else int(getattr(stream, "cuda_stream", stream))
+        _check(lib().sdmm_stree_set_stream(self.h, C.c_void_p(ptr)))
+
+    def guide(self, node_mix, c, u, out=None, node_out=None):
+        """Per query: leaf = find(c), then conditional/sample/pdf against
+        node_mix[leaf] (None: no trained mixture -> comp -1, pdf 0)."""
+        import torch
+        nq = c[0].numel()
+        tab = self._node_table(node_mix)
+        if out is None:
+            dev = c[0].device
+            out = ([torch.empty(nq, device=dev) for _ in range(3)], torch.empty(nq, device=dev),
+                   torch.empty(nq, device=dev, dtype=torch.int32))
+        d, pdf, comp = out
+        cc = (C.c_void_p * 3)(*[t.data_ptr() for t in c])
+        uu = (C.c_void_p * 3)(*[t.data_ptr() for t in u])
+        dd = (C.c_void_p * 3)(*[t.data_ptr() for t in d])
+        _check(lib().sdmm_guide_wavefront(self.h, tab, nq, cc, uu, dd, pdf.data_ptr(), comp.data_ptr(),
+                                          None if node_out is None else node_out.data_ptr()))
+        return d, pdf, comp
+
+    def pdf(self, node_mix, c, d, out=None):
+        import torch
+        nq = c[0].numel()
+        tab = self._node_table(node_mix)
+        if out is None:
+            out = torch.empty(nq, device=c[0].device)
+        cc = (C.c_void_p * 3)(*[t.data_ptr() for t in c])
+        dd = (C.c_void_p * 3)(*[t.data_ptr() for t in d])
+        _check(lib().sdmm_pdf_wavefront(self.h, tab, nq, cc, dd, out.data_ptr()))
+        return out

@@ -343,43 +343,112 @@ __device__ __forceinline__ int build_candidates(const float* gp, int Kp, int K, 
     return (ncand == K) ? K : -1;
 }
 
-// LDS list capacity LCAP (24 or 40): the lists are 6 B per entry per thread,
-// so the capacity sets the workgroups per CU (LDS-limited occupancy).
-template <bool PDF_ONLY, int LCAP>
-__global__ void __launch_bounds__(64)
-guide_cand_kernel(const float* __restrict__ gp, int Kp, int K, int64_t nq, const float* __restrict__ c0,
-                  const float* __restrict__ c1, const float* __restrict__ c2, const float* __restrict__ u0,
-                  const float* __restrict__ u1, const float* __restrict__ u2, const float* __restrict__ e0,
-                  const float* __restrict__ e1, const float* __restrict__ e2, float* __restrict__ d0,
-                  float* __restrict__ d1, float* __restrict__ d2, float* __restrict__ pdf,
-                  int32_t* __restrict__ comp, GuideConsts gc, int cap, int* __restrict__ fb_count,
-                  int32_t* __restrict__ fb_list, const int32_t* __restrict__ perm) {
-    __shared__ float cw[LCAP * 64];
-    __shared__ unsigned short ck[LCAP * 64];
-    const int T = 64;
-    const int tid = threadIdx.x;
-    const int64_t t = (int64_t)blockIdx.x * T + tid;
-    if (t >= nq) return;
-    // coherent order: thread t serves query perm[t] (Morton order of c)
-    const int64_t q = perm ? (int64_t)perm[t] : t;
-    const float c[3] = {c0[q], c1[q], c2[q]};
+// Plane pointers of one guided batch (inputs c, u or given directions e;
+// outputs d, pdf, comp).
+struct GuideIO {
+    const float *c0, *c1, *c2, *u0, *u1, *u2, *e0, *e1, *e2;
+    float *d0, *d1, *d2, *pdf;
+    int32_t* comp;
+};
+
+// One mixture's guide record as the wavefront kernels see it (per tree node;
+// K = 0: the node has no trained mixture -> BSDF only, sdmm_proc.cpp:316-323).
+struct GuideMix {
+    const float* gp;
+    int Kp, K;
+};
+static_assert(sizeof(GuideMix) == 16, "GuideMix");
+
+// Query q with no valid conditional: the reference falls back to BSDF
+// sampling (comp -1, gmmPdf 0).
+template <bool PDF_ONLY>
+__device__ __forceinline__ void write_invalid(const GuideIO& io, int64_t q) {
+    io.pdf[q] = 0.0f;
+    if constexpr (!PDF_ONLY) {
+        io.d0[q] = 0.0f; io.d1[q] = 0.0f; io.d2[q] = 0.0f;
+        io.comp[q] = -1;
+    }
+}
+
+template <bool PDF_ONLY, class Slots>
+__device__ __forceinline__ void finish_and_write(const float* gp, int Kp, const float c[3], int lastIdx,
+                                                 float accum, const Slots& S, const GuideIO& io, int64_t q,
+                                                 GuideConsts gc) {
+    if constexpr (PDF_ONLY) {
+        const float dir[3] = {io.e0[q], io.e1[q], io.e2[q]};
+        io.pdf[q] = finish_query(gp, Kp, c, nullptr, lastIdx, accum, S, dir, gc).pdf;
+    } else {
+        const float u[3] = {io.u0[q], io.u1[q], io.u2[q]};
+        const QueryOut o = finish_query(gp, Kp, c, u, lastIdx, accum, S, nullptr, gc);
+        io.d0[q] = o.d[0]; io.d1[q] = o.d[1]; io.d2[q] = o.d[2];
+        io.pdf[q] = o.pdf;
+        io.comp[q] = o.comp;
+    }
+}
+
+// Candidate path of query q against one mixture; false: q needs the full-K
+// fallback (appended to fb_list).
+template <bool PDF_ONLY>
+__device__ __forceinline__ void serve_cand(const float* gp, int Kp, int K, const GuideIO& io, int64_t q,
+                                           const float c[3], float* cw, unsigned short* ck, int tid, int cap,
+                                           GuideConsts gc, int* fb_count, int32_t* fb_list) {
     float accum = 0.0f;
-    const int lastIdx = build_candidates(gp, Kp, K, c, cw, ck, T, tid, gc.norm3, cap, accum);
+    const int lastIdx = build_candidates(gp, Kp, K, c, cw, ck, 64, tid, gc.norm3, cap, accum);
     if (lastIdx < 0) {
         fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
         return;
     }
-    const CandSlots S{cw, ck, T, tid};
-    if constexpr (PDF_ONLY) {
-        const float dir[3] = {e0[q], e1[q], e2[q]};
-        const QueryOut o = finish_query(gp, Kp, c, nullptr, lastIdx, accum, S, dir, gc);
-        pdf[q] = o.pdf;
-    } else {
-        const float u[3] = {u0[q], u1[q], u2[q]};
-        const QueryOut o = finish_query(gp, Kp, c, u, lastIdx, accum, S, nullptr, gc);
-        d0[q] = o.d[0]; d1[q] = o.d[1]; d2[q] = o.d[2];
-        pdf[q] = o.pdf;
-        comp[q] = o.comp;
+    finish_and_write<PDF_ONLY>(gp, Kp, c, lastIdx, accum, CandSlots{cw, ck, 64, tid}, io, q, gc);
+}
+
+// LDS list capacity LCAP (24 or 40): the lists are 6 B per entry per thread,
+// so the capacity sets the workgroups per CU (LDS-limited occupancy).
+template <bool PDF_ONLY, int LCAP>
+__global__ void __launch_bounds__(64)
+guide_cand_kernel(const float* __restrict__ gp, int Kp, int K, int64_t nq, GuideIO io, GuideConsts gc, int cap,
+                  int* __restrict__ fb_count, int32_t* __restrict__ fb_list, const int32_t* __restrict__ perm) {
+    __shared__ float cw[LCAP * 64];
+    __shared__ unsigned short ck[LCAP * 64];
+    const int tid = threadIdx.x;
+    const int64_t t = (int64_t)blockIdx.x * 64 + tid;
+    if (t >= nq) return;
+    // coherent order: thread t serves query perm[t] (Morton order of c)
+    const int64_t q = perm ? (int64_t)perm[t] : t;
+    const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
+    serve_cand<PDF_ONLY>(gp, Kp, K, io, q, c, cw, ck, tid, cap, gc, fb_count, fb_list);
+}
+
+// Wavefront over the spatial tree's leaves (SDMMRenderer::sampleSurface,
+// sdmm_proc.cpp:309-368): node = STree.find(c) (:314), that node's mixture
+// (tab[node]; none -> BSDF only), then the query exactly as
+// guide_cand_kernel serves it against that one mixture.  The waves are
+// Morton-ordered, so a wave's queries mostly share a leaf; the waterfall loop
+// serves one distinct mixture per trip with its record address uniform
+// (readfirstlane), keeping the record loads scalar.
+template <bool PDF_ONLY, int LCAP>
+__global__ void __launch_bounds__(64)
+guide_tree_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __restrict__ tab, int64_t nq,
+                       GuideIO io, GuideConsts gc, int cap, int* __restrict__ fb_count,
+                       int32_t* __restrict__ fb_list, const int32_t* __restrict__ perm,
+                       int32_t* __restrict__ node_out) {
+    __shared__ float cw[LCAP * 64];
+    __shared__ unsigned short ck[LCAP * 64];
+    const int tid = threadIdx.x;
+    const int64_t t = (int64_t)blockIdx.x * 64 + tid;
+    if (t >= nq) return;
+    const int64_t q = perm ? (int64_t)perm[t] : t;
+    const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
+    const int node = stree_find_point(nodes, c[0], c[1], c[2]);
+    if (node_out) node_out[q] = node;
+    for (;;) {
+        const int n0 = __builtin_amdgcn_readfirstlane(node);
+        if (node != n0) continue;
+        const GuideMix mx = (n0 >= 0) ? tab[n0] : GuideMix{nullptr, 0, 0};
+        if (mx.K <= 0)
+            write_invalid<PDF_ONLY>(io, q);
+        else
+            serve_cand<PDF_ONLY>(mx.gp, mx.Kp, mx.K, io, q, c, cw, ck, tid, cap, gc, fb_count, fb_list);
+        break;
     }
 }
 
@@ -428,14 +497,19 @@ __device__ __forceinline__ int build_full(const float* gp, int Kp, int K, const 
 }
 
 template <bool PDF_ONLY>
+__device__ __forceinline__ void serve_full(const float* gp, int Kp, int K, const GuideIO& io, int64_t q,
+                                           const float c[3], float* wl, int* sl, int T, int tid,
+                                           GuideConsts gc) {
+    float accum = 0.0f;
+    const int lastIdx = build_full(gp, Kp, K, c, wl, sl, T, tid, gc.norm3, accum);
+    finish_and_write<PDF_ONLY>(gp, Kp, c, lastIdx, accum, FullSlots{gp, Kp, c, wl, sl, T, tid}, io, q, gc);
+}
+
+// LDS: K x blockDim floats + ints (blockDim <= 64, chosen so K_max fits)
+template <bool PDF_ONLY>
 __global__ void __launch_bounds__(64)
-guide_fallback_kernel(const float* __restrict__ gp, int Kp, int K, const float* __restrict__ c0,
-                      const float* __restrict__ c1, const float* __restrict__ c2, const float* __restrict__ u0,
-                      const float* __restrict__ u1, const float* __restrict__ u2, const float* __restrict__ e0,
-                      const float* __restrict__ e1, const float* __restrict__ e2, float* __restrict__ d0,
-                      float* __restrict__ d1, float* __restrict__ d2, float* __restrict__ pdf,
-                      int32_t* __restrict__ comp, GuideConsts gc, const int* __restrict__ fb_count,
-                      const int32_t* __restrict__ fb_list) {
+guide_fallback_kernel(const float* __restrict__ gp, int Kp, int K, GuideIO io, GuideConsts gc,
+                      const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int T = blockDim.x;
     const int tid = threadIdx.x;
@@ -444,19 +518,33 @@ guide_fallback_kernel(const float* __restrict__ gp, int Kp, int K, const float* 
     const int count = *fb_count;
     for (int idx = blockIdx.x * T + tid; idx < count; idx += gridDim.x * T) {
         const int64_t q = fb_list[idx];
-        const float c[3] = {c0[q], c1[q], c2[q]};
-        float accum = 0.0f;
-        const int lastIdx = build_full(gp, Kp, K, c, wl, sl, T, tid, gc.norm3, accum);
-        const FullSlots S{gp, Kp, c, wl, sl, T, tid};
-        if constexpr (PDF_ONLY) {
-            const float dir[3] = {e0[q], e1[q], e2[q]};
-            pdf[q] = finish_query(gp, Kp, c, nullptr, lastIdx, accum, S, dir, gc).pdf;
-        } else {
-            const float u[3] = {u0[q], u1[q], u2[q]};
-            const QueryOut o = finish_query(gp, Kp, c, u, lastIdx, accum, S, nullptr, gc);
-            d0[q] = o.d[0]; d1[q] = o.d[1]; d2[q] = o.d[2];
-            pdf[q] = o.pdf;
-            comp[q] = o.comp;
+        const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
+        serve_full<PDF_ONLY>(gp, Kp, K, io, q, c, wl, sl, T, tid, gc);
+    }
+}
+
+// Fallback queries of the tree wavefront; kmax = the largest K in tab.
+template <bool PDF_ONLY>
+__global__ void __launch_bounds__(64)
+guide_tree_fallback_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __restrict__ tab, int kmax,
+                           GuideIO io, GuideConsts gc, const int* __restrict__ fb_count,
+                           const int32_t* __restrict__ fb_list) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int T = blockDim.x;
+    const int tid = threadIdx.x;
+    float* wl = lds;
+    int* sl = (int*)(lds + (size_t)kmax * T);
+    const int count = *fb_count;
+    for (int idx = blockIdx.x * T + tid; idx < count; idx += gridDim.x * T) {
+        const int64_t q = fb_list[idx];
+        const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
+        const int node = stree_find_point(nodes, c[0], c[1], c[2]);   // a listed query has a mixture
+        for (;;) {
+            const int n0 = __builtin_amdgcn_readfirstlane(node);
+            if (node != n0) continue;
+            const GuideMix mx = tab[n0];
+            serve_full<PDF_ONLY>(mx.gp, mx.Kp, mx.K, io, q, c, wl, sl, T, tid, gc);
+            break;
         }
     }
 }
@@ -530,6 +618,30 @@ static hipError_t coherent_order(const float* const c[3], int n, uint32_t* keys_
     return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, idx_in, idx_out, n, 0, 30, st);
 }
 
+// Workgroup width of the fallback kernels: the widest T <= 64 (a power of
+// two) whose K x T weight + index lists fit the 160 KB LDS (K = 512 -> 32).
+static int fallback_width(int kmax) {
+    int T = 64;
+    while (T > 1 && (size_t)kmax * T * (sizeof(float) + sizeof(int)) > 160 * 1024) T >>= 1;
+    return T;
+}
+
+static GuideIO make_io(const float* const c[3], const float* const u[3], const float* const dgiven[3],
+                       float* const d[3], float* pdf, int32_t* comp) {
+    const bool pdf_only = dgiven != nullptr;
+    GuideIO io{};
+    io.c0 = c[0]; io.c1 = c[1]; io.c2 = c[2];
+    if (pdf_only) {
+        io.e0 = dgiven[0]; io.e1 = dgiven[1]; io.e2 = dgiven[2];
+    } else {
+        io.u0 = u[0]; io.u1 = u[1]; io.u2 = u[2];
+        io.d0 = d[0]; io.d1 = d[1]; io.d2 = d[2];
+        io.comp = comp;
+    }
+    io.pdf = pdf;
+    return io;
+}
+
 // Candidate pass over all queries, then the fallback queries (listed by the
 // candidate kernel) through the full-K path; both on stream st.
 // fb_count: one device int, fb_list: nq device ints (scratch).
@@ -541,7 +653,8 @@ hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float*
     cap = (cap < 0) ? 0 : (cap > kGuideCap ? kGuideCap : cap);
     if (nq > INT32_MAX) return hipErrorInvalidValue;
     const int T = 64;
-    const size_t lds_fb = (size_t)K * T * (sizeof(float) + sizeof(int));
+    const int Tfb = fallback_width(K);
+    const size_t lds_fb = (size_t)K * Tfb * (sizeof(float) + sizeof(int));
     if (lds_fb > 160 * 1024) return hipErrorInvalidValue;
     GuideConsts gc{norm2, norm3};
     hipError_t e = hipMemsetAsync(fb_count, 0, sizeof(int), st);
@@ -553,44 +666,89 @@ hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float*
         if (e != hipSuccess) return e;
         perm = sort->idx[1];
     }
-    const int64_t blocks = (nq + T - 1) / T;
+    const dim3 grid((unsigned)((nq + T - 1) / T));
     const int fb_blocks = cus * 2;
-    const bool pdf_only = dgiven != nullptr;
-    const float* g0 = pdf_only ? dgiven[0] : nullptr;
-    const float* g1 = pdf_only ? dgiven[1] : nullptr;
-    const float* g2 = pdf_only ? dgiven[2] : nullptr;
-    const float* v0 = pdf_only ? nullptr : u[0];
-    const float* v1 = pdf_only ? nullptr : u[1];
-    const float* v2 = pdf_only ? nullptr : u[2];
-    float* o0 = pdf_only ? nullptr : d[0];
-    float* o1 = pdf_only ? nullptr : d[1];
-    float* o2 = pdf_only ? nullptr : d[2];
-    if (pdf_only) {
+    const GuideIO io = make_io(c, u, dgiven, d, pdf, comp);
+    if (dgiven) {
         if (cap <= 24)
-            hipLaunchKernelGGL((guide_cand_kernel<true, 24>), dim3((unsigned)blocks), dim3(T), 0, st, gp, Kp, K, nq,
-                               c[0], c[1], c[2], v0, v1, v2, g0, g1, g2, o0, o1, o2, pdf, comp, gc, cap, fb_count,
-                               fb_list, perm);
-        else
-            hipLaunchKernelGGL((guide_cand_kernel<true, kGuideCap>), dim3((unsigned)blocks), dim3(T), 0, st, gp, Kp,
-                               K, nq, c[0], c[1], c[2], v0, v1, v2, g0, g1, g2, o0, o1, o2, pdf, comp, gc, cap,
+            hipLaunchKernelGGL((guide_cand_kernel<true, 24>), grid, dim3(T), 0, st, gp, Kp, K, nq, io, gc, cap,
                                fb_count, fb_list, perm);
+        else
+            hipLaunchKernelGGL((guide_cand_kernel<true, kGuideCap>), grid, dim3(T), 0, st, gp, Kp, K, nq, io, gc,
+                               cap, fb_count, fb_list, perm);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(guide_fallback_kernel<true>, dim3(fb_blocks), dim3(T), lds_fb, st, gp, Kp, K, c[0],
-                           c[1], c[2], v0, v1, v2, g0, g1, g2, o0, o1, o2, pdf, comp, gc, fb_count, fb_list);
+        hipLaunchKernelGGL(guide_fallback_kernel<true>, dim3(fb_blocks), dim3(Tfb), lds_fb, st, gp, Kp, K, io, gc,
+                           fb_count, fb_list);
     } else {
         if (cap <= 24)
-            hipLaunchKernelGGL((guide_cand_kernel<false, 24>), dim3((unsigned)blocks), dim3(T), 0, st, gp, Kp, K, nq,
-                               c[0], c[1], c[2], v0, v1, v2, g0, g1, g2, o0, o1, o2, pdf, comp, gc, cap, fb_count,
-                               fb_list, perm);
-        else
-            hipLaunchKernelGGL((guide_cand_kernel<false, kGuideCap>), dim3((unsigned)blocks), dim3(T), 0, st, gp,
-                               Kp, K, nq, c[0], c[1], c[2], v0, v1, v2, g0, g1, g2, o0, o1, o2, pdf, comp, gc, cap,
+            hipLaunchKernelGGL((guide_cand_kernel<false, 24>), grid, dim3(T), 0, st, gp, Kp, K, nq, io, gc, cap,
                                fb_count, fb_list, perm);
+        else
+            hipLaunchKernelGGL((guide_cand_kernel<false, kGuideCap>), grid, dim3(T), 0, st, gp, Kp, K, nq, io,
+                               gc, cap, fb_count, fb_list, perm);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(guide_fallback_kernel<false>, dim3(fb_blocks), dim3(T), lds_fb, st, gp, Kp, K, c[0],
-                           c[1], c[2], v0, v1, v2, g0, g1, g2, o0, o1, o2, pdf, comp, gc, fb_count, fb_list);
+        hipLaunchKernelGGL(guide_fallback_kernel<false>, dim3(fb_blocks), dim3(Tfb), lds_fb, st, gp, Kp, K, io,
+                           gc, fb_count, fb_list);
+    }
+    return hipGetLastError();
+}
+
+// The tree wavefront: every query against its own node's mixture (tab, one
+// GuideMix per tree node; kmax = the largest K in it).  Same two-pass shape
+// and the same per-query arithmetic as launch_guide.  sort: always used
+// (Morton order keeps a wave inside one leaf) unless null.
+hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64_t nq, const float* const c[3],
+                             const float* const u[3], const float* const dgiven[3], float* const d[3],
+                             float* pdf, int32_t* comp, int32_t* node_out, float norm2, float norm3, int cap,
+                             int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
+                             const GuideSortScratch* sort) {
+    if (nq <= 0) return hipSuccess;
+    cap = (cap < 0) ? 0 : (cap > kGuideCap ? kGuideCap : cap);
+    if (nq > INT32_MAX) return hipErrorInvalidValue;
+    const int T = 64;
+    if (kmax < 1) kmax = 1;
+    const int Tfb = fallback_width(kmax);
+    const size_t lds_fb = (size_t)kmax * Tfb * (sizeof(float) + sizeof(int));
+    if (lds_fb > 160 * 1024) return hipErrorInvalidValue;
+    GuideConsts gc{norm2, norm3};
+    hipError_t e = hipMemsetAsync(fb_count, 0, sizeof(int), st);
+    if (e != hipSuccess) return e;
+    const int32_t* perm = nullptr;
+    if (sort) {
+        e = coherent_order(c, (int)nq, sort->keys[0], sort->keys[1], sort->idx[0], sort->idx[1], sort->temp,
+                           sort->temp_bytes, st);
+        if (e != hipSuccess) return e;
+        perm = sort->idx[1];
+    }
+    const STNodeDev* nd = (const STNodeDev*)nodes;
+    const GuideMix* tb = (const GuideMix*)tab;
+    const dim3 grid((unsigned)((nq + T - 1) / T));
+    const int fb_blocks = cus * 2;
+    const GuideIO io = make_io(c, u, dgiven, d, pdf, comp);
+    if (dgiven) {
+        if (cap <= 24)
+            hipLaunchKernelGGL((guide_tree_cand_kernel<true, 24>), grid, dim3(T), 0, st, nd, tb, nq, io, gc, cap,
+                               fb_count, fb_list, perm, node_out);
+        else
+            hipLaunchKernelGGL((guide_tree_cand_kernel<true, kGuideCap>), grid, dim3(T), 0, st, nd, tb, nq, io, gc,
+                               cap, fb_count, fb_list, perm, node_out);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(guide_tree_fallback_kernel<true>, dim3(fb_blocks), dim3(Tfb), lds_fb, st, nd, tb, kmax,
+                           io, gc, fb_count, fb_list);
+    } else {
+        if (cap <= 24)
+            hipLaunchKernelGGL((guide_tree_cand_kernel<false, 24>), grid, dim3(T), 0, st, nd, tb, nq, io, gc, cap,
+                               fb_count, fb_list, perm, node_out);
+        else
+            hipLaunchKernelGGL((guide_tree_cand_kernel<false, kGuideCap>), grid, dim3(T), 0, st, nd, tb, nq, io,
+                               gc, cap, fb_count, fb_list, perm, node_out);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(guide_tree_fallback_kernel<false>, dim3(fb_blocks), dim3(Tfb), lds_fb, st, nd, tb,
+                           kmax, io, gc, fb_count, fb_list);
     }
     return hipGetLastError();
 }

@@ -64,6 +64,11 @@ hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float*
                         const float* const u[3], const float* const dgiven[3], float* const d[3], float* pdf,
                         int32_t* comp, float norm2, float norm3, int cap, int* fb_count, int32_t* fb_list,
                         int cus, hipStream_t st, const GuideSortScratch* sort);
+hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64_t nq, const float* const c[3],
+                             const float* const u[3], const float* const dgiven[3], float* const d[3],
+                             float* pdf, int32_t* comp, int32_t* node_out, float norm2, float norm3, int cap,
+                             int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
+                             const GuideSortScratch* sort);
 constexpr int kGuideCapMax = 40;
 hipError_t launch_sample_cdf(const float* cdf, int n, const float* u, int64_t nq, int32_t* out,
                              hipStream_t st);
@@ -307,13 +312,13 @@ int ensure_partials(sdmm_mix* m, int rows) {
 // list...] (cap + 1 ints), then the coherent-order buffers (2 x cap keys,
 // 2 x cap indices, the radix sort's temporary storage).  The previous buffer
 // is only released after a stream sync.
-int ensure_guide_scratch(const sdmm_mix* m, int64_t nq) {
-    if (nq + 1 <= m->guide_fb_cap) return SDMM_OK;
-    if (m->guide_fb) {
-        HIP_TRY(hipStreamSynchronize(m->stream));
-        HIP_TRY(hipFree(m->guide_fb));
-        m->guide_fb = nullptr;
-        m->guide_fb_cap = 0;
+int grow_guide_scratch(int*& fb, int64_t& fb_cap, GuideSortScratch& sort, hipStream_t st, int64_t nq) {
+    if (nq + 1 <= fb_cap) return SDMM_OK;
+    if (fb) {
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipFree(fb));
+        fb = nullptr;
+        fb_cap = 0;
     }
     const int64_t cap = (nq + 1 < (1 << 20)) ? (1 << 20) : nq + 1;
     const size_t a = ((sizeof(int) * (size_t)cap + 255) / 256) * 256;
@@ -321,15 +326,18 @@ int ensure_guide_scratch(const sdmm_mix* m, int64_t nq) {
     const size_t tb = guide_sort_temp_bytes((int)(cap > INT32_MAX ? INT32_MAX : cap));
     char* base = nullptr;
     HIP_TRY(hipMalloc((void**)&base, a + 4 * kb + tb + 256));
-    m->guide_fb = (int*)base;
-    m->guide_sort.keys[0] = (uint32_t*)(base + a);
-    m->guide_sort.keys[1] = (uint32_t*)(base + a + kb);
-    m->guide_sort.idx[0] = (int32_t*)(base + a + 2 * kb);
-    m->guide_sort.idx[1] = (int32_t*)(base + a + 3 * kb);
-    m->guide_sort.temp = base + a + 4 * kb;
-    m->guide_sort.temp_bytes = tb;
-    m->guide_fb_cap = cap;
+    fb = (int*)base;
+    sort.keys[0] = (uint32_t*)(base + a);
+    sort.keys[1] = (uint32_t*)(base + a + kb);
+    sort.idx[0] = (int32_t*)(base + a + 2 * kb);
+    sort.idx[1] = (int32_t*)(base + a + 3 * kb);
+    sort.temp = base + a + 4 * kb;
+    sort.temp_bytes = tb;
+    fb_cap = cap;
     return SDMM_OK;
+}
+int ensure_guide_scratch(const sdmm_mix* m, int64_t nq) {
+    return grow_guide_scratch(m->guide_fb, m->guide_fb_cap, m->guide_sort, m->stream, nq);
 }
 
 // coherent order for batches large enough to fill the chip several times
@@ -997,6 +1005,14 @@ struct STNodeHost {
     int child[2] = {-1, -1};
 };
 
+// host image of guide.hip's GuideMix (one per tree node)
+struct GuideMixHost {
+    const float* gp;
+    int Kp, K;
+    bool operator!=(const GuideMixHost& o) const { return gp != o.gp || Kp != o.Kp || K != o.K; }
+};
+static_assert(sizeof(GuideMixHost) == 16, "GuideMix");
+
 struct sdmm_stree {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -1006,6 +1022,17 @@ struct sdmm_stree {
     bool dirty = true;
     void* scratch = nullptr;
     size_t scratch_bytes = 0;
+    bool own_stream = true;
+    // guided wavefront: per-node mixture table (device + the host copy it
+    // was uploaded from) and the guided-batch scratch
+    std::vector<GuideMixHost> tab_host;
+    void* dtab = nullptr;
+    size_t dtab_cap = 0;
+    int tab_kmax = 0;
+    bool tab_valid = false;     // bound table matches the current nodes
+    int* guide_fb = nullptr;
+    int64_t guide_fb_cap = 0;
+    GuideSortScratch guide_sort{};
 };
 
 namespace {
@@ -1158,7 +1185,9 @@ void sdmm_stree_destroy(sdmm_stree* t) {
     if (t->stream) (void)hipStreamSynchronize(t->stream);
     if (t->dnodes) (void)hipFree(t->dnodes);
     if (t->scratch) (void)hipFree(t->scratch);
-    if (t->stream) (void)hipStreamDestroy(t->stream);
+    if (t->dtab) (void)hipFree(t->dtab);
+    if (t->guide_fb) (void)hipFree(t->guide_fb);
+    if (t->stream && t->own_stream) (void)hipStreamDestroy(t->stream);
     delete t;
 }
 
@@ -1166,6 +1195,7 @@ int sdmm_stree_split_to_depth(sdmm_stree* t, int max_depth) {
     if (!t || max_depth < 0 || max_depth > 8) return fail(SDMM_E_INVALID, "max_depth must be in [0, 8]");
     st_split_depth(t, 0, 0, max_depth);
     t->dirty = true;
+    t->tab_valid = false;
     return SDMM_OK;
 }
 
@@ -1183,6 +1213,7 @@ int sdmm_stree_split(sdmm_stree* t, const float* const p[3], int64_t n, int thre
     for (size_t id = 0; id < n0; ++id)
         if (t->nodes[id].child[0] < 0) st_split_recurse(t, (int)id, per[id], p[0], p[1], p[2], threshold);
     t->dirty = true;
+    t->tab_valid = false;
     return SDMM_OK;
 }
 
@@ -1260,4 +1291,114 @@ int sdmm_stree_route(sdmm_stree* t, const sdmm_samples* in, const sdmm_samples* 
     return SDMM_OK;
 }
 
+
+int sdmm_stree_set_stream(sdmm_stree* t, void* hip_stream) {
+    if (!t) return fail(SDMM_E_INVALID, "invalid argument");
+    HIP_TRY(hipSetDevice(t->device));
+    if (t->stream) {
+        HIP_TRY(hipStreamSynchronize(t->stream));
+        if (t->own_stream) HIP_TRY(hipStreamDestroy(t->stream));
+    }
+    if (hip_stream) {
+        t->stream = (hipStream_t)hip_stream;
+        t->own_stream = false;
+    } else {
+        t->stream = nullptr;   // recreated (own, non-blocking) on next device use
+        t->own_stream = true;
+    }
+    return SDMM_OK;
+}
+
+void* sdmm_stree_get_stream(const sdmm_stree* t) { return t ? (void*)t->stream : nullptr; }
+
 }  // extern "C"
+
+namespace {
+
+// Per-node mixture table for the wavefront; re-uploaded only when it changes
+// (the host copy stays alive as the source of the async copy until then).
+int st_upload_table(sdmm_stree* t, const sdmm_mix* const* node_mix) {
+    const size_t nn = t->nodes.size();
+    std::vector<GuideMixHost> tab(nn);
+    int kmax = 0;
+    for (size_t i = 0; i < nn; ++i) {
+        const sdmm_mix* m = node_mix[i];
+        tab[i] = GuideMixHost{nullptr, 0, 0};
+        if (!m || !m->initialised) continue;
+        if (m->device != t->device) return fail(SDMM_E_INVALID, "wavefront: mixture on another device");
+        tab[i] = GuideMixHost{m->gp, m->Kp, m->K};
+        kmax = std::max(kmax, m->K);
+    }
+    bool same = tab.size() == t->tab_host.size();
+    for (size_t i = 0; same && i < nn; ++i) same = !(tab[i] != t->tab_host[i]);
+    t->tab_kmax = kmax;
+    t->tab_valid = true;
+    if (same && t->dtab) return SDMM_OK;
+    HIP_TRY(hipStreamSynchronize(t->stream));   // the previous copy may still read tab_host
+    const size_t bytes = sizeof(GuideMixHost) * (nn ? nn : 1);
+    if (bytes > t->dtab_cap) {
+        if (t->dtab) HIP_TRY(hipFree(t->dtab));
+        t->dtab = nullptr;
+        HIP_TRY(hipMalloc(&t->dtab, bytes));
+        t->dtab_cap = bytes;
+    }
+    t->tab_host.swap(tab);
+    HIP_TRY(hipMemcpyAsync(t->dtab, t->tab_host.data(), sizeof(GuideMixHost) * nn, hipMemcpyHostToDevice,
+                           t->stream));
+    return SDMM_OK;
+}
+
+int st_guide(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
+             const float* const u[3], const float* const dgiven[3], float* const d[3], float* pdf, int32_t* comp,
+             int32_t* node_out) {
+    HIP_TRY(hipSetDevice(t->device));
+    int r = st_upload(t);
+    if (r) return r;
+    if (node_mix) {
+        r = st_upload_table(t, node_mix);
+        if (r) return r;
+    } else if (!t->tab_valid) {
+        return fail(SDMM_E_STATE, "wavefront: no mixtures bound to the current tree (sdmm_stree_bind_mixtures)");
+    }
+    r = grow_guide_scratch(t->guide_fb, t->guide_fb_cap, t->guide_sort, t->stream, nq);
+    if (r) return r;
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, t->device);
+    const GuideSortScratch* sort = nq >= (1 << 14) ? &t->guide_sort : nullptr;
+    HIP_TRY(launch_guide_tree(t->dnodes, t->dtab, t->tab_kmax, nq, c, u, dgiven, d, pdf, comp, node_out,
+                              norm_const(2), norm_const(3), kGuideCapMax, t->guide_fb, t->guide_fb + 1,
+                              cus > 0 ? cus : 256, t->stream, sort));
+    return SDMM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sdmm_stree_bind_mixtures(sdmm_stree* t, const sdmm_mix* const* node_mix) {
+    if (!t || !node_mix) return fail(SDMM_E_INVALID, "invalid argument");
+    HIP_TRY(hipSetDevice(t->device));
+    int r = st_upload(t);
+    if (r) return r;
+    return st_upload_table(t, node_mix);
+}
+
+int sdmm_guide_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
+                         const float* const u[3], float* const d[3], float* pdf, int32_t* comp,
+                         int32_t* node_out) {
+    if (!t || nq < 0) return fail(SDMM_E_INVALID, "invalid argument");
+    if (nq == 0) return SDMM_OK;
+    if (!c || !u || !d || !pdf || !comp) return fail(SDMM_E_INVALID, "invalid argument");
+    return st_guide(t, node_mix, nq, c, u, nullptr, d, pdf, comp, node_out);
+}
+
+int sdmm_pdf_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
+                       const float* const d[3], float* pdf) {
+    if (!t || nq < 0) return fail(SDMM_E_INVALID, "invalid argument");
+    if (nq == 0) return SDMM_OK;
+    if (!c || !d || !pdf) return fail(SDMM_E_INVALID, "invalid argument");
+    return st_guide(t, node_mix, nq, c, nullptr, d, nullptr, pdf, nullptr, nullptr);
+}
+
+}  // extern "C"
+

@@ -147,6 +147,35 @@ struct GuideSortScratch {
     size_t temp_bytes;
 };
 
+// ---- spatial tree node (stree.hip, guide.hip) ------------------------------
+// min[3], max[3], child0, child1 (-1 for a leaf); SNTreeNode::find
+// (jmm/sntree.h:62-83) as a single descent.
+struct STNodeDev {
+    float mn[3], mx[3];
+    int c0, c1;
+};
+static_assert(sizeof(STNodeDev) == 32, "node record");
+
+__device__ __forceinline__ bool box_contains(const STNodeDev& n, float x, float y, float z) {
+    return n.mn[0] <= x && x <= n.mx[0] && n.mn[1] <= y && y <= n.mx[1] && n.mn[2] <= z && z <= n.mx[2];
+}
+
+__device__ __forceinline__ int stree_find_point(const STNodeDev* __restrict__ nodes, float x, float y, float z) {
+    STNodeDev n = nodes[0];
+    if (!box_contains(n, x, y, z)) return -1;
+    int id = 0;
+    for (int guard = 0; guard < 4096; ++guard) {
+        if (n.c0 < 0) return id;
+        const STNodeDev a = nodes[n.c0];
+        if (box_contains(a, x, y, z)) { id = n.c0; n = a; continue; }
+        const int c1 = n.c1;
+        const STNodeDev b = nodes[c1];
+        if (box_contains(b, x, y, z)) { id = c1; n = b; continue; }
+        return -1;
+    }
+    return -1;
+}
+
 constexpr float kHeuristicWeight = 0.5f;     // mixture_model.h:398
 constexpr double kPi = 3.14159265358979323846;
 

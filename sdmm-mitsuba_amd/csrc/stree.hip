@@ -15,31 +15,7 @@
 
 namespace sdmm {
 
-struct STNodeDev {
-    float mn[3], mx[3];
-    int c0, c1;
-};
-static_assert(sizeof(STNodeDev) == 32, "node record");
-
-__device__ __forceinline__ bool box_contains(const STNodeDev& n, float x, float y, float z) {
-    return n.mn[0] <= x && x <= n.mx[0] && n.mn[1] <= y && y <= n.mx[1] && n.mn[2] <= z && z <= n.mx[2];
-}
-
-__device__ __forceinline__ int stree_find_point(const STNodeDev* __restrict__ nodes, float x, float y, float z) {
-    STNodeDev n = nodes[0];
-    if (!box_contains(n, x, y, z)) return -1;
-    int id = 0;
-    for (int guard = 0; guard < 4096; ++guard) {
-        if (n.c0 < 0) return id;
-        const STNodeDev a = nodes[n.c0];
-        if (box_contains(a, x, y, z)) { id = n.c0; n = a; continue; }
-        const int c1 = n.c1;
-        const STNodeDev b = nodes[c1];
-        if (box_contains(b, x, y, z)) { id = c1; n = b; continue; }
-        return -1;
-    }
-    return -1;
-}
+// STNodeDev, box_contains, stree_find_point: sdmm_device.h (shared with guide.hip)
 
 __global__ void stree_find_kernel(const STNodeDev* __restrict__ nodes, int64_t n, const float* __restrict__ p0,
                                   const float* __restrict__ p1, const float* __restrict__ p2,

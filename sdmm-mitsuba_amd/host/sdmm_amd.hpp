@@ -189,6 +189,58 @@ inline void sample_guided(const Mixture& m, const GuidingBatch& q) {
           "sdmm_guide_batch");
 }
 
+// The guiding accelerator (the plugin's m_accelerator STree: split_to_depth,
+// split(threshold), find; volpath_sdmm.cpp:355-358,161,226, sdmm_proc.cpp:314)
+// with one Mixture per node, and the guided wavefront over its leaves: every
+// query is served by the mixture of the leaf its condition falls in
+// (sampleSurface, sdmm_proc.cpp:309-421), BSDF-only (comp -1, pdf 0) where
+// the leaf has none.
+class SpatialTree {
+public:
+    SpatialTree(const float aabb_min[3], const float aabb_max[3], int device = 0) {
+        check(sdmm_stree_create(aabb_min, aabb_max, device, &t_), "sdmm_stree_create");
+    }
+    ~SpatialTree() { sdmm_stree_destroy(t_); }
+    SpatialTree(const SpatialTree&) = delete;
+    SpatialTree& operator=(const SpatialTree&) = delete;
+
+    sdmm_stree* handle() { return t_; }
+    int nodes() const { return sdmm_stree_num_nodes(t_); }
+    void set_stream(void* hip_stream) { check(sdmm_stree_set_stream(t_, hip_stream), "sdmm_stree_set_stream"); }
+    void split_to_depth(int depth) { check(sdmm_stree_split_to_depth(t_, depth), "sdmm_stree_split_to_depth"); }
+    // split(threshold) over host positions (the plugin's context.stats)
+    void split(const float* const p[3], int64_t n, int threshold) {
+        check(sdmm_stree_split(t_, p, n, threshold), "sdmm_stree_split");
+    }
+    bool is_leaf(int node) const {
+        std::vector<int32_t> child(2 * (size_t)nodes());
+        check(sdmm_stree_get_nodes(t_, nullptr, child.data(), nullptr), "sdmm_stree_get_nodes");
+        return child[2 * (size_t)node] < 0;
+    }
+    // device points -> node ids (-1 outside)
+    void find(int64_t n, const float* const p[3], int32_t* node_out) {
+        check(sdmm_stree_find(t_, n, p, node_out), "sdmm_stree_find");
+    }
+    // one entry per node, nullptr where there is no trained mixture
+    void bind(const std::vector<Mixture*>& node_mix) {
+        if ((int)node_mix.size() != nodes()) throw Error(SDMM_E_INVALID, "bind: one mixture slot per node");
+        std::vector<const sdmm_mix*> h(node_mix.size());
+        for (size_t i = 0; i < h.size(); ++i) h[i] = node_mix[i] ? node_mix[i]->handle() : nullptr;
+        check(sdmm_stree_bind_mixtures(t_, h.data()), "sdmm_stree_bind_mixtures");
+    }
+    // the wavefront against the bound mixtures; node_out optional
+    void sample_guided(const GuidingBatch& q, int32_t* node_out = nullptr) {
+        check(sdmm_guide_wavefront(t_, nullptr, q.n, q.c, q.u, q.d, q.pdf, q.comp, node_out),
+              "sdmm_guide_wavefront");
+    }
+    void pdf_guided(int64_t n, const float* const c[3], const float* const d[3], float* pdf) {
+        check(sdmm_pdf_wavefront(t_, nullptr, n, c, d, pdf), "sdmm_pdf_wavefront");
+    }
+
+private:
+    sdmm_stree* t_ = nullptr;
+};
+
 // pdfSurface's mixing of BSDF and guiding densities (sdmm_proc.cpp:587-589):
 // pdf = h * bsdfPdf + (1 - h) * gmmPdf, h = 0.5 (0.3 with product sampling).
 inline float mixed_pdf(float heuristicConditionalWeight, float bsdfPdf, float gmmPdf) {

@@ -74,3 +74,15 @@ def test_shard_ranges_partition_the_batch(pkg):
             assert rs[0][0] == 0 and rs[-1][1] == n
             for (a, b), (c, d) in zip(rs, rs[1:]):
                 assert b == c and a <= b
+
+
+def test_cpp_mirror_header_compiles(tmp_path):
+    """The C++ host mirror (sdmm-mitsuba_amd/host/sdmm_amd.hpp) compiles and
+    links against the C ABI without a GPU (the plugin-side include)."""
+    import subprocess
+    src = tmp_path / "m.cpp"
+    src.write_text('#include "sdmm_amd.hpp"\nint main() { return sdmm_abi_version() == 1 ? 0 : 1; }\n')
+    lib = ROOT / "sdmm-mitsuba_amd" / "lib"
+    exe = tmp_path / "m"
+    subprocess.run(["g++", "-std=c++17", f"-I{ROOT / 'sdmm-mitsuba_amd' / 'host'}", f"-I{ROOT / 'include'}",
+                    str(src), f"-L{lib}", "-lsdmm_amd", f"-Wl,-rpath,{lib}", "-o", str(exe)], check=True)
