@@ -167,6 +167,39 @@ int sdmm_guide_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], con
 /* gmmPdf of given directions d (device SoA). */
 int sdmm_pdf_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], const float* const d[3],
                    float* pdf);
+/* Product sampling with a learned BSDF -- sampleSurface / pdfSurface with
+ * sampleProduct (sdmm_proc.cpp:327-392, :474-486): the query's conditional
+ * times the learned-BSDF lobes of its material (sdmm::product, absent;
+ * restated from jmm MixtureModel::multiply, mixture_model.h:345-370, and
+ * MVTN::multiply, multivariate_tangent_normal.h:555-617), then sample / pdf
+ * of the product.  Device arrays:
+ *   bsdf      B materials x M (<= 64) directional lobes in the LOCAL shading
+ *             frame, already oriented for wi (sdmm-lib's rotate_to_wo is the
+ *             caller's): weights [B][M], unit means [B][M][3], 2x2 covariances
+ *             [B][M][4] in each lobe's tangent frame Coordinates(mean)
+ *   material  per query; < 0 (or >= B): no learned BSDF
+ *   frame[9]  per-query to-world matrix F, row-major, columns s, t, n
+ *             (sdmm_proc.cpp:348-352); lobes go to world as mean F m,
+ *             frame to F^T (:353-356)
+ *   heuristic (nullable) per query heuristicConditionalWeight (:383-392):
+ *             0.3 product, 0.5 plain conditional (no BSDF / empty product),
+ *             1 no valid conditional (BSDF only)
+ * comp = k * M + j (joint component k, lobe j) for product samples, the
+ * joint index for plain-conditional samples, -1 for BSDF only.  Bit-exact
+ * against oracle/sdmm_oracle_product.inc in comp; pdf of given directions
+ * d with sdmm_pdf_product_batch. */
+typedef struct {
+    const float* weights;
+    const float* means;
+    const float* covs;
+    int B, M;
+} sdmm_bsdf_table;
+int sdmm_guide_product_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], const float* const u[3],
+                             const sdmm_bsdf_table* bsdf, const int32_t* material, const float* const frame[9],
+                             float* const d[3], float* pdf, int32_t* comp, float* heuristic);
+int sdmm_pdf_product_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], const float* const d[3],
+                           const sdmm_bsdf_table* bsdf, const int32_t* material, const float* const frame[9],
+                           float* pdf, float* heuristic);
 /* lower_bound + tie walk of utils.h:104-115 on a caller CDF (device). */
 int sdmm_sample_discrete_cdf(const sdmm_mix* m, const float* cdf, int n, const float* u, int64_t nq,
                              int32_t* out);

@@ -89,6 +89,10 @@ def lib():
         L.or_ts_exp.argtypes = [_f, _f, _f, _f]
         L.or_coordinates.argtypes = [_f, _f]
         L.or_component_set.argtypes = [C.c_void_p, C.c_int, _d, _d, C.c_int]
+        L.or_guide_product_batch.argtypes = [C.c_void_p, C.c_int64, _f, _f, C.POINTER(C.c_int32), _f, _f, _f,
+                                             _f, C.c_int, _f, _f, _f, C.POINTER(C.c_int32), _f]
+        L.or_mvtn_multiply.restype = C.c_float
+        L.or_mvtn_multiply.argtypes = [_f, _f, _f, _f, _f]
         _lib = L
     return _lib
 
@@ -249,6 +253,41 @@ def guide_batch(m: Mixture, c: np.ndarray, u: np.ndarray):
     lib().or_guide_batch(m.ptr, nq, _fp(c), _fp(u), _fp(d), _fp(pdf),
                          comp.ctypes.data_as(I32), slot.ctypes.data_as(I32))
     return d, pdf, comp, slot
+
+
+def guide_product_batch(m: Mixture, c, u, material, frames, bw, bmean, bcov, dgiven=None):
+    """Product sampling with a learned-BSDF table (sdmm_oracle_product.inc).
+    c, u: (nq, 3); material: (nq,) int (-1: none); frames: (nq, 9) row-major
+    to-world [s t n] columns; bw (B, M), bmean (B, M, 3) local, bcov (B, M, 4).
+    Returns dir (nq, 3), pdf, comp (k * M + j for product samples), h."""
+    c = np.ascontiguousarray(c, np.float32)
+    u = np.ascontiguousarray(u, np.float32)
+    nq = c.shape[0]
+    material = np.ascontiguousarray(material, np.int32)
+    frames = np.ascontiguousarray(frames, np.float32)
+    bw = np.ascontiguousarray(bw, np.float32)
+    M = bw.shape[1]
+    bmean = np.ascontiguousarray(bmean, np.float32)
+    bcov = np.ascontiguousarray(bcov, np.float32)
+    d = np.zeros((nq, 3), np.float32)
+    pdf = np.zeros(nq, np.float32)
+    comp = np.zeros(nq, np.int32)
+    h = np.zeros(nq, np.float32)
+    I32 = C.POINTER(C.c_int32)
+    dg = None if dgiven is None else np.ascontiguousarray(dgiven, np.float32)
+    lib().or_guide_product_batch(m.ptr, nq, _fp(c), _fp(u), material.ctypes.data_as(I32), _fp(frames), _fp(bw),
+                                 _fp(bmean), _fp(bcov), M, None if dg is None else _fp(dg), _fp(d), _fp(pdf),
+                                 comp.ctypes.data_as(I32), _fp(h))
+    return d, pdf, comp, h
+
+
+def mvtn_multiply(e, ci, mj, cj):
+    """MVTN::multiply test hook: (weight, product mean (3), L (2x2), Linv (2x2), detInv)."""
+    out = np.zeros(13, np.float32)
+    f = lambda a: np.ascontiguousarray(a, np.float32)
+    e, ci, mj, cj = f(e), f(ci), f(mj), f(cj)
+    lib().or_mvtn_multiply(_fp(e), _fp(ci), _fp(mj), _fp(cj), _fp(out))
+    return float(out[0]), out[1:4].copy(), out[4:8].reshape(2, 2).copy(), out[8:12].reshape(2, 2).copy(), float(out[12])
 
 
 def pdf_batch(m: Mixture, c: np.ndarray, d: np.ndarray):

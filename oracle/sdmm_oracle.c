@@ -843,3 +843,5 @@ void or_pdf_batch(const or_mixture* m, int64_t nq, const float* c, const float* 
     }
     cond_free(&cd);
 }
+
+#include "sdmm_oracle_product.inc"

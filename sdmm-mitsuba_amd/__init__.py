@@ -112,6 +112,11 @@ def lib():
         L.sdmm_stree_get_stream.argtypes = [C.c_void_p]
         L.sdmm_guide_wavefront.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p * 3, C.c_void_p * 3,
                                            C.c_void_p * 3, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.sdmm_guide_product_batch.argtypes = [C.c_void_p, C.c_int64, C.c_void_p * 3, C.c_void_p * 3, C.c_void_p,
+                                               C.c_void_p, C.c_void_p * 9, C.c_void_p * 3, C.c_void_p, C.c_void_p,
+                                               C.c_void_p]
+        L.sdmm_pdf_product_batch.argtypes = [C.c_void_p, C.c_int64, C.c_void_p * 3, C.c_void_p * 3, C.c_void_p,
+                                             C.c_void_p, C.c_void_p * 9, C.c_void_p, C.c_void_p]
         L.sdmm_stree_bind_mixtures.argtypes = [C.c_void_p, C.c_void_p]
         L.sdmm_pdf_wavefront.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p * 3, C.c_void_p * 3,
                                          C.c_void_p]
@@ -142,7 +147,7 @@ EXPORTED_SYMBOLS = [
     "sdmm_stree_create", "sdmm_stree_destroy", "sdmm_stree_split_to_depth", "sdmm_stree_split",
     "sdmm_stree_num_nodes", "sdmm_stree_get_nodes", "sdmm_stree_find", "sdmm_stree_route",
     "sdmm_stree_set_stream", "sdmm_stree_get_stream", "sdmm_guide_wavefront", "sdmm_pdf_wavefront",
-    "sdmm_stree_bind_mixtures",
+    "sdmm_stree_bind_mixtures", "sdmm_guide_product_batch", "sdmm_pdf_product_batch",
 ]
 
 
@@ -385,6 +390,37 @@ class SDMM:
         _check(lib().sdmm_pdf_batch(self.h, nq, cc, dd, out.data_ptr()))
         return out
 
+    def guide_product(self, c, u, bsdf, material, frame, out=None):
+        """Product sampling with a learned BSDF (sdmm_guide_product_batch).
+        bsdf: BsdfTable; material: int32 device tensor; frame: 9 device planes.
+        Returns (d planes, pdf, comp, heuristic)."""
+        import torch
+        nq = c[0].numel()
+        if out is None:
+            dev = c[0].device
+            out = ([torch.empty(nq, device=dev) for _ in range(3)], torch.empty(nq, device=dev),
+                   torch.empty(nq, device=dev, dtype=torch.int32), torch.empty(nq, device=dev))
+        d, pdf, comp, h = out
+        cc = (C.c_void_p * 3)(*[t.data_ptr() for t in c])
+        uu = (C.c_void_p * 3)(*[t.data_ptr() for t in u])
+        dd = (C.c_void_p * 3)(*[t.data_ptr() for t in d])
+        ff = (C.c_void_p * 9)(*[t.data_ptr() for t in frame])
+        _check(lib().sdmm_guide_product_batch(self.h, nq, cc, uu, C.byref(bsdf.c), material.data_ptr(), ff, dd,
+                                              pdf.data_ptr(), comp.data_ptr(), h.data_ptr()))
+        return d, pdf, comp, h
+
+    def pdf_product(self, c, d, bsdf, material, frame):
+        import torch
+        nq = c[0].numel()
+        pdf = torch.empty(nq, device=c[0].device)
+        h = torch.empty(nq, device=c[0].device)
+        cc = (C.c_void_p * 3)(*[t.data_ptr() for t in c])
+        dd = (C.c_void_p * 3)(*[t.data_ptr() for t in d])
+        ff = (C.c_void_p * 9)(*[t.data_ptr() for t in frame])
+        _check(lib().sdmm_pdf_product_batch(self.h, nq, cc, dd, C.byref(bsdf.c), material.data_ptr(), ff,
+                                            pdf.data_ptr(), h.data_ptr()))
+        return pdf, h
+
     def sample_discrete_cdf(self, cdf, u, out=None):
         import torch
         if out is None:
@@ -392,6 +428,25 @@ class SDMM:
         _check(lib().sdmm_sample_discrete_cdf(self.h, cdf.data_ptr(), cdf.numel(), u.data_ptr(),
                                               u.numel(), out.data_ptr()))
         return out
+
+
+class _BsdfTable(C.Structure):
+    _fields_ = [("weights", C.c_void_p), ("means", C.c_void_p), ("covs", C.c_void_p), ("B", C.c_int),
+                ("M", C.c_int)]
+
+
+class BsdfTable:
+    """Learned-BSDF lobes on the device (sdmm_bsdf_table): weights (B, M),
+    local unit means (B, M, 3), 2x2 covariances (B, M, 4)."""
+
+    def __init__(self, weights, means, covs, device="cuda"):
+        import torch
+        w = np.ascontiguousarray(weights, np.float32)
+        self.B, self.M = w.shape
+        self.w = torch.from_numpy(w.copy()).to(device)
+        self.mean = torch.from_numpy(np.ascontiguousarray(means, np.float32).reshape(self.B, self.M, 3).copy()).to(device)
+        self.cov = torch.from_numpy(np.ascontiguousarray(covs, np.float32).reshape(self.B, self.M, 4).copy()).to(device)
+        self.c = _BsdfTable(self.w.data_ptr(), self.mean.data_ptr(), self.cov.data_ptr(), self.B, self.M)
 
 
 class STree:

@@ -549,6 +549,419 @@ guide_tree_fallback_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* 
     }
 }
 
+// ---------------------------------------------------------------------------
+// Product with a learned BSDF (the plugin's sampleProduct path,
+// sdmm_proc.cpp:327-392, :474-486): MixtureModel::multiply of the query's
+// conditional with a learned-BSDF lobe set (mixture_model.h:345-370,
+// multivariate_tangent_normal.h:555-617), then sample / pdf of the product.
+// Follows oracle/sdmm_oracle_product.inc operation for operation (contract
+// off, the oracle's correctly rounded float transcendentals as
+// (float)f((double)x), IEEE division / sqrt), so the product weights -- and
+// with them the selected (joint component, lobe) index -- are bit-identical.
+// The product is never materialised: one pass sums the weights, a second
+// walks the CDF to the sampled pair, a third accumulates the pdf at the
+// sampled direction, each recomputing the pairs (a pair is ~40 small
+// matrix/vector ops; the kept conditional x lobes is tens of pairs).
+
+struct BsdfTab {
+    const float* w;      // [B][M]
+    const float* mean;   // [B][M][3]  local shading frame
+    const float* cov;    // [B][M][4]  2x2 in the lobe's own tangent frame
+    int B, M;
+};
+
+struct ProductIO {
+    const int32_t* material;   // per query; < 0: no learned BSDF
+    const float* F[9];         // per-query to-world frame, row-major [s t n]
+    float* h;                  // heuristicConditionalWeight per query
+};
+
+__device__ __forceinline__ float acos_x(float x) { return (float)acos((double)x); }
+__device__ __forceinline__ float sin_x(float x) { return (float)sin((double)x); }
+__device__ __forceinline__ float cos_x(float x) { return (float)cos((double)x); }
+__device__ __forceinline__ float log_x(float x) { return (float)log((double)x); }
+
+__device__ __forceinline__ float sinc_pi_x(float x) {
+    const float taylor_0_bound = 1.1920928955078125e-07f;
+    const float taylor_2_bound = 3.4526698300124393e-04f;
+    const float taylor_n_bound = 1.8581361171917516e-02f;
+    const float ax = fabsf(x);
+    if (ax >= taylor_n_bound) return sin_x(x) / x;
+    float result = 1.0f;
+    if (ax >= taylor_0_bound) {
+        const float x2 = x * x;
+        result -= x2 / 6.0f;
+        if (ax >= taylor_2_bound) result += (x2 * x2) / 120.0f;
+    }
+    return result;
+}
+
+// or_ts_log (TangentSpace::log, mvtn.h:146-177), directional part
+__device__ __forceinline__ bool ts_log_x(const float to[9], const float d[3], float& t0, float& t1,
+                                         float& jac) {
+    if (d[0] == 0.0f && d[1] == 0.0f && d[2] == 0.0f) return false;
+    const float r0 = to[0] * d[0] + to[1] * d[1] + to[2] * d[2];
+    const float r1 = to[3] * d[0] + to[4] * d[1] + to[5] * d[2];
+    float c = to[6] * d[0] + to[7] * d[1] + to[8] * d[2];
+    if (c <= -1.0f) return false;
+    c = (c < 1.0f) ? c : 1.0f;
+    const float angle = acos_x(c);
+    const float s = sqrtf(1.0f - c * c);
+    const float a = ((double)s < 1e-3) ? 1.0f : (angle / s);
+    t0 = r0 * a;
+    t1 = r1 * a;
+    jac = a;
+    return true;
+}
+
+// or_ts_exp (TangentSpace::exp, mvtn.h:93-120), directional part
+__device__ __forceinline__ bool ts_exp_x(const float to[9], float t0, float t1, float e[3]) {
+    const float length = sqrtf(t0 * t0 + t1 * t1);
+    if ((double)length >= kPi) { e[0] = e[1] = e[2] = 0.0f; return false; }
+    const float s = sinc_pi_x(length);
+    const float rel0 = t0 * s, rel1 = t1 * s, rel2 = cos_x(length);
+    e[0] = to[0] * rel0 + to[3] * rel1 + to[6] * rel2;
+    e[1] = to[1] * rel0 + to[4] * rel1 + to[7] * rel2;
+    e[2] = to[2] * rel0 + to[5] * rel1 + to[8] * rel2;
+    return true;
+}
+
+// the conditional mean direction of joint component k with the oracle's
+// transcendentals (cond_mean_dir uses the fast float ones)
+__device__ __forceinline__ void cond_mean_dir_x(const float* gp, int Kp, int k, const float c[3], float e[3]) {
+    const float d0 = c[0] - gp_ld(gp, Kp, GP_MU0, k);
+    const float d1 = c[1] - gp_ld(gp, Kp, GP_MU1, k);
+    const float d2 = c[2] - gp_ld(gp, Kp, GP_MU2, k);
+    const float t0 = gp_ld(gp, Kp, GP_P00, k) * d0 + gp_ld(gp, Kp, GP_P01, k) * d1 + gp_ld(gp, Kp, GP_P02, k) * d2;
+    const float t1 = gp_ld(gp, Kp, GP_P10, k) * d0 + gp_ld(gp, Kp, GP_P11, k) * d1 + gp_ld(gp, Kp, GP_P12, k) * d2;
+    float to[9];
+    for (int i = 0; i < 9; ++i) to[i] = gp_ld(gp, Kp, GP_T00 + i, k);
+    ts_exp_x(to, t0, t1, e);
+}
+
+__device__ __forceinline__ void m22_mul(const float* a, const float* b, float* r) {
+    r[0] = a[0] * b[0] + a[1] * b[2];
+    r[1] = a[0] * b[1] + a[1] * b[3];
+    r[2] = a[2] * b[0] + a[3] * b[2];
+    r[3] = a[2] * b[1] + a[3] * b[3];
+}
+__device__ __forceinline__ void m22_mul_t(const float* a, const float* b, float* r) {
+    r[0] = a[0] * b[0] + a[1] * b[1];
+    r[1] = a[0] * b[2] + a[1] * b[3];
+    r[2] = a[2] * b[0] + a[3] * b[1];
+    r[3] = a[2] * b[2] + a[3] * b[3];
+}
+__device__ __forceinline__ void m22_inv(const float* m, float* r) {
+    const float invdet = 1.0f / (m[0] * m[3] - m[2] * m[1]);
+    r[0] = m[3] * invdet;
+    r[1] = -m[1] * invdet;
+    r[2] = -m[2] * invdet;
+    r[3] = m[0] * invdet;
+}
+__device__ __forceinline__ bool llt22(const float* A, float* L) {
+    float x = A[0];
+    if (!(x > 0.0f)) return false;
+    const float l00 = sqrtf(x);
+    const float l10 = A[2] / l00;
+    x = A[3] - l10 * l10;
+    if (!(x > 0.0f)) return false;
+    L[0] = l00; L[1] = 0.0f; L[2] = l10; L[3] = sqrtf(x);
+    return true;
+}
+__device__ __forceinline__ void m23_33(const float* a, const float* b, float* r) {
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 3; ++j)
+            r[3 * i + j] = a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j] + a[3 * i + 2] * b[6 + j];
+}
+__device__ __forceinline__ void m23_32(const float* a, const float* b, float* r) {
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 2; ++j)
+            r[2 * i + j] = a[3 * i] * b[j] + a[3 * i + 1] * b[2 + j] + a[3 * i + 2] * b[4 + j];
+}
+// TangentSpace::logJacobian (mvtn.h:211-246), 2x3
+__device__ __forceinline__ void log_jacobian(const float to[9], const float mean[3], const float x[3],
+                                             float J[6]) {
+    const float r0 = to[0] * x[0] + to[1] * x[1] + to[2] * x[2];
+    const float r1 = to[3] * x[0] + to[4] * x[1] + to[5] * x[2];
+    float c = to[6] * x[0] + to[7] * x[1] + to[8] * x[2];
+    c = (c < 1.0f) ? c : 1.0f;
+    for (int i = 0; i < 6; ++i) J[i] = 0.0f;
+    if (c <= -1.0f) return;
+    if (c == 1.0f || (x[0] == mean[0] && x[1] == mean[1] && x[2] == mean[2])) {
+        J[0] = 1.0f; J[4] = 1.0f;
+        return;
+    }
+    const float angle = acos_x(c);
+    const float aos = 1.0f / sinc_pi_x(angle);
+    J[0] = aos; J[4] = aos;
+    const float iss = 1.0f / (1.0f - c * c);
+    J[2] = r0 * c * aos * iss - r0 * iss;
+    J[5] = r1 * c * aos * iss - r1 * iss;
+}
+// TangentSpace::expJacobian (mvtn.h:179-209), 3x2
+__device__ __forceinline__ void exp_jacobian(float t0, float t1, float J[6]) {
+    const float length = sqrtf(t0 * t0 + t1 * t1);
+    for (int i = 0; i < 6; ++i) J[i] = 0.0f;
+    if (length == 0.0f) {
+        J[0] = 1.0f; J[3] = 1.0f;
+        return;
+    }
+    const float lsq = length * length;
+    const float cs = cos_x(length);
+    const float sinc = sinc_pi_x(length);
+    const float cms = (cs - sinc) / lsq;
+    J[0] = sinc + t0 * t0 * cms;
+    J[3] = sinc + t1 * t1 * cms;
+    const float off = t0 * t1 * cms;
+    J[2] = off;
+    J[1] = off;
+    J[4] = -t0 * sinc;
+    J[5] = -t1 * sinc;
+}
+
+// One product component: the conditional slot (e, to_i, ci) times the world
+// lobe (mj, to_j, cj).  Returns the weight factor newWeight (0: dropped).
+struct ProdComp {
+    float mean[3];
+    float L[4];
+    float Linv[4];
+    float detInv;
+};
+__device__ __noinline__ float mvtn_multiply(const float e[3], const float to_i[9], const float ci[4],
+                                            const float mj[3], const float to_j[9], const float cj[4],
+                                            float norm2, ProdComp& out) {
+    float om0, om1, jac;
+    if (!ts_log_x(to_i, mj, om0, om1, jac)) return 0.0f;
+    float lj[6], a[6], from_j[9], b[6], ej[6], J[4], t[4], ocov[4];
+    log_jacobian(to_i, e, mj, lj);
+    m23_33(lj, to_i, a);
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) from_j[3 * r + c] = to_j[3 * c + r];
+    m23_33(a, from_j, b);
+    exp_jacobian(0.0f, 0.0f, ej);
+    m23_32(b, ej, J);
+    m22_mul(J, cj, t);
+    m22_mul_t(t, J, ocov);
+    float csum[4], icsum[4], ci_ics[4], cnt[4];
+    for (int i = 0; i < 4; ++i) csum[i] = ci[i] + ocov[i];
+    m22_inv(csum, icsum);
+    m22_mul(ci, icsum, ci_ics);
+    const float mt0 = 0.0f + (ci_ics[0] * om0 + ci_ics[1] * om1);
+    const float mt1 = 0.0f + (ci_ics[2] * om0 + ci_ics[3] * om1);
+    m22_mul(ci_ics, ocov, cnt);
+    if (!ts_exp_x(to_i, mt0, mt1, out.mean)) return 0.0f;
+    float to_n[9];
+    coordinates_f(out.mean, to_n);
+    float ln[6], a2[6], from_i[9], b2[6], ei[6], J2[4], t2[4], cov_n[4];
+    log_jacobian(to_n, out.mean, out.mean, ln);
+    m23_33(ln, to_n, a2);
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) from_i[3 * r + c] = to_i[3 * c + r];
+    m23_33(a2, from_i, b2);
+    exp_jacobian(mt0, mt1, ei);
+    m23_32(b2, ei, J2);
+    m22_mul(J2, cnt, t2);
+    m22_mul_t(t2, J2, cov_n);
+    float Ls[4];
+    if (!llt22(csum, Ls)) return 0.0f;
+    const float invDet = 1.0f / (Ls[0] * Ls[3]);
+    const float s0 = om0 / Ls[0];
+    const float s1 = (om1 - Ls[2] * s0) / Ls[3];
+    float w = (float)((double)norm2 * exp(-0.5 * (double)(s0 * s0 + s1 * s1)));
+    w = w * (invDet * jac);
+    if (!llt22(cov_n, out.L)) return 0.0f;
+    m22_inv(out.L, out.Linv);
+    out.detInv = 1.0f / (out.L[0] * out.L[3]);
+    return w;
+}
+
+// the world-frame lobe j of material b: mean F m, frame Coordinates(m) F^T
+__device__ __forceinline__ void bsdf_world(const float F[9], const BsdfTab& bt, int b, int j, float mw[3],
+                                           float tw[9], float cj[4], float& wj) {
+    const int idx = b * bt.M + j;
+    wj = bt.w[idx];
+    const float ml[3] = {bt.mean[3 * idx], bt.mean[3 * idx + 1], bt.mean[3 * idx + 2]};
+    for (int i = 0; i < 4; ++i) cj[i] = bt.cov[4 * idx + i];
+    float tl[9];
+    coordinates_f(ml, tl);
+    for (int i = 0; i < 3; ++i) mw[i] = F[3 * i] * ml[0] + F[3 * i + 1] * ml[1] + F[3 * i + 2] * ml[2];
+    for (int i = 0; i < 3; ++i)
+        for (int jj = 0; jj < 3; ++jj)
+            tw[3 * i + jj] = tl[3 * i] * F[3 * jj] + tl[3 * i + 1] * F[3 * jj + 1] + tl[3 * i + 2] * F[3 * jj + 2];
+}
+
+// Walk the product pairs in the reference's order (slot i asc, lobe j asc)
+// calling fn(pair_index, k, j, weight, comp) for every kept pair.
+template <class Slots, class Fn>
+__device__ __forceinline__ void for_each_pair(const float* gp, int Kp, const float* condCov, const float c[3],
+                                              int lastIdx, float invSum, bool scaled, float sum2,
+                                              const Slots& S, const BsdfTab& bt, int b, const float F[9],
+                                              float norm2, Fn&& fn) {
+    int p = 0;
+    for (int i = 0; i < lastIdx; ++i) {
+        float wi = S.valid(i) ? S.weight(i) : 0.0f;
+        if (scaled) wi = wi * invSum;
+        wi = wi / sum2;
+        if (wi == 0.0f) continue;
+        const int k = S.comp(i);
+        float e[3], to_i[9], ci[4];
+        cond_mean_dir_x(gp, Kp, k, c, e);
+        coordinates_f(e, to_i);
+        for (int l = 0; l < 4; ++l) ci[l] = condCov[4 * k + l];
+        for (int j = 0; j < bt.M; ++j) {
+            float mw[3], tw[9], cj[4], wj;
+            bsdf_world(F, bt, b, j, mw, tw, cj, wj);
+            if (wj == 0.0f) continue;
+            if (e[0] * mw[0] + e[1] * mw[1] + e[2] * mw[2] < 0.0f) continue;
+            ProdComp pc;
+            const float nw = mvtn_multiply(e, to_i, ci, mw, tw, cj, norm2, pc);
+            if (fn(p, k, j, wi * wj * nw, pc)) return;
+            ++p;
+        }
+    }
+}
+
+// MVTN<3,3>::pdf of a product component at d
+__device__ __forceinline__ float prod_comp_pdf(const ProdComp& pc, const float d[3], float norm2) {
+    float to[9];
+    coordinates_f(pc.mean, to);
+    float t0, t1, jac;
+    if (!ts_log_x(to, d, t0, t1, jac)) return 0.0f;
+    const float s0 = pc.Linv[0] * t0 + pc.Linv[1] * t1;
+    const float s1 = pc.Linv[2] * t0 + pc.Linv[3] * t1;
+    float v = (float)((double)norm2 * exp(-0.5 * (double)(s0 * s0 + s1 * s1)));
+    v *= pc.detInv * jac;
+    return v;
+}
+
+// Query q after its conditional's kept prefix is known.  Returns false when
+// the product is unusable (no learned BSDF, no pair, zero mass): the caller
+// then serves the plain conditional (h = 0.5).
+template <bool PDF_ONLY, class Slots>
+__device__ bool finish_product(const float* gp, int Kp, const float* condCov, const float c[3], int lastIdx,
+                               float accum, const Slots& S, const BsdfTab& bt, int b, const float F[9],
+                               const float* u, const float* dir_in, GuideConsts gc, QueryOut& o) {
+    const float invSum = 1.0f / accum;
+    const bool scaled = __builtin_isfinite(invSum);
+    float sum2 = 0.0f;
+    for (int i = 0; i < lastIdx; ++i) {
+        float wi = S.valid(i) ? S.weight(i) : 0.0f;
+        if (scaled) wi = wi * invSum;
+        sum2 += wi;
+    }
+    // pass 1: the product mass (createCdf(true)'s sum)
+    float total = 0.0f;
+    int P = 0;
+    for_each_pair(gp, Kp, condCov, c, lastIdx, invSum, scaled, sum2, S, bt, b, F, gc.norm2,
+                  [&](int, int, int, float w, const ProdComp&) { total += w; ++P; return false; });
+    if (P == 0 || total == 0.0f) return false;
+    float dir[3];
+    o.comp = -1;
+    if constexpr (!PDF_ONLY) {
+        // pass 2: sampleDiscreteCdf over the normalised weights (lower_bound,
+        // then the tie walk), keeping the selected pair
+        float cdf = 0.0f, prev = 0.0f;
+        int runStart = 0, sel = -1, selComp = -1, runComp = -1;
+        ProdComp pcs{}, runPc{};
+        for_each_pair(gp, Kp, condCov, c, lastIdx, invSum, scaled, sum2, S, bt, b, F, gc.norm2,
+                      [&](int p, int k, int j, float w, const ProdComp& pc) {
+                          cdf += w / total;
+                          if (p == 0 || cdf != prev) { runStart = p; runComp = k * bt.M + j; runPc = pc; }
+                          prev = cdf;
+                          if (cdf >= u[0]) { sel = p; selComp = k * bt.M + j; pcs = pc; return true; }
+                          return false;
+                      });
+        if (sel < 0) { sel = runStart; selComp = runComp; pcs = runPc; }
+        const float radius = sqrtf(-2.0f * log_x(1.0f - u[1]));
+        const float theta = (float)(2.0 * kPi * (double)u[2]);
+        const float z0 = radius * sin_x(theta), z1 = radius * cos_x(theta);
+        const float v0 = pcs.L[0] * z0 + pcs.L[1] * z1;
+        const float v1 = pcs.L[2] * z0 + pcs.L[3] * z1;
+        float to[9];
+        coordinates_f(pcs.mean, to);
+        if (!ts_exp_x(to, v0, v1, dir)) dir[0] = dir[1] = dir[2] = 0.0f;
+        o.comp = selComp;
+    } else {
+        dir[0] = dir_in[0]; dir[1] = dir_in[1]; dir[2] = dir_in[2];
+    }
+    // pass 3: the product mixture pdf at dir
+    float acc = 0.0f;
+    for_each_pair(gp, Kp, condCov, c, lastIdx, invSum, scaled, sum2, S, bt, b, F, gc.norm2,
+                  [&](int, int, int, float w, const ProdComp& pc) {
+                      const float wn = w / total;
+                      if (wn != 0.0f) acc += wn * prod_comp_pdf(pc, dir, gc.norm2);
+                      return false;
+                  });
+    o.d[0] = dir[0]; o.d[1] = dir[1]; o.d[2] = dir[2];
+    o.pdf = acc;
+    return true;
+}
+
+// One thread per query over the full-K conditional (LDS K x blockDim).
+template <bool PDF_ONLY>
+__global__ void __launch_bounds__(64)
+guide_product_kernel(const float* __restrict__ gp, int Kp, int K, const float* __restrict__ condCov, int64_t nq,
+                     GuideIO io, ProductIO pio, BsdfTab bt, GuideConsts gc) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int T = blockDim.x;
+    const int tid = threadIdx.x;
+    const int64_t q = (int64_t)blockIdx.x * T + tid;
+    if (q >= nq) return;
+    float* wl = lds;
+    int* sl = (int*)(lds + (size_t)K * T);
+    const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
+    float accum = 0.0f;
+    const int lastIdx = build_full(gp, Kp, K, c, wl, sl, T, tid, gc.norm3, accum);
+    const FullSlots S{gp, Kp, c, wl, sl, T, tid};
+    int b = pio.material ? pio.material[q] : -1;
+    if (b >= bt.B) b = -1;
+    // createCdf(true) of the conditional (finish_query's validity test)
+    float sum2 = 0.0f;
+    {
+        const float invSum = 1.0f / accum;
+        const bool scaled = __builtin_isfinite(invSum);
+        for (int i = 0; i < lastIdx; ++i) {
+            float wi = S.valid(i) ? S.weight(i) : 0.0f;
+            if (scaled) wi = wi * invSum;
+            sum2 += wi;
+        }
+    }
+    const bool cvalid = lastIdx > 0 && sum2 != 0.0f;
+    QueryOut o{{0.0f, 0.0f, 0.0f}, 0.0f, -1};
+    float h = 1.0f;                       // no valid conditional: BSDF only
+    if (cvalid) {
+        bool used = false;
+        if (b >= 0 && bt.M > 0) {
+            float F[9];
+            for (int i = 0; i < 9; ++i) F[i] = pio.F[i][q];
+            float u[3] = {0.0f, 0.0f, 0.0f}, dg[3] = {0.0f, 0.0f, 0.0f};
+            if constexpr (PDF_ONLY) { dg[0] = io.e0[q]; dg[1] = io.e1[q]; dg[2] = io.e2[q]; }
+            else { u[0] = io.u0[q]; u[1] = io.u1[q]; u[2] = io.u2[q]; }
+            used = finish_product<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, accum, S, bt, b, F, u, dg, gc, o);
+        }
+        if (used) {
+            h = 0.3f;
+        } else {
+            h = 0.5f;
+            if constexpr (PDF_ONLY) {
+                const float dir[3] = {io.e0[q], io.e1[q], io.e2[q]};
+                o = finish_query(gp, Kp, c, nullptr, lastIdx, accum, S, dir, gc);
+            } else {
+                const float u[3] = {io.u0[q], io.u1[q], io.u2[q]};
+                o = finish_query(gp, Kp, c, u, lastIdx, accum, S, nullptr, gc);
+            }
+        }
+    }
+    if constexpr (PDF_ONLY) {
+        io.pdf[q] = o.pdf;
+    } else {
+        io.d0[q] = o.d[0]; io.d1[q] = o.d[1]; io.d2[q] = o.d[2];
+        io.pdf[q] = o.pdf;
+        io.comp[q] = o.comp;
+    }
+    if (pio.h) pio.h[q] = h;
+}
+
 // lower_bound + tie walk on caller-provided CDFs (the bit-exact index KAT).
 __global__ void sample_cdf_kernel(const float* __restrict__ cdf, int n, const float* __restrict__ u,
                                   int64_t nq, int32_t* __restrict__ out) {
@@ -750,6 +1163,35 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
         hipLaunchKernelGGL(guide_tree_fallback_kernel<false>, dim3(fb_blocks), dim3(Tfb), lds_fb, st, nd, tb,
                            kmax, io, gc, fb_count, fb_list);
     }
+    return hipGetLastError();
+}
+
+// Product sampling (or its pdf, dgiven != null) against one mixture; one
+// thread per query, workgroups as wide as the full-K lists allow.
+hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* condCov, int64_t nq,
+                                const float* const c[3], const float* const u[3], const float* const dgiven[3],
+                                float* const d[3], float* pdf, int32_t* comp, const int32_t* material,
+                                const float* const frame[9], float* h, const float* bw, const float* bmean,
+                                const float* bcov, int B, int M, float norm2, float norm3, hipStream_t st) {
+    if (nq <= 0) return hipSuccess;
+    if (nq > INT32_MAX) return hipErrorInvalidValue;
+    const int T = fallback_width(K);
+    const size_t lds = (size_t)K * T * (sizeof(float) + sizeof(int));
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    GuideConsts gc{norm2, norm3};
+    const GuideIO io = make_io(c, u, dgiven, d, pdf, comp);
+    ProductIO pio{};
+    pio.material = material;
+    for (int i = 0; i < 9; ++i) pio.F[i] = frame[i];
+    pio.h = h;
+    const BsdfTab bt{bw, bmean, bcov, B, M};
+    const dim3 grid((unsigned)((nq + T - 1) / T));
+    if (dgiven)
+        hipLaunchKernelGGL(guide_product_kernel<true>, grid, dim3(T), lds, st, gp, Kp, K, condCov, nq, io, pio, bt,
+                           gc);
+    else
+        hipLaunchKernelGGL(guide_product_kernel<false>, grid, dim3(T), lds, st, gp, Kp, K, condCov, nq, io, pio,
+                           bt, gc);
     return hipGetLastError();
 }
 

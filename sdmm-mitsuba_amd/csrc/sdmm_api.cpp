@@ -69,6 +69,11 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
                              float* pdf, int32_t* comp, int32_t* node_out, float norm2, float norm3, int cap,
                              int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
                              const GuideSortScratch* sort);
+hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* condCov, int64_t nq,
+                                const float* const c[3], const float* const u[3], const float* const dgiven[3],
+                                float* const d[3], float* pdf, int32_t* comp, const int32_t* material,
+                                const float* const frame[9], float* h, const float* bw, const float* bmean,
+                                const float* bcov, int B, int M, float norm2, float norm3, hipStream_t st);
 constexpr int kGuideCapMax = 40;
 hipError_t launch_sample_cdf(const float* cdf, int n, const float* u, int64_t nq, int32_t* out,
                              hipStream_t st);
@@ -906,6 +911,44 @@ int sdmm_pdf_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], const
     if (r) return r;
     HIP_TRY(launch_guide(m->gp, m->Kp, m->K, nq, c, nullptr, d, nullptr, pdf, nullptr, m->norm2, m->norm3,
                          m->guide_cap, m->guide_fb, m->guide_fb + 1, m->cus, m->stream, guide_order(m, nq)));
+    return SDMM_OK;
+}
+
+static int check_bsdf(const sdmm_bsdf_table* b, const int32_t* material, const float* const frame[9]) {
+    if (!b || !material || !frame) return fail(SDMM_E_INVALID, "product: bsdf table, material and frame required");
+    if (b->B < 0 || b->M < 0 || b->M > 64) return fail(SDMM_E_INVALID, "product: need B >= 0, 0 <= M <= 64");
+    if (b->B > 0 && b->M > 0 && (!b->weights || !b->means || !b->covs))
+        return fail(SDMM_E_INVALID, "product: bsdf table arrays missing");
+    for (int i = 0; i < 9; ++i)
+        if (!frame[i]) return fail(SDMM_E_INVALID, "product: frame plane missing");
+    return SDMM_OK;
+}
+
+int sdmm_guide_product_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], const float* const u[3],
+                             const sdmm_bsdf_table* bsdf, const int32_t* material, const float* const frame[9],
+                             float* const d[3], float* pdf, int32_t* comp, float* heuristic) {
+    if (!m || !c || !u || !d || !pdf || !comp) return fail(SDMM_E_INVALID, "invalid argument");
+    if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
+    if (nq <= 0) return SDMM_OK;
+    int r = check_bsdf(bsdf, material, frame);
+    if (r) return r;
+    HIP_TRY(launch_guide_product(m->gp, m->Kp, m->K, m->C.condCov, nq, c, u, nullptr, d, pdf, comp, material,
+                                 frame, heuristic, bsdf->weights, bsdf->means, bsdf->covs, bsdf->B, bsdf->M,
+                                 m->norm2, m->norm3, m->stream));
+    return SDMM_OK;
+}
+
+int sdmm_pdf_product_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], const float* const d[3],
+                           const sdmm_bsdf_table* bsdf, const int32_t* material, const float* const frame[9],
+                           float* pdf, float* heuristic) {
+    if (!m || !c || !d || !pdf) return fail(SDMM_E_INVALID, "invalid argument");
+    if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
+    if (nq <= 0) return SDMM_OK;
+    int r = check_bsdf(bsdf, material, frame);
+    if (r) return r;
+    HIP_TRY(launch_guide_product(m->gp, m->Kp, m->K, m->C.condCov, nq, c, nullptr, d, nullptr, pdf, nullptr,
+                                 material, frame, heuristic, bsdf->weights, bsdf->means, bsdf->covs, bsdf->B,
+                                 bsdf->M, m->norm2, m->norm3, m->stream));
     return SDMM_OK;
 }
 

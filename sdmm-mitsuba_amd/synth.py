@@ -135,3 +135,38 @@ def sample_queries_near(batch: dict, nq: int, seed: int = SEED_QUERIES):
     u = rng.uniform(0.0, 1.0, size=(3, nq)).astype(np.float32)
     u = np.minimum(u, np.float32(0.99999994))
     return c, u
+
+
+SEED_BSDF = 0xB5DF
+
+
+def bsdf_table(B: int, M: int, seed: int = SEED_BSDF):
+    """Synthetic learned-BSDF lobes (the plugin's `.sdmm` files are LFS
+    pointers): B materials x M directional tangent normals in
+    the local shading frame -- weights (B, M) summing to 1, unit means (B, M, 3)
+    in the upper hemisphere (z >= 0.3), SPD 2x2 covariances (B, M, 4) with
+    standard deviations in [0.05, 0.6]."""
+    rng = np.random.default_rng(seed)
+    w = rng.uniform(0.2, 1.0, size=(B, M))
+    w /= w.sum(1, keepdims=True)
+    m = rng.normal(size=(B, M, 3))
+    m[..., 2] = np.abs(m[..., 2]) + 0.6
+    m /= np.linalg.norm(m, axis=-1, keepdims=True)
+    sd = rng.uniform(0.05, 0.6, size=(B, M, 2))
+    ang = rng.uniform(0, np.pi, size=(B, M))
+    c, s = np.cos(ang), np.sin(ang)
+    cov = np.zeros((B, M, 4))
+    cov[..., 0] = c * c * sd[..., 0] ** 2 + s * s * sd[..., 1] ** 2
+    cov[..., 3] = s * s * sd[..., 0] ** 2 + c * c * sd[..., 1] ** 2
+    cov[..., 1] = cov[..., 2] = c * s * (sd[..., 0] ** 2 - sd[..., 1] ** 2)
+    return w.astype(np.float32), m.astype(np.float32), cov.astype(np.float32)
+
+
+def shading_frames(nq: int, seed: int = SEED_BSDF + 1):
+    """Per-query to-world frames F = [s t n] (row-major 3x3, columns s, t, n)
+    with n uniform on the sphere: (nq, 9) float32."""
+    rng = np.random.default_rng(seed)
+    n = random_unit(rng, nq).astype(np.float64)
+    to = coordinates(n)                      # rows s, t, n of Coordinates(n)
+    F = np.transpose(to, (0, 2, 1))          # columns s, t, n
+    return F.reshape(nq, 9).astype(np.float32)
