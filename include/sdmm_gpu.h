@@ -293,6 +293,35 @@ int sdmm_guide_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t
 int sdmm_pdf_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
                        const float* const d[3], float* pdf);
 
+/* Checkpoints (.asdmm, JSON; schema in DESIGN.md section 9).
+ *   sdmm_save_json      the accelerator: sdmm::save_json(m_accelerator, path),
+ *                       volpath_sdmm.cpp:117-126 (model_%05i.asdmm, once per
+ *                       render iteration, :441).  Writes the tree's node table
+ *                       and, for every node with a non-NULL node_mix entry
+ *                       (node_mix may be NULL: tree only), that mixture's
+ *                       canonical + derived arrays and its stepwise-EM state.
+ *   sdmm_load_json      the inverse.  tree_out NULL: size query, only
+ *                       *num_nodes_out is set.  Otherwise node_mix_out (cap >=
+ *                       num_nodes) receives one new handle per saved mixture and
+ *                       NULL elsewhere; restored mixtures are bitwise the saved
+ *                       ones (guide outputs, later EM steps).  A malformed file
+ *                       creates nothing and returns SDMM_E_INVALID.
+ *   sdmm_mix_save_json / sdmm_mix_load_json   one mixture: jmm
+ *                       MixtureModel::save/load (mixture_model.h:315-326).
+ *   sdmm_get_em_params  the constructor arguments the handle was created with.
+ *   sdmm_restore_params exact inverse of sdmm_get_params (every array required;
+ *                       no MVTN::set re-derivation).
+ *   sdmm_stree_set_nodes replace the node table (as sdmm_stree_get_nodes
+ *                       returns it; children must follow their parent). */
+int sdmm_save_json(const sdmm_stree* t, const sdmm_mix* const* node_mix, const char* path);
+int sdmm_load_json(const char* path, int device, sdmm_stree** tree_out, sdmm_mix** node_mix_out, int cap,
+                   int* num_nodes_out);
+int sdmm_mix_save_json(const sdmm_mix* m, const char* path);
+int sdmm_mix_load_json(const char* path, int device, sdmm_mix** out);
+int sdmm_get_em_params(const sdmm_mix* m, sdmm_em_params* p);
+int sdmm_restore_params(sdmm_mix* m, const sdmm_params_out* in);
+int sdmm_stree_set_nodes(sdmm_stree* t, int n, const float* aabb, const int32_t* child, const int32_t* axis);
+
 const char* sdmm_last_error(void);
 int sdmm_abi_version(void);
 

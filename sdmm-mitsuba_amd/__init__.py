@@ -120,6 +120,13 @@ def lib():
         L.sdmm_stree_bind_mixtures.argtypes = [C.c_void_p, C.c_void_p]
         L.sdmm_pdf_wavefront.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p * 3, C.c_void_p * 3,
                                          C.c_void_p]
+        L.sdmm_save_json.argtypes = [C.c_void_p, C.c_void_p, C.c_char_p]
+        L.sdmm_load_json.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_int)]
+        L.sdmm_mix_save_json.argtypes = [C.c_void_p, C.c_char_p]
+        L.sdmm_mix_load_json.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_void_p)]
+        L.sdmm_get_em_params.argtypes = [C.c_void_p, C.c_void_p]
+        L.sdmm_restore_params.argtypes = [C.c_void_p, C.c_void_p]
+        L.sdmm_stree_set_nodes.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -148,6 +155,8 @@ EXPORTED_SYMBOLS = [
     "sdmm_stree_num_nodes", "sdmm_stree_get_nodes", "sdmm_stree_find", "sdmm_stree_route",
     "sdmm_stree_set_stream", "sdmm_stree_get_stream", "sdmm_guide_wavefront", "sdmm_pdf_wavefront",
     "sdmm_stree_bind_mixtures", "sdmm_guide_product_batch", "sdmm_pdf_product_batch",
+    "sdmm_save_json", "sdmm_load_json", "sdmm_mix_save_json", "sdmm_mix_load_json", "sdmm_get_em_params",
+    "sdmm_restore_params", "sdmm_stree_set_nodes",
 ]
 
 
@@ -324,6 +333,48 @@ class SDMM:
             arrs.append(np.ascontiguousarray(st[k], dt))
         _check(lib().sdmm_set_state(self.h, *[a.ctypes.data for a in arrs]))
 
+    # ---- checkpoints (jmm MixtureModel::save/load, mixture_model.h:315-326) --
+    def save_json(self, path):
+        """Write this mixture (canonical + derived arrays + stepwise state) as JSON."""
+        _check(lib().sdmm_mix_save_json(self.h, os.fsencode(path)))
+
+    @classmethod
+    def load_json(cls, path, device: int = 0, stream=None) -> "SDMM":
+        """A new handle, bitwise the saved mixture (sdmm_mix_load_json)."""
+        h = C.c_void_p()
+        _check(lib().sdmm_mix_load_json(os.fsencode(path), device, C.byref(h)))
+        return cls._adopt(h, stream)
+
+    @classmethod
+    def _adopt(cls, h, stream=None) -> "SDMM":
+        self = cls.__new__(cls)
+        self.h = h
+        self.K = int(lib().sdmm_num_components(h))
+        if stream is None:
+            import torch
+            if torch.cuda.is_available():
+                self.set_stream(torch.cuda.current_stream())
+        else:
+            self.set_stream(stream)
+        return self
+
+    def em_params(self) -> dict:
+        p = _EmParams()
+        _check(lib().sdmm_get_em_params(self.h, C.byref(p)))
+        return {"alpha": p.alpha, "bprior": list(p.bprior), "ni_prior_minus_one": p.ni_prior_minus_one,
+                "epsilon": p.epsilon, "decrease_prior": p.decrease_prior}
+
+    def restore_params(self, params: dict):
+        """Exact inverse of get_params (every array, no MVTN::set re-derivation)."""
+        K = self.K
+        keep = {n: np.ascontiguousarray(params[n], np.float32).reshape(K * w) for n, w in PARAM_FIELDS}
+        keep["valid"] = np.ascontiguousarray(params["valid"], np.int32).reshape(K)
+        o = _ParamsOut()
+        for n, _ in PARAM_FIELDS:
+            setattr(o, n, keep[n].ctypes.data)
+        o.valid = keep["valid"].ctypes.data
+        _check(lib().sdmm_restore_params(self.h, C.byref(o)))
+
     def set_guide_capacity(self, cap: int):
         """Per-query candidate-list capacity of the guided-query kernel (0..40)."""
         _check(lib().sdmm_set_guide_capacity(self.h, cap))
@@ -466,6 +517,34 @@ class STree:
         if getattr(self, "h", None) and _lib is not None:
             _lib.sdmm_stree_destroy(self.h)
             self.h = None
+
+    def set_nodes(self, aabb, child, axis):
+        """Replace the node table (the layout nodes() returns)."""
+        a = np.ascontiguousarray(aabb, np.float32).reshape(-1, 6)
+        c = np.ascontiguousarray(child, np.int32).reshape(-1, 2)
+        x = np.ascontiguousarray(axis, np.int32).reshape(-1)
+        _check(lib().sdmm_stree_set_nodes(self.h, C.c_int(a.shape[0]), a.ctypes.data_as(C.c_void_p),
+                                          c.ctypes.data_as(C.c_void_p), x.ctypes.data_as(C.c_void_p)))
+
+    def save_json(self, path, node_mix=None):
+        """The accelerator checkpoint (.asdmm): sdmm::save_json(m_accelerator, path),
+        volpath_sdmm.cpp:117-126 -- the node table plus every node's mixture
+        (node_mix: one SDMM or None per node; None: tree only)."""
+        tab = None if node_mix is None else self._node_table(node_mix)
+        _check(lib().sdmm_save_json(self.h, tab, os.fsencode(path)))
+
+    @classmethod
+    def load_json(cls, path, device: int = 0, stream=None):
+        """(tree, node_mix) from a checkpoint; node_mix[i] is a new SDMM or None."""
+        n = C.c_int(0)
+        _check(lib().sdmm_load_json(os.fsencode(path), device, None, None, 0, C.byref(n)))
+        h = C.c_void_p()
+        tab = (C.c_void_p * n.value)()
+        _check(lib().sdmm_load_json(os.fsencode(path), device, C.byref(h), tab, n.value, C.byref(n)))
+        tree = cls.__new__(cls)
+        tree.h = h
+        mixes = [None if tab[i] is None else SDMM._adopt(C.c_void_p(tab[i]), stream) for i in range(n.value)]
+        return tree, mixes
 
     def split_to_depth(self, depth: int):
         _check(lib().sdmm_stree_split_to_depth(self.h, C.c_int(depth)))

@@ -90,6 +90,15 @@ int fail(int code, const std::string& msg) {
     return code;
 }
 
+}  // namespace
+
+// the error slot for the library's other host translation units (checkpoint.cpp)
+namespace sdmm_detail {
+int set_error(int code, const char* msg) { return fail(code, msg); }
+}  // namespace sdmm_detail
+
+namespace {
+
 #define HIP_TRY(expr)                                                                     \
     do {                                                                                  \
         hipError_t e_ = (expr);                                                           \
@@ -1014,6 +1023,39 @@ int sdmm_set_state(sdmm_mix* m, const double* scalars, const double* T, const do
     return SDMM_OK;
 }
 
+int sdmm_get_em_params(const sdmm_mix* m, sdmm_em_params* p) {
+    if (!m || !p) return fail(SDMM_E_INVALID, "invalid argument");
+    *p = m->params;
+    return SDMM_OK;
+}
+
+// Checkpoint restore: the exact inverse of sdmm_get_params (every canonical and
+// derived array, so a restored mixture is bitwise the saved one -- no MVTN::set
+// re-derivation), then the kernels' packed records from them.
+int sdmm_restore_params(sdmm_mix* m, const sdmm_params_out* in) {
+    if (!m || !in) return fail(SDMM_E_INVALID, "invalid argument");
+    const size_t K = (size_t)m->K;
+    hipStream_t st = m->stream;
+    struct Item { void* dst; const void* src; size_t bytes; };
+    const Item items[] = {
+        {m->C.weights, in->weights, 4 * K}, {m->C.cdf, in->cdf, 4 * K}, {m->C.mean, in->mean, 24 * K},
+        {m->C.cov, in->cov, 100 * K}, {m->C.to, in->to, 36 * K}, {m->C.cholL, in->cholL, 100 * K},
+        {m->C.cholLInv, in->cholLInv, 100 * K}, {m->C.detInv, in->detInv, 4 * K},
+        {m->C.muPremult, in->muPremult, 24 * K}, {m->C.condCov, in->condCov, 16 * K},
+        {m->C.margL, in->margL, 36 * K}, {m->C.margDetInv, in->margDetInv, 4 * K},
+        {m->C.condL, in->condL, 16 * K}, {m->C.condLInv, in->condLInv, 16 * K},
+        {m->C.condDetInv, in->condDetInv, 4 * K}, {m->C.valid, in->valid, 4 * K},
+    };
+    for (const Item& it : items)
+        if (!it.src) return fail(SDMM_E_INVALID, "sdmm_restore_params: every array is required");
+    HIP_TRY(hipSetDevice(m->device));
+    for (const Item& it : items) HIP_TRY(hipMemcpyAsync(it.dst, it.src, it.bytes, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_pack_all(m->K, m->Kp, m->C, m->ep, m->gp, m->norm5, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    m->initialised = true;
+    return SDMM_OK;
+}
+
 }  // extern "C"
 
 // ==========================================================================
@@ -1261,6 +1303,28 @@ int sdmm_stree_split(sdmm_stree* t, const float* const p[3], int64_t n, int thre
 }
 
 int sdmm_stree_num_nodes(const sdmm_stree* t) { return t ? (int)t->nodes.size() : 0; }
+
+int sdmm_stree_set_nodes(sdmm_stree* t, int n, const float* aabb, const int32_t* child, const int32_t* axis) {
+    if (!t || n < 1 || !aabb || !child || !axis) return fail(SDMM_E_INVALID, "invalid argument");
+    std::vector<STNodeHost> nodes((size_t)n);
+    for (int i = 0; i < n; ++i) {
+        STNodeHost& d = nodes[(size_t)i];
+        for (int a = 0; a < 3; ++a) { d.mn[a] = aabb[6 * i + a]; d.mx[a] = aabb[6 * i + 3 + a]; }
+        d.axis = axis[i];
+        d.child[0] = child[2 * i];
+        d.child[1] = child[2 * i + 1];
+        const bool leaf = d.child[0] < 0 && d.child[1] < 0;
+        // children come after their parent (the builder appends them), so a
+        // valid table is acyclic and find() terminates
+        const bool inner = d.child[0] > i && d.child[0] < n && d.child[1] > i && d.child[1] < n;
+        if ((!leaf && !inner) || d.axis < 0 || d.axis > 2)
+            return fail(SDMM_E_INVALID, "sdmm_stree_set_nodes: malformed node table");
+    }
+    t->nodes.swap(nodes);
+    t->dirty = true;
+    t->tab_valid = false;
+    return SDMM_OK;
+}
 
 int sdmm_stree_get_nodes(const sdmm_stree* t, float* aabb, int32_t* child, int32_t* axis) {
     if (!t) return fail(SDMM_E_INVALID, "null tree");

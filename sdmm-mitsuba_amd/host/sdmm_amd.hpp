@@ -16,7 +16,14 @@
 // Errors surface as sdmm_amd::Error (the C ABI itself never throws).
 #pragma once
 
+#include <sys/stat.h>
+
+#include <cerrno>
+#include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <fstream>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -83,11 +90,23 @@ private:
 // One spatio-directional mixture + its stepwise EM state on one GPU
 // (jmm::MixtureModel<6,K,3,...> + StepwiseTangentEM, i.e. sdmm::SDMM + sdmm::EM).
 class Mixture {
+    explicit Mixture(sdmm_mix* h) : h_(h) {}
+
 public:
     explicit Mixture(int K, int device = 0, const sdmm_em_params* params = nullptr) {
         check(sdmm_create(K, params, device, &h_), "sdmm_create");
     }
     ~Mixture() { sdmm_destroy(h_); }
+    // take ownership of a handle (checkpoint loading)
+    static std::unique_ptr<Mixture> adopt(sdmm_mix* h) { return std::unique_ptr<Mixture>(new Mixture(h)); }
+    // jmm MixtureModel::save/load (mixture_model.h:315-326): canonical +
+    // derived arrays and the stepwise state, restored bitwise
+    void save_json(const std::string& path) const { check(sdmm_mix_save_json(h_, path.c_str()), "sdmm_mix_save_json"); }
+    static std::unique_ptr<Mixture> load_json(const std::string& path, int device = 0) {
+        sdmm_mix* h = nullptr;
+        check(sdmm_mix_load_json(path.c_str(), device, &h), "sdmm_mix_load_json");
+        return adopt(h);
+    }
     Mixture(const Mixture&) = delete;
     Mixture& operator=(const Mixture&) = delete;
 
@@ -237,8 +256,108 @@ public:
         check(sdmm_pdf_wavefront(t_, nullptr, n, c, d, pdf), "sdmm_pdf_wavefront");
     }
 
+    // sdmm::save_json(m_accelerator, path) (volpath_sdmm.cpp:125): the node
+    // table plus every node's mixture (node_mix empty: the tree only)
+    void save_json(const std::string& path, const std::vector<Mixture*>& node_mix = {}) const {
+        std::vector<const sdmm_mix*> h;
+        if (!node_mix.empty()) {
+            if ((int)node_mix.size() != nodes()) throw Error(SDMM_E_INVALID, "save_json: one mixture slot per node");
+            for (Mixture* m : node_mix) h.push_back(m ? m->handle() : nullptr);
+        }
+        check(sdmm_save_json(t_, h.empty() ? nullptr : h.data(), path.c_str()), "sdmm_save_json");
+    }
+    // the inverse: a new tree, node_mix[i] the node's mixture or null
+    static std::unique_ptr<SpatialTree> load_json(const std::string& path, int device,
+                                                  std::vector<std::unique_ptr<Mixture>>& node_mix) {
+        int n = 0;
+        check(sdmm_load_json(path.c_str(), device, nullptr, nullptr, 0, &n), "sdmm_load_json");
+        std::vector<sdmm_mix*> h((size_t)n, nullptr);
+        sdmm_stree* t = nullptr;
+        check(sdmm_load_json(path.c_str(), device, &t, h.data(), n, &n), "sdmm_load_json");
+        node_mix.clear();
+        for (sdmm_mix* m : h) node_mix.push_back(m ? Mixture::adopt(m) : nullptr);
+        return std::unique_ptr<SpatialTree>(new SpatialTree(t));
+    }
+
 private:
+    explicit SpatialTree(sdmm_stree* t) : t_(t) {}
     sdmm_stree* t_ = nullptr;
+};
+
+// ---- run outputs the integrator writes next to the render ------------------
+namespace detail {
+inline std::string num(double v) {
+    if (!std::isfinite(v)) return "null";   // nlohmann::json dumps non-finite numbers as null
+    char b[40];
+    std::snprintf(b, sizeof b, "%.17g", v);
+    return b;
+}
+inline void make_dirs(const std::string& dir) {
+    for (size_t i = 1; i <= dir.size(); ++i)
+        if (i == dir.size() || dir[i] == '/') {
+            const std::string d = dir.substr(0, i);
+            if (::mkdir(d.c_str(), 0755) != 0 && errno != EEXIST) throw Error(SDMM_E_INVALID, "cannot create " + d);
+        }
+}
+inline void write_text(const std::string& path, const std::string& text) {
+    std::ofstream f(path);
+    f << text;
+    if (!f) throw Error(SDMM_E_INVALID, "cannot write " + path);
+}
+}  // namespace detail
+
+// saveCheckpoint (volpath_sdmm.cpp:117-126): <dir>/checkpoints/model_%05i.asdmm
+inline std::string save_checkpoint(const std::string& experiment_dir, int iteration, const SpatialTree& tree,
+                                   const std::vector<Mixture*>& node_mix) {
+    const std::string dir = experiment_dir + "/checkpoints";
+    detail::make_dirs(dir);
+    char name[32];
+    std::snprintf(name, sizeof name, "/model_%05i.asdmm", iteration);
+    tree.save_json(dir + name, node_mix);
+    return dir + name;
+}
+
+// scene_norm.json (volpath_sdmm.cpp:340-351): the scene AABB's min corner and
+// the largest extent, the normalisation of the guiding positions
+inline void write_scene_norm(const std::string& path, const float scene_min[3], float spatial_norm) {
+    detail::write_text(path, "{\n    \"scene_min\": [\n        " + detail::num(scene_min[0]) + ",\n        " +
+                                 detail::num(scene_min[1]) + ",\n        " + detail::num(scene_min[2]) +
+                                 "\n    ],\n    \"spatial_norm\": " + detail::num(spatial_norm) + "\n}\n");
+}
+
+// stats.json (volpath_sdmm.cpp:365, :421-428, :443-446): one record per render
+// iteration, keys as the reference writes them (scripts/combine_renders.py and
+// run_tests.py read total_elapsed_seconds / spp / mean_path_length)
+class RunStats {
+public:
+    void push(int iteration, double elapsed_seconds, double total_elapsed_seconds, double mean_path_length,
+              int spp, int total_spp) {
+        rows_.push_back({iteration, elapsed_seconds, total_elapsed_seconds, mean_path_length, spp, total_spp});
+    }
+    size_t size() const { return rows_.size(); }
+    void write(const std::string& path) const {   // std::setw(4) layout, keys sorted like nlohmann's
+        std::string s = "[";
+        for (size_t i = 0; i < rows_.size(); ++i) {
+            const Row& r = rows_[i];
+            s += i ? ",\n    {\n" : "\n    {\n";
+            s += "        \"elapsed_seconds\": " + detail::num(r.elapsed) + ",\n";
+            s += "        \"iteration\": " + std::to_string(r.iteration) + ",\n";
+            s += "        \"mean_path_length\": " + detail::num(r.mean_path_length) + ",\n";
+            s += "        \"spp\": " + std::to_string(r.spp) + ",\n";
+            s += "        \"total_elapsed_seconds\": " + detail::num(r.total_elapsed) + ",\n";
+            s += "        \"total_spp\": " + std::to_string(r.total_spp) + "\n    }";
+        }
+        s += rows_.empty() ? "]\n" : "\n]\n";
+        detail::write_text(path, s);
+    }
+
+private:
+    struct Row {
+        int iteration;
+        double elapsed, total_elapsed, mean_path_length;
+        int spp, total_spp;
+    };
+    std::vector<Row> rows_;
 };
 
 // pdfSurface's mixing of BSDF and guiding densities (sdmm_proc.cpp:587-589):
