@@ -164,7 +164,10 @@ def wavefront_bench(pkg, synth, batch, shard, tree, dev, stream, ct, ut, gout, t
     tree.bind(mixes)                               # once per training iteration in the plugin
     tree.guide(None, ct, ut, gout)
     steps = max(3, args.steps // 4)
-    w_wall, w_kern = timed(lambda: tree.guide(None, ct, ut, gout), steps)
+    # the tree runs on its own stream when handed torch's null stream (handle
+    # 0): its device time is measured with events on THAT stream
+    tree_stream = torch.cuda.ExternalStream(tree.stream_ptr) if tree.stream_ptr else stream
+    w_wall, w_kern = timed(lambda: tree.guide(None, ct, ut, gout), steps, ev_stream=tree_stream)
     comp = gout[2].cpu().numpy()
     q = ct[0].numel()
     return {"queries_per_s": q * world / (w_wall / steps), "Q": q * world, "ms_per_step": w_wall / steps * 1e3,
@@ -239,20 +242,21 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    def timed(fn, steps, events=True):
+    def timed(fn, steps, events=True, ev_stream=None):
         """Wall time of `steps` calls (barrier + synchronize on both sides, max
         over ranks) and, with events, the average device time per call from ONE
         pair of HIP events on the kernels' stream around the whole run (per-call
         event pairs would add their own marker cost to every launch)."""
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if events else None
+        es = stream if ev_stream is None else ev_stream
         barrier()
         t = time.perf_counter()
         if events:
-            ev[0].record(stream)
+            ev[0].record(es)
         for _ in range(steps):
             fn()
         if events:
-            ev[1].record(stream)
+            ev[1].record(es)
         barrier()
         wall = time.perf_counter() - t
         wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)

@@ -608,6 +608,12 @@ class STree:
         ptr = None if stream is None else int(getattr(stream, "cuda_stream", stream))
         _check(lib().sdmm_stree_set_stream(self.h, C.c_void_p(ptr)))
 
+    @property
+    def stream_ptr(self) -> int:
+        """The hipStream_t the tree's work runs on (its own non-blocking stream
+        when set_stream got None or torch's null stream, whose handle is 0)."""
+        return int(lib().sdmm_stree_get_stream(self.h) or 0)
+
     def guide(self, node_mix, c, u, out=None, node_out=None):
         """Per query: leaf = find(c), then conditional/sample/pdf against
         node_mix[leaf] (None: no trained mixture -> comp -1, pdf 0)."""

@@ -267,7 +267,10 @@ __device__ __forceinline__ QueryOut finish_query(const float* gp, int Kp, const 
 // the list overflows, or the list runs out before the cutoff (only possible
 // when invalid conditionals zero out kept weights).  With K = 128 the list
 // holds a median of ~10 and a 99th percentile of ~34 entries.
-constexpr int kGuideCap = 40;
+#ifndef SDMM_GUIDE_CAP_MAX
+#define SDMM_GUIDE_CAP_MAX 40
+#endif
+constexpr int kGuideCap = SDMM_GUIDE_CAP_MAX;
 
 struct CandSlots {
     const float* cw;
@@ -298,13 +301,17 @@ __device__ __forceinline__ int build_candidates(const float* gp, int Kp, int K, 
     float total = 0.0f;
     float dropped = 0.0f;
     int cnt = 0;
+    // 0.0089 / K (< the 0.009 / K of the bound below; the float product's
+    // rounding, 2^-24 relative, stays far inside the margin): one multiply per
+    // component instead of a double division
+    const float skip_f = 0.0089f / (float)K;
     for (int k = 0; k < K; ++k) {
         const float w = gp_ld(gp, Kp, GP_W, k) * marginal_pdf_q(gp, Kp, k, marginal_q(gp, Kp, k, c), norm3);
         total += w;
         // the float sum of non-negative terms never decreases, so the final
         // tau >= (0.01 total - ulp) 0.999 / K > 0.009 total_so_far / K: a weight
         // below that is neither a candidate nor a dropped weight that matters
-        if (!(w > 0.0f) || (double)w < 0.009 * (double)total / (double)K) continue;
+        if (!(w > 0.0f) || w < total * skip_f) continue;
         if (cnt == cap) {
             // full: w joins only if it sorts before the last entry (ties keep
             // the lower index, which arrived first)
@@ -1055,6 +1062,42 @@ static GuideIO make_io(const float* const c[3], const float* const u[3], const f
     return io;
 }
 
+// The candidate kernels' LDS list is sized by the template capacity LCAP
+// (6 B per entry per thread), which sets the workgroups per CU.  A list never
+// holds more than K entries, so the launch uses the smallest LCAP >= min(cap,
+// K): identical results (no overflow can occur that the larger list would
+// avoid), fewer LDS bytes for small mixtures (the tree's K=16 leaves).
+template <bool PDF_ONLY>
+static hipError_t launch_cand(int cap, dim3 grid, hipStream_t st, const float* gp, int Kp, int K, int64_t nq,
+                              const GuideIO& io, GuideConsts gc, int* fb_count, int32_t* fb_list,
+                              const int32_t* perm) {
+    if (cap <= 16)
+        hipLaunchKernelGGL((guide_cand_kernel<PDF_ONLY, 16>), grid, dim3(64), 0, st, gp, Kp, K, nq, io, gc, cap,
+                           fb_count, fb_list, perm);
+    else if (cap <= 24)
+        hipLaunchKernelGGL((guide_cand_kernel<PDF_ONLY, 24>), grid, dim3(64), 0, st, gp, Kp, K, nq, io, gc, cap,
+                           fb_count, fb_list, perm);
+    else
+        hipLaunchKernelGGL((guide_cand_kernel<PDF_ONLY, kGuideCap>), grid, dim3(64), 0, st, gp, Kp, K, nq, io, gc,
+                           cap, fb_count, fb_list, perm);
+    return hipGetLastError();
+}
+template <bool PDF_ONLY>
+static hipError_t launch_tree_cand(int cap, dim3 grid, hipStream_t st, const STNodeDev* nd, const GuideMix* tb,
+                                   int64_t nq, const GuideIO& io, GuideConsts gc, int* fb_count, int32_t* fb_list,
+                                   const int32_t* perm, int32_t* node_out) {
+    if (cap <= 16)
+        hipLaunchKernelGGL((guide_tree_cand_kernel<PDF_ONLY, 16>), grid, dim3(64), 0, st, nd, tb, nq, io, gc, cap,
+                           fb_count, fb_list, perm, node_out);
+    else if (cap <= 24)
+        hipLaunchKernelGGL((guide_tree_cand_kernel<PDF_ONLY, 24>), grid, dim3(64), 0, st, nd, tb, nq, io, gc, cap,
+                           fb_count, fb_list, perm, node_out);
+    else
+        hipLaunchKernelGGL((guide_tree_cand_kernel<PDF_ONLY, kGuideCap>), grid, dim3(64), 0, st, nd, tb, nq, io,
+                           gc, cap, fb_count, fb_list, perm, node_out);
+    return hipGetLastError();
+}
+
 // Candidate pass over all queries, then the fallback queries (listed by the
 // candidate kernel) through the full-K path; both on stream st.
 // fb_count: one device int, fb_list: nq device ints (scratch).
@@ -1082,29 +1125,16 @@ hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float*
     const dim3 grid((unsigned)((nq + T - 1) / T));
     const int fb_blocks = cus * 2;
     const GuideIO io = make_io(c, u, dgiven, d, pdf, comp);
-    if (dgiven) {
-        if (cap <= 24)
-            hipLaunchKernelGGL((guide_cand_kernel<true, 24>), grid, dim3(T), 0, st, gp, Kp, K, nq, io, gc, cap,
-                               fb_count, fb_list, perm);
-        else
-            hipLaunchKernelGGL((guide_cand_kernel<true, kGuideCap>), grid, dim3(T), 0, st, gp, Kp, K, nq, io, gc,
-                               cap, fb_count, fb_list, perm);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
+    cap = cap < K ? cap : K;
+    e = dgiven ? launch_cand<true>(cap, grid, st, gp, Kp, K, nq, io, gc, fb_count, fb_list, perm)
+               : launch_cand<false>(cap, grid, st, gp, Kp, K, nq, io, gc, fb_count, fb_list, perm);
+    if (e != hipSuccess) return e;
+    if (dgiven)
         hipLaunchKernelGGL(guide_fallback_kernel<true>, dim3(fb_blocks), dim3(Tfb), lds_fb, st, gp, Kp, K, io, gc,
                            fb_count, fb_list);
-    } else {
-        if (cap <= 24)
-            hipLaunchKernelGGL((guide_cand_kernel<false, 24>), grid, dim3(T), 0, st, gp, Kp, K, nq, io, gc, cap,
-                               fb_count, fb_list, perm);
-        else
-            hipLaunchKernelGGL((guide_cand_kernel<false, kGuideCap>), grid, dim3(T), 0, st, gp, Kp, K, nq, io,
-                               gc, cap, fb_count, fb_list, perm);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
+    else
         hipLaunchKernelGGL(guide_fallback_kernel<false>, dim3(fb_blocks), dim3(Tfb), lds_fb, st, gp, Kp, K, io,
                            gc, fb_count, fb_list);
-    }
     return hipGetLastError();
 }
 
@@ -1140,29 +1170,16 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
     const dim3 grid((unsigned)((nq + T - 1) / T));
     const int fb_blocks = cus * 2;
     const GuideIO io = make_io(c, u, dgiven, d, pdf, comp);
-    if (dgiven) {
-        if (cap <= 24)
-            hipLaunchKernelGGL((guide_tree_cand_kernel<true, 24>), grid, dim3(T), 0, st, nd, tb, nq, io, gc, cap,
-                               fb_count, fb_list, perm, node_out);
-        else
-            hipLaunchKernelGGL((guide_tree_cand_kernel<true, kGuideCap>), grid, dim3(T), 0, st, nd, tb, nq, io, gc,
-                               cap, fb_count, fb_list, perm, node_out);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
+    cap = cap < kmax ? cap : kmax;
+    e = dgiven ? launch_tree_cand<true>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_out)
+               : launch_tree_cand<false>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_out);
+    if (e != hipSuccess) return e;
+    if (dgiven)
         hipLaunchKernelGGL(guide_tree_fallback_kernel<true>, dim3(fb_blocks), dim3(Tfb), lds_fb, st, nd, tb, kmax,
                            io, gc, fb_count, fb_list);
-    } else {
-        if (cap <= 24)
-            hipLaunchKernelGGL((guide_tree_cand_kernel<false, 24>), grid, dim3(T), 0, st, nd, tb, nq, io, gc, cap,
-                               fb_count, fb_list, perm, node_out);
-        else
-            hipLaunchKernelGGL((guide_tree_cand_kernel<false, kGuideCap>), grid, dim3(T), 0, st, nd, tb, nq, io,
-                               gc, cap, fb_count, fb_list, perm, node_out);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
+    else
         hipLaunchKernelGGL(guide_tree_fallback_kernel<false>, dim3(fb_blocks), dim3(Tfb), lds_fb, st, nd, tb,
                            kmax, io, gc, fb_count, fb_list);
-    }
     return hipGetLastError();
 }
 

@@ -74,7 +74,10 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
                                 float* const d[3], float* pdf, int32_t* comp, const int32_t* material,
                                 const float* const frame[9], float* h, const float* bw, const float* bmean,
                                 const float* bcov, int B, int M, float norm2, float norm3, hipStream_t st);
-constexpr int kGuideCapMax = 40;
+#ifndef SDMM_GUIDE_CAP_MAX
+#define SDMM_GUIDE_CAP_MAX 40
+#endif
+constexpr int kGuideCapMax = SDMM_GUIDE_CAP_MAX;
 hipError_t launch_sample_cdf(const float* cdf, int n, const float* u, int64_t nq, int32_t* out,
                              hipStream_t st);
 }  // namespace sdmm
