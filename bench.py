@@ -196,10 +196,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; SDMM_BENCH_REHEARSE=1 rehearses the N>1 path on a
+    # box with fewer GPUs (ranks share devices, collectives over gloo) -- a
+    # correctness rehearsal only, never a reported scaling number
+    rehearse = os.environ.get("SDMM_BENCH_REHEARSE") == "1"
+    gpu = local % torch.cuda.device_count() if rehearse else local
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
+        torch.cuda.set_device(gpu)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+    dev = torch.device("cuda", gpu if world > 1 else 0)
     torch.cuda.set_device(dev)
 
     pkg = load_pkg()
