@@ -892,7 +892,7 @@ int sdmm_responsibilities(sdmm_mix* m, const sdmm_samples* s, float* resp) {
         const int64_t resident = (int64_t)m->cus * 4 * (m->resp_blocks > 0 ? m->resp_blocks : 1);
         int64_t chunk = (s->n + 3 * resident - 1) / (3 * resident);
         chunk = ((chunk + 63) / 64) * 64;
-        if (chunk < 128) chunk = 128;
+        if (chunk < 64) chunk = 64;   // one staged 64-sample block: small (per-rank) batches still fill the chip
         HIP_TRY(launch_estep_resp_tile(m->rvariant, m->ep, m->Kp, m->K, to_dev(s), s->n, chunk, resp, m->stream));
         return SDMM_OK;
     }
