@@ -526,8 +526,8 @@ __device__ __forceinline__ void serve_full(const float* gp, int Kp, int K, const
 //   * the cutoff walk and finish_query (lane 0) unchanged.
 // LDS: K floats + K ints per wave (workgroup = one wave).
 __device__ __forceinline__ int build_full_wave(const float* gp, int Kp, int K, const float c[3], float* wl,
-                                               int* sl, int lane, float norm3, float& accum) {
-    for (int k = lane; k < K; k += 64) wl[k] = gp_ld(gp, Kp, GP_W, k) * marginal_pdf(gp, Kp, k, c, norm3);
+                                               int* sl, int lane, int T, float norm3, float& accum) {
+    for (int k = lane; k < K; k += T) wl[k] = gp_ld(gp, Kp, GP_W, k) * marginal_pdf(gp, Kp, k, c, norm3);
     __syncthreads();
     float total = 0.0f;
     if (lane == 0)
@@ -540,7 +540,7 @@ __device__ __forceinline__ int build_full_wave(const float* gp, int Kp, int K, c
         int best = -1;
         float bw = 0.0f;
         bool nan_seen = false;
-        for (int k = lane; k < K; k += 64) {   // this lane's entries in increasing k
+        for (int k = lane; k < K; k += T) {   // this lane's entries in increasing k
             const float x = wl[k];
             if (__builtin_signbit(x)) continue;
             nan_seen |= (x != x);
@@ -559,8 +559,7 @@ __device__ __forceinline__ int build_full_wave(const float* gp, int Kp, int K, c
             best = __shfl(best, 0);
             bw = __shfl(bw, 0);
         } else {
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) {
+            for (int off = T >> 1; off >= 1; off >>= 1) {
                 const int ob = __shfl_xor(best, off);
                 const float ow = __shfl_xor(bw, off);
                 if (ob >= 0 && (best < 0 || ow > bw || (ow == bw && ob < best))) { best = ob; bw = ow; }
@@ -580,30 +579,45 @@ __device__ __forceinline__ int build_full_wave(const float* gp, int Kp, int K, c
 
 template <bool PDF_ONLY>
 __device__ __forceinline__ void serve_full_wave(const float* gp, int Kp, int K, const GuideIO& io, int64_t q,
-                                                const float c[3], float* wl, int* sl, int lane, GuideConsts gc) {
+                                                const float c[3], float* wl, int* sl, int lane, int T,
+                                                GuideConsts gc) {
     float accum = 0.0f;
-    const int lastIdx = build_full_wave(gp, Kp, K, c, wl, sl, lane, gc.norm3, accum);
+    const int lastIdx = build_full_wave(gp, Kp, K, c, wl, sl, lane, T, gc.norm3, accum);
     if (lane == 0)
         finish_and_write<PDF_ONLY>(gp, Kp, c, lastIdx, accum, FullSlots{gp, Kp, c, wl, sl, 1, 0}, io, q, gc);
     __syncthreads();   // wl / sl are reused by the wave's next query
 }
 
+// A handful of fallback queries (at most one per workgroup): one query per
+// workgroup, its lanes cooperating (above).  Many (a small list capacity, or
+// a batch where most queries overflow): one query per thread, for throughput
+// (build_full).  Same bits either way.  LDS: K x blockDim floats + ints (the
+// per-thread form; blockDim <= 64, chosen so K_max fits).
 template <bool PDF_ONLY>
 __global__ void __launch_bounds__(64)
 guide_fallback_kernel(const float* __restrict__ gp, int Kp, int K, GuideIO io, GuideConsts gc,
                       const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    float* wl = lds;
-    int* sl = (int*)(lds + K);
+    const int T = blockDim.x;
+    const int tid = threadIdx.x;
     const int count = *fb_count;
-    for (int idx = blockIdx.x; idx < count; idx += gridDim.x) {
+    if (count <= (int)gridDim.x) {
+        if ((int)blockIdx.x >= count) return;
+        const int64_t q = fb_list[blockIdx.x];
+        const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
+        serve_full_wave<PDF_ONLY>(gp, Kp, K, io, q, c, lds, (int*)(lds + K), tid, T, gc);
+        return;
+    }
+    float* wl = lds;
+    int* sl = (int*)(lds + (size_t)K * T);
+    for (int idx = blockIdx.x * T + tid; idx < count; idx += gridDim.x * T) {
         const int64_t q = fb_list[idx];
         const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
-        serve_full_wave<PDF_ONLY>(gp, Kp, K, io, q, c, wl, sl, threadIdx.x, gc);
+        serve_full<PDF_ONLY>(gp, Kp, K, io, q, c, wl, sl, T, tid, gc);
     }
 }
 
-// Fallback queries of the tree wavefront (one per wave, as above); kmax = the
+// Fallback queries of the tree wavefront, the same two forms; kmax = the
 // largest K in tab.
 template <bool PDF_ONLY>
 __global__ void __launch_bounds__(64)
@@ -611,15 +625,31 @@ guide_tree_fallback_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* 
                            GuideIO io, GuideConsts gc, const int* __restrict__ fb_count,
                            const int32_t* __restrict__ fb_list) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    float* wl = lds;
-    int* sl = (int*)(lds + kmax);
+    const int T = blockDim.x;
+    const int tid = threadIdx.x;
     const int count = *fb_count;
-    for (int idx = blockIdx.x; idx < count; idx += gridDim.x) {
-        const int64_t q = fb_list[idx];
+    if (count <= (int)gridDim.x) {
+        if ((int)blockIdx.x >= count) return;
+        const int64_t q = fb_list[blockIdx.x];
         const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
         const int node = stree_find_point(nodes, c[0], c[1], c[2]);   // uniform: a listed query has a mixture
         const GuideMix mx = tab[node];
-        serve_full_wave<PDF_ONLY>(mx.gp, mx.Kp, mx.K, io, q, c, wl, sl, threadIdx.x, gc);
+        serve_full_wave<PDF_ONLY>(mx.gp, mx.Kp, mx.K, io, q, c, lds, (int*)(lds + mx.K), tid, T, gc);
+        return;
+    }
+    float* wl = lds;
+    int* sl = (int*)(lds + (size_t)kmax * T);
+    for (int idx = blockIdx.x * T + tid; idx < count; idx += gridDim.x * T) {
+        const int64_t q = fb_list[idx];
+        const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
+        const int node = stree_find_point(nodes, c[0], c[1], c[2]);   // a listed query has a mixture
+        for (;;) {
+            const int n0 = __builtin_amdgcn_readfirstlane(node);
+            if (node != n0) continue;
+            const GuideMix mx = tab[n0];
+            serve_full<PDF_ONLY>(mx.gp, mx.Kp, mx.K, io, q, c, wl, sl, T, tid, gc);
+            break;
+        }
     }
 }
 
@@ -1176,8 +1206,9 @@ hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float*
     cap = (cap < 0) ? 0 : (cap > kGuideCap ? kGuideCap : cap);
     if (nq > INT32_MAX) return hipErrorInvalidValue;
     const int T = 64;
-    const int Tfb = 64;   // one fallback query per wave
-    const size_t lds_fb = (size_t)K * (sizeof(float) + sizeof(int));
+    const int Tfb = fallback_width(K);
+    const size_t lds_fb = (size_t)K * Tfb * (sizeof(float) + sizeof(int));
+    if (lds_fb > 160 * 1024) return hipErrorInvalidValue;
     GuideConsts gc{norm2, norm3};
     hipError_t e = hipMemsetAsync(fb_count, 0, sizeof(int), st);
     if (e != hipSuccess) return e;
@@ -1189,7 +1220,7 @@ hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float*
         perm = sort->idx[1];
     }
     const dim3 grid((unsigned)((nq + T - 1) / T));
-    const int fb_blocks = cus * 4;
+    const int fb_blocks = cus * 2;
     const GuideIO io = make_io(c, u, dgiven, d, pdf, comp);
     cap = cap < K ? cap : K;
     e = dgiven ? launch_cand<true>(cap, grid, st, gp, Kp, K, nq, io, gc, fb_count, fb_list, perm)
@@ -1218,8 +1249,9 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
     if (nq > INT32_MAX) return hipErrorInvalidValue;
     const int T = 64;
     if (kmax < 1) kmax = 1;
-    const int Tfb = 64;   // one fallback query per wave
-    const size_t lds_fb = (size_t)kmax * (sizeof(float) + sizeof(int));
+    const int Tfb = fallback_width(kmax);
+    const size_t lds_fb = (size_t)kmax * Tfb * (sizeof(float) + sizeof(int));
+    if (lds_fb > 160 * 1024) return hipErrorInvalidValue;
     GuideConsts gc{norm2, norm3};
     hipError_t e = hipMemsetAsync(fb_count, 0, sizeof(int), st);
     if (e != hipSuccess) return e;
@@ -1233,7 +1265,7 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
     const STNodeDev* nd = (const STNodeDev*)nodes;
     const GuideMix* tb = (const GuideMix*)tab;
     const dim3 grid((unsigned)((nq + T - 1) / T));
-    const int fb_blocks = cus * 4;
+    const int fb_blocks = cus * 2;
     const GuideIO io = make_io(c, u, dgiven, d, pdf, comp);
     cap = cap < kmax ? cap : kmax;
     e = dgiven ? launch_tree_cand<true>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_out)
