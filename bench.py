@@ -175,6 +175,52 @@ def wavefront_bench(pkg, synth, batch, shard, tree, dev, stream, ct, ut, gout, t
             "guided_frac": float((comp >= 0).mean()), "scaling": "weak (replicas: queries per rank)"}
 
 
+def large_k_bench(pkg, synth, batch, shard, dev, stream, timed, args, world, N):
+    """BASELINE configs[3] and [4] on one GPU: a full EM step at K=256 (Pool)
+    and K=512 (Kitchen) on the same 2^20-sample batch (sample-sharded, RCCL
+    all-reduce of the statistics when world > 1), and the Kitchen's guided
+    bounce with learned-BSDF product sampling at K=512 (replicas: Q/world
+    queries per rank; 8 materials x 8 lobes, every query with a material)."""
+    import torch
+    res = {}
+    for K in (256, 512):
+        pos, nrm = synth.model_seed_points(batch, K)
+        m = pkg.SDMM(K, device=dev.index, stream=stream)
+        m.init_hemisphere(pos, nrm, synth.DEPTH_PRIOR, synth.SPATIAL_DISTANCE, synth.SEED_MODEL)
+        stats = torch.zeros(pkg.stats_len(K), dtype=torch.float64, device=dev)
+
+        def em_step():
+            if world > 1:
+                m.estep_stats(shard, stats)
+                torch.distributed.all_reduce(stats)
+                m.mstep(stats, N)
+            else:
+                m.optimize(shard)
+        for _ in range(3):
+            em_step()
+        steps = max(3, args.steps // 4)
+        w, _ = timed(em_step, steps, events=False)
+        res[f"em_step_K{K}"] = {"samples_per_s": N / (w / steps), "ms_per_step": w / steps * 1e3}
+        if K == 512:
+            q = (1 << 18) // world
+            c, u = synth.sample_queries_near(batch, q, seed=synth.SEED_QUERIES + 7)
+            B, M = 8, 8
+            bw, bmean, bcov = synth.bsdf_table(B, M)
+            F = synth.shading_frames(q)
+            mat = (np.arange(q) % B).astype(np.int32)
+            tt = lambda a: [torch.from_numpy(np.ascontiguousarray(a[i])).to(dev) for i in range(a.shape[0])]
+            ct, ut, Ft = tt(c), tt(u), tt(F.T)
+            matt = torch.from_numpy(mat).to(dev)
+            table = pkg.BsdfTable(bw, bmean, bcov, device=dev)
+            m.guide_product(ct, ut, table, matt, Ft)
+            ps = max(3, args.steps // 4)
+            pw, pk = timed(lambda: m.guide_product(ct, ut, table, matt, Ft), ps)
+            res["guide_product_K512"] = {"queries_per_s": q * world / (pw / ps), "Q": q * world,
+                                         "ms_per_step": pw / ps * 1e3, "kernel_us": pk * 1e6,
+                                         "materials": B, "lobes": M}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -186,6 +232,7 @@ def main():
     ap.add_argument("--em-warm", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="headline E-step only (profiling)")
+    ap.add_argument("--no-large-k", action="store_true", help="skip the K=256/512 lines")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
     ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
@@ -371,6 +418,9 @@ def main():
         # one sdmm_guide_wavefront call (replicas: Q/world queries per rank) ----
         out["guide_wavefront"] = wavefront_bench(pkg, synth, batch, shard, tree, dev, stream, ct, ut, gout,
                                                  timed, args, world)
+
+    if not args.no_extra and not args.no_large_k:
+        out["large_k"] = large_k_bench(pkg, synth, batch, shard, dev, stream, timed, args, world, N)
 
     if rank == 0 and world == 1 and not args.no_cpu:
         try:

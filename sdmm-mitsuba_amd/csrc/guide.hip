@@ -1002,21 +1002,13 @@ __device__ bool finish_product(const float* gp, int Kp, const float* condCov, co
 }
 
 // One thread per query over the full-K conditional (LDS K x blockDim).
-template <bool PDF_ONLY>
-__global__ void __launch_bounds__(64)
-guide_product_kernel(const float* __restrict__ gp, int Kp, int K, const float* __restrict__ condCov, int64_t nq,
-                     GuideIO io, ProductIO pio, BsdfTab bt, GuideConsts gc) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int T = blockDim.x;
-    const int tid = threadIdx.x;
-    const int64_t q = (int64_t)blockIdx.x * T + tid;
-    if (q >= nq) return;
-    float* wl = lds;
-    int* sl = (int*)(lds + (size_t)K * T);
-    const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
-    float accum = 0.0f;
-    const int lastIdx = build_full(gp, Kp, K, c, wl, sl, T, tid, gc.norm3, accum);
-    const FullSlots S{gp, Kp, c, wl, sl, T, tid};
+// Everything after the kept prefix of query q's conditional is known
+// (slots S, lastIdx, accum): the product with the query's learned BSDF, or the
+// plain conditional, and the outputs.
+template <bool PDF_ONLY, class Slots>
+__device__ __forceinline__ void product_tail(const float* gp, int Kp, const float* condCov, const float c[3],
+                                             int lastIdx, float accum, const Slots& S, const GuideIO& io,
+                                             const ProductIO& pio, const BsdfTab& bt, int64_t q, GuideConsts gc) {
     int b = pio.material ? pio.material[q] : -1;
     if (b >= bt.B) b = -1;
     // createCdf(true) of the conditional (finish_query's validity test)
@@ -1064,6 +1056,54 @@ guide_product_kernel(const float* __restrict__ gp, int Kp, int K, const float* _
         io.comp[q] = o.comp;
     }
     if (pio.h) pio.h[q] = h;
+}
+
+// Candidate path (as guide_cand_kernel: the kept prefix from the per-query LDS
+// list, bit-identical to the full-K selection); queries the list cannot serve
+// exactly go to fb_list for guide_product_kernel.  perm: coherent order.
+template <bool PDF_ONLY, int LCAP>
+__global__ void __launch_bounds__(64)
+guide_product_cand_kernel(const float* __restrict__ gp, int Kp, int K, const float* __restrict__ condCov,
+                          int64_t nq, GuideIO io, ProductIO pio, BsdfTab bt, GuideConsts gc, int cap,
+                          int* __restrict__ fb_count, int32_t* __restrict__ fb_list,
+                          const int32_t* __restrict__ perm) {
+    __shared__ float cw[LCAP * 64];
+    __shared__ unsigned short ck[LCAP * 64];
+    const int tid = threadIdx.x;
+    const int64_t t = (int64_t)blockIdx.x * 64 + tid;
+    if (t >= nq) return;
+    const int64_t q = perm ? (int64_t)perm[t] : t;
+    const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
+    float accum = 0.0f;
+    const int lastIdx = build_candidates(gp, Kp, K, c, cw, ck, 64, tid, gc.norm3, cap, accum);
+    if (lastIdx < 0) {
+        fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
+        return;
+    }
+    product_tail<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, accum, CandSlots{cw, ck, 64, tid}, io, pio, bt, q, gc);
+}
+
+// Full-K path: the queries listed by the candidate kernel (fb_list != null,
+// grid-stride), or every query.  Workgroups as wide as the K-entry lists allow.
+template <bool PDF_ONLY>
+__global__ void __launch_bounds__(64)
+guide_product_kernel(const float* __restrict__ gp, int Kp, int K, const float* __restrict__ condCov, int64_t nq,
+                     GuideIO io, ProductIO pio, BsdfTab bt, GuideConsts gc, const int* __restrict__ fb_count,
+                     const int32_t* __restrict__ fb_list) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int T = blockDim.x;
+    const int tid = threadIdx.x;
+    float* wl = lds;
+    int* sl = (int*)(lds + (size_t)K * T);
+    const int64_t n = fb_list ? (int64_t)*fb_count : nq;
+    for (int64_t idx = (int64_t)blockIdx.x * T + tid; idx < n; idx += (int64_t)gridDim.x * T) {
+        const int64_t q = fb_list ? (int64_t)fb_list[idx] : idx;
+        const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
+        float accum = 0.0f;
+        const int lastIdx = build_full(gp, Kp, K, c, wl, sl, T, tid, gc.norm3, accum);
+        product_tail<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, accum, FullSlots{gp, Kp, c, wl, sl, T, tid}, io,
+                               pio, bt, q, gc);
+    }
 }
 
 // lower_bound + tie walk on caller-provided CDFs (the bit-exact index KAT).
@@ -1286,12 +1326,15 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
                                 const float* const c[3], const float* const u[3], const float* const dgiven[3],
                                 float* const d[3], float* pdf, int32_t* comp, const int32_t* material,
                                 const float* const frame[9], float* h, const float* bw, const float* bmean,
-                                const float* bcov, int B, int M, float norm2, float norm3, hipStream_t st) {
+                                const float* bcov, int B, int M, float norm2, float norm3, int cap, int* fb_count,
+                                int32_t* fb_list, int cus, hipStream_t st, const GuideSortScratch* sort) {
     if (nq <= 0) return hipSuccess;
     if (nq > INT32_MAX) return hipErrorInvalidValue;
     const int T = fallback_width(K);
     const size_t lds = (size_t)K * T * (sizeof(float) + sizeof(int));
     if (lds > 160 * 1024) return hipErrorInvalidValue;
+    cap = (cap < 0) ? 0 : (cap > kGuideCap ? kGuideCap : cap);
+    cap = cap < K ? cap : K;
     GuideConsts gc{norm2, norm3};
     const GuideIO io = make_io(c, u, dgiven, d, pdf, comp);
     ProductIO pio{};
@@ -1299,13 +1342,38 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
     for (int i = 0; i < 9; ++i) pio.F[i] = frame[i];
     pio.h = h;
     const BsdfTab bt{bw, bmean, bcov, B, M};
-    const dim3 grid((unsigned)((nq + T - 1) / T));
+    hipError_t e = hipMemsetAsync(fb_count, 0, sizeof(int), st);
+    if (e != hipSuccess) return e;
+    const int32_t* perm = nullptr;
+    if (sort) {
+        e = coherent_order(c, (int)nq, sort->keys[0], sort->keys[1], sort->idx[0], sort->idx[1], sort->temp,
+                           sort->temp_bytes, st);
+        if (e != hipSuccess) return e;
+        perm = sort->idx[1];
+    }
+    const dim3 grid((unsigned)((nq + 63) / 64));
+#define SDMM_PRODUCT_CAND(P, L)                                                                           \
+    hipLaunchKernelGGL((guide_product_cand_kernel<P, L>), grid, dim3(64), 0, st, gp, Kp, K, condCov, nq, io, pio, \
+                       bt, gc, cap, fb_count, fb_list, perm)
+    if (dgiven) {
+        if (cap <= 16) SDMM_PRODUCT_CAND(true, 16);
+        else if (cap <= 24) SDMM_PRODUCT_CAND(true, 24);
+        else SDMM_PRODUCT_CAND(true, kGuideCap);
+    } else {
+        if (cap <= 16) SDMM_PRODUCT_CAND(false, 16);
+        else if (cap <= 24) SDMM_PRODUCT_CAND(false, 24);
+        else SDMM_PRODUCT_CAND(false, kGuideCap);
+    }
+#undef SDMM_PRODUCT_CAND
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const dim3 fgrid((unsigned)(cus * 2));
     if (dgiven)
-        hipLaunchKernelGGL(guide_product_kernel<true>, grid, dim3(T), lds, st, gp, Kp, K, condCov, nq, io, pio, bt,
-                           gc);
+        hipLaunchKernelGGL(guide_product_kernel<true>, fgrid, dim3(T), lds, st, gp, Kp, K, condCov, nq, io, pio, bt,
+                           gc, fb_count, fb_list);
     else
-        hipLaunchKernelGGL(guide_product_kernel<false>, grid, dim3(T), lds, st, gp, Kp, K, condCov, nq, io, pio,
-                           bt, gc);
+        hipLaunchKernelGGL(guide_product_kernel<false>, fgrid, dim3(T), lds, st, gp, Kp, K, condCov, nq, io, pio,
+                           bt, gc, fb_count, fb_list);
     return hipGetLastError();
 }
 

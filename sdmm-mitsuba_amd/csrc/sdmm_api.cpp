@@ -73,7 +73,8 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
                                 const float* const c[3], const float* const u[3], const float* const dgiven[3],
                                 float* const d[3], float* pdf, int32_t* comp, const int32_t* material,
                                 const float* const frame[9], float* h, const float* bw, const float* bmean,
-                                const float* bcov, int B, int M, float norm2, float norm3, hipStream_t st);
+                                const float* bcov, int B, int M, float norm2, float norm3, int cap, int* fb_count,
+                                int32_t* fb_list, int cus, hipStream_t st, const GuideSortScratch* sort);
 #ifndef SDMM_GUIDE_CAP_MAX
 #define SDMM_GUIDE_CAP_MAX 40
 #endif
@@ -944,9 +945,11 @@ int sdmm_guide_product_batch(const sdmm_mix* m, int64_t nq, const float* const c
     if (nq <= 0) return SDMM_OK;
     int r = check_bsdf(bsdf, material, frame);
     if (r) return r;
+    if ((r = ensure_guide_scratch(m, nq))) return r;
     HIP_TRY(launch_guide_product(m->gp, m->Kp, m->K, m->C.condCov, nq, c, u, nullptr, d, pdf, comp, material,
                                  frame, heuristic, bsdf->weights, bsdf->means, bsdf->covs, bsdf->B, bsdf->M,
-                                 m->norm2, m->norm3, m->stream));
+                                 m->norm2, m->norm3, m->guide_cap, m->guide_fb, m->guide_fb + 1, m->cus, m->stream,
+                                 guide_order(m, nq)));
     return SDMM_OK;
 }
 
@@ -958,9 +961,11 @@ int sdmm_pdf_product_batch(const sdmm_mix* m, int64_t nq, const float* const c[3
     if (nq <= 0) return SDMM_OK;
     int r = check_bsdf(bsdf, material, frame);
     if (r) return r;
+    if ((r = ensure_guide_scratch(m, nq))) return r;
     HIP_TRY(launch_guide_product(m->gp, m->Kp, m->K, m->C.condCov, nq, c, nullptr, d, nullptr, pdf, nullptr,
                                  material, frame, heuristic, bsdf->weights, bsdf->means, bsdf->covs, bsdf->B,
-                                 bsdf->M, m->norm2, m->norm3, m->stream));
+                                 bsdf->M, m->norm2, m->norm3, m->guide_cap, m->guide_fb, m->guide_fb + 1, m->cus,
+                                 m->stream, guide_order(m, nq)));
     return SDMM_OK;
 }
 
