@@ -447,6 +447,23 @@ guide_tree_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __re
     const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
     const int node = stree_find_point(nodes, c[0], c[1], c[2]);
     if (node_out) node_out[q] = node;
+    {
+        // the common case (Morton order): every lane of the wave in one leaf,
+        // served in uniform control flow (a ballot), without the waterfall
+        // loop (-4 %).  The record fields behind mx.gp still compile to vector
+        // loads here (ISA: 54 global_load, 21 s_load; the single-mixture
+        // kernel, whose gp is a kernel argument, reads them with s_load) --
+        // see DESIGN.md, guided wavefront.
+        const int n0 = __builtin_amdgcn_readfirstlane(node);
+        if (__builtin_amdgcn_ballot_w64(node != n0) == 0) {
+            const GuideMix mx = (n0 >= 0) ? tab[n0] : GuideMix{nullptr, 0, 0};
+            if (mx.K <= 0)
+                write_invalid<PDF_ONLY>(io, q);
+            else
+                serve_cand<PDF_ONLY>(mx.gp, mx.Kp, mx.K, io, q, c, cw, ck, tid, cap, gc, fb_count, fb_list);
+            return;
+        }
+    }
     for (;;) {
         const int n0 = __builtin_amdgcn_readfirstlane(node);
         if (node != n0) continue;
