@@ -594,15 +594,152 @@ __device__ __forceinline__ int build_full_wave(const float* gp, int Kp, int K, c
     return lastIdx;
 }
 
+struct WaveLds {
+    float* wl;     // K   marginal weights (taken entries negated)
+    int* sl;       // K   kept slot -> component
+    float* fw;     // K   normalised slot weights slot_w(i)
+    float* pw;     // 64  per-lane chunk values
+    int* pf;       // 64  per-lane chunk flags
+    float* pall;   // pcap  product pair weights of pass 1 (when they fit)
+    int* pfall;    // pcap  their inclusion flags
+    int pcap;
+    int T;         // lanes of the workgroup (one wave, <= 64)
+};
+
+// fw[i] = slot_w(i) (finish_query's normalisation) for i < lastIdx; returns
+// sum2 (uniform over the wave).
+__device__ __forceinline__ float wave_slot_weights(const float* gp, int Kp, const float c[3], int lastIdx,
+                                                   float accum, const WaveLds& L, int lane) {
+    const float invSum = 1.0f / accum;
+    const bool scaled = __builtin_isfinite(invSum);
+    for (int i = lane; i < lastIdx; i += L.T) {
+        const int k = L.sl[i];
+        float wi = cond_valid(gp, Kp, k, c) ? -L.wl[k] : 0.0f;
+        if (scaled) wi = wi * invSum;
+        L.fw[i] = wi;
+    }
+    __syncthreads();
+    float sum2 = 0.0f;
+    if (lane == 0)
+        for (int i = 0; i < lastIdx; ++i) sum2 += L.fw[i];
+    sum2 = __shfl(sum2, 0);
+    if (lastIdx > 0 && sum2 != 0.0f)
+        for (int i = lane; i < lastIdx; i += L.T) L.fw[i] = L.fw[i] / sum2;
+    __syncthreads();
+    return sum2;
+}
+
+// lane 0: acc += chunk values in lane order (flagged entries only)
+__device__ __forceinline__ void wave_chunk_sum(const WaveLds& L, int n, int lane, float& acc) {
+    __syncthreads();
+    if (lane == 0)
+        for (int l = 0; l < n; ++l)
+            if (L.pf[l]) acc += L.pw[l];
+    __syncthreads();
+}
+
+// finish_query with the lanes sharing the slots (the plain conditional: the
+// guide's fallback, and the product path's h = 0.5 case).  Valid on lane 0.
+template <bool PDF_ONLY>
+__device__ QueryOut finish_query_wave(const float* gp, int Kp, const float c[3], const float u[3],
+                                      const float* dir_in, int lastIdx, float sum2, const WaveLds& L, int lane,
+                                      GuideConsts gc) {
+    QueryOut o{{0.0f, 0.0f, 0.0f}, 0.0f, -1};
+    if (lastIdx == 0 || sum2 == 0.0f) return o;   // createCdf(true) fails: BSDF only
+    float dir[3];
+    if constexpr (!PDF_ONLY) {
+        int ksel = 0;
+        if (lane == 0) {
+            float cdf = 0.0f, prev = 0.0f;
+            int slot = -1, runStart = 0;
+            for (int i = 0; i < lastIdx; ++i) {
+                cdf += L.fw[i];
+                if (i == 0 || cdf != prev) runStart = i;
+                prev = cdf;
+                if (cdf >= u[0]) { slot = i; break; }
+            }
+            if (slot < 0) slot = runStart;
+            ksel = L.sl[slot];
+        }
+        ksel = __shfl(ksel, 0);
+        // every lane samples the same component identically (no broadcast)
+        float esel[3];
+        cond_mean_dir(gp, Kp, ksel, c, esel);
+        const float radius = sqrtf(-2.0f * logf(1.0f - u[1]));
+        const float theta = (float)(2.0 * kPi * (double)u[2]);
+        float res0, res1;
+        sincosf(theta, &res0, &res1);
+        const float z0 = radius * res0, z1 = radius * res1;
+        const float L00 = gp_ld(gp, Kp, GP_CL00, ksel), L10 = gp_ld(gp, Kp, GP_CL10, ksel);
+        const float L11 = gp_ld(gp, Kp, GP_CL11, ksel);
+        const float v0 = L00 * z0 + 0.0f * z1;
+        const float v1 = L10 * z0 + L11 * z1;
+        float tof[9];
+        coordinates_f(esel, tof);
+        ts_exp_dir(tof, v0, v1, dir);
+        o.comp = ksel;
+    } else {
+        dir[0] = dir_in[0]; dir[1] = dir_in[1]; dir[2] = dir_in[2];
+    }
+    float acc = 0.0f;
+    for (int base = 0; base < lastIdx; base += L.T) {
+        const int i = base + lane;
+        float term = 0.0f;
+        int use = 0;
+        if (i < lastIdx) {
+            const float f = L.fw[i];
+            if (f != 0.0f) {
+                const int k = L.sl[i];
+                float e[3];
+                cond_mean_dir(gp, Kp, k, c, e);
+                term = f * cond_component_pdf(gp, Kp, k, e, dir, gc.norm2);
+                use = 1;
+            }
+        }
+        L.pw[lane] = term;
+        L.pf[lane] = use;
+        wave_chunk_sum(L, min(L.T, lastIdx - base), lane, acc);
+    }
+    o.d[0] = dir[0]; o.d[1] = dir[1]; o.d[2] = dir[2];
+    o.pdf = acc;
+    return o;
+}
+
+// LDS carve-up of a one-wave workgroup: wl, sl, fw (K each), the 64-entry
+// chunk, then the pass-1 pair weights and flags (pcap each).
+__device__ __forceinline__ WaveLds wave_lds(float* lds, int K, int pcap, int T) {
+    WaveLds L;
+    L.T = T;
+    L.wl = lds;
+    L.sl = (int*)(lds + K);
+    L.fw = lds + 2 * K;
+    L.pw = lds + 3 * K;
+    L.pf = (int*)(lds + 3 * K + 64);
+    L.pall = lds + 3 * K + 128;
+    L.pfall = (int*)(lds + 3 * K + 128 + pcap);
+    L.pcap = pcap;
+    return L;
+}
+static size_t wave_lds_bytes(int K, int pcap) { return sizeof(float) * (3 * (size_t)K + 128 + 2 * (size_t)pcap); }
+
 template <bool PDF_ONLY>
 __device__ __forceinline__ void serve_full_wave(const float* gp, int Kp, int K, const GuideIO& io, int64_t q,
-                                                const float c[3], float* wl, int* sl, int lane, int T,
-                                                GuideConsts gc) {
+                                                const float c[3], const WaveLds& L, int lane, GuideConsts gc) {
     float accum = 0.0f;
-    const int lastIdx = build_full_wave(gp, Kp, K, c, wl, sl, lane, T, gc.norm3, accum);
-    if (lane == 0)
-        finish_and_write<PDF_ONLY>(gp, Kp, c, lastIdx, accum, FullSlots{gp, Kp, c, wl, sl, 1, 0}, io, q, gc);
-    __syncthreads();   // wl / sl are reused by the wave's next query
+    const int lastIdx = build_full_wave(gp, Kp, K, c, L.wl, L.sl, lane, L.T, gc.norm3, accum);
+    const float sum2 = wave_slot_weights(gp, Kp, c, lastIdx, accum, L, lane);
+    float u[3] = {0.0f, 0.0f, 0.0f}, dg[3] = {0.0f, 0.0f, 0.0f};
+    if constexpr (PDF_ONLY) { dg[0] = io.e0[q]; dg[1] = io.e1[q]; dg[2] = io.e2[q]; }
+    else { u[0] = io.u0[q]; u[1] = io.u1[q]; u[2] = io.u2[q]; }
+    const QueryOut o = finish_query_wave<PDF_ONLY>(gp, Kp, c, u, dg, lastIdx, sum2, L, lane, gc);
+    if (lane == 0) {
+        io.pdf[q] = o.pdf;
+        if constexpr (!PDF_ONLY) {
+            io.d0[q] = o.d[0]; io.d1[q] = o.d[1]; io.d2[q] = o.d[2];
+            io.comp[q] = o.comp;
+        }
+    }
+    __syncthreads();   // the LDS is reused by the wave's next query
 }
 
 // A handful of fallback queries (at most one per workgroup): one query per
@@ -622,7 +759,7 @@ guide_fallback_kernel(const float* __restrict__ gp, int Kp, int K, GuideIO io, G
         if ((int)blockIdx.x >= count) return;
         const int64_t q = fb_list[blockIdx.x];
         const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
-        serve_full_wave<PDF_ONLY>(gp, Kp, K, io, q, c, lds, (int*)(lds + K), tid, T, gc);
+        serve_full_wave<PDF_ONLY>(gp, Kp, K, io, q, c, wave_lds(lds, K, 0, T), tid, gc);
         return;
     }
     float* wl = lds;
@@ -651,7 +788,7 @@ guide_tree_fallback_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* 
         const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
         const int node = stree_find_point(nodes, c[0], c[1], c[2]);   // uniform: a listed query has a mixture
         const GuideMix mx = tab[node];
-        serve_full_wave<PDF_ONLY>(mx.gp, mx.Kp, mx.K, io, q, c, lds, (int*)(lds + mx.K), tid, T, gc);
+        serve_full_wave<PDF_ONLY>(mx.gp, mx.Kp, mx.K, io, q, c, wave_lds(lds, mx.K, 0, T), tid, gc);
         return;
     }
     float* wl = lds;
@@ -1077,7 +1214,7 @@ __device__ __forceinline__ void product_tail(const float* gp, int Kp, const floa
 
 // Candidate path (as guide_cand_kernel: the kept prefix from the per-query LDS
 // list, bit-identical to the full-K selection); queries the list cannot serve
-// exactly go to fb_list for guide_product_kernel.  perm: coherent order.
+// exactly go to fb_list for guide_product_wave_kernel.  perm: coherent order.
 template <bool PDF_ONLY, int LCAP>
 __global__ void __launch_bounds__(64)
 guide_product_cand_kernel(const float* __restrict__ gp, int Kp, int K, const float* __restrict__ condCov,
@@ -1100,26 +1237,229 @@ guide_product_cand_kernel(const float* __restrict__ gp, int Kp, int K, const flo
     product_tail<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, accum, CandSlots{cw, ck, 64, tid}, io, pio, bt, q, gc);
 }
 
-// Full-K path: the queries listed by the candidate kernel (fb_list != null,
-// grid-stride), or every query.  Workgroups as wide as the K-entry lists allow.
+// ---------------------------------------------------------------------------
+// Full-K fallback, ONE query per wave, for the product path (round 1's
+// thread-per-query guide_product_kernel took 97 % of a Kitchen K = 512 product
+// call) and the tail of the plain guide's fallback.  The kept prefix comes from
+// build_full_wave (bit-identical to build_full).  After it, every per-slot and
+// per-pair quantity is evaluated by the lanes in parallel, and every
+// order-dependent float reduction -- sum2 (createCdf), the product mass, the
+// CDF walks, the pdf accumulations -- is formed by lane 0 from LDS in the
+// reference order: the same operands, added in the same order, as
+// finish_query / finish_product, hence the same bits.
+// Product pair (slot i, lobe j) of for_each_pair: false when the walk skips
+// it (zero slot weight, zero lobe weight, opposite hemisphere); else its
+// weight wi * wj * nw and product component.
+__device__ __forceinline__ bool pair_eval(const float* gp, int Kp, const float* condCov, const float c[3],
+                                          const WaveLds& L, int i, int j, const BsdfTab& bt, int b,
+                                          const float F[9], float norm2, float& w, ProdComp& pc, int& k) {
+    const float wi = L.fw[i];
+    if (wi == 0.0f) return false;
+    k = L.sl[i];
+    float e[3], to_i[9], ci[4];
+    cond_mean_dir_x(gp, Kp, k, c, e);
+    coordinates_f(e, to_i);
+    for (int l = 0; l < 4; ++l) ci[l] = condCov[4 * k + l];
+    float mw[3], tw[9], cj[4], wj;
+    bsdf_world(F, bt, b, j, mw, tw, cj, wj);
+    if (wj == 0.0f) return false;
+    if (e[0] * mw[0] + e[1] * mw[1] + e[2] * mw[2] < 0.0f) return false;
+    const float nw = mvtn_multiply(e, to_i, ci, mw, tw, cj, norm2, pc);
+    w = wi * wj * nw;
+    return true;
+}
+
+// finish_product with the pairs spread over the lanes (64 per chunk, flat
+// index f = slot * M + lobe: the reference's walk order).  Returns false when
+// the product is unusable (no pair / zero mass); uniform over the wave.
+template <bool PDF_ONLY>
+__device__ bool finish_product_wave(const float* gp, int Kp, const float* condCov, const float c[3], int lastIdx,
+                                    const WaveLds& L, const BsdfTab& bt, int b, const float F[9], const float* u,
+                                    const float* dir_in, int lane, GuideConsts gc, QueryOut& o) {
+    const int M = bt.M;
+    const int NP = lastIdx * M;
+    const bool keep = NP <= L.pcap;   // pass 1's weights stay in LDS for the CDF walk
+    // pass 1: the product mass (createCdf(true)'s sum) and the pair count
+    float total = 0.0f;
+    int P = 0;
+    for (int base = 0; base < NP; base += L.T) {
+        const int f = base + lane;
+        float w = 0.0f;
+        int inc = 0;
+        if (f < NP) {
+            ProdComp pc{};
+            int k;
+            inc = pair_eval(gp, Kp, condCov, c, L, f / M, f % M, bt, b, F, gc.norm2, w, pc, k) ? 1 : 0;
+            if (keep) { L.pall[f] = w; L.pfall[f] = inc; }
+        }
+        L.pw[lane] = w;
+        L.pf[lane] = inc;
+        __syncthreads();
+        if (lane == 0) {
+            const int n = min(L.T, NP - base);
+            for (int l = 0; l < n; ++l)
+                if (L.pf[l]) { total += L.pw[l]; ++P; }
+        }
+        __syncthreads();
+    }
+    total = __shfl(total, 0);
+    P = __shfl(P, 0);
+    if (P == 0 || total == 0.0f) return false;
+    float dir[3];
+    o.comp = -1;
+    if constexpr (!PDF_ONLY) {
+        // pass 2: sampleDiscreteCdf over w / total (lower_bound + tie walk)
+        int sel_f = -1;
+        if (keep) {
+            if (lane == 0) {
+                float cdf = 0.0f, prev = 0.0f;
+                int p = 0, run_f = -1;
+                for (int f = 0; f < NP; ++f) {
+                    if (!L.pfall[f]) continue;
+                    cdf += L.pall[f] / total;
+                    if (p == 0 || cdf != prev) run_f = f;
+                    prev = cdf;
+                    ++p;
+                    if (cdf >= u[0]) { sel_f = f; break; }
+                }
+                if (sel_f < 0) sel_f = run_f;
+            }
+        } else {
+            float cdf = 0.0f, prev = 0.0f;   // lane 0's walk state
+            int p = 0, run_f = -1, done = 0;
+            for (int base = 0; base < NP; base += L.T) {
+                const int f = base + lane;
+                float x = 0.0f;
+                int inc = 0;
+                if (f < NP) {
+                    ProdComp pc{};
+                    int k;
+                    float w = 0.0f;
+                    inc = pair_eval(gp, Kp, condCov, c, L, f / M, f % M, bt, b, F, gc.norm2, w, pc, k) ? 1 : 0;
+                    if (inc) x = w / total;
+                }
+                L.pw[lane] = x;
+                L.pf[lane] = inc;
+                __syncthreads();
+                if (lane == 0) {
+                    const int n = min(L.T, NP - base);
+                    for (int l = 0; l < n; ++l) {
+                        if (!L.pf[l]) continue;
+                        cdf += L.pw[l];
+                        if (p == 0 || cdf != prev) run_f = base + l;
+                        prev = cdf;
+                        ++p;
+                        if (cdf >= u[0]) { sel_f = base + l; done = 1; break; }
+                    }
+                }
+                __syncthreads();
+                if (__shfl(done, 0)) break;
+            }
+            if (lane == 0 && sel_f < 0) sel_f = run_f;
+        }
+        sel_f = __shfl(sel_f, 0);
+        // the selected pair's product component, recomputed (uniform)
+        ProdComp pcs{};
+        int ksel = 0;
+        float wsel = 0.0f;
+        (void)pair_eval(gp, Kp, condCov, c, L, sel_f / M, sel_f % M, bt, b, F, gc.norm2, wsel, pcs, ksel);
+        const float radius = sqrtf(-2.0f * log_x(1.0f - u[1]));
+        const float theta = (float)(2.0 * kPi * (double)u[2]);
+        const float z0 = radius * sin_x(theta), z1 = radius * cos_x(theta);
+        const float v0 = pcs.L[0] * z0 + pcs.L[1] * z1;
+        const float v1 = pcs.L[2] * z0 + pcs.L[3] * z1;
+        float to[9];
+        coordinates_f(pcs.mean, to);
+        if (!ts_exp_x(to, v0, v1, dir)) dir[0] = dir[1] = dir[2] = 0.0f;
+        o.comp = ksel * M + sel_f % M;
+    } else {
+        dir[0] = dir_in[0]; dir[1] = dir_in[1]; dir[2] = dir_in[2];
+    }
+    // pass 3: the product mixture pdf at dir
+    float acc = 0.0f;
+    for (int base = 0; base < NP; base += L.T) {
+        const int f = base + lane;
+        float term = 0.0f;
+        int use = 0;
+        if (f < NP && (!keep || L.pfall[f])) {
+            ProdComp pc{};
+            int k;
+            float w = 0.0f;
+            if (pair_eval(gp, Kp, condCov, c, L, f / M, f % M, bt, b, F, gc.norm2, w, pc, k)) {
+                const float wn = w / total;
+                if (wn != 0.0f) {
+                    term = wn * prod_comp_pdf(pc, dir, gc.norm2);
+                    use = 1;
+                }
+            }
+        }
+        L.pw[lane] = term;
+        L.pf[lane] = use;
+        wave_chunk_sum(L, min(L.T, NP - base), lane, acc);
+    }
+    o.d[0] = dir[0]; o.d[1] = dir[1]; o.d[2] = dir[2];
+    o.pdf = acc;
+    return true;
+}
+
+// product_tail for one query served by a whole wave; lane 0 writes.
+template <bool PDF_ONLY>
+__device__ void product_tail_wave(const float* gp, int Kp, const float* condCov, const float c[3], int lastIdx,
+                                  float accum, const WaveLds& L, const GuideIO& io, const ProductIO& pio,
+                                  const BsdfTab& bt, int64_t q, int lane, GuideConsts gc) {
+    int b = pio.material ? pio.material[q] : -1;
+    if (b >= bt.B) b = -1;
+    const float sum2 = wave_slot_weights(gp, Kp, c, lastIdx, accum, L, lane);
+    const bool cvalid = lastIdx > 0 && sum2 != 0.0f;
+    QueryOut o{{0.0f, 0.0f, 0.0f}, 0.0f, -1};
+    float h = 1.0f;                       // no valid conditional: BSDF only
+    float u[3] = {0.0f, 0.0f, 0.0f}, dg[3] = {0.0f, 0.0f, 0.0f};
+    if constexpr (PDF_ONLY) { dg[0] = io.e0[q]; dg[1] = io.e1[q]; dg[2] = io.e2[q]; }
+    else { u[0] = io.u0[q]; u[1] = io.u1[q]; u[2] = io.u2[q]; }
+    if (cvalid) {
+        bool used = false;
+        if (b >= 0 && bt.M > 0) {
+            float F[9];
+            for (int i = 0; i < 9; ++i) F[i] = pio.F[i][q];
+            used = finish_product_wave<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, L, bt, b, F, u, dg, lane, gc, o);
+        }
+        if (used) {
+            h = 0.3f;
+        } else {
+            h = 0.5f;
+            o = finish_query_wave<PDF_ONLY>(gp, Kp, c, u, dg, lastIdx, sum2, L, lane, gc);
+        }
+    }
+    if (lane == 0) {
+        if constexpr (PDF_ONLY) {
+            io.pdf[q] = o.pdf;
+        } else {
+            io.d0[q] = o.d[0]; io.d1[q] = o.d[1]; io.d2[q] = o.d[2];
+            io.pdf[q] = o.pdf;
+            io.comp[q] = o.comp;
+        }
+        if (pio.h) pio.h[q] = h;
+    }
+}
+
+// The product path's full-K queries (listed by guide_product_cand_kernel, or
+// every query when fb_list is null): one wave per query, grid-stride.
 template <bool PDF_ONLY>
 __global__ void __launch_bounds__(64)
-guide_product_kernel(const float* __restrict__ gp, int Kp, int K, const float* __restrict__ condCov, int64_t nq,
-                     GuideIO io, ProductIO pio, BsdfTab bt, GuideConsts gc, const int* __restrict__ fb_count,
-                     const int32_t* __restrict__ fb_list) {
+guide_product_wave_kernel(const float* __restrict__ gp, int Kp, int K, const float* __restrict__ condCov,
+                          int64_t nq, GuideIO io, ProductIO pio, BsdfTab bt, GuideConsts gc, int pcap,
+                          const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int T = blockDim.x;
-    const int tid = threadIdx.x;
-    float* wl = lds;
-    int* sl = (int*)(lds + (size_t)K * T);
+    const int lane = threadIdx.x;
+    const WaveLds L = wave_lds(lds, K, pcap, 64);
     const int64_t n = fb_list ? (int64_t)*fb_count : nq;
-    for (int64_t idx = (int64_t)blockIdx.x * T + tid; idx < n; idx += (int64_t)gridDim.x * T) {
+    for (int64_t idx = blockIdx.x; idx < n; idx += gridDim.x) {
         const int64_t q = fb_list ? (int64_t)fb_list[idx] : idx;
         const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
         float accum = 0.0f;
-        const int lastIdx = build_full(gp, Kp, K, c, wl, sl, T, tid, gc.norm3, accum);
-        product_tail<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, accum, FullSlots{gp, Kp, c, wl, sl, T, tid}, io,
-                               pio, bt, q, gc);
+        const int lastIdx = build_full_wave(gp, Kp, K, c, L.wl, L.sl, lane, 64, gc.norm3, accum);
+        product_tail_wave<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, accum, L, io, pio, bt, q, lane, gc);
+        __syncthreads();   // the LDS is reused by the next query
     }
 }
 
@@ -1264,7 +1604,7 @@ hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float*
     if (nq > INT32_MAX) return hipErrorInvalidValue;
     const int T = 64;
     const int Tfb = fallback_width(K);
-    const size_t lds_fb = (size_t)K * Tfb * (sizeof(float) + sizeof(int));
+    const size_t lds_fb = std::max((size_t)K * Tfb * (sizeof(float) + sizeof(int)), wave_lds_bytes(K, 0));
     if (lds_fb > 160 * 1024) return hipErrorInvalidValue;
     GuideConsts gc{norm2, norm3};
     hipError_t e = hipMemsetAsync(fb_count, 0, sizeof(int), st);
@@ -1307,7 +1647,7 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
     const int T = 64;
     if (kmax < 1) kmax = 1;
     const int Tfb = fallback_width(kmax);
-    const size_t lds_fb = (size_t)kmax * Tfb * (sizeof(float) + sizeof(int));
+    const size_t lds_fb = std::max((size_t)kmax * Tfb * (sizeof(float) + sizeof(int)), wave_lds_bytes(kmax, 0));
     if (lds_fb > 160 * 1024) return hipErrorInvalidValue;
     GuideConsts gc{norm2, norm3};
     hipError_t e = hipMemsetAsync(fb_count, 0, sizeof(int), st);
@@ -1337,8 +1677,8 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
     return hipGetLastError();
 }
 
-// Product sampling (or its pdf, dgiven != null) against one mixture; one
-// thread per query, workgroups as wide as the full-K lists allow.
+// Product sampling (or its pdf, dgiven != null) against one mixture: the
+// candidate kernel (thread per query), then its full-K queries one per wave.
 hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* condCov, int64_t nq,
                                 const float* const c[3], const float* const u[3], const float* const dgiven[3],
                                 float* const d[3], float* pdf, int32_t* comp, const int32_t* material,
@@ -1347,9 +1687,10 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
                                 int32_t* fb_list, int cus, hipStream_t st, const GuideSortScratch* sort) {
     if (nq <= 0) return hipSuccess;
     if (nq > INT32_MAX) return hipErrorInvalidValue;
-    const int T = fallback_width(K);
-    const size_t lds = (size_t)K * T * (sizeof(float) + sizeof(int));
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    // pass-1 pair weights kept in LDS up to 2048 pairs (16 KB + the K lists)
+    const int pcap = 2048;
+    const size_t lds = wave_lds_bytes(K, pcap);
+    if (lds > 64 * 1024) return hipErrorInvalidValue;
     cap = (cap < 0) ? 0 : (cap > kGuideCap ? kGuideCap : cap);
     cap = cap < K ? cap : K;
     GuideConsts gc{norm2, norm3};
@@ -1384,13 +1725,13 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
 #undef SDMM_PRODUCT_CAND
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const dim3 fgrid((unsigned)(cus * 2));
+    const dim3 fgrid((unsigned)(cus * 8));
     if (dgiven)
-        hipLaunchKernelGGL(guide_product_kernel<true>, fgrid, dim3(T), lds, st, gp, Kp, K, condCov, nq, io, pio, bt,
-                           gc, fb_count, fb_list);
+        hipLaunchKernelGGL(guide_product_wave_kernel<true>, fgrid, dim3(64), lds, st, gp, Kp, K, condCov, nq, io,
+                           pio, bt, gc, pcap, fb_count, fb_list);
     else
-        hipLaunchKernelGGL(guide_product_kernel<false>, fgrid, dim3(T), lds, st, gp, Kp, K, condCov, nq, io, pio,
-                           bt, gc, fb_count, fb_list);
+        hipLaunchKernelGGL(guide_product_wave_kernel<false>, fgrid, dim3(64), lds, st, gp, Kp, K, condCov, nq, io,
+                           pio, bt, gc, pcap, fb_count, fb_list);
     return hipGetLastError();
 }
 

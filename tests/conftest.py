@@ -6,6 +6,8 @@ tests proper: they call the HIP library through the C ABI and compare it with
 the CPU oracle (oracle/) on the same seeded inputs.
 """
 import importlib.util
+import json
+import os
 import sys
 from pathlib import Path
 
@@ -50,6 +52,26 @@ def oracle():
 def synth(pkg):
     import importlib
     return importlib.import_module("sdmm_mitsuba_amd.synth")
+
+
+@pytest.fixture
+def plog(request):
+    """record(quantity, realized, bound): append the realized max error of a
+    parity check next to the bound it was held to, one JSON line per check, to
+    $SDMM_PARITY_LOG (default gpurun_out/parity_errors.jsonl; the round's copy
+    is committed under profiles/)."""
+    path = Path(os.environ.get("SDMM_PARITY_LOG", ROOT / "gpurun_out" / "parity_errors.jsonl"))
+
+    def record(quantity, realized, bound, **extra):
+        path.parent.mkdir(parents=True, exist_ok=True)
+        row = {"test": request.node.nodeid, "quantity": quantity, "realized": float(realized),
+               "bound": float(bound), "ok": bool(float(realized) <= float(bound))}
+        row.update({k: (v if isinstance(v, (int, float, str, bool)) else str(v)) for k, v in extra.items()})
+        with open(path, "a") as f:
+            f.write(json.dumps(row) + "\n")
+        return realized
+
+    return record
 
 
 @pytest.fixture(scope="session")

@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 RTOL_PARAMS = 1e-4
 
 
-def _check_resp(got, ref, params, x):
+def _check_resp(got, ref, params, x, plog=None):
     """got: GPU, ref: fp32 oracle, exact: fp64 of the same parameters."""
     exact = posterior_f64(params, x)
     live = ref.sum(1) > 0
@@ -32,8 +32,13 @@ def _check_resp(got, ref, params, x):
     both = live & ~mism
     eg = np.abs(got[both] - exact[both]).max(initial=0.0)
     eo = np.abs(ref[both] - exact[both]).max(initial=0.0)
+    rs = np.abs(got[both].sum(1) - 1.0).max(initial=0.0)
+    if plog is not None:
+        plog("resp_abs_err_vs_fp64", eg, 4 * eo + 1e-5, oracle_fp32_err=eo)
+        plog("resp_live_row_mismatch_frac", mism.mean(), 2e-3)
+        plog("resp_rowsum_abs_err", rs, 1e-5)
     assert eg <= 4 * eo + 1e-5, f"gpu err {eg} vs oracle-fp32 err {eo}"
-    np.testing.assert_allclose(got[both].sum(1), 1.0, atol=1e-5)
+    assert rs <= 1e-5, f"row sums off by {rs}"
     return eg, eo
 
 
@@ -89,7 +94,7 @@ def test_init_params_match_oracle(pkg, oracle, synth, gpu, K):
 
 @pytest.mark.parametrize("K,N", [(16, 4099), (32, 2048), (64, 3000), (128, 4096), (128, 1001), (72, 777),
                                  (120, 2050), (256, 1500), (512, 700)])
-def test_responsibilities_match_oracle(pkg, oracle, synth, gpu, K, N):
+def test_responsibilities_match_oracle(pkg, oracle, synth, gpu, plog, K, N):
     import torch
     b, mix, om, ost, ds, os_ = _setup(pkg, oracle, synth, K, N)
     resp = torch.full((N, K), -1.0, device=gpu)
@@ -98,7 +103,7 @@ def test_responsibilities_match_oracle(pkg, oracle, synth, gpu, K, N):
     got = resp.cpu().numpy()
     ref = oracle.responsibilities(om, os_)
     assert np.isfinite(got).all()
-    _check_resp(got, ref, mix.get_params(), b["x"])
+    _check_resp(got, ref, mix.get_params(), b["x"], plog)
 
 
 @pytest.mark.parametrize("heuristic", [False, True])
@@ -127,7 +132,7 @@ def _stats_err(a, b, K):
 
 @pytest.mark.parametrize("K,N,heuristic", [(16, 5000, False), (128, 8192, False), (128, 4096, True),
                                            (256, 3000, False), (512, 1024, False), (32, 999, True)])
-def test_stats_match_oracle(pkg, oracle, synth, gpu, K, N, heuristic):
+def test_stats_match_oracle(pkg, oracle, synth, gpu, plog, K, N, heuristic):
     """GPU stats vs the fp64-exact E-step: no further than the fp32 oracle is."""
     import torch
     b, mix, om, ost, ds, os_ = _setup(pkg, oracle, synth, K, N, heuristic=heuristic)
@@ -139,6 +144,7 @@ def test_stats_match_oracle(pkg, oracle, synth, gpu, K, N, heuristic):
     np.testing.assert_allclose(got[1], exact[1], rtol=1e-6)      # weightSum: finite weights
     eg, eo = _stats_err(got, exact, K), _stats_err(ref, exact, K)
     print(f"K={K} N={N} h={heuristic}: stats err gpu {eg:.2e}  oracle-fp32 {eo:.2e}")
+    plog("stats_rel_err_vs_fp64", eg, 2 * eo + 2e-6, oracle_fp32_err=eo)
     assert eg <= 2 * eo + 2e-6
 
 
@@ -159,8 +165,8 @@ def _param_err(p, q):
 
 
 @pytest.mark.parametrize("K,N,iters,heuristic", [(128, 16384, 5, False), (16, 8192, 6, True),
-                                                 (256, 6000, 3, False)])
-def test_em_matches_oracle(pkg, oracle, synth, gpu, K, N, iters, heuristic):
+                                                 (256, 6000, 3, False), (512, 4096, 2, False)])
+def test_em_matches_oracle(pkg, oracle, synth, gpu, plog, K, N, iters, heuristic):
     """StepwiseTangentEM::optimize x iters vs the exact (fp64 E-step) EM.
     Bound at every step: max(1e-4, 2 x the fp32 oracle's own distance to
     exact).  Where the fp32 reference arithmetic is well conditioned this is
@@ -182,6 +188,8 @@ def test_em_matches_oracle(pkg, oracle, synth, gpu, K, N, iters, heuristic):
         x = {k: getattr(xm, k) for k in ("weights", "mean", "cov")}
         eg, eo = _param_err(p, x), _param_err(o, x)
         print(f"K={K} it={it + 1}: param err vs exact: gpu {eg:.2e}  oracle-fp32-E {eo:.2e}")
+        plog("em_param_rel_err_vs_exact", eg, max(RTOL_PARAMS, 2 * eo), iteration=it + 1, oracle_fp32_err=eo,
+             within_north_star=bool(eg <= RTOL_PARAMS))
         assert eg <= max(RTOL_PARAMS, 2 * eo)
     st = mix.get_state()
     assert int(st["scalars"][3]) == iters
@@ -316,7 +324,7 @@ def _em_model(pkg, oracle, synth, K, N, iters):
 
 @pytest.mark.parametrize("K,iters,cap", [(16, 3, 40), (128, 4, 40), (128, 4, 4), (128, 4, 0),
                                          (256, 2, 40), (512, 2, 40), (512, 2, 0)])
-def test_guide_indices_bit_exact(pkg, oracle, synth, gpu, K, iters, cap):
+def test_guide_indices_bit_exact(pkg, oracle, synth, gpu, plog, K, iters, cap):
     """Guided bounces vs the oracle.  cap: per-query candidate-list capacity;
     4 sends most K=128 queries and 0 sends all of them down the full-K
     fallback path, which must give the same bits.  K=512 (the Kitchen
@@ -337,6 +345,9 @@ def test_guide_indices_bit_exact(pkg, oracle, synth, gpu, K, iters, cap):
     dg = np.stack([t.cpu().numpy() for t in d], 1)
     pg, cg = pdf.cpu().numpy(), comp.cpu().numpy()
     dr, pr, cr, sr = oracle.guide_batch(om, c.T, u.T)
+    plog("guide_index_mismatches", int((cg != cr).sum()), 0)
+    plog("guide_dir_abs_err", np.abs(dg - dr).max(), 1e-5)
+    plog("guide_pdf_err_over_tol(1e-4 rel + 1e-7 abs)", (np.abs(pg - pr) / (1e-7 + 1e-4 * np.abs(pr))).max(), 1.0)
     np.testing.assert_array_equal(cg, cr)            # bit-exact component selection
     np.testing.assert_allclose(dg, dr, atol=1e-5)
     np.testing.assert_allclose(pg, pr, rtol=1e-4, atol=1e-7)
