@@ -103,6 +103,9 @@ int sdmm_set_guide_capacity(sdmm_mix* m, int cap);
  * batch), so the queries of a wave touch the same components.  Outputs are
  * written at each query's own index and are identical either way. */
 int sdmm_set_guide_order(sdmm_mix* m, int coherent);
+/* Diagnostics: how many queries of the handle's last guided call (guide, pdf,
+ * product) took the full-K fallback path.  Synchronises the handle's stream. */
+int sdmm_guide_fallback_count(const sdmm_mix* m, int* count);
 /* Work is enqueued on this hipStream_t, taken literally (NULL = the HIP null
  * stream).  A new handle starts on its own non-blocking stream, whose value
  * sdmm_get_stream returns before any sdmm_set_stream call. */

@@ -23,7 +23,8 @@ from pathlib import Path
 import numpy as np
 
 PKG_DIR = Path(__file__).resolve().parent
-LIB_PATH = PKG_DIR / "lib" / "libsdmm_amd.so"
+# SDMM_LIB_PATH: an A/B variant of the library (tools/build_variant.sh)
+LIB_PATH = Path(os.environ.get("SDMM_LIB_PATH", PKG_DIR / "lib" / "libsdmm_amd.so"))
 REPO = PKG_DIR.parent
 
 
@@ -86,6 +87,7 @@ def lib():
         L.sdmm_kernel_name.argtypes = [C.c_void_p, C.c_int]
         L.sdmm_kernel_name.restype = C.c_char_p
         L.sdmm_set_guide_capacity.argtypes = [C.c_void_p, C.c_int]
+        L.sdmm_guide_fallback_count.argtypes = [C.c_void_p, C.c_void_p]
         L.sdmm_set_stream.argtypes = [C.c_void_p, C.c_void_p]
         L.sdmm_synchronize.argtypes = [C.c_void_p]
         L.sdmm_init_hemisphere.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_float,
@@ -143,7 +145,7 @@ def stats_len(K: int) -> int:
 EXPORTED_SYMBOLS = [
     "sdmm_em_params_default", "sdmm_create", "sdmm_destroy", "sdmm_num_components", "sdmm_layout",
     "sdmm_kernel_name",
-    "sdmm_set_guide_capacity", "sdmm_set_guide_order",
+    "sdmm_set_guide_capacity", "sdmm_set_guide_order", "sdmm_guide_fallback_count",
     "sdmm_set_stream", "sdmm_get_stream", "sdmm_synchronize", "sdmm_init_hemisphere",
     "sdmm_hemisphere_init_host", "sdmm_em_step", "sdmm_em_step_host", "sdmm_em_step_batched",
     "sdmm_em_step_batched_host",
@@ -378,6 +380,12 @@ class SDMM:
     def set_guide_capacity(self, cap: int):
         """Per-query candidate-list capacity of the guided-query kernel (0..40)."""
         _check(lib().sdmm_set_guide_capacity(self.h, cap))
+
+    def guide_fallback_count(self) -> int:
+        """Queries of the last guided call that took the full-K path (syncs)."""
+        n = C.c_int(0)
+        _check(lib().sdmm_guide_fallback_count(self.h, C.byref(n)))
+        return int(n.value)
 
     def set_guide_order(self, coherent: bool):
         """Serve large guided batches in Morton order of c (default) or as given."""

@@ -477,169 +477,182 @@ guide_tree_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __re
 }
 
 // ---------------------------------------------------------------------------
-// Fallback: the full-K conditional of one query.  The per-query marginal
-// weights live in LDS laid out [k][thread] (conflict-free); the sort is an
-// incremental selection that stops at the 0.99-mass cutoff.
-struct FullSlots {
-    const float* gp;
-    int Kp;
-    const float* c;
-    const float* wl;
-    const int* sl;
-    int T, tid;
-    __device__ int comp(int i) const { return sl[i * T + tid]; }
-    __device__ float weight(int i) const { return -wl[comp(i) * T + tid]; }
-    __device__ bool valid(int i) const { return cond_valid(gp, Kp, comp(i), c); }
-};
+// Fallback: the full-K conditional of one query, as the reference forms it
+// (mixture_model.h:248-284; oracle or_conditional_create):
+//
+//   total = sum_k w_k in component order;  cutoff = (float)(0.99 total);
+//   repeat: take the largest untaken w (lowest index among equals; the scan
+//   replaces only on a strictly larger value), accum += valid ? w : 0,
+//   stop once accum >= cutoff (lastIdx = K if never reached).
+//
+// build_full_wave below evaluates exactly this with a whole wave per query.
+// ---------------------------------------------------------------------------
+// Full-K queries, ONE query per wave (the fallback of the plain guide and of
+// the product path).  A full-K query costs O(K x kept) selection steps and,
+// with a learned BSDF, kept x M product pairs; served by a single thread it
+// was the long pole of a batch (round 1: 97 % of a Kitchen K = 512 product
+// call).  Same results as the selection above / finish_query / finish_product,
+// bit for bit:
+//   * lane l holds the weights of components l, l + 64, ... (K <= 512) in
+//     registers, by the same expression;
+//   * every order-dependent float reduction -- the total in component order,
+//     the kept weights' sum2 (createCdf), the product mass, the CDF walks, the
+//     pdf accumulations -- is formed in the reference order from v_readlane
+//     broadcasts, uniformly in every lane (no LDS round trip per term); a term
+//     the reference skips is added as -0.0f, an exact no-op (x + -0 == x for
+//     every x, NaN included);
+//   * each selection step picks what the reference scan picks -- among the
+//     untaken entries (sign bit clear) the largest, the lowest index among
+//     equals -- as a wave max then a wave min of the candidate indices; with a
+//     NaN among the untaken entries the scan's rule is order-dependent, so the
+//     scan itself runs (uniformly, in component order);
+//   * per-slot and per-pair quantities are evaluated by the lanes in parallel.
+// Needs all 64 lanes active (workgroup = one wave).
 
-__device__ __forceinline__ int build_full(const float* gp, int Kp, int K, const float c[3], float* wl, int* sl,
-                                          int T, int tid, float norm3, float& accum) {
-    float total = 0.0f;
-    for (int k = 0; k < K; ++k) {
-        const float wk = gp_ld(gp, Kp, GP_W, k) * marginal_pdf(gp, Kp, k, c, norm3);
-        wl[k * T + tid] = wk;
-        total += wk;
-    }
-    const float cutoff = (float)(0.99 * (double)total);
-    accum = 0.0f;
-    int lastIdx = K;   // the reference leaves it uninitialised if never reached
-    for (int i = 0; i < K; ++i) {
-        int best = -1;
-        float bw = 0.0f;
-        for (int k = 0; k < K; ++k) {
-            const float x = wl[k * T + tid];
-            if (__builtin_signbit(x)) continue;
-            if (best < 0 || x > bw) { best = k; bw = x; }
-        }
-        if (best < 0) { lastIdx = i; break; }
-        wl[best * T + tid] = -bw;
-        sl[i * T + tid] = best;
-        accum += cond_valid(gp, Kp, best, c) ? bw : 0.0f;
-        if (accum >= cutoff) { lastIdx = i + 1; break; }
-    }
-    return lastIdx;
+__device__ __forceinline__ float rl(float x, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
+}
+// acc += x of lanes 0 .. n-1, in lane order (uniform result)
+__device__ __forceinline__ float seq_sum(float acc, float x, int n) {
+    for (int l = 0; l < n; ++l) acc += rl(x, l);
+    return acc;
+}
+__device__ __forceinline__ float wave_max_f(float x) {   // no NaN
+    x = fmaxf(x, dpp<0xB1>(x));
+    x = fmaxf(x, dpp<0x4E>(x));
+    x = fmaxf(x, dpp<0x141>(x));
+    x = fmaxf(x, dpp<0x140>(x));
+    return fmaxf(fmaxf(rl(x, 0), rl(x, 16)), fmaxf(rl(x, 32), rl(x, 48)));
+}
+template <int CTRL>
+__device__ __forceinline__ int dppi(int x) { return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false); }
+__device__ __forceinline__ int wave_min_i(int x) {
+    x = min(x, dppi<0xB1>(x));
+    x = min(x, dppi<0x4E>(x));
+    x = min(x, dppi<0x141>(x));
+    x = min(x, dppi<0x140>(x));
+    return min(min(__builtin_amdgcn_readlane(x, 0), __builtin_amdgcn_readlane(x, 16)),
+               min(__builtin_amdgcn_readlane(x, 32), __builtin_amdgcn_readlane(x, 48)));
 }
 
-template <bool PDF_ONLY>
-__device__ __forceinline__ void serve_full(const float* gp, int Kp, int K, const GuideIO& io, int64_t q,
-                                           const float c[3], float* wl, int* sl, int T, int tid,
-                                           GuideConsts gc) {
-    float accum = 0.0f;
-    const int lastIdx = build_full(gp, Kp, K, c, wl, sl, T, tid, gc.norm3, accum);
-    finish_and_write<PDF_ONLY>(gp, Kp, c, lastIdx, accum, FullSlots{gp, Kp, c, wl, sl, T, tid}, io, q, gc);
-}
-
-// The fallback serves ONE query per wave (the lanes share its K components):
-// a fallback query is rare but costs O(K x kept) selection steps, and run by
-// a single thread it was the long pole of a batch (one such query, ~400 us at
-// K = 128).  Same results as build_full, bit for bit:
-//   * the weights, per component, by the same expression;
-//   * the total, summed by lane 0 in component order;
-//   * each selection step picks what build_full's scan picks -- among the
-//     untaken entries (sign bit clear), the largest, the lowest index among
-//     equals (the scan replaces only on a strictly larger value) -- as a wave
-//     reduction; with a NaN among the untaken entries the scan's rule is
-//     order-dependent, so lane 0 runs that scan itself;
-//   * the cutoff walk and finish_query (lane 0) unchanged.
-// LDS: K floats + K ints per wave (workgroup = one wave).
-__device__ __forceinline__ int build_full_wave(const float* gp, int Kp, int K, const float c[3], float* wl,
-                                               int* sl, int lane, int T, float norm3, float& accum) {
-    for (int k = lane; k < K; k += T) wl[k] = gp_ld(gp, Kp, GP_W, k) * marginal_pdf(gp, Kp, k, c, norm3);
-    __syncthreads();
-    float total = 0.0f;
-    if (lane == 0)
-        for (int k = 0; k < K; ++k) total += wl[k];
-    total = __shfl(total, 0);
-    const float cutoff = (float)(0.99 * (double)total);
-    accum = 0.0f;
-    int lastIdx = K;   // the reference leaves it uninitialised if never reached
-    for (int i = 0; i < K; ++i) {
-        int best = -1;
-        float bw = 0.0f;
-        bool nan_seen = false;
-        for (int k = lane; k < K; k += T) {   // this lane's entries in increasing k
-            const float x = wl[k];
-            if (__builtin_signbit(x)) continue;
-            nan_seen |= (x != x);
-            if (best < 0 || x > bw) { best = k; bw = x; }
-        }
-        if (__any(nan_seen)) {
-            if (lane == 0) {
-                best = -1;
-                bw = 0.0f;
-                for (int k = 0; k < K; ++k) {
-                    const float x = wl[k];
-                    if (__builtin_signbit(x)) continue;
-                    if (best < 0 || x > bw) { best = k; bw = x; }
-                }
-            }
-            best = __shfl(best, 0);
-            bw = __shfl(bw, 0);
-        } else {
-            for (int off = T >> 1; off >= 1; off >>= 1) {
-                const int ob = __shfl_xor(best, off);
-                const float ow = __shfl_xor(bw, off);
-                if (ob >= 0 && (best < 0 || ow > bw || (ow == bw && ob < best))) { best = ob; bw = ow; }
-            }
-        }
-        if (best < 0) { lastIdx = i; break; }
-        if (lane == 0) {
-            wl[best] = -bw;
-            sl[i] = best;
-        }
-        __syncthreads();
-        accum += cond_valid(gp, Kp, best, c) ? bw : 0.0f;   // uniform over the wave
-        if (accum >= cutoff) { lastIdx = i + 1; break; }
-    }
-    return lastIdx;
-}
+constexpr int kWaveKMax = 512;            // components per wave query: 8 per lane
+constexpr int kWaveSlots = kWaveKMax / 64;
 
 struct WaveLds {
-    float* wl;     // K   marginal weights (taken entries negated)
-    int* sl;       // K   kept slot -> component
-    float* fw;     // K   normalised slot weights slot_w(i)
-    float* pw;     // 64  per-lane chunk values
-    int* pf;       // 64  per-lane chunk flags
-    float* pall;   // pcap  product pair weights of pass 1 (when they fit)
-    int* pfall;    // pcap  their inclusion flags
+    int* sl;         // K   kept slot -> component | (conditional valid) << 31
+    float* fw;       // K   slot weights: raw, then slot_w(i)
+    float* se;       // 3K  conditional mean direction of each kept slot (product)
+    float* lobe;     // 20M world-frame learned-BSDF lobes of the query's material (product)
+    float* pc;       // this workgroup's global scratch: kPcStride x pcap floats, the product
+                     // pairs of pass 1 {w, included, mean, Linv, detInv} (when they fit)
     int pcap;
-    int T;         // lanes of the workgroup (one wave, <= 64)
 };
+constexpr int kPcStride = 10;
+constexpr int kProductPairCap = 1024;   // kept x lobes per full-K product query kept in scratch
 
-// fw[i] = slot_w(i) (finish_query's normalisation) for i < lastIdx; returns
-// sum2 (uniform over the wave).
-__device__ __forceinline__ float wave_slot_weights(const float* gp, int Kp, const float c[3], int lastIdx,
-                                                   float accum, const WaveLds& L, int lane) {
-    const float invSum = 1.0f / accum;
-    const bool scaled = __builtin_isfinite(invSum);
-    for (int i = lane; i < lastIdx; i += L.T) {
-        const int k = L.sl[i];
-        float wi = cond_valid(gp, Kp, k, c) ? -L.wl[k] : 0.0f;
-        if (scaled) wi = wi * invSum;
-        L.fw[i] = wi;
+// LDS carve-up of a one-wave workgroup (+ its slice of the pair scratch).
+__device__ __forceinline__ WaveLds wave_lds(float* lds, int K, float* pscratch = nullptr, int pcap = 0, int M = 0) {
+    WaveLds L;
+    L.sl = (int*)lds;
+    L.fw = lds + K;
+    L.se = lds + 2 * K;
+    L.lobe = L.se + 3 * K;
+    L.pc = pscratch ? pscratch + (size_t)blockIdx.x * kPcStride * pcap : nullptr;
+    L.pcap = pscratch ? pcap : 0;
+    return L;
+}
+static size_t wave_lds_bytes(int K, int M = 0) { return sizeof(float) * (5 * (size_t)K + 20 * (size_t)M) + 16; }
+
+// The kept prefix of query c's full-K conditional (above): slots
+// i < lastIdx in L.sl / L.fw (raw weight); returns lastIdx and accum.
+__device__ __forceinline__ int build_full_wave(const float* gp, int Kp, int K, const float c[3], const WaveLds& L,
+                                               int lane, float norm3, float& accum) {
+    float wr[kWaveSlots];
+    unsigned vmask = 0;   // bit i: the conditional of component lane + 64 i is valid
+#pragma unroll
+    for (int i = 0; i < kWaveSlots; ++i) {
+        const int k = lane + 64 * i;
+        wr[i] = -0.0f;    // absent: never a candidate
+        if (k < K) {
+            wr[i] = gp_ld(gp, Kp, GP_W, k) * marginal_pdf(gp, Kp, k, c, norm3);
+            vmask |= (cond_valid(gp, Kp, k, c) ? 1u : 0u) << i;
+        }
+    }
+    float total = 0.0f;   // component order
+#pragma unroll
+    for (int i = 0; i < kWaveSlots; ++i)
+        if (64 * i < K) total = seq_sum(total, wr[i], min(64, K - 64 * i));
+    const float cutoff = (float)(0.99 * (double)total);
+    accum = 0.0f;
+    int lastIdx = K;   // the reference leaves it uninitialised if never reached
+    for (int it = 0; it < K; ++it) {
+        float bv = -1.0f;
+        int bi = -1;
+        bool nan_seen = false;
+#pragma unroll
+        for (int i = 0; i < kWaveSlots; ++i) {
+            const float x = wr[i];
+            if (__builtin_signbit(x)) continue;
+            nan_seen |= (x != x);
+            if (bi < 0 || x > bv) { bv = x; bi = i; }
+        }
+        int best = -1;
+        float bw = 0.0f;
+        if (__any(nan_seen)) {
+            // the reference scan itself, in component order
+#pragma unroll
+            for (int i = 0; i < kWaveSlots; ++i)
+                for (int l = 0; l < 64 && 64 * i + l < K; ++l) {
+                    const float x = rl(wr[i], l);
+                    if (__builtin_signbit(x)) continue;
+                    if (best < 0 || x > bw) { best = 64 * i + l; bw = x; }
+                }
+        } else {
+            bw = wave_max_f(bi >= 0 ? bv : -1.0f);
+            if (bw >= 0.0f) best = wave_min_i((bi >= 0 && bv == bw) ? lane + 64 * bi : 0x7fffffff);
+        }
+        if (best < 0) { lastIdx = it; break; }
+#pragma unroll
+        for (int i = 0; i < kWaveSlots; ++i)
+            if (best == lane + 64 * i) wr[i] = -bw;
+        const bool ok = ((unsigned)__builtin_amdgcn_readlane((int)vmask, best & 63) >> (best >> 6)) & 1u;
+        if (lane == 0) {
+            L.sl[it] = best | (ok ? (int)0x80000000 : 0);
+            L.fw[it] = bw;
+        }
+        accum += ok ? bw : 0.0f;
+        if (accum >= cutoff) { lastIdx = it + 1; break; }
     }
     __syncthreads();
+    return lastIdx;
+}
+
+__device__ __forceinline__ int slot_comp(const WaveLds& L, int i) { return L.sl[i] & 0x7fffffff; }
+
+// L.fw[i] = slot_w(i) (finish_query's normalisation) for i < lastIdx;
+// returns sum2 (uniform).
+__device__ __forceinline__ float wave_slot_weights(int lastIdx, float accum, const WaveLds& L, int lane) {
+    const float invSum = 1.0f / accum;
+    const bool scaled = __builtin_isfinite(invSum);
     float sum2 = 0.0f;
-    if (lane == 0)
-        for (int i = 0; i < lastIdx; ++i) sum2 += L.fw[i];
-    sum2 = __shfl(sum2, 0);
+    for (int base = 0; base < lastIdx; base += 64) {
+        const int i = base + lane;
+        float wi = -0.0f;
+        if (i < lastIdx) {
+            wi = (L.sl[i] < 0) ? L.fw[i] : 0.0f;   // bit 31: valid conditional
+            if (scaled) wi = wi * invSum;
+            L.fw[i] = wi;
+        }
+        sum2 = seq_sum(sum2, wi, min(64, lastIdx - base));
+    }
     if (lastIdx > 0 && sum2 != 0.0f)
-        for (int i = lane; i < lastIdx; i += L.T) L.fw[i] = L.fw[i] / sum2;
+        for (int i = lane; i < lastIdx; i += 64) L.fw[i] = L.fw[i] / sum2;
     __syncthreads();
     return sum2;
 }
 
-// lane 0: acc += chunk values in lane order (flagged entries only)
-__device__ __forceinline__ void wave_chunk_sum(const WaveLds& L, int n, int lane, float& acc) {
-    __syncthreads();
-    if (lane == 0)
-        for (int l = 0; l < n; ++l)
-            if (L.pf[l]) acc += L.pw[l];
-    __syncthreads();
-}
-
 // finish_query with the lanes sharing the slots (the plain conditional: the
-// guide's fallback, and the product path's h = 0.5 case).  Valid on lane 0.
+// guide's fallback, and the product path's h = 0.5 case).  Uniform result.
 template <bool PDF_ONLY>
 __device__ QueryOut finish_query_wave(const float* gp, int Kp, const float c[3], const float u[3],
                                       const float* dir_in, int lastIdx, float sum2, const WaveLds& L, int lane,
@@ -648,21 +661,21 @@ __device__ QueryOut finish_query_wave(const float* gp, int Kp, const float c[3],
     if (lastIdx == 0 || sum2 == 0.0f) return o;   // createCdf(true) fails: BSDF only
     float dir[3];
     if constexpr (!PDF_ONLY) {
-        int ksel = 0;
-        if (lane == 0) {
-            float cdf = 0.0f, prev = 0.0f;
-            int slot = -1, runStart = 0;
-            for (int i = 0; i < lastIdx; ++i) {
-                cdf += L.fw[i];
-                if (i == 0 || cdf != prev) runStart = i;
+        // sampleDiscreteCdf: lower_bound == first slot with cdf >= u, else the tie walk
+        float cdf = 0.0f, prev = 0.0f;
+        int slot = -1, runStart = 0;
+        for (int base = 0; base < lastIdx && slot < 0; base += 64) {
+            const float x = (base + lane < lastIdx) ? L.fw[base + lane] : 0.0f;
+            const int n = min(64, lastIdx - base);
+            for (int l = 0; l < n; ++l) {
+                cdf += rl(x, l);
+                if (base + l == 0 || cdf != prev) runStart = base + l;
                 prev = cdf;
-                if (cdf >= u[0]) { slot = i; break; }
+                if (cdf >= u[0]) { slot = base + l; break; }
             }
-            if (slot < 0) slot = runStart;
-            ksel = L.sl[slot];
         }
-        ksel = __shfl(ksel, 0);
-        // every lane samples the same component identically (no broadcast)
+        if (slot < 0) slot = runStart;
+        const int ksel = slot_comp(L, slot);
         float esel[3];
         cond_mean_dir(gp, Kp, ksel, c, esel);
         const float radius = sqrtf(-2.0f * logf(1.0f - u[1]));
@@ -681,53 +694,33 @@ __device__ QueryOut finish_query_wave(const float* gp, int Kp, const float c[3],
     } else {
         dir[0] = dir_in[0]; dir[1] = dir_in[1]; dir[2] = dir_in[2];
     }
+    // MixtureModel::pdf over the conditional: terms in parallel, summed in slot order
     float acc = 0.0f;
-    for (int base = 0; base < lastIdx; base += L.T) {
+    for (int base = 0; base < lastIdx; base += 64) {
         const int i = base + lane;
-        float term = 0.0f;
-        int use = 0;
+        float term = -0.0f;
         if (i < lastIdx) {
             const float f = L.fw[i];
             if (f != 0.0f) {
-                const int k = L.sl[i];
+                const int k = slot_comp(L, i);
                 float e[3];
                 cond_mean_dir(gp, Kp, k, c, e);
                 term = f * cond_component_pdf(gp, Kp, k, e, dir, gc.norm2);
-                use = 1;
             }
         }
-        L.pw[lane] = term;
-        L.pf[lane] = use;
-        wave_chunk_sum(L, min(L.T, lastIdx - base), lane, acc);
+        acc = seq_sum(acc, term, min(64, lastIdx - base));
     }
     o.d[0] = dir[0]; o.d[1] = dir[1]; o.d[2] = dir[2];
     o.pdf = acc;
     return o;
 }
 
-// LDS carve-up of a one-wave workgroup: wl, sl, fw (K each), the 64-entry
-// chunk, then the pass-1 pair weights and flags (pcap each).
-__device__ __forceinline__ WaveLds wave_lds(float* lds, int K, int pcap, int T) {
-    WaveLds L;
-    L.T = T;
-    L.wl = lds;
-    L.sl = (int*)(lds + K);
-    L.fw = lds + 2 * K;
-    L.pw = lds + 3 * K;
-    L.pf = (int*)(lds + 3 * K + 64);
-    L.pall = lds + 3 * K + 128;
-    L.pfall = (int*)(lds + 3 * K + 128 + pcap);
-    L.pcap = pcap;
-    return L;
-}
-static size_t wave_lds_bytes(int K, int pcap) { return sizeof(float) * (3 * (size_t)K + 128 + 2 * (size_t)pcap); }
-
 template <bool PDF_ONLY>
 __device__ __forceinline__ void serve_full_wave(const float* gp, int Kp, int K, const GuideIO& io, int64_t q,
                                                 const float c[3], const WaveLds& L, int lane, GuideConsts gc) {
     float accum = 0.0f;
-    const int lastIdx = build_full_wave(gp, Kp, K, c, L.wl, L.sl, lane, L.T, gc.norm3, accum);
-    const float sum2 = wave_slot_weights(gp, Kp, c, lastIdx, accum, L, lane);
+    const int lastIdx = build_full_wave(gp, Kp, K, c, L, lane, gc.norm3, accum);
+    const float sum2 = wave_slot_weights(lastIdx, accum, L, lane);
     float u[3] = {0.0f, 0.0f, 0.0f}, dg[3] = {0.0f, 0.0f, 0.0f};
     if constexpr (PDF_ONLY) { dg[0] = io.e0[q]; dg[1] = io.e1[q]; dg[2] = io.e2[q]; }
     else { u[0] = io.u0[q]; u[1] = io.u1[q]; u[2] = io.u2[q]; }
@@ -742,68 +735,40 @@ __device__ __forceinline__ void serve_full_wave(const float* gp, int Kp, int K, 
     __syncthreads();   // the LDS is reused by the wave's next query
 }
 
-// A handful of fallback queries (at most one per workgroup): one query per
-// workgroup, its lanes cooperating (above).  Many (a small list capacity, or
-// a batch where most queries overflow): one query per thread, for throughput
-// (build_full).  Same bits either way.  LDS: K x blockDim floats + ints (the
-// per-thread form; blockDim <= 64, chosen so K_max fits).
+// The fallback queries listed by the candidate kernel, one per workgroup
+// (one wave), grid-stride.
 template <bool PDF_ONLY>
 __global__ void __launch_bounds__(64)
 guide_fallback_kernel(const float* __restrict__ gp, int Kp, int K, GuideIO io, GuideConsts gc,
                       const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int T = blockDim.x;
-    const int tid = threadIdx.x;
+    const int lane = threadIdx.x;
     const int count = *fb_count;
-    if (count <= (int)gridDim.x) {
-        if ((int)blockIdx.x >= count) return;
-        const int64_t q = fb_list[blockIdx.x];
-        const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
-        serve_full_wave<PDF_ONLY>(gp, Kp, K, io, q, c, wave_lds(lds, K, 0, T), tid, gc);
-        return;
-    }
-    float* wl = lds;
-    int* sl = (int*)(lds + (size_t)K * T);
-    for (int idx = blockIdx.x * T + tid; idx < count; idx += gridDim.x * T) {
+    const WaveLds L = wave_lds(lds, K);
+    for (int idx = blockIdx.x; idx < count; idx += gridDim.x) {
         const int64_t q = fb_list[idx];
         const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
-        serve_full<PDF_ONLY>(gp, Kp, K, io, q, c, wl, sl, T, tid, gc);
+        serve_full_wave<PDF_ONLY>(gp, Kp, K, io, q, c, L, lane, gc);
     }
 }
 
-// Fallback queries of the tree wavefront, the same two forms; kmax = the
-// largest K in tab.
+// Fallback queries of the tree wavefront (each against its own leaf's mixture;
+// kmax = the largest K in tab sizes the LDS).
 template <bool PDF_ONLY>
 __global__ void __launch_bounds__(64)
 guide_tree_fallback_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __restrict__ tab, int kmax,
                            GuideIO io, GuideConsts gc, const int* __restrict__ fb_count,
                            const int32_t* __restrict__ fb_list) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int T = blockDim.x;
-    const int tid = threadIdx.x;
+    const int lane = threadIdx.x;
     const int count = *fb_count;
-    if (count <= (int)gridDim.x) {
-        if ((int)blockIdx.x >= count) return;
-        const int64_t q = fb_list[blockIdx.x];
+    const WaveLds L = wave_lds(lds, kmax);
+    for (int idx = blockIdx.x; idx < count; idx += gridDim.x) {
+        const int64_t q = fb_list[idx];
         const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
         const int node = stree_find_point(nodes, c[0], c[1], c[2]);   // uniform: a listed query has a mixture
         const GuideMix mx = tab[node];
-        serve_full_wave<PDF_ONLY>(mx.gp, mx.Kp, mx.K, io, q, c, wave_lds(lds, mx.K, 0, T), tid, gc);
-        return;
-    }
-    float* wl = lds;
-    int* sl = (int*)(lds + (size_t)kmax * T);
-    for (int idx = blockIdx.x * T + tid; idx < count; idx += gridDim.x * T) {
-        const int64_t q = fb_list[idx];
-        const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
-        const int node = stree_find_point(nodes, c[0], c[1], c[2]);   // a listed query has a mixture
-        for (;;) {
-            const int n0 = __builtin_amdgcn_readfirstlane(node);
-            if (node != n0) continue;
-            const GuideMix mx = tab[n0];
-            serve_full<PDF_ONLY>(mx.gp, mx.Kp, mx.K, io, q, c, wl, sl, T, tid, gc);
-            break;
-        }
+        serve_full_wave<PDF_ONLY>(mx.gp, mx.Kp, mx.K, io, q, c, L, lane, gc);
     }
 }
 
@@ -985,16 +950,36 @@ struct ProdComp {
     float Linv[4];
     float detInv;
 };
-__device__ __noinline__ float mvtn_multiply(const float e[3], const float to_i[9], const float ci[4],
+__device__ __forceinline__ float mvtn_multiply(const float e[3], const float to_i[9], const float ci[4],
                                             const float mj[3], const float to_j[9], const float cj[4],
-                                            float norm2, ProdComp& out) {
-    float om0, om1, jac;
-    if (!ts_log_x(to_i, mj, om0, om1, jac)) return 0.0f;
-    float lj[6], a[6], from_j[9], b[6], ej[6], J[4], t[4], ocov[4];
-    log_jacobian(to_i, e, mj, lj);
+                                            float norm2, ProdComp& out, bool lazy) {
+    // ts_log_x(to_i, mj), keeping acos(c): logJacobian(to_i, e, mj) below forms
+    // the same r0, r1, clamped c and acos(c) (the same float expressions), so
+    // both share one evaluation -- bitwise what the two separate calls give
+    if (mj[0] == 0.0f && mj[1] == 0.0f && mj[2] == 0.0f) return 0.0f;
+    const float r0 = to_i[0] * mj[0] + to_i[1] * mj[1] + to_i[2] * mj[2];
+    const float r1 = to_i[3] * mj[0] + to_i[4] * mj[1] + to_i[5] * mj[2];
+    float c = to_i[6] * mj[0] + to_i[7] * mj[1] + to_i[8] * mj[2];
+    if (c <= -1.0f) return 0.0f;
+    c = (c < 1.0f) ? c : 1.0f;
+    const float angle = acos_x(c);
+    const float sang = sqrtf(1.0f - c * c);
+    const float jac = ((double)sang < 1e-3) ? 1.0f : (angle / sang);
+    const float om0 = r0 * jac, om1 = r1 * jac;
+    float lj[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    if (c == 1.0f || (mj[0] == e[0] && mj[1] == e[1] && mj[2] == e[2])) {
+        lj[0] = 1.0f; lj[4] = 1.0f;
+    } else {
+        const float aos = 1.0f / sinc_pi_x(angle);
+        lj[0] = aos; lj[4] = aos;
+        const float iss = 1.0f / (1.0f - c * c);
+        lj[2] = r0 * c * aos * iss - r0 * iss;
+        lj[5] = r1 * c * aos * iss - r1 * iss;
+    }
+    float a[6], from_j[9], b[6], ej[6], J[4], t[4], ocov[4];
     m23_33(lj, to_i, a);
     for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) from_j[3 * r + c] = to_j[3 * c + r];
+        for (int cc = 0; cc < 3; ++cc) from_j[3 * r + cc] = to_j[3 * cc + r];
     m23_33(a, from_j, b);
     exp_jacobian(0.0f, 0.0f, ej);
     m23_32(b, ej, J);
@@ -1007,19 +992,11 @@ __device__ __noinline__ float mvtn_multiply(const float e[3], const float to_i[9
     const float mt0 = 0.0f + (ci_ics[0] * om0 + ci_ics[1] * om1);
     const float mt1 = 0.0f + (ci_ics[2] * om0 + ci_ics[3] * om1);
     m22_mul(ci_ics, ocov, cnt);
-    if (!ts_exp_x(to_i, mt0, mt1, out.mean)) return 0.0f;
-    float to_n[9];
-    coordinates_f(out.mean, to_n);
-    float ln[6], a2[6], from_i[9], b2[6], ei[6], J2[4], t2[4], cov_n[4];
-    log_jacobian(to_n, out.mean, out.mean, ln);
-    m23_33(ln, to_n, a2);
-    for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) from_i[3 * r + c] = to_i[3 * c + r];
-    m23_33(a2, from_i, b2);
-    exp_jacobian(mt0, mt1, ei);
-    m23_32(b2, ei, J2);
-    m22_mul(J2, cnt, t2);
-    m22_mul_t(t2, J2, cov_n);
+    // The weight depends only on om, csum and jac.  Evaluated first: a pair
+    // whose weight is exactly 0 (FTZ) contributes nothing to a mass or a pdf
+    // whatever the rest gives (every later exit also returns 0), so with
+    // `lazy` it stops here.  The sampled pair is evaluated in full (a
+    // zero-weight pair is sampled only by u = 0 on the first pair).
     float Ls[4];
     if (!llt22(csum, Ls)) return 0.0f;
     const float invDet = 1.0f / (Ls[0] * Ls[3]);
@@ -1027,6 +1004,54 @@ __device__ __noinline__ float mvtn_multiply(const float e[3], const float to_i[9
     const float s1 = (om1 - Ls[2] * s0) / Ls[3];
     float w = (float)((double)norm2 * exp(-0.5 * (double)(s0 * s0 + s1 * s1)));
     w = w * (invDet * jac);
+    if (lazy && w == 0.0f) return 0.0f;
+    // ts_exp_x(to_i, mt) and expJacobian(mt) share |mt|, its sinc and cos
+    const float length = sqrtf(mt0 * mt0 + mt1 * mt1);
+    if ((double)length >= kPi) { out.mean[0] = out.mean[1] = out.mean[2] = 0.0f; return 0.0f; }
+    // sinc_pi_x(length) and cos_x(length) from one double sincos (one argument
+    // reduction; the same double values as the separate sin and cos)
+    double sd, cd;
+    sincos((double)length, &sd, &cd);
+    const float cs = (float)cd;
+    float sinc = 1.0f;
+    if (length >= 1.8581361171917516e-02f) {
+        sinc = (float)sd / length;
+    } else if (length >= 1.1920928955078125e-07f) {
+        const float x2 = length * length;
+        sinc -= x2 / 6.0f;
+        if (length >= 3.4526698300124393e-04f) sinc += (x2 * x2) / 120.0f;
+    }
+    {
+        const float rel0 = mt0 * sinc, rel1 = mt1 * sinc, rel2 = cs;
+        out.mean[0] = to_i[0] * rel0 + to_i[3] * rel1 + to_i[6] * rel2;
+        out.mean[1] = to_i[1] * rel0 + to_i[4] * rel1 + to_i[7] * rel2;
+        out.mean[2] = to_i[2] * rel0 + to_i[5] * rel1 + to_i[8] * rel2;
+    }
+    float to_n[9];
+    coordinates_f(out.mean, to_n);
+    float ln[6], a2[6], from_i[9], b2[6], ei[6], J2[4], t2[4], cov_n[4];
+    log_jacobian(to_n, out.mean, out.mean, ln);
+    m23_33(ln, to_n, a2);
+    for (int r = 0; r < 3; ++r)
+        for (int cc = 0; cc < 3; ++cc) from_i[3 * r + cc] = to_i[3 * cc + r];
+    m23_33(a2, from_i, b2);
+    for (int i = 0; i < 6; ++i) ei[i] = 0.0f;
+    if (length == 0.0f) {
+        ei[0] = 1.0f; ei[3] = 1.0f;
+    } else {
+        const float lsq = length * length;
+        const float cms = (cs - sinc) / lsq;
+        ei[0] = sinc + mt0 * mt0 * cms;
+        ei[3] = sinc + mt1 * mt1 * cms;
+        const float off = mt0 * mt1 * cms;
+        ei[2] = off;
+        ei[1] = off;
+        ei[4] = -mt0 * sinc;
+        ei[5] = -mt1 * sinc;
+    }
+    m23_32(b2, ei, J2);
+    m22_mul(J2, cnt, t2);
+    m22_mul_t(t2, J2, cov_n);
     if (!llt22(cov_n, out.L)) return 0.0f;
     m22_inv(out.L, out.Linv);
     out.detInv = 1.0f / (out.L[0] * out.L[3]);
@@ -1054,7 +1079,7 @@ template <class Slots, class Fn>
 __device__ __forceinline__ void for_each_pair(const float* gp, int Kp, const float* condCov, const float c[3],
                                               int lastIdx, float invSum, bool scaled, float sum2,
                                               const Slots& S, const BsdfTab& bt, int b, const float F[9],
-                                              float norm2, Fn&& fn) {
+                                              float norm2, bool lazy, Fn&& fn) {
     int p = 0;
     for (int i = 0; i < lastIdx; ++i) {
         float wi = S.valid(i) ? S.weight(i) : 0.0f;
@@ -1072,7 +1097,7 @@ __device__ __forceinline__ void for_each_pair(const float* gp, int Kp, const flo
             if (wj == 0.0f) continue;
             if (e[0] * mw[0] + e[1] * mw[1] + e[2] * mw[2] < 0.0f) continue;
             ProdComp pc;
-            const float nw = mvtn_multiply(e, to_i, ci, mw, tw, cj, norm2, pc);
+            const float nw = mvtn_multiply(e, to_i, ci, mw, tw, cj, norm2, pc, lazy);
             if (fn(p, k, j, wi * wj * nw, pc)) return;
             ++p;
         }
@@ -1110,7 +1135,7 @@ __device__ bool finish_product(const float* gp, int Kp, const float* condCov, co
     // pass 1: the product mass (createCdf(true)'s sum)
     float total = 0.0f;
     int P = 0;
-    for_each_pair(gp, Kp, condCov, c, lastIdx, invSum, scaled, sum2, S, bt, b, F, gc.norm2,
+    for_each_pair(gp, Kp, condCov, c, lastIdx, invSum, scaled, sum2, S, bt, b, F, gc.norm2, true,
                   [&](int, int, int, float w, const ProdComp&) { total += w; ++P; return false; });
     if (P == 0 || total == 0.0f) return false;
     float dir[3];
@@ -1121,7 +1146,7 @@ __device__ bool finish_product(const float* gp, int Kp, const float* condCov, co
         float cdf = 0.0f, prev = 0.0f;
         int runStart = 0, sel = -1, selComp = -1, runComp = -1;
         ProdComp pcs{}, runPc{};
-        for_each_pair(gp, Kp, condCov, c, lastIdx, invSum, scaled, sum2, S, bt, b, F, gc.norm2,
+        for_each_pair(gp, Kp, condCov, c, lastIdx, invSum, scaled, sum2, S, bt, b, F, gc.norm2, false,
                       [&](int p, int k, int j, float w, const ProdComp& pc) {
                           cdf += w / total;
                           if (p == 0 || cdf != prev) { runStart = p; runComp = k * bt.M + j; runPc = pc; }
@@ -1144,7 +1169,7 @@ __device__ bool finish_product(const float* gp, int Kp, const float* condCov, co
     }
     // pass 3: the product mixture pdf at dir
     float acc = 0.0f;
-    for_each_pair(gp, Kp, condCov, c, lastIdx, invSum, scaled, sum2, S, bt, b, F, gc.norm2,
+    for_each_pair(gp, Kp, condCov, c, lastIdx, invSum, scaled, sum2, S, bt, b, F, gc.norm2, true,
                   [&](int, int, int, float w, const ProdComp& pc) {
                       const float wn = w / total;
                       if (wn != 0.0f) acc += wn * prod_comp_pdf(pc, dir, gc.norm2);
@@ -1238,131 +1263,128 @@ guide_product_cand_kernel(const float* __restrict__ gp, int Kp, int K, const flo
 }
 
 // ---------------------------------------------------------------------------
-// Full-K fallback, ONE query per wave, for the product path (round 1's
-// thread-per-query guide_product_kernel took 97 % of a Kitchen K = 512 product
-// call) and the tail of the plain guide's fallback.  The kept prefix comes from
-// build_full_wave (bit-identical to build_full).  After it, every per-slot and
-// per-pair quantity is evaluated by the lanes in parallel, and every
-// order-dependent float reduction -- sum2 (createCdf), the product mass, the
-// CDF walks, the pdf accumulations -- is formed by lane 0 from LDS in the
-// reference order: the same operands, added in the same order, as
-// finish_query / finish_product, hence the same bits.
+// Product path, full-K queries one per wave (the section above for the
+// selection; the product terms follow finish_product / for_each_pair).
+//
+// Per query, before the pair passes (lanes in parallel): the conditional
+// mean direction of every kept slot with nonzero weight (cond_mean_dir_x) and
+// the world-frame lobes of the query's material (bsdf_world) -- the values
+// for_each_pair forms inside its loops, evaluated once instead of per pair.
+__device__ __forceinline__ void wave_prepare_product(const float* gp, int Kp, const float c[3], int lastIdx,
+                                                     const WaveLds& L, const BsdfTab& bt, int b, const float F[9],
+                                                     int lane) {
+    for (int i = lane; i < lastIdx; i += 64) {
+        if (L.fw[i] == 0.0f) continue;
+        float e[3];
+        cond_mean_dir_x(gp, Kp, slot_comp(L, i), c, e);
+        L.se[3 * i] = e[0]; L.se[3 * i + 1] = e[1]; L.se[3 * i + 2] = e[2];
+    }
+    for (int j = lane; j < bt.M; j += 64) {
+        float* lb = L.lobe + 20 * j;
+        bsdf_world(F, bt, b, j, lb, lb + 3, lb + 12, lb[16]);
+    }
+    __syncthreads();
+}
+
 // Product pair (slot i, lobe j) of for_each_pair: false when the walk skips
 // it (zero slot weight, zero lobe weight, opposite hemisphere); else its
 // weight wi * wj * nw and product component.
-__device__ __forceinline__ bool pair_eval(const float* gp, int Kp, const float* condCov, const float c[3],
-                                          const WaveLds& L, int i, int j, const BsdfTab& bt, int b,
-                                          const float F[9], float norm2, float& w, ProdComp& pc, int& k) {
+__device__ __forceinline__ bool pair_eval(const float* condCov, const WaveLds& L, int i, int j, float norm2,
+                                          float& w, ProdComp& pc, int& k, bool lazy = true) {
     const float wi = L.fw[i];
     if (wi == 0.0f) return false;
-    k = L.sl[i];
-    float e[3], to_i[9], ci[4];
-    cond_mean_dir_x(gp, Kp, k, c, e);
+    k = slot_comp(L, i);
+    const float e[3] = {L.se[3 * i], L.se[3 * i + 1], L.se[3 * i + 2]};
+    const float* lb = L.lobe + 20 * j;
+    const float wj = lb[16];
+    if (wj == 0.0f) return false;
+    if (e[0] * lb[0] + e[1] * lb[1] + e[2] * lb[2] < 0.0f) return false;
+    float to_i[9], ci[4];
     coordinates_f(e, to_i);
     for (int l = 0; l < 4; ++l) ci[l] = condCov[4 * k + l];
-    float mw[3], tw[9], cj[4], wj;
-    bsdf_world(F, bt, b, j, mw, tw, cj, wj);
-    if (wj == 0.0f) return false;
-    if (e[0] * mw[0] + e[1] * mw[1] + e[2] * mw[2] < 0.0f) return false;
-    const float nw = mvtn_multiply(e, to_i, ci, mw, tw, cj, norm2, pc);
+    const float nw = mvtn_multiply(e, to_i, ci, lb, lb + 3, lb + 12, norm2, pc, lazy);
     w = wi * wj * nw;
     return true;
 }
 
 // finish_product with the pairs spread over the lanes (64 per chunk, flat
-// index f = slot * M + lobe: the reference's walk order).  Returns false when
-// the product is unusable (no pair / zero mass); uniform over the wave.
+// index f = slot * M + lobe: the reference's walk order).  When the kept x M
+// pairs fit L.pcap, pass 1 keeps each pair's {w, mean, Linv, detInv} in the
+// workgroup's scratch (written and re-read by the same wave: L2-resident) and
+// the CDF walk and the pdf read them; otherwise they are recomputed.
+// Returns false when the product is unusable (no pair / zero mass).
 template <bool PDF_ONLY>
 __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCov, const float c[3], int lastIdx,
                                     const WaveLds& L, const BsdfTab& bt, int b, const float F[9], const float* u,
                                     const float* dir_in, int lane, GuideConsts gc, QueryOut& o) {
     const int M = bt.M;
     const int NP = lastIdx * M;
-    const bool keep = NP <= L.pcap;   // pass 1's weights stay in LDS for the CDF walk
+    const bool keep = NP <= L.pcap;
+    wave_prepare_product(gp, Kp, c, lastIdx, L, bt, b, F, lane);
     // pass 1: the product mass (createCdf(true)'s sum) and the pair count
     float total = 0.0f;
     int P = 0;
-    for (int base = 0; base < NP; base += L.T) {
+    for (int base = 0; base < NP; base += 64) {
         const int f = base + lane;
         float w = 0.0f;
-        int inc = 0;
+        bool inc = false;
         if (f < NP) {
             ProdComp pc{};
             int k;
-            inc = pair_eval(gp, Kp, condCov, c, L, f / M, f % M, bt, b, F, gc.norm2, w, pc, k) ? 1 : 0;
-            if (keep) { L.pall[f] = w; L.pfall[f] = inc; }
+            inc = pair_eval(condCov, L, f / M, f % M, gc.norm2, w, pc, k);
+            if (keep) {
+                float* r = L.pc + kPcStride * f;
+                r[0] = w;
+                r[1] = inc ? 1.0f : 0.0f;
+                r[2] = pc.mean[0]; r[3] = pc.mean[1]; r[4] = pc.mean[2];
+                r[5] = pc.Linv[0]; r[6] = pc.Linv[1]; r[7] = pc.Linv[2]; r[8] = pc.Linv[3];
+                r[9] = pc.detInv;
+            }
         }
-        L.pw[lane] = w;
-        L.pf[lane] = inc;
-        __syncthreads();
-        if (lane == 0) {
-            const int n = min(L.T, NP - base);
-            for (int l = 0; l < n; ++l)
-                if (L.pf[l]) { total += L.pw[l]; ++P; }
-        }
-        __syncthreads();
+        total = seq_sum(total, inc ? w : -0.0f, min(64, NP - base));
+        P += __builtin_popcountll(__builtin_amdgcn_ballot_w64(inc));
     }
-    total = __shfl(total, 0);
-    P = __shfl(P, 0);
+    __syncthreads();
     if (P == 0 || total == 0.0f) return false;
     float dir[3];
     o.comp = -1;
     if constexpr (!PDF_ONLY) {
         // pass 2: sampleDiscreteCdf over w / total (lower_bound + tie walk)
-        int sel_f = -1;
-        if (keep) {
-            if (lane == 0) {
-                float cdf = 0.0f, prev = 0.0f;
-                int p = 0, run_f = -1;
-                for (int f = 0; f < NP; ++f) {
-                    if (!L.pfall[f]) continue;
-                    cdf += L.pall[f] / total;
-                    if (p == 0 || cdf != prev) run_f = f;
-                    prev = cdf;
-                    ++p;
-                    if (cdf >= u[0]) { sel_f = f; break; }
-                }
-                if (sel_f < 0) sel_f = run_f;
-            }
-        } else {
-            float cdf = 0.0f, prev = 0.0f;   // lane 0's walk state
-            int p = 0, run_f = -1, done = 0;
-            for (int base = 0; base < NP; base += L.T) {
-                const int f = base + lane;
-                float x = 0.0f;
-                int inc = 0;
-                if (f < NP) {
+        float cdf = 0.0f, prev = 0.0f;
+        int p = 0, run_f = -1, sel_f = -1;
+        for (int base = 0; base < NP && sel_f < 0; base += 64) {
+            const int f = base + lane;
+            float x = 0.0f;
+            bool inc = false;
+            if (f < NP) {
+                float w = 0.0f;
+                if (keep) {
+                    inc = L.pc[kPcStride * f + 1] != 0.0f;
+                    w = L.pc[kPcStride * f];
+                } else {
                     ProdComp pc{};
                     int k;
-                    float w = 0.0f;
-                    inc = pair_eval(gp, Kp, condCov, c, L, f / M, f % M, bt, b, F, gc.norm2, w, pc, k) ? 1 : 0;
-                    if (inc) x = w / total;
+                    inc = pair_eval(condCov, L, f / M, f % M, gc.norm2, w, pc, k);
                 }
-                L.pw[lane] = x;
-                L.pf[lane] = inc;
-                __syncthreads();
-                if (lane == 0) {
-                    const int n = min(L.T, NP - base);
-                    for (int l = 0; l < n; ++l) {
-                        if (!L.pf[l]) continue;
-                        cdf += L.pw[l];
-                        if (p == 0 || cdf != prev) run_f = base + l;
-                        prev = cdf;
-                        ++p;
-                        if (cdf >= u[0]) { sel_f = base + l; done = 1; break; }
-                    }
-                }
-                __syncthreads();
-                if (__shfl(done, 0)) break;
+                if (inc) x = w / total;
             }
-            if (lane == 0 && sel_f < 0) sel_f = run_f;
+            const uint64_t incm = __builtin_amdgcn_ballot_w64(inc);
+            const int n = min(64, NP - base);
+            for (int l = 0; l < n; ++l) {
+                if (!((incm >> l) & 1)) continue;
+                cdf += rl(x, l);
+                if (p == 0 || cdf != prev) run_f = base + l;
+                prev = cdf;
+                ++p;
+                if (cdf >= u[0]) { sel_f = base + l; break; }
+            }
         }
-        sel_f = __shfl(sel_f, 0);
-        // the selected pair's product component, recomputed (uniform)
+        if (sel_f < 0) sel_f = run_f;
+        // the selected pair's product component, evaluated in full (uniform)
         ProdComp pcs{};
         int ksel = 0;
         float wsel = 0.0f;
-        (void)pair_eval(gp, Kp, condCov, c, L, sel_f / M, sel_f % M, bt, b, F, gc.norm2, wsel, pcs, ksel);
+        (void)pair_eval(condCov, L, sel_f / M, sel_f % M, gc.norm2, wsel, pcs, ksel, false);
         const float radius = sqrtf(-2.0f * log_x(1.0f - u[1]));
         const float theta = (float)(2.0 * kPi * (double)u[2]);
         const float z0 = radius * sin_x(theta), z1 = radius * cos_x(theta);
@@ -1377,25 +1399,33 @@ __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCo
     }
     // pass 3: the product mixture pdf at dir
     float acc = 0.0f;
-    for (int base = 0; base < NP; base += L.T) {
+    for (int base = 0; base < NP; base += 64) {
         const int f = base + lane;
-        float term = 0.0f;
-        int use = 0;
-        if (f < NP && (!keep || L.pfall[f])) {
-            ProdComp pc{};
-            int k;
-            float w = 0.0f;
-            if (pair_eval(gp, Kp, condCov, c, L, f / M, f % M, bt, b, F, gc.norm2, w, pc, k)) {
-                const float wn = w / total;
-                if (wn != 0.0f) {
-                    term = wn * prod_comp_pdf(pc, dir, gc.norm2);
-                    use = 1;
+        float term = -0.0f;
+        if (f < NP) {
+            if (keep) {
+                const float* r = L.pc + kPcStride * f;
+                if (r[1] != 0.0f) {
+                    const float wn = r[0] / total;
+                    if (wn != 0.0f) {
+                        ProdComp pc{};
+                        pc.mean[0] = r[2]; pc.mean[1] = r[3]; pc.mean[2] = r[4];
+                        pc.Linv[0] = r[5]; pc.Linv[1] = r[6]; pc.Linv[2] = r[7]; pc.Linv[3] = r[8];
+                        pc.detInv = r[9];
+                        term = wn * prod_comp_pdf(pc, dir, gc.norm2);
+                    }
+                }
+            } else {
+                ProdComp pc{};
+                int k;
+                float w = 0.0f;
+                if (pair_eval(condCov, L, f / M, f % M, gc.norm2, w, pc, k)) {
+                    const float wn = w / total;
+                    if (wn != 0.0f) term = wn * prod_comp_pdf(pc, dir, gc.norm2);
                 }
             }
         }
-        L.pw[lane] = term;
-        L.pf[lane] = use;
-        wave_chunk_sum(L, min(L.T, NP - base), lane, acc);
+        acc = seq_sum(acc, term, min(64, NP - base));
     }
     o.d[0] = dir[0]; o.d[1] = dir[1]; o.d[2] = dir[2];
     o.pdf = acc;
@@ -1409,7 +1439,7 @@ __device__ void product_tail_wave(const float* gp, int Kp, const float* condCov,
                                   const BsdfTab& bt, int64_t q, int lane, GuideConsts gc) {
     int b = pio.material ? pio.material[q] : -1;
     if (b >= bt.B) b = -1;
-    const float sum2 = wave_slot_weights(gp, Kp, c, lastIdx, accum, L, lane);
+    const float sum2 = wave_slot_weights(lastIdx, accum, L, lane);
     const bool cvalid = lastIdx > 0 && sum2 != 0.0f;
     QueryOut o{{0.0f, 0.0f, 0.0f}, 0.0f, -1};
     float h = 1.0f;                       // no valid conditional: BSDF only
@@ -1442,22 +1472,25 @@ __device__ void product_tail_wave(const float* gp, int Kp, const float* condCov,
     }
 }
 
-// The product path's full-K queries (listed by guide_product_cand_kernel, or
-// every query when fb_list is null): one wave per query, grid-stride.
+// The product path's full-K queries (listed by guide_product_cand_kernel):
+// one wave per query, grid-stride.
+#ifndef SDMM_PRODUCT_WPE
+#define SDMM_PRODUCT_WPE 2   // waves per SIMD the register budget is sized for (A/B knob)
+#endif
 template <bool PDF_ONLY>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDMM_PRODUCT_WPE)))
 guide_product_wave_kernel(const float* __restrict__ gp, int Kp, int K, const float* __restrict__ condCov,
-                          int64_t nq, GuideIO io, ProductIO pio, BsdfTab bt, GuideConsts gc, int pcap,
-                          const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list) {
+                          GuideIO io, ProductIO pio, BsdfTab bt, GuideConsts gc, float* __restrict__ pscratch,
+                          int pcap, const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x;
-    const WaveLds L = wave_lds(lds, K, pcap, 64);
-    const int64_t n = fb_list ? (int64_t)*fb_count : nq;
-    for (int64_t idx = blockIdx.x; idx < n; idx += gridDim.x) {
-        const int64_t q = fb_list ? (int64_t)fb_list[idx] : idx;
+    const WaveLds L = wave_lds(lds, K, pscratch, pcap, bt.M);
+    const int n = *fb_count;
+    for (int idx = blockIdx.x; idx < n; idx += gridDim.x) {
+        const int64_t q = fb_list[idx];
         const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
         float accum = 0.0f;
-        const int lastIdx = build_full_wave(gp, Kp, K, c, L.wl, L.sl, lane, 64, gc.norm3, accum);
+        const int lastIdx = build_full_wave(gp, Kp, K, c, L, lane, gc.norm3, accum);
         product_tail_wave<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, accum, L, io, pio, bt, q, lane, gc);
         __syncthreads();   // the LDS is reused by the next query
     }
@@ -1532,14 +1565,6 @@ static hipError_t coherent_order(const float* const c[3], int n, uint32_t* keys_
     return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, idx_in, idx_out, n, 0, 30, st);
 }
 
-// Workgroup width of the fallback kernels: the widest T <= 64 (a power of
-// two) whose K x T weight + index lists fit the 160 KB LDS (K = 512 -> 32).
-static int fallback_width(int kmax) {
-    int T = 64;
-    while (T > 1 && (size_t)kmax * T * (sizeof(float) + sizeof(int)) > 160 * 1024) T >>= 1;
-    return T;
-}
-
 static GuideIO make_io(const float* const c[3], const float* const u[3], const float* const dgiven[3],
                        float* const d[3], float* pdf, int32_t* comp) {
     const bool pdf_only = dgiven != nullptr;
@@ -1603,9 +1628,9 @@ hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float*
     cap = (cap < 0) ? 0 : (cap > kGuideCap ? kGuideCap : cap);
     if (nq > INT32_MAX) return hipErrorInvalidValue;
     const int T = 64;
-    const int Tfb = fallback_width(K);
-    const size_t lds_fb = std::max((size_t)K * Tfb * (sizeof(float) + sizeof(int)), wave_lds_bytes(K, 0));
-    if (lds_fb > 160 * 1024) return hipErrorInvalidValue;
+    if (K > kWaveKMax) return hipErrorInvalidValue;
+    const int Tfb = 64;
+    const size_t lds_fb = wave_lds_bytes(K);
     GuideConsts gc{norm2, norm3};
     hipError_t e = hipMemsetAsync(fb_count, 0, sizeof(int), st);
     if (e != hipSuccess) return e;
@@ -1617,7 +1642,7 @@ hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float*
         perm = sort->idx[1];
     }
     const dim3 grid((unsigned)((nq + T - 1) / T));
-    const int fb_blocks = cus * 2;
+    const int fb_blocks = cus * 8;
     const GuideIO io = make_io(c, u, dgiven, d, pdf, comp);
     cap = cap < K ? cap : K;
     e = dgiven ? launch_cand<true>(cap, grid, st, gp, Kp, K, nq, io, gc, fb_count, fb_list, perm)
@@ -1646,9 +1671,9 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
     if (nq > INT32_MAX) return hipErrorInvalidValue;
     const int T = 64;
     if (kmax < 1) kmax = 1;
-    const int Tfb = fallback_width(kmax);
-    const size_t lds_fb = std::max((size_t)kmax * Tfb * (sizeof(float) + sizeof(int)), wave_lds_bytes(kmax, 0));
-    if (lds_fb > 160 * 1024) return hipErrorInvalidValue;
+    if (kmax > kWaveKMax) return hipErrorInvalidValue;
+    const int Tfb = 64;
+    const size_t lds_fb = wave_lds_bytes(kmax);
     GuideConsts gc{norm2, norm3};
     hipError_t e = hipMemsetAsync(fb_count, 0, sizeof(int), st);
     if (e != hipSuccess) return e;
@@ -1662,7 +1687,7 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
     const STNodeDev* nd = (const STNodeDev*)nodes;
     const GuideMix* tb = (const GuideMix*)tab;
     const dim3 grid((unsigned)((nq + T - 1) / T));
-    const int fb_blocks = cus * 2;
+    const int fb_blocks = cus * 8;
     const GuideIO io = make_io(c, u, dgiven, d, pdf, comp);
     cap = cap < kmax ? cap : kmax;
     e = dgiven ? launch_tree_cand<true>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_out)
@@ -1687,10 +1712,8 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
                                 int32_t* fb_list, int cus, hipStream_t st, const GuideSortScratch* sort) {
     if (nq <= 0) return hipSuccess;
     if (nq > INT32_MAX) return hipErrorInvalidValue;
-    // pass-1 pair weights kept in LDS up to 2048 pairs (16 KB + the K lists)
-    const int pcap = 2048;
-    const size_t lds = wave_lds_bytes(K, pcap);
-    if (lds > 64 * 1024) return hipErrorInvalidValue;
+    if (K > kWaveKMax || M > 64) return hipErrorInvalidValue;
+    const size_t lds = wave_lds_bytes(K, M);
     cap = (cap < 0) ? 0 : (cap > kGuideCap ? kGuideCap : cap);
     cap = cap < K ? cap : K;
     GuideConsts gc{norm2, norm3};
@@ -1725,14 +1748,27 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
 #undef SDMM_PRODUCT_CAND
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const dim3 fgrid((unsigned)(cus * 8));
+    // the full-K queries' product pairs (up to kProductPairCap per query) live in a
+    // stream-ordered scratch for the call: one slice per workgroup
+    const unsigned fblocks = (unsigned)(cus * 8);
+    float* pscratch = nullptr;
+    const size_t sbytes = sizeof(float) * kPcStride * (size_t)kProductPairCap * fblocks;
+    if (hipMallocAsync((void**)&pscratch, sbytes, st) != hipSuccess) {
+        (void)hipGetLastError();
+        pscratch = nullptr;   // no scratch: the pairs are recomputed (same results)
+    }
     if (dgiven)
-        hipLaunchKernelGGL(guide_product_wave_kernel<true>, fgrid, dim3(64), lds, st, gp, Kp, K, condCov, nq, io,
-                           pio, bt, gc, pcap, fb_count, fb_list);
+        hipLaunchKernelGGL(guide_product_wave_kernel<true>, dim3(fblocks), dim3(64), lds, st, gp, Kp, K, condCov, io,
+                           pio, bt, gc, pscratch, kProductPairCap, fb_count, fb_list);
     else
-        hipLaunchKernelGGL(guide_product_wave_kernel<false>, fgrid, dim3(64), lds, st, gp, Kp, K, condCov, nq, io,
-                           pio, bt, gc, pcap, fb_count, fb_list);
-    return hipGetLastError();
+        hipLaunchKernelGGL(guide_product_wave_kernel<false>, dim3(fblocks), dim3(64), lds, st, gp, Kp, K, condCov,
+                           io, pio, bt, gc, pscratch, kProductPairCap, fb_count, fb_list);
+    e = hipGetLastError();
+    if (pscratch) {
+        const hipError_t f = hipFreeAsync(pscratch, st);
+        if (e == hipSuccess) e = f;
+    }
+    return e;
 }
 
 hipError_t launch_sample_cdf(const float* cdf, int n, const float* u, int64_t nq, int32_t* out,

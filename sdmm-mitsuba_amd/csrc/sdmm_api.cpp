@@ -574,6 +574,16 @@ int sdmm_set_guide_capacity(sdmm_mix* m, int cap) {
     return SDMM_OK;
 }
 
+int sdmm_guide_fallback_count(const sdmm_mix* m, int* count) {
+    if (!m || !count) return fail(SDMM_E_INVALID, "invalid argument");
+    *count = 0;
+    if (!m->guide_fb) return SDMM_OK;
+    HIP_TRY(hipSetDevice(m->device));
+    HIP_TRY(hipMemcpyAsync(count, m->guide_fb, sizeof(int), hipMemcpyDeviceToHost, m->stream));
+    HIP_TRY(hipStreamSynchronize(m->stream));
+    return SDMM_OK;
+}
+
 int sdmm_layout(const sdmm_mix* m, int* resp_cpl, int* resp_lps, int* stats_cpl, int* stats_lps) {
     if (!m) return fail(SDMM_E_INVALID, "null handle");
     if (resp_cpl) *resp_cpl = m->rcpl;
