@@ -10,8 +10,10 @@ before timing; the N x K fp32 responsibilities are written to HBM.
 
 Multi-GPU (torchrun, one process per GPU): the N samples are sharded
 contiguously across ranks (strong scaling, no data-path collective for the
-E-step); warm EM iterations all-reduce the fp64 sufficient statistics with
-RCCL before each M-step.  value = N / max-over-ranks step time.
+E-step); EM steps go through the library's own RCCL communicator
+(sdmm_comm_init_rccl, sdmm_em_step_sharded: the fp64 sufficient statistics are
+all-reduced over xGMI before each M-step).  value = N / max-over-ranks step
+time.
 
 Also reported (same JSON line): the full EM step (E-step + statistics +
 all-reduce + M-step), guided queries/sec (conditional + sample + pdf, Q = 2^20,
@@ -94,42 +96,53 @@ def cpu_baseline(batch, K, pos, nrm, synth, n_sample, threads):
             "single_thread": {"value": n1 / t1, "cores": 1, "sample": f"{n1} samples, 1 pass", "seconds": t1}}
 
 
-def leaf_em_bench(pkg, synth, batch, n_local, shard, dev, stream, args, timed, world,
-                  K=16, leaf_samples=4096):
-    """One batched EM step over n_local / leaf_samples leaves of K components
-    (sdmm_em_step_batched), against the same leaves stepped one call each."""
-    n_leaves = n_local // leaf_samples
+def leaf_em_bench(pkg, synth, full, N, dev, stream, args, timed, world, rank, comm, K=16, leaf_samples=4096):
+    """The plugin's per-leaf EM over N / leaf_samples leaves of K components
+    (volpath_sdmm.cpp:287-311), leaf-sharded: rank r steps the
+    leaves it owns (owner = leaf % world) in one batched call
+    (sdmm_em_step_batched), then every leaf's parameters are broadcast from its
+    owner (sdmm_mix_broadcast, one fused RCCL group) so every rank can guide
+    with all of them.  Strong scaling (the leaves are fixed); also the same
+    owned leaves stepped by per-leaf calls, for comparison."""
+    n_leaves = N // leaf_samples
     seg = np.arange(n_leaves + 1, dtype=np.int64) * leaf_samples
-    x = np.stack([t.cpu().numpy() for t in shard.x])
+    x = np.stack([t.cpu().numpy() for t in full.x])
     nrm = np.ascontiguousarray(x[3:6].T)    # seed "normals": any unit vectors (directions)
     n_pos = K // 8
+    mixes = []
+    for i in range(n_leaves):
+        a = int(seg[i])
+        m = pkg.SDMM(K, device=dev.index, stream=stream)
+        m.init_hemisphere(x[0:3, a:a + n_pos].T.copy(), nrm[a:a + n_pos].copy(), synth.DEPTH_PRIOR,
+                          synth.SPATIAL_DISTANCE, synth.SEED_MODEL + i)
+        mixes.append(m)
+    owner = (np.arange(n_leaves) % world).astype(np.int32)
+    mine = [i for i in range(n_leaves) if owner[i] == rank]
+    own_mixes = [mixes[i] for i in mine]
+    import torch
+    idx = torch.from_numpy(np.concatenate([np.arange(seg[i], seg[i + 1]) for i in mine])).to(dev)
+    own = pkg.DeviceSamples([t[idx] for t in full.x], full.w[idx])
+    own_seg = np.arange(len(mine) + 1, dtype=np.int64) * leaf_samples
 
-    def make():
-        mixes = []
-        for i in range(n_leaves):
-            a = int(seg[i])
-            m = pkg.SDMM(K, device=dev.index, stream=stream)
-            m.init_hemisphere(x[0:3, a:a + n_pos].T.copy(), nrm[a:a + n_pos].copy(), synth.DEPTH_PRIOR,
-                              synth.SPATIAL_DISTANCE, synth.SEED_MODEL + i)
-            mixes.append(m)
-        return mixes
-
-    mixes = make()
-    leaves = [pkg.DeviceSamples([t[int(seg[i]):int(seg[i + 1])] for t in shard.x],
-                                shard.w[int(seg[i]):int(seg[i + 1])]) for i in range(n_leaves)]
-    pkg.em_step_batched(mixes, shard, seg, 1)          # warm-up (tables, partial rows)
+    def step():
+        pkg.em_step_batched(own_mixes, own, own_seg, 1)
+        if comm is not None:
+            pkg.mix_broadcast(mixes, owner, comm)
+    step()                                          # warm-up (tables, partial rows)
     steps = max(3, args.steps // 4)
-    b_wall, b_kern = timed(lambda: pkg.em_step_batched(mixes, shard, seg, 1), steps)
+    b_wall, b_kern = timed(step, steps)
+    leaves = [pkg.DeviceSamples([t[int(own_seg[j]):int(own_seg[j + 1])] for t in own.x],
+                                own.w[int(own_seg[j]):int(own_seg[j + 1])]) for j in range(len(mine))]
 
     def sequential():
-        for m, leaf in zip(mixes, leaves):
+        for m, leaf in zip(own_mixes, leaves):
             m.optimize(leaf)
     sequential()
     s_wall, _ = timed(sequential, 2, events=False)
-    n_all = n_leaves * leaf_samples * world
-    return {"samples_per_s": n_all / (b_wall / steps), "ms_per_step": b_wall / steps * 1e3,
-            "device_ms_per_step": b_kern * 1e3, "leaves": n_leaves * world, "K": K,
-            "samples_per_leaf": leaf_samples, "scaling": "weak (leaves sharded, no exchange)",
+    return {"samples_per_s": n_leaves * leaf_samples / (b_wall / steps), "ms_per_step": b_wall / steps * 1e3,
+            "device_ms_per_step": b_kern * 1e3, "leaves": n_leaves, "leaves_per_rank": len(mine), "K": K,
+            "samples_per_leaf": leaf_samples,
+            "scaling": "strong (leaves sharded over ranks, parameters broadcast from their owners)",
             "sequential_per_leaf_calls_ms": s_wall / 2 * 1e3}
 
 
@@ -175,7 +188,7 @@ def wavefront_bench(pkg, synth, batch, shard, tree, dev, stream, ct, ut, gout, t
             "guided_frac": float((comp >= 0).mean()), "scaling": "weak (replicas: queries per rank)"}
 
 
-def large_k_bench(pkg, synth, batch, shard, dev, stream, timed, args, world, N):
+def large_k_bench(pkg, synth, batch, shard, dev, stream, timed, args, world, N, comm):
     """BASELINE configs[3] and [4] on one GPU: a full EM step at K=256 (Pool)
     and K=512 (Kitchen) on the same 2^20-sample batch (sample-sharded, RCCL
     all-reduce of the statistics when world > 1), and the Kitchen's guided
@@ -187,13 +200,9 @@ def large_k_bench(pkg, synth, batch, shard, dev, stream, timed, args, world, N):
         pos, nrm = synth.model_seed_points(batch, K)
         m = pkg.SDMM(K, device=dev.index, stream=stream)
         m.init_hemisphere(pos, nrm, synth.DEPTH_PRIOR, synth.SPATIAL_DISTANCE, synth.SEED_MODEL)
-        stats = torch.zeros(pkg.stats_len(K), dtype=torch.float64, device=dev)
-
         def em_step():
-            if world > 1:
-                m.estep_stats(shard, stats)
-                torch.distributed.all_reduce(stats)
-                m.mstep(stats, N)
+            if comm is not None:
+                m.optimize_sharded(comm, shard)      # RCCL sum of the statistics (library)
             else:
                 m.optimize(shard)
         for _ in range(3):
@@ -274,12 +283,16 @@ def main():
     mix = pkg.SDMM(K, device=dev.index, stream=stream)
     mix.init_hemisphere(pos, nrm, synth.DEPTH_PRIOR, synth.SPATIAL_DISTANCE, synth.SEED_MODEL)
     stats = torch.zeros(pkg.stats_len(K), dtype=torch.float64, device=dev)
+    # the library's own communicator: RCCL over xGMI (the unique id travels
+    # through torch.distributed); the rehearsal shares one GPU, where RCCL
+    # refuses two ranks, so it uses the host transport over gloo
+    comm = None
+    if world > 1:
+        comm = pkg.Comm.from_torch_gloo(dev.index) if rehearse else pkg.Comm.from_torch(dev.index)
 
     def em_step():
-        if world > 1:
-            mix.estep_stats(shard, stats)
-            dist.all_reduce(stats)                 # RCCL sum of sufficient statistics
-            mix.mstep(stats, N)
+        if comm is not None:
+            mix.optimize_sharded(comm, shard)      # stats -> RCCL all-reduce -> M-step (sdmm_em_step_sharded)
         else:
             mix.optimize(shard)
 
@@ -394,7 +407,7 @@ def main():
         # ---- batched per-leaf EM: the plugin's tree leaves,
         # each its own K=16 mixture over its own samples (volpath_sdmm.cpp:287-311);
         # leaves shard across ranks with no exchange (weak scaling per rank) ----
-        out["leaf_em"] = leaf_em_bench(pkg, synth, batch, n_local, shard, dev, stream, args, timed, world)
+        out["leaf_em"] = leaf_em_bench(pkg, synth, full, N, dev, stream, args, timed, world, rank, comm)
         # ---- spatial tree (jmm SNTree restatement; the plugin's split_to_depth(3)
         # and split(16000), volpath_sdmm.cpp:358, :161): device find over the
         # batch positions (STree.find, sdmm_proc.cpp:351) and the leaf routing ----
@@ -420,7 +433,7 @@ def main():
                                                  timed, args, world)
 
     if not args.no_extra and not args.no_large_k:
-        out["large_k"] = large_k_bench(pkg, synth, batch, shard, dev, stream, timed, args, world, N)
+        out["large_k"] = large_k_bench(pkg, synth, batch, shard, dev, stream, timed, args, world, N, comm)
 
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
@@ -431,6 +444,8 @@ def main():
 
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

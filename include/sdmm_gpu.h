@@ -142,6 +142,12 @@ int sdmm_em_step_host(sdmm_mix* m, const sdmm_samples* host_samples, int iterati
  * bitwise those of sdmm_em_step(mixes[i], leaf i) called one by one. */
 int sdmm_em_step_batched(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* device_samples,
                          const int64_t* seg, int iterations);
+/* Per-leaf iteration counts (the built plugin's optimize(): 2 EM iterations
+ * for a leaf while its em.iterations_run < 4, else 1, volpath_sdmm.cpp:299-305):
+ * round t steps every leaf with iterations[i] > t; bitwise the same as
+ * sdmm_em_step(mixes[i], leaf i, iterations[i]) one by one. */
+int sdmm_em_step_batched_iters(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* device_samples,
+                               const int64_t* seg, const int* iterations);
 /* Same with host-resident planes (staged through mixes[0]'s buffers; returns
  * after the batch, so the host planes may be reused). */
 int sdmm_em_step_batched_host(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* host_samples,
@@ -157,6 +163,50 @@ int sdmm_em_step_batched_host(sdmm_mix* const* mixes, int n_mix, const sdmm_samp
 size_t sdmm_stats_len(int K);
 int sdmm_estep_stats(sdmm_mix* m, const sdmm_samples* device_samples, double* stats);
 int sdmm_mstep(sdmm_mix* m, const double* stats, int64_t n_total);
+
+/* Multi-GPU.  One process per GPU; a communicator joins the ranks
+ * that train the same mixtures.  Transports:
+ *   RCCL   sdmm_comm_unique_id on one rank, the 128 bytes shared by the caller
+ *          (MPI, a file, torch.distributed), then sdmm_comm_init_rccl on every
+ *          rank (collectives on the mixtures' HIP streams, over xGMI);
+ *   host   sdmm_comm_init_host with the caller's own collective on HOST buffers
+ *          (allreduce: in-place SUM of count doubles; broadcast: in-place from
+ *          rank root); the library stages through pinned memory.  Callbacks
+ *          return 0 on success.
+ * Every rank must make the same sequence of sharded calls.
+ *   sdmm_em_step_sharded   sample-sharded StepwiseTangentEM::optimize
+ *                          (stepwise_tangent.h:597-1053): this rank's shard's
+ *                          statistics, ONE all-reduce (sum) of [H, wsum, W, M,
+ *                          Clow, n] fp64, then the same M-step on every rank
+ *                          (identical parameters everywhere, no broadcast).
+ *                          The reference's own sharded-statistics pattern is the
+ *                          legacy jmm/opt/stepwise.h:248-396 (threads + mutex).
+ *   sdmm_em_step_batched_sharded  the per-leaf EM with every rank holding
+ *                          samples of every leaf: the batched statistics of all
+ *                          leaves (+ counts) in ONE all-reduce per iteration
+ *                          round, then the batched M-step on every rank.
+ *   sdmm_mix_broadcast     leaf-sharded EM: after each rank stepped the leaves it
+ *                          owns (owner[i] == rank, e.g. sdmm_em_step_batched on
+ *                          that subset), every leaf's parameters and stepwise
+ *                          state are broadcast from its owner (RCCL: one fused
+ *                          group), so all ranks hold all leaves for guiding. */
+typedef struct sdmm_comm sdmm_comm;
+#define SDMM_COMM_ID_BYTES 128
+typedef int (*sdmm_host_allreduce_f64)(double* buf, size_t count, void* user);
+typedef int (*sdmm_host_broadcast)(void* buf, size_t bytes, int root, void* user);
+int sdmm_comm_unique_id(void* id /* SDMM_COMM_ID_BYTES */);
+int sdmm_comm_init_rccl(const void* id, int nranks, int rank, int device, sdmm_comm** out);
+int sdmm_comm_init_host(int nranks, int rank, int device, sdmm_host_allreduce_f64 allreduce,
+                        sdmm_host_broadcast broadcast, void* user, sdmm_comm** out);
+void sdmm_comm_destroy(sdmm_comm* c);
+int sdmm_comm_rank(const sdmm_comm* c);
+int sdmm_comm_size(const sdmm_comm* c);
+/* in-place SUM of count device doubles over the ranks, on hip_stream */
+int sdmm_comm_allreduce_f64(sdmm_comm* c, double* buf, size_t count, void* hip_stream);
+int sdmm_em_step_sharded(sdmm_mix* m, sdmm_comm* c, const sdmm_samples* device_shard, int iterations);
+int sdmm_em_step_batched_sharded(sdmm_mix* const* mixes, int n_mix, sdmm_comm* c, const sdmm_samples* device_samples,
+                                 const int64_t* seg, const int* iterations);
+int sdmm_mix_broadcast(sdmm_mix* const* mixes, int n_mix, const int32_t* owner, sdmm_comm* c);
 
 /* Posterior (responsibility) of every sample: resp[n*K + k], device, fp32. */
 int sdmm_responsibilities(sdmm_mix* m, const sdmm_samples* device_samples, float* resp);

@@ -41,6 +41,11 @@ def build(arch: str = "gfx950", jobs: int = 4) -> Path:
     return LIB_PATH
 
 
+# host-transport callbacks of sdmm_comm_init_host (include/sdmm_gpu.h)
+_HOST_ALLREDUCE = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_size_t, C.c_void_p)
+_HOST_BCAST = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p)
+
+
 class _Samples(C.Structure):
     _fields_ = [("x", C.c_void_p * 6), ("w", C.c_void_p), ("hpdf", C.c_void_p),
                 ("is_diffuse", C.c_void_p), ("n", C.c_int64)]
@@ -129,6 +134,19 @@ def lib():
         L.sdmm_get_em_params.argtypes = [C.c_void_p, C.c_void_p]
         L.sdmm_restore_params.argtypes = [C.c_void_p, C.c_void_p]
         L.sdmm_stree_set_nodes.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.sdmm_comm_unique_id.argtypes = [C.c_void_p]
+        L.sdmm_comm_init_rccl.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+        L.sdmm_comm_init_host.argtypes = [C.c_int, C.c_int, C.c_int, _HOST_ALLREDUCE, _HOST_BCAST, C.c_void_p,
+                                          C.POINTER(C.c_void_p)]
+        L.sdmm_comm_destroy.argtypes = [C.c_void_p]
+        L.sdmm_comm_rank.argtypes = [C.c_void_p]
+        L.sdmm_comm_size.argtypes = [C.c_void_p]
+        L.sdmm_comm_allreduce_f64.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.sdmm_em_step_sharded.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.sdmm_em_step_batched_sharded.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                   C.c_void_p]
+        L.sdmm_em_step_batched_iters.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.sdmm_mix_broadcast.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -159,6 +177,9 @@ EXPORTED_SYMBOLS = [
     "sdmm_stree_bind_mixtures", "sdmm_guide_product_batch", "sdmm_pdf_product_batch",
     "sdmm_save_json", "sdmm_load_json", "sdmm_mix_save_json", "sdmm_mix_load_json", "sdmm_get_em_params",
     "sdmm_restore_params", "sdmm_stree_set_nodes",
+    "sdmm_comm_unique_id", "sdmm_comm_init_rccl", "sdmm_comm_init_host", "sdmm_comm_destroy", "sdmm_comm_rank",
+    "sdmm_comm_size", "sdmm_comm_allreduce_f64", "sdmm_em_step_sharded", "sdmm_em_step_batched_sharded",
+    "sdmm_em_step_batched_iters", "sdmm_mix_broadcast",
 ]
 
 
@@ -174,6 +195,143 @@ def em_step_batched(mixes, samples, seg, iterations: int = 1):
     hs = (C.c_void_p * max(n, 1))(*[m.h for m in mixes])
     _check(lib().sdmm_em_step_batched(hs, n, samples.ptr, seg.ctypes.data_as(C.POINTER(C.c_int64)),
                                       iterations))
+
+
+def _iters(n, iterations):
+    it = np.full(n, iterations, np.int32) if np.isscalar(iterations) else np.ascontiguousarray(iterations, np.int32)
+    assert it.shape == (n,), "one iteration count per mixture"
+    return it
+
+
+def em_step_batched_iters(mixes, samples, seg, iterations):
+    """Batched per-leaf EM with per-leaf iteration counts (the plugin's 2 while
+    em.iterations_run < 4, else 1; volpath_sdmm.cpp:299-305)."""
+    seg = np.ascontiguousarray(seg, np.int64)
+    n = len(mixes)
+    it = _iters(n, iterations)
+    hs = (C.c_void_p * max(n, 1))(*[m.h for m in mixes])
+    _check(lib().sdmm_em_step_batched_iters(hs, n, samples.ptr, seg.ctypes.data, it.ctypes.data))
+
+
+def em_step_batched_sharded(mixes, comm, samples, seg, iterations=1):
+    """Per-leaf EM sample-sharded over the ranks of `comm`: this rank's samples
+    of every leaf; one all-reduce of all leaves' statistics per round."""
+    seg = np.ascontiguousarray(seg, np.int64)
+    n = len(mixes)
+    it = _iters(n, iterations)
+    hs = (C.c_void_p * max(n, 1))(*[m.h for m in mixes])
+    _check(lib().sdmm_em_step_batched_sharded(hs, n, comm.h, samples.ptr, seg.ctypes.data, it.ctypes.data))
+
+
+def mix_broadcast(mixes, owner, comm):
+    """Leaf-sharded EM: every mixture's parameters and EM state from its owner rank."""
+    n = len(mixes)
+    own = np.ascontiguousarray(owner, np.int32)
+    assert own.shape == (n,)
+    hs = (C.c_void_p * max(n, 1))(*[m.h for m in mixes])
+    _check(lib().sdmm_mix_broadcast(hs, n, own.ctypes.data, comm.h))
+
+
+class Comm:
+    """A multi-GPU communicator (sdmm_comm).  Comm.rccl: RCCL over xGMI, one
+    rank per GPU; Comm.host: the caller's own collective on host buffers (any
+    backend -- e.g. torch.distributed gloo via Comm.from_torch_gloo)."""
+
+    ID_BYTES = 128
+
+    def __init__(self, h, keep=()):
+        self.h = h
+        self._keep = keep          # the host callbacks must outlive the communicator
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(Comm.ID_BYTES)
+        _check(lib().sdmm_comm_unique_id(buf))
+        return buf.raw
+
+    @classmethod
+    def rccl(cls, uid: bytes, nranks: int, rank: int, device: int = 0) -> "Comm":
+        assert len(uid) == Comm.ID_BYTES
+        h = C.c_void_p()
+        _check(lib().sdmm_comm_init_rccl(C.create_string_buffer(uid, Comm.ID_BYTES), nranks, rank, device,
+                                         C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def from_torch(cls, device: int = 0, group=None) -> "Comm":
+        """RCCL communicator over the ranks of a torch.distributed group (the
+        unique id travels through it)."""
+        import torch
+        import torch.distributed as dist
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        uid = Comm.unique_id() if rank == 0 else bytes(Comm.ID_BYTES)
+        t = torch.tensor(list(uid), dtype=torch.uint8)
+        if dist.get_backend(group) == "nccl":
+            t = t.to(torch.device("cuda", device))
+        dist.broadcast(t, 0, group=group)
+        return cls.rccl(bytes(t.cpu().tolist()), world, rank, device)
+
+    @classmethod
+    def host(cls, nranks: int, rank: int, allreduce, broadcast, device: int = 0) -> "Comm":
+        """allreduce(np.ndarray float64) and broadcast(np.ndarray uint8, root)
+        operate in place on host arrays."""
+        def ar(ptr, count, _):
+            try:
+                allreduce(np.ctypeslib.as_array(ptr, shape=(count,)))
+                return 0
+            except Exception:
+                return 1
+
+        def bc(ptr, nbytes, root, _):
+            try:
+                broadcast(np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), shape=(nbytes,)), root)
+                return 0
+            except Exception:
+                return 1
+        fa, fb = _HOST_ALLREDUCE(ar), _HOST_BCAST(bc)
+        h = C.c_void_p()
+        _check(lib().sdmm_comm_init_host(nranks, rank, device, fa, fb, None, C.byref(h)))
+        return cls(h, keep=(fa, fb))
+
+    @classmethod
+    def from_torch_gloo(cls, device: int = 0, group=None) -> "Comm":
+        """Host transport over a torch.distributed CPU (gloo) group."""
+        import torch
+        import torch.distributed as dist
+
+        def allreduce(a):
+            dist.all_reduce(torch.from_numpy(a), group=group)
+
+        def broadcast(a, root):
+            dist.broadcast(torch.from_numpy(a), root, group=group)
+        return cls.host(dist.get_world_size(group), dist.get_rank(group), allreduce, broadcast, device)
+
+    @property
+    def rank(self) -> int:
+        return int(lib().sdmm_comm_rank(self.h))
+
+    @property
+    def size(self) -> int:
+        return int(lib().sdmm_comm_size(self.h))
+
+    def allreduce_f64(self, t, stream=None):
+        """In-place SUM over ranks of a float64 device tensor."""
+        import torch
+        assert t.dtype == torch.float64 and t.is_cuda
+        st = stream if stream is not None else torch.cuda.current_stream(t.device)
+        _check(lib().sdmm_comm_allreduce_f64(self.h, t.data_ptr(), t.numel(),
+                                             C.c_void_p(getattr(st, "cuda_stream", st) or 0)))
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().sdmm_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
@@ -407,6 +565,11 @@ class SDMM:
         _check(lib().sdmm_em_step(self.h, samples.ptr, iterations))
 
     em_step = optimize
+
+    def optimize_sharded(self, comm: "Comm", shard: DeviceSamples, iterations: int = 1):
+        """Sample-sharded EM step(s): this rank's shard, statistics summed over
+        the ranks of `comm` (sdmm_em_step_sharded)."""
+        _check(lib().sdmm_em_step_sharded(self.h, comm.h, shard.ptr, iterations))
 
     def estep_stats(self, samples: DeviceSamples, stats):
         """Shard statistics into `stats` (fp64 device tensor of stats_len(K))."""

@@ -260,6 +260,7 @@ __device__ __forceinline__ void mstep_body(int K, int Kp, const double* __restri
     extern __shared__ double newW[];
     int* setk = (int*)(newW + K);
     const int t = threadIdx.x;
+    if (nSamples < 0) nSamples = (int64_t)stats[2 + ST_FIELDS * K];   // sharded: the all-reduced count
     if (t == 0) {
         const double weightSum = stats[1];
         sh[0] = (weightSum == 0.0) ? 0.0 : 1.0;
@@ -418,11 +419,19 @@ mstep_kernel(int K, int Kp, const double* __restrict__ stats, int64_t nSamples, 
 __global__ void __launch_bounds__(512)
 mstep_batched_kernel(int K, int Kp, const MixDesc* __restrict__ mixes, float norm5) {
     const MixDesc& d = mixes[blockIdx.x];
-    if (d.n <= 0) return;   // no samples: optimize() returns early (weightSum == 0)
-    mstep_body(K, Kp, d.stats, d.n, d.C, d.S, d.ep, d.gp, norm5, d.wmean, d.wcov);
+    const int64_t n = d.ncount ? (int64_t)*d.ncount : d.n;
+    if (n <= 0) return;   // no samples: optimize() returns early (weightSum == 0)
+    mstep_body(K, Kp, d.stats, n, d.C, d.S, d.ep, d.gp, norm5, d.wmean, d.wcov);
 }
 
+__global__ void set_f64_kernel(double* p, double v) { *p = v; }
+
 // ---------------------------------------------------------------------------
+hipError_t launch_set_f64(double* p, double v, hipStream_t st) {
+    hipLaunchKernelGGL(set_f64_kernel, dim3(1), dim3(1), 0, st, p, v);
+    return hipGetLastError();
+}
+
 hipError_t launch_set_all(int K, int Kp, const double* mean, const double* cov, const CanonDev& C,
                           float* ep, float* gp, float norm5, hipStream_t st) {
     const int threads = Kp < 64 ? 64 : (Kp > 512 ? 512 : Kp);

@@ -5,6 +5,7 @@
 // The reference counterpart is the per-leaf SDMMContext of the sdmm plugin
 // (sdmm_proc.h:92-93) driving sdmm-lib's em_step / create_conditional.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <cmath>
 #include <cstdlib>
@@ -30,6 +31,7 @@ hipError_t launch_estep_stats(int cpl, int lps, const float* ep, int Kp, int K, 
 hipError_t launch_reduce_finalize_batched(const float* partials, int pstride, int Kp, int K,
                                           const LeafDesc* leaves, int n_leaves, hipStream_t st);
 hipError_t launch_mstep_batched(int K, int Kp, const MixDesc* mixes, int n_mix, float norm5, hipStream_t st);
+hipError_t launch_set_f64(double* p, double v, hipStream_t st);
 hipError_t estep_occupancy(int cpl, int lps, int Kp, int* resp_blocks, int* stats_blocks);
 hipError_t launch_estep_resp_tile(int variant, const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
                                   int64_t chunk, float* resp, hipStream_t st);
@@ -261,7 +263,82 @@ struct sdmm_mix {
     size_t batch_bytes = 0;
     hipEvent_t batch_copied = nullptr;   // the last table upload has completed
     hipEvent_t batch_done = nullptr;     // the last batch's kernels have completed
+    // sample-sharded batched EM: the leaves' stats + counts, all-reduced as one buffer
+    double* shard_stats = nullptr;
+    size_t shard_bytes = 0;
 };
+
+// ==========================================================================
+// Multi-GPU transport (include/sdmm_gpu.h, sdmm_comm_*).  The reference has no
+// collective; the library's exchange steps are (a) the SUM of
+// the fp64 sufficient statistics before each M-step of a sample-sharded EM and
+// (b) broadcasts of leaf mixtures from their owner rank (leaf-sharded EM).
+// Transports: RCCL (one rank per GPU, over xGMI) or host callbacks (the caller's
+// own collective on host buffers -- MPI, gloo -- staged through pinned memory).
+struct sdmm_comm {
+    int rank = 0, nranks = 1, device = 0;
+    ncclComm_t nccl = nullptr;
+    sdmm_host_allreduce_f64 h_allreduce = nullptr;
+    sdmm_host_broadcast h_broadcast = nullptr;
+    void* user = nullptr;
+    void* pinned = nullptr;   // host transport staging
+    size_t pinned_bytes = 0;
+};
+
+namespace {
+
+int nccl_fail(ncclResult_t r, const char* what) {
+    return fail(SDMM_E_HIP, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+int comm_pinned(sdmm_comm* c, size_t bytes) {
+    if (bytes <= c->pinned_bytes) return SDMM_OK;
+    if (c->pinned) HIP_TRY(hipHostFree(c->pinned));
+    c->pinned = nullptr;
+    c->pinned_bytes = 0;
+    HIP_TRY(hipHostMalloc(&c->pinned, bytes, hipHostMallocDefault));
+    c->pinned_bytes = bytes;
+    return SDMM_OK;
+}
+
+// SUM over ranks of count doubles in device memory, in place, ordered on st.
+int comm_allreduce(sdmm_comm* c, double* dbuf, size_t count, hipStream_t st) {
+    if (c->nranks == 1 && !c->nccl) return SDMM_OK;
+    if (c->nccl) {
+        const ncclResult_t r = ncclAllReduce(dbuf, dbuf, count, ncclFloat64, ncclSum, c->nccl, st);
+        return r == ncclSuccess ? SDMM_OK : nccl_fail(r, "ncclAllReduce");
+    }
+    int r = comm_pinned(c, sizeof(double) * count);
+    if (r) return r;
+    HIP_TRY(hipMemcpyAsync(c->pinned, dbuf, sizeof(double) * count, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (c->h_allreduce((double*)c->pinned, count, c->user) != 0)
+        return fail(SDMM_E_STATE, "host all-reduce callback failed");
+    HIP_TRY(hipMemcpyAsync(dbuf, c->pinned, sizeof(double) * count, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return SDMM_OK;
+}
+
+// bytes of device memory broadcast from rank root, in place, ordered on st
+// (RCCL: call between ncclGroupStart/End to fuse several).
+int comm_broadcast(sdmm_comm* c, void* dbuf, size_t bytes, int root, hipStream_t st) {
+    if (c->nranks == 1 && !c->nccl) return SDMM_OK;
+    if (c->nccl) {
+        const ncclResult_t r = ncclBroadcast(dbuf, dbuf, bytes, ncclUint8, root, c->nccl, st);
+        return r == ncclSuccess ? SDMM_OK : nccl_fail(r, "ncclBroadcast");
+    }
+    int r = comm_pinned(c, bytes);
+    if (r) return r;
+    HIP_TRY(hipMemcpyAsync(c->pinned, dbuf, bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (c->h_broadcast(c->pinned, bytes, root, c->user) != 0)
+        return fail(SDMM_E_STATE, "host broadcast callback failed");
+    HIP_TRY(hipMemcpyAsync(dbuf, c->pinned, bytes, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return SDMM_OK;
+}
+
+}  // namespace
 
 namespace {
 
@@ -500,7 +577,7 @@ int sdmm_create(int K, const sdmm_em_params* params, int device, sdmm_mix** out)
     add(&sc, 8 * SC_COUNT); add(&T, 8 * Kc); add(&sgW, 8 * Kc); add(&sgM, 40 * Kc); add(&sgC, 200 * Kc);
     add(&bp, 100 * Kc); add(&bd, 36 * Kc);
     add(&m->ep, 4 * (size_t)EP_FIELDS * m->Kp); add(&m->gp, 4 * (size_t)GP_STRIDE * m->Kp);
-    add(&m->stats, 8 * sdmm_stats_len(K));
+    add(&m->stats, 8 * (sdmm_stats_len(K) + 1));   // + the sample count of a sharded step
     add(&m->rscratch, 8 * 16 * sdmm_stats_len(K));
     add(&m->tmp_mean, 48 * Kc); add(&m->tmp_cov, 200 * Kc);
     (void)f_canon;
@@ -553,6 +630,7 @@ void sdmm_destroy(sdmm_mix* m) {
     if (m->staging) (void)hipFree(m->staging);
     if (m->batch_dev) (void)hipFree(m->batch_dev);
     if (m->batch_host) (void)hipHostFree(m->batch_host);
+    if (m->shard_stats) (void)hipFree(m->shard_stats);
     if (m->batch_copied) (void)hipEventDestroy(m->batch_copied);
     if (m->batch_done) (void)hipEventDestroy(m->batch_done);
     if (m->own_stream) (void)hipStreamDestroy(m->own_stream);
@@ -691,6 +769,130 @@ int sdmm_mstep(sdmm_mix* m, const double* stats, int64_t n_total) {
     return SDMM_OK;
 }
 
+// ---- multi-GPU -------------------------------------------------------------
+int sdmm_comm_unique_id(void* id) {
+    if (!id) return fail(SDMM_E_INVALID, "id is NULL");
+    ncclUniqueId u;
+    const ncclResult_t r = ncclGetUniqueId(&u);
+    if (r != ncclSuccess) return nccl_fail(r, "ncclGetUniqueId");
+    std::memcpy(id, &u, sizeof(u));
+    return SDMM_OK;
+}
+
+int sdmm_comm_init_rccl(const void* id, int nranks, int rank, int device, sdmm_comm** out) {
+    if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(SDMM_E_INVALID, "invalid argument");
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(device));
+    sdmm_comm* c = new (std::nothrow) sdmm_comm();
+    if (!c) return fail(SDMM_E_NOMEM, "out of host memory");
+    c->rank = rank;
+    c->nranks = nranks;
+    c->device = device;
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    const ncclResult_t r = ncclCommInitRank(&c->nccl, nranks, u, rank);
+    if (r != ncclSuccess) {
+        delete c;
+        return nccl_fail(r, "ncclCommInitRank");
+    }
+    *out = c;
+    return SDMM_OK;
+}
+
+int sdmm_comm_init_host(int nranks, int rank, int device, sdmm_host_allreduce_f64 allreduce,
+                        sdmm_host_broadcast broadcast, void* user, sdmm_comm** out) {
+    if (!out || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && (!allreduce || !broadcast)))
+        return fail(SDMM_E_INVALID, "invalid argument");
+    sdmm_comm* c = new (std::nothrow) sdmm_comm();
+    if (!c) return fail(SDMM_E_NOMEM, "out of host memory");
+    c->rank = rank;
+    c->nranks = nranks;
+    c->device = device;
+    c->h_allreduce = allreduce;
+    c->h_broadcast = broadcast;
+    c->user = user;
+    *out = c;
+    return SDMM_OK;
+}
+
+void sdmm_comm_destroy(sdmm_comm* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->nccl) (void)ncclCommDestroy(c->nccl);
+    if (c->pinned) (void)hipHostFree(c->pinned);
+    delete c;
+}
+
+int sdmm_comm_rank(const sdmm_comm* c) { return c ? c->rank : -1; }
+int sdmm_comm_size(const sdmm_comm* c) { return c ? c->nranks : 0; }
+
+int sdmm_comm_allreduce_f64(sdmm_comm* c, double* buf, size_t count, void* hip_stream) {
+    if (!c || (count > 0 && !buf)) return fail(SDMM_E_INVALID, "invalid argument");
+    if (count == 0) return SDMM_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    return comm_allreduce(c, buf, count, (hipStream_t)hip_stream);
+}
+
+int sdmm_em_step_sharded(sdmm_mix* m, sdmm_comm* c, const sdmm_samples* shard, int iterations) {
+    if (!m || !c) return fail(SDMM_E_INVALID, "invalid argument");
+    if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
+    if (c->device != m->device) return fail(SDMM_E_INVALID, "communicator on another device");
+    int r = check_samples(shard);
+    if (r) return r;
+    HIP_TRY(hipSetDevice(m->device));
+    const size_t len = sdmm_stats_len(m->K);
+    for (int it = 0; it < iterations; ++it) {
+        // this shard's statistics (zero for an empty shard) and its sample count
+        if (shard->n == 0) {
+            HIP_TRY(hipMemsetAsync(m->stats, 0, 8 * len, m->stream));
+        } else if ((r = run_estep_stats(m, shard, m->stats))) {
+            return r;
+        }
+        HIP_TRY(launch_set_f64(m->stats + len, (double)shard->n, m->stream));
+        // SUM over ranks, then the same M-step everywhere (n from the summed count)
+        if ((r = comm_allreduce(c, m->stats, len + 1, m->stream))) return r;
+        HIP_TRY(launch_mstep(m->K, m->Kp, m->stats, -1, m->C, m->S, m->ep, m->gp, m->norm5, m->tmp_mean,
+                             m->tmp_cov, m->stream));
+    }
+    return SDMM_OK;
+}
+
+int sdmm_mix_broadcast(sdmm_mix* const* mixes, int n_mix, const int32_t* owner, sdmm_comm* c) {
+    if (n_mix < 0 || !c || (n_mix > 0 && (!mixes || !owner))) return fail(SDMM_E_INVALID, "invalid argument");
+    if (n_mix == 0) return SDMM_OK;
+    for (int i = 0; i < n_mix; ++i) {
+        if (!mixes[i]) return fail(SDMM_E_INVALID, "NULL handle in mixes");
+        if (owner[i] < 0 || owner[i] >= c->nranks) return fail(SDMM_E_INVALID, "owner rank out of range");
+        if (mixes[i]->device != c->device) return fail(SDMM_E_INVALID, "mixture on another device");
+        if (mixes[i]->K != mixes[0]->K) return fail(SDMM_E_INVALID, "mixtures must share K");
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    const hipStream_t st = mixes[0]->stream;
+    for (int i = 1; i < n_mix; ++i)
+        if (mixes[i]->stream != st) HIP_TRY(hipStreamSynchronize(mixes[i]->stream));
+    // a mixture's parameters, derived arrays, packed records and stepwise state
+    // are one contiguous prefix of its device block (everything before the stats)
+    const size_t bytes = (size_t)((char*)mixes[0]->stats - (char*)mixes[0]->block);
+    if (c->nccl) {
+        ncclResult_t g = ncclGroupStart();
+        if (g != ncclSuccess) return nccl_fail(g, "ncclGroupStart");
+        for (int i = 0; i < n_mix; ++i) {
+            const int r = comm_broadcast(c, mixes[i]->block, bytes, owner[i], st);
+            if (r) { (void)ncclGroupEnd(); return r; }
+        }
+        g = ncclGroupEnd();
+        if (g != ncclSuccess) return nccl_fail(g, "ncclGroupEnd");
+    } else {
+        for (int i = 0; i < n_mix; ++i) {
+            const int r = comm_broadcast(c, mixes[i]->block, bytes, owner[i], st);
+            if (r) return r;
+        }
+    }
+    for (int i = 0; i < n_mix; ++i) mixes[i]->initialised = true;
+    HIP_TRY(hipStreamSynchronize(st));
+    return SDMM_OK;
+}
+
 int sdmm_em_step(sdmm_mix* m, const sdmm_samples* s, int iterations) {
     if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
     if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
@@ -706,47 +908,129 @@ int sdmm_em_step(sdmm_mix* m, const sdmm_samples* s, int iterations) {
     return SDMM_OK;
 }
 
-int sdmm_em_step_batched(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* s, const int64_t* seg,
-                         int iterations) {
-    if (n_mix < 0 || (n_mix > 0 && (!mixes || !seg))) return fail(SDMM_E_INVALID, "invalid argument");
-    if (n_mix == 0) return SDMM_OK;
-    int r = check_samples(s);
-    if (r) return r;
-    sdmm_mix* m0 = mixes[0];
-    if (!m0) return fail(SDMM_E_INVALID, "mixes[0] is NULL");
-    if (seg[0] < 0 || seg[n_mix] > s->n) return fail(SDMM_E_INVALID, "segment offsets outside the sample batch");
+}  // extern "C"
+
+namespace {
+
+// Validation shared by the batched entry points: handles present, initialised,
+// distinct, one K and one device; offsets/counts inside the batch.
+int check_batch(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* s, const int64_t* s0, const int64_t* cnt) {
     std::vector<const sdmm_mix*> seen;
     seen.reserve((size_t)n_mix);
+    const sdmm_mix* m0 = mixes[0];
     for (int i = 0; i < n_mix; ++i) {
         const sdmm_mix* m = mixes[i];
         if (!m) return fail(SDMM_E_INVALID, "NULL handle in mixes");
         if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
         if (m->K != m0->K || m->device != m0->device)
             return fail(SDMM_E_INVALID, "batched mixtures must share K and the device");
-        if (seg[i + 1] < seg[i]) return fail(SDMM_E_INVALID, "segment offsets must be non-decreasing");
+        if (cnt[i] < 0 || s0[i] < 0 || s0[i] + cnt[i] > s->n)
+            return fail(SDMM_E_INVALID, "segment offsets outside the sample batch");
         seen.push_back(m);
     }
     std::sort(seen.begin(), seen.end());
     if (std::adjacent_find(seen.begin(), seen.end()) != seen.end())
         return fail(SDMM_E_INVALID, "a handle appears twice in mixes");
-    if (iterations <= 0 || seg[n_mix] == seg[0]) return SDMM_OK;
+    return SDMM_OK;
+}
+
+// ONE stepwise EM iteration of every listed leaf: mixes[i] over samples
+// [s0[i], s0[i] + cnt[i]) of the device planes s, on mixes[0]'s stream.
+// comm == nullptr: a leaf with no samples is left unchanged.  comm != null
+// (sample-sharded over ranks): each rank's statistics of every leaf -- and the
+// leaves' sample counts -- go to one contiguous fp64 buffer, ONE all-reduce
+// sums them, and every rank runs the same M-steps on the global statistics.
+int batched_iteration(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* s, const int64_t* s0,
+                      const int64_t* cnt, sdmm_comm* comm);
+
+}  // namespace
+
+extern "C" {
+
+int sdmm_em_step_batched(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* s, const int64_t* seg,
+                         int iterations) {
+    if (n_mix < 0 || (n_mix > 0 && (!mixes || !seg))) return fail(SDMM_E_INVALID, "invalid argument");
+    if (n_mix == 0) return SDMM_OK;
+    std::vector<int> it((size_t)n_mix, iterations > 0 ? iterations : 0);
+    return sdmm_em_step_batched_iters(mixes, n_mix, s, seg, it.data());
+}
+
+int sdmm_em_step_batched_iters(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* s, const int64_t* seg,
+                               const int* iterations) {
+    return sdmm_em_step_batched_sharded(mixes, n_mix, nullptr, s, seg, iterations);
+}
+
+int sdmm_em_step_batched_sharded(sdmm_mix* const* mixes, int n_mix, sdmm_comm* comm, const sdmm_samples* s,
+                                 const int64_t* seg, const int* iterations) {
+    if (n_mix < 0 || (n_mix > 0 && (!mixes || !seg || !iterations))) return fail(SDMM_E_INVALID, "invalid argument");
+    if (n_mix == 0) return SDMM_OK;
+    int r = check_samples(s);
+    if (r) return r;
+    if (!mixes[0]) return fail(SDMM_E_INVALID, "mixes[0] is NULL");
+    for (int i = 0; i < n_mix; ++i)
+        if (seg[i + 1] < seg[i]) return fail(SDMM_E_INVALID, "segment offsets must be non-decreasing");
+    std::vector<int64_t> s0((size_t)n_mix), cnt((size_t)n_mix);
+    int max_it = 0;
+    for (int i = 0; i < n_mix; ++i) {
+        s0[(size_t)i] = seg[i];
+        cnt[(size_t)i] = seg[i + 1] - seg[i];
+        max_it = std::max(max_it, iterations[i]);
+    }
+    if ((r = check_batch(mixes, n_mix, s, s0.data(), cnt.data()))) return r;
+    if (comm && comm->device != mixes[0]->device) return fail(SDMM_E_INVALID, "communicator on another device");
+    // iteration t steps the leaves that asked for more than t iterations (the
+    // plugin: 2 while a leaf's em.iterations_run < 4, else 1, volpath_sdmm.cpp:299-305)
+    std::vector<sdmm_mix*> am;
+    std::vector<int64_t> as0, acnt;
+    for (int t = 0; t < max_it; ++t) {
+        am.clear(); as0.clear(); acnt.clear();
+        for (int i = 0; i < n_mix; ++i)
+            if (iterations[i] > t) {
+                am.push_back(mixes[i]);
+                as0.push_back(s0[(size_t)i]);
+                acnt.push_back(cnt[(size_t)i]);
+            }
+        if (am.empty()) break;
+        // leaves stepped in this round run on the first one's stream: make the
+        // caller's mixes[0] stream the one, so the ordering is the caller's
+        if (am[0] != mixes[0]) {
+            am.insert(am.begin(), mixes[0]);
+            as0.insert(as0.begin(), 0);
+            acnt.insert(acnt.begin(), -1);   // placeholder: not stepped (see below)
+        }
+        r = batched_iteration(am.data(), (int)am.size(), s, as0.data(), acnt.data(), comm);
+        if (r) return r;
+    }
+    return SDMM_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+int batched_iteration(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* s, const int64_t* s0,
+                      const int64_t* cnt, sdmm_comm* comm) {
+    sdmm_mix* m0 = mixes[0];
     HIP_TRY(hipSetDevice(m0->device));
     const hipStream_t st = m0->stream;
     for (int i = 1; i < n_mix; ++i)
         if (mixes[i]->stream != st) HIP_TRY(hipStreamSynchronize(mixes[i]->stream));
-
-    // tables: leaves, M-step operands, (leaf, block) work items
+    // a leaf with cnt < 0 only carries mixes[0]'s stream: no work, no M-step
     std::vector<StatsPlan> plans((size_t)n_mix);
-    int64_t rows = 0;
+    int64_t rows = 0, any = 0;
     for (int i = 0; i < n_mix; ++i) {
-        const int64_t n = seg[i + 1] - seg[i];
+        const int64_t n = cnt[i];
         plans[(size_t)i] = n > 0 ? stats_plan(mixes[i], n) : StatsPlan{0, 0};
         rows += plans[(size_t)i].blocks;
+        any += n > 0 ? n : 0;
     }
+    if (!comm && any == 0) return SDMM_OK;   // nothing to step
     if (rows > (int64_t)1 << 30) return fail(SDMM_E_INVALID, "batch too large");
+    const size_t len = sdmm_stats_len(m0->K);
     const size_t off_mix = ((sizeof(LeafDesc) * (size_t)n_mix + 255) / 256) * 256;
     const size_t off_items = off_mix + ((sizeof(MixDesc) * (size_t)n_mix + 255) / 256) * 256;
-    const size_t need = off_items + sizeof(int2) * (size_t)rows;
+    const size_t off_cnt = off_items + ((sizeof(int2) * (size_t)rows + 255) / 256) * 256;
+    const size_t need = off_cnt + sizeof(double) * (size_t)n_mix;
     if (!m0->batch_copied) {
         HIP_TRY(hipEventCreateWithFlags(&m0->batch_copied, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&m0->batch_done, hipEventDisableTiming));
@@ -763,19 +1047,39 @@ int sdmm_em_step_batched(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* 
         HIP_TRY(hipHostMalloc(&m0->batch_host, cap, hipHostMallocDefault));
         m0->batch_bytes = cap;
     }
-    r = ensure_partials(m0, (int)(rows > 0 ? rows : 1));
+    // sharded: the leaves' statistics + counts, contiguous (one all-reduce)
+    double* sh = nullptr;
+    if (comm) {
+        const size_t sbytes = sizeof(double) * (len + 1) * (size_t)n_mix;
+        if (sbytes > m0->shard_bytes) {
+            HIP_TRY(hipStreamSynchronize(st));
+            if (m0->shard_stats) HIP_TRY(hipFree(m0->shard_stats));
+            m0->shard_stats = nullptr;
+            m0->shard_bytes = 0;
+            HIP_TRY(hipMalloc((void**)&m0->shard_stats, sbytes));
+            m0->shard_bytes = sbytes;
+        }
+        sh = m0->shard_stats;
+        HIP_TRY(hipMemsetAsync(sh, 0, sizeof(double) * len * (size_t)n_mix, st));
+    }
+    int r = ensure_partials(m0, (int)(rows > 0 ? rows : 1));
     if (r) return r;
     char* hb = (char*)m0->batch_host;
     char* db = (char*)m0->batch_dev;
     LeafDesc* leaves = (LeafDesc*)hb;
     MixDesc* mixd = (MixDesc*)(hb + off_mix);
     int2* items = (int2*)(hb + off_items);
+    double* counts = (double*)(hb + off_cnt);
+    const double* dcounts = (const double*)(db + off_cnt);
     int row = 0;
     for (int i = 0; i < n_mix; ++i) {
         sdmm_mix* m = mixes[i];
-        const int64_t n = seg[i + 1] - seg[i];
-        leaves[i] = LeafDesc{m->ep, m->stats, seg[i], n, plans[(size_t)i].chunk, row, plans[(size_t)i].blocks};
-        mixd[i] = MixDesc{m->C, m->S, m->ep, m->gp, m->stats, m->tmp_mean, m->tmp_cov, n};
+        const int64_t n = cnt[i] > 0 ? cnt[i] : 0;
+        double* lstats = comm ? sh + len * (size_t)i : m->stats;
+        leaves[i] = LeafDesc{m->ep, lstats, s0[i], n, plans[(size_t)i].chunk, row, plans[(size_t)i].blocks};
+        mixd[i] = MixDesc{m->C, m->S, m->ep, m->gp, lstats, m->tmp_mean, m->tmp_cov, cnt[i] < 0 ? 0 : n,
+                          (comm && cnt[i] >= 0) ? sh + len * (size_t)n_mix + i : nullptr};
+        counts[i] = (double)n;
         for (int b = 0; b < plans[(size_t)i].blocks; ++b) items[row + b] = int2{i, b};
         row += plans[(size_t)i].blocks;
     }
@@ -785,17 +1089,25 @@ int sdmm_em_step_batched(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* 
     const MixDesc* dmix = (const MixDesc*)(db + off_mix);
     const int2* ditems = (const int2*)(db + off_items);
     const SamplesDev d = to_dev(s);
-    for (int it = 0; it < iterations; ++it) {
-        if (rows > 0)
-            HIP_TRY(launch_stats_kernel(m0, d, 0, StatsPlan{0, 0}, (int)rows, m0->partials, st, dleaves, ditems));
-        HIP_TRY(launch_reduce_finalize_batched(m0->partials, m0->pstride, m0->Kp, m0->K, dleaves, n_mix, st));
-        HIP_TRY(launch_mstep_batched(m0->K, m0->Kp, dmix, n_mix, m0->norm5, st));
+    if (rows > 0)
+        HIP_TRY(launch_stats_kernel(m0, d, 0, StatsPlan{0, 0}, (int)rows, m0->partials, st, dleaves, ditems));
+    HIP_TRY(launch_reduce_finalize_batched(m0->partials, m0->pstride, m0->Kp, m0->K, dleaves, n_mix, st));
+    if (comm) {
+        HIP_TRY(hipMemcpyAsync(sh + len * (size_t)n_mix, dcounts, sizeof(double) * (size_t)n_mix,
+                               hipMemcpyDeviceToDevice, st));
+        r = comm_allreduce(comm, sh, (len + 1) * (size_t)n_mix, st);
+        if (r) return r;
     }
+    HIP_TRY(launch_mstep_batched(m0->K, m0->Kp, dmix, n_mix, m0->norm5, st));
     HIP_TRY(hipEventRecord(m0->batch_done, st));
     for (int i = 1; i < n_mix; ++i)
         if (mixes[i]->stream != st) HIP_TRY(hipStreamWaitEvent(mixes[i]->stream, m0->batch_done, 0));
     return SDMM_OK;
 }
+
+}  // namespace
+
+extern "C" {
 
 // Stage host sample planes into m's staging buffer (device SoA view in *d).
 static int stage_host_samples(sdmm_mix* m, const sdmm_samples* s, sdmm_samples* d) {

@@ -137,6 +137,7 @@ struct MixDesc {
     double* wmean;
     double* wcov;
     int64_t n;
+    const double* ncount;   // non-null: the sample count is *ncount (all-reduced over ranks)
 };
 
 // scratch of the coherent (Morton) ordering of a guided batch

@@ -86,3 +86,16 @@ def test_cpp_mirror_header_compiles(tmp_path):
     exe = tmp_path / "m"
     subprocess.run(["g++", "-std=c++17", f"-I{ROOT / 'sdmm-mitsuba_amd' / 'host'}", f"-I{ROOT / 'include'}",
                     str(src), f"-L{lib}", "-lsdmm_amd", f"-Wl,-rpath,{lib}", "-o", str(exe)], check=True)
+
+
+def test_comm_host_transport_without_gpu(pkg):
+    """sdmm_comm_init_host validates its arguments and reports rank/size; the
+    host transport needs no device until a collective runs."""
+    lib = pkg.lib()
+    h = C.c_void_p()
+    assert lib.sdmm_comm_init_host(2, 0, 0, pkg._HOST_ALLREDUCE(), pkg._HOST_BCAST(), None, C.byref(h)) == -1
+    assert lib.sdmm_comm_init_host(1, 1, 0, pkg._HOST_ALLREDUCE(), pkg._HOST_BCAST(), None, C.byref(h)) == -1
+    comm = pkg.Comm.host(3, 2, lambda a: None, lambda a, root: None)
+    assert comm.rank == 2 and comm.size == 3
+    comm.close()
+    assert lib.sdmm_comm_rank(None) == -1 and lib.sdmm_comm_size(None) == 0

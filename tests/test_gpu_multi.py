@@ -1,0 +1,224 @@
+"""GPU: the library's native multi-GPU path (include/sdmm_gpu.h, sdmm_comm_*).
+
+  * RCCL, world size 1 (this pool's boxes have one GPU and RCCL refuses two
+    ranks on one device): sdmm_em_step_sharded / _batched_sharded /
+    sdmm_mix_broadcast through a real RCCL communicator are bitwise the
+    single-process calls.
+  * world size 2: two FRESH child processes (spawn) share the GPU, the library's
+    host transport carrying the collectives over torch.distributed gloo:
+      - sample-sharded EM (sdmm_estep_stats -> all-reduce -> sdmm_mstep inside
+        sdmm_em_step_sharded): ranks bitwise identical, equal to the
+        single-process EM within the split-phase bound of test_gpu_parity
+        (the fp64 statistics are summed in another order);
+      - per-leaf EM sample-sharded (sdmm_em_step_batched_sharded), with the
+        plugin's per-leaf iteration counts;
+      - leaf-sharded EM + sdmm_mix_broadcast: every rank ends with every leaf,
+        bitwise the single-process per-leaf EM.
+  * per-leaf iteration counts (sdmm_em_step_batched_iters) == per-leaf calls,
+    bitwise.
+"""
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+pytestmark = pytest.mark.gpu
+
+KEYS = ("weights", "mean", "cov", "cholLInv", "detInv", "cdf")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _leaves(synth, n_leaves=6, K=16, seed=11):
+    """Leaf batches of different sizes from the synthetic generator."""
+    rng = np.random.default_rng(seed)
+    sizes = rng.integers(300, 2500, size=n_leaves)
+    sizes[2] = 0                                     # an empty leaf
+    b = synth.em_batch(int(sizes.sum()) + 64, 128)
+    seg = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    return b, seg, K
+
+
+def _init_leaf(pkg, synth, b, seg, i, K):
+    a = int(seg[i])
+    m = pkg.SDMM(K)
+    m.init_hemisphere(b["x"][0:3, a:a + K // 8].T.copy(), b["normals"][a:a + K // 8].copy(), synth.DEPTH_PRIOR,
+                      synth.SPATIAL_DISTANCE, synth.SEED_MODEL + i)
+    return m
+
+
+def _params(m):
+    p = m.get_params()
+    st = m.get_state()
+    return {k: p[k] for k in KEYS} | {"sgC": st["sgC"], "it": st["scalars"][3]}
+
+
+def _mp_worker(rank, world, port, out_dir):
+    import importlib
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "tests"))
+    from conftest import load_pkg
+    pkg = load_pkg()
+    synth = importlib.import_module("sdmm_mitsuba_amd.synth")
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    comm = pkg.Comm.from_torch_gloo(device=0)
+    assert comm.rank == rank and comm.size == world
+    out = {}
+
+    # (1) sample-sharded EM of one mixture
+    K, N = 128, 16384
+    b = synth.em_batch(N, 128, heuristic=True)
+    pos, nrm = synth.model_seed_points(b, K)
+    ds = pkg.DeviceSamples.from_numpy(b["x"], b["w"], b["hpdf"], b["is_diffuse"])
+    mix = pkg.SDMM(K)
+    mix.init_hemisphere(pos, nrm, synth.DEPTH_PRIOR, synth.SPATIAL_DISTANCE, synth.SEED_MODEL)
+    for _ in range(3):
+        mix.optimize_sharded(comm, ds.shard(rank, world))
+    out.update({f"s_{k}": v for k, v in _params(mix).items()})
+
+    # (2) per-leaf EM, every rank holding half of every leaf's samples
+    lb, seg, Kl = _leaves(synth)
+    iters = np.array([2, 1, 2, 1, 2, 2], np.int32)
+    mixes = [_init_leaf(pkg, synth, lb, seg, i, Kl) for i in range(len(seg) - 1)]
+    idx = np.concatenate([np.arange(seg[i], seg[i + 1])[rank::world] for i in range(len(seg) - 1)])
+    lseg = np.concatenate([[0], np.cumsum([len(np.arange(seg[i], seg[i + 1])[rank::world])
+                                           for i in range(len(seg) - 1)])]).astype(np.int64)
+    lds = pkg.DeviceSamples.from_numpy(lb["x"][:, idx], lb["w"][idx], lb["hpdf"][idx], lb["is_diffuse"][idx])
+    pkg.em_step_batched_sharded(mixes, comm, lds, lseg, iters)
+    for i, m in enumerate(mixes):
+        out.update({f"b{i}_{k}": v for k, v in _params(m).items()})
+
+    # (3) leaf-sharded EM (each rank steps the leaves it owns on their full
+    # data) + the parameter broadcast from each leaf's owner
+    mixes = [_init_leaf(pkg, synth, lb, seg, i, Kl) for i in range(len(seg) - 1)]
+    owner = np.arange(len(mixes), dtype=np.int32) % world
+    full = pkg.DeviceSamples.from_numpy(lb["x"], lb["w"], lb["hpdf"], lb["is_diffuse"])
+    mine = [i for i in range(len(mixes)) if owner[i] == rank]
+    sub_x = np.concatenate([np.arange(seg[i], seg[i + 1]) for i in mine])
+    sub_seg = np.concatenate([[0], np.cumsum([seg[i + 1] - seg[i] for i in mine])]).astype(np.int64)
+    sub = pkg.DeviceSamples.from_numpy(lb["x"][:, sub_x], lb["w"][sub_x], lb["hpdf"][sub_x],
+                                       lb["is_diffuse"][sub_x])
+    pkg.em_step_batched_iters([mixes[i] for i in mine], sub, sub_seg, 2)
+    pkg.mix_broadcast(mixes, owner, comm)
+    for i, m in enumerate(mixes):
+        out.update({f"o{i}_{k}": v for k, v in _params(m).items()})
+
+    if rank == 0:
+        # single-process references
+        ref = pkg.SDMM(K)
+        ref.init_hemisphere(pos, nrm, synth.DEPTH_PRIOR, synth.SPATIAL_DISTANCE, synth.SEED_MODEL)
+        for _ in range(3):
+            ref.optimize(ds)
+        out.update({f"rs_{k}": v for k, v in _params(ref).items()})
+        refs = [_init_leaf(pkg, synth, lb, seg, i, Kl) for i in range(len(seg) - 1)]
+        pkg.em_step_batched_iters(refs, full, seg, iters)
+        for i, m in enumerate(refs):
+            out.update({f"rb{i}_{k}": v for k, v in _params(m).items()})
+        refs = [_init_leaf(pkg, synth, lb, seg, i, Kl) for i in range(len(seg) - 1)]
+        pkg.em_step_batched_iters(refs, full, seg, 2)
+        for i, m in enumerate(refs):
+            out.update({f"ro{i}_{k}": v for k, v in _params(m).items()})
+    torch.cuda.synchronize()
+    np.savez(Path(out_dir) / f"rank{rank}.npz", **out)
+    comm.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _close(a, b, plog, name):
+    from test_gpu_parity import _cov_close
+    ew = float(np.max(np.abs(a["weights"] - b["weights"]) / np.maximum(np.abs(b["weights"]), 1e-7)))
+    ec = _cov_close(a["cov"], b["cov"], 0)
+    plog(f"{name}_weights_rel", ew, 1e-5)
+    plog(f"{name}_cov_rel", ec, 1e-5)
+    assert ew <= 1e-5 and ec <= 1e-5
+
+
+def test_world2_host_transport(tmp_path, pkg, gpu, plog):
+    import torch.multiprocessing as mp
+    mp.spawn(_mp_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    r0 = dict(np.load(tmp_path / "rank0.npz"))
+    r1 = dict(np.load(tmp_path / "rank1.npz"))
+    for k, v in r1.items():                        # every replicated result: bitwise on both ranks
+        np.testing.assert_array_equal(r0[k], v, err_msg=k)
+    pick = lambda d, p: {k: d[f"{p}_{k}"] for k in ("weights", "cov")}
+    assert int(r0["s_it"]) == 3
+    _close(pick(r0, "s"), pick(r0, "rs"), plog, "sample_sharded_em")
+    n_leaves = 6
+    for i in range(n_leaves):
+        _close(pick(r0, f"b{i}"), pick(r0, f"rb{i}"), plog, f"batched_sharded_leaf{i}")
+        np.testing.assert_array_equal(r0[f"b{i}_it"], r0[f"rb{i}_it"])
+        for k in KEYS + ("sgC", "it"):             # leaf-sharded + broadcast: bitwise
+            np.testing.assert_array_equal(r0[f"o{i}_{k}"], r0[f"ro{i}_{k}"], err_msg=f"leaf {i} {k}")
+
+
+def test_rccl_world1_bitwise(pkg, synth, gpu):
+    """A real RCCL communicator (world size 1) through every sharded entry point."""
+    comm = pkg.Comm.rccl(pkg.Comm.unique_id(), 1, 0, 0)
+    K, N = 128, 8192
+    b = synth.em_batch(N, 128)
+    pos, nrm = synth.model_seed_points(b, K)
+    ds = pkg.DeviceSamples.from_numpy(b["x"], b["w"], b["hpdf"], b["is_diffuse"])
+    a, r = pkg.SDMM(K), pkg.SDMM(K)
+    for m in (a, r):
+        m.init_hemisphere(pos, nrm, synth.DEPTH_PRIOR, synth.SPATIAL_DISTANCE, synth.SEED_MODEL)
+    for _ in range(3):
+        a.optimize_sharded(comm, ds)
+        r.optimize(ds)
+    pa, pr = _params(a), _params(r)
+    for k in pa:
+        np.testing.assert_array_equal(pa[k], pr[k], err_msg=k)
+    lb, seg, Kl = _leaves(synth)
+    full = pkg.DeviceSamples.from_numpy(lb["x"], lb["w"], lb["hpdf"], lb["is_diffuse"])
+    iters = np.array([2, 1, 2, 1, 1, 2], np.int32)
+    xs = [_init_leaf(pkg, synth, lb, seg, i, Kl) for i in range(len(seg) - 1)]
+    ys = [_init_leaf(pkg, synth, lb, seg, i, Kl) for i in range(len(seg) - 1)]
+    pkg.em_step_batched_sharded(xs, comm, full, seg, iters)
+    pkg.em_step_batched_iters(ys, full, seg, iters)
+    pkg.mix_broadcast(xs, np.zeros(len(xs), np.int32), comm)
+    for x, y in zip(xs, ys):
+        px, py = _params(x), _params(y)
+        for k in px:
+            np.testing.assert_array_equal(px[k], py[k], err_msg=k)
+    # the exposed all-reduce
+    import torch
+    t = torch.arange(10, dtype=torch.float64, device=gpu)
+    comm.allreduce_f64(t)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(t.cpu().numpy(), np.arange(10.0))
+    comm.close()
+
+
+def test_batched_per_leaf_iterations_bitwise(pkg, synth, gpu):
+    """sdmm_em_step_batched_iters == sdmm_em_step(leaf i, iterations[i]) per leaf."""
+    lb, seg, Kl = _leaves(synth, n_leaves=9, seed=5)
+    full = pkg.DeviceSamples.from_numpy(lb["x"], lb["w"], lb["hpdf"], lb["is_diffuse"])
+    iters = np.array([2, 1, 0, 2, 1, 2, 3, 1, 2], np.int32)
+    xs = [_init_leaf(pkg, synth, lb, seg, i, Kl) for i in range(len(seg) - 1)]
+    ys = [_init_leaf(pkg, synth, lb, seg, i, Kl) for i in range(len(seg) - 1)]
+    for _ in range(2):                               # the plugin's first two optimize() calls
+        pkg.em_step_batched_iters(xs, full, seg, iters)
+        for i, y in enumerate(ys):
+            leaf = pkg.DeviceSamples([t[int(seg[i]):int(seg[i + 1])] for t in full.x],
+                                     full.w[int(seg[i]):int(seg[i + 1])], full.hpdf[int(seg[i]):int(seg[i + 1])],
+                                     full.is_diffuse[int(seg[i]):int(seg[i + 1])])
+            y.optimize(leaf, int(iters[i]))
+    for i, (x, y) in enumerate(zip(xs, ys)):
+        px, py = _params(x), _params(y)
+        for k in px:
+            np.testing.assert_array_equal(px[k], py[k], err_msg=f"leaf {i} {k}")
