@@ -408,12 +408,14 @@ def main():
         # each its own K=16 mixture over its own samples (volpath_sdmm.cpp:287-311);
         # leaves shard across ranks with no exchange (weak scaling per rank) ----
         out["leaf_em"] = leaf_em_bench(pkg, synth, full, N, dev, stream, args, timed, world, rank, comm)
-        # ---- spatial tree (jmm SNTree restatement; the plugin's split_to_depth(3)
-        # and split(16000), volpath_sdmm.cpp:358, :161): device find over the
-        # batch positions (STree.find, sdmm_proc.cpp:351) and the leaf routing ----
+        # ---- spatial tree (jmm SNTree restatement) as the built plugin sets it
+        # up: split_to_depth(2) (sdmm/volpath_sdmm.cpp:398), then the splitting
+        # block of optimize() -- split_leaf_recurse(i, 4000) over the nodes while
+        # leaf_nodes() <= 2048 (:253-260, :528-529); device find over the batch
+        # positions (STree.find, sdmm_proc.cpp:314) and the leaf routing ----
         tree = pkg.STree(np.float32([0, 0, 0]), np.float32([1, 1, 1]), device=dev.index)
-        tree.split_to_depth(3)
-        tree.split(batch["x"][0:3], 16000)
+        tree.split_to_depth(2)
+        tree.split_leaves(batch["x"][0:3], 4000, 2048)
         node_ids = torch.empty(n_local, dtype=torch.int32, device=dev)
         pts = shard.x[0:3]
         tree.find(pts, node_ids)
@@ -421,7 +423,8 @@ def main():
         f_steps = max(5, args.steps)
         f_wall, _ = timed(lambda: (tree.find(pts, node_ids), torch.cuda.synchronize()), f_steps, events=False)
         r_wall, _ = timed(lambda: tree.route(shard), max(3, args.steps // 4), events=False)
-        out["stree"] = {"nodes": tree.num_nodes, "find_queries_per_s": n_local * world / (f_wall / f_steps),
+        out["stree"] = {"nodes": tree.num_nodes, "leaves": tree.leaf_nodes,
+                        "find_queries_per_s": n_local * world / (f_wall / f_steps),
                         "find_ms": f_wall / f_steps * 1e3,
                         "route_ms": r_wall / max(3, args.steps // 4) * 1e3,
                         "route_samples_per_s": n_local * world / (r_wall / max(3, args.steps // 4))}

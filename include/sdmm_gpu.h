@@ -297,11 +297,13 @@ int sdmm_set_state(sdmm_mix* m, const double* scalars, const double* T, const do
  * a split.  Construction is host work (as in the reference); find and route
  * run on the device, on the tree's own stream.
  *   sdmm_stree_create          root = the AABB enlarged to a cube (:101-106)
- *   sdmm_stree_split_to_depth  split_to_depth (:195-233), volpath_sdmm.cpp:358
+ *   sdmm_stree_split_to_depth  split_to_depth (:195-233); the built plugin
+ *                              calls split_to_depth(2) (sdmm/volpath_sdmm.cpp:398)
  *   sdmm_stree_split           split(threshold) (:235-283) on HOST position
- *                              planes p[3] (n points), volpath_sdmm.cpp:161,226
- *   sdmm_stree_find            STree.find(key) (sdmm_proc.cpp:351, :931, :958)
- *                              for n DEVICE points -> node id or -1 (outside)
+ *                              planes p[3] (n points): every leaf, no leaf cap
+ *   sdmm_stree_find            STree.find(key) (sdmm_proc.cpp:314, :923, :954)
+ *                              for n DEVICE points -> node id or -1 (outside);
+ *                              depth first with backtracking (sntree.h:62-83)
  *   sdmm_stree_route           device samples -> device planes `out` (same n,
  *                              same optional planes) in leaf-contiguous order,
  *                              stable within a leaf; seg (host, num_nodes + 1):
@@ -315,13 +317,32 @@ void sdmm_stree_destroy(sdmm_stree* t);
 int sdmm_stree_split_to_depth(sdmm_stree* t, int max_depth);
 int sdmm_stree_split(sdmm_stree* t, const float* const p[3], int64_t n, int threshold);
 int sdmm_stree_num_nodes(const sdmm_stree* t);
+/* The built plugin's tree calls (sdmm/volpath_sdmm.cpp):
+ *   sdmm_stree_leaf_nodes          m_accelerator->leaf_nodes() (:182, :253)
+ *   sdmm_stree_split_leaf_recurse  split_leaf_recurse(node_i, threshold)
+ *                                  (:184, :257): node's samples p (host planes,
+ *                                  the node's stats positions); a leaf holding
+ *                                  more than threshold is split and its children
+ *                                  recursively; an inner node is left alone
+ *   sdmm_stree_split_leaves        the whole splitting block of optimize() /
+ *                                  optimize_async_run() (:181-186, :253-260):
+ *                                  if leaf_nodes() <= max_leaf_nodes (2048,
+ *                                  :529), split_leaf_recurse(i, threshold (4000,
+ *                                  :528)) for every node, the samples routed to
+ *                                  the leaves by find. */
+int sdmm_stree_leaf_nodes(const sdmm_stree* t);
+int sdmm_stree_split_leaf_recurse(sdmm_stree* t, int node, const float* const p[3], int64_t n, int threshold);
+int sdmm_stree_split_leaves(sdmm_stree* t, const float* const p[3], int64_t n, int threshold, int max_leaf_nodes);
 /* aabb[6 * i] = min(3), max(3); child[2 * i] = children (-1, -1 for a leaf);
  * axis[i]: split axis.  Any output may be NULL. */
 int sdmm_stree_get_nodes(const sdmm_stree* t, float* aabb, int32_t* child, int32_t* axis);
 int sdmm_stree_find(sdmm_stree* t, int64_t n, const float* const p[3], int32_t* node_out);
 int sdmm_stree_route(sdmm_stree* t, const sdmm_samples* device_samples, const sdmm_samples* out, int64_t* seg);
-/* The tree's HIP stream (NULL: its own non-blocking stream).  Put the leaf
- * mixtures and the tree on one stream to order EM steps before wavefronts. */
+/* The tree's HIP stream, taken literally (NULL = the HIP null stream); before
+ * any sdmm_stree_set_stream call the tree uses its own non-blocking stream.  A
+ * wavefront waits (events) for pending work of the bound mixtures on their own
+ * streams, so an EM step enqueued before it is complete when it reads the
+ * mixtures; its outputs are ready once the tree's stream is. */
 int sdmm_stree_set_stream(sdmm_stree* t, void* hip_stream);
 void* sdmm_stree_get_stream(const sdmm_stree* t);
 

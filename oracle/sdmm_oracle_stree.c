@@ -83,16 +83,22 @@ static int st_depth(st_tree* t, int i, int depth, int max_depth) {
     return 0;
 }
 
+/* SNTreeNode::find (jmm/sntree.h:62-83): recursive, child 0 before child 1,
+ * entering only nodes whose box contains the point; a subtree without a leaf
+ * box holding the point returns nullptr and the search goes on (backtracks). */
+static int st_find_rec(const st_tree* t, int i, const float p[3]) {
+    if (!st_in(t, i, p[0], p[1], p[2])) return -1;
+    if (t->child[2 * i] < 0) return i;
+    for (int c = 0; c < 2; ++c) {
+        const int f = st_find_rec(t, t->child[2 * i + c], p);
+        if (f >= 0) return f;
+    }
+    return -1;
+}
+
 int or_stree_find(const float* mn, const float* mx, const int* child, const float p[3]) {
     st_tree t = {(float*)mn, (float*)mx, NULL, (int*)child, 0, 0};
-    if (!st_in(&t, 0, p[0], p[1], p[2])) return -1;
-    int i = 0;
-    while (child[2 * i] >= 0) {
-        if (st_in(&t, child[2 * i], p[0], p[1], p[2])) i = child[2 * i];
-        else if (st_in(&t, child[2 * i + 1], p[0], p[1], p[2])) i = child[2 * i + 1];
-        else return -1;
-    }
-    return i;
+    return st_find_rec(&t, 0, p);
 }
 
 static int st_split(st_tree* t, int i, int64_t* idx, int64_t n, const float* px, const float* py,

@@ -147,6 +147,9 @@ def lib():
                                                    C.c_void_p]
         L.sdmm_em_step_batched_iters.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.sdmm_mix_broadcast.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        L.sdmm_stree_leaf_nodes.argtypes = [C.c_void_p]
+        L.sdmm_stree_split_leaf_recurse.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_int]
+        L.sdmm_stree_split_leaves.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int]
         _lib = L
     return _lib
 
@@ -180,6 +183,7 @@ EXPORTED_SYMBOLS = [
     "sdmm_comm_unique_id", "sdmm_comm_init_rccl", "sdmm_comm_init_host", "sdmm_comm_destroy", "sdmm_comm_rank",
     "sdmm_comm_size", "sdmm_comm_allreduce_f64", "sdmm_em_step_sharded", "sdmm_em_step_batched_sharded",
     "sdmm_em_step_batched_iters", "sdmm_mix_broadcast",
+    "sdmm_stree_leaf_nodes", "sdmm_stree_split_leaf_recurse", "sdmm_stree_split_leaves",
 ]
 
 
@@ -676,13 +680,21 @@ class STree:
     sntree.h:93-299; the plugin's sdmm-lib DMMSTree is absent).  Built on the
     host; find / route run on the device (sdmm_stree_* in include/sdmm_gpu.h)."""
 
-    def __init__(self, aabb_min, aabb_max, device: int = 0):
+    def __init__(self, aabb_min, aabb_max, device: int = 0, stream=None):
         lo = np.ascontiguousarray(aabb_min, np.float32)
         hi = np.ascontiguousarray(aabb_max, np.float32)
         h = C.c_void_p()
         _check(lib().sdmm_stree_create(lo.ctypes.data_as(C.c_void_p), hi.ctypes.data_as(C.c_void_p),
                                        C.c_int(device), C.byref(h)))
         self.h = h
+        # like SDMM: ordered with the torch ops that fill and read its buffers
+        # (torch's current stream unless one is given)
+        if stream is None:
+            import torch
+            if torch.cuda.is_available():
+                self.set_stream(torch.cuda.current_stream(device))
+        else:
+            self.set_stream(stream)
 
     def __del__(self):
         if getattr(self, "h", None) and _lib is not None:
@@ -714,6 +726,12 @@ class STree:
         _check(lib().sdmm_load_json(os.fsencode(path), device, C.byref(h), tab, n.value, C.byref(n)))
         tree = cls.__new__(cls)
         tree.h = h
+        if stream is None:
+            import torch
+            if torch.cuda.is_available():
+                tree.set_stream(torch.cuda.current_stream(device))
+        else:
+            tree.set_stream(stream)
         mixes = [None if tab[i] is None else SDMM._adopt(C.c_void_p(tab[i]), stream) for i in range(n.value)]
         return tree, mixes
 
@@ -725,6 +743,24 @@ class STree:
         p = [np.ascontiguousarray(positions[i], np.float32) for i in range(3)]
         arr = (C.c_void_p * 3)(*[x.ctypes.data for x in p])
         _check(lib().sdmm_stree_split(self.h, arr, C.c_int64(p[0].shape[0]), C.c_int(threshold)))
+
+    def split_leaf_recurse(self, node: int, positions, threshold: int):
+        """split_leaf_recurse(node, threshold) with that node's positions (3, n)."""
+        p = [np.ascontiguousarray(positions[i], np.float32) for i in range(3)]
+        arr = (C.c_void_p * 3)(*[x.ctypes.data for x in p])
+        _check(lib().sdmm_stree_split_leaf_recurse(self.h, int(node), arr, C.c_int64(p[0].shape[0]),
+                                                   int(threshold)))
+
+    def split_leaves(self, positions, threshold: int = 4000, max_leaf_nodes: int = 2048):
+        """The built plugin's splitting block (volpath_sdmm.cpp:253-260)."""
+        p = [np.ascontiguousarray(positions[i], np.float32) for i in range(3)]
+        arr = (C.c_void_p * 3)(*[x.ctypes.data for x in p])
+        _check(lib().sdmm_stree_split_leaves(self.h, arr, C.c_int64(p[0].shape[0]), int(threshold),
+                                             int(max_leaf_nodes)))
+
+    @property
+    def leaf_nodes(self) -> int:
+        return int(lib().sdmm_stree_leaf_nodes(self.h))
 
     @property
     def num_nodes(self) -> int:
@@ -775,14 +811,14 @@ class STree:
         _check(lib().sdmm_stree_bind_mixtures(self.h, self._node_table(node_mix)))
 
     def set_stream(self, stream):
-        """Run on `stream` (a torch.cuda.Stream, a raw hipStream_t int, or None for the tree's own)."""
+        """Run on `stream` (a torch.cuda.Stream or a raw hipStream_t int; None /
+        0 = the HIP null stream)."""
         ptr = None if stream is None else int(getattr(stream, "cuda_stream", stream))
-        _check(lib().sdmm_stree_set_stream(self.h, C.c_void_p(ptr)))
+        _check(lib().sdmm_stree_set_stream(self.h, C.c_void_p(ptr or None)))
 
     @property
     def stream_ptr(self) -> int:
-        """The hipStream_t the tree's work runs on (its own non-blocking stream
-        when set_stream got None or torch's null stream, whose handle is 0)."""
+        """The hipStream_t the tree's work runs on (0: the null stream)."""
         return int(lib().sdmm_stree_get_stream(self.h) or 0)
 
     def guide(self, node_mix, c, u, out=None, node_out=None):

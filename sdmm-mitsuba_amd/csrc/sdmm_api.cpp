@@ -694,6 +694,10 @@ const char* sdmm_kernel_name(const sdmm_mix* m, int which) {
 
 int sdmm_set_stream(sdmm_mix* m, void* hip_stream) {
     if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
+    HIP_TRY(hipSetDevice(m->device));
+    // the handle's scratch (partial rows, staging, guide lists) may still be in
+    // use by work on the old stream
+    if ((hipStream_t)hip_stream != m->stream) HIP_TRY(hipStreamSynchronize(m->stream));
     m->stream = (hipStream_t)hip_stream;  // taken literally: NULL is the HIP null stream
     return SDMM_OK;
 }
@@ -702,6 +706,7 @@ void* sdmm_get_stream(const sdmm_mix* m) { return m ? (void*)m->stream : nullptr
 
 int sdmm_synchronize(sdmm_mix* m) {
     if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
+    HIP_TRY(hipSetDevice(m->device));
     HIP_TRY(hipStreamSynchronize(m->stream));
     return SDMM_OK;
 }
@@ -733,6 +738,7 @@ static int upload_and_set(sdmm_mix* m, const float* weights, const float* means,
 int sdmm_init_hemisphere(sdmm_mix* m, const float* positions, const float* normals, int n_pos,
                          float depth_prior, float min_spatial_distance, uint64_t seed) {
     if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
+    HIP_TRY(hipSetDevice(m->device));
     if (n_pos * 8 != m->K) return fail(SDMM_E_INVALID, "K must equal 8 * n_pos");
     const size_t K = (size_t)m->K;
     std::vector<float> w(K), mean(6 * K), cov(25 * K), bp(25 * K), bd(9 * K);
@@ -746,12 +752,14 @@ int sdmm_init_hemisphere(sdmm_mix* m, const float* positions, const float* norma
 
 int sdmm_set_params(sdmm_mix* m, const float* weights, const float* means, const float* covs) {
     if (!m || !weights || !means || !covs) return fail(SDMM_E_INVALID, "invalid argument");
+    HIP_TRY(hipSetDevice(m->device));
     return upload_and_set(m, weights, means, covs);
 }
 
 int sdmm_estep_stats(sdmm_mix* m, const sdmm_samples* s, double* stats) {
     if (!m || !stats) return fail(SDMM_E_INVALID, "invalid argument");
     if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
+    HIP_TRY(hipSetDevice(m->device));
     int r = check_samples(s);
     if (r) return r;
     if (s->n == 0) {
@@ -764,6 +772,7 @@ int sdmm_estep_stats(sdmm_mix* m, const sdmm_samples* s, double* stats) {
 int sdmm_mstep(sdmm_mix* m, const double* stats, int64_t n_total) {
     if (!m || !stats) return fail(SDMM_E_INVALID, "invalid argument");
     if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
+    HIP_TRY(hipSetDevice(m->device));
     HIP_TRY(launch_mstep(m->K, m->Kp, stats, n_total, m->C, m->S, m->ep, m->gp, m->norm5, m->tmp_mean,
                          m->tmp_cov, m->stream));
     return SDMM_OK;
@@ -896,6 +905,7 @@ int sdmm_mix_broadcast(sdmm_mix* const* mixes, int n_mix, const int32_t* owner, 
 int sdmm_em_step(sdmm_mix* m, const sdmm_samples* s, int iterations) {
     if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
     if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
+    HIP_TRY(hipSetDevice(m->device));
     int r = check_samples(s);
     if (r) return r;
     if (s->n == 0) return SDMM_OK;  // weightSum == 0: optimize() returns early
@@ -1160,6 +1170,7 @@ int sdmm_em_step_batched_host(sdmm_mix* const* mixes, int n_mix, const sdmm_samp
 
 int sdmm_em_step_host(sdmm_mix* m, const sdmm_samples* s, int iterations) {
     if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
+    HIP_TRY(hipSetDevice(m->device));
     int r = check_samples(s);
     if (r) return r;
     if (s->n == 0) return SDMM_OK;
@@ -1197,6 +1208,7 @@ int sdmm_em_step_host(sdmm_mix* m, const sdmm_samples* s, int iterations) {
 int sdmm_responsibilities(sdmm_mix* m, const sdmm_samples* s, float* resp) {
     if (!m || !resp) return fail(SDMM_E_INVALID, "invalid argument");
     if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
+    HIP_TRY(hipSetDevice(m->device));
     int r = check_samples(s);
     if (r) return r;
     if (s->n == 0) return SDMM_OK;
@@ -1229,6 +1241,7 @@ int sdmm_guide_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], con
                      float* const d[3], float* pdf, int32_t* comp) {
     if (!m || !c || !u || !d || !pdf || !comp) return fail(SDMM_E_INVALID, "invalid argument");
     if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
+    HIP_TRY(hipSetDevice(m->device));
     if (nq <= 0) return SDMM_OK;
     int r = ensure_guide_scratch(m, nq);
     if (r) return r;
@@ -1241,6 +1254,7 @@ int sdmm_pdf_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], const
                    float* pdf) {
     if (!m || !c || !d || !pdf) return fail(SDMM_E_INVALID, "invalid argument");
     if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
+    HIP_TRY(hipSetDevice(m->device));
     if (nq <= 0) return SDMM_OK;
     int r = ensure_guide_scratch(m, nq);
     if (r) return r;
@@ -1264,6 +1278,7 @@ int sdmm_guide_product_batch(const sdmm_mix* m, int64_t nq, const float* const c
                              float* const d[3], float* pdf, int32_t* comp, float* heuristic) {
     if (!m || !c || !u || !d || !pdf || !comp) return fail(SDMM_E_INVALID, "invalid argument");
     if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
+    HIP_TRY(hipSetDevice(m->device));
     if (nq <= 0) return SDMM_OK;
     int r = check_bsdf(bsdf, material, frame);
     if (r) return r;
@@ -1280,6 +1295,7 @@ int sdmm_pdf_product_batch(const sdmm_mix* m, int64_t nq, const float* const c[3
                            float* pdf, float* heuristic) {
     if (!m || !c || !d || !pdf) return fail(SDMM_E_INVALID, "invalid argument");
     if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
+    HIP_TRY(hipSetDevice(m->device));
     if (nq <= 0) return SDMM_OK;
     int r = check_bsdf(bsdf, material, frame);
     if (r) return r;
@@ -1294,12 +1310,14 @@ int sdmm_pdf_product_batch(const sdmm_mix* m, int64_t nq, const float* const c[3
 int sdmm_sample_discrete_cdf(const sdmm_mix* m, const float* cdf, int n, const float* u, int64_t nq,
                              int32_t* out) {
     if (!m || !cdf || n <= 0 || !u || !out) return fail(SDMM_E_INVALID, "invalid argument");
+    HIP_TRY(hipSetDevice(m->device));
     HIP_TRY(launch_sample_cdf(cdf, n, u, nq, out, m->stream));
     return SDMM_OK;
 }
 
 int sdmm_get_params(const sdmm_mix* m, const sdmm_params_out* o) {
     if (!m || !o) return fail(SDMM_E_INVALID, "invalid argument");
+    HIP_TRY(hipSetDevice(m->device));
     const size_t K = (size_t)m->K;
     hipStream_t st = m->stream;
     struct Item { void* dst; const void* src; size_t bytes; };
@@ -1324,6 +1342,7 @@ int sdmm_get_params(const sdmm_mix* m, const sdmm_params_out* o) {
 int sdmm_get_state(const sdmm_mix* m, double* scalars, double* T, double* sgW, double* sgM, double* sgC,
                    float* bpriors, float* bdepth) {
     if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
+    HIP_TRY(hipSetDevice(m->device));
     const size_t K = (size_t)m->K;
     hipStream_t st = m->stream;
     if (scalars) HIP_TRY(hipMemcpyAsync(scalars, m->S.scalars, 8 * SC_COUNT, hipMemcpyDeviceToHost, st));
@@ -1340,6 +1359,7 @@ int sdmm_get_state(const sdmm_mix* m, double* scalars, double* T, double* sgW, d
 int sdmm_set_state(sdmm_mix* m, const double* scalars, const double* T, const double* sgW, const double* sgM,
                    const double* sgC, const float* bpriors, const float* bdepth) {
     if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
+    HIP_TRY(hipSetDevice(m->device));
     const size_t K = (size_t)m->K;
     hipStream_t st = m->stream;
     if (scalars) HIP_TRY(hipMemcpyAsync(m->S.scalars, scalars, 8 * SC_COUNT, hipMemcpyHostToDevice, st));
@@ -1448,6 +1468,11 @@ struct sdmm_stree {
     int* guide_fb = nullptr;
     int64_t guide_fb_cap = 0;
     GuideSortScratch guide_sort{};
+    bool stream_set = false;    // sdmm_stree_set_stream called (NULL then means the null stream)
+    // the bound mixtures' streams other than the tree's: a wavefront waits for
+    // their pending work (EM steps) through one event per stream
+    std::vector<hipStream_t> mix_streams;
+    std::vector<hipEvent_t> mix_events;
 };
 
 namespace {
@@ -1534,20 +1559,24 @@ void st_split_recurse(sdmm_stree* t, int node, std::vector<int64_t>& idx, const 
         st_split_recurse(t, t->nodes[node].child[c], sub[c], px, py, pz, threshold);
 }
 
+// SNTreeNode::find (jmm/sntree.h:62-83): depth first, child 0 first, with
+// backtracking out of subtrees that hold no leaf box with the point.
 int st_find_host(const sdmm_stree* t, const float p[3]) {
     if (!st_contains(t->nodes[0], p)) return -1;
-    int id = 0;
-    while (t->nodes[id].child[0] >= 0) {
-        const int c0 = t->nodes[id].child[0], c1 = t->nodes[id].child[1];
-        if (st_contains(t->nodes[c0], p)) id = c0;
-        else if (st_contains(t->nodes[c1], p)) id = c1;
-        else return -1;
+    std::vector<int> stack{0};
+    while (!stack.empty()) {
+        const int i = stack.back();
+        stack.pop_back();
+        const STNodeHost& n = t->nodes[(size_t)i];
+        if (n.child[0] < 0) return i;
+        if (st_contains(t->nodes[(size_t)n.child[1]], p)) stack.push_back(n.child[1]);
+        if (st_contains(t->nodes[(size_t)n.child[0]], p)) stack.push_back(n.child[0]);
     }
-    return id;
+    return -1;
 }
 
 int st_upload(sdmm_stree* t) {
-    if (!t->stream) HIP_TRY(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
+    if (!t->stream && !t->stream_set) HIP_TRY(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
     if (!t->dirty) return SDMM_OK;
     const size_t bytes = 32 * t->nodes.size();
     if (bytes > t->dnodes_cap) {
@@ -1602,6 +1631,7 @@ void sdmm_stree_destroy(sdmm_stree* t) {
     if (t->scratch) (void)hipFree(t->scratch);
     if (t->dtab) (void)hipFree(t->dtab);
     if (t->guide_fb) (void)hipFree(t->guide_fb);
+    for (hipEvent_t e : t->mix_events) (void)hipEventDestroy(e);
     if (t->stream && t->own_stream) (void)hipStreamDestroy(t->stream);
     delete t;
 }
@@ -1633,6 +1663,32 @@ int sdmm_stree_split(sdmm_stree* t, const float* const p[3], int64_t n, int thre
 }
 
 int sdmm_stree_num_nodes(const sdmm_stree* t) { return t ? (int)t->nodes.size() : 0; }
+
+int sdmm_stree_leaf_nodes(const sdmm_stree* t) {
+    if (!t) return 0;
+    int n = 0;
+    for (const STNodeHost& nd : t->nodes) n += nd.child[0] < 0 ? 1 : 0;
+    return n;
+}
+
+int sdmm_stree_split_leaf_recurse(sdmm_stree* t, int node, const float* const p[3], int64_t n, int threshold) {
+    if (!t || node < 0 || node >= (int)t->nodes.size() || n < 0 || threshold < 1 ||
+        (n > 0 && (!p || !p[0] || !p[1] || !p[2])))
+        return fail(SDMM_E_INVALID, "invalid argument");
+    if (t->nodes[(size_t)node].child[0] >= 0) return SDMM_OK;   // an inner node: nothing to split
+    std::vector<int64_t> idx((size_t)n);
+    for (int64_t i = 0; i < n; ++i) idx[(size_t)i] = i;
+    st_split_recurse(t, node, idx, p[0], p[1], p[2], threshold);
+    t->dirty = true;
+    t->tab_valid = false;
+    return SDMM_OK;
+}
+
+int sdmm_stree_split_leaves(sdmm_stree* t, const float* const p[3], int64_t n, int threshold, int max_leaf_nodes) {
+    if (!t) return fail(SDMM_E_INVALID, "invalid argument");
+    if (max_leaf_nodes >= 0 && sdmm_stree_leaf_nodes(t) > max_leaf_nodes) return SDMM_OK;
+    return sdmm_stree_split(t, p, n, threshold);
+}
 
 int sdmm_stree_set_nodes(sdmm_stree* t, int n, const float* aabb, const int32_t* child, const int32_t* axis) {
     if (!t || n < 1 || !aabb || !child || !axis) return fail(SDMM_E_INVALID, "invalid argument");
@@ -1732,17 +1788,13 @@ int sdmm_stree_route(sdmm_stree* t, const sdmm_samples* in, const sdmm_samples* 
 int sdmm_stree_set_stream(sdmm_stree* t, void* hip_stream) {
     if (!t) return fail(SDMM_E_INVALID, "invalid argument");
     HIP_TRY(hipSetDevice(t->device));
-    if (t->stream) {
-        HIP_TRY(hipStreamSynchronize(t->stream));
-        if (t->own_stream) HIP_TRY(hipStreamDestroy(t->stream));
+    if (t->stream || t->stream_set) {
+        HIP_TRY(hipStreamSynchronize(t->stream));   // scratch in use by the old stream
+        if (t->own_stream && t->stream) HIP_TRY(hipStreamDestroy(t->stream));
     }
-    if (hip_stream) {
-        t->stream = (hipStream_t)hip_stream;
-        t->own_stream = false;
-    } else {
-        t->stream = nullptr;   // recreated (own, non-blocking) on next device use
-        t->own_stream = true;
-    }
+    t->stream = (hipStream_t)hip_stream;   // taken literally: NULL is the HIP null stream
+    t->own_stream = false;
+    t->stream_set = true;
     return SDMM_OK;
 }
 
@@ -1758,6 +1810,7 @@ int st_upload_table(sdmm_stree* t, const sdmm_mix* const* node_mix) {
     const size_t nn = t->nodes.size();
     std::vector<GuideMixHost> tab(nn);
     int kmax = 0;
+    t->mix_streams.clear();
     for (size_t i = 0; i < nn; ++i) {
         const sdmm_mix* m = node_mix[i];
         tab[i] = GuideMixHost{nullptr, 0, 0};
@@ -1765,6 +1818,14 @@ int st_upload_table(sdmm_stree* t, const sdmm_mix* const* node_mix) {
         if (m->device != t->device) return fail(SDMM_E_INVALID, "wavefront: mixture on another device");
         tab[i] = GuideMixHost{m->gp, m->Kp, m->K};
         kmax = std::max(kmax, m->K);
+        if (m->stream != t->stream &&
+            std::find(t->mix_streams.begin(), t->mix_streams.end(), m->stream) == t->mix_streams.end())
+            t->mix_streams.push_back(m->stream);
+    }
+    while (t->mix_events.size() < t->mix_streams.size()) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        t->mix_events.push_back(e);
     }
     bool same = tab.size() == t->tab_host.size();
     for (size_t i = 0; same && i < nn; ++i) same = !(tab[i] != t->tab_host[i]);
@@ -1799,6 +1860,11 @@ int st_guide(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const f
     }
     r = grow_guide_scratch(t->guide_fb, t->guide_fb_cap, t->guide_sort, t->stream, nq);
     if (r) return r;
+    // order the wavefront after the mixtures' pending work on their own streams
+    for (size_t i = 0; i < t->mix_streams.size(); ++i) {
+        HIP_TRY(hipEventRecord(t->mix_events[i], t->mix_streams[i]));
+        HIP_TRY(hipStreamWaitEvent(t->stream, t->mix_events[i], 0));
+    }
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, t->device);
     const GuideSortScratch* sort = nq >= (1 << 14) ? &t->guide_sort : nullptr;

@@ -149,8 +149,7 @@ struct GuideSortScratch {
 };
 
 // ---- spatial tree node (stree.hip, guide.hip) ------------------------------
-// min[3], max[3], child0, child1 (-1 for a leaf); SNTreeNode::find
-// (jmm/sntree.h:62-83) as a single descent.
+// min[3], max[3], child0, child1 (-1 for a leaf).
 struct STNodeDev {
     float mn[3], mx[3];
     int c0, c1;
@@ -161,6 +160,13 @@ __device__ __forceinline__ bool box_contains(const STNodeDev& n, float x, float 
     return n.mn[0] <= x && x <= n.mx[0] && n.mn[1] <= y && y <= n.mx[1] && n.mn[2] <= z && z <= n.mx[2];
 }
 
+// SNTreeNode::find (jmm/sntree.h:62-83): depth first, child 0 before child 1,
+// into every child whose (inclusive) box holds the point, BACKTRACKING when a
+// subtree holds no leaf box with the point (split planes computed as
+// min + s diag and max - (1 - s) diag can leave an ulp gap between siblings).
+// The greedy descent is the common case; only a dead end restarts as the full
+// depth-first search, with the pending siblings on a small stack.
+constexpr int kFindStack = 64;
 __device__ __forceinline__ int stree_find_point(const STNodeDev* __restrict__ nodes, float x, float y, float z) {
     STNodeDev n = nodes[0];
     if (!box_contains(n, x, y, z)) return -1;
@@ -172,6 +178,18 @@ __device__ __forceinline__ int stree_find_point(const STNodeDev* __restrict__ no
         const int c1 = n.c1;
         const STNodeDev b = nodes[c1];
         if (box_contains(b, x, y, z)) { id = c1; n = b; continue; }
+        // dead end below a node that holds the point: the reference's search
+        int stack[kFindStack];
+        int sp = 0;
+        stack[sp++] = 0;
+        while (sp > 0) {
+            const int i = stack[--sp];
+            const STNodeDev m = nodes[i];
+            if (m.c0 < 0) return i;
+            const STNodeDev m0 = nodes[m.c0], m1 = nodes[m.c1];
+            if (box_contains(m1, x, y, z) && sp < kFindStack) stack[sp++] = m.c1;
+            if (box_contains(m0, x, y, z) && sp < kFindStack) stack[sp++] = m.c0;
+        }
         return -1;
     }
     return -1;

@@ -156,3 +156,45 @@ def test_wavefront_table_update_and_stream(pkg, synth, gpu):
     with pytest.raises(pkg.SDMMError):
         t.guide(None, ct, ut)
     t.set_stream(None)
+
+
+def test_wavefront_orders_after_em_on_other_streams(pkg, synth, gpu):
+    """the leaf mixtures step on their own stream, the tree guides on
+    torch's stream, with NO synchronisation in between -- the wavefront waits for
+    the EM (events on the mixtures' streams), so its outputs equal those of a
+    run with a device synchronisation between the two."""
+    import torch
+    b = synth.em_batch(200000, 128)
+    ds = pkg.DeviceSamples.from_numpy(b["x"], b["w"])
+    side = torch.cuda.Stream()
+
+    def run(sync):
+        t = pkg.STree(np.float32([0, 0, 0]), np.float32([1, 1, 1]))
+        t.split_to_depth(1)
+        out, seg = t.route(ds)
+        torch.cuda.synchronize()
+        xs = np.stack([x.cpu().numpy() for x in out.x])
+        mixes = [None] * (len(seg) - 1)
+        for v in range(len(seg) - 1):
+            a, e = int(seg[v]), int(seg[v + 1])
+            if e - a < 64:
+                continue
+            m = pkg.SDMM(128, stream=side)
+            m.init_hemisphere(xs[0:3, a:a + 16].T.copy(), xs[3:6, a:a + 16].T.copy(), synth.DEPTH_PRIOR,
+                              synth.SPATIAL_DISTANCE, 3 + v)
+            mixes[v] = (m, pkg.DeviceSamples([x[a:e] for x in out.x], out.w[a:e]))
+        side.synchronize()
+        t.bind([None if x is None else x[0] for x in mixes])
+        for x in mixes:                              # enqueued on `side`, not waited for
+            if x is not None:
+                x[0].optimize(x[1], 3)
+        if sync:
+            torch.cuda.synchronize()
+        c, u, d, ct, ut, dt = _queries(gpu, 1 << 16, 9)
+        dd, pdf, comp = t.guide(None, ct, ut)
+        torch.cuda.current_stream().synchronize()
+        return np.stack([x.cpu().numpy() for x in dd]), pdf.cpu().numpy(), comp.cpu().numpy()
+
+    a, r = run(False), run(True)
+    for x, y in zip(a, r):
+        np.testing.assert_array_equal(x, y)

@@ -115,3 +115,80 @@ def test_routed_leaves_batched_em(pkg, synth, gpu):
         pa, pb = ma.get_params(), mb.get_params()
         for k in ("weights", "mean", "cov"):
             np.testing.assert_array_equal(pa[k], pb[k])
+
+
+def _gap_tree(pkg):
+    """Root [0,1]^3 split on x at 0.5; its upper child split on y with an
+    ulp-scale GAP (y in (0.59, 0.6) belongs to neither grandchild), the lower
+    child split on y at 0.5.  Node ids in creation order."""
+    aabb = np.float32([
+        [0, 0, 0, 1, 1, 1],            # 0 root
+        [0.5, 0, 0, 1, 1, 1],          # 1 upper x (child 0)
+        [0, 0, 0, 0.5, 1, 1],          # 2 lower x (child 1)
+        [0.5, 0.6, 0, 1, 1, 1],        # 3 child 0 of 1
+        [0.5, 0, 0, 1, 0.59, 1],       # 4 child 1 of 1 (gap below 0.6)
+        [0, 0.5, 0, 0.5, 1, 1],        # 5 child 0 of 2
+        [0, 0, 0, 0.5, 0.5, 1]])       # 6 child 1 of 2
+    child = np.int32([[1, 2], [3, 4], [5, 6], [-1, -1], [-1, -1], [-1, -1], [-1, -1]])
+    axis = np.int32([0, 1, 1, 2, 2, 2, 2])
+    t = pkg.STree(np.float32([0, 0, 0]), np.float32([1, 1, 1]))
+    t.set_nodes(aabb, child, axis)
+    return t, aabb, child
+
+
+def _gap_queries():
+    # on the root's plane x = 0.5 (in both children) inside the upper child's
+    # y gap: the depth-first search leaves node 1 empty-handed and finds node 5
+    q = np.float32([[0.5, 0.595, 0.5], [0.5, 0.59, 0.5], [0.5, 0.6, 0.5], [0.75, 0.595, 0.5],
+                    [0.25, 0.595, 0.5], [0.5, 0.3, 0.2], [0.5, 0.595, 1.0]])
+    expect = np.int32([5, 4, 3, -1, 5, 4, 5])
+    return q, expect
+
+
+def test_find_backtracks_like_sntree(pkg, oracle):
+    """SNTreeNode::find (jmm/sntree.h:62-83) backtracks out of a subtree whose
+    children miss the point; the oracle restates it."""
+    t, aabb, child = _gap_tree(pkg)
+    q, expect = _gap_queries()
+    np.testing.assert_array_equal(oracle.stree_find(aabb, child, q), expect)
+
+
+def test_split_leaves_plugin_block(pkg, oracle, synth):
+    """sdmm_stree_split_leaves: the built plugin's splitting block
+    (volpath_sdmm.cpp:253-260) -- split_to_depth(2), then split_leaf_recurse(i,
+    4000) over the nodes while leaf_nodes() <= 2048; == the oracle's split, and
+    nothing happens above the leaf cap."""
+    b, p = _points(synth, 120000)
+    lo, hi = np.float32([0, 0, 0]), np.float32([1, 1, 1])
+    t = pkg.STree(lo, hi)
+    t.split_to_depth(2)
+    assert t.leaf_nodes == 64
+    t.split_leaves(p, 4000, 2048)
+    aabb, child, axis = t.nodes()
+    oa, oc, ox = oracle.stree_build(lo, hi, 2, p, 4000)
+    np.testing.assert_array_equal(child, oc)
+    np.testing.assert_array_equal(aabb, oa)
+    assert t.leaf_nodes == int((child[:, 0] < 0).sum()) > 64
+    u = pkg.STree(lo, hi)
+    u.split_to_depth(2)
+    u.split_leaves(p, 4000, 10)                      # 64 leaves > cap: no split
+    assert u.num_nodes == 127 and u.leaf_nodes == 64
+    # split_leaf_recurse on one leaf with that leaf's samples == split() of a
+    # one-leaf tree
+    v = pkg.STree(lo, hi)
+    v.split_leaf_recurse(0, p, 4000)
+    w = pkg.STree(lo, hi)
+    w.split(p, 4000)
+    for x, y in zip(v.nodes(), w.nodes()):
+        np.testing.assert_array_equal(x, y)
+    v.split_leaf_recurse(0, p, 10)                   # an inner node now: no-op
+    np.testing.assert_array_equal(v.nodes()[1], w.nodes()[1])
+
+
+@pytest.mark.gpu
+def test_device_find_backtracks(pkg, oracle, gpu):
+    import torch
+    t, aabb, child = _gap_tree(pkg)
+    q, expect = _gap_queries()
+    got = t.find([torch.from_numpy(q[:, i].copy()).to(gpu) for i in range(3)]).cpu().numpy()
+    np.testing.assert_array_equal(got, expect)
