@@ -74,6 +74,76 @@ __device__ __forceinline__ V angle_over_sin(V c) {
     return (s2 < sp(1e-6f)) ? sp(1.0f) : f;
 }
 
+// ---- cancellation-free 1 + cos(theta) (the statistics kernels) -----------
+// Near a component's antipode (c -> -1) theta/sin(theta) ~ pi / sqrt(1 - c^2)
+// amplifies the rounding of c: fl(R2.d) + 1 carries an absolute error ~2^-24,
+// a relative error 2^-24 / (1 + c) of 1 + c.  Rounding R2.d to fp32 alone puts
+// the K = 128 EM parameters ~2e-4 from the exact evaluation of the same float
+// parameters, twice the north-star 1e-4.  The statistics kernels
+// therefore form delta = 1 + c without the cancellation:
+//   n.d = (|n + d|^2 - |n|^2 - |d|^2) / 2   (n = R2, the mean direction)
+//   1 + n.d = |n + d|^2 / 2 + (1 - |n|^2) / 2 + (1 - |d|^2) / 2,
+// where n_i + d_i is exact near the antipode (Sterbenz) and the two defect
+// halves are fp64-rounded constants (EP_CN per component, half_defect per
+// sample): delta carries a few ulps of RELATIVE error everywhere.  The
+// responsibility kernels (the metric) keep fl(R2.d), within their bound.
+__device__ __forceinline__ float half_defect(float d0, float d1, float d2) {
+    const double n2 = (double)d0 * (double)d0 + (double)d1 * (double)d1 + (double)d2 * (double)d2;
+    return (float)(0.5 * (1.0 - n2));
+}
+__device__ __forceinline__ V one_plus_c(const V* __restrict__ P, float d0, float d1, float d2, float cd) {
+    const V e0 = P[EP_R20] + d0, e1 = P[EP_R21] + d1, e2 = P[EP_R22] + d2;
+    return vfma(sp(0.5f), vfma(e2, e2, vfma(e1, e1, e0 * e0)), P[EP_CN] + cd);
+}
+// u = (1 - |c|)/2 = min(delta, 2 - delta)/2 and s^2 = 1 - c^2 = delta (2 - delta)
+__device__ __forceinline__ V half_gap(V dl, V om) { return sp(0.5f) * V{fminf(dl.x, om.x), fminf(dl.y, om.y)}; }
+
+// angle_over_sin (degree-9 polynomial, quirks included) from delta = 1 + c
+__device__ __forceinline__ V angle_over_sin_d(V dl) {
+    const V om = sp(2.0f) - dl;
+    const V u = half_gap(dl, om);
+    V h = sp(5.659248352050781f);
+    h = vfma(h, u, sp(-8.219043731689453f));
+    h = vfma(h, u, sp(6.410147190093994f));
+    h = vfma(h, u, sp(-2.090447187423706f));
+    h = vfma(h, u, sp(0.9454659819602966f));
+    h = vfma(h, u, sp(0.32539111375808716f));
+    h = vfma(h, u, sp(0.46356001496315f));
+    h = vfma(h, u, sp(0.533078670501709f));
+    h = vfma(h, u, sp(0.666670560836792f));
+    h = vfma(h, u, sp(1.0f));
+    const V s2 = dl * om;
+    const V fneg = vfma(sp(3.14159265358979f), vrsq(s2), -h);
+    const V f = (dl < sp(1.0f)) ? fneg : h;     // c < 0
+    return (s2 < sp(1e-6f)) ? sp(1.0f) : f;
+}
+
+// pair_pdf<true> with delta: pi_k pdf_k and the directional tangent (t0, t1);
+// dfail = 0 (the log map fails at c <= -1, i.e. delta <= 0) or +inf (d == 0).
+__device__ __forceinline__ V pair_pdf_stats(const V* __restrict__ P, float p0, float p1, float p2, float d0,
+                                            float d1, float d2, float cd, float dfail, V& t0, V& t1) {
+    const V tp0 = p0 - P[EP_MU0], tp1 = p1 - P[EP_MU1], tp2 = p2 - P[EP_MU2];
+    const V dl = one_plus_c(P, d0, d1, d2, cd);
+    const V a = angle_over_sin_d(dl);
+    const V u0 = P[EP_L00] * tp0;
+    const V u1 = vfma(P[EP_L11], tp1, P[EP_L10] * tp0);
+    const V u2 = vfma(P[EP_L22], tp2, vfma(P[EP_L21], tp1, P[EP_L20] * tp0));
+    const V s3 = vfma(P[EP_L32], tp2, vfma(P[EP_L31], tp1, P[EP_L30] * tp0));
+    const V s4 = vfma(P[EP_L42], tp2, vfma(P[EP_L41], tp1, P[EP_L40] * tp0));
+    const V r0 = vfma(P[EP_R02], sp(d2), vfma(P[EP_R01], sp(d1), P[EP_R00] * d0));
+    const V r1 = vfma(P[EP_R12], sp(d2), vfma(P[EP_R11], sp(d1), P[EP_R10] * d0));
+    const V ta = r0 * a, tb = r1 * a;
+    const V u3 = vfma(P[EP_L33], ta, s3);
+    const V u4 = vfma(P[EP_L44], tb, vfma(P[EP_L43], ta, s4));
+    const auto ok = dl > sp(dfail);
+    t0 = ok ? ta : sp(0.0f);
+    t1 = ok ? tb : sp(0.0f);
+    const V q = vfma(u4, u4, vfma(u3, u3, vfma(u2, u2, vfma(u1, u1, u0 * u0))));
+    const V e = vexp2(vfma(q, sp(-0.72134752044448170368f), sp(kLog2Norm5)));
+    const V pdf = e * (P[EP_DIPI] * a);
+    return ok ? pdf : sp(0.0f);
+}
+
 // pi_k * pdf_k(x) (unnormalised posterior) of two components and the
 // directional tangent of the sample in their frames.  p: sample position,
 // d: sample direction.  cfail: -1 for a valid sample, +inf when d == 0
@@ -118,11 +188,14 @@ __device__ __forceinline__ V pair_pdf(const V* __restrict__ P, float p0, float p
 
 struct SampleVals {
     float x0, x1, x2, x3, x4, x5, w, h;
+    float cd;   // half_defect of the direction (statistics kernels)
     bool diffuse;
     // c > cfail selects valid log maps; d == 0 fails for every component
     __device__ float cfail() const {
         return (x3 == 0.0f && x4 == 0.0f && x5 == 0.0f) ? __builtin_inff() : -1.0f;
     }
+    // the same on delta = 1 + c
+    __device__ float dfail() const { return (x3 == 0.0f && x4 == 0.0f && x5 == 0.0f) ? __builtin_inff() : 0.0f; }
 };
 
 // Sample staging.  The wave walks its chunk in blocks of 64 consecutive
@@ -134,6 +207,7 @@ struct SampleVals {
 struct SampleBlock {
     float x0, x1, x2, x3, x4, x5, w, h;
     int diff;
+    float cd;   // half_defect of this lane's sample (set when consumed, statistics kernels)
 };
 
 __device__ __forceinline__ SampleBlock load_block(const SamplesDev& s, int64_t base, int64_t s1, int lane) {
@@ -170,7 +244,7 @@ __device__ __forceinline__ float bcast(float v, int src) {
 }
 
 // sample t + g of the block (t: wave-uniform offset, g: this lane's group)
-template <int LPS>
+template <int LPS, bool WANT_CD = false>
 __device__ __forceinline__ SampleVals take_sample(const SampleBlock& b, int t, int g, bool has_h,
                                                   bool has_d, uintptr_t dpos) {
     const int src = (LPS == 64) ? t : t + g;
@@ -178,6 +252,7 @@ __device__ __forceinline__ SampleVals take_sample(const SampleBlock& b, int t, i
     v.x0 = bcast<LPS>(b.x0, src); v.x1 = bcast<LPS>(b.x1, src); v.x2 = bcast<LPS>(b.x2, src);
     v.x3 = bcast<LPS>(b.x3, src); v.x4 = bcast<LPS>(b.x4, src); v.x5 = bcast<LPS>(b.x5, src);
     v.w = bcast<LPS>(b.w, src);
+    v.cd = WANT_CD ? bcast<LPS>(b.cd, src) : 0.0f;
     v.h = has_h ? bcast<LPS>(b.h, src) : 0.0f;
     int word;
     if constexpr (LPS == 64)
@@ -192,31 +267,32 @@ __device__ __forceinline__ SampleVals take_sample(const SampleBlock& b, int t, i
 // group's sample.  Two block buffers, each reloaded right after the block it
 // holds has been consumed, so the loads of block b+1 fly during block b and
 // no register copy (which would force an early vmcnt wait) is needed.
-template <int LPS, class F>
-__device__ __forceinline__ void run_block(const SampleBlock& b, int64_t blk, int64_t s1, int g,
+template <int LPS, bool WANT_CD, class F>
+__device__ __forceinline__ void run_block(SampleBlock b, int64_t blk, int64_t s1, int g,
                                           const SamplesDev& s, F& body) {
     constexpr int SPW = 64 / LPS;
     const int cnt = (s1 - blk < 64) ? (int)(s1 - blk) : 64;
     const bool has_h = s.hpdf != nullptr, has_d = s.isDiffuse != nullptr;
+    if constexpr (WANT_CD) b.cd = half_defect(b.x3, b.x4, b.x5);   // once per sample (its own lane)
     for (int t = 0; t < cnt; t += SPW) {
         // block lane t+g held sample blk+t+g (clamped to s1-1 past the end)
         int64_t si = blk + t + g;
         si = (si < s1) ? si : s1 - 1;
-        const SampleVals sv = take_sample<LPS>(b, t, g, has_h, has_d, (uintptr_t)(s.isDiffuse + si));
+        const SampleVals sv = take_sample<LPS, WANT_CD>(b, t, g, has_h, has_d, (uintptr_t)(s.isDiffuse + si));
         body(sv, blk + t + g, t + g < cnt);
     }
 }
 
-template <int LPS, class F>
+template <int LPS, bool WANT_CD = false, class F>
 __device__ __forceinline__ void walk_samples(const SamplesDev& s, int64_t s0, int64_t s1, int lane, int g,
                                              F&& body) {
     if (s0 >= s1) return;
     SampleBlock A = load_block(s, s0, s1, lane);
     for (int64_t blk = s0; blk < s1; blk += 128) {
         const SampleBlock B = load_block(s, blk + 64, s1, lane);   // clamped past the end
-        run_block<LPS>(A, blk, s1, g, s, body);
+        run_block<LPS, WANT_CD>(A, blk, s1, g, s, body);
         A = load_block(s, blk + 128, s1, lane);
-        if (blk + 64 < s1) run_block<LPS>(B, blk + 64, s1, g, s, body);
+        if (blk + 64 < s1) run_block<LPS, WANT_CD>(B, blk + 64, s1, g, s, body);
     }
 }
 
@@ -668,19 +744,19 @@ estep_stats_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, in
         for (int f = 0; f < ST_FIELDS; ++f) acc[c][f] = sp(0.0f);
     float accH = 0.0f, accWs = 0.0f;
 
-    walk_samples<LPS>(s, s0, s1, lane, g, [&](const SampleVals& sv, int64_t, bool in)
-                                              __attribute__((always_inline)) {
+    walk_samples<LPS, true>(s, s0, s1, lane, g, [&](const SampleVals& sv, int64_t, bool in)
+                                                    __attribute__((always_inline)) {
         const bool finite_w = __builtin_isfinite(sv.w);
         // sumWeights counts every finite weight (stepwise_tangent.h:462-475)
         accWs += (in && finite_w) ? sv.w : 0.0f;
         // calculateStats skips non-finite and zero weights (:288-293)
         const bool use = in && finite_w && (sv.w != 0.0f);
-        const float cf = sv.cfail();
+        const float df = sv.dfail();
         V q[NP], ta[NP], tb[NP];
         V qs = sp(0.0f);
 #pragma unroll
         for (int c = 0; c < NP; ++c) {
-            q[c] = pair_pdf<true>(P[c], sv.x0, sv.x1, sv.x2, sv.x3, sv.x4, sv.x5, cf, ta[c], tb[c]);
+            q[c] = pair_pdf_stats(P[c], sv.x0, sv.x1, sv.x2, sv.x3, sv.x4, sv.x5, sv.cd, df, ta[c], tb[c]);
             qs += q[c];
         }
         const Norm nm = normalise<LPS>(qs.x + qs.y, sv);
@@ -780,14 +856,37 @@ estep_stats_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, in
 
 constexpr int kStatTile = 4;
 
-// pi_k pdf_k and the directional tangent (mvtn.h:146-177 with the quirks of
-// angle_over_sin_fast: a = 0 when the log map fails, so ta = tb = 0 then).
+// theta/sin(theta) from delta = 1 + c for the statistics tiles: the degree-7
+// main-path polynomial of angle_over_sin_main; RARE adds the quirks of
+// angle_over_sin_fast (s^2 < 1e-6: 1, or 0 when the log map fails, delta <= 0).
+template <bool RARE>
+__device__ __forceinline__ V angle_over_sin_tile_d(V dl) {
+    const V om = sp(2.0f) - dl;
+    const V u = half_gap(dl, om);
+    V h = vfma(sp(3.3755881786346436f), u, sp(-3.17423415184021f));
+    h = vfma(h, u, sp(2.1241207122802734f));
+    h = vfma(h, u, sp(-0.04515757039189339f));
+    h = vfma(h, u, sp(0.5178175568580627f));
+    h = vfma(h, u, sp(0.5294308066368103f));
+    h = vfma(h, u, sp(0.6667603850364685f));
+    h = vfma(h, u, sp(0.9999996423721313f));
+    const V s2 = dl * om;
+    const V fneg = vfma(sp(3.14159265358979f), vrsq(s2), -h);
+    const V f = V{dl.x < 1.0f ? fneg.x : h.x, dl.y < 1.0f ? fneg.y : h.y};
+    if constexpr (!RARE) return f;
+    const V one = V{dl.x > 0.0f ? 1.0f : 0.0f, dl.y > 0.0f ? 1.0f : 0.0f};
+    return V{s2.x < 1e-6f ? one.x : f.x, s2.y < 1e-6f ? one.y : f.y};
+}
+
+// pi_k pdf_k and the directional tangent (mvtn.h:146-177; a = 0 when the log
+// map fails, so ta = tb = 0 then) with the cancellation-free delta = 1 + c,
+// returned in dl for the tile's rare-angle detector.
 template <bool RARE>
 __device__ __forceinline__ V pair_qt_fast(const V* __restrict__ P, float p0, float p1, float p2, float d0,
-                                          float d1, float d2, V& ta, V& tb) {
+                                          float d1, float d2, float cd, V& ta, V& tb, V& dl) {
     const V tp0 = p0 - P[EP_MU0], tp1 = p1 - P[EP_MU1], tp2 = p2 - P[EP_MU2];
-    const V c = vfma(P[EP_R22], sp(d2), vfma(P[EP_R21], sp(d1), P[EP_R20] * d0));
-    const V a = RARE ? angle_over_sin_fast(c) : angle_over_sin_main(c);
+    dl = one_plus_c(P, d0, d1, d2, cd);
+    const V a = angle_over_sin_tile_d<RARE>(dl);
     const V r0 = vfma(P[EP_R02], sp(d2), vfma(P[EP_R01], sp(d1), P[EP_R00] * d0));
     const V r1 = vfma(P[EP_R12], sp(d2), vfma(P[EP_R11], sp(d1), P[EP_R10] * d0));
     ta = r0 * a;
@@ -842,7 +941,7 @@ estep_stats_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
         prow = partials + (int64_t)(L.row0 + it.y) * pstride;
     }
     __shared__ float4 sblk[WPB][64][2];      // x0 x1 x2 x3 | x4 x5 hpdf diffuse
-    __shared__ float sw[WPB][64];            // weight
+    __shared__ float2 sw[WPB][64];           // weight, half_defect of the direction
     __shared__ float4 sg[WPB][kStatTile];    // {gamma scale, weight, threshold, -}
     extern __shared__ __attribute__((aligned(16))) float red[];
     const int lane = threadIdx.x & 63;
@@ -861,7 +960,7 @@ estep_stats_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
     float accH = 0.0f, accWs = 0.0f;   // lanes < kStatTile: their samples' H and sumWeights terms
     const bool has_h = s.hpdf != nullptr, has_d = s.isDiffuse != nullptr;
     float4 (*blk_lds)[2] = sblk[wid];
-    float* w_lds = sw[wid];
+    float2* w_lds = sw[wid];
     float4* g_lds = sg[wid];
 
     if (s0 < s1) {
@@ -873,35 +972,36 @@ estep_stats_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
                 const bool dif = has_d && ((A.diff >> sh) & 0xff) != 0;
                 blk_lds[lane][0] = float4{A.x0, A.x1, A.x2, A.x3};
                 blk_lds[lane][1] = float4{A.x4, A.x5, has_h ? A.h : 0.0f, dif ? 1.0f : 0.0f};
-                w_lds[lane] = A.w;
+                w_lds[lane] = float2{A.w, half_defect(A.x3, A.x4, A.x5)};
             }
             A = load_block(s, blk + 64, s1, lane);
             const int cnt = (s1 - blk < 64) ? (int)(s1 - blk) : 64;
             for (int tb = 0; tb < cnt; tb += kStatTile) {
                 V q[kStatTile], ta[kStatTile], tb2[kStatTile];
-                uint32_t cbits = 0;   // rare-angle detector (see estep_resp_tile_kernel)
+                float dmin = 1.0f;   // rare-angle detector: the smallest 1 + c of the tile
 #pragma unroll
                 for (int t = 0; t < kStatTile; ++t) {
                     const float4 a = blk_lds[tb + t][0];
                     const float4 b = blk_lds[tb + t][1];
-                    q[t] = pair_qt_fast<false>(P, a.x, a.y, a.z, a.w, b.x, b.y, ta[t], tb2[t]);
-                    const V c = vfma(P[EP_R22], sp(b.y), vfma(P[EP_R21], sp(b.x), P[EP_R20] * a.w));
-                    cbits = __builtin_elementwise_max(
-                        cbits, __builtin_elementwise_max(__builtin_bit_cast(uint32_t, c.x), __builtin_bit_cast(uint32_t, c.y)));
+                    V dl;
+                    q[t] = pair_qt_fast<false>(P, a.x, a.y, a.z, a.w, b.x, b.y, w_lds[tb + t].y, ta[t], tb2[t], dl);
+                    dmin = fminf(dmin, fminf(dl.x, dl.y));
                 }
                 {
-                    // c < -0.9999995 somewhere in the tile: redo it with the
-                    // reference's angle quirks (a NaN sum takes the redo too)
+                    // 1 + c < 1e-6 somewhere in the tile (sin < 1e-3 near the
+                    // antipode, or a failed log map): redo it with the reference's
+                    // angle quirks (a NaN sum takes the redo too)
                     const V qs = (q[0] + q[1]) + (q[2] + q[3]);
-                    const bool odd = cbits > __builtin_bit_cast(uint32_t, -0.9999995f) || !(qs.x + qs.y >= 0.0f);
+                    const bool odd = dmin < 1e-6f || !(qs.x + qs.y >= 0.0f);
                     if (__builtin_amdgcn_ballot_w64(odd) != 0) {
                         // (a loop, so that the compiler does not speculate it)
 #pragma unroll 1
                         for (int t = 0; t < kStatTile; ++t) {
                             const float4 a = blk_lds[tb + t][0];
                             const float4 b = blk_lds[tb + t][1];
-                            V ta1, tb1;
-                            const V q1 = pair_qt_fast<true>(P, a.x, a.y, a.z, a.w, b.x, b.y, ta1, tb1);
+                            V ta1, tb1, dl1;
+                            const V q1 = pair_qt_fast<true>(P, a.x, a.y, a.z, a.w, b.x, b.y, w_lds[tb + t].y, ta1,
+                                                            tb1, dl1);
 #pragma unroll
                             for (int u = 0; u < kStatTile; ++u) {
                                 q[u] = (u == t) ? q1 : q[u];
@@ -923,7 +1023,7 @@ estep_stats_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
                     const bool in = t < cnt;
                     const float4 a = blk_lds[t][0];
                     const float4 b = blk_lds[t][1];
-                    const float w = w_lds[t];
+                    const float w = w_lds[t].x;
                     const bool dzero = (a.w == 0.0f && b.x == 0.0f && b.y == 0.0f);
                     const bool dif = b.w != 0.0f;
                     const float Se = dzero ? 0.0f : S;

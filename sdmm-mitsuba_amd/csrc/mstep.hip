@@ -189,6 +189,11 @@ __device__ static void pack_component(int k, int K, int Kp, const CanonDev& C, f
                 acc += (double)e[EP_L00 + row + j] * ((double)mu[j] - (double)kOrigin);
             e[EP_NC0 + m] = (float)(-acc);
         }
+        {
+            const double n2 = (double)to[6] * (double)to[6] + (double)to[7] * (double)to[7] +
+                              (double)to[8] * (double)to[8];
+            e[EP_CN] = (float)(0.5 * (1.0 - n2));
+        }
         g[GP_W] = w;
         g[GP_MU0] = mu[0]; g[GP_MU1] = mu[1]; g[GP_MU2] = mu[2];
         const float* ML = C.margL + 9 * k;

@@ -35,6 +35,9 @@ enum : int {
     // with o = kOrigin (the centre of the normalised scene box), so the
     // subtraction p - mu costs nothing per pair
     EP_NC0, EP_NC1, EP_NC2, EP_NC3, EP_NC4,
+    // (1 - |R2|^2) / 2 in fp64, rounded: the component half of the cancellation-free
+    // 1 + cos(theta) of the statistics kernels (estep.hip one_plus_c)
+    EP_CN,
     EP_FIELDS
 };
 constexpr float kOrigin = 0.5f;

@@ -4,7 +4,7 @@ from pathlib import Path
 import numpy as np
 import pytest
 
-from helpers import estep_f64
+from helpers import estep_f64, posterior_f64
 
 pytestmark = pytest.mark.gpu
 GOLDEN = Path(__file__).resolve().parent / "golden"
@@ -15,7 +15,7 @@ def _load(name):
 
 
 @pytest.mark.parametrize("K", [16, 128])
-def test_gpu_estep_vs_golden(pkg, gpu, K):
+def test_gpu_estep_vs_golden(pkg, gpu, plog, K):
     import torch
     g = _load(f"golden_estep_K{K}.npz")
     mix = pkg.SDMM(K)
@@ -28,15 +28,29 @@ def test_gpu_estep_vs_golden(pkg, gpu, K):
     resp = torch.empty((N, K), device=gpu)
     mix.posterior(ds, resp)
     got = resp.cpu().numpy()
+    # the golden responsibilities (fp32 oracle) and the GPU's, both judged by
+    # the fp64 evaluation of the same float parameters (test_gpu_parity._check_resp)
+    exact = posterior_f64(p, g["x"])
     live = (g["resp"].sum(1) > 0) & (got.sum(1) > 0)
-    assert np.abs(got[live] - g["resp"][live]).max() <= 1e-3
+    eg = np.abs(got[live] - exact[live]).max()
+    eo = np.abs(g["resp"][live] - exact[live]).max()
+    plog("golden_resp_abs_err_vs_fp64", eg, 4 * eo + 1e-5, golden_fp32_err=eo)
+    # and against the committed fixture itself: 1e-4 absolute (both evaluate the
+    # same float parameters in fp32; where the fp64 evaluation departs from both
+    # -- different FTZ flush points of tiny densities -- they still agree)
+    dg = np.abs(got[live] - g["resp"][live]).max()
+    plog("golden_resp_abs_diff_vs_golden", dg, 1e-4)
+    assert eg <= 4 * eo + 1e-5
+    assert dg <= 1e-4
     st = torch.zeros(pkg.stats_len(K), dtype=torch.float64, device=gpu)
     mix.estep_stats(ds, st)
     s = st.cpu().numpy()
     ex = g["stats_exact"]
     W, Wx = s[2:2 + K], ex[2:2 + K]
-    ef = np.abs(g["stats_faithful"][2:2 + K] - Wx).max()
-    assert np.abs(W - Wx).max() <= max(2 * ef, 1e-6 * ex[1])
+    ew = np.abs(W - Wx).max() / ex[1]
+    plog("golden_stats_W_rel_err_vs_exact", ew, 1e-6,
+         golden_fp32_err=np.abs(g["stats_faithful"][2:2 + K] - Wx).max() / ex[1])
+    assert ew <= 1e-6
     np.testing.assert_allclose(s[1], ex[1], rtol=1e-6)
 
 

@@ -7,9 +7,14 @@ Tolerances (stated here, see DESIGN.md "Parity"):
     for far samples (q ~ 1e3..1e5) is ~q*6e-8 in the exponent), and
     |gpu - oracle| <= 2e-5 on samples the mixture explains (max posterior of
     the fp64 evaluation found at q < 100);
-  * sufficient statistics: relative 2e-5 of each statistic's scale;
+  * sufficient statistics: within 1e-6 of the total weight of the fp64
+    evaluation of the same float parameters (the statistics kernels form
+    1 + cos(theta) without cancellation, estep.hip one_plus_c; the fp32
+    reference arithmetic is itself up to ~1e-5 away);
   * mixture parameters after EM iterations (north star): weights, means and
-    covariances within 1e-4 relative (covariances scaled by sqrt(S_ii S_jj));
+    covariances within 1e-4 relative of the exact EM (fp64 E-step of the float
+    parameters + the oracle's M-step; covariances scaled by sqrt(S_ii S_jj)) --
+    flat, whatever the fp32 reference's own distance (2e-4..3e-4 at K >= 128);
   * guided sampling: component indices BIT-EXACT; directions 1e-5, pdf 1e-4 rel.
 """
 import numpy as np
@@ -144,8 +149,8 @@ def test_stats_match_oracle(pkg, oracle, synth, gpu, plog, K, N, heuristic):
     np.testing.assert_allclose(got[1], exact[1], rtol=1e-6)      # weightSum: finite weights
     eg, eo = _stats_err(got, exact, K), _stats_err(ref, exact, K)
     print(f"K={K} N={N} h={heuristic}: stats err gpu {eg:.2e}  oracle-fp32 {eo:.2e}")
-    plog("stats_rel_err_vs_fp64", eg, 2 * eo + 2e-6, oracle_fp32_err=eo)
-    assert eg <= 2 * eo + 2e-6
+    plog("stats_rel_err_vs_fp64", eg, 1e-6, oracle_fp32_err=eo)
+    assert eg <= 1e-6
 
 
 def _exact_em(oracle, om, ost, b, iters):
@@ -167,13 +172,11 @@ def _param_err(p, q):
 @pytest.mark.parametrize("K,N,iters,heuristic", [(128, 16384, 5, False), (16, 8192, 6, True),
                                                  (256, 6000, 3, False), (512, 4096, 2, False)])
 def test_em_matches_oracle(pkg, oracle, synth, gpu, plog, K, N, iters, heuristic):
-    """StepwiseTangentEM::optimize x iters vs the exact (fp64 E-step) EM.
-    Bound at every step: max(1e-4, 2 x the fp32 oracle's own distance to
-    exact).  Where the fp32 reference arithmetic is well conditioned this is
-    the north-star 1e-4; samples near the antipode of a broad component make
-    the log map ill-conditioned in fp32 (theta/sin(theta) with sin ~ 1e-3
-    amplifies the rounding of to*d ~1e3-fold) and then both fp32 paths sit
-    ~1e-4..1e-3 from exact."""
+    """StepwiseTangentEM::optimize x iters vs the exact (fp64 E-step) EM: the
+    north-star 1e-4 at every step, flat.  (The fp32 oracle, evaluating the
+    reference's arithmetic, is logged beside it: near the antipode of a broad
+    component theta/sin(theta) amplifies the fp32 rounding of to*d, and the
+    reference itself sits 2e-4..3e-4 from exact at K >= 128.)"""
     b, mix, om, ost, ds, os_ = _setup(pkg, oracle, synth, K, N, heuristic=heuristic)
     n_pos = K // 8
     pos, nrm = synth.model_seed_points(b, K)
@@ -188,9 +191,8 @@ def test_em_matches_oracle(pkg, oracle, synth, gpu, plog, K, N, iters, heuristic
         x = {k: getattr(xm, k) for k in ("weights", "mean", "cov")}
         eg, eo = _param_err(p, x), _param_err(o, x)
         print(f"K={K} it={it + 1}: param err vs exact: gpu {eg:.2e}  oracle-fp32-E {eo:.2e}")
-        plog("em_param_rel_err_vs_exact", eg, max(RTOL_PARAMS, 2 * eo), iteration=it + 1, oracle_fp32_err=eo,
-             within_north_star=bool(eg <= RTOL_PARAMS))
-        assert eg <= max(RTOL_PARAMS, 2 * eo)
+        plog("em_param_rel_err_vs_exact", eg, RTOL_PARAMS, iteration=it + 1, oracle_fp32_err=eo)
+        assert eg <= RTOL_PARAMS
     st = mix.get_state()
     assert int(st["scalars"][3]) == iters
     np.testing.assert_allclose(p["normalization"], om.s.normalization, rtol=1e-5)
