@@ -481,8 +481,8 @@ __device__ __forceinline__ V angle_over_sin_main(V c) {
 // directional rows, and the main-path angle (RARE selects the quirk path).
 template <bool RARE>
 __device__ __forceinline__ V pair_q_tile(const V* __restrict__ P, float p0, float p1, float p2, float d0,
-                                         float d1, float d2) {
-    const V c = vfma(P[EP_R22], sp(d2), vfma(P[EP_R21], sp(d1), P[EP_R20] * d0));
+                                         float d1, float d2, V& c) {
+    c = vfma(P[EP_R22], sp(d2), vfma(P[EP_R21], sp(d1), P[EP_R20] * d0));
     const V a = RARE ? angle_over_sin_fast(c) : angle_over_sin_main(c);
     const V u0 = vfma(P[EP_L00], sp(p0), P[EP_NC0]);
     const V u1 = vfma(P[EP_L11], sp(p1), vfma(P[EP_L10], sp(p0), P[EP_NC1]));
@@ -584,7 +584,7 @@ estep_resp_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s
     // per wave: the staged sample block (x0 x1 x2 x3 | x4 x5 hpdf diffuse) and
     // the tile's normalisation scales
     __shared__ float4 sblk[WPB][64][2];
-    __shared__ float sg[WPB][KT];
+    __shared__ __attribute__((aligned(16))) float sg[WPB][KT];
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t wave = (int64_t)blockIdx.x * WPB + wid;
@@ -623,8 +623,8 @@ estep_resp_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s
             for (int t = 0; t < KT; ++t) {
                 const float4 a = blk_lds[tb + t][0];
                 const float4 b = blk_lds[tb + t][1];
-                q[t] = pair_q_tile<false>(P, a.x, a.y, a.z, a.w, b.x, b.y);
-                const V c = vfma(P[EP_R22], sp(b.y), vfma(P[EP_R21], sp(b.x), P[EP_R20] * a.w));
+                V c;
+                q[t] = pair_q_tile<false>(P, a.x, a.y, a.z, a.w, b.x, b.y, c);
                 cbits = __builtin_elementwise_max(cbits, __builtin_elementwise_max(__builtin_bit_cast(uint32_t, c.x),
                                                                                    __builtin_bit_cast(uint32_t, c.y)));
                 // keep the scheduler from hoisting every sample's LDS reads
@@ -645,7 +645,8 @@ estep_resp_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s
                     for (int t = 0; t < KT; ++t) {
                         const float4 a = blk_lds[tb + t][0];
                         const float4 b = blk_lds[tb + t][1];
-                        const V qt = pair_q_tile<true>(P, a.x, a.y, a.z, a.w, b.x, b.y);
+                        V c;
+                        const V qt = pair_q_tile<true>(P, a.x, a.y, a.z, a.w, b.x, b.y, c);
 #pragma unroll
                         for (int u = 0; u < KT; ++u) q[u] = (u == t) ? qt : q[u];
                     }
@@ -672,17 +673,30 @@ estep_resp_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s
             // a non-finite sum means a non-finite q (NaN input): zero by select
             const bool bad = __builtin_amdgcn_ballot_w64(!__builtin_isfinite(S)) != 0;
             const int tcnt = (cnt - tb < KT) ? cnt - tb : KT;
+            float* row0 = resp + (blk + tb) * (int64_t)K + kbase;
+            if (tcnt == KT && !bad && K == Kp) {
+                // the common tile: straight-line stores, the scales read four at a time
 #pragma unroll
-            for (int t = 0; t < KT; ++t) {
-                if (t >= tcnt) break;
-                const float g = g_lds[t];
-                V o = q[t] * g;
-                if (bad) o = (g != 0.0f) ? o : sp(0.0f);
-                float* row = resp + (blk + tb + t) * (int64_t)K + kbase;
-                if (full) {
-                    __builtin_nontemporal_store(o, (V*)row);
-                } else {
-                    if (kbase < K) __builtin_nontemporal_store(o.x, row);
+                for (int t = 0; t < KT; t += 4) {
+                    const float4 g4 = *(const float4*)&g_lds[t];
+                    __builtin_nontemporal_store(q[t] * g4.x, (V*)(row0 + (int64_t)t * K));
+                    __builtin_nontemporal_store(q[t + 1] * g4.y, (V*)(row0 + (int64_t)(t + 1) * K));
+                    __builtin_nontemporal_store(q[t + 2] * g4.z, (V*)(row0 + (int64_t)(t + 2) * K));
+                    __builtin_nontemporal_store(q[t + 3] * g4.w, (V*)(row0 + (int64_t)(t + 3) * K));
+                }
+            } else {
+#pragma unroll
+                for (int t = 0; t < KT; ++t) {
+                    if (t >= tcnt) break;
+                    const float g = g_lds[t];
+                    V o = q[t] * g;
+                    if (bad) o = (g != 0.0f) ? o : sp(0.0f);
+                    float* row = row0 + (int64_t)t * K;
+                    if (full) {
+                        __builtin_nontemporal_store(o, (V*)row);
+                    } else {
+                        if (kbase < K) __builtin_nontemporal_store(o.x, row);
+                    }
                 }
             }
         }
