@@ -937,7 +937,16 @@ __device__ __forceinline__ float transpose_sum4(const float (&v)[kStatTile], int
     return x;
 }
 
-template <int WPB, int OCC>
+// GROUP = false: each of the WPB waves walks its own sample chunk against all
+// K <= 128 components (one packed pair per lane).  GROUP = true (128 < K <=
+// 128 WPB: Pool K = 256 with WPB = 2, Kitchen K = 512 with WPB = 4): the waves
+// of a workgroup walk the SAME chunk, wave w holding components 128 w ..
+// 128 w + 127 -- the K = 128 register budget per lane at any K (round 1 kept
+// 4 / 8 components per lane: 265 / 512 VGPRs with spills, one wave per SIMD).
+// Per 4-sample tile each wave's partial normaliser goes through LDS and one
+// workgroup barrier; every wave then sums the partials in wave order.  The
+// waves' component ranges are disjoint, so the partial row needs no fold.
+template <int WPB, int OCC, bool GROUP = false>
 __global__ void __launch_bounds__(64 * WPB, OCC)
 estep_stats_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, int64_t n,
                         int64_t chunk, float* __restrict__ partials, int pstride,
@@ -957,14 +966,16 @@ estep_stats_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
     __shared__ float4 sblk[WPB][64][2];      // x0 x1 x2 x3 | x4 x5 hpdf diffuse
     __shared__ float2 sw[WPB][64];           // weight, half_defect of the direction
     __shared__ float4 sg[WPB][kStatTile];    // {gamma scale, weight, threshold, -}
+    __shared__ float spart[2][WPB][kStatTile];   // GROUP: per-wave partial normalisers (tile parity)
     extern __shared__ __attribute__((aligned(16))) float red[];
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t wave = bid * WPB + wid;
+    const int64_t wave = GROUP ? bid : bid * WPB + wid;
     const int64_t s0 = wave * chunk;
     const int64_t s1 = (s0 + chunk < n) ? s0 + chunk : n;   // s1 <= s0: no samples
 
-    const int kbase = 2 * lane;
+    const int kbase = (GROUP ? 128 * wid : 0) + 2 * lane;
+    int parity = 0;
     V P[EP_FIELDS];
 #pragma unroll
     for (int f = 0; f < EP_FIELDS; ++f) P[f] = *(const V*)(ep + f * Kp + kbase);
@@ -1028,7 +1039,16 @@ estep_stats_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
                 float ps[kStatTile];
 #pragma unroll
                 for (int t = 0; t < kStatTile; ++t) ps[t] = q[t].x + q[t].y;
-                const float S = transpose_sum4(ps, lane);
+                float S = transpose_sum4(ps, lane);
+                if constexpr (GROUP) {
+                    // the workgroup's partial sums of sample tb + (lane & 3), in wave order
+                    if (lane < kStatTile) spart[parity][wid][lane] = S;
+                    __syncthreads();
+                    S = spart[parity][0][lane & 3];
+#pragma unroll
+                    for (int w = 1; w < WPB; ++w) S += spart[parity][w][lane & 3];
+                    parity ^= 1;
+                }
                 {
                     // posteriorAndLog normalisation (mixture_model.h:170-191) and the
                     // weight guards of calculateStats / sumWeights (:288-293, :462-475)
@@ -1050,8 +1070,12 @@ estep_stats_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
                     const float hpost = (fin && dif) ? kHeuristicWeight * b.z * inv : 0.0f;
                     const float weff = use ? w : 0.0f;
                     if (lane < kStatTile) {
-                        accWs += (in && finite_w) ? w : 0.0f;
-                        accH = fmaf(weff, hpost, accH);
+                        // (GROUP: every wave sees the same samples; H and sumWeights
+                        // are counted by wave 0's lanes only)
+                        if (!GROUP || wid == 0) {
+                            accWs += (in && finite_w) ? w : 0.0f;
+                            accH = fmaf(weff, hpost, accH);
+                        }
                         // gamma < 1e-10 is skipped (:312); nothing passes when 1/S' is
                         // not finite (posterior zeroed, mixture_model.h:182-191)
                         g_lds[lane] = float4{g, weff, (fin && !dzero) ? 1e-10f : __builtin_inff(), 0.0f};
@@ -1099,14 +1123,15 @@ estep_stats_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
         accH += __shfl_xor(accH, off);
         accWs += __shfl_xor(accWs, off);
     }
-    // fold the workgroup's waves in a fixed order through LDS
+    // fold the workgroup's waves in a fixed order through LDS (GROUP: the
+    // waves' component ranges are disjoint, each writes its own)
     const int rowlen = ST_FIELDS * Kp + 2;
     for (int w = 0; w < WPB; ++w) {
         if (wid == w) {
 #pragma unroll
             for (int f = 0; f < ST_FIELDS; ++f) {
                 V* dst = (V*)&red[f * Kp + kbase];
-                *dst = (w == 0) ? acc[f] : *dst + acc[f];
+                *dst = (w == 0 || GROUP) ? acc[f] : *dst + acc[f];
             }
             if (lane == 0) {
                 red[ST_FIELDS * Kp] = (w == 0) ? accH : red[ST_FIELDS * Kp] + accH;
@@ -1355,19 +1380,34 @@ const char* estep_resp_tile_name(int variant) {
 hipError_t launch_estep_stats_tile(int variant, const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
                                    int64_t chunk, int blocks, float* partials, int pstride, hipStream_t st,
                                    const LeafDesc* leaves, const int2* items) {
-    if (Kp != 128 || K <= 64 || K > 128) return hipErrorInvalidValue;
     const size_t lds = sizeof(float) * (size_t)(ST_FIELDS * Kp + 2);
-    if (variant == 1)
-        hipLaunchKernelGGL((estep_stats_tile_kernel<4, 3>), dim3(blocks), dim3(256), lds, st, ep, Kp, K, s, n,
+    if (Kp == 128 && K > 64 && K <= 128) {
+        if (variant == 1)
+            hipLaunchKernelGGL((estep_stats_tile_kernel<4, 3>), dim3(blocks), dim3(256), lds, st, ep, Kp, K, s, n,
+                               chunk, partials, pstride, leaves, items);
+        else
+            hipLaunchKernelGGL((estep_stats_tile_kernel<4, 2>), dim3(blocks), dim3(256), lds, st, ep, Kp, K, s, n,
+                               chunk, partials, pstride, leaves, items);
+    } else if (Kp == 256 && K > 128 && K <= 256) {
+        hipLaunchKernelGGL((estep_stats_tile_kernel<2, 2, true>), dim3(blocks), dim3(128), lds, st, ep, Kp, K, s, n,
                            chunk, partials, pstride, leaves, items);
-    else
-        hipLaunchKernelGGL((estep_stats_tile_kernel<4, 2>), dim3(blocks), dim3(256), lds, st, ep, Kp, K, s, n,
+    } else if (Kp == 512 && K > 256 && K <= 512) {
+        hipLaunchKernelGGL((estep_stats_tile_kernel<4, 2, true>), dim3(blocks), dim3(256), lds, st, ep, Kp, K, s, n,
                            chunk, partials, pstride, leaves, items);
+    } else {
+        return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
-
+// resident workgroups per CU; *waves_per_wg: the waves of one (GROUP: one chunk)
 hipError_t estep_stats_tile_occupancy(int variant, int Kp, int* blocks_per_cu) {
     const size_t lds = sizeof(float) * (size_t)(ST_FIELDS * Kp + 2);
+    if (Kp == 256)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            blocks_per_cu, reinterpret_cast<const void*>(&estep_stats_tile_kernel<2, 2, true>), 128, lds);
+    if (Kp == 512)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            blocks_per_cu, reinterpret_cast<const void*>(&estep_stats_tile_kernel<4, 2, true>), 256, lds);
     const void* f = variant == 1 ? reinterpret_cast<const void*>(&estep_stats_tile_kernel<4, 3>)
                                  : reinterpret_cast<const void*>(&estep_stats_tile_kernel<4, 2>);
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, 256, lds);

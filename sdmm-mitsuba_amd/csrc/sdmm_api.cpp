@@ -225,6 +225,7 @@ struct sdmm_mix {
                                              // 2: estep_resp_mfma_kernel (every K)
     int rvariant = 4;                        // tile kernel variant (SDMM_RESP_VARIANT): KT=8, 3 waves/SIMD
     int stile = 0;                           // 1: estep_stats_tile_kernel (64 < K <= 128)
+                                             // 2: its GROUP form (128 < K <= 512: Kp / 128 waves per chunk)
     int svariant = 0;                        // its occupancy variant (SDMM_STATS_VARIANT)
     int device = 0;
     int cus = 256;
@@ -447,6 +448,16 @@ struct StatsPlan {
     int blocks;
 };
 StatsPlan stats_plan(const sdmm_mix* m, int64_t n) {
+    if (m->stile == 2) {
+        // GROUP form: a workgroup (Kp / 128 waves) per chunk; one round of
+        // resident workgroups, chunks of whole 64-sample blocks
+        const int64_t resident = (int64_t)m->cus * (m->stats_blocks > 0 ? m->stats_blocks : 1);
+        int64_t chunk = (n + resident - 1) / resident;
+        chunk = ((chunk + 63) / 64) * 64;
+        if (chunk < 64) chunk = 64;
+        const int64_t blocks = (n + chunk - 1) / chunk;
+        return StatsPlan{chunk, (int)(blocks > 0 ? blocks : 1)};
+    }
     if (m->stile) {
         // one round of resident waves, each a whole number of 64-sample blocks
         const int64_t resident = (int64_t)m->cus * 4 * (m->stats_blocks > 0 ? m->stats_blocks : 1);
@@ -543,6 +554,7 @@ int sdmm_create(int K, const sdmm_em_params* params, int device, sdmm_mix** out)
         if (vv) m->rvariant = std::atoi(vv);
         const char* sv = std::getenv("SDMM_STATS_KERNEL");
         if (K > 64 && K <= 128 && !(sv && std::strcmp(sv, "legacy") == 0)) m->stile = 1;
+        if (K > 128 && K <= 512 && !(sv && std::strcmp(sv, "legacy") == 0)) m->stile = 2;
         const char* svv = std::getenv("SDMM_STATS_VARIANT");
         if (svv) m->svariant = std::atoi(svv);
     }
@@ -685,7 +697,9 @@ const char* sdmm_kernel_name(const sdmm_mix* m, int which) {
         std::snprintf(buf, sizeof buf, "estep_resp_kernel<%d,%d>", m->rcpl, m->rlps);
         return buf;
     }
-    if (m->stile)
+    if (m->stile == 2)
+        std::snprintf(buf, sizeof buf, "estep_stats_tile_kernel<%d,2,true>", m->Kp / 128);
+    else if (m->stile)
         std::snprintf(buf, sizeof buf, "estep_stats_tile_kernel<4,%d>", m->svariant == 1 ? 3 : 2);
     else
         std::snprintf(buf, sizeof buf, "estep_stats_kernel<%d,%d>", m->cpl, m->lps);

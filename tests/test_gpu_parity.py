@@ -444,3 +444,43 @@ def test_guide_coherent_order_identical(pkg, oracle, synth, gpu, K):
     sub = np.r_[0:7, 8:6000]
     dr, pr, cr, sr = oracle.guide_batch(om, c[:, sub].T, u[:, sub].T)
     np.testing.assert_array_equal(outs[0][2][sub], cr)
+
+
+def test_mstep_pd_kill_matches_oracle(pkg, oracle, synth, gpu, plog):
+    """The M-step kills a component whose covariance is not positive definite
+    (stepwise_tangent.h:945-960) by jmm::isPositiveDefinite -- all eigenvalues
+    > 0 (opt/util.h:29-41).  Near-singular covariances (smallest eigenvalue
+    +-1e-12 .. 1e-17 relative, where rounding decides) are killed identically by
+    the GPU (Jacobi, mstep.hip pd_jacobi_d) and the oracle (is_pd_f64), fed the
+    same statistics; a Cholesky success test would not agree on all of them."""
+    import torch
+    K = 16
+    b, mix, om, ost, ds, os_ = _setup(pkg, oracle, synth, K, 256)
+    st = mix.get_state()
+    st["bpriors"][:] = 0.0                     # no priors: cov = the statistics' own
+    st["bdepth"][:] = 0.0
+    mix.set_state(st)
+    ost.bPriors[:] = 0.0
+    ost.bDepth[:] = 0.0
+    lams = [1e-3, 1e-12, 1e-14, 1e-15, 1e-16, 3e-17, 1e-17, 0.0,
+            -1e-17, -3e-17, -1e-16, -1e-15, -1e-14, -1e-12, -1e-3, 2e-16]
+    rng = np.random.default_rng(5)
+    W = np.ones(K)
+    Cf = np.zeros((K, 5, 5))
+    for k in range(K):
+        Q, _ = np.linalg.qr(rng.normal(size=(5, 5)))
+        D = Q @ np.diag([1.0, 0.5, 0.25, 0.125, lams[k]]) @ Q.T * 1e-2
+        Cf[k] = (D + D.T) / 2
+    full = np.concatenate([[0.0, float(W.sum())], W, np.zeros(5 * K), Cf.reshape(-1)])
+    low = np.concatenate([[0.0, float(W.sum())], W, np.zeros(5 * K),
+                          np.stack([Cf[:, i, j] for i in range(5) for j in range(i + 1)], 1).reshape(-1)])
+    stats = torch.from_numpy(low).to(gpu)
+    mix.mstep(stats, 256)
+    p = mix.get_params()
+    assert oracle.mstep(om, ost, full, 256, accurate=True) == 1
+    killed_g = p["weights"] == 0
+    killed_o = om.weights == 0
+    plog("mstep_pd_kill_mismatches", int((killed_g != killed_o).sum()), 0, kills=int(killed_o.sum()))
+    np.testing.assert_array_equal(killed_g, killed_o)
+    assert not killed_o[0] and killed_o[14]          # clearly PD kept, clearly indefinite killed
+    np.testing.assert_array_equal(p["valid"][~killed_o], om.valid[~killed_o])
