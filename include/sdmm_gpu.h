@@ -366,6 +366,16 @@ int sdmm_guide_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t
                          int32_t* node_out);
 int sdmm_pdf_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
                        const float* const d[3], float* pdf);
+/* One guided bounce of a whole wavefront, sampleSurface + pdfSurface with the
+ * plugin's BSDF/guide mixing (sdmm_proc.cpp:383-421, :474-502): the per-query
+ * conditional is built ONCE; query q then either samples it (pdf_mode[q] == 0:
+ * d, pdf, comp exactly as sdmm_guide_wavefront) or evaluates its gmmPdf at the
+ * BSDF-sampled direction dgiven[q] (pdf_mode[q] != 0: pdf exactly as
+ * sdmm_pdf_wavefront, d[q] = dgiven[q], comp[q] = -2 when the conditional is
+ * valid, -1 when not -- the reference's validConditional, :368-392). */
+int sdmm_guide_pdf_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
+                             const float* const u[3], const float* const dgiven[3], const uint8_t* pdf_mode,
+                             float* const d[3], float* pdf, int32_t* comp, int32_t* node_out);
 
 /* Checkpoints (.asdmm, JSON; schema in DESIGN.md section 9).
  *   sdmm_save_json      the accelerator: sdmm::save_json(m_accelerator, path),
@@ -393,8 +403,176 @@ int sdmm_load_json(const char* path, int device, sdmm_stree** tree_out, sdmm_mix
 int sdmm_mix_save_json(const sdmm_mix* m, const char* path);
 int sdmm_mix_load_json(const char* path, int device, sdmm_mix** out);
 int sdmm_get_em_params(const sdmm_mix* m, sdmm_em_params* p);
+/* A new handle holding a copy of m's mixture and stepwise EM state (device to
+ * device, on m's stream; the new handle uses m's stream) -- a split leaf's
+ * children start from their parent's distribution and optimizer (jmm
+ * SNTree::createChildNode, sntree.h:172-205). */
+int sdmm_clone(const sdmm_mix* m, sdmm_mix** out);
 int sdmm_restore_params(sdmm_mix* m, const sdmm_params_out* in);
 int sdmm_stree_set_nodes(sdmm_stree* t, int n, const float* aabb, const int32_t* child, const int32_t* axis);
+
+/* ---- Guided path tracing on the device (SDMMRenderer::Li) ----------------
+ * An analytic scene of parallelograms (Mitsuba rectangles; a cube is six) with
+ * diffuse BSDFs and one-sided area emitters, rendered by a wavefront path
+ * tracer whose every bounce goes through sdmm_guide_pdf_wavefront -- the
+ * plugin's per-bounce sampleSurface / pdfSurface (sdmm_proc.cpp:275-590,
+ * :592-871) on the device.  The Cornell Box of the test suite
+ * (test-suite/scenes/cornell-box/cornell-box.xml:75-143) is this kind of
+ * scene (sdmm-mitsuba_amd/scenes.py).
+ *
+ *   sdmm_scene_create   quads: 9 floats each (corner, edge1, edge2, world);
+ *                       normal = normalize(edge1 x edge2), negated where
+ *                       flip_normals[q] (nullable); bsdf[q] indexes
+ *                       reflectance (3 per BSDF); emitter[q] (nullable, -1 =
+ *                       none) indexes radiance (3 per emitter, Le on the
+ *                       normal side); camera_to_world row major 4x4 (Mitsuba's
+ *                       toWorld, camera looks along +z), fov along x.
+ *   sdmm_scene_normalization  render() (volpath_sdmm.cpp:375-393): the scene
+ *                       AABB without the camera gives scene_min and
+ *                       spatial_norm = its largest extent (scene_norm.json),
+ *                       the tree box = [0, extent / norm] -+ 1e-5 (getAABB).
+ *   sdmm_li_render      spp samples for pixels [pixel_begin, pixel_end) (row
+ *                       major), one path per sample; image (device, 3 planes
+ *                       of width * height floats) receives each pixel's mean
+ *                       radiance.  guided = 0: BSDF sampling only (iteration
+ *                       0, :311-323); otherwise every bounce queries the
+ *                       leaves' mixtures (node_mix, or the table bound to t)
+ *                       with the BSDF/guide choice of probability
+ *                       bsdf_fraction (0.5, :383).  Conditions are
+ *                       (p - scene_min) / spatial_norm (createCondition,
+ *                       :263-273).  Runs on the tree's stream.  The saved
+ *                       vertices (Li's Vertex records, :606-637, :815-846)
+ *                       stay in the scene's buffers; *vertices_out (nullable)
+ *                       points at them until the next sdmm_li_render.
+ * Random numbers are counter based: sample (path, stream, dimension) of a
+ * path are fixed, whatever runs beside it (render_device.h). */
+typedef struct sdmm_scene sdmm_scene;
+typedef struct {
+    int n_quads;
+    const float* quads;
+    const int32_t* flip_normals;
+    const int32_t* bsdf;
+    int n_bsdfs;
+    const float* reflectance;
+    const int32_t* emitter;
+    int n_emitters;
+    const float* radiance;
+    float camera_to_world[16];
+    float fov_x_deg;
+    float near_clip;
+    int width, height;
+} sdmm_scene_desc;
+typedef struct {
+    int spp;
+    int max_depth;            /* maxDepth (:649, :684), -1 = unbounded (capped by the vertex slots) */
+    int rr_depth;             /* rrDepth (:858) */
+    int guided;
+    float bsdf_fraction;      /* heuristicConditionalWeight (0.5) */
+    int saved_vertices;       /* vertex slots per path (>= max_depth - 1; the reference's array holds 10) */
+    uint64_t seed;
+    int64_t pixel_begin, pixel_end;
+} sdmm_li_params;
+/* Vertex records of the last render (device): field f of vertex v of path p
+ * at rec[(f * max_vertices + v) * n_paths + p]; f: 0-2 weight (RGB), 3-5
+ * throughput, 6 clamped sampling pdf, 7-12 point (condition, world
+ * direction), 13-15 normal; nv[p] vertices per path; path p's global index
+ * (the RNG's path counter) is path0 + p. */
+typedef struct {
+    int64_t n_paths;
+    int max_vertices;
+    int64_t path0;
+    const float* rec;
+    const int32_t* nv;
+} sdmm_path_vertices;
+typedef struct {
+    int64_t paths;      /* paths started (pixels x spp) */
+    int64_t segments;   /* bounce rays traced after the camera rays (= saved vertices) */
+} sdmm_li_stats;
+int sdmm_scene_create(const sdmm_scene_desc* desc, int device, sdmm_scene** out);
+void sdmm_scene_destroy(sdmm_scene* s);
+int sdmm_scene_normalization(const sdmm_scene* s, float scene_min[3], float* spatial_norm, float tree_min[3],
+                             float tree_max[3]);
+int sdmm_li_render(sdmm_scene* s, sdmm_stree* t, const sdmm_mix* const* node_mix, const sdmm_li_params* p,
+                   float* image, sdmm_path_vertices* vertices_out, sdmm_li_stats* stats);
+
+/* Training-data producer: the tail of Li (sdmm_proc.cpp:876-965) for a batch
+ * of paths' saved vertices.  Per path, vertices nv-1 down to
+ * max(nv - saved_per_path, 0): the vertex's leaf (STree.find with its box,
+ * :921-930) gets (point, normal, average weight) plus a stats entry when the
+ * average is finite (push_back_data, :880-914); then 1 (last vertex) + 1
+ * (average > 1000) jittered copies go to the leaf at point + (u - 1/2) x leaf
+ * diagonal, a draw outside the tree or in the same leaf retried while fewer
+ * than 8 draws failed (:932-964); u from stream 1024 + vertex of the path's
+ * counter RNG under `seed`.  Output (device planes, capacity records): the
+ * records in leaf order, a leaf's records in (path, push) order; node = leaf
+ * id, source = p * max_vertices + v, stats = 1 for the vertex's own leaf.
+ * *n_out = number of records (also when it exceeds capacity: then nothing is
+ * written and SDMM_E_INVALID is returned; out NULL: count only); seg (host, nullable,
+ * num_nodes + 1): leaf v's records are [seg[v], seg[v+1]).  lost (nullable):
+ * vertices outside the tree (the reference throws).  Synchronous. */
+typedef struct {
+    float* x[6];
+    float* normal[3];        /* nullable (all three) */
+    float* w;
+    uint8_t* stats;          /* nullable */
+    int32_t* node;           /* nullable */
+    int64_t* source;         /* nullable */
+    int64_t capacity;
+} sdmm_training_out;
+int sdmm_push_training(sdmm_stree* t, const sdmm_path_vertices* v, int saved_per_path, uint64_t seed,
+                       const sdmm_training_out* out, int64_t* n_out, int64_t* seg, int64_t* lost);
+
+/* ---- The plugin's guiding model (SDMMVolumetricPathTracer) ----------------
+ * volpath_sdmm.cpp:132-312, :411-507 on the device: the accelerator tree
+ * (split_to_depth(split_depth) at creation, :398), one SDMM + EM state per
+ * trained leaf, the leaves' training data and the per-iteration schedule.
+ *   sdmm_guiding_push      Li's tail for a render pass (sdmm_push_training):
+ *                          records appended to the leaves' data, own-leaf
+ *                          positions to their stats (:894-902)
+ *   sdmm_guiding_optimize  optimize() (:244-312): split every leaf by its stats
+ *                          (split_leaf_recurse(threshold) under the leaf cap,
+ *                          :253-259; a split leaf's data, stats and mixture go
+ *                          to its new leaves -- jmm sntree.h:172-205), then per
+ *                          leaf canBeOptimized (:140-149, with m_totalSpp of the
+ *                          previous passes), initializeSDMMContext on first use
+ *                          (K/8 positions = the leaf's first records, spatial
+ *                          distance 3 hmax(diagonal) / (K/8), :132-138, :291),
+ *                          2 EM iterations while iterations_run < 4 else 1
+ *                          (:299-305) as ONE batched launch, the optimised
+ *                          leaves' data cleared (:308-309); the trained leaves
+ *                          are bound to the tree for the next pass.  spp: the
+ *                          pass's samples per pixel (m_totalSpp += spp after).
+ *   sdmm_guiding_iteration one pass of render()'s loop (:411-507): sdmm_li_render
+ *                          (guided once a leaf is trained, :311-316), then
+ *                          push + optimize when train (m_still_training).
+ * Everything runs on the model's stream (= its tree's); calls return when
+ * the host-side state is updated. */
+typedef struct sdmm_guiding sdmm_guiding;
+typedef struct {
+    int K;                  /* components per leaf (16, SDMMProcess::NComponents) */
+    int split_depth;        /* 2 */
+    int split_threshold;    /* 4000 */
+    int max_leaf_nodes;     /* 2048 */
+    int saved_per_path;     /* 8 */
+    float depth_prior;      /* 0.01 (sdmm-lib initialize is absent: jmm uniformHemisphereInit's) */
+    uint64_t init_seed;     /* leaf v's hemisphere init seed = init_seed + v */
+} sdmm_guiding_config;
+typedef struct {
+    int leaves;             /* leaf_nodes() after the split */
+    int optimized;          /* leaves stepped this call */
+    int64_t records;        /* pool records before the optimised leaves' were dropped */
+} sdmm_guiding_stats;
+void sdmm_guiding_config_default(sdmm_guiding_config* c);
+int sdmm_guiding_create(const float tree_min[3], const float tree_max[3], const sdmm_guiding_config* cfg,
+                        int device, sdmm_guiding** out);
+void sdmm_guiding_destroy(sdmm_guiding* g);
+sdmm_stree* sdmm_guiding_tree(sdmm_guiding* g);
+int sdmm_guiding_node_mixtures(const sdmm_guiding* g, const sdmm_mix** out, int cap);
+int sdmm_guiding_trained(const sdmm_guiding* g);
+int sdmm_guiding_push(sdmm_guiding* g, const sdmm_path_vertices* v, uint64_t seed);
+int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out);
+int sdmm_guiding_iteration(sdmm_guiding* g, sdmm_scene* scene, const sdmm_li_params* p, uint64_t push_seed,
+                           int train, float* image, sdmm_li_stats* li_stats, sdmm_guiding_stats* out);
 
 const char* sdmm_last_error(void);
 int sdmm_abi_version(void);

@@ -375,3 +375,37 @@ def stree_find(aabb, child, pts):
     for i, q in enumerate(np.ascontiguousarray(pts, np.float32)):
         out[i] = f(_fp(mn), _fp(mx), ch.ctypes.data_as(C.c_void_p), _fp(q))
     return out
+
+
+def rng_uniform(seed, path, stream, dim):
+    """The library's counter-based uniform (render_device.h), restated in C."""
+    f = lib().or_rng_uniform
+    f.restype = C.c_float
+    f.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32]
+    return f(seed, path, stream, dim)
+
+
+def push_training(aabb, child, rec, nv, V, path0, saved, seed):
+    """Host-routed training records of Li's tail (sdmm_proc.cpp:876-965) in
+    (path, push) order: dict node, source, stats, w (+ lost)."""
+    mn = np.ascontiguousarray(aabb[:, :3].reshape(-1), np.float32)
+    mx = np.ascontiguousarray(aabb[:, 3:].reshape(-1), np.float32)
+    ch = np.ascontiguousarray(child.reshape(-1), np.int32)
+    rec = np.ascontiguousarray(rec, np.float32)
+    nv = np.ascontiguousarray(nv, np.int32)
+    P = int(nv.shape[0])
+    cap = int(nv.sum()) * 3 + 1
+    node = np.empty(cap, np.int32)
+    src = np.empty(cap, np.int64)
+    st = np.empty(cap, np.uint8)
+    w = np.empty(cap, np.float32)
+    lost = C.c_int64(0)
+    f = lib().or_push_training
+    f.restype = C.c_int64
+    n = f(_fp(mn), _fp(mx), ch.ctypes.data_as(C.c_void_p), _fp(rec), nv.ctypes.data_as(C.c_void_p),
+          C.c_int64(P), C.c_int(V), C.c_int64(path0), C.c_int(saved), C.c_uint64(seed),
+          node.ctypes.data_as(C.c_void_p), src.ctypes.data_as(C.c_void_p), st.ctypes.data_as(C.c_void_p),
+          _fp(w), C.c_int64(cap), C.byref(lost))
+    assert n <= cap
+    return {"node": node[:n].copy(), "source": src[:n].copy(), "stats": st[:n].copy(), "w": w[:n].copy(),
+            "lost": int(lost.value)}

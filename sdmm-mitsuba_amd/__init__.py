@@ -150,6 +150,28 @@ def lib():
         L.sdmm_stree_leaf_nodes.argtypes = [C.c_void_p]
         L.sdmm_stree_split_leaf_recurse.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_int]
         L.sdmm_stree_split_leaves.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int]
+        L.sdmm_guide_pdf_wavefront.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p * 3, C.c_void_p * 3,
+                                               C.c_void_p * 3, C.c_void_p, C.c_void_p * 3, C.c_void_p, C.c_void_p,
+                                               C.c_void_p]
+        L.sdmm_clone.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
+        L.sdmm_guiding_config_default.argtypes = [C.c_void_p]
+        L.sdmm_guiding_create.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
+        L.sdmm_guiding_destroy.argtypes = [C.c_void_p]
+        L.sdmm_guiding_tree.argtypes = [C.c_void_p]
+        L.sdmm_guiding_tree.restype = C.c_void_p
+        L.sdmm_guiding_node_mixtures.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        L.sdmm_guiding_trained.argtypes = [C.c_void_p]
+        L.sdmm_guiding_push.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        L.sdmm_guiding_optimize.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        L.sdmm_guiding_iteration.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p,
+                                             C.c_void_p, C.c_void_p]
+        L.sdmm_scene_create.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
+        L.sdmm_scene_destroy.argtypes = [C.c_void_p]
+        L.sdmm_scene_normalization.argtypes = [C.c_void_p] + [C.c_void_p] * 4
+        L.sdmm_li_render.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                     C.c_void_p]
+        L.sdmm_push_training.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_uint64, C.c_void_p,
+                                         C.POINTER(C.c_int64), C.c_void_p, C.POINTER(C.c_int64)]
         _lib = L
     return _lib
 
@@ -184,6 +206,11 @@ EXPORTED_SYMBOLS = [
     "sdmm_comm_size", "sdmm_comm_allreduce_f64", "sdmm_em_step_sharded", "sdmm_em_step_batched_sharded",
     "sdmm_em_step_batched_iters", "sdmm_mix_broadcast",
     "sdmm_stree_leaf_nodes", "sdmm_stree_split_leaf_recurse", "sdmm_stree_split_leaves",
+    "sdmm_guide_pdf_wavefront", "sdmm_scene_create", "sdmm_scene_destroy", "sdmm_scene_normalization",
+    "sdmm_li_render", "sdmm_push_training", "sdmm_clone",
+    "sdmm_guiding_config_default", "sdmm_guiding_create", "sdmm_guiding_destroy", "sdmm_guiding_tree",
+    "sdmm_guiding_node_mixtures", "sdmm_guiding_trained", "sdmm_guiding_push", "sdmm_guiding_optimize",
+    "sdmm_guiding_iteration",
 ]
 
 
@@ -429,8 +456,19 @@ class SDMM:
 
     def close(self):
         if getattr(self, "h", None):
-            lib().sdmm_destroy(self.h)
+            if getattr(self, "_owned", True):
+                lib().sdmm_destroy(self.h)
             self.h = None
+
+    @classmethod
+    def _borrow(cls, h, owner) -> "SDMM":
+        """A non-owning view of a handle that `owner` keeps alive (its stream untouched)."""
+        self = cls.__new__(cls)
+        self.h = C.c_void_p(h)
+        self._owned = False
+        self._owner = owner
+        self.K = int(lib().sdmm_num_components(self.h))
+        return self
 
     def __del__(self):
         try:
@@ -521,6 +559,12 @@ class SDMM:
         else:
             self.set_stream(stream)
         return self
+
+    def clone(self) -> "SDMM":
+        """A copy of this mixture and its stepwise EM state (sdmm_clone)."""
+        h = C.c_void_p()
+        _check(lib().sdmm_clone(self.h, C.byref(h)))
+        return SDMM._adopt(h, self.stream_ptr or None)
 
     def em_params(self) -> dict:
         p = _EmParams()
@@ -697,9 +741,9 @@ class STree:
             self.set_stream(stream)
 
     def __del__(self):
-        if getattr(self, "h", None) and _lib is not None:
+        if getattr(self, "h", None) and _lib is not None and getattr(self, "_owned", True):
             _lib.sdmm_stree_destroy(self.h)
-            self.h = None
+        self.h = None
 
     def set_nodes(self, aabb, child, axis):
         """Replace the node table (the layout nodes() returns)."""
@@ -849,3 +893,240 @@ class STree:
         dd = (C.c_void_p * 3)(*[t.data_ptr() for t in d])
         _check(lib().sdmm_pdf_wavefront(self.h, tab, nq, cc, dd, out.data_ptr()))
         return out
+
+    def guide_pdf(self, node_mix, c, u, dgiven, pdf_mode, node_out=None):
+        """One mixed bounce (sdmm_guide_pdf_wavefront): query q samples its
+        conditional (pdf_mode[q] == 0) or evaluates its gmmPdf at dgiven[q]."""
+        import torch
+        nq = c[0].numel()
+        tab = self._node_table(node_mix)
+        dev = c[0].device
+        d = [torch.empty(nq, device=dev) for _ in range(3)]
+        pdf = torch.empty(nq, device=dev)
+        comp = torch.empty(nq, device=dev, dtype=torch.int32)
+        cc = (C.c_void_p * 3)(*[t.data_ptr() for t in c])
+        uu = (C.c_void_p * 3)(*[t.data_ptr() for t in u])
+        gg = (C.c_void_p * 3)(*[t.data_ptr() for t in dgiven])
+        dd = (C.c_void_p * 3)(*[t.data_ptr() for t in d])
+        _check(lib().sdmm_guide_pdf_wavefront(self.h, tab, nq, cc, uu, gg, pdf_mode.data_ptr(), dd, pdf.data_ptr(),
+                                              comp.data_ptr(), None if node_out is None else node_out.data_ptr()))
+        return d, pdf, comp
+
+    def push_training(self, vertices: "PathVertices", saved_per_path: int = 8, seed: int = 0):
+        """Training records of Li's tail (sdmm_push_training): dict of device
+        tensors x (6 planes), normal (3), w, stats, node, source; seg (host);
+        lost (vertices outside the tree)."""
+        import torch
+        n = C.c_int64(0)
+        lost = C.c_int64(0)
+        _check(lib().sdmm_push_training(self.h, C.byref(vertices.s), int(saved_per_path), C.c_uint64(seed), None,
+                                        C.byref(n), None, C.byref(lost)))
+        m = n.value
+        dev = torch.device("cuda", vertices.device)
+        out = {"x": [torch.empty(m, device=dev) for _ in range(6)],
+               "normal": [torch.empty(m, device=dev) for _ in range(3)],
+               "w": torch.empty(m, device=dev), "stats": torch.empty(m, device=dev, dtype=torch.uint8),
+               "node": torch.empty(m, device=dev, dtype=torch.int32),
+               "source": torch.empty(m, device=dev, dtype=torch.int64)}
+        o = _TrainingOut()
+        for i in range(6):
+            o.x[i] = out["x"][i].data_ptr()
+        for i in range(3):
+            o.normal[i] = out["normal"][i].data_ptr()
+        o.w, o.stats = out["w"].data_ptr(), out["stats"].data_ptr()
+        o.node, o.source, o.capacity = out["node"].data_ptr(), out["source"].data_ptr(), m
+        seg = np.zeros(self.num_nodes + 1, np.int64)
+        _check(lib().sdmm_push_training(self.h, C.byref(vertices.s), int(saved_per_path), C.c_uint64(seed),
+                                        C.byref(o), C.byref(n), seg.ctypes.data_as(C.c_void_p), C.byref(lost)))
+        out["seg"] = seg
+        out["lost"] = lost.value
+        return out
+
+
+class _GuidingConfig(C.Structure):
+    _fields_ = [("K", C.c_int), ("split_depth", C.c_int), ("split_threshold", C.c_int),
+                ("max_leaf_nodes", C.c_int), ("saved_per_path", C.c_int), ("depth_prior", C.c_float),
+                ("init_seed", C.c_uint64)]
+
+
+class _GuidingStats(C.Structure):
+    _fields_ = [("leaves", C.c_int), ("optimized", C.c_int), ("records", C.c_int64)]
+
+
+class Guiding:
+    """The plugin's guiding model on the device (sdmm_guiding_*): tree, per-leaf
+    mixtures, training data and the render/optimize schedule."""
+
+    def __init__(self, tree_min, tree_max, device: int = 0, **cfg):
+        c = _GuidingConfig()
+        lib().sdmm_guiding_config_default(C.byref(c))
+        for k, v in cfg.items():
+            setattr(c, k, v)
+        lo = np.ascontiguousarray(tree_min, np.float32)
+        hi = np.ascontiguousarray(tree_max, np.float32)
+        h = C.c_void_p()
+        _check(lib().sdmm_guiding_create(lo.ctypes.data_as(C.c_void_p), hi.ctypes.data_as(C.c_void_p), C.byref(c),
+                                         int(device), C.byref(h)))
+        self.h, self.device, self.cfg = h, device, c
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.sdmm_guiding_destroy(self.h)
+            self.h = None
+
+    @property
+    def tree(self) -> "STree":
+        t = STree.__new__(STree)
+        t.h = C.c_void_p(lib().sdmm_guiding_tree(self.h))
+        t._owned = False
+        t._owner = self
+        return t
+
+    def node_mixtures(self):
+        n = self.tree.num_nodes
+        tab = (C.c_void_p * n)()
+        _check(lib().sdmm_guiding_node_mixtures(self.h, tab, n))
+        return [None if tab[i] is None else SDMM._borrow(tab[i], self) for i in range(n)]
+
+    @property
+    def trained(self) -> int:
+        return int(lib().sdmm_guiding_trained(self.h))
+
+    def push(self, vertices: "PathVertices", seed: int):
+        _check(lib().sdmm_guiding_push(self.h, C.byref(vertices.s), C.c_uint64(seed)))
+
+    def optimize(self, spp: int) -> dict:
+        st = _GuidingStats()
+        _check(lib().sdmm_guiding_optimize(self.h, int(spp), C.byref(st)))
+        return {"leaves": st.leaves, "optimized": st.optimized, "records": st.records}
+
+    def iteration(self, scene: "Scene", spp: int, seed: int, push_seed: int, train: bool = True,
+                  max_depth: int = 10, rr_depth: int = 10, bsdf_fraction: float = 0.5, saved_vertices: int = 9,
+                  image=None):
+        """One pass of render()'s loop -> (image, li stats, optimize stats)."""
+        import torch
+        if image is None:
+            image = torch.zeros(3, scene.height, scene.width, device=torch.device("cuda", self.device))
+        p = _LiParams()
+        p.spp, p.max_depth, p.rr_depth, p.guided = int(spp), int(max_depth), int(rr_depth), 0
+        p.bsdf_fraction, p.saved_vertices, p.seed = float(bsdf_fraction), int(saved_vertices), int(seed)
+        p.pixel_begin, p.pixel_end = 0, scene.width * scene.height
+        ls = _LiStats()
+        gs = _GuidingStats()
+        _check(lib().sdmm_guiding_iteration(self.h, scene.h, C.byref(p), C.c_uint64(push_seed), int(train),
+                                            C.c_void_p(image.data_ptr()), C.byref(ls), C.byref(gs)))
+        return image, {"paths": ls.paths, "segments": ls.segments}, \
+            {"leaves": gs.leaves, "optimized": gs.optimized, "records": gs.records}
+
+
+class _TrainingOut(C.Structure):
+    _fields_ = [("x", C.c_void_p * 6), ("normal", C.c_void_p * 3), ("w", C.c_void_p), ("stats", C.c_void_p),
+                ("node", C.c_void_p), ("source", C.c_void_p), ("capacity", C.c_int64)]
+
+
+class _SceneDesc(C.Structure):
+    _fields_ = [("n_quads", C.c_int), ("quads", C.c_void_p), ("flip_normals", C.c_void_p), ("bsdf", C.c_void_p),
+                ("n_bsdfs", C.c_int), ("reflectance", C.c_void_p), ("emitter", C.c_void_p),
+                ("n_emitters", C.c_int), ("radiance", C.c_void_p), ("camera_to_world", C.c_float * 16),
+                ("fov_x_deg", C.c_float), ("near_clip", C.c_float), ("width", C.c_int), ("height", C.c_int)]
+
+
+class _LiParams(C.Structure):
+    _fields_ = [("spp", C.c_int), ("max_depth", C.c_int), ("rr_depth", C.c_int), ("guided", C.c_int),
+                ("bsdf_fraction", C.c_float), ("saved_vertices", C.c_int), ("seed", C.c_uint64),
+                ("pixel_begin", C.c_int64), ("pixel_end", C.c_int64)]
+
+
+class _PathVertices(C.Structure):
+    _fields_ = [("n_paths", C.c_int64), ("max_vertices", C.c_int), ("path0", C.c_int64), ("rec", C.c_void_p),
+                ("nv", C.c_void_p)]
+
+
+class _LiStats(C.Structure):
+    _fields_ = [("paths", C.c_int64), ("segments", C.c_int64)]
+
+
+def _hip():
+    return C.CDLL("libamdhip64.so")
+
+
+class PathVertices:
+    """The saved vertices of the last Scene.render (scene-owned device memory,
+    valid until the scene renders again)."""
+
+    def __init__(self, s, scene, device):
+        self.s, self.scene, self.device = s, scene, device
+
+    def to_numpy(self):
+        P, V = self.s.n_paths, self.s.max_vertices
+        rec = np.empty(16 * V * P, np.float32)
+        nv = np.empty(P, np.int32)
+        import torch
+        torch.cuda.synchronize(self.device)
+        h = _hip()
+        h.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        assert h.hipMemcpy(rec.ctypes.data, self.s.rec, rec.nbytes, 2) == 0
+        assert h.hipMemcpy(nv.ctypes.data, self.s.nv, nv.nbytes, 2) == 0
+        return rec, nv
+
+
+class Scene:
+    """Analytic quad scene for the device Li (sdmm_scene_*); desc as
+    scenes.cornell_box() returns it."""
+
+    def __init__(self, desc: dict, device: int = 0):
+        self._keep = {k: np.ascontiguousarray(v) for k, v in desc.items() if isinstance(v, np.ndarray)}
+        d = _SceneDesc()
+        d.n_quads = self._keep["quads"].size // 9
+        d.quads = self._keep["quads"].ctypes.data
+        d.flip_normals = self._keep["flip_normals"].ctypes.data if "flip_normals" in self._keep else None
+        d.bsdf = self._keep["bsdf"].ctypes.data
+        d.n_bsdfs = self._keep["reflectance"].size // 3
+        d.reflectance = self._keep["reflectance"].ctypes.data
+        if "emitter" in self._keep:
+            d.emitter = self._keep["emitter"].ctypes.data
+            d.n_emitters = self._keep["radiance"].size // 3
+            d.radiance = self._keep["radiance"].ctypes.data
+        for i, v in enumerate(np.asarray(desc["camera_to_world"], np.float32).reshape(-1)):
+            d.camera_to_world[i] = float(v)
+        d.fov_x_deg = float(desc["fov_x_deg"])
+        d.near_clip = float(desc.get("near_clip", 1e-2))
+        d.width, d.height = int(desc["width"]), int(desc["height"])
+        self.width, self.height, self.device = d.width, d.height, device
+        h = C.c_void_p()
+        _check(lib().sdmm_scene_create(C.byref(d), int(device), C.byref(h)))
+        self.h = h
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.sdmm_scene_destroy(self.h)
+            self.h = None
+
+    def normalization(self):
+        """(scene_min, spatial_norm, tree_min, tree_max) -- render(), volpath_sdmm.cpp:375-393."""
+        smin = np.zeros(3, np.float32)
+        norm = np.zeros(1, np.float32)
+        tmin = np.zeros(3, np.float32)
+        tmax = np.zeros(3, np.float32)
+        _check(lib().sdmm_scene_normalization(self.h, smin.ctypes.data, norm.ctypes.data, tmin.ctypes.data,
+                                              tmax.ctypes.data))
+        return smin, float(norm[0]), tmin, tmax
+
+    def render(self, tree: "STree", node_mix=None, spp: int = 1, max_depth: int = 10, rr_depth: int = 10,
+               guided: bool = False, bsdf_fraction: float = 0.5, saved_vertices: int = 9, seed: int = 0,
+               pixels=None, image=None):
+        """One render pass (sdmm_li_render) -> (image (3, H, W) device tensor,
+        PathVertices, stats dict)."""
+        import torch
+        if image is None:
+            image = torch.zeros(3, self.height, self.width, device=torch.device("cuda", self.device))
+        p = _LiParams()
+        p.spp, p.max_depth, p.rr_depth, p.guided = int(spp), int(max_depth), int(rr_depth), int(guided)
+        p.bsdf_fraction, p.saved_vertices, p.seed = float(bsdf_fraction), int(saved_vertices), int(seed)
+        p.pixel_begin, p.pixel_end = (0, self.width * self.height) if pixels is None else pixels
+        v = _PathVertices()
+        st = _LiStats()
+        tab = None if not guided else tree._node_table(node_mix)
+        _check(lib().sdmm_li_render(self.h, tree.h, tab, C.byref(p), C.c_void_p(image.data_ptr()), C.byref(v),
+                                    C.byref(st)))
+        return image, PathVertices(v, self, self.device), {"paths": st.paths, "segments": st.segments}

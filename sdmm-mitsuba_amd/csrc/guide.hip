@@ -182,6 +182,9 @@ struct QueryOut {
     float pdf;
     int comp;
 };
+// comp of a query evaluated at a given direction (the mixed wavefront's pdf
+// queries) whose conditional is valid; -1 stays "no valid conditional".
+constexpr int kCompPdfValid = -2;
 
 template <class Slots>
 __device__ __forceinline__ QueryOut finish_query(const float* gp, int Kp, const float c[3], const float u[3],
@@ -234,6 +237,7 @@ __device__ __forceinline__ QueryOut finish_query(const float* gp, int Kp, const 
         o.comp = ksel;
     } else {
         dir[0] = dir_in[0]; dir[1] = dir_in[1]; dir[2] = dir_in[2];
+        o.comp = kCompPdfValid;
     }
     // MixtureModel::pdf over the conditional (the gmmPdf of pdfSurface)
     float acc = 0.0f;
@@ -356,6 +360,9 @@ struct GuideIO {
     const float *c0, *c1, *c2, *u0, *u1, *u2, *e0, *e1, *e2;
     float *d0, *d1, *d2, *pdf;
     int32_t* comp;
+    // mixed wavefront (sampling kernels only): pmode[q] != 0 makes query q a
+    // pdf query at the given direction e[q] (d[q] = e[q], comp -2 / -1)
+    const uint8_t* pmode;
 };
 
 // One mixture's guide record as the wavefront kernels see it (per tree node;
@@ -386,7 +393,9 @@ __device__ __forceinline__ void finish_and_write(const float* gp, int Kp, const 
         io.pdf[q] = finish_query(gp, Kp, c, nullptr, lastIdx, accum, S, dir, gc).pdf;
     } else {
         const float u[3] = {io.u0[q], io.u1[q], io.u2[q]};
-        const QueryOut o = finish_query(gp, Kp, c, u, lastIdx, accum, S, nullptr, gc);
+        const float dg[3] = {io.pmode && io.pmode[q] ? io.e0[q] : 0.0f, io.pmode && io.pmode[q] ? io.e1[q] : 0.0f,
+                             io.pmode && io.pmode[q] ? io.e2[q] : 0.0f};
+        const QueryOut o = finish_query(gp, Kp, c, u, lastIdx, accum, S, (io.pmode && io.pmode[q]) ? dg : nullptr, gc);
         io.d0[q] = o.d[0]; io.d1[q] = o.d[1]; io.d2[q] = o.d[2];
         io.pdf[q] = o.pdf;
         io.comp[q] = o.comp;
@@ -693,6 +702,7 @@ __device__ QueryOut finish_query_wave(const float* gp, int Kp, const float c[3],
         o.comp = ksel;
     } else {
         dir[0] = dir_in[0]; dir[1] = dir_in[1]; dir[2] = dir_in[2];
+        o.comp = kCompPdfValid;
     }
     // MixtureModel::pdf over the conditional: terms in parallel, summed in slot order
     float acc = 0.0f;
@@ -722,9 +732,12 @@ __device__ __forceinline__ void serve_full_wave(const float* gp, int Kp, int K, 
     const int lastIdx = build_full_wave(gp, Kp, K, c, L, lane, gc.norm3, accum);
     const float sum2 = wave_slot_weights(lastIdx, accum, L, lane);
     float u[3] = {0.0f, 0.0f, 0.0f}, dg[3] = {0.0f, 0.0f, 0.0f};
-    if constexpr (PDF_ONLY) { dg[0] = io.e0[q]; dg[1] = io.e1[q]; dg[2] = io.e2[q]; }
+    bool pdf_q = PDF_ONLY;
+    if constexpr (!PDF_ONLY) pdf_q = io.pmode && io.pmode[q];   // uniform: one query per wave
+    if (pdf_q) { dg[0] = io.e0[q]; dg[1] = io.e1[q]; dg[2] = io.e2[q]; }
     else { u[0] = io.u0[q]; u[1] = io.u1[q]; u[2] = io.u2[q]; }
-    const QueryOut o = finish_query_wave<PDF_ONLY>(gp, Kp, c, u, dg, lastIdx, sum2, L, lane, gc);
+    const QueryOut o = pdf_q ? finish_query_wave<true>(gp, Kp, c, u, dg, lastIdx, sum2, L, lane, gc)
+                             : finish_query_wave<false>(gp, Kp, c, u, dg, lastIdx, sum2, L, lane, gc);
     if (lane == 0) {
         io.pdf[q] = o.pdf;
         if constexpr (!PDF_ONLY) {
@@ -1566,16 +1579,19 @@ static hipError_t coherent_order(const float* const c[3], int n, uint32_t* keys_
 }
 
 static GuideIO make_io(const float* const c[3], const float* const u[3], const float* const dgiven[3],
-                       float* const d[3], float* pdf, int32_t* comp) {
-    const bool pdf_only = dgiven != nullptr;
+                       float* const d[3], float* pdf, int32_t* comp, const uint8_t* pmode = nullptr) {
+    // pdf only: dgiven without pmode; mixed: dgiven with pmode (sampling kernels)
+    const bool pdf_only = dgiven != nullptr && pmode == nullptr;
     GuideIO io{};
     io.c0 = c[0]; io.c1 = c[1]; io.c2 = c[2];
-    if (pdf_only) {
+    if (dgiven) {
         io.e0 = dgiven[0]; io.e1 = dgiven[1]; io.e2 = dgiven[2];
-    } else {
+    }
+    if (!pdf_only) {
         io.u0 = u[0]; io.u1 = u[1]; io.u2 = u[2];
         io.d0 = d[0]; io.d1 = d[1]; io.d2 = d[2];
         io.comp = comp;
+        io.pmode = pmode;
     }
     io.pdf = pdf;
     return io;
@@ -1665,7 +1681,7 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
                              const float* const u[3], const float* const dgiven[3], float* const d[3],
                              float* pdf, int32_t* comp, int32_t* node_out, float norm2, float norm3, int cap,
                              int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
-                             const GuideSortScratch* sort) {
+                             const GuideSortScratch* sort, const uint8_t* pmode) {
     if (nq <= 0) return hipSuccess;
     cap = (cap < 0) ? 0 : (cap > kGuideCap ? kGuideCap : cap);
     if (nq > INT32_MAX) return hipErrorInvalidValue;
@@ -1688,7 +1704,8 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
     const GuideMix* tb = (const GuideMix*)tab;
     const dim3 grid((unsigned)((nq + T - 1) / T));
     const int fb_blocks = cus * 8;
-    const GuideIO io = make_io(c, u, dgiven, d, pdf, comp);
+    const GuideIO io = make_io(c, u, dgiven, d, pdf, comp, pmode);
+    if (pmode) dgiven = nullptr;   // mixed: the sampling kernels, pdf queries per pmode
     cap = cap < kmax ? cap : kmax;
     e = dgiven ? launch_tree_cand<true>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_out)
                : launch_tree_cand<false>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_out);

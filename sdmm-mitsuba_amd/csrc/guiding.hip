@@ -1,0 +1,555 @@
+// guiding.hip -- the plugin's guiding model (SDMMVolumetricPathTracer,
+// volpath_sdmm.cpp:132-312, :411-507) on the device, behind sdmm_guiding_* in
+// include/sdmm_gpu.h: the accelerator tree, one SDMM + stepwise EM state per
+// trained leaf (SDMMContext, sdmm_proc.h:92-93), the leaves' training data
+// and the per-iteration schedule.
+//
+// Data layout.  The reference keeps a Samples buffer per leaf context, filled
+// under a mutex.  Here every leaf's records live in ONE device pool (SoA
+// planes: point 6, normal 3, weight, leaf id), appended per render iteration
+// in the producer's leaf order; optimize() orders the pool by leaf with a
+// stable radix sort (a leaf's records stay in arrival order), so the leaves
+// that can be optimised form one contiguous prefix that feeds the batched
+// per-leaf EM directly, and are then dropped.  The leaves' stats positions
+// (context.stats, used only for splitting) stay on the host, where the tree
+// is built.
+//
+// Split leaves (split_leaf_recurse): records and stats positions move to the
+// child leaf that holds them (a record outside the split leaf's subtree is
+// dropped), and every new leaf starts from a copy of the parent's mixture and
+// EM state -- jmm SNTree::createChildNode (sntree.h:172-205); sdmm-lib's tree,
+// which the plugin instantiates, is absent (parity unpinned for this rule).
+#include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/sdmm_gpu.h"
+
+namespace sdmm_detail {
+int set_error(int code, const char* msg);
+}  // namespace sdmm_detail
+
+namespace {
+
+constexpr int kPlanes = 10;   // x 6, normal 3, w
+
+int fail(int code, const std::string& m) { return sdmm_detail::set_error(code, m.c_str()); }
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(SDMM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
+    } while (0)
+#define SDMM_TRY(expr)            \
+    do {                          \
+        const int r_ = (expr);    \
+        if (r_) return r_;        \
+    } while (0)
+
+// key per record: its leaf for the ordering sort; `ready` leaves (flag) first
+__global__ void pool_keys_kernel(const int32_t* __restrict__ node, int64_t n, const uint8_t* __restrict__ ready,
+                                 int num_nodes, uint32_t* __restrict__ keys, int32_t* __restrict__ idx) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int v = node[i];
+    uint32_t k = 2u * (uint32_t)num_nodes;   // dropped records sort last
+    if (v >= 0) k = ready && ready[v] ? (uint32_t)v : (uint32_t)(num_nodes + v);
+    keys[i] = k;
+    idx[i] = (int32_t)i;
+}
+
+__global__ void pool_gather_kernel(const float* __restrict__ src, float* __restrict__ dst, const int32_t* __restrict__ node_in,
+                                   int32_t* __restrict__ node_out, const int32_t* __restrict__ perm, int64_t n,
+                                   int64_t cap) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const int64_t i = perm[j];
+    for (int p = 0; p < kPlanes; ++p) dst[p * cap + j] = src[p * cap + i];
+    node_out[j] = node_in[i];
+}
+
+// first position with key >= v for v = 0 .. nk
+__global__ void pool_seg_kernel(const uint32_t* __restrict__ keys, int64_t n, int nk, int64_t* __restrict__ seg) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v > nk) return;
+    int64_t lo = 0, count = n;
+    while (count > 0) {
+        const int64_t step = count / 2, it = lo + step;
+        if (keys[it] < (uint32_t)v) { lo = it + 1; count -= step + 1; }
+        else count = step;
+    }
+    seg[v] = lo;
+}
+
+// records of split leaves: the leaf found in the new tree if it descends from
+// the old one (parent table), else dropped (-1)
+__global__ void pool_relabel_kernel(int32_t* __restrict__ node, const int32_t* __restrict__ found, int64_t n,
+                                    const uint8_t* __restrict__ was_split, const int32_t* __restrict__ parent) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int v = node[i];
+    if (v < 0 || !was_split[v]) return;
+    int f = found[i];
+    int a = f;
+    while (a >= 0 && a != v) a = parent[a];
+    node[i] = (a == v) ? f : -1;
+}
+
+inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+
+}  // namespace
+
+struct sdmm_guiding {
+    int device = 0;
+    sdmm_guiding_config cfg{};
+    sdmm_stree* tree = nullptr;
+    hipStream_t st = nullptr;
+    std::vector<sdmm_mix*> mix;                 // per node (NULL: untrained / inner)
+    std::vector<std::vector<float>> stats;      // per node: stats positions x, y, z interleaved
+    int64_t total_spp = 0;
+    int iteration = 0;
+    // record pool: planes [kPlanes][cap] + node ids, double-buffered for the sorts
+    float* pool[2] = {nullptr, nullptr};
+    int32_t* pnode[2] = {nullptr, nullptr};
+    int cur = 0;
+    int64_t n = 0, cap = 0;
+    void* scratch = nullptr;
+    size_t scratch_bytes = 0;
+    std::vector<int64_t> seg;
+};
+
+namespace {
+
+int grow_pool(sdmm_guiding* g, int64_t need) {
+    if (need <= g->cap) return SDMM_OK;
+    int64_t cap = std::max<int64_t>(need, g->cap * 2);
+    cap = std::max<int64_t>(cap, 1 << 16);
+    float* np[2] = {nullptr, nullptr};
+    int32_t* nn[2] = {nullptr, nullptr};
+    for (int b = 0; b < 2; ++b) {
+        HIP_TRY(hipMalloc(&np[b], sizeof(float) * kPlanes * (size_t)cap));
+        HIP_TRY(hipMalloc(&nn[b], sizeof(int32_t) * (size_t)cap));
+    }
+    if (g->n > 0) {
+        for (int p = 0; p < kPlanes; ++p)
+            HIP_TRY(hipMemcpyAsync(np[0] + p * cap, g->pool[g->cur] + p * g->cap, sizeof(float) * (size_t)g->n,
+                                   hipMemcpyDeviceToDevice, g->st));
+        HIP_TRY(hipMemcpyAsync(nn[0], g->pnode[g->cur], sizeof(int32_t) * (size_t)g->n, hipMemcpyDeviceToDevice,
+                               g->st));
+    }
+    HIP_TRY(hipStreamSynchronize(g->st));
+    for (int b = 0; b < 2; ++b) {
+        if (g->pool[b]) HIP_TRY(hipFree(g->pool[b]));
+        if (g->pnode[b]) HIP_TRY(hipFree(g->pnode[b]));
+        g->pool[b] = np[b];
+        g->pnode[b] = nn[b];
+    }
+    g->cur = 0;
+    g->cap = cap;
+    return SDMM_OK;
+}
+
+int grow_scratch(sdmm_guiding* g, size_t bytes) {
+    if (bytes <= g->scratch_bytes) return SDMM_OK;
+    HIP_TRY(hipStreamSynchronize(g->st));
+    if (g->scratch) HIP_TRY(hipFree(g->scratch));
+    g->scratch = nullptr;
+    HIP_TRY(hipMalloc(&g->scratch, bytes));
+    g->scratch_bytes = bytes;
+    return SDMM_OK;
+}
+
+size_t al(size_t b) { return (b + 255) / 256 * 256; }
+
+// Stable reorder of the pool by key (ready leaves first, then the other
+// leaves, dropped records last); seg over keys 0 .. 2 * num_nodes.
+int order_pool(sdmm_guiding* g, const std::vector<uint8_t>& ready) {
+    const int nn = sdmm_stree_num_nodes(g->tree);
+    const int nk = 2 * nn;
+    g->seg.assign((size_t)nk + 1, 0);
+    if (g->n == 0) return SDMM_OK;
+    int bits = 1;
+    while ((1u << bits) <= (unsigned)nk) ++bits;
+    size_t tb = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                             (const int32_t*)nullptr, (int32_t*)nullptr, (int)g->n, 0, bits);
+    const size_t kb = al(sizeof(uint32_t) * (size_t)g->n);
+    const size_t sb = al(sizeof(int64_t) * (size_t)(nk + 1));
+    const size_t rb = al((size_t)std::max(nn, 1));
+    SDMM_TRY(grow_scratch(g, 4 * kb + sb + rb + al(tb)));
+    char* b = (char*)g->scratch;
+    uint32_t* k0 = (uint32_t*)b;
+    uint32_t* k1 = (uint32_t*)(b + kb);
+    int32_t* i0 = (int32_t*)(b + 2 * kb);
+    int32_t* i1 = (int32_t*)(b + 3 * kb);
+    int64_t* sdev = (int64_t*)(b + 4 * kb);
+    uint8_t* rdev = (uint8_t*)(b + 4 * kb + sb);
+    void* temp = b + 4 * kb + sb + rb;
+    HIP_TRY(hipMemcpyAsync(rdev, ready.data(), (size_t)nn, hipMemcpyHostToDevice, g->st));
+    hipLaunchKernelGGL(pool_keys_kernel, grid_for(g->n), dim3(256), 0, g->st, g->pnode[g->cur], g->n, rdev, nn, k0,
+                       i0);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(temp, tb, k0, k1, i0, i1, (int)g->n, 0, bits, g->st));
+    hipLaunchKernelGGL(pool_gather_kernel, grid_for(g->n), dim3(256), 0, g->st, g->pool[g->cur], g->pool[1 - g->cur],
+                       g->pnode[g->cur], g->pnode[1 - g->cur], i1, g->n, g->cap);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(pool_seg_kernel, grid_for(nk + 1), dim3(256), 0, g->st, k1, g->n, nk, sdev);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(g->seg.data(), sdev, sizeof(int64_t) * (size_t)(nk + 1), hipMemcpyDeviceToHost, g->st));
+    HIP_TRY(hipStreamSynchronize(g->st));   // (ready is a host temporary)
+    g->cur = 1 - g->cur;
+    g->n = g->seg[(size_t)nk];              // dropped records are gone
+    return SDMM_OK;
+}
+
+// After a split: stats positions, pool records and mixtures of every split
+// leaf move to its new leaves.
+int redistribute(sdmm_guiding* g, int old_nodes) {
+    const int nn = sdmm_stree_num_nodes(g->tree);
+    std::vector<int32_t> child(2 * (size_t)nn), parent((size_t)nn, -1);
+    SDMM_TRY(sdmm_stree_get_nodes(g->tree, nullptr, child.data(), nullptr));
+    for (int i = 0; i < nn; ++i)
+        for (int c = 0; c < 2; ++c)
+            if (child[2 * (size_t)i + c] >= 0) parent[(size_t)child[2 * (size_t)i + c]] = i;
+    std::vector<uint8_t> was_split((size_t)nn, 0);
+    bool any = false;
+    for (int v = 0; v < old_nodes; ++v)   // records only ever name leaves: an old node with children was split
+        if (child[2 * (size_t)v] >= 0) {
+            was_split[(size_t)v] = 1;
+            any = true;
+        }
+    g->mix.resize((size_t)nn, nullptr);
+    g->stats.resize((size_t)nn);
+    if (!any && g->n == 0) return SDMM_OK;
+    auto descends = [&](int f, int v) {
+        while (f >= 0 && f != v) f = parent[(size_t)f];
+        return f == v;
+    };
+    // mixtures: a copy of the parent's in every new leaf of its subtree
+    for (int v = 0; v < old_nodes; ++v) {
+        if (child[2 * (size_t)v] < 0 || !g->mix[(size_t)v]) continue;
+        for (int c = 0; c < nn; ++c) {
+            if (child[2 * (size_t)c] >= 0 || !descends(c, v)) continue;
+            sdmm_mix* m = nullptr;
+            SDMM_TRY(sdmm_clone(g->mix[(size_t)v], &m));
+            SDMM_TRY(sdmm_set_stream(m, (void*)g->st));
+            g->mix[(size_t)c] = m;
+        }
+        sdmm_destroy(g->mix[(size_t)v]);
+        g->mix[(size_t)v] = nullptr;
+    }
+    // stats positions (host): through find on the device
+    for (int v = 0; v < old_nodes; ++v) {
+        if (child[2 * (size_t)v] < 0 || g->stats[(size_t)v].empty()) continue;
+        std::vector<float> pos;
+        pos.swap(g->stats[(size_t)v]);
+        const int64_t m = (int64_t)pos.size() / 3;
+        std::vector<float> planes(3 * (size_t)m);
+        for (int64_t i = 0; i < m; ++i)
+            for (int a = 0; a < 3; ++a) planes[(size_t)a * (size_t)m + (size_t)i] = pos[3 * (size_t)i + (size_t)a];
+        float* dp = nullptr;
+        int32_t* df = nullptr;
+        HIP_TRY(hipMallocAsync((void**)&dp, sizeof(float) * 3 * (size_t)m, g->st));
+        HIP_TRY(hipMallocAsync((void**)&df, sizeof(int32_t) * (size_t)m, g->st));
+        HIP_TRY(hipMemcpyAsync(dp, planes.data(), sizeof(float) * 3 * (size_t)m, hipMemcpyHostToDevice, g->st));
+        const float* pp[3] = {dp, dp + m, dp + 2 * m};
+        SDMM_TRY(sdmm_stree_find(g->tree, m, pp, df));
+        std::vector<int32_t> f((size_t)m);
+        HIP_TRY(hipMemcpyAsync(f.data(), df, sizeof(int32_t) * (size_t)m, hipMemcpyDeviceToHost, g->st));
+        HIP_TRY(hipFreeAsync(dp, g->st));
+        HIP_TRY(hipFreeAsync(df, g->st));
+        HIP_TRY(hipStreamSynchronize(g->st));
+        for (int64_t i = 0; i < m; ++i) {
+            const int c = f[(size_t)i];
+            if (c < 0 || !descends(c, v)) continue;
+            auto& s = g->stats[(size_t)c];
+            s.insert(s.end(), pos.begin() + 3 * i, pos.begin() + 3 * i + 3);
+        }
+    }
+    // pool records: relabel on the device
+    if (g->n > 0) {
+        int32_t* dfound = nullptr;
+        uint8_t* dsplit = nullptr;
+        int32_t* dparent = nullptr;
+        HIP_TRY(hipMallocAsync((void**)&dfound, sizeof(int32_t) * (size_t)g->n, g->st));
+        HIP_TRY(hipMallocAsync((void**)&dsplit, (size_t)nn, g->st));
+        HIP_TRY(hipMallocAsync((void**)&dparent, sizeof(int32_t) * (size_t)nn, g->st));
+        HIP_TRY(hipMemcpyAsync(dsplit, was_split.data(), (size_t)nn, hipMemcpyHostToDevice, g->st));
+        HIP_TRY(hipMemcpyAsync(dparent, parent.data(), sizeof(int32_t) * (size_t)nn, hipMemcpyHostToDevice, g->st));
+        float* P = g->pool[g->cur];
+        const float* pp[3] = {P, P + g->cap, P + 2 * g->cap};
+        SDMM_TRY(sdmm_stree_find(g->tree, g->n, pp, dfound));
+        hipLaunchKernelGGL(pool_relabel_kernel, grid_for(g->n), dim3(256), 0, g->st, g->pnode[g->cur], dfound, g->n,
+                           dsplit, dparent);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipFreeAsync(dfound, g->st));
+        HIP_TRY(hipFreeAsync(dsplit, g->st));
+        HIP_TRY(hipFreeAsync(dparent, g->st));
+        HIP_TRY(hipStreamSynchronize(g->st));   // host tables above are temporaries
+    }
+    return SDMM_OK;
+}
+
+int bind(sdmm_guiding* g) {
+    std::vector<const sdmm_mix*> tab(g->mix.begin(), g->mix.end());
+    return sdmm_stree_bind_mixtures(g->tree, tab.data());
+}
+
+}  // namespace
+
+extern "C" {
+
+void sdmm_guiding_config_default(sdmm_guiding_config* c) {
+    if (!c) return;
+    c->K = 16;                  // SDMMProcess::NComponents of the built plugin
+    c->split_depth = 2;         // split_to_depth(2), volpath_sdmm.cpp:398
+    c->split_threshold = 4000;  // m_splitThreshold (:528)
+    c->max_leaf_nodes = 2048;   // m_maxLeafNodes (:529)
+    c->saved_per_path = 8;      // savedSamplesPerPath (:62)
+    c->depth_prior = 0.01f;
+    c->init_seed = 0x1A17;
+}
+
+int sdmm_guiding_create(const float tree_min[3], const float tree_max[3], const sdmm_guiding_config* cfg,
+                        int device, sdmm_guiding** out) {
+    if (!tree_min || !tree_max || !cfg || !out || cfg->K < 8 || cfg->K % 8 || cfg->split_threshold < 1 ||
+        cfg->saved_per_path < 1)
+        return fail(SDMM_E_INVALID, "sdmm_guiding_create: invalid argument");
+    *out = nullptr;
+    sdmm_guiding* g = new (std::nothrow) sdmm_guiding();
+    if (!g) return fail(SDMM_E_NOMEM, "out of host memory");
+    g->device = device;
+    g->cfg = *cfg;
+    int r = sdmm_stree_create(tree_min, tree_max, device, &g->tree);
+    if (!r) r = sdmm_stree_split_to_depth(g->tree, cfg->split_depth);
+    if (!r) {
+        hipError_t e = hipSetDevice(device);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&g->st, hipStreamNonBlocking);
+        if (e != hipSuccess) r = fail(SDMM_E_HIP, std::string("sdmm_guiding_create: ") + hipGetErrorString(e));
+    }
+    if (!r) r = sdmm_stree_set_stream(g->tree, (void*)g->st);
+    if (r) {
+        sdmm_guiding_destroy(g);
+        return r;
+    }
+    const int nn = sdmm_stree_num_nodes(g->tree);
+    g->mix.assign((size_t)nn, nullptr);
+    g->stats.assign((size_t)nn, {});
+    *out = g;
+    return SDMM_OK;
+}
+
+void sdmm_guiding_destroy(sdmm_guiding* g) {
+    if (!g) return;
+    (void)hipSetDevice(g->device);
+    if (g->st) (void)hipStreamSynchronize(g->st);
+    for (sdmm_mix* m : g->mix) sdmm_destroy(m);
+    if (g->tree) sdmm_stree_destroy(g->tree);
+    for (int b = 0; b < 2; ++b) {
+        if (g->pool[b]) (void)hipFree(g->pool[b]);
+        if (g->pnode[b]) (void)hipFree(g->pnode[b]);
+    }
+    if (g->scratch) (void)hipFree(g->scratch);
+    if (g->st) (void)hipStreamDestroy(g->st);
+    delete g;
+}
+
+sdmm_stree* sdmm_guiding_tree(sdmm_guiding* g) { return g ? g->tree : nullptr; }
+
+int sdmm_guiding_node_mixtures(const sdmm_guiding* g, const sdmm_mix** out, int cap) {
+    if (!g || !out) return fail(SDMM_E_INVALID, "invalid argument");
+    const int nn = (int)g->mix.size();
+    if (cap < nn) return fail(SDMM_E_INVALID, "sdmm_guiding_node_mixtures: cap < num_nodes");
+    for (int i = 0; i < nn; ++i) out[i] = g->mix[(size_t)i];
+    return SDMM_OK;
+}
+
+int sdmm_guiding_trained(const sdmm_guiding* g) {
+    if (!g) return 0;
+    int n = 0;
+    for (const sdmm_mix* m : g->mix) n += m ? 1 : 0;
+    return n;
+}
+
+// push_back_data for a render pass's paths (Li's tail): records appended to
+// the pool, stats positions to their leaves
+int sdmm_guiding_push(sdmm_guiding* g, const sdmm_path_vertices* v, uint64_t seed) {
+    if (!g || !v) return fail(SDMM_E_INVALID, "invalid argument");
+    HIP_TRY(hipSetDevice(g->device));
+    int64_t count = 0;
+    SDMM_TRY(sdmm_push_training(g->tree, v, g->cfg.saved_per_path, seed, nullptr, &count, nullptr, nullptr));
+    SDMM_TRY(grow_pool(g, g->n + count));
+    uint8_t* dstats = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&dstats, (size_t)std::max<int64_t>(count, 1), g->st));
+    float* P = g->pool[g->cur];
+    sdmm_training_out o{};
+    for (int i = 0; i < 6; ++i) o.x[i] = P + i * g->cap + g->n;
+    for (int i = 0; i < 3; ++i) o.normal[i] = P + (6 + i) * g->cap + g->n;
+    o.w = P + 9 * g->cap + g->n;
+    o.stats = dstats;
+    o.node = g->pnode[g->cur] + g->n;
+    o.capacity = count;
+    int64_t got = 0;
+    SDMM_TRY(sdmm_push_training(g->tree, v, g->cfg.saved_per_path, seed, &o, &got, nullptr, nullptr));
+    // the stats positions, in record order (leaf order, producer order inside)
+    std::vector<float> px(3 * (size_t)count);
+    std::vector<int32_t> nd((size_t)count);
+    std::vector<uint8_t> sf((size_t)count);
+    for (int a = 0; a < 3; ++a)
+        HIP_TRY(hipMemcpyAsync(px.data() + (size_t)a * (size_t)count, P + a * g->cap + g->n,
+                               sizeof(float) * (size_t)count, hipMemcpyDeviceToHost, g->st));
+    HIP_TRY(hipMemcpyAsync(nd.data(), o.node, sizeof(int32_t) * (size_t)count, hipMemcpyDeviceToHost, g->st));
+    HIP_TRY(hipMemcpyAsync(sf.data(), dstats, (size_t)count, hipMemcpyDeviceToHost, g->st));
+    HIP_TRY(hipFreeAsync(dstats, g->st));
+    HIP_TRY(hipStreamSynchronize(g->st));
+    for (int64_t i = 0; i < count; ++i) {
+        if (!sf[(size_t)i]) continue;
+        auto& s = g->stats[(size_t)nd[(size_t)i]];
+        for (int a = 0; a < 3; ++a) s.push_back(px[(size_t)a * (size_t)count + (size_t)i]);
+    }
+    g->n += count;
+    return SDMM_OK;
+}
+
+// optimize() (volpath_sdmm.cpp:244-312) with the render loop's spp accounting
+// (:495-506): split, canBeOptimized (:140-149), initialise new leaves
+// (initializeSDMMContext with hmax(diagonal), :132-138, :291-293), 2 EM
+// iterations while iterations_run < 4 else 1 (:299-305), drop their data,
+// bind the trained leaves for the next render pass.
+int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
+    if (!g || spp < 0) return fail(SDMM_E_INVALID, "invalid argument");
+    HIP_TRY(hipSetDevice(g->device));
+    // (1) split by the leaves' stats positions, nodes in id order
+    const int old_nodes = sdmm_stree_num_nodes(g->tree);
+    {
+        size_t tot = 0;
+        for (const auto& s : g->stats) tot += s.size() / 3;
+        std::vector<float> planes(3 * tot);
+        size_t k = 0;
+        for (const auto& s : g->stats)
+            for (size_t i = 0; i < s.size() / 3; ++i, ++k)
+                for (int a = 0; a < 3; ++a) planes[(size_t)a * tot + k] = s[3 * i + (size_t)a];
+        const float* p[3] = {planes.data(), planes.data() + tot, planes.data() + 2 * tot};
+        SDMM_TRY(sdmm_stree_split_leaves(g->tree, p, (int64_t)tot, g->cfg.split_threshold, g->cfg.max_leaf_nodes));
+    }
+    if (sdmm_stree_num_nodes(g->tree) != old_nodes) SDMM_TRY(redistribute(g, old_nodes));
+    const int nn = sdmm_stree_num_nodes(g->tree);
+    std::vector<float> aabb(6 * (size_t)nn);
+    std::vector<int32_t> child(2 * (size_t)nn);
+    SDMM_TRY(sdmm_stree_get_nodes(g->tree, aabb.data(), child.data(), nullptr));
+    // (2) records per leaf (pool ordered by leaf, nothing ready yet)
+    std::vector<uint8_t> ready((size_t)nn, 0);
+    SDMM_TRY(order_pool(g, ready));
+    int n_ready = 0;
+    for (int v = 0; v < nn; ++v) {
+        const int64_t n_data = g->seg[(size_t)(nn + v + 1)] - g->seg[(size_t)(nn + v)];
+        const int64_t n_stats = (int64_t)g->stats[(size_t)v].size() / 3;
+        if ((g->total_spp > 12 || n_data > 1000) && child[2 * (size_t)v] < 0 && n_stats >= 64 && n_data >= 8) {
+            ready[(size_t)v] = 1;
+            ++n_ready;
+        }
+    }
+    g->total_spp += spp;
+    if (out) {
+        out->leaves = sdmm_stree_leaf_nodes(g->tree);
+        out->optimized = n_ready;
+        out->records = g->n;
+    }
+    ++g->iteration;
+    if (n_ready == 0) return bind(g);
+    // (3) the ready leaves' records as one prefix, in leaf order
+    SDMM_TRY(order_pool(g, ready));
+    std::vector<sdmm_mix*> mixes;
+    std::vector<int64_t> bseg{0};
+    std::vector<int> iters;
+    const int K = g->cfg.K, npos = K / 8;
+    float* P = g->pool[g->cur];
+    for (int v = 0; v < nn; ++v) {
+        if (!ready[(size_t)v]) continue;
+        const int64_t a = g->seg[(size_t)v], b = g->seg[(size_t)v + 1];
+        if (!g->mix[(size_t)v]) {
+            // the first K/8 records' positions and normals (kMeansPlusPlus off,
+            // mixture_model_init.h:139-141); spatial distance 3 hmax / (K/8)
+            std::vector<float> pl(6 * (size_t)npos);
+            for (int f = 0; f < 3; ++f) {
+                HIP_TRY(hipMemcpyAsync(pl.data() + (size_t)f * npos, P + f * g->cap + a, sizeof(float) * npos,
+                                       hipMemcpyDeviceToHost, g->st));
+                HIP_TRY(hipMemcpyAsync(pl.data() + (size_t)(3 + f) * npos, P + (6 + f) * g->cap + a,
+                                       sizeof(float) * npos, hipMemcpyDeviceToHost, g->st));
+            }
+            HIP_TRY(hipStreamSynchronize(g->st));
+            std::vector<float> pos(3 * (size_t)npos), nrm(3 * (size_t)npos);
+            for (int i = 0; i < npos; ++i)
+                for (int f = 0; f < 3; ++f) {
+                    pos[3 * (size_t)i + f] = pl[(size_t)f * npos + i];
+                    nrm[3 * (size_t)i + f] = pl[(size_t)(3 + f) * npos + i];
+                }
+            float diag = 0.0f;
+            for (int a3 = 0; a3 < 3; ++a3)
+                diag = std::max(diag, aabb[6 * (size_t)v + 3 + a3] - aabb[6 * (size_t)v + a3]);
+            sdmm_em_params ep;
+            sdmm_em_params_default(&ep);
+            sdmm_mix* m = nullptr;
+            SDMM_TRY(sdmm_create(K, &ep, g->device, &m));
+            int r = sdmm_set_stream(m, (void*)g->st);
+            if (!r) r = sdmm_init_hemisphere(m, pos.data(), nrm.data(), npos, g->cfg.depth_prior,
+                                             (float)(3.0 * (double)diag / (double)npos), g->cfg.init_seed + (uint64_t)v);
+            if (r) { sdmm_destroy(m); return r; }
+            g->mix[(size_t)v] = m;
+        }
+        double sc[9];
+        SDMM_TRY(sdmm_get_state(g->mix[(size_t)v], sc, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr));
+        iters.push_back(sc[3] < 4.0 ? 2 : 1);
+        mixes.push_back(g->mix[(size_t)v]);
+        bseg.push_back(b);
+    }
+    const int64_t prefix = bseg.back();
+    sdmm_samples s{};
+    for (int i = 0; i < 6; ++i) s.x[i] = P + i * g->cap;
+    s.w = P + 9 * g->cap;
+    s.n = prefix;
+    SDMM_TRY(sdmm_em_step_batched_iters(mixes.data(), (int)mixes.size(), &s, bseg.data(), iters.data()));
+    // (4) the optimised leaves' data is cleared (:308-309): drop the prefix
+    if (prefix > 0) {
+        const int64_t rest = g->n - prefix;
+        float* Q = g->pool[1 - g->cur];
+        if (rest > 0) {
+            for (int p = 0; p < kPlanes; ++p)
+                HIP_TRY(hipMemcpyAsync(Q + p * g->cap, P + p * g->cap + prefix, sizeof(float) * (size_t)rest,
+                                       hipMemcpyDeviceToDevice, g->st));
+            HIP_TRY(hipMemcpyAsync(g->pnode[1 - g->cur], g->pnode[g->cur] + prefix, sizeof(int32_t) * (size_t)rest,
+                                   hipMemcpyDeviceToDevice, g->st));
+        }
+        g->cur = 1 - g->cur;
+        g->n = rest;
+    }
+    SDMM_TRY(bind(g));
+    HIP_TRY(hipStreamSynchronize(g->st));
+    return SDMM_OK;
+}
+
+// One iteration of render(): a render pass (guided once any leaf is trained,
+// :311-316), its training data, then optimize() while training
+// (m_still_training, :416, :495-501).
+int sdmm_guiding_iteration(sdmm_guiding* g, sdmm_scene* scene, const sdmm_li_params* p, uint64_t push_seed,
+                           int train, float* image, sdmm_li_stats* li_stats, sdmm_guiding_stats* out) {
+    if (!g || !scene || !p || !image) return fail(SDMM_E_INVALID, "invalid argument");
+    sdmm_li_params q = *p;
+    q.guided = sdmm_guiding_trained(g) > 0 ? 1 : 0;
+    sdmm_path_vertices v{};
+    SDMM_TRY(sdmm_li_render(scene, g->tree, nullptr, &q, image, train ? &v : nullptr, li_stats));
+    if (!train) return SDMM_OK;
+    SDMM_TRY(sdmm_guiding_push(g, &v, push_seed));
+    return sdmm_guiding_optimize(g, p->spp * 1, out);
+}
+
+}  // extern "C"

@@ -1,0 +1,493 @@
+// render.hip -- the guided path tracer's device side: SDMMRenderer::Li
+// (sdmm_proc.cpp:592-968) as a wavefront over an analytic quad scene, and the
+// training-data producer of its tail (push_back_data + jittered neighbour
+// routing, :876-965).
+//
+// One path per thread, path state in SoA planes in HBM.  A bounce is three
+// launches on one stream:
+//   li_query_kernel   the loop head for every live path (:649-691): depth cap,
+//                     condition c = (p - scene_min) / spatial_norm
+//                     (createCondition :263-273), the BSDF direction and the
+//                     plugin's BSDF/guide choice (h = 0.5, :383-392);
+//   the guided wavefront (guide.hip, sdmm_guide_pdf_wavefront): the leaf's
+//                     conditional built once per query, then a GMM sample or
+//                     the gmmPdf of the BSDF direction (:368-421, :510-590);
+//   li_shade_kernel   the rest of sampleSurface (:392-507) and of the loop
+//                     body (:759-871): BSDF weight / mixture pdf, throughput,
+//                     the next ray, the emitter it hits, recordRadiance and the
+//                     saved vertex (:815-846), Russian roulette.
+// The camera kernel starts the paths (first hit, its emission: :641-677); the
+// film kernel averages each pixel's samples in sample order (box filter).
+//
+// Scene: parallelograms (Mitsuba rectangles; a cube is six), diffuse BSDFs
+// (diffuse.cpp: cosine-hemisphere sampling, f = rho / pi), one-sided area
+// emitters (area.cpp: Le = radiance on the normal side).  No NEE (the plugin's
+// NEE block is compiled out, :700-734; emitterPdf = 0, MIS weight 1, :811-816).
+//
+// Random numbers: counter-based (rng_uniform below), one fixed slot per
+// (path, stream, dimension) -- a path's outcome does not depend on which other
+// paths run, nor on the order the reference's sampler would consume numbers;
+// the reference's Mitsuba sampler itself is not reproducible here.
+#include "sdmm_device.h"
+#include "render_device.h"
+
+#include <hipcub/hipcub.hpp>
+
+#pragma clang fp contract(off)
+
+namespace sdmm {
+
+// RNG, scene / path / query records: render_device.h
+constexpr float kEpsilon = 1e-4f;          // Mitsuba single-precision Epsilon (ray mint)
+constexpr float kInvPi = 0.31830988618379067154f;
+
+__device__ __forceinline__ float dot3(const float a[3], const float b[3]) {
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+}
+
+// closest hit with t in (mint, maxt); -1: none
+__device__ __forceinline__ int intersect(const SceneDev& S, const float o[3], const float d[3], float mint,
+                                         float maxt, float& t_hit) {
+    int best = -1;
+    float tb = maxt;
+    for (int q = 0; q < S.n_quads; ++q) {
+        const QuadDev& Q = S.quads[q];
+        const float denom = dot3(d, Q.n);
+        if (denom == 0.0f) continue;
+        const float r0[3] = {Q.p0[0] - o[0], Q.p0[1] - o[1], Q.p0[2] - o[2]};
+        const float t = dot3(r0, Q.n) / denom;
+        if (!(t > mint && t < tb)) continue;
+        const float r[3] = {o[0] + t * d[0] - Q.p0[0], o[1] + t * d[1] - Q.p0[1], o[2] + t * d[2] - Q.p0[2]};
+        const float a = dot3(r, Q.g1), b = dot3(r, Q.g2);
+        if (a < 0.0f || a > 1.0f || b < 0.0f || b > 1.0f) continue;
+        tb = t;
+        best = q;
+    }
+    t_hit = tb;
+    return best;
+}
+
+// Frame(n): Mitsuba coordinateSystem (s, t, n)
+__device__ __forceinline__ void frame_of(const float n[3], float s[3], float t[3]) {
+    if (fabsf(n[0]) > fabsf(n[1])) {
+        const float inv = 1.0f / sqrtf(n[0] * n[0] + n[2] * n[2]);
+        t[0] = n[2] * inv; t[1] = 0.0f; t[2] = -n[0] * inv;
+    } else {
+        const float inv = 1.0f / sqrtf(n[1] * n[1] + n[2] * n[2]);
+        t[0] = 0.0f; t[1] = n[2] * inv; t[2] = -n[1] * inv;
+    }
+    s[0] = t[1] * n[2] - t[2] * n[1];
+    s[1] = t[2] * n[0] - t[0] * n[2];
+    s[2] = t[0] * n[1] - t[1] * n[0];
+}
+
+// warp::squareToCosineHemisphere (concentric disk, z guarded to 1e-10)
+__device__ __forceinline__ void cosine_hemisphere(float u0, float u1, float w[3]) {
+    const float r1 = 2.0f * u0 - 1.0f, r2 = 2.0f * u1 - 1.0f;
+    float r, phi;
+    if (r1 == 0.0f && r2 == 0.0f) {
+        r = 0.0f; phi = 0.0f;
+    } else if (r1 * r1 > r2 * r2) {
+        r = r1; phi = (float)(kPi / 4.0) * (r2 / r1);
+    } else {
+        r = r2; phi = (float)(kPi / 2.0) - (r1 / r2) * (float)(kPi / 4.0);
+    }
+    float sp, cp;
+    sincosf(phi, &sp, &cp);
+    w[0] = r * cp;
+    w[1] = r * sp;
+    float z = sqrtf(fmaxf(0.0f, 1.0f - w[0] * w[0] - w[1] * w[1]));
+    if (z == 0.0f) z = 1e-10f;
+    w[2] = z;
+}
+
+__device__ __forceinline__ float& vrec(const PathsDev& P, int f, int v, int64_t p) {
+    return P.rec[((int64_t)f * P.V + v) * P.P + p];
+}
+
+// recordRadiance (:628-637): every saved vertex's weight gets the radiance
+// divided by its throughput and sampling pdf (Vertex::record, :615-621)
+__device__ __forceinline__ void record_radiance(const PathsDev& P, int64_t p, int nv, const float rad[3]) {
+    for (int v = 0; v < nv; ++v) {
+        const float pdf = vrec(P, 6, v, p);
+        for (int ch = 0; ch < 3; ++ch) {
+            const float thr = vrec(P, 3 + ch, v, p);
+            if (thr > kEpsilon) vrec(P, ch, v, p) += rad[ch] / (thr * pdf);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// camera rays: pixel = path / spp (box filter, uniform jitter), Mitsuba's
+// perspective mapping (fov along x): local d = ((1 - 2 sx) tan, (1 - 2 sy) tan / aspect, 1)
+__global__ void __launch_bounds__(256)
+li_camera_kernel(SceneDev S, PathsDev P, int64_t path0, int spp, uint64_t seed) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.P) return;
+    const int64_t gp = path0 + i;
+    const int64_t pix = gp / spp;
+    const int px = (int)(pix % S.width), py = (int)(pix / S.width);
+    const float sx = ((float)px + rng_uniform(seed, (uint64_t)gp, 0, 0)) / (float)S.width;
+    const float sy = ((float)py + rng_uniform(seed, (uint64_t)gp, 0, 1)) / (float)S.height;
+    float l[3] = {(1.0f - 2.0f * sx) * S.tanx, (1.0f - 2.0f * sy) * S.tanx / S.aspect, 1.0f};
+    const float inv = 1.0f / sqrtf(dot3(l, l));
+    for (int a = 0; a < 3; ++a) l[a] *= inv;
+    float d[3], o[3];
+    for (int r = 0; r < 3; ++r) {
+        d[r] = S.cam[4 * r] * l[0] + S.cam[4 * r + 1] * l[1] + S.cam[4 * r + 2] * l[2];
+        o[r] = S.cam[4 * r + 3];
+    }
+    const float dn = 1.0f / sqrtf(dot3(d, d));
+    for (int a = 0; a < 3; ++a) d[a] *= dn;
+    float t;
+    const int q = intersect(S, o, d, S.near_clip / l[2], INFINITY, t);
+    P.tr[i] = 1.0f; P.tg[i] = 1.0f; P.tb[i] = 1.0f;
+    P.nv[i] = 0;
+    P.dx[i] = d[0]; P.dy[i] = d[1]; P.dz[i] = d[2];
+    float L[3] = {0.0f, 0.0f, 0.0f};
+    if (q >= 0) {
+        const QuadDev& Q = S.quads[q];
+        P.px[i] = o[0] + t * d[0]; P.py[i] = o[1] + t * d[1]; P.pz[i] = o[2] + t * d[2];
+        // emission seen directly (:674-677), before any vertex exists
+        if (Q.emitter >= 0 && -dot3(d, Q.n) > 0.0f)
+            for (int ch = 0; ch < 3; ++ch) L[ch] = S.rad[3 * Q.emitter + ch];
+    }
+    P.lr[i] = L[0]; P.lg[i] = L[1]; P.lb[i] = L[2];
+    P.quad[i] = q;
+    P.depth[i] = q >= 0 ? 1 : -1;   // no hit: no environment emitter, the path ends
+}
+
+// ---------------------------------------------------------------------------
+// Loop head of bounce b for every live path.  guided: the tree holds trained
+// leaves (m_iteration != 0, :311-316); otherwise every query is BSDF only.
+__global__ void __launch_bounds__(256)
+li_query_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, int max_depth, int guided,
+                float h, uint64_t seed) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.P) return;
+    int depth = P.depth[i];
+    bool live = depth >= 0;
+    if (live && max_depth >= 0 && depth >= max_depth) live = false;   // :684-685
+    int q = live ? P.quad[i] : -1;
+    float n[3] = {0, 0, 0}, wi[3] = {0, 0, 0};
+    if (live) {
+        const QuadDev& QD = S.quads[q];
+        n[0] = QD.n[0]; n[1] = QD.n[1]; n[2] = QD.n[2];
+        wi[0] = -P.dx[i]; wi[1] = -P.dy[i]; wi[2] = -P.dz[i];
+        const float* rho = S.refl + 3 * QD.bsdf;
+        // diffuse: no reflection from the back side or with rho = 0 (the
+        // light's BSDF): sample and eval are 0, the path ends (:772-774)
+        if (!(dot3(wi, n) > 0.0f) || (rho[0] == 0.0f && rho[1] == 0.0f && rho[2] == 0.0f)) live = false;
+    }
+    if (!live) {
+        P.depth[i] = -1;
+        Q.c0[i] = -1.0f; Q.c1[i] = -1.0f; Q.c2[i] = -1.0f;   // outside the tree: no query work
+        Q.mode[i] = 1;
+        return;
+    }
+    const uint64_t gp = (uint64_t)(path0 + i);
+    const uint32_t stream = 1u + (uint32_t)bounce;
+    const float p[3] = {P.px[i], P.py[i], P.pz[i]};
+    Q.c0[i] = (p[0] - S.smin[0]) / S.snorm;
+    Q.c1[i] = (p[1] - S.smin[1]) / S.snorm;
+    Q.c2[i] = (p[2] - S.smin[2]) / S.snorm;
+    float s[3], t[3], w[3];
+    frame_of(n, s, t);
+    cosine_hemisphere(rng_uniform(seed, gp, stream, 0), rng_uniform(seed, gp, stream, 1), w);
+    Q.b0[i] = s[0] * w[0] + t[0] * w[1] + n[0] * w[2];
+    Q.b1[i] = s[1] * w[0] + t[1] * w[1] + n[1] * w[2];
+    Q.b2[i] = s[2] * w[0] + t[2] * w[1] + n[2] * w[2];
+    Q.u0[i] = rng_uniform(seed, gp, stream, 3);
+    Q.u1[i] = rng_uniform(seed, gp, stream, 4);
+    Q.u2[i] = rng_uniform(seed, gp, stream, 5);
+    Q.mode[i] = (!guided || rng_uniform(seed, gp, stream, 2) <= h) ? 1 : 0;
+    if (!guided) { Q.comp[i] = -1; Q.pdf[i] = 0.0f; }
+}
+
+// ---------------------------------------------------------------------------
+// The rest of the bounce (:392-507, :759-871).
+__global__ void __launch_bounds__(256)
+li_shade_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, int rr_depth, float h,
+                uint64_t seed) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.P) return;
+    int depth = P.depth[i];
+    if (depth < 0) return;
+    const QuadDev& QD = S.quads[P.quad[i]];
+    const float n[3] = {QD.n[0], QD.n[1], QD.n[2]};
+    const float* rho = S.refl + 3 * QD.bsdf;
+    const float c[3] = {Q.c0[i], Q.c1[i], Q.c2[i]};
+    const int comp = Q.comp[i];
+    const bool valid = comp != -1;      // validConditional (:368)
+    float wo[3], weight[3], mis_pdf;
+    if (!valid) {
+        // BSDF only, h = 1 (:316-323, :392-405): weight = rho, pdf = bsdfPdf
+        wo[0] = Q.b0[i]; wo[1] = Q.b1[i]; wo[2] = Q.b2[i];
+        const float cos_o = dot3(wo, n);
+        mis_pdf = kInvPi * cos_o;
+        for (int ch = 0; ch < 3; ++ch) weight[ch] = rho[ch];
+    } else if (Q.mode[i]) {
+        // BSDF chosen: (bsdf weight * bsdfPdf) / (h bsdfPdf + (1 - h) gmmPdf) (:393-407, :587-589)
+        wo[0] = Q.b0[i]; wo[1] = Q.b1[i]; wo[2] = Q.b2[i];
+        const float bsdf_pdf = kInvPi * dot3(wo, n);
+        mis_pdf = bsdf_pdf > 0.0f ? h * bsdf_pdf + (1.0f - h) * Q.pdf[i] : 0.0f;   // pdfSurface (:531-534)
+        for (int ch = 0; ch < 3; ++ch) weight[ch] = mis_pdf == 0.0f ? 0.0f : (rho[ch] * bsdf_pdf) / mis_pdf;
+    } else {
+        // guide sample: bsdf->eval / pdf (:456-463, :504-507)
+        wo[0] = Q.d0[i]; wo[1] = Q.d1[i]; wo[2] = Q.d2[i];
+        const float cos_o = dot3(wo, n);
+        const bool zero = (wo[0] == 0.0f && wo[1] == 0.0f && wo[2] == 0.0f) || !__builtin_isfinite(cos_o);
+        const float bsdf_pdf = (!zero && cos_o > 0.0f) ? kInvPi * cos_o : 0.0f;
+        mis_pdf = bsdf_pdf > 0.0f ? h * bsdf_pdf + (1.0f - h) * Q.pdf[i] : 0.0f;   // pdfSurface (:531-534)
+        for (int ch = 0; ch < 3; ++ch) weight[ch] = mis_pdf == 0.0f ? 0.0f : (rho[ch] * (kInvPi * cos_o)) / mis_pdf;
+    }
+    const float cos_o = dot3(wo, n);
+    // zero weight, or strict normals (wo . n_geo * cos(wo) <= 0, :777-780): the path ends
+    if ((weight[0] == 0.0f && weight[1] == 0.0f && weight[2] == 0.0f) || !(cos_o * cos_o > 0.0f) ||
+        !__builtin_isfinite(weight[0] + weight[1] + weight[2])) {
+        P.depth[i] = -1;
+        return;
+    }
+    float thr[3] = {P.tr[i] * weight[0], P.tg[i] * weight[1], P.tb[i] * weight[2]};
+    // trace and look for an emitter (rayIntersectAndLookForEmitter)
+    const float o[3] = {P.px[i], P.py[i], P.pz[i]};
+    float t;
+    const int q = intersect(S, o, wo, kEpsilon, INFINITY, t);
+    float value[3] = {0.0f, 0.0f, 0.0f};
+    if (q >= 0) {
+        const QuadDev& H = S.quads[q];
+        if (H.emitter >= 0 && -dot3(wo, H.n) > 0.0f)
+            for (int ch = 0; ch < 3; ++ch) value[ch] = S.rad[3 * H.emitter + ch];
+    }
+    int nv = P.nv[i];
+    if (value[0] != 0.0f || value[1] != 0.0f || value[2] != 0.0f) {
+        const float rad[3] = {thr[0] * value[0], thr[1] * value[1], thr[2] * value[2]};
+        P.lr[i] += rad[0]; P.lg[i] += rad[1]; P.lb[i] += rad[2];
+        record_radiance(P, i, nv, rad);
+    }
+    // the saved vertex (cacheable: diffuse, :821-845)
+    if (nv < P.V) {
+        const float clamped = fmaxf(mis_pdf, 0.1f);
+        const float inv_pdf = 1.0f / clamped;
+        for (int ch = 0; ch < 3; ++ch) {
+            vrec(P, ch, nv, i) = value[ch] * inv_pdf;
+            vrec(P, 3 + ch, nv, i) = thr[ch];
+        }
+        vrec(P, 6, nv, i) = clamped;
+        for (int a = 0; a < 3; ++a) {
+            vrec(P, 7 + a, nv, i) = c[a];
+            vrec(P, 10 + a, nv, i) = wo[a];
+            vrec(P, 13 + a, nv, i) = n[a];
+        }
+        P.nv[i] = nv + 1;
+    }
+    // Russian roulette (:858-868)
+    bool live = q >= 0;
+    if (depth >= rr_depth && live) {
+        const float qq = fminf(fmaxf(thr[0], fmaxf(thr[1], thr[2])), 0.95f);
+        if (rng_uniform(seed, (uint64_t)(path0 + i), 1u + (uint32_t)bounce, 6) >= qq) live = false;
+        else for (int ch = 0; ch < 3; ++ch) thr[ch] /= qq;
+    }
+    P.tr[i] = thr[0]; P.tg[i] = thr[1]; P.tb[i] = thr[2];
+    P.dx[i] = wo[0]; P.dy[i] = wo[1]; P.dz[i] = wo[2];
+    if (live) {
+        P.px[i] = o[0] + t * wo[0]; P.py[i] = o[1] + t * wo[1]; P.pz[i] = o[2] + t * wo[2];
+        P.quad[i] = q;
+    }
+    P.depth[i] = live ? depth + 1 : -1;
+}
+
+// pixel mean over its spp samples, in sample order; image planes [3][W*H]
+__global__ void __launch_bounds__(256)
+li_film_kernel(PathsDev P, int64_t pix0, int64_t npix, int spp, int64_t plane, float* __restrict__ image) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= npix) return;
+    float acc[3] = {0.0f, 0.0f, 0.0f};
+    for (int s = 0; s < spp; ++s) {
+        const int64_t i = j * spp + s;
+        acc[0] += P.lr[i]; acc[1] += P.lg[i]; acc[2] += P.lb[i];
+    }
+    const float inv = 1.0f / (float)spp;
+    for (int ch = 0; ch < 3; ++ch) image[ch * plane + pix0 + j] = acc[ch] * inv;
+}
+
+// ---------------------------------------------------------------------------
+// Training-data producer (:876-965).  Per path, vertices d = nv-1 .. firstSaved:
+// find its leaf (with the leaf's box), push (point, normal, average weight)
+// there with a stats entry when the weight is finite (jmm isValidSample); then
+// nJitters = (d == nv-1) + (average > 1000) pushes to the leaf at position +
+// (u - 1/2) * leaf diagonal, a draw that lands outside the tree or in the same
+// leaf (equal box min) retried while fewer than 8 draws failed.  Pass 0 counts
+// a path's records, pass 1 writes (leaf, code) at its offset; code =
+// ((path * V + d) << 1) | stats.  Records keep (path, push) order.
+template <bool WRITE>
+__device__ __forceinline__ int produce_path(const STNodeDev* __restrict__ nodes, const PathsDev& P, int64_t p,
+                                            int64_t path0, int saved, uint64_t seed, uint32_t* keys,
+                                            int64_t* codes, int64_t off, int* lost) {
+    const int nv = P.nv[p];
+    const int first = nv - saved > 0 ? nv - saved : 0;
+    int cnt = 0;
+    for (int d = nv - 1; d >= first; --d) {
+        const float pos[3] = {vrec(P, 7, d, p), vrec(P, 8, d, p), vrec(P, 9, d, p)};
+        const int leaf = stree_find_point(nodes, pos[0], pos[1], pos[2]);
+        if (leaf < 0) {   // the reference throws (:924-930)
+            if (WRITE) atomicAdd(lost, 1);
+            continue;
+        }
+        const STNodeDev box = nodes[leaf];
+        const float avg = (vrec(P, 0, d, p) + vrec(P, 1, d, p) + vrec(P, 2, d, p)) * (1.0f / 3.0f);
+        const bool ok = __builtin_isfinite(avg);
+        const int64_t code = ((int64_t)p * P.V + d) << 1;
+        if (ok) {
+            if (WRITE) { keys[off + cnt] = (uint32_t)leaf; codes[off + cnt] = code | 1; }
+            ++cnt;
+        }
+        int jitters = (d >= nv - 1 ? 1 : 0) + (avg > 1000.0f ? 1 : 0);
+        int attempts = 0, draw = 0;
+        const float diag[3] = {box.mx[0] - box.mn[0], box.mx[1] - box.mn[1], box.mx[2] - box.mn[2]};
+        for (int j = 0; j < jitters; ++j) {
+            const uint64_t gp = (uint64_t)(path0 + p);
+            float jp[3];
+            for (int a = 0; a < 3; ++a)
+                jp[a] = pos[a] + (rng_uniform(seed, gp, kJitterStream + (uint32_t)d, 3 * draw + a) - 0.5f) * diag[a];
+            ++draw;
+            const int nb = stree_find_point(nodes, jp[0], jp[1], jp[2]);
+            bool same = nb < 0;
+            if (!same) {
+                const STNodeDev b = nodes[nb];
+                same = b.mn[0] == box.mn[0] && b.mn[1] == box.mn[1] && b.mn[2] == box.mn[2];
+            }
+            if (same) {
+                ++attempts;
+                if (attempts < 8) --j;
+                continue;
+            }
+            if (ok) {
+                if (WRITE) { keys[off + cnt] = (uint32_t)nb; codes[off + cnt] = code; }
+                ++cnt;
+            }
+        }
+    }
+    return cnt;
+}
+
+__global__ void __launch_bounds__(256)
+produce_count_kernel(const STNodeDev* __restrict__ nodes, PathsDev P, int64_t path0, int saved, uint64_t seed,
+                     int64_t* __restrict__ count) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P.P) return;
+    count[p] = produce_path<false>(nodes, P, p, path0, saved, seed, nullptr, nullptr, 0, nullptr);
+}
+
+__global__ void __launch_bounds__(256)
+produce_write_kernel(const STNodeDev* __restrict__ nodes, PathsDev P, int64_t path0, int saved, uint64_t seed,
+                     const int64_t* __restrict__ offset, uint32_t* __restrict__ keys, int64_t* __restrict__ codes,
+                     int* __restrict__ lost) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P.P) return;
+    (void)produce_path<true>(nodes, P, p, path0, saved, seed, keys, codes, offset[p], lost);
+}
+
+// leaf-contiguous records -> training planes
+__global__ void __launch_bounds__(256)
+produce_gather_kernel(PathsDev P, const int64_t* __restrict__ codes, int64_t n, float* x0, float* x1, float* x2,
+                      float* x3, float* x4, float* x5, float* n0, float* n1, float* n2, float* w,
+                      uint8_t* stats, const uint32_t* __restrict__ keys, int32_t* node, int64_t* source) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const int64_t code = codes[j];
+    const int64_t pv = code >> 1;
+    const int64_t p = pv / P.V;
+    const int d = (int)(pv % P.V);
+    x0[j] = vrec(P, 7, d, p); x1[j] = vrec(P, 8, d, p); x2[j] = vrec(P, 9, d, p);
+    x3[j] = vrec(P, 10, d, p); x4[j] = vrec(P, 11, d, p); x5[j] = vrec(P, 12, d, p);
+    if (n0) { n0[j] = vrec(P, 13, d, p); n1[j] = vrec(P, 14, d, p); n2[j] = vrec(P, 15, d, p); }
+    w[j] = (vrec(P, 0, d, p) + vrec(P, 1, d, p) + vrec(P, 2, d, p)) * (1.0f / 3.0f);
+    if (stats) stats[j] = (uint8_t)(code & 1);
+    if (node) node[j] = (int32_t)keys[j];
+    if (source) source[j] = pv;   // p * V + d
+}
+
+// seg[v] = first sorted position with key >= v, v = 0..num_nodes
+__global__ void produce_seg_kernel(const uint32_t* __restrict__ keys, int64_t n, int num_nodes,
+                                   int64_t* __restrict__ seg) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v > num_nodes) return;
+    int64_t lo = 0, count = n;
+    while (count > 0) {
+        const int64_t step = count / 2, it = lo + step;
+        if (keys[it] < (uint32_t)v) { lo = it + 1; count -= step + 1; }
+        else count = step;
+    }
+    seg[v] = lo;
+}
+
+// ---------------------------------------------------------------------------
+// host launchers
+static inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+
+hipError_t launch_li_camera(const SceneDev& S, const PathsDev& P, int64_t path0, int spp, uint64_t seed,
+                            hipStream_t st) {
+    hipLaunchKernelGGL(li_camera_kernel, grid_for(P.P), dim3(256), 0, st, S, P, path0, spp, seed);
+    return hipGetLastError();
+}
+hipError_t launch_li_query(const SceneDev& S, const PathsDev& P, const QueryDev& Q, int64_t path0, int bounce,
+                           int max_depth, int guided, float h, uint64_t seed, hipStream_t st) {
+    hipLaunchKernelGGL(li_query_kernel, grid_for(P.P), dim3(256), 0, st, S, P, Q, path0, bounce, max_depth, guided,
+                       h, seed);
+    return hipGetLastError();
+}
+hipError_t launch_li_shade(const SceneDev& S, const PathsDev& P, const QueryDev& Q, int64_t path0, int bounce,
+                           int rr_depth, float h, uint64_t seed, hipStream_t st) {
+    hipLaunchKernelGGL(li_shade_kernel, grid_for(P.P), dim3(256), 0, st, S, P, Q, path0, bounce, rr_depth, h, seed);
+    return hipGetLastError();
+}
+hipError_t launch_li_film(const PathsDev& P, int64_t pix0, int64_t npix, int spp, int64_t plane, float* image,
+                          hipStream_t st) {
+    hipLaunchKernelGGL(li_film_kernel, grid_for(npix), dim3(256), 0, st, P, pix0, npix, spp, plane, image);
+    return hipGetLastError();
+}
+
+size_t produce_temp_bytes(int64_t n_paths, int64_t n_records, int key_bits) {
+    size_t a = 0, b = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, a, (const int64_t*)nullptr, (int64_t*)nullptr, (int)n_paths);
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                             (const int64_t*)nullptr, (int64_t*)nullptr, (int)n_records, 0,
+                                             key_bits);
+    return a > b ? a : b;
+}
+
+// count + scan: offsets[p] (n_paths + 1 entries; offsets[n_paths] = total)
+hipError_t launch_produce_count(const void* nodes, const PathsDev& P, int64_t path0, int saved, uint64_t seed,
+                                int64_t* count, int64_t* offsets, void* temp, size_t temp_bytes, hipStream_t st) {
+    hipLaunchKernelGGL(produce_count_kernel, grid_for(P.P), dim3(256), 0, st, (const STNodeDev*)nodes, P, path0,
+                       saved, seed, count);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, count, offsets, (int)P.P + 1, st);
+}
+
+hipError_t launch_produce_records(const void* nodes, int num_nodes, int key_bits, const PathsDev& P, int64_t path0,
+                                  int saved, uint64_t seed, const int64_t* offsets, int64_t n_rec, uint32_t* keys0,
+                                  uint32_t* keys1, int64_t* codes0, int64_t* codes1, void* temp, size_t temp_bytes,
+                                  int64_t* seg_dev, int* lost, float* const x[6], float* const nrm[3], float* w,
+                                  uint8_t* stats, int32_t* node, int64_t* source, hipStream_t st) {
+    hipLaunchKernelGGL(produce_write_kernel, grid_for(P.P), dim3(256), 0, st, (const STNodeDev*)nodes, P, path0,
+                       saved, seed, offsets, keys0, codes0, lost);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || n_rec == 0) return e;
+    // stable: a leaf's records stay in (path, push) order
+    e = hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys0, keys1, codes0, codes1, (int)n_rec, 0, key_bits,
+                                           st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(produce_seg_kernel, grid_for(num_nodes + 1), dim3(256), 0, st, keys1, n_rec, num_nodes,
+                       seg_dev);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(produce_gather_kernel, grid_for(n_rec), dim3(256), 0, st, P, codes1, n_rec, x[0], x[1], x[2],
+                       x[3], x[4], x[5], nrm ? nrm[0] : nullptr, nrm ? nrm[1] : nullptr, nrm ? nrm[2] : nullptr, w,
+                       stats, keys1, node, source);
+    return hipGetLastError();
+}
+
+}  // namespace sdmm

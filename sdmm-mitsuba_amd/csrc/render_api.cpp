@@ -1,0 +1,282 @@
+// render_api.cpp -- host side of the device Li (render.hip) behind
+// include/sdmm_gpu.h: the analytic scene, the per-bounce launch sequence
+// (camera -> [query -> guided wavefront -> shade] x bounces -> film) and the
+// path / query / vertex buffers, grown on demand and reused across renders.
+#include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/sdmm_gpu.h"
+#include "render_device.h"
+
+namespace sdmm {
+hipError_t launch_li_camera(const SceneDev& S, const PathsDev& P, int64_t path0, int spp, uint64_t seed,
+                            hipStream_t st);
+hipError_t launch_li_query(const SceneDev& S, const PathsDev& P, const QueryDev& Q, int64_t path0, int bounce,
+                           int max_depth, int guided, float h, uint64_t seed, hipStream_t st);
+hipError_t launch_li_shade(const SceneDev& S, const PathsDev& P, const QueryDev& Q, int64_t path0, int bounce,
+                           int rr_depth, float h, uint64_t seed, hipStream_t st);
+hipError_t launch_li_film(const PathsDev& P, int64_t pix0, int64_t npix, int spp, int64_t plane, float* image,
+                          hipStream_t st);
+}  // namespace sdmm
+
+namespace sdmm_detail {
+int set_error(int code, const char* msg);
+int tree_stream(sdmm_stree* t, hipStream_t* st);   // sdmm_api.cpp: device nodes uploaded, the tree's stream
+}  // namespace sdmm_detail
+
+using namespace sdmm;
+
+struct sdmm_scene {
+    int device = 0;
+    SceneDev S{};
+    QuadDev* dquads = nullptr;
+    float* drefl = nullptr;
+    float* drad = nullptr;
+    float smin[3] = {0, 0, 0}, snorm = 1.0f, tmin[3] = {0, 0, 0}, tmax[3] = {0, 0, 0};
+    // per-render buffers (grown)
+    void* buf = nullptr;
+    size_t buf_bytes = 0;
+    int64_t cap_paths = 0;
+    int cap_v = 0;
+    PathsDev P{};
+    QueryDev Q{};
+    int64_t* dsum = nullptr;
+    void* temp = nullptr;
+    size_t temp_bytes = 0;
+};
+
+namespace {
+
+int fail(int code, const std::string& m) { return sdmm_detail::set_error(code, m.c_str()); }
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(SDMM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
+    } while (0)
+
+void cross3(const float a[3], const float b[3], float c[3]) {
+    c[0] = a[1] * b[2] - a[2] * b[1];
+    c[1] = a[2] * b[0] - a[0] * b[2];
+    c[2] = a[0] * b[1] - a[1] * b[0];
+}
+float dot3h(const float a[3], const float b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+
+// path + query + vertex planes for P paths with V vertex slots
+int grow(sdmm_scene* s, int64_t P, int V, hipStream_t st) {
+    if (P <= s->cap_paths && V <= s->cap_v && s->buf) return SDMM_OK;
+    const int64_t cap = std::max<int64_t>(P, s->cap_paths);
+    const int cv = std::max(V, s->cap_v);
+    auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+    const size_t f = al(sizeof(float) * (size_t)cap), i4 = al(sizeof(int32_t) * (size_t)cap), u1 = al((size_t)cap);
+    const size_t recb = al(sizeof(float) * (size_t)kVertexFields * (size_t)cv * (size_t)cap);
+    size_t tb = 0;
+    (void)hipcub::DeviceReduce::Sum(nullptr, tb, (const int32_t*)nullptr, (int64_t*)nullptr, (int)cap);
+    const size_t need = 12 * f + 3 * i4 + recb + 13 * f + u1 + i4 + 256 + al(tb);
+    HIP_TRY(hipStreamSynchronize(st));
+    if (s->buf) HIP_TRY(hipFree(s->buf));
+    s->buf = nullptr;
+    HIP_TRY(hipMalloc(&s->buf, need));
+    s->buf_bytes = need;
+    s->cap_paths = cap;
+    s->cap_v = cv;
+    char* b = (char*)s->buf;
+    auto take = [&](size_t n) { char* r = b; b += n; return r; };
+    float** pf[12] = {&s->P.px, &s->P.py, &s->P.pz, &s->P.dx, &s->P.dy, &s->P.dz,
+                      &s->P.tr, &s->P.tg, &s->P.tb, &s->P.lr, &s->P.lg, &s->P.lb};
+    for (float** q : pf) *q = (float*)take(f);
+    s->P.depth = (int*)take(i4);
+    s->P.quad = (int*)take(i4);
+    s->P.nv = (int*)take(i4);
+    s->P.rec = (float*)take(recb);
+    float** qf[13] = {&s->Q.c0, &s->Q.c1, &s->Q.c2, &s->Q.u0, &s->Q.u1, &s->Q.u2, &s->Q.b0,
+                      &s->Q.b1, &s->Q.b2, &s->Q.d0, &s->Q.d1, &s->Q.d2, &s->Q.pdf};
+    for (float** q : qf) *q = (float*)take(f);
+    s->Q.mode = (uint8_t*)take(u1);
+    s->Q.comp = (int32_t*)take(i4);
+    s->dsum = (int64_t*)take(256);
+    s->temp = take(al(tb));
+    s->temp_bytes = al(tb);
+    return SDMM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sdmm_scene_create(const sdmm_scene_desc* d, int device, sdmm_scene** out) {
+    if (!out || !d || d->n_quads < 1 || !d->quads || !d->bsdf || d->n_bsdfs < 1 || !d->reflectance ||
+        d->width < 1 || d->height < 1 || !(d->fov_x_deg > 0.0f && d->fov_x_deg < 180.0f))
+        return fail(SDMM_E_INVALID, "sdmm_scene_create: invalid description");
+    if (d->emitter && (d->n_emitters < 1 || !d->radiance))
+        return fail(SDMM_E_INVALID, "sdmm_scene_create: emitters without radiance");
+    *out = nullptr;
+    std::vector<QuadDev> qs((size_t)d->n_quads);
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int q = 0; q < d->n_quads; ++q) {
+        QuadDev& Q = qs[(size_t)q];
+        const float* v = d->quads + 9 * q;
+        for (int a = 0; a < 3; ++a) { Q.p0[a] = v[a]; Q.e1[a] = v[3 + a]; Q.e2[a] = v[6 + a]; }
+        float n[3];
+        cross3(Q.e1, Q.e2, n);
+        const float len = std::sqrt(dot3h(n, n));
+        if (!(len > 0.0f)) return fail(SDMM_E_INVALID, "sdmm_scene_create: degenerate quad");
+        const float sg = (d->flip_normals && d->flip_normals[q]) ? -1.0f : 1.0f;
+        for (int a = 0; a < 3; ++a) Q.n[a] = sg * n[a] / len;
+        // duals: g1 . e1 = 1, g1 . e2 = 0 (g1 ~ e2 x n), likewise g2
+        float a1[3], a2[3];
+        cross3(Q.e2, n, a1);
+        cross3(n, Q.e1, a2);
+        const float s1 = dot3h(Q.e1, a1), s2 = dot3h(Q.e2, a2);
+        for (int a = 0; a < 3; ++a) { Q.g1[a] = a1[a] / s1; Q.g2[a] = a2[a] / s2; }
+        Q.bsdf = d->bsdf[q];
+        Q.emitter = d->emitter ? d->emitter[q] : -1;
+        if (Q.bsdf < 0 || Q.bsdf >= d->n_bsdfs || Q.emitter < -1 || (Q.emitter >= 0 && Q.emitter >= d->n_emitters))
+            return fail(SDMM_E_INVALID, "sdmm_scene_create: material index out of range");
+        // scene AABB without the camera: the four corners
+        for (int c = 0; c < 4; ++c)
+            for (int a = 0; a < 3; ++a) {
+                const float x = Q.p0[a] + ((c & 1) ? Q.e1[a] : 0.0f) + ((c & 2) ? Q.e2[a] : 0.0f);
+                mn[a] = std::min(mn[a], x);
+                mx[a] = std::max(mx[a], x);
+            }
+    }
+    sdmm_scene* s = new (std::nothrow) sdmm_scene();
+    if (!s) return fail(SDMM_E_NOMEM, "out of host memory");
+    s->device = device;
+    // render() (volpath_sdmm.cpp:375-393): spatialNormalization = the largest
+    // extent; the tree box getAABB (:314-332)
+    float ext[3], norm = 0.0f;
+    for (int a = 0; a < 3; ++a) { ext[a] = mx[a] - mn[a]; norm = std::max(norm, ext[a]); }
+    for (int a = 0; a < 3; ++a) {
+        s->smin[a] = mn[a];
+        s->tmin[a] = 0.0f - 1e-5f;
+        s->tmax[a] = ext[a] / norm + 1e-5f;
+    }
+    s->snorm = norm;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipMalloc(&s->dquads, sizeof(QuadDev) * qs.size());
+    if (e == hipSuccess) e = hipMalloc(&s->drefl, sizeof(float) * 3 * (size_t)d->n_bsdfs);
+    if (e == hipSuccess && d->emitter) e = hipMalloc(&s->drad, sizeof(float) * 3 * (size_t)d->n_emitters);
+    if (e == hipSuccess) e = hipMemcpy(s->dquads, qs.data(), sizeof(QuadDev) * qs.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(s->drefl, d->reflectance, sizeof(float) * 3 * (size_t)d->n_bsdfs, hipMemcpyHostToDevice);
+    if (e == hipSuccess && d->emitter)
+        e = hipMemcpy(s->drad, d->radiance, sizeof(float) * 3 * (size_t)d->n_emitters, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        sdmm_scene_destroy(s);
+        return fail(SDMM_E_HIP, std::string("sdmm_scene_create: ") + hipGetErrorString(e));
+    }
+    SceneDev& S = s->S;
+    S.quads = s->dquads;
+    S.n_quads = d->n_quads;
+    S.refl = s->drefl;
+    S.rad = s->drad;
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 4; ++c) S.cam[4 * r + c] = d->camera_to_world[4 * r + c];
+    S.tanx = (float)std::tan(0.5 * (double)d->fov_x_deg * 3.14159265358979323846 / 180.0);
+    S.aspect = (float)d->width / (float)d->height;
+    S.near_clip = d->near_clip > 0.0f ? d->near_clip : 1e-2f;
+    S.width = d->width;
+    S.height = d->height;
+    for (int a = 0; a < 3; ++a) S.smin[a] = s->smin[a];
+    S.snorm = s->snorm;
+    *out = s;
+    return SDMM_OK;
+}
+
+void sdmm_scene_destroy(sdmm_scene* s) {
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    (void)hipDeviceSynchronize();
+    if (s->dquads) (void)hipFree(s->dquads);
+    if (s->drefl) (void)hipFree(s->drefl);
+    if (s->drad) (void)hipFree(s->drad);
+    if (s->buf) (void)hipFree(s->buf);
+    delete s;
+}
+
+int sdmm_scene_normalization(const sdmm_scene* s, float scene_min[3], float* spatial_norm, float tree_min[3],
+                             float tree_max[3]) {
+    if (!s) return fail(SDMM_E_INVALID, "null scene");
+    for (int a = 0; a < 3; ++a) {
+        if (scene_min) scene_min[a] = s->smin[a];
+        if (tree_min) tree_min[a] = s->tmin[a];
+        if (tree_max) tree_max[a] = s->tmax[a];
+    }
+    if (spatial_norm) *spatial_norm = s->snorm;
+    return SDMM_OK;
+}
+
+int sdmm_li_render(sdmm_scene* s, sdmm_stree* t, const sdmm_mix* const* node_mix, const sdmm_li_params* p,
+                   float* image, sdmm_path_vertices* vout, sdmm_li_stats* stats) {
+    if (!s || !t || !p || !image) return fail(SDMM_E_INVALID, "invalid argument");
+    const int64_t npix_all = (int64_t)s->S.width * s->S.height;
+    if (p->spp < 1 || p->pixel_begin < 0 || p->pixel_end > npix_all || p->pixel_end <= p->pixel_begin ||
+        p->rr_depth < 1 || p->max_depth == 0 || p->max_depth < -1 || p->saved_vertices < 1)
+        return fail(SDMM_E_INVALID, "sdmm_li_render: invalid parameters");
+    if (p->max_depth > 0 && p->saved_vertices < p->max_depth - 1)
+        return fail(SDMM_E_INVALID, "sdmm_li_render: saved_vertices < max_depth - 1");
+    if (p->guided && !(p->bsdf_fraction >= 0.0f && p->bsdf_fraction <= 1.0f))
+        return fail(SDMM_E_INVALID, "sdmm_li_render: bsdf_fraction outside [0, 1]");
+    const int64_t npix = p->pixel_end - p->pixel_begin;
+    const int64_t P = npix * p->spp;
+    if (P > INT32_MAX) return fail(SDMM_E_INVALID, "sdmm_li_render: at most 2^31 - 1 paths per call");
+    HIP_TRY(hipSetDevice(s->device));
+    hipStream_t st = nullptr;
+    int r = sdmm_detail::tree_stream(t, &st);
+    if (r) return r;
+    const int V = p->saved_vertices;
+    r = grow(s, P, V, st);
+    if (r) return r;
+    s->P.V = V;
+    s->P.P = P;
+    const int64_t path0 = p->pixel_begin * p->spp;
+    HIP_TRY(launch_li_camera(s->S, s->P, path0, p->spp, p->seed, st));
+    // bounces: rRec.depth 1 .. maxDepth - 1 scatter (:649, :684); unbounded
+    // paths stop at the vertex slots
+    const int bounces = p->max_depth > 0 ? p->max_depth - 1 : V;
+    const float h = p->bsdf_fraction;
+    for (int b = 0; b < bounces; ++b) {
+        HIP_TRY(launch_li_query(s->S, s->P, s->Q, path0, b, p->max_depth > 0 ? p->max_depth : INT32_MAX, p->guided,
+                                h, p->seed, st));
+        if (p->guided) {
+            const float* c[3] = {s->Q.c0, s->Q.c1, s->Q.c2};
+            const float* u[3] = {s->Q.u0, s->Q.u1, s->Q.u2};
+            const float* bd[3] = {s->Q.b0, s->Q.b1, s->Q.b2};
+            float* d[3] = {s->Q.d0, s->Q.d1, s->Q.d2};
+            r = sdmm_guide_pdf_wavefront(t, node_mix, P, c, u, bd, s->Q.mode, d, s->Q.pdf, s->Q.comp, nullptr);
+            if (r) return r;
+        }
+        HIP_TRY(launch_li_shade(s->S, s->P, s->Q, path0, b, p->rr_depth, h, p->seed, st));
+    }
+    HIP_TRY(launch_li_film(s->P, p->pixel_begin, npix, p->spp, npix_all, image, st));
+    if (vout) {
+        vout->n_paths = P;
+        vout->max_vertices = V;
+        vout->path0 = path0;
+        vout->rec = s->P.rec;
+        vout->nv = s->P.nv;
+    }
+    if (stats) {
+        // every traced bounce ray saves a vertex (all BSDFs here are cacheable)
+        size_t tb = s->temp_bytes;
+        HIP_TRY(hipcub::DeviceReduce::Sum(s->temp, tb, (const int32_t*)s->P.nv, s->dsum, (int)P, st));
+        int64_t seg = 0;
+        HIP_TRY(hipMemcpyAsync(&seg, s->dsum, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        stats->paths = P;
+        stats->segments = seg;
+    }
+    return SDMM_OK;
+}
+
+}  // extern "C"

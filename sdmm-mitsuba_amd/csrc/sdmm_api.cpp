@@ -18,6 +18,7 @@
 
 #include "../../include/sdmm_gpu.h"
 #include "sdmm_device.h"
+#include "render_device.h"
 
 #pragma clang fp contract(off)
 
@@ -70,7 +71,7 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
                              const float* const u[3], const float* const dgiven[3], float* const d[3],
                              float* pdf, int32_t* comp, int32_t* node_out, float norm2, float norm3, int cap,
                              int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
-                             const GuideSortScratch* sort);
+                             const GuideSortScratch* sort, const uint8_t* pmode = nullptr);
 hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* condCov, int64_t nq,
                                 const float* const c[3], const float* const u[3], const float* const dgiven[3],
                                 float* const d[3], float* pdf, int32_t* comp, const int32_t* material,
@@ -83,6 +84,14 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
 constexpr int kGuideCapMax = SDMM_GUIDE_CAP_MAX;
 hipError_t launch_sample_cdf(const float* cdf, int n, const float* u, int64_t nq, int32_t* out,
                              hipStream_t st);
+hipError_t launch_produce_count(const void* nodes, const PathsDev& P, int64_t path0, int saved, uint64_t seed,
+                                int64_t* count, int64_t* offsets, void* temp, size_t temp_bytes, hipStream_t st);
+hipError_t launch_produce_records(const void* nodes, int num_nodes, int key_bits, const PathsDev& P, int64_t path0,
+                                  int saved, uint64_t seed, const int64_t* offsets, int64_t n_rec, uint32_t* keys0,
+                                  uint32_t* keys1, int64_t* codes0, int64_t* codes1, void* temp, size_t temp_bytes,
+                                  int64_t* seg_dev, int* lost, float* const x[6], float* const nrm[3], float* w,
+                                  uint8_t* stats, int32_t* node, int64_t* source, hipStream_t st);
+size_t produce_temp_bytes(int64_t n_paths, int64_t n_records, int key_bits);
 }  // namespace sdmm
 
 using namespace sdmm;
@@ -913,6 +922,32 @@ int sdmm_mix_broadcast(sdmm_mix* const* mixes, int n_mix, const int32_t* owner, 
     }
     for (int i = 0; i < n_mix; ++i) mixes[i]->initialised = true;
     HIP_TRY(hipStreamSynchronize(st));
+    return SDMM_OK;
+}
+
+int sdmm_clone(const sdmm_mix* src, sdmm_mix** out) {
+    if (!src || !out) return fail(SDMM_E_INVALID, "invalid argument");
+    *out = nullptr;
+    sdmm_mix* m = nullptr;
+    int r = sdmm_create(src->K, &src->params, src->device, &m);
+    if (r) return r;
+    m->guide_cap = src->guide_cap;
+    m->guide_order = src->guide_order;
+    if (src->stream != m->stream) {
+        r = sdmm_set_stream(m, (void*)src->stream);   // ordered with the source's pending work
+        if (r) { sdmm_destroy(m); return r; }
+    }
+    // parameters, derived arrays, packed records and stepwise state: the block
+    // prefix before the stats (as sdmm_mix_broadcast)
+    const size_t bytes = (size_t)((char*)src->stats - (char*)src->block);
+    hipError_t e = hipSetDevice(src->device);
+    if (e == hipSuccess) e = hipMemcpyAsync(m->block, src->block, bytes, hipMemcpyDeviceToDevice, m->stream);
+    if (e != hipSuccess) {
+        sdmm_destroy(m);
+        return fail(SDMM_E_HIP, std::string("sdmm_clone: ") + hipGetErrorString(e));
+    }
+    m->initialised = src->initialised;
+    *out = m;
     return SDMM_OK;
 }
 
@@ -1862,7 +1897,7 @@ int st_upload_table(sdmm_stree* t, const sdmm_mix* const* node_mix) {
 
 int st_guide(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
              const float* const u[3], const float* const dgiven[3], float* const d[3], float* pdf, int32_t* comp,
-             int32_t* node_out) {
+             int32_t* node_out, const uint8_t* pmode = nullptr) {
     HIP_TRY(hipSetDevice(t->device));
     int r = st_upload(t);
     if (r) return r;
@@ -1884,7 +1919,7 @@ int st_guide(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const f
     const GuideSortScratch* sort = nq >= (1 << 14) ? &t->guide_sort : nullptr;
     HIP_TRY(launch_guide_tree(t->dnodes, t->dtab, t->tab_kmax, nq, c, u, dgiven, d, pdf, comp, node_out,
                               norm_const(2), norm_const(3), kGuideCapMax, t->guide_fb, t->guide_fb + 1,
-                              cus > 0 ? cus : 256, t->stream, sort));
+                              cus > 0 ? cus : 256, t->stream, sort, pmode));
     return SDMM_OK;
 }
 
@@ -1909,6 +1944,15 @@ int sdmm_guide_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t
     return st_guide(t, node_mix, nq, c, u, nullptr, d, pdf, comp, node_out);
 }
 
+int sdmm_guide_pdf_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
+                             const float* const u[3], const float* const dgiven[3], const uint8_t* pdf_mode,
+                             float* const d[3], float* pdf, int32_t* comp, int32_t* node_out) {
+    if (!t || nq < 0) return fail(SDMM_E_INVALID, "invalid argument");
+    if (nq == 0) return SDMM_OK;
+    if (!c || !u || !dgiven || !pdf_mode || !d || !pdf || !comp) return fail(SDMM_E_INVALID, "invalid argument");
+    return st_guide(t, node_mix, nq, c, u, dgiven, d, pdf, comp, node_out, pdf_mode);
+}
+
 int sdmm_pdf_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
                        const float* const d[3], float* pdf) {
     if (!t || nq < 0) return fail(SDMM_E_INVALID, "invalid argument");
@@ -1919,3 +1963,112 @@ int sdmm_pdf_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t n
 
 }  // extern "C"
 
+
+// ---------------------------------------------------------------------------
+// the device Li (render_api.cpp) runs on the tree's stream
+namespace sdmm_detail {
+int tree_stream(sdmm_stree* t, hipStream_t* st) {
+    HIP_TRY(hipSetDevice(t->device));
+    const int r = st_upload(t);
+    if (r) return r;
+    *st = t->stream;
+    return SDMM_OK;
+}
+}  // namespace sdmm_detail
+
+extern "C" {
+
+int sdmm_push_training(sdmm_stree* t, const sdmm_path_vertices* v, int saved_per_path, uint64_t seed,
+                       const sdmm_training_out* out, int64_t* n_out, int64_t* seg, int64_t* lost) {
+    if (!t || !v || !n_out || saved_per_path < 1 || v->n_paths < 0 || v->max_vertices < 1 ||
+        (v->n_paths > 0 && (!v->rec || !v->nv)))
+        return fail(SDMM_E_INVALID, "invalid argument");
+    const int64_t P = v->n_paths;
+    const int nn = (int)t->nodes.size();
+    *n_out = 0;
+    if (lost) *lost = 0;
+    if (P == 0) {
+        if (seg) for (int i = 0; i <= nn; ++i) seg[i] = 0;
+        return SDMM_OK;
+    }
+    if (P > INT32_MAX - 1) return fail(SDMM_E_INVALID, "push_training: at most 2^31 - 2 paths");
+    HIP_TRY(hipSetDevice(t->device));
+    int r = st_upload(t);
+    if (r) return r;
+    int key_bits = 1;
+    while ((1 << key_bits) <= nn) ++key_bits;
+    const int64_t max_rec = P * 3 * (int64_t)std::min(saved_per_path, v->max_vertices);
+    auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+    const size_t tb = al(produce_temp_bytes(P + 1, max_rec, key_bits));
+    const size_t cb = al(sizeof(int64_t) * (size_t)(P + 1));
+    // the records' count first: the sorted arrays are sized by it
+    const size_t need0 = 2 * cb + tb + al(sizeof(int64_t) * (size_t)(nn + 2)) + 256;
+    if (need0 > t->scratch_bytes) {
+        HIP_TRY(hipStreamSynchronize(t->stream));
+        if (t->scratch) HIP_TRY(hipFree(t->scratch));
+        t->scratch = nullptr;
+        HIP_TRY(hipMalloc(&t->scratch, need0));
+        t->scratch_bytes = need0;
+    }
+    PathsDev PD{};
+    PD.rec = const_cast<float*>(v->rec);
+    PD.nv = const_cast<int*>(v->nv);
+    PD.V = v->max_vertices;
+    PD.P = P;
+    char* b = (char*)t->scratch;
+    int64_t* count = (int64_t*)b;
+    int64_t* offs = (int64_t*)(b + cb);
+    void* temp = b + 2 * cb;
+    HIP_TRY(hipMemsetAsync(count + P, 0, sizeof(int64_t), t->stream));
+    HIP_TRY(launch_produce_count(t->dnodes, PD, v->path0, saved_per_path, seed, count, offs, temp, tb, t->stream));
+    int64_t n_rec = 0;
+    HIP_TRY(hipMemcpyAsync(&n_rec, offs + P, sizeof(int64_t), hipMemcpyDeviceToHost, t->stream));
+    HIP_TRY(hipStreamSynchronize(t->stream));
+    *n_out = n_rec;
+    if (!out) return SDMM_OK;   // count only
+    if (n_rec > out->capacity) return fail(SDMM_E_INVALID, "push_training: output capacity too small");
+    if (n_rec > 0) {
+        for (int i = 0; i < 6; ++i)
+            if (!out->x[i]) return fail(SDMM_E_INVALID, "push_training: output plane missing");
+        if (!out->w) return fail(SDMM_E_INVALID, "push_training: output weight plane missing");
+    }
+    const size_t kb = al(sizeof(uint32_t) * (size_t)std::max<int64_t>(n_rec, 1));
+    const size_t qb = al(sizeof(int64_t) * (size_t)std::max<int64_t>(n_rec, 1));
+    const size_t sb = al(sizeof(int64_t) * (size_t)(nn + 2));
+    const size_t need = 2 * cb + tb + 2 * kb + 2 * qb + sb + 256;
+    if (need > t->scratch_bytes) {
+        // keep the offsets: copy them out through a fresh buffer
+        void* nb = nullptr;
+        HIP_TRY(hipMalloc(&nb, need));
+        HIP_TRY(hipMemcpyAsync(nb, t->scratch, 2 * cb, hipMemcpyDeviceToDevice, t->stream));
+        HIP_TRY(hipStreamSynchronize(t->stream));
+        HIP_TRY(hipFree(t->scratch));
+        t->scratch = nb;
+        t->scratch_bytes = need;
+    }
+    b = (char*)t->scratch;
+    offs = (int64_t*)(b + cb);
+    temp = b + 2 * cb;
+    uint32_t* k0 = (uint32_t*)(b + 2 * cb + tb);
+    uint32_t* k1 = (uint32_t*)(b + 2 * cb + tb + kb);
+    int64_t* q0 = (int64_t*)(b + 2 * cb + tb + 2 * kb);
+    int64_t* q1 = (int64_t*)(b + 2 * cb + tb + 2 * kb + qb);
+    int64_t* sdev = (int64_t*)(b + 2 * cb + tb + 2 * kb + 2 * qb);
+    int* dlost = (int*)(b + 2 * cb + tb + 2 * kb + 2 * qb + sb);
+    HIP_TRY(hipMemsetAsync(dlost, 0, sizeof(int), t->stream));
+    if (n_rec == 0) HIP_TRY(hipMemsetAsync(sdev, 0, sizeof(int64_t) * (size_t)(nn + 1), t->stream));
+    float* ox[6];
+    for (int i = 0; i < 6; ++i) ox[i] = out->x[i];
+    float* on[3] = {out->normal[0], out->normal[1], out->normal[2]};
+    HIP_TRY(launch_produce_records(t->dnodes, nn, key_bits, PD, v->path0, saved_per_path, seed, offs, n_rec, k0, k1,
+                                   q0, q1, temp, tb, sdev, dlost, ox, out->normal[0] ? on : nullptr, out->w,
+                                   out->stats, out->node, out->source, t->stream));
+    int hl = 0;
+    if (seg) HIP_TRY(hipMemcpyAsync(seg, sdev, sizeof(int64_t) * (size_t)(nn + 1), hipMemcpyDeviceToHost, t->stream));
+    HIP_TRY(hipMemcpyAsync(&hl, dlost, sizeof(int), hipMemcpyDeviceToHost, t->stream));
+    HIP_TRY(hipStreamSynchronize(t->stream));
+    if (lost) *lost = hl;
+    return SDMM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,135 @@
+"""Analytic scenes for the device Li (sdmm_scene_* in include/sdmm_gpu.h).
+
+cornell_box(): the test suite's Cornell Box, test-suite/scenes/cornell-box/
+cornell-box.xml -- film 640x360 (:26-28), perspective fov 35 along x with the
+toWorld of :17-19, five rectangles (:75-116; flipNormals on the back, right
+and left walls), two cubes (:118-132), the area light (:134-143) and the
+diffuse reflectances of :36-73.  The integrator settings of the suite's
+_integrators/sdmm.xml: maxDepth = rrDepth = 10.
+
+Mitsuba shapes as parallelograms: a rectangle is [-1, 1]^2 x {0} under
+toWorld (normal +z), a cube [-1, 1]^3 (outward normals), both transformed by
+the 4x4 matrix of the XML (row major).
+
+The emitter's spectrum "400:0, 500:1600, 600:3180, 700:3680" (piecewise
+linear) is converted to linear sRGB here: integrated against the CIE 1931
+2-degree observer (the analytic multi-lobe fit of Wyman, Sloan and Shirley,
+JCGT 2013) over 360-830 nm, normalised by the integral of y-bar, then XYZ ->
+linear sRGB (D65).  Mitsuba's own RGB-mode conversion is not reproducible
+here (no Mitsuba); the image is therefore not compared with Mitsuba renders --
+the device Li is checked for unbiasedness and its training batches for
+parity with the host-routed reference instead (tests/test_gpu_li.py).
+"""
+import numpy as np
+
+CORNELL_MAX_DEPTH = 10       # _integrators/sdmm.xml: maxDepth
+CORNELL_RR_DEPTH = 10        # rrDepth = maxDepth
+
+_RECTS = [
+    # (matrix row major 3x4, bsdf, flipNormals)
+    ("-4.37114e-008 1 4.37114e-008 0 0 -8.74228e-008 2 0 1 4.37114e-008 1.91069e-015 0", "Floor", False),
+    ("-1 7.64274e-015 -1.74846e-007 0 8.74228e-008 8.74228e-008 -2 2 0 -1 -4.37114e-008 0", "Ceiling", False),
+    ("1.91069e-015 1 1.31134e-007 0 1 3.82137e-015 -8.74228e-008 1 -4.37114e-008 1.31134e-007 -2 -1",
+     "BackWall", True),
+    ("4.37114e-008 -1.74846e-007 2 1 1 3.82137e-015 -8.74228e-008 1 3.82137e-015 1 2.18557e-007 0",
+     "RightWall", True),
+    ("-4.37114e-008 8.74228e-008 -2 -1 1 3.82137e-015 -8.74228e-008 1 0 -1 -4.37114e-008 0", "LeftWall", True),
+]
+_CUBES = [
+    ("0.0851643 0.289542 1.31134e-008 0.328631 3.72265e-009 1.26563e-008 -0.3 0.3 "
+     "-0.284951 0.0865363 5.73206e-016 0.374592", "ShortBox"),
+    ("0.286776 0.098229 -2.29282e-015 -0.335439 -4.36233e-009 1.23382e-008 -0.6 0.6 "
+     "-0.0997984 0.282266 2.62268e-008 -0.291415", "TallBox"),
+]
+_LIGHT = ("4.700000e-02 -3.322060e-09 -1.561370e-09 -5.000000e-03 -4.108880e-09 7.806860e-10 -1.786000e-02 "
+          "1.980000e+00 4.108880e-09 3.800000e-02 1.661032e-09 -3.000000e-02")
+_BSDFS = {
+    "LeftWall": (0.63, 0.065, 0.05), "RightWall": (0.14, 0.45, 0.091), "Floor": (0.725, 0.71, 0.68),
+    "Ceiling": (0.725, 0.71, 0.68), "BackWall": (0.725, 0.71, 0.68), "ShortBox": (0.725, 0.71, 0.68),
+    "TallBox": (0.725, 0.71, 0.68), "Light": (0.0, 0.0, 0.0),
+}
+_LIGHT_SPD = [(400.0, 0.0), (500.0, 1600.0), (600.0, 3180.0), (700.0, 3680.0)]
+_CAMERA = "-1 0 0 0 0 1 0 1 0 0 -1 6.8 0 0 0 1"
+
+
+def _mat(s):
+    return np.array([float(x) for x in s.split()], np.float64).reshape(3, 4)
+
+
+def _cie_xyz(lam):
+    """CIE 1931 colour matching functions, multi-lobe analytic fit (Wyman et al. 2013)."""
+    def g(x, mu, s1, s2):
+        s = np.where(x < mu, s1, s2)
+        return np.exp(-0.5 * ((x - mu) / s) ** 2)
+    x = 1.056 * g(lam, 599.8, 37.9, 31.0) + 0.362 * g(lam, 442.0, 16.0, 26.7) - 0.065 * g(lam, 501.1, 20.4, 26.2)
+    y = 0.821 * g(lam, 568.8, 46.9, 40.5) + 0.286 * g(lam, 530.9, 16.3, 31.1)
+    z = 1.217 * g(lam, 437.0, 11.8, 36.0) + 0.681 * g(lam, 459.0, 26.0, 13.8)
+    return x, y, z
+
+
+def spectrum_to_rgb(spd):
+    """Piecewise-linear SPD (wavelength, value) -> linear sRGB (zero outside the samples)."""
+    lam = np.arange(360.0, 831.0, 1.0)
+    w, v = zip(*spd)
+    s = np.interp(lam, w, v, left=0.0, right=0.0)
+    xb, yb, zb = _cie_xyz(lam)
+    X, Y, Z = (np.sum(s * xb), np.sum(s * yb), np.sum(s * zb))
+    k = 1.0 / np.sum(yb)
+    X, Y, Z = X * k, Y * k, Z * k
+    m = np.array([[3.240479, -1.537150, -0.498535], [-0.969256, 1.875991, 0.041556],
+                  [0.055648, -0.204043, 1.057311]])
+    return np.maximum(m @ np.array([X, Y, Z]), 0.0)
+
+
+def _rect(M):
+    """Corner and edges with e1 x e2 along Mitsuba's normal (inverse transpose of +z)."""
+    A, t = M[:, :3], M[:, 3]
+    p0 = A @ np.array([-1.0, -1.0, 0.0]) + t
+    e1, e2 = A @ np.array([2.0, 0.0, 0.0]), A @ np.array([0.0, 2.0, 0.0])
+    return (p0, e2, e1) if np.linalg.det(A) < 0 else (p0, e1, e2)
+
+
+def _cube_faces(M):
+    A, t = M[:, :3], M[:, 3]
+    flip = np.linalg.det(A) < 0
+    faces = []
+    for ax in range(3):
+        b, c = (ax + 1) % 3, (ax + 2) % 3
+        for s in (1.0, -1.0):
+            u = np.zeros(3); u[b] = 2.0
+            v = np.zeros(3); v[c] = 2.0
+            if (s < 0) != flip:                 # u x v must point along s e_ax after the transform
+                u, v = v, u
+            corner = np.zeros(3); corner[ax] = s
+            corner -= 0.5 * u + 0.5 * v
+            faces.append((A @ corner + t, A @ u, A @ v))
+    return faces
+
+
+def cornell_box(width=640, height=360):
+    """sdmm_scene_desc fields for the Cornell Box (numpy arrays)."""
+    names = list(_BSDFS)
+    quads, bsdf, flip, emitter = [], [], [], []
+    for m, name, fl in _RECTS:
+        quads.append(np.concatenate(_rect(_mat(m))))
+        bsdf.append(names.index(name)); flip.append(int(fl)); emitter.append(-1)
+    for m, name in _CUBES:
+        for f in _cube_faces(_mat(m)):
+            quads.append(np.concatenate(f))
+            bsdf.append(names.index(name)); flip.append(0); emitter.append(-1)
+    quads.append(np.concatenate(_rect(_mat(_LIGHT))))
+    bsdf.append(names.index("Light")); flip.append(0); emitter.append(0)
+    cam = np.array([float(x) for x in _CAMERA.split()], np.float32)
+    return {
+        "quads": np.asarray(quads, np.float32).reshape(-1),
+        "flip_normals": np.asarray(flip, np.int32),
+        "bsdf": np.asarray(bsdf, np.int32),
+        "reflectance": np.asarray([_BSDFS[n] for n in names], np.float32).reshape(-1),
+        "emitter": np.asarray(emitter, np.int32),
+        "radiance": spectrum_to_rgb(_LIGHT_SPD).astype(np.float32),
+        "camera_to_world": cam,
+        "fov_x_deg": 35.0,
+        "near_clip": 1e-2,
+        "width": width,
+        "height": height,
+    }

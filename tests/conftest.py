@@ -62,10 +62,14 @@ def plog(request):
     is committed under profiles/)."""
     path = Path(os.environ.get("SDMM_PARITY_LOG", ROOT / "gpurun_out" / "parity_errors.jsonl"))
 
-    def record(quantity, realized, bound, **extra):
+    def record(quantity, realized, bound, lower=False, **extra):
+        """lower=True: `bound` is a lower bound (ok when realized >= bound)."""
         path.parent.mkdir(parents=True, exist_ok=True)
+        ok = float(realized) >= float(bound) if lower else float(realized) <= float(bound)
         row = {"test": request.node.nodeid, "quantity": quantity, "realized": float(realized),
-               "bound": float(bound), "ok": bool(float(realized) <= float(bound))}
+               "bound": float(bound), "ok": bool(ok)}
+        if lower:
+            row["bound_kind"] = "lower"
         row.update({k: (v if isinstance(v, (int, float, str, bool)) else str(v)) for k, v in extra.items()})
         with open(path, "a") as f:
             f.write(json.dumps(row) + "\n")
