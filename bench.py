@@ -188,6 +188,47 @@ def wavefront_bench(pkg, synth, batch, shard, tree, dev, stream, ct, ut, gout, t
             "guided_frac": float((comp >= 0).mean()), "scaling": "weak (replicas: queries per rank)"}
 
 
+def cornell_bench(pkg, dev, args, world):
+    """configs[0] on the device: the test suite's Cornell Box (640x360), K=16
+    per leaf, 64 spp rendered 8 spp per iteration, training (push + optimize)
+    while samplesRendered < sampleCount / 4 (volpath_sdmm.cpp:411-507), the
+    native guiding model (sdmm_guiding_iteration) with the device Li.  Replicas
+    only (each rank renders the whole image; no exchange).  "guided rays/s" =
+    bounce rays traced per second in the guided passes."""
+    import torch
+    scenes = importlib.import_module("sdmm_mitsuba_amd.scenes")
+    sc = pkg.Scene(scenes.cornell_box(640, 360), device=dev.index)
+    _, _, tmin, tmax = sc.normalization()
+    spp_total, spp_it = 64, 8
+    img = torch.zeros(3, 360, 640, device=dev)
+    acc = torch.zeros_like(img)
+    its = []
+    for rep in range(2):                          # the first run pages in code and scratch (untimed)
+        g = pkg.Guiding(tmin, tmax, device=dev.index)
+        acc.zero_()
+        its = []
+        torch.cuda.synchronize()
+        t_all = time.perf_counter()
+        for it, done in enumerate(range(0, spp_total, spp_it)):
+            train = done < spp_total // 4
+            t = time.perf_counter()
+            _, ls, gs = g.iteration(sc, spp_it, seed=1 + it, push_seed=1001 + it, train=train, image=img)
+            acc += img
+            torch.cuda.synchronize()
+            its.append({"ms": (time.perf_counter() - t) * 1e3, "train": train, "segments": ls["segments"],
+                        "paths": ls["paths"], "leaves": gs["leaves"] if train else None,
+                        "optimized": gs["optimized"] if train else None, "trained": g.trained})
+        total = time.perf_counter() - t_all
+    guided = [x for x in its if not x["train"]]
+    seg = sum(x["segments"] for x in guided)
+    gms = sum(x["ms"] for x in guided)
+    return {"workload": "Cornell Box 640x360, K=16 per leaf, 64 spp (8 per iteration, training for the first 16)",
+            "total_ms": total * 1e3, "guided_rays_per_s": seg / (gms * 1e-3),
+            "guided_paths_per_s": sum(x["paths"] for x in guided) / (gms * 1e-3),
+            "trained_leaves": its[-1]["trained"], "iterations": its,
+            "image_mean": float((acc / len(its)).mean().item()), "replicas": world}
+
+
 def large_k_bench(pkg, synth, batch, shard, dev, stream, timed, args, world, N, comm):
     """BASELINE configs[3] and [4] on one GPU: a full EM step at K=256 (Pool)
     and K=512 (Kitchen) on the same 2^20-sample batch (sample-sharded, RCCL
@@ -434,6 +475,9 @@ def main():
         # one sdmm_guide_wavefront call (replicas: Q/world queries per rank) ----
         out["guide_wavefront"] = wavefront_bench(pkg, synth, batch, shard, tree, dev, stream, ct, ut, gout,
                                                  timed, args, world)
+
+    if not args.no_extra:
+        out["cornell"] = cornell_bench(pkg, dev, args, world)
 
     if not args.no_extra and not args.no_large_k:
         out["large_k"] = large_k_bench(pkg, synth, batch, shard, dev, stream, timed, args, world, N, comm)

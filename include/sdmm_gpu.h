@@ -85,6 +85,15 @@ void sdmm_em_params_default(sdmm_em_params* p);
 
 /* Create a K-component mixture (1 <= K <= 512) on HIP device `device`. */
 int sdmm_create(int K, const sdmm_em_params* params, int device, sdmm_mix** out);
+/* Stream-ordered creation: the allocation (hipMallocAsync) and initialisation
+ * are enqueued on hip_stream, which the handle then uses; nothing waits on the
+ * host.  For the many small per-leaf mixtures of a guiding tree.  The stream
+ * must outlive the handle (its memory is freed on it). */
+int sdmm_create_on_stream(int K, const sdmm_em_params* params, int device, void* hip_stream, sdmm_mix** out);
+/* n such handles from ONE stream-ordered slab (one allocation, one
+ * initialisation launch for all); the slab is freed with its last handle. */
+int sdmm_create_many_on_stream(int K, const sdmm_em_params* params, int device, void* hip_stream, int n,
+                               sdmm_mix** out);
 void sdmm_destroy(sdmm_mix* m);
 int sdmm_num_components(const sdmm_mix* m);
 /* Diagnostics: E-step kernel layouts (components per lane, lanes per sample)
@@ -118,6 +127,13 @@ int sdmm_synchronize(sdmm_mix* m);
  * scene units; seed drives the PCG32 direction jitter. */
 int sdmm_init_hemisphere(sdmm_mix* m, const float* positions, const float* normals, int n_pos,
                          float depth_prior, float min_spatial_distance, uint64_t seed);
+
+/* sdmm_init_hemisphere for n mixtures of one K at once (mixture i: K/8
+ * positions / normals at positions + 3 (K/8) i, its own spatial distance and
+ * seed): one host synchronisation for the whole set (the guiding model's new
+ * leaves). */
+int sdmm_init_hemisphere_batched(sdmm_mix* const* mixes, int n, const float* positions, const float* normals,
+                                 float depth_prior, const float* min_spatial_distance, const uint64_t* seeds);
 
 /* Host-only variant (no device, no handle): writes the initial component
  * parameters, for data generators and tests.  Arrays sized K=8*n_pos. */
@@ -286,6 +302,9 @@ int sdmm_set_params(sdmm_mix* m, const float* weights, const float* means, const
  * scalars[9] = {heuristicTotalWeight, sgH, normalization, iterationsRun,
  * alpha, niPriorMinusOne, decreasePrior, trainingCutoff, lastStatus};
  * T[K], sgW[K], sgM[5K], sgC[25K] (double); bpriors[25K], bdepth[9K] (float). */
+/* iterations_run of n mixtures (StepwiseTangentEM::iterationsRun, the
+ * plugin's 2-while-below-4 schedule, volpath_sdmm.cpp:299-302), one wait. */
+int sdmm_iterations_run(const sdmm_mix* const* mixes, int n, int* out);
 int sdmm_get_state(const sdmm_mix* m, double* scalars, double* T, double* sgW, double* sgM,
                    double* sgC, float* bpriors, float* bdepth);
 int sdmm_set_state(sdmm_mix* m, const double* scalars, const double* T, const double* sgW,
@@ -333,6 +352,11 @@ int sdmm_stree_num_nodes(const sdmm_stree* t);
 int sdmm_stree_leaf_nodes(const sdmm_stree* t);
 int sdmm_stree_split_leaf_recurse(sdmm_stree* t, int node, const float* const p[3], int64_t n, int threshold);
 int sdmm_stree_split_leaves(sdmm_stree* t, const float* const p[3], int64_t n, int threshold, int max_leaf_nodes);
+/* split_leaf_recurse for n nodes at once (increasing ids), node i with its
+ * own counts[i] positions at planes p[3i..3i+2]: leaves split on parallel host
+ * threads, the new nodes numbered exactly as n sequential calls would. */
+int sdmm_stree_split_leaf_recurse_many(sdmm_stree* t, int n, const int32_t* nodes, const float* const* p,
+                                       const int64_t* counts, int threshold);
 /* aabb[6 * i] = min(3), max(3); child[2 * i] = children (-1, -1 for a leaf);
  * axis[i]: split axis.  Any output may be NULL. */
 int sdmm_stree_get_nodes(const sdmm_stree* t, float* aabb, int32_t* child, int32_t* axis);
@@ -408,6 +432,8 @@ int sdmm_get_em_params(const sdmm_mix* m, sdmm_em_params* p);
  * children start from their parent's distribution and optimizer (jmm
  * SNTree::createChildNode, sntree.h:172-205). */
 int sdmm_clone(const sdmm_mix* m, sdmm_mix** out);
+/* sdmm_clone of n handles of one K into one slab (on src[0]'s stream). */
+int sdmm_clone_many(const sdmm_mix* const* src, int n, sdmm_mix** out);
 int sdmm_restore_params(sdmm_mix* m, const sdmm_params_out* in);
 int sdmm_stree_set_nodes(sdmm_stree* t, int n, const float* aabb, const int32_t* child, const int32_t* axis);
 

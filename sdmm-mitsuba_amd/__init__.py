@@ -210,7 +210,8 @@ EXPORTED_SYMBOLS = [
     "sdmm_li_render", "sdmm_push_training", "sdmm_clone",
     "sdmm_guiding_config_default", "sdmm_guiding_create", "sdmm_guiding_destroy", "sdmm_guiding_tree",
     "sdmm_guiding_node_mixtures", "sdmm_guiding_trained", "sdmm_guiding_push", "sdmm_guiding_optimize",
-    "sdmm_guiding_iteration",
+    "sdmm_guiding_iteration", "sdmm_create_on_stream", "sdmm_create_many_on_stream", "sdmm_clone_many",
+    "sdmm_init_hemisphere_batched", "sdmm_iterations_run", "sdmm_stree_split_leaf_recurse_many",
 ]
 
 

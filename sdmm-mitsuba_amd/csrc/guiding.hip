@@ -24,6 +24,9 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -105,6 +108,36 @@ __global__ void pool_relabel_kernel(int32_t* __restrict__ node, const int32_t* _
 }
 
 inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+
+// out[(i * npos + j) * 6 + f]: point (f < 3) / normal (f >= 3) of record starts[i] + j
+__global__ void init_gather_kernel(const float* __restrict__ pool, int64_t cap, const int64_t* __restrict__ starts,
+                                   int nf, int npos, float* __restrict__ out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nf * npos) return;
+    const int i = t / npos, j = t % npos;
+    const int64_t r = starts[i] + j;
+    for (int f = 0; f < 3; ++f) {
+        out[(size_t)t * 6 + f] = pool[f * cap + r];
+        out[(size_t)t * 6 + 3 + f] = pool[(6 + f) * cap + r];
+    }
+}
+
+// SDMM_GUIDING_TIMING=1: host-clock phase times of optimize() on stderr
+struct PhaseClock {
+    bool on;
+    hipStream_t st;
+    std::chrono::steady_clock::time_point t;
+    explicit PhaseClock(hipStream_t s) : on(std::getenv("SDMM_GUIDING_TIMING") != nullptr), st(s),
+                                         t(std::chrono::steady_clock::now()) {}
+    void lap(const char* what) {
+        if (!on) return;
+        (void)hipStreamSynchronize(st);
+        const auto n = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[guiding] %-12s %8.2f ms\n", what,
+                     std::chrono::duration<double, std::milli>(n - t).count());
+        t = n;
+    }
+};
 
 }  // namespace
 
@@ -212,7 +245,8 @@ int order_pool(sdmm_guiding* g, const std::vector<uint8_t>& ready) {
 }
 
 // After a split: stats positions, pool records and mixtures of every split
-// leaf move to its new leaves.
+// leaf move to its new leaves.  A new node's split leaf is its first ancestor
+// that existed before (new nodes are numbered after every old one).
 int redistribute(sdmm_guiding* g, int old_nodes) {
     const int nn = sdmm_stree_num_nodes(g->tree);
     std::vector<int32_t> child(2 * (size_t)nn), parent((size_t)nn, -1);
@@ -221,41 +255,54 @@ int redistribute(sdmm_guiding* g, int old_nodes) {
         for (int c = 0; c < 2; ++c)
             if (child[2 * (size_t)i + c] >= 0) parent[(size_t)child[2 * (size_t)i + c]] = i;
     std::vector<uint8_t> was_split((size_t)nn, 0);
-    bool any = false;
     for (int v = 0; v < old_nodes; ++v)   // records only ever name leaves: an old node with children was split
-        if (child[2 * (size_t)v] >= 0) {
-            was_split[(size_t)v] = 1;
-            any = true;
-        }
+        if (child[2 * (size_t)v] >= 0) was_split[(size_t)v] = 1;
+    std::vector<int> origin((size_t)nn, -1);   // new node -> the split leaf it came from
+    for (int c = old_nodes; c < nn; ++c) {
+        int a = parent[(size_t)c];
+        while (a >= old_nodes) a = parent[(size_t)a];
+        origin[(size_t)c] = a;
+    }
     g->mix.resize((size_t)nn, nullptr);
     g->stats.resize((size_t)nn);
-    if (!any && g->n == 0) return SDMM_OK;
-    auto descends = [&](int f, int v) {
-        while (f >= 0 && f != v) f = parent[(size_t)f];
-        return f == v;
-    };
-    // mixtures: a copy of the parent's in every new leaf of its subtree
-    for (int v = 0; v < old_nodes; ++v) {
-        if (child[2 * (size_t)v] < 0 || !g->mix[(size_t)v]) continue;
-        for (int c = 0; c < nn; ++c) {
-            if (child[2 * (size_t)c] >= 0 || !descends(c, v)) continue;
-            sdmm_mix* m = nullptr;
-            SDMM_TRY(sdmm_clone(g->mix[(size_t)v], &m));
-            SDMM_TRY(sdmm_set_stream(m, (void*)g->st));
-            g->mix[(size_t)c] = m;
+    // mixtures: a copy of the split leaf's in each of its new leaves (one slab)
+    {
+        std::vector<const sdmm_mix*> src;
+        std::vector<int> dst;
+        for (int c = old_nodes; c < nn; ++c) {
+            const int v = origin[(size_t)c];
+            if (child[2 * (size_t)c] >= 0 || v < 0 || !g->mix[(size_t)v]) continue;
+            src.push_back(g->mix[(size_t)v]);
+            dst.push_back(c);
         }
-        sdmm_destroy(g->mix[(size_t)v]);
-        g->mix[(size_t)v] = nullptr;
+        std::vector<sdmm_mix*> made(src.size(), nullptr);
+        SDMM_TRY(sdmm_clone_many(src.data(), (int)src.size(), made.data()));   // (on the model's stream)
+        for (size_t i = 0; i < dst.size(); ++i) g->mix[(size_t)dst[i]] = made[i];
     }
-    // stats positions (host): through find on the device
-    for (int v = 0; v < old_nodes; ++v) {
-        if (child[2 * (size_t)v] < 0 || g->stats[(size_t)v].empty()) continue;
-        std::vector<float> pos;
-        pos.swap(g->stats[(size_t)v]);
-        const int64_t m = (int64_t)pos.size() / 3;
-        std::vector<float> planes(3 * (size_t)m);
-        for (int64_t i = 0; i < m; ++i)
-            for (int a = 0; a < 3; ++a) planes[(size_t)a * (size_t)m + (size_t)i] = pos[3 * (size_t)i + (size_t)a];
+    for (int v = 0; v < old_nodes; ++v)
+        if (was_split[(size_t)v] && g->mix[(size_t)v]) {
+            sdmm_destroy(g->mix[(size_t)v]);
+            g->mix[(size_t)v] = nullptr;
+        }
+    // stats positions of every split leaf through one device find; a position
+    // stays if its leaf descends from its split leaf (appended in order)
+    std::vector<int> src;
+    std::vector<float> planes;
+    int64_t m = 0;
+    for (int v = 0; v < old_nodes; ++v)
+        if (was_split[(size_t)v]) m += (int64_t)g->stats[(size_t)v].size() / 3;
+    if (m > 0) {
+        planes.resize(3 * (size_t)m);
+        src.reserve((size_t)m);
+        int64_t k = 0;
+        for (int v = 0; v < old_nodes; ++v) {
+            if (!was_split[(size_t)v]) continue;
+            const auto& st = g->stats[(size_t)v];
+            for (size_t i = 0; i < st.size() / 3; ++i, ++k) {
+                for (int a = 0; a < 3; ++a) planes[(size_t)a * (size_t)m + (size_t)k] = st[3 * i + (size_t)a];
+                src.push_back(v);
+            }
+        }
         float* dp = nullptr;
         int32_t* df = nullptr;
         HIP_TRY(hipMallocAsync((void**)&dp, sizeof(float) * 3 * (size_t)m, g->st));
@@ -268,11 +315,13 @@ int redistribute(sdmm_guiding* g, int old_nodes) {
         HIP_TRY(hipFreeAsync(dp, g->st));
         HIP_TRY(hipFreeAsync(df, g->st));
         HIP_TRY(hipStreamSynchronize(g->st));
+        for (int v = 0; v < old_nodes; ++v)
+            if (was_split[(size_t)v]) std::vector<float>().swap(g->stats[(size_t)v]);
         for (int64_t i = 0; i < m; ++i) {
             const int c = f[(size_t)i];
-            if (c < 0 || !descends(c, v)) continue;
+            if (c < old_nodes || origin[(size_t)c] != src[(size_t)i]) continue;   // outside the split leaf
             auto& s = g->stats[(size_t)c];
-            s.insert(s.end(), pos.begin() + 3 * i, pos.begin() + 3 * i + 3);
+            for (int a = 0; a < 3; ++a) s.push_back(planes[(size_t)a * (size_t)m + (size_t)i]);
         }
     }
     // pool records: relabel on the device
@@ -336,6 +385,17 @@ int sdmm_guiding_create(const float tree_min[3], const float tree_max[3], const 
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&g->st, hipStreamNonBlocking);
         if (e != hipSuccess) r = fail(SDMM_E_HIP, std::string("sdmm_guiding_create: ") + hipGetErrorString(e));
     }
+    if (!r) {
+        // the per-leaf mixtures are stream-ordered allocations from the
+        // device's default pool: keep its memory between synchronisations
+        // (the default threshold returns it at every sync, so each new leaf
+        // would grow the pool again)
+        hipMemPool_t pool = nullptr;
+        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess && pool) {
+            uint64_t keep = UINT64_MAX;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+        }
+    }
     if (!r) r = sdmm_stree_set_stream(g->tree, (void*)g->st);
     if (r) {
         sdmm_guiding_destroy(g);
@@ -385,6 +445,7 @@ int sdmm_guiding_trained(const sdmm_guiding* g) {
 int sdmm_guiding_push(sdmm_guiding* g, const sdmm_path_vertices* v, uint64_t seed) {
     if (!g || !v) return fail(SDMM_E_INVALID, "invalid argument");
     HIP_TRY(hipSetDevice(g->device));
+    PhaseClock clk(g->st);
     int64_t count = 0;
     SDMM_TRY(sdmm_push_training(g->tree, v, g->cfg.saved_per_path, seed, nullptr, &count, nullptr, nullptr));
     SDMM_TRY(grow_pool(g, g->n + count));
@@ -417,6 +478,7 @@ int sdmm_guiding_push(sdmm_guiding* g, const sdmm_path_vertices* v, uint64_t see
         for (int a = 0; a < 3; ++a) s.push_back(px[(size_t)a * (size_t)count + (size_t)i]);
     }
     g->n += count;
+    clk.lap("push");
     return SDMM_OK;
 }
 
@@ -428,20 +490,39 @@ int sdmm_guiding_push(sdmm_guiding* g, const sdmm_path_vertices* v, uint64_t see
 int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
     if (!g || spp < 0) return fail(SDMM_E_INVALID, "invalid argument");
     HIP_TRY(hipSetDevice(g->device));
+    PhaseClock clk(g->st);
     // (1) split by the leaves' stats positions, nodes in id order
     const int old_nodes = sdmm_stree_num_nodes(g->tree);
-    {
-        size_t tot = 0;
-        for (const auto& s : g->stats) tot += s.size() / 3;
-        std::vector<float> planes(3 * tot);
-        size_t k = 0;
-        for (const auto& s : g->stats)
-            for (size_t i = 0; i < s.size() / 3; ++i, ++k)
-                for (int a = 0; a < 3; ++a) planes[(size_t)a * tot + k] = s[3 * i + (size_t)a];
-        const float* p[3] = {planes.data(), planes.data() + tot, planes.data() + 2 * tot};
-        SDMM_TRY(sdmm_stree_split_leaves(g->tree, p, (int64_t)tot, g->cfg.split_threshold, g->cfg.max_leaf_nodes));
+    // split_leaf_recurse(i, threshold) for every node while leaf_nodes() <=
+    // the cap (:253-259), each leaf with its own stats positions (only a leaf
+    // holding more than the threshold can split)
+    if (sdmm_stree_leaf_nodes(g->tree) <= g->cfg.max_leaf_nodes) {
+        std::vector<int32_t> ch(2 * (size_t)old_nodes), nodes;
+        SDMM_TRY(sdmm_stree_get_nodes(g->tree, nullptr, ch.data(), nullptr));
+        std::vector<std::vector<float>> planes;
+        std::vector<const float*> pp;
+        std::vector<int64_t> counts;
+        for (int v = 0; v < old_nodes; ++v) {
+            const auto& st = g->stats[(size_t)v];
+            const int64_t m = (int64_t)st.size() / 3;
+            if (ch[2 * (size_t)v] >= 0 || m <= g->cfg.split_threshold) continue;
+            std::vector<float> pl(3 * (size_t)m);
+            for (int64_t i = 0; i < m; ++i)
+                for (int a3 = 0; a3 < 3; ++a3) pl[(size_t)a3 * (size_t)m + (size_t)i] = st[3 * (size_t)i + (size_t)a3];
+            planes.push_back(std::move(pl));
+            nodes.push_back(v);
+            counts.push_back(m);
+        }
+        for (size_t i = 0; i < planes.size(); ++i) {
+            const int64_t m = counts[i];
+            pp.insert(pp.end(), {planes[i].data(), planes[i].data() + m, planes[i].data() + 2 * m});
+        }
+        SDMM_TRY(sdmm_stree_split_leaf_recurse_many(g->tree, (int)nodes.size(), nodes.data(), pp.data(),
+                                                    counts.data(), g->cfg.split_threshold));
     }
+    clk.lap("split");
     if (sdmm_stree_num_nodes(g->tree) != old_nodes) SDMM_TRY(redistribute(g, old_nodes));
+    clk.lap("redistribute");
     const int nn = sdmm_stree_num_nodes(g->tree);
     std::vector<float> aabb(6 * (size_t)nn);
     std::vector<int32_t> child(2 * (size_t)nn);
@@ -458,6 +539,7 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
             ++n_ready;
         }
     }
+    clk.lap("order");
     g->total_spp += spp;
     if (out) {
         out->leaves = sdmm_stree_leaf_nodes(g->tree);
@@ -470,54 +552,78 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
     SDMM_TRY(order_pool(g, ready));
     std::vector<sdmm_mix*> mixes;
     std::vector<int64_t> bseg{0};
-    std::vector<int> iters;
     const int K = g->cfg.K, npos = K / 8;
     float* P = g->pool[g->cur];
-    for (int v = 0; v < nn; ++v) {
-        if (!ready[(size_t)v]) continue;
-        const int64_t a = g->seg[(size_t)v], b = g->seg[(size_t)v + 1];
-        if (!g->mix[(size_t)v]) {
-            // the first K/8 records' positions and normals (kMeansPlusPlus off,
-            // mixture_model_init.h:139-141); spatial distance 3 hmax / (K/8)
-            std::vector<float> pl(6 * (size_t)npos);
-            for (int f = 0; f < 3; ++f) {
-                HIP_TRY(hipMemcpyAsync(pl.data() + (size_t)f * npos, P + f * g->cap + a, sizeof(float) * npos,
-                                       hipMemcpyDeviceToHost, g->st));
-                HIP_TRY(hipMemcpyAsync(pl.data() + (size_t)(3 + f) * npos, P + (6 + f) * g->cap + a,
-                                       sizeof(float) * npos, hipMemcpyDeviceToHost, g->st));
-            }
-            HIP_TRY(hipStreamSynchronize(g->st));
-            std::vector<float> pos(3 * (size_t)npos), nrm(3 * (size_t)npos);
-            for (int i = 0; i < npos; ++i)
+    // new leaves: initializeSDMMContext from the first K/8 records' positions
+    // and normals (kMeansPlusPlus off, mixture_model_init.h:139-141), spatial
+    // distance 3 hmax(diagonal) / (K/8) (:132-135); one gather, one init batch
+    std::vector<int> fresh;
+    std::vector<int64_t> starts;
+    for (int v = 0; v < nn; ++v)
+        if (ready[(size_t)v] && !g->mix[(size_t)v]) {
+            fresh.push_back(v);
+            starts.push_back(g->seg[(size_t)v]);
+        }
+    if (!fresh.empty()) {
+        const int nf = (int)fresh.size();
+        int64_t* dstart = nullptr;
+        float* dinit = nullptr;
+        HIP_TRY(hipMallocAsync((void**)&dstart, sizeof(int64_t) * (size_t)nf, g->st));
+        HIP_TRY(hipMallocAsync((void**)&dinit, sizeof(float) * 6 * (size_t)npos * (size_t)nf, g->st));
+        HIP_TRY(hipMemcpyAsync(dstart, starts.data(), sizeof(int64_t) * (size_t)nf, hipMemcpyHostToDevice, g->st));
+        hipLaunchKernelGGL(init_gather_kernel, grid_for((int64_t)nf * npos), dim3(256), 0, g->st, P, g->cap, dstart,
+                           nf, npos, dinit);
+        HIP_TRY(hipGetLastError());
+        std::vector<float> init(6 * (size_t)npos * (size_t)nf);
+        HIP_TRY(hipMemcpyAsync(init.data(), dinit, sizeof(float) * init.size(), hipMemcpyDeviceToHost, g->st));
+        HIP_TRY(hipFreeAsync(dstart, g->st));
+        HIP_TRY(hipFreeAsync(dinit, g->st));
+        HIP_TRY(hipStreamSynchronize(g->st));
+        std::vector<float> pos(3 * (size_t)npos * (size_t)nf), nrm(3 * (size_t)npos * (size_t)nf), dist((size_t)nf);
+        std::vector<uint64_t> seeds((size_t)nf);
+        std::vector<sdmm_mix*> made((size_t)nf, nullptr);
+        sdmm_em_params ep;
+        sdmm_em_params_default(&ep);
+        int r = sdmm_create_many_on_stream(K, &ep, g->device, (void*)g->st, nf, made.data());
+        if (r) return r;
+        for (int i = 0; i < nf; ++i) {
+            const int v = fresh[(size_t)i];
+            for (int j = 0; j < npos; ++j)
                 for (int f = 0; f < 3; ++f) {
-                    pos[3 * (size_t)i + f] = pl[(size_t)f * npos + i];
-                    nrm[3 * (size_t)i + f] = pl[(size_t)(3 + f) * npos + i];
+                    const size_t o = ((size_t)i * npos + (size_t)j) * 6;
+                    pos[((size_t)i * npos + (size_t)j) * 3 + (size_t)f] = init[o + (size_t)f];
+                    nrm[((size_t)i * npos + (size_t)j) * 3 + (size_t)f] = init[o + 3 + (size_t)f];
                 }
             float diag = 0.0f;
             for (int a3 = 0; a3 < 3; ++a3)
                 diag = std::max(diag, aabb[6 * (size_t)v + 3 + a3] - aabb[6 * (size_t)v + a3]);
-            sdmm_em_params ep;
-            sdmm_em_params_default(&ep);
-            sdmm_mix* m = nullptr;
-            SDMM_TRY(sdmm_create(K, &ep, g->device, &m));
-            int r = sdmm_set_stream(m, (void*)g->st);
-            if (!r) r = sdmm_init_hemisphere(m, pos.data(), nrm.data(), npos, g->cfg.depth_prior,
-                                             (float)(3.0 * (double)diag / (double)npos), g->cfg.init_seed + (uint64_t)v);
-            if (r) { sdmm_destroy(m); return r; }
-            g->mix[(size_t)v] = m;
+            dist[(size_t)i] = (float)(3.0 * (double)diag / (double)npos);
+            seeds[(size_t)i] = g->cfg.init_seed + (uint64_t)v;
         }
-        double sc[9];
-        SDMM_TRY(sdmm_get_state(g->mix[(size_t)v], sc, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr));
-        iters.push_back(sc[3] < 4.0 ? 2 : 1);
-        mixes.push_back(g->mix[(size_t)v]);
-        bseg.push_back(b);
+        r = sdmm_init_hemisphere_batched(made.data(), nf, pos.data(), nrm.data(), g->cfg.depth_prior,
+                                                 dist.data(), seeds.data());
+        if (r) {
+            for (sdmm_mix* m : made) sdmm_destroy(m);
+            return r;
+        }
+        for (int i = 0; i < nf; ++i) g->mix[(size_t)fresh[(size_t)i]] = made[(size_t)i];
     }
+    for (int v = 0; v < nn; ++v) {
+        if (!ready[(size_t)v]) continue;
+        mixes.push_back(g->mix[(size_t)v]);
+        bseg.push_back(g->seg[(size_t)v + 1]);
+    }
+    std::vector<int> iters(mixes.size());
+    SDMM_TRY(sdmm_iterations_run(mixes.data(), (int)mixes.size(), iters.data()));
+    for (int& it : iters) it = it < 4 ? 2 : 1;   // (:299-302)
+    clk.lap("init");
     const int64_t prefix = bseg.back();
     sdmm_samples s{};
     for (int i = 0; i < 6; ++i) s.x[i] = P + i * g->cap;
     s.w = P + 9 * g->cap;
     s.n = prefix;
     SDMM_TRY(sdmm_em_step_batched_iters(mixes.data(), (int)mixes.size(), &s, bseg.data(), iters.data()));
+    clk.lap("em");
     // (4) the optimised leaves' data is cleared (:308-309): drop the prefix
     if (prefix > 0) {
         const int64_t rest = g->n - prefix;
@@ -534,6 +640,7 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
     }
     SDMM_TRY(bind(g));
     HIP_TRY(hipStreamSynchronize(g->st));
+    clk.lap("drop+bind");
     return SDMM_OK;
 }
 

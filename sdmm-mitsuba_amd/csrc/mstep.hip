@@ -517,6 +517,77 @@ mstep_single_kernel(int K, int Kp, const double* __restrict__ stats, int64_t nSa
 
 __global__ void set_f64_kernel(double* p, double v) { *p = v; }
 
+// StepwiseTangentEM constructor state: scalars, diagonal bPriors (bprior[i])
+// and bDepth (eps) per component
+struct InitScalars {
+    double v[SC_COUNT];
+    float bprior[5];
+};
+__global__ void init_state_kernel(int K, InitScalars a, float eps, double* __restrict__ sc, float* __restrict__ bp,
+                                  float* __restrict__ bd) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k == 0)
+        for (int i = 0; i < SC_COUNT; ++i) sc[i] = a.v[i];
+    if (k >= K) return;
+    for (int i = 0; i < 25; ++i) bp[25 * k + i] = (i % 6 == 0) ? a.bprior[i / 6] : 0.0f;
+    for (int i = 0; i < 9; ++i) bd[9 * k + i] = (i % 4 == 0) ? eps : 0.0f;
+}
+
+// n mixtures carved from one slab at a fixed byte stride: mixture i's arrays
+// are mixture 0's shifted by i * stride (blockIdx.y = i)
+template <class T>
+__device__ __forceinline__ T* shifted(T* p, size_t bytes) {
+    return p ? (T*)((char*)p + bytes) : p;
+}
+__global__ void init_state_many_kernel(int K, InitScalars a, float eps, double* sc, float* bp, float* bd,
+                                       size_t stride) {
+    const size_t off = (size_t)blockIdx.y * stride;
+    sc = shifted(sc, off); bp = shifted(bp, off); bd = shifted(bd, off);
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k == 0)
+        for (int i = 0; i < SC_COUNT; ++i) sc[i] = a.v[i];
+    if (k >= K) return;
+    for (int i = 0; i < 25; ++i) bp[25 * k + i] = (i % 6 == 0) ? a.bprior[i / 6] : 0.0f;
+    for (int i = 0; i < 9; ++i) bd[9 * k + i] = (i % 4 == 0) ? eps : 0.0f;
+}
+__global__ void __launch_bounds__(256)
+pack_many_kernel(int K, int Kp, CanonDev C, float* ep, float* gp, float norm5, size_t stride) {
+    const size_t off = (size_t)blockIdx.x * stride;
+    C.weights = shifted(C.weights, off); C.cdf = shifted(C.cdf, off); C.mean = shifted(C.mean, off);
+    C.cov = shifted(C.cov, off); C.to = shifted(C.to, off); C.cholL = shifted(C.cholL, off);
+    C.cholLInv = shifted(C.cholLInv, off); C.detInv = shifted(C.detInv, off);
+    C.muPremult = shifted(C.muPremult, off); C.condCov = shifted(C.condCov, off); C.margL = shifted(C.margL, off);
+    C.margDetInv = shifted(C.margDetInv, off); C.condL = shifted(C.condL, off);
+    C.condLInv = shifted(C.condLInv, off); C.condDetInv = shifted(C.condDetInv, off);
+    C.valid = shifted(C.valid, off);
+    ep = shifted(ep, off);
+    gp = shifted(gp, off);
+    for (int kk = threadIdx.x; kk < Kp; kk += blockDim.x) pack_component(kk, K, Kp, C, ep, gp, norm5);
+}
+
+hipError_t launch_init_pack_many(int n, int K, int Kp, const double* scal, const float* bprior, float eps,
+                                 double* sc, float* bp, float* bd, const CanonDev& C, float* ep, float* gp,
+                                 float norm5, size_t stride, hipStream_t st) {
+    InitScalars a;
+    for (int i = 0; i < SC_COUNT; ++i) a.v[i] = scal[i];
+    for (int i = 0; i < 5; ++i) a.bprior[i] = bprior[i];
+    hipLaunchKernelGGL(init_state_many_kernel, dim3((unsigned)((K + 63) / 64), (unsigned)n), dim3(64), 0, st, K, a,
+                       eps, sc, bp, bd, stride);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(pack_many_kernel, dim3((unsigned)n), dim3(256), 0, st, K, Kp, C, ep, gp, norm5, stride);
+    return hipGetLastError();
+}
+
+hipError_t launch_init_state(int K, const double* scal, const float* bprior, float eps, double* sc, float* bp,
+                             float* bd, hipStream_t st) {
+    InitScalars a;
+    for (int i = 0; i < SC_COUNT; ++i) a.v[i] = scal[i];
+    for (int i = 0; i < 5; ++i) a.bprior[i] = bprior[i];
+    hipLaunchKernelGGL(init_state_kernel, dim3((unsigned)((K + 63) / 64)), dim3(64), 0, st, K, a, eps, sc, bp, bd);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 hipError_t launch_set_f64(double* p, double v, hipStream_t st) {
     hipLaunchKernelGGL(set_f64_kernel, dim3(1), dim3(1), 0, st, p, v);

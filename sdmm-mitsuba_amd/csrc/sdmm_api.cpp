@@ -15,6 +15,8 @@
 #include <string>
 #include <vector>
 #include <algorithm>
+#include <atomic>
+#include <thread>
 
 #include "../../include/sdmm_gpu.h"
 #include "sdmm_device.h"
@@ -52,6 +54,11 @@ hipError_t launch_set_all(int K, int Kp, const double* mean, const double* cov, 
                           float* ep, float* gp, float norm5, hipStream_t st);
 hipError_t launch_pack_all(int K, int Kp, const CanonDev& C, float* ep, float* gp, float norm5,
                            hipStream_t st);
+hipError_t launch_init_state(int K, const double* scal, const float* bprior, float eps, double* sc, float* bp,
+                             float* bd, hipStream_t st);
+hipError_t launch_init_pack_many(int n, int K, int Kp, const double* scal, const float* bprior, float eps,
+                                 double* sc, float* bp, float* bd, const CanonDev& C, float* ep, float* gp,
+                                 float norm5, size_t stride, hipStream_t st);
 hipError_t launch_mstep(int K, int Kp, const double* stats, int64_t nSamples, const CanonDev& C,
                         const EmStateDev& S, float* ep, float* gp, float norm5, double* wmean, double* wcov,
                         hipStream_t st);
@@ -227,6 +234,14 @@ void hemisphere_init(const float* positions, const float* normals, int nPosition
 }  // namespace
 
 // ==========================================================================
+// one stream-ordered allocation holding the blocks of many mixtures; freed
+// with its last mixture
+struct Slab {
+    void* p = nullptr;
+    int refs = 0;
+    hipStream_t st = nullptr;
+};
+
 struct sdmm_mix {
     int K = 0, Kp = 0, cpl = 1, lps = 64;   // statistics E-step layout
     int rcpl = 2, rlps = 64;                 // responsibility E-step layout (same Kp)
@@ -253,6 +268,8 @@ struct sdmm_mix {
 
     // device memory
     void* block = nullptr;       // canonical + state + packed records
+    bool block_async = false;    // stream-ordered allocation (sdmm_create_on_stream)
+    struct Slab* slab = nullptr; // block carved from a shared slab (sdmm_create_many_on_stream)
     CanonDev C{};
     EmStateDev S{};
     float* ep = nullptr;
@@ -519,7 +536,95 @@ void sdmm_em_params_default(sdmm_em_params* p) {
 
 size_t sdmm_stats_len(int K) { return 2 + (size_t)ST_FIELDS * (size_t)K; }
 
+namespace {
+int create_impl(int K, const sdmm_em_params* params, int device, hipStream_t ordered, bool on_stream,
+                sdmm_mix** out, void* ext_block = nullptr);
+}  // namespace
+
 int sdmm_create(int K, const sdmm_em_params* params, int device, sdmm_mix** out) {
+    return create_impl(K, params, device, nullptr, false, out);
+}
+
+int sdmm_create_on_stream(int K, const sdmm_em_params* params, int device, void* hip_stream, sdmm_mix** out) {
+    return create_impl(K, params, device, (hipStream_t)hip_stream, true, out);
+}
+
+}  // extern "C"
+
+namespace {
+
+// The handle's fixed-size device arrays, all 16-byte aligned, carved from one
+// block at base (base NULL: only the size); returns the block size.  The
+// parameters, derived arrays, packed records and stepwise state come first:
+// everything before `stats` is the mixture (copied by sdmm_clone, broadcast by
+// sdmm_mix_broadcast).
+size_t layout_block(sdmm_mix* m, char* base) {
+    const size_t Kc = (size_t)m->K;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        char* p = base ? base + off : nullptr;
+        off += (bytes + 15) / 16 * 16;
+        return p;
+    };
+    float* w = (float*)take(4 * Kc);
+    float* cdf = (float*)take(4 * Kc);
+    float* mean = (float*)take(24 * Kc);
+    float* cov = (float*)take(100 * Kc);
+    float* to = (float*)take(36 * Kc);
+    float* cl = (float*)take(100 * Kc);
+    float* cli = (float*)take(100 * Kc);
+    float* di = (float*)take(4 * Kc);
+    float* mp = (float*)take(24 * Kc);
+    float* cc = (float*)take(16 * Kc);
+    float* ml = (float*)take(36 * Kc);
+    float* mdi = (float*)take(4 * Kc);
+    float* cdl = (float*)take(16 * Kc);
+    float* cdli = (float*)take(16 * Kc);
+    float* cdi = (float*)take(4 * Kc);
+    int* valid = (int*)take(4 * Kc);
+    double* sc = (double*)take(8 * SC_COUNT);
+    double* T = (double*)take(8 * Kc);
+    double* sgW = (double*)take(8 * Kc);
+    double* sgM = (double*)take(40 * Kc);
+    double* sgC = (double*)take(200 * Kc);
+    float* bp = (float*)take(100 * Kc);
+    float* bd = (float*)take(36 * Kc);
+    float* ep = (float*)take(4 * (size_t)EP_FIELDS * m->Kp);
+    float* gp = (float*)take(4 * (size_t)GP_STRIDE * m->Kp);
+    double* stats = (double*)take(8 * (sdmm_stats_len(m->K) + 1));   // + the sample count of a sharded step
+    double* rscratch = (double*)take(8 * 16 * sdmm_stats_len(m->K));
+    double* tmean = (double*)take(48 * Kc);
+    double* tcov = (double*)take(200 * Kc);
+    if (base) {
+        m->C = CanonDev{w, cdf, mean, cov, to, cl, cli, di, mp, cc, ml, mdi, cdl, cdli, cdi, valid};
+        m->S = EmStateDev{sc, T, sgW, sgM, sgC, bp, bd};
+        m->ep = ep;
+        m->gp = gp;
+        m->stats = stats;
+        m->rscratch = rscratch;
+        m->tmp_mean = tmean;
+        m->tmp_cov = tcov;
+    }
+    return (off + 255) / 256 * 256;
+}
+
+void constructor_scalars(const sdmm_mix* m, double* scal) {
+    for (int i = 0; i < SC_COUNT; ++i) scal[i] = 0.0;
+    scal[SC_NORM] = 1.0;
+    scal[SC_ALPHA] = (double)m->params.alpha;
+    scal[SC_NI] = (double)m->params.ni_prior_minus_one;
+    scal[SC_DECP] = m->params.decrease_prior ? 1.0 : 0.0;
+    scal[SC_CUT] = 32.0;
+}
+
+// E-step occupancy per K (the layout choice depends on K and the process's
+// environment only): queried once
+struct OccCache {
+    int K = -1, resp = 0, stats = 0;
+};
+
+int create_impl(int K, const sdmm_em_params* params, int device, hipStream_t ordered, bool on_stream,
+                sdmm_mix** out, void* ext_block) {
     if (!out) return fail(SDMM_E_INVALID, "out is NULL");
     *out = nullptr;
     int cpl, lps;
@@ -567,85 +672,138 @@ int sdmm_create(int K, const sdmm_em_params* params, int device, sdmm_mix** out)
         const char* svv = std::getenv("SDMM_STATS_VARIANT");
         if (svv) m->svariant = std::atoi(svv);
     }
-    int unused = 0;
-    if (estep_occupancy(m->rcpl, m->rlps, m->Kp, &m->resp_blocks, &unused) != hipSuccess ||
-        estep_occupancy(m->cpl, m->lps, m->Kp, &unused, &m->stats_blocks) != hipSuccess)
-        return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
-    if (m->rtile == 2 && estep_resp_mfma_occupancy(m->rvariant, m->Kp, &m->resp_blocks) != hipSuccess)
-        return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
-    if (m->rtile == 1 && estep_resp_tile_occupancy(m->rvariant, &m->resp_blocks) != hipSuccess)
-        return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
-    if (m->stile && estep_stats_tile_occupancy(m->svariant, m->Kp, &m->stats_blocks) != hipSuccess)
-        return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
-    if (hipStreamCreateWithFlags(&m->own_stream, hipStreamNonBlocking) != hipSuccess)
-        return cleanup(fail(SDMM_E_HIP, "hipStreamCreate failed"));
-    m->stream = m->own_stream;
-
-    // one allocation for every fixed-size array (all 16-byte aligned)
-    const size_t Kc = (size_t)K;
-    const size_t f_canon = Kc * (1 + 1 + 6 + 25 + 9 + 25 + 25 + 1 + 6 + 4 + 9 + 1 + 4 + 4 + 1);
-    struct Piece { void** p; size_t bytes; };
-    std::vector<Piece> pieces;
-    float *w, *cdf, *mean, *cov, *to, *cl, *cli, *di, *mp, *cc, *ml, *mdi, *cdl, *cdli, *cdi;
-    int* valid;
-    double *sc, *T, *sgW, *sgM, *sgC;
-    float *bp, *bd;
-    auto add = [&](void* pp, size_t bytes) { pieces.push_back({(void**)pp, (bytes + 15) / 16 * 16}); };
-    add(&w, 4 * Kc); add(&cdf, 4 * Kc); add(&mean, 24 * Kc); add(&cov, 100 * Kc); add(&to, 36 * Kc);
-    add(&cl, 100 * Kc); add(&cli, 100 * Kc); add(&di, 4 * Kc); add(&mp, 24 * Kc); add(&cc, 16 * Kc);
-    add(&ml, 36 * Kc); add(&mdi, 4 * Kc); add(&cdl, 16 * Kc); add(&cdli, 16 * Kc); add(&cdi, 4 * Kc);
-    add(&valid, 4 * Kc);
-    add(&sc, 8 * SC_COUNT); add(&T, 8 * Kc); add(&sgW, 8 * Kc); add(&sgM, 40 * Kc); add(&sgC, 200 * Kc);
-    add(&bp, 100 * Kc); add(&bd, 36 * Kc);
-    add(&m->ep, 4 * (size_t)EP_FIELDS * m->Kp); add(&m->gp, 4 * (size_t)GP_STRIDE * m->Kp);
-    add(&m->stats, 8 * (sdmm_stats_len(K) + 1));   // + the sample count of a sharded step
-    add(&m->rscratch, 8 * 16 * sdmm_stats_len(K));
-    add(&m->tmp_mean, 48 * Kc); add(&m->tmp_cov, 200 * Kc);
-    (void)f_canon;
-    size_t total = 0;
-    for (auto& pc : pieces) total += pc.bytes;
-    if (hipMalloc(&m->block, total) != hipSuccess) return cleanup(fail(SDMM_E_HIP, "hipMalloc failed"));
-    if (hipMemset(m->block, 0, total) != hipSuccess) return cleanup(fail(SDMM_E_HIP, "hipMemset failed"));
-    char* base = (char*)m->block;
-    for (auto& pc : pieces) { *pc.p = base; base += pc.bytes; }
-    m->C = CanonDev{w, cdf, mean, cov, to, cl, cli, di, mp, cc, ml, mdi, cdl, cdli, cdi, valid};
-    m->S = EmStateDev{sc, T, sgW, sgM, sgC, bp, bd};
-
-    // StepwiseTangentEM constructor state (stepwise_tangent.h:221-252)
-    double scal[SC_COUNT] = {0};
-    scal[SC_HTW] = 0.0;
-    scal[SC_SGH] = 0.0;
-    scal[SC_NORM] = 1.0;
-    scal[SC_IT] = 0.0;
-    scal[SC_ALPHA] = (double)m->params.alpha;
-    scal[SC_NI] = (double)m->params.ni_prior_minus_one;
-    scal[SC_DECP] = m->params.decrease_prior ? 1.0 : 0.0;
-    scal[SC_CUT] = 32.0;
-    std::vector<float> bpr(25 * Kc, 0.0f), bde(9 * Kc, 0.0f);
-    const float eps = (float)m->params.epsilon;
-    for (size_t k = 0; k < Kc; ++k) {
-        for (int i = 0; i < 5; ++i) bpr[25 * k + 6 * i] = m->params.bprior[i];
-        for (int i = 0; i < 3; ++i) bde[9 * k + 4 * i] = eps;
+    static thread_local OccCache occ[8];
+    OccCache& oc = occ[(K * 7 + device) & 7];
+    if (oc.K == K * 64 + device) {
+        m->resp_blocks = oc.resp;
+        m->stats_blocks = oc.stats;
+    } else {
+        int unused = 0;
+        if (estep_occupancy(m->rcpl, m->rlps, m->Kp, &m->resp_blocks, &unused) != hipSuccess ||
+            estep_occupancy(m->cpl, m->lps, m->Kp, &unused, &m->stats_blocks) != hipSuccess)
+            return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
+        if (m->rtile == 2 && estep_resp_mfma_occupancy(m->rvariant, m->Kp, &m->resp_blocks) != hipSuccess)
+            return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
+        if (m->rtile == 1 && estep_resp_tile_occupancy(m->rvariant, &m->resp_blocks) != hipSuccess)
+            return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
+        if (m->stile && estep_stats_tile_occupancy(m->svariant, m->Kp, &m->stats_blocks) != hipSuccess)
+            return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
+        oc.K = K * 64 + device;
+        oc.resp = m->resp_blocks;
+        oc.stats = m->stats_blocks;
     }
-    if (hipMemcpy(sc, scal, sizeof(scal), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(bp, bpr.data(), 100 * Kc, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(bd, bde.data(), 36 * Kc, hipMemcpyHostToDevice) != hipSuccess)
-        return cleanup(fail(SDMM_E_HIP, "hipMemcpy of the initial state failed"));
+    if (on_stream) {
+        m->stream = ordered;
+        m->block_async = true;
+    } else {
+        if (hipStreamCreateWithFlags(&m->own_stream, hipStreamNonBlocking) != hipSuccess)
+            return cleanup(fail(SDMM_E_HIP, "hipStreamCreate failed"));
+        m->stream = m->own_stream;
+    }
+
+    if (ext_block) {   // a slab member: carve only (the caller initialises)
+        layout_block(m, (char*)ext_block);
+        *out = m;
+        return SDMM_OK;
+    }
+    // one allocation for every fixed-size array (all 16-byte aligned)
+    const size_t total = layout_block(m, nullptr);
+    if (on_stream) {
+        if (hipMallocAsync(&m->block, total, m->stream) != hipSuccess)
+            return cleanup(fail(SDMM_E_HIP, "hipMallocAsync failed"));
+        if (hipMemsetAsync(m->block, 0, total, m->stream) != hipSuccess)
+            return cleanup(fail(SDMM_E_HIP, "hipMemsetAsync failed"));
+    } else {
+        if (hipMalloc(&m->block, total) != hipSuccess) return cleanup(fail(SDMM_E_HIP, "hipMalloc failed"));
+        // on the handle's own stream: ordered before the init kernels below (a
+        // plain hipMemset runs on the null stream, which a non-blocking stream
+        // does not wait for -- it could land after them and zero the state)
+        if (hipMemsetAsync(m->block, 0, total, m->stream) != hipSuccess)
+            return cleanup(fail(SDMM_E_HIP, "hipMemsetAsync failed"));
+    }
+    layout_block(m, (char*)m->block);
+    const size_t Kc = (size_t)K;
+    double* sc = m->S.scalars;
+    float* bp = m->S.bPriors;
+    float* bd = m->S.bDepth;
+    // StepwiseTangentEM constructor state (stepwise_tangent.h:221-252)
+    double scal[SC_COUNT];
+    constructor_scalars(m, scal);
+    (void)Kc;
+    const float eps = (float)m->params.epsilon;
+    // the constructor state by a kernel, ordered on the handle's stream
+    if (launch_init_state(K, scal, m->params.bprior, eps, sc, bp, bd, m->stream) != hipSuccess)
+        return cleanup(fail(SDMM_E_HIP, "state init kernel launch failed"));
     // packed records: every component dead until init/set_params
     if (launch_pack_all(K, m->Kp, m->C, m->ep, m->gp, m->norm5, m->stream) != hipSuccess)
         return cleanup(fail(SDMM_E_HIP, "pack kernel launch failed"));
-    if (hipStreamSynchronize(m->stream) != hipSuccess)
+    if (!on_stream && hipStreamSynchronize(m->stream) != hipSuccess)
         return cleanup(fail(SDMM_E_HIP, "hipStreamSynchronize failed"));
     *out = m;
     return SDMM_OK;
 }
+
+// n handles whose blocks are carved from ONE stream-ordered slab: one
+// allocation, one memset, one init + one pack launch for the whole set
+int create_many(int K, const sdmm_em_params* params, int device, hipStream_t st, int n, sdmm_mix** out) {
+    if (n < 0 || (n > 0 && !out)) return fail(SDMM_E_INVALID, "invalid argument");
+    for (int i = 0; i < n; ++i) out[i] = nullptr;
+    if (n == 0) return SDMM_OK;
+    if (hipSetDevice(device) != hipSuccess) return fail(SDMM_E_HIP, "hipSetDevice failed");
+    Slab* slab = new (std::nothrow) Slab();
+    if (!slab) return fail(SDMM_E_NOMEM, "out of host memory");
+    slab->st = st;
+    sdmm_mix probe;
+    probe.K = K;
+    {
+        int cpl, lps;
+        if (K < 1 || choose_layout(K, cpl, lps)) { delete slab; return fail(SDMM_E_INVALID, "K must be in [1, 512]"); }
+        probe.Kp = cpl * lps;
+    }
+    const size_t stride = layout_block(&probe, nullptr);
+    if (hipMallocAsync(&slab->p, stride * (size_t)n, st) != hipSuccess) {
+        delete slab;
+        return fail(SDMM_E_HIP, "hipMallocAsync failed");
+    }
+    int r = SDMM_OK;
+    for (int i = 0; i < n && !r; ++i) {
+        r = create_impl(K, params, device, st, true, &out[i], (char*)slab->p + stride * (size_t)i);
+        if (!r) { out[i]->slab = slab; ++slab->refs; out[i]->block_async = false; }
+    }
+    hipError_t e = r ? hipSuccess : hipMemsetAsync(slab->p, 0, stride * (size_t)n, st);
+    if (!r && e == hipSuccess) {
+        sdmm_mix* m0 = out[0];
+        double scal[SC_COUNT];
+        constructor_scalars(m0, scal);
+        e = launch_init_pack_many(n, K, m0->Kp, scal, m0->params.bprior, (float)m0->params.epsilon, m0->S.scalars,
+                                  m0->S.bPriors, m0->S.bDepth, m0->C, m0->ep, m0->gp, m0->norm5, stride, st);
+    }
+    if (r || e != hipSuccess) {
+        for (int i = 0; i < n; ++i) { sdmm_destroy(out[i]); out[i] = nullptr; }
+        if (slab->refs == 0) { (void)hipFreeAsync(slab->p, st); delete slab; }
+        return r ? r : fail(SDMM_E_HIP, std::string("create_many: ") + hipGetErrorString(e));
+    }
+    return SDMM_OK;
+}
+
+}  // namespace
+
+extern "C" {
 
 void sdmm_destroy(sdmm_mix* m) {
     if (!m) return;
     (void)hipSetDevice(m->device);
     if (m->own_stream) (void)hipStreamSynchronize(m->own_stream);
     if (m->stream && m->stream != m->own_stream) (void)hipStreamSynchronize(m->stream);
-    if (m->block) (void)hipFree(m->block);
+    if (m->slab) {
+        if (--m->slab->refs == 0) {
+            (void)hipFreeAsync(m->slab->p, m->slab->st);
+            delete m->slab;
+        }
+    } else if (m->block) {
+        if (m->block_async) (void)hipFreeAsync(m->block, m->stream);
+        else (void)hipFree(m->block);
+    }
     if (m->partials) (void)hipFree(m->partials);
     if (m->guide_fb) (void)hipFree(m->guide_fb);
     if (m->staging) (void)hipFree(m->staging);
@@ -656,6 +814,40 @@ void sdmm_destroy(sdmm_mix* m) {
     if (m->batch_done) (void)hipEventDestroy(m->batch_done);
     if (m->own_stream) (void)hipStreamDestroy(m->own_stream);
     delete m;
+}
+
+int sdmm_create_many_on_stream(int K, const sdmm_em_params* params, int device, void* hip_stream, int n,
+                               sdmm_mix** out) {
+    return create_many(K, params, device, (hipStream_t)hip_stream, n, out);
+}
+
+int sdmm_clone_many(const sdmm_mix* const* src, int n, sdmm_mix** out) {
+    if (n < 0 || (n > 0 && (!src || !out))) return fail(SDMM_E_INVALID, "invalid argument");
+    if (n == 0) return SDMM_OK;
+    for (int i = 0; i < n; ++i) {
+        if (!src[i]) return fail(SDMM_E_INVALID, "NULL handle in src");
+        if (src[i]->K != src[0]->K || src[i]->device != src[0]->device)
+            return fail(SDMM_E_INVALID, "sources must share K and device");
+    }
+    const hipStream_t st = src[0]->stream;
+    HIP_TRY(hipSetDevice(src[0]->device));
+    for (int i = 1; i < n; ++i)
+        if (src[i]->stream != st) HIP_TRY(hipStreamSynchronize(src[i]->stream));
+    int r = create_many(src[0]->K, &src[0]->params, src[0]->device, st, n, out);
+    if (r) return r;
+    const size_t bytes = (size_t)((char*)src[0]->stats - (char*)src[0]->C.weights);
+    for (int i = 0; i < n; ++i) {
+        out[i]->params = src[i]->params;
+        out[i]->guide_cap = src[i]->guide_cap;
+        out[i]->guide_order = src[i]->guide_order;
+        const hipError_t e = hipMemcpyAsync(out[i]->C.weights, src[i]->C.weights, bytes, hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) {
+            for (int j = 0; j < n; ++j) { sdmm_destroy(out[j]); out[j] = nullptr; }
+            return fail(SDMM_E_HIP, std::string("sdmm_clone_many: ") + hipGetErrorString(e));
+        }
+        out[i]->initialised = src[i]->initialised;
+    }
+    return SDMM_OK;
 }
 
 int sdmm_num_components(const sdmm_mix* m) { return m ? m->K : 0; }
@@ -771,6 +963,86 @@ int sdmm_init_hemisphere(sdmm_mix* m, const float* positions, const float* norma
     HIP_TRY(hipMemcpyAsync(m->S.bPriors, bp.data(), 4 * 25 * K, hipMemcpyHostToDevice, m->stream));
     HIP_TRY(hipMemcpyAsync(m->S.bDepth, bd.data(), 4 * 9 * K, hipMemcpyHostToDevice, m->stream));
     return upload_and_set(m, w.data(), mean.data(), cov.data());
+}
+
+int sdmm_init_hemisphere_batched(sdmm_mix* const* mixes, int n, const float* positions, const float* normals,
+                                 float depth_prior, const float* min_spatial_distance, const uint64_t* seeds) {
+    if (n < 0 || (n > 0 && (!mixes || !positions || !normals || !min_spatial_distance || !seeds)))
+        return fail(SDMM_E_INVALID, "invalid argument");
+    if (n == 0) return SDMM_OK;
+    const int K = mixes[0]->K;
+    for (int i = 0; i < n; ++i) {
+        if (!mixes[i] || mixes[i]->K != K) return fail(SDMM_E_INVALID, "mixtures must share K");
+        if (mixes[i]->device != mixes[0]->device) return fail(SDMM_E_INVALID, "mixtures on different devices");
+    }
+    if (K % 8) return fail(SDMM_E_INVALID, "K must be a multiple of 8");
+    const int npos = K / 8;
+    HIP_TRY(hipSetDevice(mixes[0]->device));
+    const hipStream_t st = mixes[0]->stream;
+    for (int i = 1; i < n; ++i)
+        if (mixes[i]->stream != st) HIP_TRY(hipStreamSynchronize(mixes[i]->stream));
+    // per mixture: weights K, means 6K (f64), covs 25K (f64), bPriors 25K, bDepth 9K
+    const size_t Kz = (size_t)K;
+    const size_t per = 4 * Kz + 8 * 6 * Kz + 8 * 25 * Kz + 4 * 25 * Kz + 4 * 9 * Kz;
+    char* pin = nullptr;
+    HIP_TRY(hipHostMalloc((void**)&pin, per * (size_t)n, hipHostMallocDefault));
+    std::vector<float> w(Kz), mean(6 * Kz), cov(25 * Kz);
+    int r = SDMM_OK;
+    for (int i = 0; i < n && !r; ++i) {
+        char* b = pin + per * (size_t)i;
+        float* pw = (float*)b;
+        double* pm = (double*)(b + 4 * Kz);
+        double* pc = (double*)(b + 4 * Kz + 48 * Kz);
+        float* pb = (float*)(b + 4 * Kz + 48 * Kz + 200 * Kz);
+        float* pd = (float*)(b + 4 * Kz + 48 * Kz + 200 * Kz + 100 * Kz);
+        r = sdmm_hemisphere_init_host(positions + 3 * (size_t)npos * i, normals + 3 * (size_t)npos * i, npos,
+                                      depth_prior, min_spatial_distance[i], seeds[i], pw, mean.data(), cov.data(),
+                                      pb, pd);
+        for (size_t j = 0; j < 6 * Kz; ++j) pm[j] = (double)mean[j];
+        for (size_t j = 0; j < 25 * Kz; ++j) pc[j] = (double)cov[j];
+    }
+    for (int i = 0; i < n && !r; ++i) {
+        sdmm_mix* m = mixes[i];
+        char* b = pin + per * (size_t)i;
+        hipError_t e = hipMemcpyAsync(m->C.weights, b, 4 * Kz, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(m->tmp_mean, b + 4 * Kz, 48 * Kz, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(m->tmp_cov, b + 52 * Kz, 200 * Kz, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(m->S.bPriors, b + 252 * Kz, 100 * Kz, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(m->S.bDepth, b + 352 * Kz, 36 * Kz, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess)
+            e = launch_set_all(m->K, m->Kp, m->tmp_mean, m->tmp_cov, m->C, m->ep, m->gp, m->norm5, st);
+        if (e != hipSuccess) r = fail(SDMM_E_HIP, std::string("init_hemisphere_batched: ") + hipGetErrorString(e));
+    }
+    const hipError_t e = hipStreamSynchronize(st);   // the pinned staging is freed below
+    (void)hipHostFree(pin);
+    if (r) return r;
+    if (e != hipSuccess) return fail(SDMM_E_HIP, std::string("init_hemisphere_batched: ") + hipGetErrorString(e));
+    for (int i = 0; i < n; ++i) mixes[i]->initialised = true;
+    return SDMM_OK;
+}
+
+int sdmm_iterations_run(const sdmm_mix* const* mixes, int n, int* out) {
+    if (n < 0 || (n > 0 && (!mixes || !out))) return fail(SDMM_E_INVALID, "invalid argument");
+    if (n == 0) return SDMM_OK;
+    for (int i = 0; i < n; ++i)
+        if (!mixes[i]) return fail(SDMM_E_INVALID, "NULL handle in mixes");
+    HIP_TRY(hipSetDevice(mixes[0]->device));
+    double* pin = nullptr;
+    HIP_TRY(hipHostMalloc((void**)&pin, sizeof(double) * (size_t)n, hipHostMallocDefault));
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < n && e == hipSuccess; ++i)
+        e = hipMemcpyAsync(pin + i, mixes[i]->S.scalars + SC_IT, sizeof(double), hipMemcpyDeviceToHost,
+                           mixes[i]->stream);
+    std::vector<hipStream_t> seen;
+    for (int i = 0; i < n && e == hipSuccess; ++i)
+        if (std::find(seen.begin(), seen.end(), mixes[i]->stream) == seen.end()) {
+            seen.push_back(mixes[i]->stream);
+            e = hipStreamSynchronize(mixes[i]->stream);
+        }
+    for (int i = 0; i < n && e == hipSuccess; ++i) out[i] = (int)pin[i];
+    (void)hipHostFree(pin);
+    if (e != hipSuccess) return fail(SDMM_E_HIP, std::string("sdmm_iterations_run: ") + hipGetErrorString(e));
+    return SDMM_OK;
 }
 
 int sdmm_set_params(sdmm_mix* m, const float* weights, const float* means, const float* covs) {
@@ -904,19 +1176,19 @@ int sdmm_mix_broadcast(sdmm_mix* const* mixes, int n_mix, const int32_t* owner, 
         if (mixes[i]->stream != st) HIP_TRY(hipStreamSynchronize(mixes[i]->stream));
     // a mixture's parameters, derived arrays, packed records and stepwise state
     // are one contiguous prefix of its device block (everything before the stats)
-    const size_t bytes = (size_t)((char*)mixes[0]->stats - (char*)mixes[0]->block);
+    const size_t bytes = (size_t)((char*)mixes[0]->stats - (char*)mixes[0]->C.weights);
     if (c->nccl) {
         ncclResult_t g = ncclGroupStart();
         if (g != ncclSuccess) return nccl_fail(g, "ncclGroupStart");
         for (int i = 0; i < n_mix; ++i) {
-            const int r = comm_broadcast(c, mixes[i]->block, bytes, owner[i], st);
+            const int r = comm_broadcast(c, mixes[i]->C.weights, bytes, owner[i], st);
             if (r) { (void)ncclGroupEnd(); return r; }
         }
         g = ncclGroupEnd();
         if (g != ncclSuccess) return nccl_fail(g, "ncclGroupEnd");
     } else {
         for (int i = 0; i < n_mix; ++i) {
-            const int r = comm_broadcast(c, mixes[i]->block, bytes, owner[i], st);
+            const int r = comm_broadcast(c, mixes[i]->C.weights, bytes, owner[i], st);
             if (r) return r;
         }
     }
@@ -929,19 +1201,16 @@ int sdmm_clone(const sdmm_mix* src, sdmm_mix** out) {
     if (!src || !out) return fail(SDMM_E_INVALID, "invalid argument");
     *out = nullptr;
     sdmm_mix* m = nullptr;
-    int r = sdmm_create(src->K, &src->params, src->device, &m);
+    // stream-ordered on the source's stream: after its pending work
+    int r = sdmm_create_on_stream(src->K, &src->params, src->device, (void*)src->stream, &m);
     if (r) return r;
     m->guide_cap = src->guide_cap;
     m->guide_order = src->guide_order;
-    if (src->stream != m->stream) {
-        r = sdmm_set_stream(m, (void*)src->stream);   // ordered with the source's pending work
-        if (r) { sdmm_destroy(m); return r; }
-    }
     // parameters, derived arrays, packed records and stepwise state: the block
     // prefix before the stats (as sdmm_mix_broadcast)
-    const size_t bytes = (size_t)((char*)src->stats - (char*)src->block);
+    const size_t bytes = (size_t)((char*)src->stats - (char*)src->C.weights);
     hipError_t e = hipSetDevice(src->device);
-    if (e == hipSuccess) e = hipMemcpyAsync(m->block, src->block, bytes, hipMemcpyDeviceToDevice, m->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(m->C.weights, src->C.weights, bytes, hipMemcpyDeviceToDevice, m->stream);
     if (e != hipSuccess) {
         sdmm_destroy(m);
         return fail(SDMM_E_HIP, std::string("sdmm_clone: ") + hipGetErrorString(e));
@@ -1563,10 +1832,14 @@ void st_split_depth(sdmm_stree* t, int node, int depth, int max_depth) {
     }
 }
 
-// samples: indices into the position planes px/py/pz owned by node
-void st_split_recurse(sdmm_stree* t, int node, std::vector<int64_t>& idx, const float* px, const float* py,
-                      const float* pz, int threshold) {
-    if (t->nodes[node].child[0] >= 0) return;   // (inner nodes are routed by the caller)
+// split_recurse (sntree.h:235-283) of leaf `node` of the node list L (children
+// appended to L, depth first); samples: indices into the position planes
+// px/py/pz owned by node.  Works on a LOCAL list so that independent leaves
+// can split in parallel; st_merge_local then appends the new nodes to the
+// tree in the order a sequential split would have created them.
+void st_split_local(std::vector<STNodeHost>& L, int node, std::vector<int64_t>& idx, const float* px,
+                    const float* py, const float* pz, int threshold) {
+    if (L[(size_t)node].child[0] >= 0) return;   // (inner nodes are routed by the caller)
     const int64_t n = (int64_t)idx.size();
     if (n <= threshold) return;
     double mean[3] = {0, 0, 0}, sq[3] = {0, 0, 0};
@@ -1583,7 +1856,7 @@ void st_split_recurse(sdmm_stree* t, int node, std::vector<int64_t>& idx, const 
     int ax = 0;
     for (int a = 0; a < 3; ++a)
         if (var[a] > var[ax]) ax = a;
-    const STNodeHost& nd = t->nodes[node];
+    const STNodeHost& nd = L[(size_t)node];
     const float split = (m[ax] - nd.mn[ax]) / (nd.mx[ax] - nd.mn[ax]);
     if (!(split > 0.0f && split < 1.0f)) return;   // degenerate (zero variance / outside)
     STNodeHost parent = nd;
@@ -1597,29 +1870,68 @@ void st_split_recurse(sdmm_stree* t, int node, std::vector<int64_t>& idx, const 
         }
         if ((int64_t)sub[c].size() == n) return;   // would not separate the samples
     }
-    t->nodes[node].axis = ax;
+    L[(size_t)node].axis = ax;
     for (int c = 0; c < 2; ++c) {
-        t->nodes[node].child[c] = (int)t->nodes.size();
-        t->nodes.push_back(ch[c]);
+        L[(size_t)node].child[c] = (int)L.size();
+        L.push_back(ch[c]);
     }
     idx.clear();
     idx.shrink_to_fit();
     for (int c = 0; c < 2; ++c)
-        st_split_recurse(t, t->nodes[node].child[c], sub[c], px, py, pz, threshold);
+        st_split_local(L, L[(size_t)node].child[c], sub[c], px, py, pz, threshold);
+}
+
+// L[0] is tree node v after st_split_local; its new nodes get the next ids
+void st_merge_local(sdmm_stree* t, int v, const std::vector<STNodeHost>& L) {
+    const int base = (int)t->nodes.size() - 1;
+    auto gid = [&](int i) { return i == 0 ? v : base + i; };
+    auto remap = [&](STNodeHost n) {
+        if (n.child[0] >= 0) { n.child[0] = gid(n.child[0]); n.child[1] = gid(n.child[1]); }
+        return n;
+    };
+    t->nodes[(size_t)v] = remap(L[0]);
+    for (size_t i = 1; i < L.size(); ++i) t->nodes.push_back(remap(L[i]));
+}
+
+// split_leaf_recurse of leaves[i] with its own positions, independent leaves
+// on parallel host threads, merged in the given order
+void st_split_many(sdmm_stree* t, int n, const int* leaves, std::vector<int64_t>* idx, const float* const* p,
+                   int threshold) {
+    std::vector<std::vector<STNodeHost>> L((size_t)n);
+    for (int i = 0; i < n; ++i) L[(size_t)i].push_back(t->nodes[(size_t)leaves[i]]);
+    unsigned nt = std::thread::hardware_concurrency();
+    nt = std::max(1u, std::min(nt, 32u));
+    if ((int)nt > n) nt = (unsigned)std::max(n, 1);
+    std::atomic<int> next{0};
+    auto work = [&]() {
+        for (int i = next++; i < n; i = next++)
+            st_split_local(L[(size_t)i], 0, idx[i], p[3 * i], p[3 * i + 1], p[3 * i + 2], threshold);
+    };
+    if (nt <= 1) {
+        work();
+    } else {
+        std::vector<std::thread> th;
+        for (unsigned k = 0; k < nt; ++k) th.emplace_back(work);
+        for (auto& x : th) x.join();
+    }
+    for (int i = 0; i < n; ++i) st_merge_local(t, leaves[i], L[(size_t)i]);
 }
 
 // SNTreeNode::find (jmm/sntree.h:62-83): depth first, child 0 first, with
 // backtracking out of subtrees that hold no leaf box with the point.
 int st_find_host(const sdmm_stree* t, const float p[3]) {
     if (!st_contains(t->nodes[0], p)) return -1;
-    std::vector<int> stack{0};
-    while (!stack.empty()) {
-        const int i = stack.back();
-        stack.pop_back();
+    // pending siblings: at most one per level (a few dozen levels at most)
+    int stack[256];
+    int sp = 0;
+    stack[sp++] = 0;
+    while (sp > 0) {
+        const int i = stack[--sp];
         const STNodeHost& n = t->nodes[(size_t)i];
         if (n.child[0] < 0) return i;
-        if (st_contains(t->nodes[(size_t)n.child[1]], p)) stack.push_back(n.child[1]);
-        if (st_contains(t->nodes[(size_t)n.child[0]], p)) stack.push_back(n.child[0]);
+        if (sp + 2 > 256) return -1;
+        if (st_contains(t->nodes[(size_t)n.child[1]], p)) stack[sp++] = n.child[1];
+        if (st_contains(t->nodes[(size_t)n.child[0]], p)) stack[sp++] = n.child[0];
     }
     return -1;
 }
@@ -1703,9 +2015,16 @@ int sdmm_stree_split(sdmm_stree* t, const float* const p[3], int64_t n, int thre
         const int id = st_find_host(t, q);
         if (id >= 0) per[(size_t)id].push_back(i);
     }
-    const size_t n0 = t->nodes.size();
-    for (size_t id = 0; id < n0; ++id)
-        if (t->nodes[id].child[0] < 0) st_split_recurse(t, (int)id, per[id], p[0], p[1], p[2], threshold);
+    std::vector<int> leaves;
+    std::vector<std::vector<int64_t>> idx;
+    std::vector<const float*> planes;
+    for (size_t id = 0; id < t->nodes.size(); ++id)
+        if (t->nodes[id].child[0] < 0 && (int64_t)per[id].size() > threshold) {
+            leaves.push_back((int)id);
+            idx.push_back(std::move(per[id]));
+            planes.insert(planes.end(), {p[0], p[1], p[2]});
+        }
+    st_split_many(t, (int)leaves.size(), leaves.data(), idx.data(), planes.data(), threshold);
     t->dirty = true;
     t->tab_valid = false;
     return SDMM_OK;
@@ -1727,7 +2046,35 @@ int sdmm_stree_split_leaf_recurse(sdmm_stree* t, int node, const float* const p[
     if (t->nodes[(size_t)node].child[0] >= 0) return SDMM_OK;   // an inner node: nothing to split
     std::vector<int64_t> idx((size_t)n);
     for (int64_t i = 0; i < n; ++i) idx[(size_t)i] = i;
-    st_split_recurse(t, node, idx, p[0], p[1], p[2], threshold);
+    const float* planes[3] = {p[0], p[1], p[2]};
+    st_split_many(t, 1, &node, &idx, planes, threshold);
+    t->dirty = true;
+    t->tab_valid = false;
+    return SDMM_OK;
+}
+
+int sdmm_stree_split_leaf_recurse_many(sdmm_stree* t, int n, const int32_t* nodes, const float* const* p,
+                                       const int64_t* counts, int threshold) {
+    if (!t || n < 0 || threshold < 1 || (n > 0 && (!nodes || !p || !counts)))
+        return fail(SDMM_E_INVALID, "invalid argument");
+    std::vector<int> leaves;
+    std::vector<std::vector<int64_t>> idx;
+    std::vector<const float*> planes;
+    for (int i = 0; i < n; ++i) {
+        const int v = nodes[i];
+        if (v < 0 || v >= (int)t->nodes.size() || counts[i] < 0 || (counts[i] > 0 && (!p[3 * i] || !p[3 * i + 1] ||
+                                                                                        !p[3 * i + 2])))
+            return fail(SDMM_E_INVALID, "invalid argument");
+        if (i > 0 && v <= nodes[i - 1]) return fail(SDMM_E_INVALID, "nodes must be increasing");
+        if (t->nodes[(size_t)v].child[0] >= 0 || counts[i] <= threshold) continue;
+        leaves.push_back(v);
+        std::vector<int64_t> ix((size_t)counts[i]);
+        for (int64_t k = 0; k < counts[i]; ++k) ix[(size_t)k] = k;
+        idx.push_back(std::move(ix));
+        planes.insert(planes.end(), {p[3 * i], p[3 * i + 1], p[3 * i + 2]});
+    }
+    if (leaves.empty()) return SDMM_OK;
+    st_split_many(t, (int)leaves.size(), leaves.data(), idx.data(), planes.data(), threshold);
     t->dirty = true;
     t->tab_valid = false;
     return SDMM_OK;
