@@ -53,27 +53,43 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(batch, K, pos, nrm, synth, n_sample, threads):
-    """The CPU oracle (faithful fp32 restatement of jmm) on the host cores.
-    Measures the same responsibility E-step on a bounded sample."""
+def host_threads() -> int:
+    """`nproc`: the CPUs this process may run on, capped by OMP_NUM_THREADS
+    (GNU nproc honours it; the GPU box sets it to this job's CPU share)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_baseline(batch, K, pos, nrm, synth, n_sample, threads, reps=20):
+    """The CPU oracle (faithful fp32 restatement of jmm) on the host cores:
+    (i) the responsibility E-step (the metric's step) and (ii) the full EM step
+    (or_calculate_stats per thread on its sample shard, summed, then or_mstep --
+    the reference's sample-sharded pattern, stepwise.h:248-396), each the MEDIAN
+    of `reps` passes over a bounded sample, on `threads` = nproc host threads;
+    plus single-thread passes (the reference EM's num_threads(1),
+    stepwise_tangent.h:611)."""
     sys.path.insert(0, str(ROOT))
     from oracle import oracle as orc
     orc.build()
-    m, _ = orc.hemisphere_init(K // 8, pos, nrm, synth.DEPTH_PRIOR, synth.SPATIAL_DISTANCE,
-                               synth.SEED_MODEL, mode=0)
-    x, w = batch["x"][:, :n_sample], batch["w"][:n_sample]
 
-    def run(nthreads, n_sample):
-        per = (n_sample + nthreads - 1) // nthreads
-        shards = []
-        for t in range(nthreads):
-            a, b = t * per, min(n_sample, (t + 1) * per)
-            shards.append(orc.Samples(x[:, a:b], w[a:b]))
-        outs = [None] * nthreads
+    def fresh():
+        m, st = orc.hemisphere_init(K // 8, pos, nrm, synth.DEPTH_PRIOR, synth.SPATIAL_DISTANCE,
+                                    synth.SEED_MODEL, mode=0)
+        return m, st
 
-        def work(t):
-            outs[t] = orc.responsibilities(m, shards[t])
-        ths = [threading.Thread(target=work, args=(t,)) for t in range(nthreads)]
+    m, st = fresh()
+
+    def shards(n, nthreads):
+        x, w = batch["x"][:, :n], batch["w"][:n]
+        per = (n + nthreads - 1) // nthreads
+        return [orc.Samples(x[:, t * per:min(n, (t + 1) * per)], w[t * per:min(n, (t + 1) * per)])
+                for t in range(nthreads)]
+
+    def parallel(fn, parts):
+        ths = [threading.Thread(target=fn, args=(t, p)) for t, p in enumerate(parts)]
         t0 = time.perf_counter()
         for th in ths:
             th.start()
@@ -81,19 +97,43 @@ def cpu_baseline(batch, K, pos, nrm, synth, n_sample, threads):
             th.join()
         return time.perf_counter() - t0
 
-    # ~5 s of sharded CPU work (repeated passes over the sample) + one
-    # single-thread pass over the whole sample (~5 s)
-    reps, tn = 0, 0.0
-    while tn < 5.0 and reps < 64:
-        tn += run(threads, n_sample)
-        reps += 1
-    n1 = n_sample
-    t1 = run(1, n1)
-    return {"value": n_sample * reps / tn, "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"{reps} passes over {n_sample} of the {batch['w'].shape[0]} samples x K={K}, oracle "
-                      f"or_responsibilities (faithful fp32 jmm restatement), {threads} host threads, "
-                      f"sample-sharded", "seconds": tn,
-            "single_thread": {"value": n1 / t1, "cores": 1, "sample": f"{n1} samples, 1 pass", "seconds": t1}}
+    def estep_pass(parts):
+        return parallel(lambda t, p: orc.responsibilities(m, p), parts)
+
+    def em_pass(parts, mm, sst):
+        acc = [None] * len(parts)
+
+        def work(t, p):
+            acc[t] = orc.calculate_stats(mm, p, accurate="faithful")
+        t0 = time.perf_counter()
+        parallel(work, parts)
+        total = np.sum(acc, axis=0)
+        orc.mstep(mm, sst, total, int(sum(p.s.n for p in parts)), accurate="faithful")
+        return time.perf_counter() - t0
+
+    n_e, n_em = min(n_sample, 1 << 18), min(n_sample, 1 << 18)
+    pe = shards(n_e, threads)
+    te = sorted(estep_pass(pe) for _ in range(reps))
+    pm = shards(n_em, threads)
+    mm, sst = fresh()
+    tm = sorted(em_pass(pm, mm, sst) for _ in range(reps))
+    n1 = 1 << 16
+    t1 = estep_pass(shards(n1, 1))
+    m1, s1 = fresh()
+    t1m = em_pass(shards(n1 // 2, 1), m1, s1)
+    med = lambda v: v[len(v) // 2]
+    return {"value": n_e / med(te), "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"responsibility E-step, median of {reps} passes over the first {n_e} of the "
+                      f"{batch['w'].shape[0]} samples, K={K}: oracle or_responsibilities (faithful fp32 jmm "
+                      f"restatement) sample-sharded over {threads} host threads (nproc)",
+            "seconds": float(sum(te)),
+            "em_step": {"value": n_em / med(tm), "unit": "samples/s", "cores": threads,
+                        "sample": f"full EM step (per-thread or_calculate_stats f32 + sum + or_mstep f32), "
+                                  f"median of {reps} passes over {n_em} samples, K={K}",
+                        "seconds": float(sum(tm))},
+            "single_thread": {"value": n1 / t1, "cores": 1, "sample": f"E-step, {n1} samples, 1 pass",
+                              "seconds": t1,
+                              "em_step": {"value": (n1 // 2) / t1m, "sample": f"EM step, {n1 // 2} samples"}}}
 
 
 def leaf_em_bench(pkg, synth, full, N, dev, stream, args, timed, world, rank, comm, K=16, leaf_samples=4096):
@@ -284,7 +324,7 @@ def main():
     ap.add_argument("--no-extra", action="store_true", help="headline E-step only (profiling)")
     ap.add_argument("--no-large-k", action="store_true", help="skip the K=256/512 lines")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: nproc")
     args = ap.parse_args()
 
     import torch
@@ -485,7 +525,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
             out["cpu_baseline"] = cpu_baseline(batch, K, pos, nrm, synth, min(args.cpu_sample, N),
-                                               args.cpu_threads)
+                                               args.cpu_threads or host_threads())
         except Exception as e:  # the baseline is reported, never required
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
 
