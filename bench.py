@@ -111,7 +111,7 @@ def cpu_baseline(batch, K, pos, nrm, synth, n_sample, threads, reps=20):
         orc.mstep(mm, sst, total, int(sum(p.s.n for p in parts)), accurate="faithful")
         return time.perf_counter() - t0
 
-    n_e, n_em = min(n_sample, 1 << 18), min(n_sample, 1 << 18)
+    n_e, n_em = n_sample, n_sample
     pe = shards(n_e, threads)
     te = sorted(estep_pass(pe) for _ in range(reps))
     pm = shards(n_em, threads)
@@ -454,13 +454,17 @@ def main():
     }
     # HBM traffic per launch from the committed rocprofv3 PMC summary of THIS
     # kernel (tools/gpu_pmc.sh + tools/pmc_summary.py), if it matches
-    pmc = ROOT / "profiles" / "round1_pmc_estep.json"
-    if pmc.exists() and world == 1:
+    # (the newest round's summary that matches this kernel, K and N)
+    for pmc in sorted((ROOT / "profiles").glob("round*_pmc_estep.json"), reverse=True):
+        if world != 1:
+            break
         try:
             pm = json.loads(pmc.read_text())
             same = pm.get("kernel", "").replace(" ", "") == mix.kernel_name("resp").replace(" ", "")
             if pm.get("K") == K and pm.get("N") == N and same:
                 out["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
+                out["roofline"]["traffic_source"] = f"profiles/{pmc.name}"
+                break
         except Exception:
             pass
 
