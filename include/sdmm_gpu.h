@@ -168,6 +168,8 @@ int sdmm_em_step_batched_iters(sdmm_mix* const* mixes, int n_mix, const sdmm_sam
  * after the batch, so the host planes may be reused). */
 int sdmm_em_step_batched_host(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* host_samples,
                               const int64_t* seg, int iterations);
+int sdmm_em_step_batched_host_iters(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* host_samples,
+                                    const int64_t* seg, const int* iterations);
 
 /* Split-phase EM step for sample-sharded multi-GPU runs:
  *   sdmm_estep_stats  writes this shard's fp64 sufficient statistics,

@@ -212,6 +212,7 @@ EXPORTED_SYMBOLS = [
     "sdmm_guiding_node_mixtures", "sdmm_guiding_trained", "sdmm_guiding_push", "sdmm_guiding_optimize",
     "sdmm_guiding_iteration", "sdmm_create_on_stream", "sdmm_create_many_on_stream", "sdmm_clone_many",
     "sdmm_init_hemisphere_batched", "sdmm_iterations_run", "sdmm_stree_split_leaf_recurse_many",
+    "sdmm_em_step_batched_host_iters",
 ]
 
 

@@ -1486,6 +1486,24 @@ int sdmm_em_step_batched_host(sdmm_mix* const* mixes, int n_mix, const sdmm_samp
     return SDMM_OK;
 }
 
+int sdmm_em_step_batched_host_iters(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* s, const int64_t* seg,
+                                    const int* iterations) {
+    if (n_mix < 0 || (n_mix > 0 && (!mixes || !mixes[0] || !iterations))) return fail(SDMM_E_INVALID, "invalid argument");
+    if (n_mix == 0) return SDMM_OK;
+    int r = check_samples(s);
+    if (r) return r;
+    if (s->n == 0) return sdmm_em_step_batched_iters(mixes, n_mix, s, seg, iterations);
+    sdmm_mix* m0 = mixes[0];
+    HIP_TRY(hipSetDevice(m0->device));
+    sdmm_samples d;
+    r = stage_host_samples(m0, s, &d);
+    if (r) return r;
+    r = sdmm_em_step_batched_iters(mixes, n_mix, &d, seg, iterations);
+    if (r) return r;
+    HIP_TRY(hipStreamSynchronize(m0->stream));  // the host planes may be reused on return
+    return SDMM_OK;
+}
+
 int sdmm_em_step_host(sdmm_mix* m, const sdmm_samples* s, int iterations) {
     if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
     HIP_TRY(hipSetDevice(m->device));

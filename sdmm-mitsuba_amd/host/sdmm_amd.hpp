@@ -137,6 +137,14 @@ public:
         check(sdmm_em_step(h_, &device_samples, iterations), "sdmm_em_step");
     }
 
+    // em.iterations_run (the plugin's 2-while-below-4 schedule, volpath_sdmm.cpp:299-302)
+    int iterations_run() const {
+        const sdmm_mix* h = h_;
+        int it = 0;
+        check(sdmm_iterations_run(&h, 1, &it), "sdmm_iterations_run");
+        return it;
+    }
+
     // sdmm::save_json counterpart: export the canonical parameters.
     void params(std::vector<float>& weights, std::vector<float>& means, std::vector<float>& covs) const {
         const int K = sdmm_num_components(h_);
@@ -189,6 +197,32 @@ inline void em_step_leaves(const std::vector<Mixture*>& leaves, const std::vecto
     for (size_t i = 0; i < leaves.size(); ++i) h[i] = leaves[i]->handle();
     check(sdmm_em_step_batched_host(h.data(), (int)h.size(), &s, seg.data(), iterations),
           "sdmm_em_step_batched_host");
+}
+
+// ... with the plugin's per-leaf iteration counts (2 while iterations_run < 4,
+// volpath_sdmm.cpp:299-305).
+inline void em_step_leaves(const std::vector<Mixture*>& leaves, const std::vector<const TrainingData*>& data,
+                           const std::vector<int>& iterations) {
+    if (data.size() != leaves.size() || iterations.size() != leaves.size())
+        throw Error(SDMM_E_INVALID, "em_step_leaves: one TrainingData and one iteration count per leaf");
+    std::vector<int64_t> seg(leaves.size() + 1, 0);
+    for (size_t i = 0; i < data.size(); ++i) seg[i + 1] = seg[i] + data[i]->size();
+    const int64_t n = seg.back();
+    std::vector<float> planes[7];
+    for (auto& p : planes) p.resize((size_t)n);
+    for (size_t i = 0; i < data.size(); ++i)
+        for (int d = 0; d < 7; ++d) {
+            const float* src = d < 6 ? data[i]->plane(d).data() : data[i]->weights();
+            std::copy(src, src + data[i]->size(), planes[d].begin() + seg[i]);
+        }
+    sdmm_samples s{};
+    for (int d = 0; d < 6; ++d) s.x[d] = planes[d].data();
+    s.w = planes[6].data();
+    s.n = n;
+    std::vector<sdmm_mix*> h(leaves.size());
+    for (size_t i = 0; i < leaves.size(); ++i) h[i] = leaves[i]->handle();
+    check(sdmm_em_step_batched_host_iters(h.data(), (int)h.size(), &s, seg.data(), iterations.data()),
+          "sdmm_em_step_batched_host_iters");
 }
 
 // A wavefront of guided-bounce queries against one mixture: the batched form
@@ -362,6 +396,61 @@ private:
 
 // pdfSurface's mixing of BSDF and guiding densities (sdmm_proc.cpp:587-589):
 // pdf = h * bsdfPdf + (1 - h) * gmmPdf, h = 0.5 (0.3 with product sampling).
+// An analytic scene for the device Li (sdmm_scene_*): the description's
+// arrays are only read during construction.
+class Scene {
+public:
+    Scene(const sdmm_scene_desc& desc, int device = 0) { check(sdmm_scene_create(&desc, device, &h_), "sdmm_scene_create"); }
+    ~Scene() { sdmm_scene_destroy(h_); }
+    Scene(const Scene&) = delete;
+    Scene& operator=(const Scene&) = delete;
+    sdmm_scene* handle() { return h_; }
+    // render() (volpath_sdmm.cpp:375-393): scene_norm.json values and the tree box
+    void normalization(float scene_min[3], float* spatial_norm, float tree_min[3], float tree_max[3]) const {
+        check(sdmm_scene_normalization(h_, scene_min, spatial_norm, tree_min, tree_max), "sdmm_scene_normalization");
+    }
+
+private:
+    sdmm_scene* h_ = nullptr;
+};
+
+// The plugin's guiding state and schedule (SDMMVolumetricPathTracer,
+// volpath_sdmm.cpp:132-312, :411-507) resident on the GPU (sdmm_guiding_*).
+class GuidingModel {
+public:
+    GuidingModel(const float tree_min[3], const float tree_max[3], const sdmm_guiding_config* cfg = nullptr,
+                 int device = 0) {
+        sdmm_guiding_config c;
+        sdmm_guiding_config_default(&c);
+        if (cfg) c = *cfg;
+        check(sdmm_guiding_create(tree_min, tree_max, &c, device, &h_), "sdmm_guiding_create");
+    }
+    ~GuidingModel() { sdmm_guiding_destroy(h_); }
+    GuidingModel(const GuidingModel&) = delete;
+    GuidingModel& operator=(const GuidingModel&) = delete;
+    sdmm_guiding* handle() { return h_; }
+    sdmm_stree* tree() { return sdmm_guiding_tree(h_); }
+    int trained() const { return sdmm_guiding_trained(h_); }
+    // Li's tail for a render pass, then optimize() (m_totalSpp += spp after)
+    void push(const sdmm_path_vertices& v, uint64_t seed) { check(sdmm_guiding_push(h_, &v, seed), "sdmm_guiding_push"); }
+    sdmm_guiding_stats optimize(int spp) {
+        sdmm_guiding_stats st{};
+        check(sdmm_guiding_optimize(h_, spp, &st), "sdmm_guiding_optimize");
+        return st;
+    }
+    // one pass of render()'s loop with the device Li (image: device, 3 planes)
+    sdmm_guiding_stats iteration(Scene& scene, const sdmm_li_params& p, uint64_t push_seed, bool train, float* image,
+                                 sdmm_li_stats* li = nullptr) {
+        sdmm_guiding_stats st{};
+        check(sdmm_guiding_iteration(h_, scene.handle(), &p, push_seed, train ? 1 : 0, image, li, &st),
+              "sdmm_guiding_iteration");
+        return st;
+    }
+
+private:
+    sdmm_guiding* h_ = nullptr;
+};
+
 inline float mixed_pdf(float heuristicConditionalWeight, float bsdfPdf, float gmmPdf) {
     return heuristicConditionalWeight * bsdfPdf + (1.0f - heuristicConditionalWeight) * gmmPdf;
 }

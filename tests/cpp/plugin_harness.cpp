@@ -1,8 +1,9 @@
 // plugin_harness.cpp -- drives the C ABI through the C++ mirror header the way
 // the Mitsuba sdmm plugin drives sdmm-lib: one mixture per spatial-tree leaf,
 // per-leaf EM on worker threads (tev::ThreadPool::parallelFor,
-// volpath_sdmm.cpp:287-311), 2 EM iterations per call while iterations_run < 4
-// (:299-305), training data pushed from host threads (sdmm_proc.cpp:894-902).
+// volpath_sdmm.cpp:287-311), 3 optimize() calls with 2 EM iterations per call
+// while iterations_run < 4 else 1 (:299-305) -- 2, 2, 1 -- training data
+// pushed from host threads (sdmm_proc.cpp:894-902).
 //
 // usage: plugin_harness in.bin out.bin [batched]
 //   batched: the leaves are stepped by ONE sdmm_em_step_batched_host call per
@@ -54,7 +55,11 @@ int main(int argc, char** argv) {
                 ptrs.push_back(mixes.back().get());
                 dptrs.push_back(&data[l]);
             }
-            for (int call = 0; call < 2; ++call) sdmm_amd::em_step_leaves(ptrs, dptrs, 2);
+            for (int call = 0; call < 3; ++call) {
+                std::vector<int> iters;   // 2 while iterations_run < 4, else 1 (volpath_sdmm.cpp:299-305)
+                for (auto* m : ptrs) iters.push_back(m->iterations_run() < 4 ? 2 : 1);
+                sdmm_amd::em_step_leaves(ptrs, dptrs, iters);
+            }
             for (int l = 0; l < L; ++l) mixes[l]->params(outW[l], outM[l], outC[l]);
         } catch (const std::exception& e) {
             std::fprintf(stderr, "batched: %s\n", e.what());
@@ -67,7 +72,7 @@ int main(int argc, char** argv) {
                 leaf_data(l, data);
                 sdmm_amd::Mixture m(K);
                 m.initialize(data, 0.01f, 0.1f, 0x1A17u + (uint64_t)l);
-                for (int call = 0; call < 2; ++call) m.em_step(data, 2);
+                for (int call = 0; call < 3; ++call) m.em_step(data, m.iterations_run() < 4 ? 2 : 1);
                 m.params(outW[l], outM[l], outC[l]);
             } catch (const std::exception& e) {
                 errors[l] = e.what();

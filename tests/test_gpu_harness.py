@@ -46,7 +46,7 @@ def test_plugin_pattern_harness(pkg, oracle, synth, gpu, tmp_path):
         mix = pkg.SDMM(K)
         mix.init_hemisphere(x[0:3, :K // 8].T, nrm[:K // 8], 0.01, 0.1, 0x1A17 + l)
         ds = pkg.DeviceSamples.from_numpy(x, ww)
-        for _ in range(4):
+        for _ in range(5):                       # 3 plugin calls: 2 + 2 + 1 EM steps
             mix.optimize(ds)
         p = mix.get_params()
         got = out[l]
@@ -59,7 +59,7 @@ def test_plugin_pattern_harness(pkg, oracle, synth, gpu, tmp_path):
         runs = {}
         for mode in ("exact", "accurate"):
             m, st = oracle.hemisphere_init(K // 8, x[0:3, :K // 8].T, nrm[:K // 8], 0.01, 0.1, 0x1A17 + l)
-            for _ in range(4):
+            for _ in range(5):
                 oracle.optimize(m, st, s, accurate=mode)
             runs[mode] = np.asarray(m.weights)
         ex = runs["exact"]
@@ -88,3 +88,52 @@ def test_plugin_pattern_batched_equals_threaded(pkg, synth, gpu, tmp_path):
     c = np.fromfile(tmp_path / "batched.bin", np.float32)
     assert a.size == L * K * 32
     np.testing.assert_array_equal(a, c)
+
+
+def test_guiding_model_cpp_driver_equals_python(pkg, gpu, tmp_path):
+    """The plugin's render() loop driven from C++ (tests/cpp/guiding_harness.cpp
+    through sdmm_amd::Scene / GuidingModel) == the same loop from Python
+    (pkg.Guiding), bitwise: every pass's image and the trained-leaf counts."""
+    import importlib
+    import torch
+    scenes = importlib.import_module("sdmm_mitsuba_amd.scenes")
+    W, H, spp_total, spp_it = 96, 54, 32, 8
+    d = scenes.cornell_box(W, H)
+    nq = d["quads"].size // 9
+    with open(tmp_path / "scene.bin", "wb") as f:
+        np.array([nq, d["reflectance"].size // 3, d["radiance"].size // 3, W, H, spp_total, spp_it],
+                 np.int32).tofile(f)
+        d["quads"].astype(np.float32).tofile(f)
+        for k in ("flip_normals", "bsdf", "emitter"):
+            d[k].astype(np.int32).tofile(f)
+        d["reflectance"].astype(np.float32).tofile(f)
+        d["radiance"].astype(np.float32).tofile(f)
+        np.asarray(d["camera_to_world"], np.float32).tofile(f)
+        np.array([d["fov_x_deg"]], np.float32).tofile(f)
+    exe = tmp_path / "guiding_harness"
+    lib = ROOT / "sdmm-mitsuba_amd" / "lib"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                    f"-I{ROOT / 'sdmm-mitsuba_amd' / 'host'}", f"-I{ROOT / 'include'}",
+                    str(ROOT / "tests" / "cpp" / "guiding_harness.cpp"), f"-L{lib}", "-lsdmm_amd",
+                    "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{lib}", "-Wl,-rpath,/opt/rocm/lib", "-pthread",
+                    "-o", str(exe)], check=True)
+    subprocess.run([str(exe), str(tmp_path / "scene.bin"), str(tmp_path / "out.bin")], check=True, timeout=300)
+    out = np.fromfile(tmp_path / "out.bin", np.uint8)
+    rec = 12 + 4 * 3 * W * H
+    passes = spp_total // spp_it
+    assert out.size == passes * rec
+    sc = pkg.Scene(d)
+    _, _, tmin, tmax = sc.normalization()
+    g = pkg.Guiding(tmin, tmax)
+    for it in range(passes):
+        train = it * spp_it < spp_total // 4
+        img, _, st = g.iteration(sc, spp_it, seed=1 + it, push_seed=1001 + it, train=train)
+        torch.cuda.synchronize()
+        chunk = out[it * rec:(it + 1) * rec]
+        head = chunk[:12].view(np.int32)
+        assert head[0] == g.trained, (it, head, g.trained)
+        if train:
+            assert head[1] == st["leaves"] and head[2] == st["optimized"]
+        np.testing.assert_array_equal(chunk[12:].view(np.float32).reshape(3, H, W), img.cpu().numpy(),
+                                      err_msg=f"pass {it}")
+    assert g.trained > 0
