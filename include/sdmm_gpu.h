@@ -513,8 +513,9 @@ typedef struct {
     const int32_t* nv;
 } sdmm_path_vertices;
 typedef struct {
-    int64_t paths;      /* paths started (pixels x spp) */
-    int64_t segments;   /* bounce rays traced after the camera rays (= saved vertices) */
+    int64_t paths;           /* paths started (pixels x spp) */
+    int64_t segments;        /* bounce rays traced after the camera rays (= saved vertices) */
+    int64_t guided_queries;  /* live bounces that queried the guide (compacted wavefront sizes summed) */
 } sdmm_li_stats;
 int sdmm_scene_create(const sdmm_scene_desc* desc, int device, sdmm_scene** out);
 void sdmm_scene_destroy(sdmm_scene* s);

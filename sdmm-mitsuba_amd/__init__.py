@@ -1017,7 +1017,7 @@ class Guiding:
         gs = _GuidingStats()
         _check(lib().sdmm_guiding_iteration(self.h, scene.h, C.byref(p), C.c_uint64(push_seed), int(train),
                                             C.c_void_p(image.data_ptr()), C.byref(ls), C.byref(gs)))
-        return image, {"paths": ls.paths, "segments": ls.segments}, \
+        return image, {"paths": ls.paths, "segments": ls.segments, "guided_queries": ls.guided_queries}, \
             {"leaves": gs.leaves, "optimized": gs.optimized, "records": gs.records}
 
 
@@ -1045,7 +1045,7 @@ class _PathVertices(C.Structure):
 
 
 class _LiStats(C.Structure):
-    _fields_ = [("paths", C.c_int64), ("segments", C.c_int64)]
+    _fields_ = [("paths", C.c_int64), ("segments", C.c_int64), ("guided_queries", C.c_int64)]
 
 
 def _hip():
@@ -1131,4 +1131,5 @@ class Scene:
         tab = None if not guided else tree._node_table(node_mix)
         _check(lib().sdmm_li_render(self.h, tree.h, tab, C.byref(p), C.c_void_p(image.data_ptr()), C.byref(v),
                                     C.byref(st)))
-        return image, PathVertices(v, self, self.device), {"paths": st.paths, "segments": st.segments}
+        return image, PathVertices(v, self, self.device), {"paths": st.paths, "segments": st.segments,
+                                                           "guided_queries": st.guided_queries}

@@ -533,6 +533,58 @@ __global__ void init_state_kernel(int K, InitScalars a, float eps, double* __res
     for (int i = 0; i < 9; ++i) bd[9 * k + i] = (i % 4 == 0) ? eps : 0.0f;
 }
 
+// Batched initialisation: mixture b takes its weights (K f32), means (6K f64),
+// covs (25K f64), bPriors (25K f32), bDepth (9K f32) from a device staging
+// block and runs set_all (MVTN::set per component, CDF, packing).
+struct InitDesc {
+    CanonDev C;
+    float *ep, *gp, *bp, *bd;
+    double *tmean, *tcov;
+};
+__global__ void __launch_bounds__(512)
+set_all_batched_kernel(int K, int Kp, const InitDesc* __restrict__ tab, const char* __restrict__ staging, size_t per,
+                       float norm5) {
+    const InitDesc d = tab[blockIdx.x];
+    const char* b = staging + per * (size_t)blockIdx.x;
+    const float* w = (const float*)b;
+    const double* mean = (const double*)(b + 4 * (size_t)K);
+    const double* cov = (const double*)(b + 52 * (size_t)K);
+    const float* bp = (const float*)(b + 252 * (size_t)K);
+    const float* bd = (const float*)(b + 352 * (size_t)K);
+    const int t = threadIdx.x;
+    for (int i = t; i < K; i += blockDim.x) d.C.weights[i] = w[i];
+    for (int i = t; i < 25 * K; i += blockDim.x) d.bp[i] = bp[i];
+    for (int i = t; i < 9 * K; i += blockDim.x) d.bd[i] = bd[i];
+    __syncthreads();
+    for (int k = t; k < K; k += blockDim.x) set_component(k, mean + 6 * k, cov + 25 * k, d.C);
+    __syncthreads();
+    if (t == 0) weights_cdf(d.C.weights, d.C.cdf, K, false);
+    __syncthreads();
+    for (int kk = t; kk < Kp; kk += blockDim.x) pack_component(kk, K, Kp, d.C, d.ep, d.gp, norm5);
+}
+
+hipError_t launch_set_all_batched(int n, int K, int Kp, const void* tab, const void* staging, size_t per, float norm5,
+                                  hipStream_t st) {
+    const int threads = Kp < 64 ? 64 : (Kp > 512 ? 512 : Kp);
+    hipLaunchKernelGGL(set_all_batched_kernel, dim3((unsigned)n), dim3(threads), 0, st, K, Kp, (const InitDesc*)tab,
+                       (const char*)staging, per, norm5);
+    return hipGetLastError();
+}
+
+// dst[i][0 .. bytes) = src[i][0 .. bytes) for n pairs (16-byte aligned), one workgroup per pair
+__global__ void __launch_bounds__(256)
+copy_many_kernel(const uint4* const* __restrict__ src, uint4* const* __restrict__ dst, size_t words) {
+    const uint4* s = src[blockIdx.x];
+    uint4* d = dst[blockIdx.x];
+    for (size_t i = threadIdx.x; i < words; i += blockDim.x) d[i] = s[i];
+}
+
+hipError_t launch_copy_many(int n, const void* src_tab, const void* dst_tab, size_t bytes, hipStream_t st) {
+    hipLaunchKernelGGL(copy_many_kernel, dim3((unsigned)n), dim3(256), 0, st, (const uint4* const*)src_tab,
+                       (uint4* const*)dst_tab, bytes / 16);
+    return hipGetLastError();
+}
+
 // n mixtures carved from one slab at a fixed byte stride: mixture i's arrays
 // are mixture 0's shifted by i * stride (blockIdx.y = i)
 template <class T>

@@ -179,10 +179,10 @@ li_query_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, i
         // light's BSDF): sample and eval are 0, the path ends (:772-774)
         if (!(dot3(wi, n) > 0.0f) || (rho[0] == 0.0f && rho[1] == 0.0f && rho[2] == 0.0f)) live = false;
     }
+    Q.live[i] = (uint8_t)((live && guided) ? 1 : 0);
+    Q.slot[i] = -1;
     if (!live) {
         P.depth[i] = -1;
-        Q.c0[i] = -1.0f; Q.c1[i] = -1.0f; Q.c2[i] = -1.0f;   // outside the tree: no query work
-        Q.mode[i] = 1;
         return;
     }
     const uint64_t gp = (uint64_t)(path0 + i);
@@ -201,7 +201,19 @@ li_query_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, i
     Q.u1[i] = rng_uniform(seed, gp, stream, 4);
     Q.u2[i] = rng_uniform(seed, gp, stream, 5);
     Q.mode[i] = (!guided || rng_uniform(seed, gp, stream, 2) <= h) ? 1 : 0;
-    if (!guided) { Q.comp[i] = -1; Q.pdf[i] = 0.0f; }
+}
+
+// the live guided queries, compacted: query j serves path idx[j]
+__global__ void __launch_bounds__(256)
+li_compact_kernel(QueryDev Q, const int32_t* __restrict__ count) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= *count) return;
+    const int i = Q.idx[j];
+    Q.k_c0[j] = Q.c0[i]; Q.k_c1[j] = Q.c1[i]; Q.k_c2[j] = Q.c2[i];
+    Q.k_u0[j] = Q.u0[i]; Q.k_u1[j] = Q.u1[i]; Q.k_u2[j] = Q.u2[i];
+    Q.k_b0[j] = Q.b0[i]; Q.k_b1[j] = Q.b1[i]; Q.k_b2[j] = Q.b2[i];
+    Q.k_mode[j] = Q.mode[i];
+    Q.slot[i] = j;
 }
 
 // ---------------------------------------------------------------------------
@@ -217,7 +229,8 @@ li_shade_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, i
     const float n[3] = {QD.n[0], QD.n[1], QD.n[2]};
     const float* rho = S.refl + 3 * QD.bsdf;
     const float c[3] = {Q.c0[i], Q.c1[i], Q.c2[i]};
-    const int comp = Q.comp[i];
+    const int j = Q.slot[i];            // the path's guided query (-1: none, BSDF only)
+    const int comp = j >= 0 ? Q.comp[j] : -1;
     const bool valid = comp != -1;      // validConditional (:368)
     float wo[3], weight[3], mis_pdf;
     if (!valid) {
@@ -230,15 +243,15 @@ li_shade_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, i
         // BSDF chosen: (bsdf weight * bsdfPdf) / (h bsdfPdf + (1 - h) gmmPdf) (:393-407, :587-589)
         wo[0] = Q.b0[i]; wo[1] = Q.b1[i]; wo[2] = Q.b2[i];
         const float bsdf_pdf = kInvPi * dot3(wo, n);
-        mis_pdf = bsdf_pdf > 0.0f ? h * bsdf_pdf + (1.0f - h) * Q.pdf[i] : 0.0f;   // pdfSurface (:531-534)
+        mis_pdf = bsdf_pdf > 0.0f ? h * bsdf_pdf + (1.0f - h) * Q.pdf[j] : 0.0f;   // pdfSurface (:531-534)
         for (int ch = 0; ch < 3; ++ch) weight[ch] = mis_pdf == 0.0f ? 0.0f : (rho[ch] * bsdf_pdf) / mis_pdf;
     } else {
         // guide sample: bsdf->eval / pdf (:456-463, :504-507)
-        wo[0] = Q.d0[i]; wo[1] = Q.d1[i]; wo[2] = Q.d2[i];
+        wo[0] = Q.d0[j]; wo[1] = Q.d1[j]; wo[2] = Q.d2[j];
         const float cos_o = dot3(wo, n);
         const bool zero = (wo[0] == 0.0f && wo[1] == 0.0f && wo[2] == 0.0f) || !__builtin_isfinite(cos_o);
         const float bsdf_pdf = (!zero && cos_o > 0.0f) ? kInvPi * cos_o : 0.0f;
-        mis_pdf = bsdf_pdf > 0.0f ? h * bsdf_pdf + (1.0f - h) * Q.pdf[i] : 0.0f;   // pdfSurface (:531-534)
+        mis_pdf = bsdf_pdf > 0.0f ? h * bsdf_pdf + (1.0f - h) * Q.pdf[j] : 0.0f;   // pdfSurface (:531-534)
         for (int ch = 0; ch < 3; ++ch) weight[ch] = mis_pdf == 0.0f ? 0.0f : (rho[ch] * (kInvPi * cos_o)) / mis_pdf;
     }
     const float cos_o = dot3(wo, n);
@@ -437,6 +450,22 @@ hipError_t launch_li_query(const SceneDev& S, const PathsDev& P, const QueryDev&
                        h, seed);
     return hipGetLastError();
 }
+size_t li_select_temp_bytes(int64_t n) {
+    size_t b = 0;
+    (void)hipcub::DeviceSelect::Flagged(nullptr, b, hipcub::CountingInputIterator<int32_t>(0), (const uint8_t*)nullptr,
+                                        (int32_t*)nullptr, (int32_t*)nullptr, (int)n);
+    return b;
+}
+// live guided queries -> compact planes; *count_dev = their number
+hipError_t launch_li_compact(const QueryDev& Q, int64_t n, int32_t* count_dev, void* temp, size_t temp_bytes,
+                             hipStream_t st) {
+    hipError_t e = hipcub::DeviceSelect::Flagged(temp, temp_bytes, hipcub::CountingInputIterator<int32_t>(0), Q.live,
+                                                 Q.idx, count_dev, (int)n, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(li_compact_kernel, grid_for(n), dim3(256), 0, st, Q, (const int32_t*)count_dev);
+    return hipGetLastError();
+}
+
 hipError_t launch_li_shade(const SceneDev& S, const PathsDev& P, const QueryDev& Q, int64_t path0, int bounce,
                            int rr_depth, float h, uint64_t seed, hipStream_t st) {
     hipLaunchKernelGGL(li_shade_kernel, grid_for(P.P), dim3(256), 0, st, S, P, Q, path0, bounce, rr_depth, h, seed);

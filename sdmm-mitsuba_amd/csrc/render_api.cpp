@@ -22,6 +22,9 @@ hipError_t launch_li_query(const SceneDev& S, const PathsDev& P, const QueryDev&
                            int max_depth, int guided, float h, uint64_t seed, hipStream_t st);
 hipError_t launch_li_shade(const SceneDev& S, const PathsDev& P, const QueryDev& Q, int64_t path0, int bounce,
                            int rr_depth, float h, uint64_t seed, hipStream_t st);
+size_t li_select_temp_bytes(int64_t n);
+hipError_t launch_li_compact(const QueryDev& Q, int64_t n, int32_t* count_dev, void* temp, size_t temp_bytes,
+                             hipStream_t st);
 hipError_t launch_li_film(const PathsDev& P, int64_t pix0, int64_t npix, int spp, int64_t plane, float* image,
                           hipStream_t st);
 }  // namespace sdmm
@@ -48,6 +51,8 @@ struct sdmm_scene {
     PathsDev P{};
     QueryDev Q{};
     int64_t* dsum = nullptr;
+    int32_t* dcount = nullptr;   // live guided queries of the current bounce
+    int32_t* hcount = nullptr;   // (pinned host copy)
     void* temp = nullptr;
     size_t temp_bytes = 0;
 };
@@ -80,7 +85,8 @@ int grow(sdmm_scene* s, int64_t P, int V, hipStream_t st) {
     const size_t recb = al(sizeof(float) * (size_t)kVertexFields * (size_t)cv * (size_t)cap);
     size_t tb = 0;
     (void)hipcub::DeviceReduce::Sum(nullptr, tb, (const int32_t*)nullptr, (int64_t*)nullptr, (int)cap);
-    const size_t need = 12 * f + 3 * i4 + recb + 13 * f + u1 + i4 + 256 + al(tb);
+    tb = std::max(tb, li_select_temp_bytes(cap));
+    const size_t need = 12 * f + 3 * i4 + recb + 13 * f + u1 + i4 + 256 + al(tb) + 9 * f + 2 * u1 + 3 * i4;
     HIP_TRY(hipStreamSynchronize(st));
     if (s->buf) HIP_TRY(hipFree(s->buf));
     s->buf = nullptr;
@@ -105,6 +111,14 @@ int grow(sdmm_scene* s, int64_t P, int V, hipStream_t st) {
     s->dsum = (int64_t*)take(256);
     s->temp = take(al(tb));
     s->temp_bytes = al(tb);
+    float** kf[9] = {&s->Q.k_c0, &s->Q.k_c1, &s->Q.k_c2, &s->Q.k_u0, &s->Q.k_u1, &s->Q.k_u2,
+                     &s->Q.k_b0, &s->Q.k_b1, &s->Q.k_b2};
+    for (float** q : kf) *q = (float*)take(f);
+    s->Q.k_mode = (uint8_t*)take(u1);
+    s->Q.live = (uint8_t*)take(u1);
+    s->Q.idx = (int32_t*)take(i4);
+    s->Q.slot = (int32_t*)take(i4);
+    s->dcount = (int32_t*)take(i4);
     return SDMM_OK;
 }
 
@@ -201,6 +215,7 @@ void sdmm_scene_destroy(sdmm_scene* s) {
     if (s->drefl) (void)hipFree(s->drefl);
     if (s->drad) (void)hipFree(s->drad);
     if (s->buf) (void)hipFree(s->buf);
+    if (s->hcount) (void)hipHostFree(s->hcount);
     delete s;
 }
 
@@ -244,17 +259,29 @@ int sdmm_li_render(sdmm_scene* s, sdmm_stree* t, const sdmm_mix* const* node_mix
     // bounces: rRec.depth 1 .. maxDepth - 1 scatter (:649, :684); unbounded
     // paths stop at the vertex slots
     const int bounces = p->max_depth > 0 ? p->max_depth - 1 : V;
+    int64_t guided_queries = 0;
+    if (!s->hcount) HIP_TRY(hipHostMalloc((void**)&s->hcount, sizeof(int32_t), hipHostMallocDefault));
     const float h = p->bsdf_fraction;
     for (int b = 0; b < bounces; ++b) {
         HIP_TRY(launch_li_query(s->S, s->P, s->Q, path0, b, p->max_depth > 0 ? p->max_depth : INT32_MAX, p->guided,
                                 h, p->seed, st));
         if (p->guided) {
-            const float* c[3] = {s->Q.c0, s->Q.c1, s->Q.c2};
-            const float* u[3] = {s->Q.u0, s->Q.u1, s->Q.u2};
-            const float* bd[3] = {s->Q.b0, s->Q.b1, s->Q.b2};
+            // only the live paths query the guide: compact them (the order of
+            // the compact queries does not change any query's outputs)
+            HIP_TRY(launch_li_compact(s->Q, P, s->dcount, s->temp, s->temp_bytes, st));
+            HIP_TRY(hipMemcpyAsync(s->hcount, s->dcount, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            const int64_t nlive = *s->hcount;
+            const float* c[3] = {s->Q.k_c0, s->Q.k_c1, s->Q.k_c2};
+            const float* u[3] = {s->Q.k_u0, s->Q.k_u1, s->Q.k_u2};
+            const float* bd[3] = {s->Q.k_b0, s->Q.k_b1, s->Q.k_b2};
             float* d[3] = {s->Q.d0, s->Q.d1, s->Q.d2};
-            r = sdmm_guide_pdf_wavefront(t, node_mix, P, c, u, bd, s->Q.mode, d, s->Q.pdf, s->Q.comp, nullptr);
-            if (r) return r;
+            if (nlive > 0) {
+                r = sdmm_guide_pdf_wavefront(t, node_mix, nlive, c, u, bd, s->Q.k_mode, d, s->Q.pdf, s->Q.comp,
+                                             nullptr);
+                if (r) return r;
+            }
+            guided_queries += nlive;
         }
         HIP_TRY(launch_li_shade(s->S, s->P, s->Q, path0, b, p->rr_depth, h, p->seed, st));
     }
@@ -275,6 +302,7 @@ int sdmm_li_render(sdmm_scene* s, sdmm_stree* t, const sdmm_mix* const* node_mix
         HIP_TRY(hipStreamSynchronize(st));
         stats->paths = P;
         stats->segments = seg;
+        stats->guided_queries = guided_queries;
     }
     return SDMM_OK;
 }

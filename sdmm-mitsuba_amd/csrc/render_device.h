@@ -60,9 +60,16 @@ struct QueryDev {
     float *u0, *u1, *u2;     // guide sample
     float *b0, *b1, *b2;     // BSDF direction (world)
     uint8_t* mode;           // 1: BSDF chosen (pdf query), 0: guide sample
-    float *d0, *d1, *d2;     // wavefront outputs
+    float *d0, *d1, *d2;     // wavefront outputs (compact: query j = path idx[j])
     float* pdf;
     int32_t* comp;
+    // compaction of the live guided queries: flag per path, the selected
+    // path ids, each path's compact slot (-1: no query), compact inputs
+    uint8_t* live;
+    int32_t* idx;
+    int32_t* slot;
+    float *k_c0, *k_c1, *k_c2, *k_u0, *k_u1, *k_u2, *k_b0, *k_b1, *k_b2;
+    uint8_t* k_mode;
 };
 
 }  // namespace sdmm

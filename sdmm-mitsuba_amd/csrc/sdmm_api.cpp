@@ -56,6 +56,14 @@ hipError_t launch_pack_all(int K, int Kp, const CanonDev& C, float* ep, float* g
                            hipStream_t st);
 hipError_t launch_init_state(int K, const double* scal, const float* bprior, float eps, double* sc, float* bp,
                              float* bd, hipStream_t st);
+hipError_t launch_set_all_batched(int n, int K, int Kp, const void* tab, const void* staging, size_t per, float norm5,
+                                  hipStream_t st);
+hipError_t launch_copy_many(int n, const void* src_tab, const void* dst_tab, size_t bytes, hipStream_t st);
+struct InitDescHost {
+    CanonDev C;
+    float *ep, *gp, *bp, *bd;
+    double *tmean, *tcov;
+};
 hipError_t launch_init_pack_many(int n, int K, int Kp, const double* scal, const float* bprior, float eps,
                                  double* sc, float* bp, float* bd, const CanonDev& C, float* ep, float* gp,
                                  float norm5, size_t stride, hipStream_t st);
@@ -835,17 +843,26 @@ int sdmm_clone_many(const sdmm_mix* const* src, int n, sdmm_mix** out) {
         if (src[i]->stream != st) HIP_TRY(hipStreamSynchronize(src[i]->stream));
     int r = create_many(src[0]->K, &src[0]->params, src[0]->device, st, n, out);
     if (r) return r;
-    const size_t bytes = (size_t)((char*)src[0]->stats - (char*)src[0]->C.weights);
+    const size_t bytes = (size_t)((char*)src[0]->stats - (char*)src[0]->C.weights);   // 16-aligned pieces
+    // one kernel over (src, dst) pointer pairs instead of n copies
+    std::vector<void*> ptrs(2 * (size_t)n);
     for (int i = 0; i < n; ++i) {
         out[i]->params = src[i]->params;
         out[i]->guide_cap = src[i]->guide_cap;
         out[i]->guide_order = src[i]->guide_order;
-        const hipError_t e = hipMemcpyAsync(out[i]->C.weights, src[i]->C.weights, bytes, hipMemcpyDeviceToDevice, st);
-        if (e != hipSuccess) {
-            for (int j = 0; j < n; ++j) { sdmm_destroy(out[j]); out[j] = nullptr; }
-            return fail(SDMM_E_HIP, std::string("sdmm_clone_many: ") + hipGetErrorString(e));
-        }
         out[i]->initialised = src[i]->initialised;
+        ptrs[(size_t)i] = src[i]->C.weights;
+        ptrs[(size_t)n + i] = out[i]->C.weights;
+    }
+    void* dtab = nullptr;
+    hipError_t e = hipMallocAsync(&dtab, sizeof(void*) * ptrs.size(), st);
+    if (e == hipSuccess) e = hipMemcpyAsync(dtab, ptrs.data(), sizeof(void*) * ptrs.size(), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = launch_copy_many(n, dtab, (void**)dtab + n, bytes, st);
+    if (dtab) (void)hipFreeAsync(dtab, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);   // ptrs is a host temporary
+    if (e != hipSuccess) {
+        for (int j = 0; j < n; ++j) { sdmm_destroy(out[j]); out[j] = nullptr; }
+        return fail(SDMM_E_HIP, std::string("sdmm_clone_many: ") + hipGetErrorString(e));
     }
     return SDMM_OK;
 }
@@ -985,7 +1002,8 @@ int sdmm_init_hemisphere_batched(sdmm_mix* const* mixes, int n, const float* pos
     const size_t Kz = (size_t)K;
     const size_t per = 4 * Kz + 8 * 6 * Kz + 8 * 25 * Kz + 4 * 25 * Kz + 4 * 9 * Kz;
     char* pin = nullptr;
-    HIP_TRY(hipHostMalloc((void**)&pin, per * (size_t)n, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&pin, (per * (size_t)n + 255) / 256 * 256 + sizeof(InitDescHost) * (size_t)n,
+                          hipHostMallocDefault));
     std::vector<float> w(Kz), mean(6 * Kz), cov(25 * Kz);
     int r = SDMM_OK;
     for (int i = 0; i < n && !r; ++i) {
@@ -1001,18 +1019,22 @@ int sdmm_init_hemisphere_batched(sdmm_mix* const* mixes, int n, const float* pos
         for (size_t j = 0; j < 6 * Kz; ++j) pm[j] = (double)mean[j];
         for (size_t j = 0; j < 25 * Kz; ++j) pc[j] = (double)cov[j];
     }
-    for (int i = 0; i < n && !r; ++i) {
+    // one upload of the staging block + the per-mixture pointer table, one
+    // kernel (a workgroup per mixture: copy in, MVTN::set, CDF, pack)
+    const size_t tab_off = (per * (size_t)n + 255) / 256 * 256;
+    InitDescHost* tab = (InitDescHost*)(pin + tab_off);
+    for (int i = 0; i < n; ++i) {
         sdmm_mix* m = mixes[i];
-        char* b = pin + per * (size_t)i;
-        hipError_t e = hipMemcpyAsync(m->C.weights, b, 4 * Kz, hipMemcpyHostToDevice, st);
-        if (e == hipSuccess) e = hipMemcpyAsync(m->tmp_mean, b + 4 * Kz, 48 * Kz, hipMemcpyHostToDevice, st);
-        if (e == hipSuccess) e = hipMemcpyAsync(m->tmp_cov, b + 52 * Kz, 200 * Kz, hipMemcpyHostToDevice, st);
-        if (e == hipSuccess) e = hipMemcpyAsync(m->S.bPriors, b + 252 * Kz, 100 * Kz, hipMemcpyHostToDevice, st);
-        if (e == hipSuccess) e = hipMemcpyAsync(m->S.bDepth, b + 352 * Kz, 36 * Kz, hipMemcpyHostToDevice, st);
-        if (e == hipSuccess)
-            e = launch_set_all(m->K, m->Kp, m->tmp_mean, m->tmp_cov, m->C, m->ep, m->gp, m->norm5, st);
-        if (e != hipSuccess) r = fail(SDMM_E_HIP, std::string("init_hemisphere_batched: ") + hipGetErrorString(e));
+        tab[i] = InitDescHost{m->C, m->ep, m->gp, m->S.bPriors, m->S.bDepth, m->tmp_mean, m->tmp_cov};
     }
+    void* dev = nullptr;
+    const size_t total = tab_off + sizeof(InitDescHost) * (size_t)n;
+    hipError_t e0 = r ? hipSuccess : hipMallocAsync(&dev, total, st);
+    if (!r && e0 == hipSuccess) e0 = hipMemcpyAsync(dev, pin, total, hipMemcpyHostToDevice, st);
+    if (!r && e0 == hipSuccess)
+        e0 = launch_set_all_batched(n, K, mixes[0]->Kp, (char*)dev + tab_off, dev, per, mixes[0]->norm5, st);
+    if (dev) (void)hipFreeAsync(dev, st);
+    if (!r && e0 != hipSuccess) r = fail(SDMM_E_HIP, std::string("init_hemisphere_batched: ") + hipGetErrorString(e0));
     const hipError_t e = hipStreamSynchronize(st);   // the pinned staging is freed below
     (void)hipHostFree(pin);
     if (r) return r;
