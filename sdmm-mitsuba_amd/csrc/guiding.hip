@@ -11,8 +11,9 @@
 // stable radix sort (a leaf's records stay in arrival order), so the leaves
 // that can be optimised form one contiguous prefix that feeds the batched
 // per-leaf EM directly, and are then dropped.  The leaves' stats positions
-// (context.stats, used only for splitting) stay on the host, where the tree
-// is built.
+// (context.stats, used only for splitting) live in a second device pool of
+// the same kind; only the positions of leaves that must split travel to the
+// host, where the tree is built.
 //
 // Split leaves (split_leaf_recurse): records and stats positions move to the
 // child leaf that holds them (a record outside the split leaf's subtree is
@@ -72,12 +73,24 @@ __global__ void pool_keys_kernel(const int32_t* __restrict__ node, int64_t n, co
 
 __global__ void pool_gather_kernel(const float* __restrict__ src, float* __restrict__ dst, const int32_t* __restrict__ node_in,
                                    int32_t* __restrict__ node_out, const int32_t* __restrict__ perm, int64_t n,
-                                   int64_t cap) {
+                                   int64_t cap, int planes) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     const int64_t i = perm[j];
-    for (int p = 0; p < kPlanes; ++p) dst[p * cap + j] = src[p * cap + i];
+    for (int p = 0; p < planes; ++p) dst[p * cap + j] = src[p * cap + i];
     node_out[j] = node_in[i];
+}
+
+// the stats records (flag set) of a pushed batch appended to the stats pool:
+// positions (planes 0..2 of the records) and the leaf id, in record order
+__global__ void stats_append_kernel(const int32_t* __restrict__ sel, const int32_t* __restrict__ count,
+                                    const float* __restrict__ rec, int64_t rcap, const int32_t* __restrict__ rnode,
+                                    float* __restrict__ sp, int64_t scap, int32_t* __restrict__ snode) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= *count) return;
+    const int i = sel[j];
+    for (int f = 0; f < 3; ++f) sp[f * scap + j] = rec[f * rcap + i];
+    snode[j] = rnode[i];
 }
 
 // first position with key >= v for v = 0 .. nk
@@ -141,53 +154,62 @@ struct PhaseClock {
 
 }  // namespace
 
+// SoA planes [planes][cap] + a leaf id per entry, double-buffered for the
+// stable reorders
+struct Pool {
+    int planes = 0;
+    float* p[2] = {nullptr, nullptr};
+    int32_t* node[2] = {nullptr, nullptr};
+    int cur = 0;
+    int64_t n = 0, cap = 0;
+    std::vector<int64_t> seg;   // after order(): per key range
+    float* plane(int f) const { return p[cur] + (int64_t)f * cap; }
+    int32_t* nodes() const { return node[cur]; }
+};
+
 struct sdmm_guiding {
     int device = 0;
     sdmm_guiding_config cfg{};
     sdmm_stree* tree = nullptr;
     hipStream_t st = nullptr;
     std::vector<sdmm_mix*> mix;                 // per node (NULL: untrained / inner)
-    std::vector<std::vector<float>> stats;      // per node: stats positions x, y, z interleaved
     int64_t total_spp = 0;
     int iteration = 0;
-    // record pool: planes [kPlanes][cap] + node ids, double-buffered for the sorts
-    float* pool[2] = {nullptr, nullptr};
-    int32_t* pnode[2] = {nullptr, nullptr};
-    int cur = 0;
-    int64_t n = 0, cap = 0;
+    Pool rec;     // training records: point 6, normal 3, weight
+    Pool stat;    // stats positions (context.stats)
     void* scratch = nullptr;
     size_t scratch_bytes = 0;
-    std::vector<int64_t> seg;
+    float* pinned = nullptr;   // host staging of the splitting leaves' positions
+    size_t pinned_floats = 0;
 };
 
 namespace {
 
-int grow_pool(sdmm_guiding* g, int64_t need) {
-    if (need <= g->cap) return SDMM_OK;
-    int64_t cap = std::max<int64_t>(need, g->cap * 2);
+int grow_pool(sdmm_guiding* g, Pool& P, int64_t need) {
+    if (need <= P.cap) return SDMM_OK;
+    int64_t cap = std::max<int64_t>(need, P.cap * 2);
     cap = std::max<int64_t>(cap, 1 << 16);
     float* np[2] = {nullptr, nullptr};
     int32_t* nn[2] = {nullptr, nullptr};
     for (int b = 0; b < 2; ++b) {
-        HIP_TRY(hipMalloc(&np[b], sizeof(float) * kPlanes * (size_t)cap));
+        HIP_TRY(hipMalloc(&np[b], sizeof(float) * (size_t)P.planes * (size_t)cap));
         HIP_TRY(hipMalloc(&nn[b], sizeof(int32_t) * (size_t)cap));
     }
-    if (g->n > 0) {
-        for (int p = 0; p < kPlanes; ++p)
-            HIP_TRY(hipMemcpyAsync(np[0] + p * cap, g->pool[g->cur] + p * g->cap, sizeof(float) * (size_t)g->n,
-                                   hipMemcpyDeviceToDevice, g->st));
-        HIP_TRY(hipMemcpyAsync(nn[0], g->pnode[g->cur], sizeof(int32_t) * (size_t)g->n, hipMemcpyDeviceToDevice,
-                               g->st));
+    if (P.n > 0) {
+        for (int f = 0; f < P.planes; ++f)
+            HIP_TRY(hipMemcpyAsync(np[0] + f * cap, P.plane(f), sizeof(float) * (size_t)P.n, hipMemcpyDeviceToDevice,
+                                   g->st));
+        HIP_TRY(hipMemcpyAsync(nn[0], P.nodes(), sizeof(int32_t) * (size_t)P.n, hipMemcpyDeviceToDevice, g->st));
     }
     HIP_TRY(hipStreamSynchronize(g->st));
     for (int b = 0; b < 2; ++b) {
-        if (g->pool[b]) HIP_TRY(hipFree(g->pool[b]));
-        if (g->pnode[b]) HIP_TRY(hipFree(g->pnode[b]));
-        g->pool[b] = np[b];
-        g->pnode[b] = nn[b];
+        if (P.p[b]) HIP_TRY(hipFree(P.p[b]));
+        if (P.node[b]) HIP_TRY(hipFree(P.node[b]));
+        P.p[b] = np[b];
+        P.node[b] = nn[b];
     }
-    g->cur = 0;
-    g->cap = cap;
+    P.cur = 0;
+    P.cap = cap;
     return SDMM_OK;
 }
 
@@ -203,19 +225,19 @@ int grow_scratch(sdmm_guiding* g, size_t bytes) {
 
 size_t al(size_t b) { return (b + 255) / 256 * 256; }
 
-// Stable reorder of the pool by key (ready leaves first, then the other
-// leaves, dropped records last); seg over keys 0 .. 2 * num_nodes.
-int order_pool(sdmm_guiding* g, const std::vector<uint8_t>& ready) {
+// Stable reorder of a pool by key (ready leaves first, then the other
+// leaves, dropped entries last); P.seg over keys 0 .. 2 * num_nodes.
+int order_pool(sdmm_guiding* g, Pool& P, const std::vector<uint8_t>& ready) {
     const int nn = sdmm_stree_num_nodes(g->tree);
     const int nk = 2 * nn;
-    g->seg.assign((size_t)nk + 1, 0);
-    if (g->n == 0) return SDMM_OK;
+    P.seg.assign((size_t)nk + 1, 0);
+    if (P.n == 0) return SDMM_OK;
     int bits = 1;
     while ((1u << bits) <= (unsigned)nk) ++bits;
     size_t tb = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                             (const int32_t*)nullptr, (int32_t*)nullptr, (int)g->n, 0, bits);
-    const size_t kb = al(sizeof(uint32_t) * (size_t)g->n);
+                                             (const int32_t*)nullptr, (int32_t*)nullptr, (int)P.n, 0, bits);
+    const size_t kb = al(sizeof(uint32_t) * (size_t)P.n);
     const size_t sb = al(sizeof(int64_t) * (size_t)(nk + 1));
     const size_t rb = al((size_t)std::max(nn, 1));
     SDMM_TRY(grow_scratch(g, 4 * kb + sb + rb + al(tb)));
@@ -228,19 +250,33 @@ int order_pool(sdmm_guiding* g, const std::vector<uint8_t>& ready) {
     uint8_t* rdev = (uint8_t*)(b + 4 * kb + sb);
     void* temp = b + 4 * kb + sb + rb;
     HIP_TRY(hipMemcpyAsync(rdev, ready.data(), (size_t)nn, hipMemcpyHostToDevice, g->st));
-    hipLaunchKernelGGL(pool_keys_kernel, grid_for(g->n), dim3(256), 0, g->st, g->pnode[g->cur], g->n, rdev, nn, k0,
-                       i0);
+    hipLaunchKernelGGL(pool_keys_kernel, grid_for(P.n), dim3(256), 0, g->st, P.nodes(), P.n, rdev, nn, k0, i0);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(temp, tb, k0, k1, i0, i1, (int)g->n, 0, bits, g->st));
-    hipLaunchKernelGGL(pool_gather_kernel, grid_for(g->n), dim3(256), 0, g->st, g->pool[g->cur], g->pool[1 - g->cur],
-                       g->pnode[g->cur], g->pnode[1 - g->cur], i1, g->n, g->cap);
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(temp, tb, k0, k1, i0, i1, (int)P.n, 0, bits, g->st));
+    hipLaunchKernelGGL(pool_gather_kernel, grid_for(P.n), dim3(256), 0, g->st, P.p[P.cur], P.p[1 - P.cur],
+                       P.node[P.cur], P.node[1 - P.cur], i1, P.n, P.cap, P.planes);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(pool_seg_kernel, grid_for(nk + 1), dim3(256), 0, g->st, k1, g->n, nk, sdev);
+    hipLaunchKernelGGL(pool_seg_kernel, grid_for(nk + 1), dim3(256), 0, g->st, k1, P.n, nk, sdev);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(g->seg.data(), sdev, sizeof(int64_t) * (size_t)(nk + 1), hipMemcpyDeviceToHost, g->st));
+    HIP_TRY(hipMemcpyAsync(P.seg.data(), sdev, sizeof(int64_t) * (size_t)(nk + 1), hipMemcpyDeviceToHost, g->st));
     HIP_TRY(hipStreamSynchronize(g->st));   // (ready is a host temporary)
-    g->cur = 1 - g->cur;
-    g->n = g->seg[(size_t)nk];              // dropped records are gone
+    P.cur = 1 - P.cur;
+    P.n = P.seg[(size_t)nk];               // dropped entries are gone
+    return SDMM_OK;
+}
+
+// entries of split leaves: the leaf found in the new tree if it descends from
+// the split leaf, else dropped
+int relabel(sdmm_guiding* g, Pool& P, const uint8_t* dsplit, const int32_t* dparent) {
+    if (P.n == 0) return SDMM_OK;
+    int32_t* dfound = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&dfound, sizeof(int32_t) * (size_t)P.n, g->st));
+    const float* pp[3] = {P.plane(0), P.plane(1), P.plane(2)};
+    SDMM_TRY(sdmm_stree_find(g->tree, P.n, pp, dfound));
+    hipLaunchKernelGGL(pool_relabel_kernel, grid_for(P.n), dim3(256), 0, g->st, P.nodes(), dfound, P.n, dsplit,
+                       dparent);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipFreeAsync(dfound, g->st));
     return SDMM_OK;
 }
 
@@ -264,7 +300,6 @@ int redistribute(sdmm_guiding* g, int old_nodes) {
         origin[(size_t)c] = a;
     }
     g->mix.resize((size_t)nn, nullptr);
-    g->stats.resize((size_t)nn);
     // mixtures: a copy of the split leaf's in each of its new leaves (one slab)
     {
         std::vector<const sdmm_mix*> src;
@@ -284,67 +319,18 @@ int redistribute(sdmm_guiding* g, int old_nodes) {
             sdmm_destroy(g->mix[(size_t)v]);
             g->mix[(size_t)v] = nullptr;
         }
-    // stats positions of every split leaf through one device find; a position
-    // stays if its leaf descends from its split leaf (appended in order)
-    std::vector<int> src;
-    std::vector<float> planes;
-    int64_t m = 0;
-    for (int v = 0; v < old_nodes; ++v)
-        if (was_split[(size_t)v]) m += (int64_t)g->stats[(size_t)v].size() / 3;
-    if (m > 0) {
-        planes.resize(3 * (size_t)m);
-        src.reserve((size_t)m);
-        int64_t k = 0;
-        for (int v = 0; v < old_nodes; ++v) {
-            if (!was_split[(size_t)v]) continue;
-            const auto& st = g->stats[(size_t)v];
-            for (size_t i = 0; i < st.size() / 3; ++i, ++k) {
-                for (int a = 0; a < 3; ++a) planes[(size_t)a * (size_t)m + (size_t)k] = st[3 * i + (size_t)a];
-                src.push_back(v);
-            }
-        }
-        float* dp = nullptr;
-        int32_t* df = nullptr;
-        HIP_TRY(hipMallocAsync((void**)&dp, sizeof(float) * 3 * (size_t)m, g->st));
-        HIP_TRY(hipMallocAsync((void**)&df, sizeof(int32_t) * (size_t)m, g->st));
-        HIP_TRY(hipMemcpyAsync(dp, planes.data(), sizeof(float) * 3 * (size_t)m, hipMemcpyHostToDevice, g->st));
-        const float* pp[3] = {dp, dp + m, dp + 2 * m};
-        SDMM_TRY(sdmm_stree_find(g->tree, m, pp, df));
-        std::vector<int32_t> f((size_t)m);
-        HIP_TRY(hipMemcpyAsync(f.data(), df, sizeof(int32_t) * (size_t)m, hipMemcpyDeviceToHost, g->st));
-        HIP_TRY(hipFreeAsync(dp, g->st));
-        HIP_TRY(hipFreeAsync(df, g->st));
-        HIP_TRY(hipStreamSynchronize(g->st));
-        for (int v = 0; v < old_nodes; ++v)
-            if (was_split[(size_t)v]) std::vector<float>().swap(g->stats[(size_t)v]);
-        for (int64_t i = 0; i < m; ++i) {
-            const int c = f[(size_t)i];
-            if (c < old_nodes || origin[(size_t)c] != src[(size_t)i]) continue;   // outside the split leaf
-            auto& s = g->stats[(size_t)c];
-            for (int a = 0; a < 3; ++a) s.push_back(planes[(size_t)a * (size_t)m + (size_t)i]);
-        }
-    }
-    // pool records: relabel on the device
-    if (g->n > 0) {
-        int32_t* dfound = nullptr;
-        uint8_t* dsplit = nullptr;
-        int32_t* dparent = nullptr;
-        HIP_TRY(hipMallocAsync((void**)&dfound, sizeof(int32_t) * (size_t)g->n, g->st));
-        HIP_TRY(hipMallocAsync((void**)&dsplit, (size_t)nn, g->st));
-        HIP_TRY(hipMallocAsync((void**)&dparent, sizeof(int32_t) * (size_t)nn, g->st));
-        HIP_TRY(hipMemcpyAsync(dsplit, was_split.data(), (size_t)nn, hipMemcpyHostToDevice, g->st));
-        HIP_TRY(hipMemcpyAsync(dparent, parent.data(), sizeof(int32_t) * (size_t)nn, hipMemcpyHostToDevice, g->st));
-        float* P = g->pool[g->cur];
-        const float* pp[3] = {P, P + g->cap, P + 2 * g->cap};
-        SDMM_TRY(sdmm_stree_find(g->tree, g->n, pp, dfound));
-        hipLaunchKernelGGL(pool_relabel_kernel, grid_for(g->n), dim3(256), 0, g->st, g->pnode[g->cur], dfound, g->n,
-                           dsplit, dparent);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipFreeAsync(dfound, g->st));
-        HIP_TRY(hipFreeAsync(dsplit, g->st));
-        HIP_TRY(hipFreeAsync(dparent, g->st));
-        HIP_TRY(hipStreamSynchronize(g->st));   // host tables above are temporaries
-    }
+    // records and stats positions: relabelled on the device (order kept)
+    uint8_t* dsplit = nullptr;
+    int32_t* dparent = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&dsplit, (size_t)nn, g->st));
+    HIP_TRY(hipMallocAsync((void**)&dparent, sizeof(int32_t) * (size_t)nn, g->st));
+    HIP_TRY(hipMemcpyAsync(dsplit, was_split.data(), (size_t)nn, hipMemcpyHostToDevice, g->st));
+    HIP_TRY(hipMemcpyAsync(dparent, parent.data(), sizeof(int32_t) * (size_t)nn, hipMemcpyHostToDevice, g->st));
+    SDMM_TRY(relabel(g, g->rec, dsplit, dparent));
+    SDMM_TRY(relabel(g, g->stat, dsplit, dparent));
+    HIP_TRY(hipFreeAsync(dsplit, g->st));
+    HIP_TRY(hipFreeAsync(dparent, g->st));
+    HIP_TRY(hipStreamSynchronize(g->st));   // host tables above are temporaries
     return SDMM_OK;
 }
 
@@ -403,7 +389,8 @@ int sdmm_guiding_create(const float tree_min[3], const float tree_max[3], const 
     }
     const int nn = sdmm_stree_num_nodes(g->tree);
     g->mix.assign((size_t)nn, nullptr);
-    g->stats.assign((size_t)nn, {});
+    g->rec.planes = kPlanes;
+    g->stat.planes = 3;
     *out = g;
     return SDMM_OK;
 }
@@ -414,11 +401,13 @@ void sdmm_guiding_destroy(sdmm_guiding* g) {
     if (g->st) (void)hipStreamSynchronize(g->st);
     for (sdmm_mix* m : g->mix) sdmm_destroy(m);
     if (g->tree) sdmm_stree_destroy(g->tree);
-    for (int b = 0; b < 2; ++b) {
-        if (g->pool[b]) (void)hipFree(g->pool[b]);
-        if (g->pnode[b]) (void)hipFree(g->pnode[b]);
-    }
+    for (Pool* P : {&g->rec, &g->stat})
+        for (int b = 0; b < 2; ++b) {
+            if (P->p[b]) (void)hipFree(P->p[b]);
+            if (P->node[b]) (void)hipFree(P->node[b]);
+        }
     if (g->scratch) (void)hipFree(g->scratch);
+    if (g->pinned) (void)hipHostFree(g->pinned);
     if (g->st) (void)hipStreamDestroy(g->st);
     delete g;
 }
@@ -441,43 +430,49 @@ int sdmm_guiding_trained(const sdmm_guiding* g) {
 }
 
 // push_back_data for a render pass's paths (Li's tail): records appended to
-// the pool, stats positions to their leaves
+// the record pool, the own-leaf entries' positions to the stats pool
 int sdmm_guiding_push(sdmm_guiding* g, const sdmm_path_vertices* v, uint64_t seed) {
     if (!g || !v) return fail(SDMM_E_INVALID, "invalid argument");
     HIP_TRY(hipSetDevice(g->device));
     PhaseClock clk(g->st);
     int64_t count = 0;
     SDMM_TRY(sdmm_push_training(g->tree, v, g->cfg.saved_per_path, seed, nullptr, &count, nullptr, nullptr));
-    SDMM_TRY(grow_pool(g, g->n + count));
-    uint8_t* dstats = nullptr;
-    HIP_TRY(hipMallocAsync((void**)&dstats, (size_t)std::max<int64_t>(count, 1), g->st));
-    float* P = g->pool[g->cur];
+    if (count == 0) return SDMM_OK;
+    if (count > INT32_MAX) return fail(SDMM_E_INVALID, "sdmm_guiding_push: too many records");
+    Pool& R = g->rec;
+    SDMM_TRY(grow_pool(g, R, R.n + count));
+    size_t tb = 0;
+    (void)hipcub::DeviceSelect::Flagged(nullptr, tb, hipcub::CountingInputIterator<int32_t>(0),
+                                        (const uint8_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, (int)count);
+    char* tmp = nullptr;
+    const size_t fb = al((size_t)count), sb = al(sizeof(int32_t) * (size_t)count);
+    HIP_TRY(hipMallocAsync((void**)&tmp, fb + sb + 256 + al(tb), g->st));
+    uint8_t* dstats = (uint8_t*)tmp;
+    int32_t* sel = (int32_t*)(tmp + fb);
+    int32_t* dcount = (int32_t*)(tmp + fb + sb);
     sdmm_training_out o{};
-    for (int i = 0; i < 6; ++i) o.x[i] = P + i * g->cap + g->n;
-    for (int i = 0; i < 3; ++i) o.normal[i] = P + (6 + i) * g->cap + g->n;
-    o.w = P + 9 * g->cap + g->n;
+    for (int i = 0; i < 6; ++i) o.x[i] = R.plane(i) + R.n;
+    for (int i = 0; i < 3; ++i) o.normal[i] = R.plane(6 + i) + R.n;
+    o.w = R.plane(9) + R.n;
     o.stats = dstats;
-    o.node = g->pnode[g->cur] + g->n;
+    o.node = R.nodes() + R.n;
     o.capacity = count;
     int64_t got = 0;
     SDMM_TRY(sdmm_push_training(g->tree, v, g->cfg.saved_per_path, seed, &o, &got, nullptr, nullptr));
-    // the stats positions, in record order (leaf order, producer order inside)
-    std::vector<float> px(3 * (size_t)count);
-    std::vector<int32_t> nd((size_t)count);
-    std::vector<uint8_t> sf((size_t)count);
-    for (int a = 0; a < 3; ++a)
-        HIP_TRY(hipMemcpyAsync(px.data() + (size_t)a * (size_t)count, P + a * g->cap + g->n,
-                               sizeof(float) * (size_t)count, hipMemcpyDeviceToHost, g->st));
-    HIP_TRY(hipMemcpyAsync(nd.data(), o.node, sizeof(int32_t) * (size_t)count, hipMemcpyDeviceToHost, g->st));
-    HIP_TRY(hipMemcpyAsync(sf.data(), dstats, (size_t)count, hipMemcpyDeviceToHost, g->st));
-    HIP_TRY(hipFreeAsync(dstats, g->st));
+    // the stats entries in record order (leaf order, producer order inside)
+    HIP_TRY(hipcub::DeviceSelect::Flagged(tmp + fb + sb + 256, tb, hipcub::CountingInputIterator<int32_t>(0), dstats,
+                                          sel, dcount, (int)count, g->st));
+    int32_t ns = 0;
+    HIP_TRY(hipMemcpyAsync(&ns, dcount, sizeof(int32_t), hipMemcpyDeviceToHost, g->st));
     HIP_TRY(hipStreamSynchronize(g->st));
-    for (int64_t i = 0; i < count; ++i) {
-        if (!sf[(size_t)i]) continue;
-        auto& s = g->stats[(size_t)nd[(size_t)i]];
-        for (int a = 0; a < 3; ++a) s.push_back(px[(size_t)a * (size_t)count + (size_t)i]);
-    }
-    g->n += count;
+    Pool& S = g->stat;
+    SDMM_TRY(grow_pool(g, S, S.n + ns));
+    hipLaunchKernelGGL(stats_append_kernel, grid_for(count), dim3(256), 0, g->st, sel, dcount, R.plane(0) + R.n, R.cap,
+                       R.nodes() + R.n, S.plane(0) + S.n, S.cap, S.nodes() + S.n);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipFreeAsync(tmp, g->st));
+    R.n += count;
+    S.n += ns;
     clk.lap("push");
     return SDMM_OK;
 }
@@ -491,34 +486,50 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
     if (!g || spp < 0) return fail(SDMM_E_INVALID, "invalid argument");
     HIP_TRY(hipSetDevice(g->device));
     PhaseClock clk(g->st);
-    // (1) split by the leaves' stats positions, nodes in id order
+    Pool& R = g->rec;
+    Pool& S = g->stat;
+    // (1) split_leaf_recurse(i, threshold) for every node while leaf_nodes() <=
+    // the cap (:253-259), each leaf with its own stats positions in push order
+    // (only a leaf holding more than the threshold can split)
     const int old_nodes = sdmm_stree_num_nodes(g->tree);
-    // split_leaf_recurse(i, threshold) for every node while leaf_nodes() <=
-    // the cap (:253-259), each leaf with its own stats positions (only a leaf
-    // holding more than the threshold can split)
     if (sdmm_stree_leaf_nodes(g->tree) <= g->cfg.max_leaf_nodes) {
+        std::vector<uint8_t> none((size_t)old_nodes, 0);
+        SDMM_TRY(order_pool(g, S, none));
         std::vector<int32_t> ch(2 * (size_t)old_nodes), nodes;
         SDMM_TRY(sdmm_stree_get_nodes(g->tree, nullptr, ch.data(), nullptr));
-        std::vector<std::vector<float>> planes;
-        std::vector<const float*> pp;
-        std::vector<int64_t> counts;
+        std::vector<int64_t> counts, starts;
         for (int v = 0; v < old_nodes; ++v) {
-            const auto& st = g->stats[(size_t)v];
-            const int64_t m = (int64_t)st.size() / 3;
+            const int64_t a = S.seg[(size_t)(old_nodes + v)], m = S.seg[(size_t)(old_nodes + v + 1)] - a;
             if (ch[2 * (size_t)v] >= 0 || m <= g->cfg.split_threshold) continue;
-            std::vector<float> pl(3 * (size_t)m);
-            for (int64_t i = 0; i < m; ++i)
-                for (int a3 = 0; a3 < 3; ++a3) pl[(size_t)a3 * (size_t)m + (size_t)i] = st[3 * (size_t)i + (size_t)a3];
-            planes.push_back(std::move(pl));
             nodes.push_back(v);
             counts.push_back(m);
+            starts.push_back(a);
         }
-        for (size_t i = 0; i < planes.size(); ++i) {
-            const int64_t m = counts[i];
-            pp.insert(pp.end(), {planes[i].data(), planes[i].data() + m, planes[i].data() + 2 * m});
+        if (!nodes.empty()) {
+            // the positions of the splitting leaves (one span of the sorted pool)
+            const int64_t lo = starts.front(), hi = starts.back() + counts.back(), m = hi - lo;
+            if (3 * (size_t)m > g->pinned_floats) {
+                if (g->pinned) HIP_TRY(hipHostFree(g->pinned));
+                g->pinned = nullptr;
+                g->pinned_floats = 0;
+                const size_t want = 3 * (size_t)m + 3 * (size_t)m / 2;
+                HIP_TRY(hipHostMalloc((void**)&g->pinned, sizeof(float) * want, hipHostMallocDefault));
+                g->pinned_floats = want;
+            }
+            float* host = g->pinned;
+            for (int f = 0; f < 3; ++f)
+                HIP_TRY(hipMemcpyAsync(host + (size_t)f * (size_t)m, S.plane(f) + lo, sizeof(float) * (size_t)m,
+                                       hipMemcpyDeviceToHost, g->st));
+            HIP_TRY(hipStreamSynchronize(g->st));
+            std::vector<const float*> pp;
+            for (size_t i = 0; i < nodes.size(); ++i) {
+                const size_t o = (size_t)(starts[i] - lo);
+                pp.insert(pp.end(), {host + o, host + (size_t)m + o, host + 2 * (size_t)m + o});
+            }
+            clk.lap("split:copy");
+            SDMM_TRY(sdmm_stree_split_leaf_recurse_many(g->tree, (int)nodes.size(), nodes.data(), pp.data(),
+                                                        counts.data(), g->cfg.split_threshold));
         }
-        SDMM_TRY(sdmm_stree_split_leaf_recurse_many(g->tree, (int)nodes.size(), nodes.data(), pp.data(),
-                                                    counts.data(), g->cfg.split_threshold));
     }
     clk.lap("split");
     if (sdmm_stree_num_nodes(g->tree) != old_nodes) SDMM_TRY(redistribute(g, old_nodes));
@@ -527,13 +538,14 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
     std::vector<float> aabb(6 * (size_t)nn);
     std::vector<int32_t> child(2 * (size_t)nn);
     SDMM_TRY(sdmm_stree_get_nodes(g->tree, aabb.data(), child.data(), nullptr));
-    // (2) records per leaf (pool ordered by leaf, nothing ready yet)
+    // (2) records and stats per leaf (both pools ordered by leaf, nothing ready yet)
     std::vector<uint8_t> ready((size_t)nn, 0);
-    SDMM_TRY(order_pool(g, ready));
+    SDMM_TRY(order_pool(g, R, ready));
+    SDMM_TRY(order_pool(g, S, ready));
     int n_ready = 0;
     for (int v = 0; v < nn; ++v) {
-        const int64_t n_data = g->seg[(size_t)(nn + v + 1)] - g->seg[(size_t)(nn + v)];
-        const int64_t n_stats = (int64_t)g->stats[(size_t)v].size() / 3;
+        const int64_t n_data = R.seg[(size_t)(nn + v + 1)] - R.seg[(size_t)(nn + v)];
+        const int64_t n_stats = S.seg[(size_t)(nn + v + 1)] - S.seg[(size_t)(nn + v)];
         if ((g->total_spp > 12 || n_data > 1000) && child[2 * (size_t)v] < 0 && n_stats >= 64 && n_data >= 8) {
             ready[(size_t)v] = 1;
             ++n_ready;
@@ -544,16 +556,17 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
     if (out) {
         out->leaves = sdmm_stree_leaf_nodes(g->tree);
         out->optimized = n_ready;
-        out->records = g->n;
+        out->records = R.n;
     }
     ++g->iteration;
     if (n_ready == 0) return bind(g);
     // (3) the ready leaves' records as one prefix, in leaf order
-    SDMM_TRY(order_pool(g, ready));
+    SDMM_TRY(order_pool(g, R, ready));
     std::vector<sdmm_mix*> mixes;
     std::vector<int64_t> bseg{0};
     const int K = g->cfg.K, npos = K / 8;
-    float* P = g->pool[g->cur];
+    float* P = R.p[R.cur];
+    const int64_t cap = R.cap;
     // new leaves: initializeSDMMContext from the first K/8 records' positions
     // and normals (kMeansPlusPlus off, mixture_model_init.h:139-141), spatial
     // distance 3 hmax(diagonal) / (K/8) (:132-135); one gather, one init batch
@@ -562,7 +575,7 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
     for (int v = 0; v < nn; ++v)
         if (ready[(size_t)v] && !g->mix[(size_t)v]) {
             fresh.push_back(v);
-            starts.push_back(g->seg[(size_t)v]);
+            starts.push_back(R.seg[(size_t)v]);
         }
     if (!fresh.empty()) {
         const int nf = (int)fresh.size();
@@ -571,7 +584,7 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
         HIP_TRY(hipMallocAsync((void**)&dstart, sizeof(int64_t) * (size_t)nf, g->st));
         HIP_TRY(hipMallocAsync((void**)&dinit, sizeof(float) * 6 * (size_t)npos * (size_t)nf, g->st));
         HIP_TRY(hipMemcpyAsync(dstart, starts.data(), sizeof(int64_t) * (size_t)nf, hipMemcpyHostToDevice, g->st));
-        hipLaunchKernelGGL(init_gather_kernel, grid_for((int64_t)nf * npos), dim3(256), 0, g->st, P, g->cap, dstart,
+        hipLaunchKernelGGL(init_gather_kernel, grid_for((int64_t)nf * npos), dim3(256), 0, g->st, P, cap, dstart,
                            nf, npos, dinit);
         HIP_TRY(hipGetLastError());
         std::vector<float> init(6 * (size_t)npos * (size_t)nf);
@@ -600,8 +613,8 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
             dist[(size_t)i] = (float)(3.0 * (double)diag / (double)npos);
             seeds[(size_t)i] = g->cfg.init_seed + (uint64_t)v;
         }
-        r = sdmm_init_hemisphere_batched(made.data(), nf, pos.data(), nrm.data(), g->cfg.depth_prior,
-                                                 dist.data(), seeds.data());
+        r = sdmm_init_hemisphere_batched(made.data(), nf, pos.data(), nrm.data(), g->cfg.depth_prior, dist.data(),
+                                         seeds.data());
         if (r) {
             for (sdmm_mix* m : made) sdmm_destroy(m);
             return r;
@@ -611,32 +624,32 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
     for (int v = 0; v < nn; ++v) {
         if (!ready[(size_t)v]) continue;
         mixes.push_back(g->mix[(size_t)v]);
-        bseg.push_back(g->seg[(size_t)v + 1]);
+        bseg.push_back(R.seg[(size_t)v + 1]);
     }
     std::vector<int> iters(mixes.size());
     SDMM_TRY(sdmm_iterations_run(mixes.data(), (int)mixes.size(), iters.data()));
     for (int& it : iters) it = it < 4 ? 2 : 1;   // (:299-302)
     clk.lap("init");
     const int64_t prefix = bseg.back();
-    sdmm_samples s{};
-    for (int i = 0; i < 6; ++i) s.x[i] = P + i * g->cap;
-    s.w = P + 9 * g->cap;
-    s.n = prefix;
-    SDMM_TRY(sdmm_em_step_batched_iters(mixes.data(), (int)mixes.size(), &s, bseg.data(), iters.data()));
+    sdmm_samples smp{};
+    for (int i = 0; i < 6; ++i) smp.x[i] = P + i * cap;
+    smp.w = P + 9 * cap;
+    smp.n = prefix;
+    SDMM_TRY(sdmm_em_step_batched_iters(mixes.data(), (int)mixes.size(), &smp, bseg.data(), iters.data()));
     clk.lap("em");
     // (4) the optimised leaves' data is cleared (:308-309): drop the prefix
     if (prefix > 0) {
-        const int64_t rest = g->n - prefix;
-        float* Q = g->pool[1 - g->cur];
+        const int64_t rest = R.n - prefix;
+        float* Q = R.p[1 - R.cur];
         if (rest > 0) {
-            for (int p = 0; p < kPlanes; ++p)
-                HIP_TRY(hipMemcpyAsync(Q + p * g->cap, P + p * g->cap + prefix, sizeof(float) * (size_t)rest,
+            for (int f = 0; f < kPlanes; ++f)
+                HIP_TRY(hipMemcpyAsync(Q + f * cap, P + f * cap + prefix, sizeof(float) * (size_t)rest,
                                        hipMemcpyDeviceToDevice, g->st));
-            HIP_TRY(hipMemcpyAsync(g->pnode[1 - g->cur], g->pnode[g->cur] + prefix, sizeof(int32_t) * (size_t)rest,
+            HIP_TRY(hipMemcpyAsync(R.node[1 - R.cur], R.node[R.cur] + prefix, sizeof(int32_t) * (size_t)rest,
                                    hipMemcpyDeviceToDevice, g->st));
         }
-        g->cur = 1 - g->cur;
-        g->n = rest;
+        R.cur = 1 - R.cur;
+        R.n = rest;
     }
     SDMM_TRY(bind(g));
     HIP_TRY(hipStreamSynchronize(g->st));
