@@ -462,7 +462,8 @@ int sdmm_stree_set_nodes(sdmm_stree* t, int n, const float* aabb, const int32_t*
  *   sdmm_li_render      spp samples for pixels [pixel_begin, pixel_end) (row
  *                       major), one path per sample; image (device, 3 planes
  *                       of width * height floats) receives each pixel's mean
- *                       radiance.  guided = 0: BSDF sampling only (iteration
+ *                       radiance, image_sqr (nullable) the mean of the squared
+ *                       samples (the reference's m_blockSqr, sdmm_wr.cpp:144).  guided = 0: BSDF sampling only (iteration
  *                       0, :311-323); otherwise every bounce queries the
  *                       leaves' mixtures (node_mix, or the table bound to t)
  *                       with the BSDF/guide choice of probability
@@ -522,7 +523,7 @@ void sdmm_scene_destroy(sdmm_scene* s);
 int sdmm_scene_normalization(const sdmm_scene* s, float scene_min[3], float* spatial_norm, float tree_min[3],
                              float tree_max[3]);
 int sdmm_li_render(sdmm_scene* s, sdmm_stree* t, const sdmm_mix* const* node_mix, const sdmm_li_params* p,
-                   float* image, sdmm_path_vertices* vertices_out, sdmm_li_stats* stats);
+                   float* image, float* image_sqr, sdmm_path_vertices* vertices_out, sdmm_li_stats* stats);
 
 /* Training-data producer: the tail of Li (sdmm_proc.cpp:876-965) for a batch
  * of paths' saved vertices.  Per path, vertices nv-1 down to
@@ -601,7 +602,15 @@ int sdmm_guiding_trained(const sdmm_guiding* g);
 int sdmm_guiding_push(sdmm_guiding* g, const sdmm_path_vertices* v, uint64_t seed);
 int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out);
 int sdmm_guiding_iteration(sdmm_guiding* g, sdmm_scene* scene, const sdmm_li_params* p, uint64_t push_seed,
-                           int train, float* image, sdmm_li_stats* li_stats, sdmm_guiding_stats* out);
+                           int train, float* image, float* image_sqr, sdmm_li_stats* li_stats,
+                           sdmm_guiding_stats* out);
+
+/* SDMMWorkResult::dumpIndividual (sdmm_wr.cpp:115-146): an RGB float OpenEXR
+ * file (uncompressed scanlines, channels B G R, attributes spp / iteration
+ * (int) and time (float) as Bitmap::setMetadata writes them) from HOST planes
+ * rgb[3][height][width].  The plugin writes iteration%05i.exr (the pass's
+ * mean) and iteration_sqr%05i.exr (its mean of squares) per render pass. */
+int sdmm_write_exr(const char* path, int width, int height, const float* rgb, int spp, int iteration, float time);
 
 const char* sdmm_last_error(void);
 int sdmm_abi_version(void);

@@ -164,12 +164,13 @@ def lib():
         L.sdmm_guiding_push.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
         L.sdmm_guiding_optimize.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
         L.sdmm_guiding_iteration.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p,
-                                             C.c_void_p, C.c_void_p]
+                                             C.c_void_p, C.c_void_p, C.c_void_p]
         L.sdmm_scene_create.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
         L.sdmm_scene_destroy.argtypes = [C.c_void_p]
         L.sdmm_scene_normalization.argtypes = [C.c_void_p] + [C.c_void_p] * 4
         L.sdmm_li_render.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                     C.c_void_p]
+                                     C.c_void_p, C.c_void_p]
+        L.sdmm_write_exr.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_float]
         L.sdmm_push_training.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_uint64, C.c_void_p,
                                          C.POINTER(C.c_int64), C.c_void_p, C.POINTER(C.c_int64)]
         _lib = L
@@ -212,7 +213,7 @@ EXPORTED_SYMBOLS = [
     "sdmm_guiding_node_mixtures", "sdmm_guiding_trained", "sdmm_guiding_push", "sdmm_guiding_optimize",
     "sdmm_guiding_iteration", "sdmm_create_on_stream", "sdmm_create_many_on_stream", "sdmm_clone_many",
     "sdmm_init_hemisphere_batched", "sdmm_iterations_run", "sdmm_stree_split_leaf_recurse_many",
-    "sdmm_em_step_batched_host_iters",
+    "sdmm_em_step_batched_host_iters", "sdmm_write_exr",
 ]
 
 
@@ -1004,7 +1005,7 @@ class Guiding:
 
     def iteration(self, scene: "Scene", spp: int, seed: int, push_seed: int, train: bool = True,
                   max_depth: int = 10, rr_depth: int = 10, bsdf_fraction: float = 0.5, saved_vertices: int = 9,
-                  image=None):
+                  image=None, image_sqr=None):
         """One pass of render()'s loop -> (image, li stats, optimize stats)."""
         import torch
         if image is None:
@@ -1016,9 +1017,22 @@ class Guiding:
         ls = _LiStats()
         gs = _GuidingStats()
         _check(lib().sdmm_guiding_iteration(self.h, scene.h, C.byref(p), C.c_uint64(push_seed), int(train),
-                                            C.c_void_p(image.data_ptr()), C.byref(ls), C.byref(gs)))
+                                            C.c_void_p(image.data_ptr()),
+                                            None if image_sqr is None else C.c_void_p(image_sqr.data_ptr()),
+                                            C.byref(ls), C.byref(gs)))
         return image, {"paths": ls.paths, "segments": ls.segments, "guided_queries": ls.guided_queries}, \
             {"leaves": gs.leaves, "optimized": gs.optimized, "records": gs.records}
+
+
+def write_exr(path, rgb, spp: int = 0, iteration: int = 0, time: float = 0.0):
+    """iteration%05i.exr / iteration_sqr%05i.exr (sdmm_write_exr): rgb is a
+    (3, H, W) array (numpy or a tensor, copied to the host)."""
+    a = rgb.detach().cpu().numpy() if hasattr(rgb, "detach") else rgb
+    a = np.ascontiguousarray(a, np.float32)
+    if a.ndim != 3 or a.shape[0] != 3:
+        raise ValueError("rgb must be (3, H, W)")
+    _check(lib().sdmm_write_exr(os.fsencode(path), a.shape[2], a.shape[1], a.ctypes.data, int(spp), int(iteration),
+                                float(time)))
 
 
 class _TrainingOut(C.Structure):
@@ -1116,7 +1130,7 @@ class Scene:
 
     def render(self, tree: "STree", node_mix=None, spp: int = 1, max_depth: int = 10, rr_depth: int = 10,
                guided: bool = False, bsdf_fraction: float = 0.5, saved_vertices: int = 9, seed: int = 0,
-               pixels=None, image=None):
+               pixels=None, image=None, image_sqr=None):
         """One render pass (sdmm_li_render) -> (image (3, H, W) device tensor,
         PathVertices, stats dict)."""
         import torch
@@ -1129,7 +1143,8 @@ class Scene:
         v = _PathVertices()
         st = _LiStats()
         tab = None if not guided else tree._node_table(node_mix)
-        _check(lib().sdmm_li_render(self.h, tree.h, tab, C.byref(p), C.c_void_p(image.data_ptr()), C.byref(v),
+        _check(lib().sdmm_li_render(self.h, tree.h, tab, C.byref(p), C.c_void_p(image.data_ptr()),
+                                    None if image_sqr is None else C.c_void_p(image_sqr.data_ptr()), C.byref(v),
                                     C.byref(st)))
         return image, PathVertices(v, self, self.device), {"paths": st.paths, "segments": st.segments,
                                                            "guided_queries": st.guided_queries}

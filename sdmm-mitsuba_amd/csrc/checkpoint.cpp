@@ -510,4 +510,75 @@ int sdmm_load_json(const char* path, int device, sdmm_stree** tree_out, sdmm_mix
     return SDMM_OK;
 }
 
+
+// ---------------------------------------------------------------------------
+// OpenEXR (scanline, NO_COMPRESSION, FLOAT channels B G R) -- the per-pass
+// image dumps of SDMMWorkResult::dumpIndividual (sdmm_wr.cpp:115-146).
+int sdmm_write_exr(const char* path, int width, int height, const float* rgb, int spp, int iteration, float time) {
+    if (!path || !rgb || width < 1 || height < 1) return err(SDMM_E_INVALID, "sdmm_write_exr: invalid argument");
+    std::string h;
+    auto put_u32 = [&](uint32_t v) { for (int i = 0; i < 4; ++i) h.push_back((char)((v >> (8 * i)) & 0xFF)); };
+    auto put_f32 = [&](float f) { uint32_t v; std::memcpy(&v, &f, 4); put_u32(v); };
+    auto put_str = [&](const char* t) { h.append(t); h.push_back('\0'); };
+    auto attr = [&](const char* name, const char* type, const std::string& value) {
+        put_str(name);
+        put_str(type);
+        put_u32((uint32_t)value.size());
+        h += value;
+    };
+    put_u32(20000630u);   // magic
+    put_u32(2u);          // version 2, single-part scanline
+    {
+        std::string ch;
+        for (const char* c : {"B", "G", "R"}) {   // channel list, alphabetical
+            ch.append(c);
+            ch.push_back('\0');
+            const int32_t v[4] = {2, 0, 1, 1};   // FLOAT, pLinear 0 + 3 reserved bytes, xSampling, ySampling
+            ch.append((const char*)&v[0], 4);
+            ch.append((const char*)&v[1], 4);
+            ch.append((const char*)&v[2], 4);
+            ch.append((const char*)&v[3], 4);
+        }
+        ch.push_back('\0');
+        attr("channels", "chlist", ch);
+    }
+    attr("compression", "compression", std::string(1, '\0'));
+    const int32_t box[4] = {0, 0, width - 1, height - 1};
+    attr("dataWindow", "box2i", std::string((const char*)box, 16));
+    attr("displayWindow", "box2i", std::string((const char*)box, 16));
+    attr("lineOrder", "lineOrder", std::string(1, '\0'));
+    {
+        const float one = 1.0f, zero[2] = {0.0f, 0.0f};
+        attr("pixelAspectRatio", "float", std::string((const char*)&one, 4));
+        attr("screenWindowCenter", "v2f", std::string((const char*)zero, 8));
+        attr("screenWindowWidth", "float", std::string((const char*)&one, 4));
+    }
+    {
+        const int32_t a = spp, b = iteration;
+        attr("spp", "int", std::string((const char*)&a, 4));
+        attr("iteration", "int", std::string((const char*)&b, 4));
+        attr("time", "float", std::string((const char*)&time, 4));
+    }
+    h.push_back('\0');   // end of header
+    (void)put_f32;
+    const uint64_t line_bytes = 8 + 3 * 4 * (uint64_t)width;
+    const uint64_t first = (uint64_t)h.size() + 8 * (uint64_t)height;
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return err(SDMM_E_INVALID, std::string("sdmm_write_exr: cannot open ") + path);
+    bool ok = std::fwrite(h.data(), 1, h.size(), f) == h.size();
+    for (int y = 0; y < height && ok; ++y) {
+        const uint64_t off = first + line_bytes * (uint64_t)y;
+        ok = std::fwrite(&off, 8, 1, f) == 1;
+    }
+    const size_t plane = (size_t)width * (size_t)height;
+    for (int y = 0; y < height && ok; ++y) {
+        const int32_t hdr[2] = {y, (int32_t)(3 * 4 * width)};
+        ok = std::fwrite(hdr, 4, 2, f) == 2;
+        for (int c = 2; c >= 0 && ok; --c)   // B, G, R
+            ok = std::fwrite(rgb + (size_t)c * plane + (size_t)y * width, 4, (size_t)width, f) == (size_t)width;
+    }
+    ok = (std::fclose(f) == 0) && ok;
+    return ok ? SDMM_OK : err(SDMM_E_INVALID, std::string("sdmm_write_exr: write failed: ") + path);
+}
+
 }  // extern "C"

@@ -661,12 +661,13 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
 // :311-316), its training data, then optimize() while training
 // (m_still_training, :416, :495-501).
 int sdmm_guiding_iteration(sdmm_guiding* g, sdmm_scene* scene, const sdmm_li_params* p, uint64_t push_seed,
-                           int train, float* image, sdmm_li_stats* li_stats, sdmm_guiding_stats* out) {
+                           int train, float* image, float* image_sqr, sdmm_li_stats* li_stats,
+                           sdmm_guiding_stats* out) {
     if (!g || !scene || !p || !image) return fail(SDMM_E_INVALID, "invalid argument");
     sdmm_li_params q = *p;
     q.guided = sdmm_guiding_trained(g) > 0 ? 1 : 0;
     sdmm_path_vertices v{};
-    SDMM_TRY(sdmm_li_render(scene, g->tree, nullptr, &q, image, train ? &v : nullptr, li_stats));
+    SDMM_TRY(sdmm_li_render(scene, g->tree, nullptr, &q, image, image_sqr, train ? &v : nullptr, li_stats));
     if (!train) return SDMM_OK;
     SDMM_TRY(sdmm_guiding_push(g, &v, push_seed));
     return sdmm_guiding_optimize(g, p->spp * 1, out);

@@ -310,18 +310,27 @@ li_shade_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, i
     P.depth[i] = live ? depth + 1 : -1;
 }
 
-// pixel mean over its spp samples, in sample order; image planes [3][W*H]
+// pixel mean over its spp samples, in sample order; image planes [3][W*H];
+// image_sqr (nullable): the mean of the squared samples (the reference's
+// m_blockSqr, sdmm_wr.cpp:144-145)
 __global__ void __launch_bounds__(256)
-li_film_kernel(PathsDev P, int64_t pix0, int64_t npix, int spp, int64_t plane, float* __restrict__ image) {
+li_film_kernel(PathsDev P, int64_t pix0, int64_t npix, int spp, int64_t plane, float* __restrict__ image,
+               float* __restrict__ image_sqr) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= npix) return;
-    float acc[3] = {0.0f, 0.0f, 0.0f};
+    float acc[3] = {0.0f, 0.0f, 0.0f}, sq[3] = {0.0f, 0.0f, 0.0f};
     for (int s = 0; s < spp; ++s) {
         const int64_t i = j * spp + s;
-        acc[0] += P.lr[i]; acc[1] += P.lg[i]; acc[2] += P.lb[i];
+        const float l[3] = {P.lr[i], P.lg[i], P.lb[i]};
+        for (int ch = 0; ch < 3; ++ch) {
+            acc[ch] += l[ch];
+            sq[ch] += l[ch] * l[ch];
+        }
     }
     const float inv = 1.0f / (float)spp;
     for (int ch = 0; ch < 3; ++ch) image[ch * plane + pix0 + j] = acc[ch] * inv;
+    if (image_sqr)
+        for (int ch = 0; ch < 3; ++ch) image_sqr[ch * plane + pix0 + j] = sq[ch] * inv;
 }
 
 // ---------------------------------------------------------------------------
@@ -472,8 +481,8 @@ hipError_t launch_li_shade(const SceneDev& S, const PathsDev& P, const QueryDev&
     return hipGetLastError();
 }
 hipError_t launch_li_film(const PathsDev& P, int64_t pix0, int64_t npix, int spp, int64_t plane, float* image,
-                          hipStream_t st) {
-    hipLaunchKernelGGL(li_film_kernel, grid_for(npix), dim3(256), 0, st, P, pix0, npix, spp, plane, image);
+                          float* image_sqr, hipStream_t st) {
+    hipLaunchKernelGGL(li_film_kernel, grid_for(npix), dim3(256), 0, st, P, pix0, npix, spp, plane, image, image_sqr);
     return hipGetLastError();
 }
 

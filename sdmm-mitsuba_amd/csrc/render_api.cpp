@@ -26,7 +26,7 @@ size_t li_select_temp_bytes(int64_t n);
 hipError_t launch_li_compact(const QueryDev& Q, int64_t n, int32_t* count_dev, void* temp, size_t temp_bytes,
                              hipStream_t st);
 hipError_t launch_li_film(const PathsDev& P, int64_t pix0, int64_t npix, int spp, int64_t plane, float* image,
-                          hipStream_t st);
+                          float* image_sqr, hipStream_t st);
 }  // namespace sdmm
 
 namespace sdmm_detail {
@@ -232,7 +232,7 @@ int sdmm_scene_normalization(const sdmm_scene* s, float scene_min[3], float* spa
 }
 
 int sdmm_li_render(sdmm_scene* s, sdmm_stree* t, const sdmm_mix* const* node_mix, const sdmm_li_params* p,
-                   float* image, sdmm_path_vertices* vout, sdmm_li_stats* stats) {
+                   float* image, float* image_sqr, sdmm_path_vertices* vout, sdmm_li_stats* stats) {
     if (!s || !t || !p || !image) return fail(SDMM_E_INVALID, "invalid argument");
     const int64_t npix_all = (int64_t)s->S.width * s->S.height;
     if (p->spp < 1 || p->pixel_begin < 0 || p->pixel_end > npix_all || p->pixel_end <= p->pixel_begin ||
@@ -285,7 +285,7 @@ int sdmm_li_render(sdmm_scene* s, sdmm_stree* t, const sdmm_mix* const* node_mix
         }
         HIP_TRY(launch_li_shade(s->S, s->P, s->Q, path0, b, p->rr_depth, h, p->seed, st));
     }
-    HIP_TRY(launch_li_film(s->P, p->pixel_begin, npix, p->spp, npix_all, image, st));
+    HIP_TRY(launch_li_film(s->P, p->pixel_begin, npix, p->spp, npix_all, image, image_sqr, st));
     if (vout) {
         vout->n_paths = P;
         vout->max_vertices = V;

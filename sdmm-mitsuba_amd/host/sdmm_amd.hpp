@@ -440,9 +440,9 @@ public:
     }
     // one pass of render()'s loop with the device Li (image: device, 3 planes)
     sdmm_guiding_stats iteration(Scene& scene, const sdmm_li_params& p, uint64_t push_seed, bool train, float* image,
-                                 sdmm_li_stats* li = nullptr) {
+                                 float* image_sqr = nullptr, sdmm_li_stats* li = nullptr) {
         sdmm_guiding_stats st{};
-        check(sdmm_guiding_iteration(h_, scene.handle(), &p, push_seed, train ? 1 : 0, image, li, &st),
+        check(sdmm_guiding_iteration(h_, scene.handle(), &p, push_seed, train ? 1 : 0, image, image_sqr, li, &st),
               "sdmm_guiding_iteration");
         return st;
     }
@@ -450,6 +450,24 @@ public:
 private:
     sdmm_guiding* h_ = nullptr;
 };
+
+// SDMMWorkResult::dumpIndividual (sdmm_wr.cpp:115-146): the pass's image and
+// squared image as dir/iteration%05i.exr and dir/iteration_sqr%05i.exr (host
+// planes [3][h][w]); returns the first path.
+inline std::string dump_iteration(const std::string& dir, int iteration, int spp, float seconds, int width,
+                                  int height, const float* rgb, const float* rgb_sqr) {
+    detail::make_dirs(dir);
+    char name[64];
+    std::snprintf(name, sizeof(name), "/iteration%05i.exr", iteration);
+    const std::string a = dir + name;
+    check(sdmm_write_exr(a.c_str(), width, height, rgb, spp, iteration, seconds), "sdmm_write_exr");
+    if (rgb_sqr) {
+        std::snprintf(name, sizeof(name), "/iteration_sqr%05i.exr", iteration);
+        const std::string b = dir + name;
+        check(sdmm_write_exr(b.c_str(), width, height, rgb_sqr, spp, iteration, seconds), "sdmm_write_exr");
+    }
+    return a;
+}
 
 inline float mixed_pdf(float heuristicConditionalWeight, float bsdfPdf, float gmmPdf) {
     return heuristicConditionalWeight * bsdfPdf + (1.0f - heuristicConditionalWeight) * gmmPdf;

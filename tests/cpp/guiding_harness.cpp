@@ -5,7 +5,9 @@
 // guided once a leaf is trained.  Writes each pass's image and the guiding
 // stats, for the bitwise comparison with the Python driver of the same loop.
 //
-// usage: guiding_harness scene.bin out.bin
+// usage: guiding_harness scene.bin out.bin [exr_dir]
+//   exr_dir: also dump iteration%05i.exr / iteration_sqr%05i.exr per pass
+//            (SDMMWorkResult::dumpIndividual, sdmm_wr.cpp:115-146)
 //   scene.bin: int32 n_quads, n_bsdfs, n_emitters, width, height, spp_total, spp_it;
 //              float quads[9 n_quads]; int32 flip[n_quads], bsdf[n_quads], emitter[n_quads];
 //              float reflectance[3 n_bsdfs], radiance[3 n_emitters], cam[16], fov
@@ -21,7 +23,7 @@ template <class T>
 static bool rd(FILE* f, T* p, size_t n) { return std::fread(p, sizeof(T), n, f) == n; }
 
 int main(int argc, char** argv) {
-    if (argc != 3) { std::fprintf(stderr, "usage: %s scene.bin out.bin\n", argv[0]); return 2; }
+    if (argc != 3 && argc != 4) { std::fprintf(stderr, "usage: %s scene.bin out.bin [exr_dir]\n", argv[0]); return 2; }
     FILE* f = std::fopen(argv[1], "rb");
     if (!f) return 2;
     int32_t hdr[7];
@@ -47,8 +49,11 @@ int main(int argc, char** argv) {
         scene.normalization(smin, &norm, tmin, tmax);
         sdmm_amd::GuidingModel model(tmin, tmax);                 // split_to_depth(2), K = 16, 4000, 2048
         float* image = nullptr;
-        if (hipMalloc(&image, sizeof(float) * 3 * (size_t)W * H) != hipSuccess) return 1;
-        std::vector<float> host(3 * (size_t)W * H);
+        float* image_sqr = nullptr;
+        if (hipMalloc(&image, sizeof(float) * 3 * (size_t)W * H) != hipSuccess ||
+            hipMalloc(&image_sqr, sizeof(float) * 3 * (size_t)W * H) != hipSuccess)
+            return 1;
+        std::vector<float> host(3 * (size_t)W * H), host_sqr(3 * (size_t)W * H);
         FILE* o = std::fopen(argv[2], "wb");
         int it = 0;
         for (int done = 0; done < spp_total; done += spp_it, ++it) {
@@ -56,16 +61,19 @@ int main(int argc, char** argv) {
             sdmm_li_params p{};
             p.spp = spp_it; p.max_depth = 10; p.rr_depth = 10; p.bsdf_fraction = 0.5f; p.saved_vertices = 9;
             p.seed = 1 + (uint64_t)it; p.pixel_begin = 0; p.pixel_end = (int64_t)W * H;
-            const sdmm_guiding_stats st = model.iteration(scene, p, 1001 + (uint64_t)it, train, image);
+            const sdmm_guiding_stats st = model.iteration(scene, p, 1001 + (uint64_t)it, train, image, image_sqr);
             if (hipDeviceSynchronize() != hipSuccess ||
-                hipMemcpy(host.data(), image, sizeof(float) * host.size(), hipMemcpyDeviceToHost) != hipSuccess)
+                hipMemcpy(host.data(), image, sizeof(float) * host.size(), hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(host_sqr.data(), image_sqr, sizeof(float) * host.size(), hipMemcpyDeviceToHost) != hipSuccess)
                 return 1;
+            if (argc == 4) sdmm_amd::dump_iteration(argv[3], it, spp_it, 0.0f, W, H, host.data(), host_sqr.data());
             const int32_t rec[3] = {model.trained(), train ? st.leaves : -1, train ? st.optimized : -1};
             std::fwrite(rec, 4, 3, o);
             std::fwrite(host.data(), 4, host.size(), o);
         }
         std::fclose(o);
         (void)hipFree(image);
+        (void)hipFree(image_sqr);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "guiding_harness: %s\n", e.what());
         return 1;

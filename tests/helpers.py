@@ -104,3 +104,47 @@ def estep_f64(mix_params: dict, x, w, hpdf=None, is_diffuse=None, h=0.5, chunk=2
         M += np.einsum("nk,nki->ki", v, tau)
         C += np.einsum("nk,nki,nkj->kij", v, tau, tau)
     return np.concatenate([[H, wsum], W, M.reshape(-1), C.reshape(-1)])
+
+
+def read_exr(path):
+    """Minimal reader for the uncompressed scanline float OpenEXR files
+    sdmm_write_exr writes: (rgb (3, H, W) float32, attributes dict)."""
+    import struct
+    data = open(path, "rb").read()
+    assert struct.unpack_from("<I", data, 0)[0] == 20000630, "not an OpenEXR file"
+    pos, attrs = 8, {}
+    while data[pos] != 0:
+        e = data.index(b"\0", pos); name = data[pos:e].decode(); pos = e + 1
+        e = data.index(b"\0", pos); typ = data[pos:e].decode(); pos = e + 1
+        size = struct.unpack_from("<i", data, pos)[0]; pos += 4
+        val = data[pos:pos + size]; pos += size
+        if typ == "int":
+            attrs[name] = struct.unpack("<i", val)[0]
+        elif typ == "float":
+            attrs[name] = struct.unpack("<f", val)[0]
+        elif typ == "box2i":
+            attrs[name] = struct.unpack("<4i", val)
+        elif typ == "compression":
+            attrs[name] = val[0]
+        elif typ == "chlist":
+            chans, q = [], 0
+            while val[q] != 0:
+                e = val.index(b"\0", q); cname = val[q:e].decode(); q = e + 1
+                ptype = struct.unpack_from("<i", val, q)[0]; q += 16
+                chans.append((cname, ptype))
+            attrs[name] = chans
+        else:
+            attrs[name] = val
+    pos += 1
+    x0, y0, x1, y1 = attrs["dataWindow"]
+    W, H = x1 - x0 + 1, y1 - y0 + 1
+    assert attrs["compression"] == 0 and all(p == 2 for _, p in attrs["channels"])
+    offsets = struct.unpack_from(f"<{H}Q", data, pos)
+    names = [c for c, _ in attrs["channels"]]
+    img = {c: np.zeros((H, W), np.float32) for c in names}
+    for off in offsets:
+        y, size = struct.unpack_from("<ii", data, off)
+        row = np.frombuffer(data, np.float32, count=len(names) * W, offset=off + 8).reshape(len(names), W)
+        for k, c in enumerate(names):
+            img[c][y - y0] = row[k]
+    return np.stack([img["R"], img["G"], img["B"]]), attrs

@@ -211,3 +211,19 @@ int main(int argc, char** argv) {
                              "spp", "total_spp"}
     assert sorted(p.name for p in (tmp_path / "run" / "checkpoints").iterdir()) == \
         ["model_00000.asdmm", "model_00001.asdmm", "model_00002.asdmm"]
+
+
+def test_write_exr_round_trip(pkg, tmp_path):
+    """iteration%05i.exr (SDMMWorkResult::dumpIndividual, sdmm_wr.cpp:115-146):
+    a float RGB OpenEXR with the spp / iteration / time attributes, read back
+    bit for bit by an independent minimal reader."""
+    from helpers import read_exr
+    rng = np.random.default_rng(3)
+    rgb = rng.standard_normal((3, 7, 11)).astype(np.float32) * 100
+    rgb[1, 2, 3] = np.inf
+    path = tmp_path / "iteration00003.exr"
+    pkg.write_exr(path, rgb, spp=8, iteration=3, time=1.25)
+    back, attrs = read_exr(path)
+    np.testing.assert_array_equal(back, rgb)
+    assert attrs["spp"] == 8 and attrs["iteration"] == 3 and attrs["time"] == 1.25
+    assert [c for c, _ in attrs["channels"]] == ["B", "G", "R"]

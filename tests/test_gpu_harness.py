@@ -117,7 +117,8 @@ def test_guiding_model_cpp_driver_equals_python(pkg, gpu, tmp_path):
                     str(ROOT / "tests" / "cpp" / "guiding_harness.cpp"), f"-L{lib}", "-lsdmm_amd",
                     "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{lib}", "-Wl,-rpath,/opt/rocm/lib", "-pthread",
                     "-o", str(exe)], check=True)
-    subprocess.run([str(exe), str(tmp_path / "scene.bin"), str(tmp_path / "out.bin")], check=True, timeout=300)
+    subprocess.run([str(exe), str(tmp_path / "scene.bin"), str(tmp_path / "out.bin"), str(tmp_path / "exr")],
+                   check=True, timeout=300)
     out = np.fromfile(tmp_path / "out.bin", np.uint8)
     rec = 12 + 4 * 3 * W * H
     passes = spp_total // spp_it
@@ -136,4 +137,11 @@ def test_guiding_model_cpp_driver_equals_python(pkg, gpu, tmp_path):
             assert head[1] == st["leaves"] and head[2] == st["optimized"]
         np.testing.assert_array_equal(chunk[12:].view(np.float32).reshape(3, H, W), img.cpu().numpy(),
                                       err_msg=f"pass {it}")
+        # the pass's dumps (sdmm_wr.cpp:144-145): the image, and the mean of squares >= its square
+        from helpers import read_exr
+        exr, attrs = read_exr(tmp_path / "exr" / f"iteration{it:05d}.exr")
+        np.testing.assert_array_equal(exr, img.cpu().numpy())
+        assert attrs["iteration"] == it and attrs["spp"] == spp_it
+        sqr, _ = read_exr(tmp_path / "exr" / f"iteration_sqr{it:05d}.exr")
+        assert np.all(sqr >= exr * exr * (1 - 1e-5) - 1e-30)
     assert g.trained > 0
