@@ -228,7 +228,7 @@ def wavefront_bench(pkg, synth, batch, shard, tree, dev, stream, ct, ut, gout, t
             "guided_frac": float((comp >= 0).mean()), "scaling": "weak (replicas: queries per rank)"}
 
 
-def cornell_bench(pkg, dev, args, world):
+def cornell_bench(pkg, dev, args, world, optimize_async=0):
     """configs[0] on the device: the test suite's Cornell Box (640x360), K=16
     per leaf, 64 spp rendered 8 spp per iteration, training (push + optimize)
     while samplesRendered < sampleCount / 4 (volpath_sdmm.cpp:411-507), the
@@ -244,7 +244,7 @@ def cornell_bench(pkg, dev, args, world):
     acc = torch.zeros_like(img)
     its = []
     for rep in range(2):                          # the first run pages in code and scratch (untimed)
-        g = pkg.Guiding(tmin, tmax, device=dev.index)
+        g = pkg.Guiding(tmin, tmax, device=dev.index, optimize_async=optimize_async)
         acc.zero_()
         its = []
         torch.cuda.synchronize()
@@ -266,7 +266,8 @@ def cornell_bench(pkg, dev, args, world):
             "total_ms": total * 1e3, "guided_rays_per_s": seg / (gms * 1e-3),
             "guided_paths_per_s": sum(x["paths"] for x in guided) / (gms * 1e-3),
             "trained_leaves": its[-1]["trained"], "iterations": its,
-            "image_mean": float((acc / len(its)).mean().item()), "replicas": world}
+            "image_mean": float((acc / len(its)).mean().item()), "replicas": world,
+            "optimize_async": bool(optimize_async)}
 
 
 def large_k_bench(pkg, synth, batch, shard, dev, stream, timed, args, world, N, comm):
@@ -522,6 +523,7 @@ def main():
 
     if not args.no_extra:
         out["cornell"] = cornell_bench(pkg, dev, args, world)
+        out["cornell_async"] = cornell_bench(pkg, dev, args, world, optimize_async=1)
 
     if not args.no_extra and not args.no_large_k:
         out["large_k"] = large_k_bench(pkg, synth, batch, shard, dev, stream, timed, args, world, N, comm)

@@ -434,8 +434,14 @@ int sdmm_get_em_params(const sdmm_mix* m, sdmm_em_params* p);
  * children start from their parent's distribution and optimizer (jmm
  * SNTree::createChildNode, sntree.h:172-205). */
 int sdmm_clone(const sdmm_mix* m, sdmm_mix** out);
-/* sdmm_clone of n handles of one K into one slab (on src[0]'s stream). */
+/* sdmm_clone of n handles of one K into one slab (on src[0]'s stream, or on
+ * hip_stream: the new handles then use it). */
 int sdmm_clone_many(const sdmm_mix* const* src, int n, sdmm_mix** out);
+int sdmm_clone_many_on_stream(const sdmm_mix* const* src, int n, void* hip_stream, sdmm_mix** out);
+/* dst[i] := src[i] (mixture + EM state), one kernel on dst[0]'s stream after
+ * the sources' pending work -- sdmm::prepare(conditioner, sdmm) of the async
+ * update (volpath_sdmm.cpp:227-242) when conditioners are separate handles. */
+int sdmm_copy_many(const sdmm_mix* const* src, sdmm_mix* const* dst, int n);
 int sdmm_restore_params(sdmm_mix* m, const sdmm_params_out* in);
 int sdmm_stree_set_nodes(sdmm_stree* t, int n, const float* aabb, const int32_t* child, const int32_t* axis);
 
@@ -586,6 +592,9 @@ typedef struct {
     int saved_per_path;     /* 8 */
     float depth_prior;      /* 0.01 (sdmm-lib initialize is absent: jmm uniformHemisphereInit's) */
     uint64_t init_seed;     /* leaf v's hemisphere init seed = init_seed + v */
+    int optimize_async;     /* optimizeAsync (volpath_sdmm.cpp:65, :180-242): one EM step per leaf (0.1 x
+                               hmax(diagonal) at init) on the model's EM stream, overlapping the next pass;
+                               renders use each leaf's conditioner, updated after the pass (sdmm_guiding_update) */
 } sdmm_guiding_config;
 typedef struct {
     int leaves;             /* leaf_nodes() after the split */
@@ -601,6 +610,9 @@ int sdmm_guiding_node_mixtures(const sdmm_guiding* g, const sdmm_mix** out, int 
 int sdmm_guiding_trained(const sdmm_guiding* g);
 int sdmm_guiding_push(sdmm_guiding* g, const sdmm_path_vertices* v, uint64_t seed);
 int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out);
+/* async: optimize_async_wait_and_update (:227-242) -- wait for the running EM,
+ * copy each stepped leaf's mixture into its conditioner; no-op otherwise. */
+int sdmm_guiding_update(sdmm_guiding* g);
 int sdmm_guiding_iteration(sdmm_guiding* g, sdmm_scene* scene, const sdmm_li_params* p, uint64_t push_seed,
                            int train, float* image, float* image_sqr, sdmm_li_stats* li_stats,
                            sdmm_guiding_stats* out);

@@ -163,6 +163,7 @@ def lib():
         L.sdmm_guiding_trained.argtypes = [C.c_void_p]
         L.sdmm_guiding_push.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
         L.sdmm_guiding_optimize.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        L.sdmm_guiding_update.argtypes = [C.c_void_p]
         L.sdmm_guiding_iteration.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p,
                                              C.c_void_p, C.c_void_p, C.c_void_p]
         L.sdmm_scene_create.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
@@ -213,7 +214,8 @@ EXPORTED_SYMBOLS = [
     "sdmm_guiding_node_mixtures", "sdmm_guiding_trained", "sdmm_guiding_push", "sdmm_guiding_optimize",
     "sdmm_guiding_iteration", "sdmm_create_on_stream", "sdmm_create_many_on_stream", "sdmm_clone_many",
     "sdmm_init_hemisphere_batched", "sdmm_iterations_run", "sdmm_stree_split_leaf_recurse_many",
-    "sdmm_em_step_batched_host_iters", "sdmm_write_exr",
+    "sdmm_em_step_batched_host_iters", "sdmm_write_exr", "sdmm_clone_many_on_stream", "sdmm_copy_many",
+    "sdmm_guiding_update",
 ]
 
 
@@ -949,7 +951,7 @@ class STree:
 class _GuidingConfig(C.Structure):
     _fields_ = [("K", C.c_int), ("split_depth", C.c_int), ("split_threshold", C.c_int),
                 ("max_leaf_nodes", C.c_int), ("saved_per_path", C.c_int), ("depth_prior", C.c_float),
-                ("init_seed", C.c_uint64)]
+                ("init_seed", C.c_uint64), ("optimize_async", C.c_int)]
 
 
 class _GuidingStats(C.Structure):
@@ -997,6 +999,10 @@ class Guiding:
 
     def push(self, vertices: "PathVertices", seed: int):
         _check(lib().sdmm_guiding_push(self.h, C.byref(vertices.s), C.c_uint64(seed)))
+
+    def update(self):
+        """async: wait for the running EM and refresh the conditioners (sdmm_guiding_update)."""
+        _check(lib().sdmm_guiding_update(self.h))
 
     def optimize(self, spp: int) -> dict:
         st = _GuidingStats()

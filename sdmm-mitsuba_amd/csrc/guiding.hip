@@ -181,6 +181,16 @@ struct sdmm_guiding {
     size_t scratch_bytes = 0;
     float* pinned = nullptr;   // host staging of the splitting leaves' positions
     size_t pinned_floats = 0;
+    // optimizeAsync (volpath_sdmm.cpp:180-242): EM on its own stream while the
+    // next pass renders with the conditioners (cond) of the previous update
+    bool async = false;
+    hipStream_t em_st = nullptr;
+    hipEvent_t em_done = nullptr, copied = nullptr;
+    std::vector<sdmm_mix*> cond;     // per node: the conditioner the renders use
+    std::vector<int> pending;        // leaves stepped by the running EM
+    bool running = false;
+    float* tbuf = nullptr;           // the running EM's training data (7 planes)
+    int64_t tcap = 0;
 };
 
 namespace {
@@ -319,6 +329,25 @@ int redistribute(sdmm_guiding* g, int old_nodes) {
             sdmm_destroy(g->mix[(size_t)v]);
             g->mix[(size_t)v] = nullptr;
         }
+    if (g->async) {   // the conditioners follow their mixtures
+        g->cond.resize((size_t)nn, nullptr);
+        std::vector<const sdmm_mix*> src;
+        std::vector<int> dst;
+        for (int c = old_nodes; c < nn; ++c) {
+            const int v = origin[(size_t)c];
+            if (child[2 * (size_t)c] >= 0 || v < 0 || !g->cond[(size_t)v]) continue;
+            src.push_back(g->cond[(size_t)v]);
+            dst.push_back(c);
+        }
+        std::vector<sdmm_mix*> made(src.size(), nullptr);
+        SDMM_TRY(sdmm_clone_many_on_stream(src.data(), (int)src.size(), (void*)g->st, made.data()));
+        for (size_t i = 0; i < dst.size(); ++i) g->cond[(size_t)dst[i]] = made[i];
+        for (int v = 0; v < old_nodes; ++v)
+            if (was_split[(size_t)v] && g->cond[(size_t)v]) {
+                sdmm_destroy(g->cond[(size_t)v]);
+                g->cond[(size_t)v] = nullptr;
+            }
+    }
     // records and stats positions: relabelled on the device (order kept)
     uint8_t* dsplit = nullptr;
     int32_t* dparent = nullptr;
@@ -334,9 +363,43 @@ int redistribute(sdmm_guiding* g, int old_nodes) {
     return SDMM_OK;
 }
 
+// the renders' table: the mixtures themselves (sync) or their conditioners (async)
+const std::vector<sdmm_mix*>& guide_table(const sdmm_guiding* g) { return g->async ? g->cond : g->mix; }
+
 int bind(sdmm_guiding* g) {
-    std::vector<const sdmm_mix*> tab(g->mix.begin(), g->mix.end());
+    const auto& src = guide_table(g);
+    std::vector<const sdmm_mix*> tab((size_t)sdmm_stree_num_nodes(g->tree), nullptr);
+    for (size_t i = 0; i < src.size() && i < tab.size(); ++i) tab[i] = src[i];
     return sdmm_stree_bind_mixtures(g->tree, tab.data());
+}
+
+// optimize_async_wait_and_update (:227-242): wait for the running EM, then
+// each stepped leaf's conditioner := its mixture (sdmm::prepare)
+int update(sdmm_guiding* g) {
+    if (!g->async || !g->running) return SDMM_OK;
+    HIP_TRY(hipEventSynchronize(g->em_done));
+    g->running = false;
+    g->cond.resize(g->mix.size(), nullptr);
+    std::vector<const sdmm_mix*> csrc, nsrc;
+    std::vector<sdmm_mix*> cdst;
+    std::vector<int> fresh;
+    for (int v : g->pending) {
+        const sdmm_mix* m = g->mix[(size_t)v];
+        if (!m) continue;
+        if (g->cond[(size_t)v]) {
+            csrc.push_back(m);
+            cdst.push_back(g->cond[(size_t)v]);
+        } else {
+            nsrc.push_back(m);
+            fresh.push_back(v);
+        }
+    }
+    g->pending.clear();
+    SDMM_TRY(sdmm_copy_many(csrc.data(), cdst.data(), (int)csrc.size()));
+    std::vector<sdmm_mix*> made(nsrc.size(), nullptr);
+    SDMM_TRY(sdmm_clone_many_on_stream(nsrc.data(), (int)nsrc.size(), (void*)g->st, made.data()));
+    for (size_t i = 0; i < fresh.size(); ++i) g->cond[(size_t)fresh[i]] = made[i];
+    return bind(g);
 }
 
 }  // namespace
@@ -352,6 +415,7 @@ void sdmm_guiding_config_default(sdmm_guiding_config* c) {
     c->saved_per_path = 8;      // savedSamplesPerPath (:62)
     c->depth_prior = 0.01f;
     c->init_seed = 0x1A17;
+    c->optimize_async = 0;      // optimizeAsync (:65; the test suite's XML default is true)
 }
 
 int sdmm_guiding_create(const float tree_min[3], const float tree_max[3], const sdmm_guiding_config* cfg,
@@ -383,6 +447,13 @@ int sdmm_guiding_create(const float tree_min[3], const float tree_max[3], const 
         }
     }
     if (!r) r = sdmm_stree_set_stream(g->tree, (void*)g->st);
+    g->async = cfg->optimize_async != 0;
+    if (!r && g->async) {
+        hipError_t e = hipStreamCreateWithFlags(&g->em_st, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&g->em_done, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&g->copied, hipEventDisableTiming);
+        if (e != hipSuccess) r = fail(SDMM_E_HIP, std::string("sdmm_guiding_create: ") + hipGetErrorString(e));
+    }
     if (r) {
         sdmm_guiding_destroy(g);
         return r;
@@ -399,7 +470,12 @@ void sdmm_guiding_destroy(sdmm_guiding* g) {
     if (!g) return;
     (void)hipSetDevice(g->device);
     if (g->st) (void)hipStreamSynchronize(g->st);
+    if (g->em_st) (void)hipStreamSynchronize(g->em_st);
     for (sdmm_mix* m : g->mix) sdmm_destroy(m);
+    for (sdmm_mix* m : g->cond) sdmm_destroy(m);
+    if (g->tbuf) (void)hipFree(g->tbuf);
+    if (g->em_done) (void)hipEventDestroy(g->em_done);
+    if (g->copied) (void)hipEventDestroy(g->copied);
     if (g->tree) sdmm_stree_destroy(g->tree);
     for (Pool* P : {&g->rec, &g->stat})
         for (int b = 0; b < 2; ++b) {
@@ -409,6 +485,7 @@ void sdmm_guiding_destroy(sdmm_guiding* g) {
     if (g->scratch) (void)hipFree(g->scratch);
     if (g->pinned) (void)hipHostFree(g->pinned);
     if (g->st) (void)hipStreamDestroy(g->st);
+    if (g->em_st) (void)hipStreamDestroy(g->em_st);
     delete g;
 }
 
@@ -416,17 +493,24 @@ sdmm_stree* sdmm_guiding_tree(sdmm_guiding* g) { return g ? g->tree : nullptr; }
 
 int sdmm_guiding_node_mixtures(const sdmm_guiding* g, const sdmm_mix** out, int cap) {
     if (!g || !out) return fail(SDMM_E_INVALID, "invalid argument");
-    const int nn = (int)g->mix.size();
+    const int nn = sdmm_stree_num_nodes(g->tree);
     if (cap < nn) return fail(SDMM_E_INVALID, "sdmm_guiding_node_mixtures: cap < num_nodes");
-    for (int i = 0; i < nn; ++i) out[i] = g->mix[(size_t)i];
+    const auto& t = guide_table(g);
+    for (int i = 0; i < nn; ++i) out[i] = (size_t)i < t.size() ? t[(size_t)i] : nullptr;
     return SDMM_OK;
 }
 
 int sdmm_guiding_trained(const sdmm_guiding* g) {
     if (!g) return 0;
     int n = 0;
-    for (const sdmm_mix* m : g->mix) n += m ? 1 : 0;
+    for (const sdmm_mix* m : guide_table(g)) n += m ? 1 : 0;
     return n;
+}
+
+int sdmm_guiding_update(sdmm_guiding* g) {
+    if (!g) return fail(SDMM_E_INVALID, "invalid argument");
+    HIP_TRY(hipSetDevice(g->device));
+    return update(g);
 }
 
 // push_back_data for a render pass's paths (Li's tail): records appended to
@@ -485,6 +569,7 @@ int sdmm_guiding_push(sdmm_guiding* g, const sdmm_path_vertices* v, uint64_t see
 int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
     if (!g || spp < 0) return fail(SDMM_E_INVALID, "invalid argument");
     HIP_TRY(hipSetDevice(g->device));
+    SDMM_TRY(update(g));   // async: no split while an EM runs
     PhaseClock clk(g->st);
     Pool& R = g->rec;
     Pool& S = g->stat;
@@ -597,7 +682,7 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
         std::vector<sdmm_mix*> made((size_t)nf, nullptr);
         sdmm_em_params ep;
         sdmm_em_params_default(&ep);
-        int r = sdmm_create_many_on_stream(K, &ep, g->device, (void*)g->st, nf, made.data());
+        int r = sdmm_create_many_on_stream(K, &ep, g->device, (void*)(g->async ? g->em_st : g->st), nf, made.data());
         if (r) return r;
         for (int i = 0; i < nf; ++i) {
             const int v = fresh[(size_t)i];
@@ -610,7 +695,10 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
             float diag = 0.0f;
             for (int a3 = 0; a3 < 3; ++a3)
                 diag = std::max(diag, aabb[6 * (size_t)v + 3 + a3] - aabb[6 * (size_t)v + a3]);
-            dist[(size_t)i] = (float)(3.0 * (double)diag / (double)npos);
+            // initializeSDMMContext(context, hmax(diag)) (:292); the async run
+            // passes 0.1 * hmax(diag) (:218)
+            const float maxd = g->async ? 0.1f * diag : diag;
+            dist[(size_t)i] = (float)(3.0 * (double)maxd / (double)npos);
             seeds[(size_t)i] = g->cfg.init_seed + (uint64_t)v;
         }
         r = sdmm_init_hemisphere_batched(made.data(), nf, pos.data(), nrm.data(), g->cfg.depth_prior, dist.data(),
@@ -626,16 +714,47 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
         mixes.push_back(g->mix[(size_t)v]);
         bseg.push_back(R.seg[(size_t)v + 1]);
     }
-    std::vector<int> iters(mixes.size());
-    SDMM_TRY(sdmm_iterations_run(mixes.data(), (int)mixes.size(), iters.data()));
-    for (int& it : iters) it = it < 4 ? 2 : 1;   // (:299-302)
+    std::vector<int> iters(mixes.size(), 1);   // async: one em_step per leaf (:220)
+    if (!g->async) {
+        SDMM_TRY(sdmm_iterations_run(mixes.data(), (int)mixes.size(), iters.data()));
+        for (int& it : iters) it = it < 4 ? 2 : 1;   // (:299-302)
+    }
     clk.lap("init");
     const int64_t prefix = bseg.back();
     sdmm_samples smp{};
-    for (int i = 0; i < 6; ++i) smp.x[i] = P + i * cap;
-    smp.w = P + 9 * cap;
-    smp.n = prefix;
-    SDMM_TRY(sdmm_em_step_batched_iters(mixes.data(), (int)mixes.size(), &smp, bseg.data(), iters.data()));
+    if (!g->async) {
+        for (int i = 0; i < 6; ++i) smp.x[i] = P + i * cap;
+        smp.w = P + 9 * cap;
+        smp.n = prefix;
+        SDMM_TRY(sdmm_em_step_batched_iters(mixes.data(), (int)mixes.size(), &smp, bseg.data(), iters.data()));
+    } else {
+        // the swap to training_data (:208-212): the prefix moves to the EM's own
+        // buffer (the pool keeps taking the next pass's records), the EM is
+        // enqueued on its stream and runs beside the next pass (:214-223)
+        if (prefix > g->tcap) {
+            HIP_TRY(hipStreamSynchronize(g->em_st));
+            if (g->tbuf) HIP_TRY(hipFree(g->tbuf));
+            g->tbuf = nullptr;
+            g->tcap = 0;
+            const int64_t want = prefix + prefix / 2;
+            HIP_TRY(hipMalloc((void**)&g->tbuf, sizeof(float) * 7 * (size_t)want));
+            g->tcap = want;
+        }
+        for (int f = 0; f < 7; ++f)
+            HIP_TRY(hipMemcpyAsync(g->tbuf + f * g->tcap, P + (f < 6 ? f : 9) * cap, sizeof(float) * (size_t)prefix,
+                                   hipMemcpyDeviceToDevice, g->st));
+        HIP_TRY(hipEventRecord(g->copied, g->st));
+        HIP_TRY(hipStreamWaitEvent(g->em_st, g->copied, 0));
+        for (int i = 0; i < 6; ++i) smp.x[i] = g->tbuf + i * g->tcap;
+        smp.w = g->tbuf + 6 * g->tcap;
+        smp.n = prefix;
+        SDMM_TRY(sdmm_em_step_batched_iters(mixes.data(), (int)mixes.size(), &smp, bseg.data(), iters.data()));
+        HIP_TRY(hipEventRecord(g->em_done, g->em_st));
+        g->running = true;
+        g->pending.clear();
+        for (int v = 0; v < nn; ++v)
+            if (ready[(size_t)v]) g->pending.push_back(v);
+    }
     clk.lap("em");
     // (4) the optimised leaves' data is cleared (:308-309): drop the prefix
     if (prefix > 0) {
@@ -668,8 +787,9 @@ int sdmm_guiding_iteration(sdmm_guiding* g, sdmm_scene* scene, const sdmm_li_par
     q.guided = sdmm_guiding_trained(g) > 0 ? 1 : 0;
     sdmm_path_vertices v{};
     SDMM_TRY(sdmm_li_render(scene, g->tree, nullptr, &q, image, image_sqr, train ? &v : nullptr, li_stats));
+    if (train) SDMM_TRY(sdmm_guiding_push(g, &v, push_seed));
+    SDMM_TRY(update(g));   // (:446-448, after every pass)
     if (!train) return SDMM_OK;
-    SDMM_TRY(sdmm_guiding_push(g, &v, push_seed));
     return sdmm_guiding_optimize(g, p->spp * 1, out);
 }
 

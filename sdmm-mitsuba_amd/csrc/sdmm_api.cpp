@@ -829,30 +829,25 @@ int sdmm_create_many_on_stream(int K, const sdmm_em_params* params, int device, 
     return create_many(K, params, device, (hipStream_t)hip_stream, n, out);
 }
 
-int sdmm_clone_many(const sdmm_mix* const* src, int n, sdmm_mix** out) {
-    if (n < 0 || (n > 0 && (!src || !out))) return fail(SDMM_E_INVALID, "invalid argument");
-    if (n == 0) return SDMM_OK;
-    for (int i = 0; i < n; ++i) {
-        if (!src[i]) return fail(SDMM_E_INVALID, "NULL handle in src");
-        if (src[i]->K != src[0]->K || src[i]->device != src[0]->device)
-            return fail(SDMM_E_INVALID, "sources must share K and device");
-    }
-    const hipStream_t st = src[0]->stream;
-    HIP_TRY(hipSetDevice(src[0]->device));
-    for (int i = 1; i < n; ++i)
+}  // extern "C"
+
+namespace {
+
+// dst[i]'s mixture (the block prefix before the stats: parameters, derived
+// arrays, packed records, stepwise state) = src[i]'s, one kernel on `st`
+// after the sources' pending work
+int copy_prefix_many(const sdmm_mix* const* src, sdmm_mix* const* dst, int n, hipStream_t st) {
+    for (int i = 0; i < n; ++i)
         if (src[i]->stream != st) HIP_TRY(hipStreamSynchronize(src[i]->stream));
-    int r = create_many(src[0]->K, &src[0]->params, src[0]->device, st, n, out);
-    if (r) return r;
     const size_t bytes = (size_t)((char*)src[0]->stats - (char*)src[0]->C.weights);   // 16-aligned pieces
-    // one kernel over (src, dst) pointer pairs instead of n copies
     std::vector<void*> ptrs(2 * (size_t)n);
     for (int i = 0; i < n; ++i) {
-        out[i]->params = src[i]->params;
-        out[i]->guide_cap = src[i]->guide_cap;
-        out[i]->guide_order = src[i]->guide_order;
-        out[i]->initialised = src[i]->initialised;
+        dst[i]->params = src[i]->params;
+        dst[i]->guide_cap = src[i]->guide_cap;
+        dst[i]->guide_order = src[i]->guide_order;
+        dst[i]->initialised = src[i]->initialised;
         ptrs[(size_t)i] = src[i]->C.weights;
-        ptrs[(size_t)n + i] = out[i]->C.weights;
+        ptrs[(size_t)n + i] = dst[i]->C.weights;
     }
     void* dtab = nullptr;
     hipError_t e = hipMallocAsync(&dtab, sizeof(void*) * ptrs.size(), st);
@@ -860,11 +855,58 @@ int sdmm_clone_many(const sdmm_mix* const* src, int n, sdmm_mix** out) {
     if (e == hipSuccess) e = launch_copy_many(n, dtab, (void**)dtab + n, bytes, st);
     if (dtab) (void)hipFreeAsync(dtab, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);   // ptrs is a host temporary
-    if (e != hipSuccess) {
-        for (int j = 0; j < n; ++j) { sdmm_destroy(out[j]); out[j] = nullptr; }
-        return fail(SDMM_E_HIP, std::string("sdmm_clone_many: ") + hipGetErrorString(e));
+    if (e != hipSuccess) return fail(SDMM_E_HIP, std::string("mixture copy: ") + hipGetErrorString(e));
+    return SDMM_OK;
+}
+
+int check_same_kind(const sdmm_mix* const* a, int n) {
+    for (int i = 0; i < n; ++i) {
+        if (!a[i]) return fail(SDMM_E_INVALID, "NULL handle");
+        if (a[i]->K != a[0]->K || a[i]->device != a[0]->device)
+            return fail(SDMM_E_INVALID, "handles must share K and device");
     }
     return SDMM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sdmm_clone_many_on_stream(const sdmm_mix* const* src, int n, void* hip_stream, sdmm_mix** out) {
+    if (n < 0 || (n > 0 && (!src || !out))) return fail(SDMM_E_INVALID, "invalid argument");
+    if (n == 0) return SDMM_OK;
+    int r = check_same_kind(src, n);
+    if (r) return r;
+    HIP_TRY(hipSetDevice(src[0]->device));
+    const hipStream_t st = (hipStream_t)hip_stream;
+    r = create_many(src[0]->K, &src[0]->params, src[0]->device, st, n, out);
+    if (r) return r;
+    r = copy_prefix_many(src, out, n, st);
+    if (r)
+        for (int j = 0; j < n; ++j) { sdmm_destroy(out[j]); out[j] = nullptr; }
+    return r;
+}
+
+int sdmm_clone_many(const sdmm_mix* const* src, int n, sdmm_mix** out) {
+    if (n < 0 || (n > 0 && (!src || !out))) return fail(SDMM_E_INVALID, "invalid argument");
+    if (n == 0) return SDMM_OK;
+    if (!src[0]) return fail(SDMM_E_INVALID, "NULL handle in src");
+    return sdmm_clone_many_on_stream(src, n, (void*)src[0]->stream, out);
+}
+
+int sdmm_copy_many(const sdmm_mix* const* src, sdmm_mix* const* dst, int n) {
+    if (n < 0 || (n > 0 && (!src || !dst))) return fail(SDMM_E_INVALID, "invalid argument");
+    if (n == 0) return SDMM_OK;
+    int r = check_same_kind(src, n);
+    if (!r) r = check_same_kind(dst, n);
+    if (r) return r;
+    if (src[0]->K != dst[0]->K || src[0]->device != dst[0]->device)
+        return fail(SDMM_E_INVALID, "sources and destinations must share K and device");
+    HIP_TRY(hipSetDevice(dst[0]->device));
+    const hipStream_t st = dst[0]->stream;
+    for (int i = 1; i < n; ++i)
+        if (dst[i]->stream != st) HIP_TRY(hipStreamSynchronize(dst[i]->stream));
+    return copy_prefix_many(src, dst, n, st);
 }
 
 int sdmm_num_components(const sdmm_mix* m) { return m ? m->K : 0; }

@@ -103,22 +103,35 @@ def _subtree(child, v):
     return np.asarray(out)
 
 
-def _train(pkg, sc, tree, iterations, spp, K=16, seed=1):
+def _train(pkg, sc, tree, iterations, spp, K=16, seed=1, async_=False, state=None):
     """The plugin's optimize() loop (volpath_sdmm.cpp:244-312, :411-507) on
     the host side of the C-ABI: per leaf data + stats, split, canBeOptimized,
     hemisphere init with 3 hmax(diag) / (K/8), 2 EM iterations while
-    iterations_run < 4, bind."""
+    iterations_run < 4, bind.  async_: optimize_async_run /
+    optimize_async_wait_and_update (:180-242) -- renders use the conditioners
+    (cond), refreshed after each pass from the leaves the previous EM stepped;
+    one EM step per leaf, init with 3 (0.1 hmax(diag)) / (K/8)."""
     import torch
     nn = lambda: tree.num_nodes
     data = {}      # leaf -> list of record dicts (device)
     stats = {}     # leaf -> list of positions (host)
     mix = {}
+    cond = {}      # async: leaf -> conditioner
+    pending = []   # async: the leaves the running EM steps
     total_spp = 0
+
+    def update():
+        for v in pending:
+            cond[v] = mix[v].clone()
+        pending.clear()
+
     for it in range(iterations):
-        node_mix = [mix.get(i) for i in range(nn())]
+        table = cond if async_ else mix
+        node_mix = [table.get(i) for i in range(nn())]
         guided = any(m is not None for m in node_mix)
         _, verts, _ = sc.render(tree, node_mix if guided else None, spp=spp, guided=guided, seed=seed + it)
         out = tree.push_training(verts, 8, seed + 1000 + it)
+        update()
         seg = out["seg"]
         for v in range(nn()):
             a, b = int(seg[v]), int(seg[v + 1])
@@ -140,10 +153,11 @@ def _train(pkg, sc, tree, iterations, spp, K=16, seed=1):
                 # split: records, stats and mixture move to the children
                 sub = _subtree(child, v)
                 leaves = [int(i) for i in sub if child[i, 0] < 0]
-                parent = mix.pop(v, None)
-                if parent is not None:
-                    for c in leaves:
-                        mix[c] = parent.clone()
+                for tab in (mix, cond):
+                    parent = tab.pop(v, None)
+                    if parent is not None:
+                        for c in leaves:
+                            tab[c] = parent.clone()
                 recs = data.pop(v, [])
                 if recs:
                     x = [torch.cat([r["x"][i] for r in recs]) for i in range(6)]
@@ -182,14 +196,16 @@ def _train(pkg, sc, tree, iterations, spp, K=16, seed=1):
             w = torch.cat([r["w"] for r in recs])
             if v not in mix:
                 m = pkg.SDMM(K)
-                diag = float(np.max(aabb[v, 3:] - aabb[v, :3]))
+                diag = np.max(aabb[v, 3:] - aabb[v, :3]).astype(np.float32)
+                if async_:
+                    diag = np.float32(0.1) * diag
                 npos = K // 8
                 pos = torch.stack(x[:3], 1)[:npos].cpu().numpy()
                 nrm = torch.stack(nr, 1)[:npos].cpu().numpy()
-                m.init_hemisphere(pos, nrm, 0.01, 3.0 * diag / npos, 0x1A17 + v)
+                m.init_hemisphere(pos, nrm, 0.01, 3.0 * float(diag) / npos, 0x1A17 + v)
                 mix[v] = m
             m = mix[v]
-            its.append(2 if m.get_state()["scalars"][3] < 4 else 1)
+            its.append(1 if async_ else (2 if m.get_state()["scalars"][3] < 4 else 1))
             mixes.append(m)
             for i in range(6):
                 xs[i].append(x[i])
@@ -198,6 +214,12 @@ def _train(pkg, sc, tree, iterations, spp, K=16, seed=1):
         samples = pkg.DeviceSamples([torch.cat(t) for t in xs], torch.cat(ws))
         pkg.em_step_batched_iters(mixes, samples, np.asarray(segs, np.int64), np.asarray(its, np.int32))
         torch.cuda.synchronize()
+        pending[:] = ready
+    if async_:
+        if state is not None:
+            state["update"] = update
+            state["cond"] = cond
+        return [cond.get(i) for i in range(nn())]
     return [mix.get(i) for i in range(nn())]
 
 
@@ -303,3 +325,59 @@ def test_native_guiding_model_equals_host_loop(pkg, scenes, gpu, plog):
     img_r = sc.render(tree, ref_mix, spp=4, guided=True, seed=31)[0].clone()
     img_g = sc.render(g.tree, None, spp=4, guided=True, seed=31)[0]
     assert torch.equal(img_r, img_g)
+
+
+def _assert_same_mixtures(ref, got):
+    assert len(got) == len(ref)
+    n = 0
+    for i, (r, m) in enumerate(zip(ref, got)):
+        assert (r is None) == (m is None), i
+        if r is None:
+            continue
+        n += 1
+        pr, pm = r.get_params(), m.get_params()
+        for k in ("weights", "mean", "cov", "cholLInv", "detInv", "cdf"):
+            np.testing.assert_array_equal(pr[k], pm[k], err_msg=f"node {i} {k}")
+        sr, sm = r.get_state(), m.get_state()
+        for k in sr:
+            np.testing.assert_array_equal(sr[k], sm[k], err_msg=f"node {i} state {k}")
+    return n
+
+
+def test_native_guiding_model_async_equals_host_loop(pkg, scenes, gpu, plog):
+    """optimizeAsync (the suite's default, volpath_sdmm.cpp:180-242, :446-448,
+    :496-497): the EM runs on the model's own stream beside the next pass and
+    the renders read the conditioners.  The C++ model equals the async host
+    loop bitwise -- the conditioners after every pass's update, and after the
+    final explicit update the stepped mixtures too -- and its guided render is
+    unbiased."""
+    import torch
+    sc = _scene(pkg, scenes, 96, 54)
+    T, spp = 5, 8
+    tree = _tree(pkg, sc)
+    st = {}
+    ref_cond = _train(pkg, sc, tree, T, spp, K=16, seed=1, async_=True, state=st)
+    _, _, tmin, tmax = sc.normalization()
+    g = pkg.Guiding(tmin, tmax, optimize_async=1)
+    for it in range(T):
+        g.iteration(sc, spp, seed=1 + it, push_seed=1 + 1000 + it)
+    torch.cuda.synchronize()
+    for a, b in zip(tree.nodes(), g.tree.nodes()):
+        np.testing.assert_array_equal(a, b)
+    n = _assert_same_mixtures(ref_cond, g.node_mixtures())
+    assert n == g.trained > 0
+    # the EM launched by the last pass, applied
+    st["update"]()
+    g.update()
+    ref_cond = [st["cond"].get(i) for i in range(len(ref_cond))]
+    n2 = _assert_same_mixtures(ref_cond, g.node_mixtures())
+    plog("guiding_model_async_trained_leaves", n2, 1, lower=True, before_update=n)
+    img_r = sc.render(tree, ref_cond, spp=4, guided=True, seed=31)[0].clone()
+    img_g = sc.render(g.tree, None, spp=4, guided=True, seed=31)[0]
+    assert torch.equal(img_r, img_g)
+    lum = lambda im: im.cpu().numpy().mean(0).reshape(-1)
+    a = lum(sc.render(g.tree, None, spp=64, guided=True, seed=1234)[0])
+    u = lum(sc.render(g.tree, None, spp=64, guided=False, seed=4321)[0])
+    se = np.sqrt(a.var() / a.size + u.var() / u.size)
+    plog("li_async_guided_vs_unguided_mean_sigma", float(abs(a.mean() - u.mean()) / se), 4.0)
+    assert abs(a.mean() - u.mean()) < 4.0 * se

@@ -13,7 +13,8 @@ spec.loader.exec_module(bench)
 if __name__ == "__main__":
     import torch
     pkg = bench.load_pkg()
-    out = bench.cornell_bench(pkg, torch.device("cuda", 0), None, 1)
-    print(json.dumps({k: v for k, v in out.items() if k != "iterations"}))
-    for it in out["iterations"]:
-        print(json.dumps(it))
+    for mode in (0, 1):
+        out = bench.cornell_bench(pkg, torch.device("cuda", 0), None, 1, optimize_async=mode)
+        print(json.dumps({k: v for k, v in out.items() if k != "iterations"}))
+        for it in out["iterations"]:
+            print(json.dumps(it))
