@@ -135,6 +135,28 @@ int sdmm_init_hemisphere(sdmm_mix* m, const float* positions, const float* norma
 int sdmm_init_hemisphere_batched(sdmm_mix* const* mixes, int n, const float* positions, const float* normals,
                                  float depth_prior, const float* min_spatial_distance, const uint64_t* seeds);
 
+/* kMeansPPInit (dmm/jmm/mixture_model_init.h:244-330) on the device: for each
+ * of n_leaves leaves -- samples [seg[l], seg[l+1]) of the device planes s->x[0..2]
+ * (positions), normals[0..2] and s->w -- the k-means++ choice of n_pos seed
+ * samples, draw i using uniforms[l * n_pos + i] (the rng() calls, in order).
+ * out_index (host, n_leaves * n_pos): leaf-relative sample indices;
+ * out_positions / out_normals (host, 3 per draw, may be NULL): the chosen
+ * samples' positions and normals.  Weights
+ * and their sums in fp64 (the reference forms a float CDF; the choice differs
+ * only where a draw falls within its rounding of a boundary).  One workgroup
+ * per leaf on hip_stream; returns after the indices are on the host. */
+int sdmm_kmeanspp_select(const sdmm_samples* s, const float* const normals[3], const int64_t* seg, int n_leaves,
+                         int n_pos, const float* uniforms, int device, void* hip_stream, int64_t* out_index,
+                         float* out_positions, float* out_normals);
+
+/* uniformHemisphereInit with kMeansPlusPlus = true (:130-138) for n mixtures
+ * of one K: mixture i's K/8 positions / normals chosen by sdmm_kmeanspp_select
+ * over samples [seg[i], seg[i+1]); its PCG32 stream (seeds[i]) gives the
+ * K/8 k-means++ draws and then the direction jitter. */
+int sdmm_init_hemisphere_kmeanspp_batched(sdmm_mix* const* mixes, int n, const sdmm_samples* s,
+                                          const float* const normals[3], const int64_t* seg, float depth_prior,
+                                          const float* min_spatial_distance, const uint64_t* seeds);
+
 /* Host-only variant (no device, no handle): writes the initial component
  * parameters, for data generators and tests.  Arrays sized K=8*n_pos. */
 int sdmm_hemisphere_init_host(const float* positions, const float* normals, int n_pos,

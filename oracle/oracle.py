@@ -91,6 +91,11 @@ def lib():
         L.or_component_set.argtypes = [C.c_void_p, C.c_int, _d, _d, C.c_int]
         L.or_guide_product_batch.argtypes = [C.c_void_p, C.c_int64, _f, _f, C.POINTER(C.c_int32), _f, _f, _f,
                                              _f, C.c_int, _f, _f, _f, C.POINTER(C.c_int32), _f]
+        _l = C.POINTER(C.c_int64)
+        L.or_kmeanspp_select.argtypes = [_f, _f, _f, _f, _f, _f, _f, C.c_int64, C.c_int, _f, C.c_int, _l]
+        L.or_uniform_hemisphere_init_kmeanspp.argtypes = [
+            C.c_void_p, C.c_void_p, _f, _f, _f, _f, _f, _f, _f, C.c_int64, C.c_int, C.c_float, C.c_float,
+            C.c_uint64, C.c_int, C.c_int, _l]
         L.or_mvtn_multiply.restype = C.c_float
         L.or_mvtn_multiply.argtypes = [_f, _f, _f, _f, _f]
         _lib = L
@@ -206,6 +211,38 @@ def hemisphere_init(K_positions, positions, normals, depth_prior, min_dist, seed
     lib().or_uniform_hemisphere_init(m.ptr, st.ptr if st else None, _fp(pos), _fp(nrm),
                                      K_positions, depth_prior, min_dist, seed, mode)
     return m, st
+
+
+def kmeanspp_select(x, normals, w, n_pos, u, mode=1):
+    """kMeansPPInit (mixture_model_init.h:244-330): the sample indices of the
+    n_pos seed positions for the draws u.  mode 0: the reference's float CDF;
+    mode 1: the device rule (fp64 weights and sums), see sdmm_oracle_kmeans.c."""
+    xs = [np.ascontiguousarray(x[i], np.float32) for i in range(3)]
+    ns = [np.ascontiguousarray(normals[i], np.float32) for i in range(3)]
+    ww = np.ascontiguousarray(w, np.float32)
+    uu = np.ascontiguousarray(u, np.float32)
+    assert uu.size >= n_pos
+    out = np.zeros(n_pos, np.int64)
+    r = lib().or_kmeanspp_select(*[_fp(a) for a in xs + ns], _fp(ww), ww.size, n_pos, _fp(uu), mode,
+                                 out.ctypes.data_as(C.POINTER(C.c_int64)))
+    assert r == 0, r
+    return out
+
+
+def hemisphere_init_kmeanspp(K_positions, x, normals, w, depth_prior, min_dist, seed, mode=1, select_mode=1):
+    """uniformHemisphereInit with kMeansPlusPlus = true (:130-138): one PCG32
+    stream for the k-means++ draws and then the direction jitter."""
+    K = K_positions * 8
+    m = Mixture(K)
+    st = EmState(K)
+    xs = [np.ascontiguousarray(x[i], np.float32) for i in range(3)]
+    ns = [np.ascontiguousarray(normals[i], np.float32) for i in range(3)]
+    ww = np.ascontiguousarray(w, np.float32)
+    idx = np.zeros(K_positions, np.int64)
+    r = lib().or_uniform_hemisphere_init_kmeanspp(m.ptr, st.ptr, *[_fp(a) for a in xs + ns], _fp(ww), ww.size,
+                                                  K_positions, depth_prior, min_dist, seed, mode, select_mode,
+                                                  idx.ctypes.data_as(C.POINTER(C.c_int64)))
+    return m, st, idx, r
 
 
 def stats_len(K):

@@ -608,9 +608,19 @@ void or_em_state_init(or_em_state* st, int K, double alpha, const double bPrior5
 int or_uniform_hemisphere_init(or_mixture* m, or_em_state* st, const float* positions,
                                const float* normals, int nPositions, float depthPrior,
                                float minAllowedSpatialDistance, uint64_t seed, int mode) {
-    FTZ_SCOPE;
     or_pcg32 rng;
     or_pcg32_seed(&rng, seed, 0xda3e39cb94b95bdbULL);
+    return or_uniform_hemisphere_init_rng(m, st, positions, normals, nPositions, depthPrior,
+                                          minAllowedSpatialDistance, &rng, mode);
+}
+
+/* the same, drawing the direction jitter from a caller's PCG32 stream (the
+ * kMeansPlusPlus branch shares one rng between the position choice and it) */
+int or_uniform_hemisphere_init_rng(or_mixture* m, or_em_state* st, const float* positions,
+                                   const float* normals, int nPositions, float depthPrior,
+                                   float minAllowedSpatialDistance, or_pcg32* rngp, int mode) {
+    FTZ_SCOPE;
+    or_pcg32 rng = *rngp;
     const float maxRadiusSqr = (float)10.644640675668422; /* chi2(6).quantile(0.90) */
     const float widthVarSqr =
         (float)(0.5 * (double)minAllowedSpatialDistance * (double)minAllowedSpatialDistance /
@@ -672,6 +682,7 @@ int or_uniform_hemisphere_init(or_mixture* m, or_em_state* st, const float* posi
             }
         }
     }
+    *rngp = rng;
     return or_mixture_configure(m);
 }
 

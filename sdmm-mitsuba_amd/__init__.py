@@ -174,6 +174,10 @@ def lib():
         L.sdmm_write_exr.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_float]
         L.sdmm_push_training.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_uint64, C.c_void_p,
                                          C.POINTER(C.c_int64), C.c_void_p, C.POINTER(C.c_int64)]
+        L.sdmm_kmeanspp_select.argtypes = [C.c_void_p, C.c_void_p * 3, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
+                                           C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.sdmm_init_hemisphere_kmeanspp_batched.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p * 3,
+                                                            C.c_void_p, C.c_float, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -215,7 +219,7 @@ EXPORTED_SYMBOLS = [
     "sdmm_guiding_iteration", "sdmm_create_on_stream", "sdmm_create_many_on_stream", "sdmm_clone_many",
     "sdmm_init_hemisphere_batched", "sdmm_iterations_run", "sdmm_stree_split_leaf_recurse_many",
     "sdmm_em_step_batched_host_iters", "sdmm_write_exr", "sdmm_clone_many_on_stream", "sdmm_copy_many",
-    "sdmm_guiding_update",
+    "sdmm_guiding_update", "sdmm_kmeanspp_select", "sdmm_init_hemisphere_kmeanspp_batched",
 ]
 
 
@@ -231,6 +235,42 @@ def em_step_batched(mixes, samples, seg, iterations: int = 1):
     hs = (C.c_void_p * max(n, 1))(*[m.h for m in mixes])
     _check(lib().sdmm_em_step_batched(hs, n, samples.ptr, seg.ctypes.data_as(C.POINTER(C.c_int64)),
                                       iterations))
+
+
+def kmeanspp_select(samples, normals, seg, n_pos, uniforms, stream=None):
+    """kMeansPPInit (mixture_model_init.h:244-330) for the leaves [seg[l],
+    seg[l+1]) of `samples` (positions x[0..2], weights w) with device normal
+    planes `normals`: (indices (n_leaves, n_pos) leaf-relative, positions
+    (n_leaves, n_pos, 3), normals (n_leaves, n_pos, 3))."""
+    import torch
+    seg = np.ascontiguousarray(seg, np.int64)
+    nl = seg.size - 1
+    u = np.ascontiguousarray(uniforms, np.float32).reshape(-1)
+    assert u.size == nl * n_pos
+    nt = [t.contiguous() for t in normals]
+    idx = np.zeros((nl, n_pos), np.int64)
+    pos = np.zeros((nl, n_pos, 3), np.float32)
+    nrm = np.zeros((nl, n_pos, 3), np.float32)
+    dev = samples.w.device.index or 0
+    st = stream if stream is not None else torch.cuda.current_stream(samples.w.device).cuda_stream
+    _check(lib().sdmm_kmeanspp_select(samples.ptr, (C.c_void_p * 3)(*[t.data_ptr() for t in nt]), seg.ctypes.data,
+                                      nl, n_pos, u.ctypes.data, dev, st, idx.ctypes.data, pos.ctypes.data,
+                                      nrm.ctypes.data))
+    return idx, pos, nrm
+
+
+def init_hemisphere_kmeanspp_batched(mixes, samples, normals, seg, depth_prior, min_spatial_distance, seeds):
+    """uniformHemisphereInit with kMeansPlusPlus (mixture_model_init.h:130-138)
+    for many mixtures of one K: mixture i over samples [seg[i], seg[i+1])."""
+    seg = np.ascontiguousarray(seg, np.int64)
+    n = len(mixes)
+    assert seg.shape == (n + 1,)
+    dist = np.ascontiguousarray(np.broadcast_to(np.asarray(min_spatial_distance, np.float32), (n,)))
+    sd = np.ascontiguousarray(np.broadcast_to(np.asarray(seeds, np.uint64), (n,)))
+    nt = [t.contiguous() for t in normals]
+    hs = (C.c_void_p * max(n, 1))(*[m.h for m in mixes])
+    _check(lib().sdmm_init_hemisphere_kmeanspp_batched(hs, n, samples.ptr, (C.c_void_p * 3)(*[t.data_ptr() for t in nt]),
+                                                       seg.ctypes.data, depth_prior, dist.ctypes.data, sd.ctypes.data))
 
 
 def _iters(n, iterations):

@@ -179,12 +179,15 @@ float fl_cos(float x) { return (float)std::cos((double)x); }
 float fl_sin(float x) { return (float)std::sin((double)x); }
 
 // mixture_model_init.h:79-242 (kMeansPlusPlus == false branch).
+// skip: draws already taken from the stream (kMeansPlusPlus: one per position
+// for the k-means++ choice, :130-138, before the direction jitter)
 void hemisphere_init(const float* positions, const float* normals, int nPositions, float depthPrior,
                      float minDist, uint64_t seed, float* weights, float* means, float* covs,
-                     float* bpriors, float* bdepth) {
+                     float* bpriors, float* bdepth, int skip = 0) {
     const double PI = 3.14159265358979323846;
     Pcg32 rng;
     rng.seed(seed, 0xda3e39cb94b95bdbULL);
+    for (int i = 0; i < skip; ++i) (void)rng.next_uint();
     const float maxRadiusSqr = (float)10.644640675668422;  // chi2(6).quantile(0.9)
     const float widthVarSqr = (float)(0.5 * (double)minDist * (double)minDist / (double)maxRadiusSqr);
     const float depthVarSqr = depthPrior * depthPrior / maxRadiusSqr;
@@ -1024,8 +1027,45 @@ int sdmm_init_hemisphere(sdmm_mix* m, const float* positions, const float* norma
     return upload_and_set(m, w.data(), mean.data(), cov.data());
 }
 
+static int init_hemisphere_batched_impl(sdmm_mix* const* mixes, int n, const float* positions,
+                                        const float* normals, float depth_prior, const float* min_spatial_distance,
+                                        const uint64_t* seeds, int skip);
+
 int sdmm_init_hemisphere_batched(sdmm_mix* const* mixes, int n, const float* positions, const float* normals,
                                  float depth_prior, const float* min_spatial_distance, const uint64_t* seeds) {
+    return init_hemisphere_batched_impl(mixes, n, positions, normals, depth_prior, min_spatial_distance, seeds, 0);
+}
+
+int sdmm_init_hemisphere_kmeanspp_batched(sdmm_mix* const* mixes, int n, const sdmm_samples* s,
+                                          const float* const normals[3], const int64_t* seg, float depth_prior,
+                                          const float* min_spatial_distance, const uint64_t* seeds) {
+    if (n < 0 || (n > 0 && (!mixes || !s || !normals || !seg || !min_spatial_distance || !seeds)))
+        return fail(SDMM_E_INVALID, "invalid argument");
+    if (n == 0) return SDMM_OK;
+    if (!mixes[0]) return fail(SDMM_E_INVALID, "NULL handle in mixes");
+    const int K = mixes[0]->K;
+    if (K % 8) return fail(SDMM_E_INVALID, "K must be a multiple of 8");
+    const int npos = K / 8;
+    // one PCG32 stream per mixture: npos draws for the k-means++ choice, then
+    // the direction jitter (uniformHemisphereInit's rng, :130-138, :199-232)
+    std::vector<float> u((size_t)n * npos);
+    for (int i = 0; i < n; ++i) {
+        Pcg32 rng;
+        rng.seed(seeds[i], 0xda3e39cb94b95bdbULL);
+        for (int j = 0; j < npos; ++j) u[(size_t)i * npos + j] = rng.next_float();
+    }
+    std::vector<int64_t> idx((size_t)n * npos);
+    std::vector<float> pos((size_t)n * npos * 3), nrm((size_t)n * npos * 3);
+    int r = sdmm_kmeanspp_select(s, normals, seg, n, npos, u.data(), mixes[0]->device, (void*)mixes[0]->stream,
+                                 idx.data(), pos.data(), nrm.data());
+    if (r) return r;
+    return init_hemisphere_batched_impl(mixes, n, pos.data(), nrm.data(), depth_prior, min_spatial_distance, seeds,
+                                        npos);
+}
+
+static int init_hemisphere_batched_impl(sdmm_mix* const* mixes, int n, const float* positions,
+                                        const float* normals, float depth_prior, const float* min_spatial_distance,
+                                        const uint64_t* seeds, int skip) {
     if (n < 0 || (n > 0 && (!mixes || !positions || !normals || !min_spatial_distance || !seeds)))
         return fail(SDMM_E_INVALID, "invalid argument");
     if (n == 0) return SDMM_OK;
@@ -1055,9 +1095,8 @@ int sdmm_init_hemisphere_batched(sdmm_mix* const* mixes, int n, const float* pos
         double* pc = (double*)(b + 4 * Kz + 48 * Kz);
         float* pb = (float*)(b + 4 * Kz + 48 * Kz + 200 * Kz);
         float* pd = (float*)(b + 4 * Kz + 48 * Kz + 200 * Kz + 100 * Kz);
-        r = sdmm_hemisphere_init_host(positions + 3 * (size_t)npos * i, normals + 3 * (size_t)npos * i, npos,
-                                      depth_prior, min_spatial_distance[i], seeds[i], pw, mean.data(), cov.data(),
-                                      pb, pd);
+        hemisphere_init(positions + 3 * (size_t)npos * i, normals + 3 * (size_t)npos * i, npos, depth_prior,
+                        min_spatial_distance[i], seeds[i], pw, mean.data(), cov.data(), pb, pd, skip);
         for (size_t j = 0; j < 6 * Kz; ++j) pm[j] = (double)mean[j];
         for (size_t j = 0; j < 25 * Kz; ++j) pc[j] = (double)cov[j];
     }

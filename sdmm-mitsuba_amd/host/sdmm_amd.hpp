@@ -433,6 +433,8 @@ public:
     int trained() const { return sdmm_guiding_trained(h_); }
     // Li's tail for a render pass, then optimize() (m_totalSpp += spp after)
     void push(const sdmm_path_vertices& v, uint64_t seed) { check(sdmm_guiding_push(h_, &v, seed), "sdmm_guiding_push"); }
+    // optimizeAsync: optimize_async_wait_and_update (volpath_sdmm.cpp:227-242)
+    void update() { check(sdmm_guiding_update(h_), "sdmm_guiding_update"); }
     sdmm_guiding_stats optimize(int spp) {
         sdmm_guiding_stats st{};
         check(sdmm_guiding_optimize(h_, spp, &st), "sdmm_guiding_optimize");

@@ -5,9 +5,10 @@
 // guided once a leaf is trained.  Writes each pass's image and the guiding
 // stats, for the bitwise comparison with the Python driver of the same loop.
 //
-// usage: guiding_harness scene.bin out.bin [exr_dir]
+// usage: guiding_harness scene.bin out.bin [exr_dir|-] [async]
 //   exr_dir: also dump iteration%05i.exr / iteration_sqr%05i.exr per pass
 //            (SDMMWorkResult::dumpIndividual, sdmm_wr.cpp:115-146)
+//   async  : optimizeAsync (volpath_sdmm.cpp:65, :180-242)
 //   scene.bin: int32 n_quads, n_bsdfs, n_emitters, width, height, spp_total, spp_it;
 //              float quads[9 n_quads]; int32 flip[n_quads], bsdf[n_quads], emitter[n_quads];
 //              float reflectance[3 n_bsdfs], radiance[3 n_emitters], cam[16], fov
@@ -15,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 #include "sdmm_amd.hpp"
@@ -23,7 +25,12 @@ template <class T>
 static bool rd(FILE* f, T* p, size_t n) { return std::fread(p, sizeof(T), n, f) == n; }
 
 int main(int argc, char** argv) {
-    if (argc != 3 && argc != 4) { std::fprintf(stderr, "usage: %s scene.bin out.bin [exr_dir]\n", argv[0]); return 2; }
+    if (argc < 3 || argc > 5) {
+        std::fprintf(stderr, "usage: %s scene.bin out.bin [exr_dir|-] [async]\n", argv[0]);
+        return 2;
+    }
+    const bool dump = argc >= 4 && std::strcmp(argv[3], "-") != 0;
+    const bool async = argc == 5 && std::strcmp(argv[4], "async") == 0;
     FILE* f = std::fopen(argv[1], "rb");
     if (!f) return 2;
     int32_t hdr[7];
@@ -47,7 +54,10 @@ int main(int argc, char** argv) {
         sdmm_amd::Scene scene(d);
         float smin[3], norm, tmin[3], tmax[3];
         scene.normalization(smin, &norm, tmin, tmax);
-        sdmm_amd::GuidingModel model(tmin, tmax);                 // split_to_depth(2), K = 16, 4000, 2048
+        sdmm_guiding_config cfg;
+        sdmm_guiding_config_default(&cfg);                       // split_to_depth(2), K = 16, 4000, 2048
+        cfg.optimize_async = async ? 1 : 0;
+        sdmm_amd::GuidingModel model(tmin, tmax, &cfg);
         float* image = nullptr;
         float* image_sqr = nullptr;
         if (hipMalloc(&image, sizeof(float) * 3 * (size_t)W * H) != hipSuccess ||
@@ -66,7 +76,7 @@ int main(int argc, char** argv) {
                 hipMemcpy(host.data(), image, sizeof(float) * host.size(), hipMemcpyDeviceToHost) != hipSuccess ||
                 hipMemcpy(host_sqr.data(), image_sqr, sizeof(float) * host.size(), hipMemcpyDeviceToHost) != hipSuccess)
                 return 1;
-            if (argc == 4) sdmm_amd::dump_iteration(argv[3], it, spp_it, 0.0f, W, H, host.data(), host_sqr.data());
+            if (dump) sdmm_amd::dump_iteration(argv[3], it, spp_it, 0.0f, W, H, host.data(), host_sqr.data());
             const int32_t rec[3] = {model.trained(), train ? st.leaves : -1, train ? st.optimized : -1};
             std::fwrite(rec, 4, 3, o);
             std::fwrite(host.data(), 4, host.size(), o);

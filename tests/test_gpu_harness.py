@@ -90,10 +90,12 @@ def test_plugin_pattern_batched_equals_threaded(pkg, synth, gpu, tmp_path):
     np.testing.assert_array_equal(a, c)
 
 
-def test_guiding_model_cpp_driver_equals_python(pkg, gpu, tmp_path):
+@pytest.mark.parametrize("async_", [0, 1])
+def test_guiding_model_cpp_driver_equals_python(pkg, gpu, tmp_path, async_):
     """The plugin's render() loop driven from C++ (tests/cpp/guiding_harness.cpp
     through sdmm_amd::Scene / GuidingModel) == the same loop from Python
-    (pkg.Guiding), bitwise: every pass's image and the trained-leaf counts."""
+    (pkg.Guiding), bitwise: every pass's image and the trained-leaf counts;
+    optimizeAsync off and on."""
     import importlib
     import torch
     scenes = importlib.import_module("sdmm_mitsuba_amd.scenes")
@@ -117,15 +119,15 @@ def test_guiding_model_cpp_driver_equals_python(pkg, gpu, tmp_path):
                     str(ROOT / "tests" / "cpp" / "guiding_harness.cpp"), f"-L{lib}", "-lsdmm_amd",
                     "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{lib}", "-Wl,-rpath,/opt/rocm/lib", "-pthread",
                     "-o", str(exe)], check=True)
-    subprocess.run([str(exe), str(tmp_path / "scene.bin"), str(tmp_path / "out.bin"), str(tmp_path / "exr")],
-                   check=True, timeout=300)
+    subprocess.run([str(exe), str(tmp_path / "scene.bin"), str(tmp_path / "out.bin"), str(tmp_path / "exr")]
+                   + (["async"] if async_ else []), check=True, timeout=300)
     out = np.fromfile(tmp_path / "out.bin", np.uint8)
     rec = 12 + 4 * 3 * W * H
     passes = spp_total // spp_it
     assert out.size == passes * rec
     sc = pkg.Scene(d)
     _, _, tmin, tmax = sc.normalization()
-    g = pkg.Guiding(tmin, tmax)
+    g = pkg.Guiding(tmin, tmax, optimize_async=async_)
     for it in range(passes):
         train = it * spp_it < spp_total // 4
         img, _, st = g.iteration(sc, spp_it, seed=1 + it, push_seed=1001 + it, train=train)
