@@ -1,0 +1,556 @@
+/*
+ * volpath_sdmm_amd.cpp -- the SDMM volumetric path tracer integrator for
+ * Mitsuba 0.6 with its guiding model on an MI355X through the C ABI of
+ * include/sdmm_gpu.h.  A maintainer drops this file in place of
+ * mitsuba/src/integrators/sdmm/volpath_sdmm.cpp (plus sdmm_proc.{h,cpp},
+ * whose roles it takes over) and links libsdmm_amd.so.
+ *
+ * NOT COMPILED in this repository: Mitsuba 0.6 and its dependencies are not in
+ * the image.  Every guiding call below is exercised by the tests through the
+ * same entry points (tests/test_gpu_li.py, tests/test_gpu_harness.py,
+ * tests/cpp/guiding_harness.cpp).
+ *
+ * What stays as in the reference plugin (mitsuba/src/integrators/sdmm/):
+ *   - the properties (volpath_sdmm.cpp:52-91) and their checks;
+ *   - the render() loop (:334-516): scene_norm.json, the tree box (getAABB,
+ *     :314-332), split_to_depth(2), sampleCount / samplesPerIteration passes,
+ *     training while samplesRendered < sampleCount / 4, optimizeAsync,
+ *     per-pass iteration%05i.exr dumps, stats.json, the final checkpoint;
+ *   - the film: each pass added with weight spp / sampleCount
+ *     (SDMMProcess::develop, sdmm_proc.cpp:1142-1158);
+ *   - Li (sdmm_proc.cpp:592-871): no NEE, BSDF / guide mixing with
+ *     heuristicConditionalWeight 0.5 (:383-392), pdf = h bsdfPdf + (1-h)
+ *     gmmPdf (:587-589), saved vertices with clamped pdf (:815-846),
+ *     recordRadiance (:615-637), Russian roulette after rrDepth (:858-868).
+ * What changes:
+ *   - the guiding state (tree, per-leaf SDMM + EM, training data, optimize)
+ *     lives on the GPU: one sdmm_guiding handle;
+ *   - Li runs bounce-synchronously over a tile of paths (a wavefront): the
+ *     CPU threads intersect and evaluate Mitsuba's BSDFs, and ONE
+ *     sdmm_guide_pdf_wavefront call per bounce and tile builds every
+ *     vertex's conditional once and samples it or evaluates its pdf;
+ *   - push_back_data (:876-965) is one sdmm_guiding_push per tile.
+ */
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <fstream>
+#include <iomanip>
+#include <memory>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include <mitsuba/core/plugin.h>
+#include <mitsuba/core/timer.h>
+#include <mitsuba/render/scene.h>
+
+#include <hip/hip_runtime.h>
+
+#include "sdmm_gpu.h"
+
+MTS_NAMESPACE_BEGIN
+
+namespace {
+
+void check_sdmm(int rc, const char* what) {
+    if (rc != SDMM_OK) SLog(EError, "%s failed (%i): %s", what, rc, sdmm_last_error());
+}
+
+void check_hip(hipError_t e, const char* what) {
+    if (e != hipSuccess) SLog(EError, "%s failed: %s", what, hipGetErrorString(e));
+}
+
+// Pinned host + device staging of one worker's wavefront (SoA planes).
+struct Staging {
+    int64_t cap = 0;
+    int V = 0;
+    // query planes: c 3, u 3, dgiven 3 (float); mode (u8); outputs d 3, pdf (float), comp (int32)
+    float* h_in = nullptr;
+    uint8_t* h_mode = nullptr;
+    float* h_out = nullptr;
+    int32_t* h_comp = nullptr;
+    float* d_in = nullptr;
+    uint8_t* d_mode = nullptr;
+    float* d_out = nullptr;
+    int32_t* d_comp = nullptr;
+    // saved-vertex records of the tile's paths (sdmm_path_vertices layout)
+    float* h_rec = nullptr;
+    int32_t* h_nv = nullptr;
+    float* d_rec = nullptr;
+    int32_t* d_nv = nullptr;
+
+    void allocate(int64_t n, int vslots) {
+        release();
+        cap = n;
+        V = vslots;
+        check_hip(hipHostMalloc((void**)&h_in, sizeof(float) * 9 * n, hipHostMallocDefault), "hipHostMalloc");
+        check_hip(hipHostMalloc((void**)&h_mode, n, hipHostMallocDefault), "hipHostMalloc");
+        check_hip(hipHostMalloc((void**)&h_out, sizeof(float) * 4 * n, hipHostMallocDefault), "hipHostMalloc");
+        check_hip(hipHostMalloc((void**)&h_comp, sizeof(int32_t) * n, hipHostMallocDefault), "hipHostMalloc");
+        check_hip(hipHostMalloc((void**)&h_rec, sizeof(float) * 16 * V * n, hipHostMallocDefault), "hipHostMalloc");
+        check_hip(hipHostMalloc((void**)&h_nv, sizeof(int32_t) * n, hipHostMallocDefault), "hipHostMalloc");
+        check_hip(hipMalloc((void**)&d_in, sizeof(float) * 9 * n), "hipMalloc");
+        check_hip(hipMalloc((void**)&d_mode, n), "hipMalloc");
+        check_hip(hipMalloc((void**)&d_out, sizeof(float) * 4 * n), "hipMalloc");
+        check_hip(hipMalloc((void**)&d_comp, sizeof(int32_t) * n), "hipMalloc");
+        check_hip(hipMalloc((void**)&d_rec, sizeof(float) * 16 * V * n), "hipMalloc");
+        check_hip(hipMalloc((void**)&d_nv, sizeof(int32_t) * n), "hipMalloc");
+    }
+    void release() {
+        for (void* p : {(void*)h_in, (void*)h_mode, (void*)h_out, (void*)h_comp, (void*)h_rec, (void*)h_nv})
+            if (p) (void)hipHostFree(p);
+        for (void* p : {(void*)d_in, (void*)d_mode, (void*)d_out, (void*)d_comp, (void*)d_rec, (void*)d_nv})
+            if (p) (void)hipFree(p);
+        h_in = h_out = d_in = d_out = h_rec = d_rec = nullptr;
+        h_mode = d_mode = nullptr;
+        h_comp = d_comp = h_nv = d_nv = nullptr;
+        cap = 0;
+    }
+    ~Staging() { release(); }
+    float& rec(int f, int v, int64_t p, int64_t n) { return h_rec[((int64_t)f * V + v) * n + p]; }
+};
+
+// One path of a tile's wavefront.
+struct PathState {
+    RayDifferential ray;
+    Intersection its;
+    Spectrum throughput, Li;
+    int depth;           // rRec.depth; -1 = finished
+    Point2 samplePos;
+    int64_t query;       // index into this bounce's query planes, -1 = BSDF only
+    // the BSDF sample drawn before the query (its direction is the pdf query's)
+    Spectrum bsdfWeight;
+    Float bsdfPdf;
+    bool pdfMode;        // the BSDF was chosen (rnd <= h)
+};
+
+}  // namespace
+
+class SDMMAmdPathTracer : public Integrator {
+public:
+    SDMMAmdPathTracer(const Properties& props) : Integrator(props) {
+        // the reference's properties (volpath_sdmm.cpp:52-65)
+        m_strictNormals = props.getBoolean("strictNormals", true);
+        m_maxDepth = props.getInteger("maxDepth", -1);
+        m_rrDepth = props.getInteger("rrDepth", 5);
+        m_samplesPerIteration = props.getInteger("samplesPerIteration", 8);
+        m_sampleProduct = props.getBoolean("sampleProduct", false);
+        m_bsdfOnly = props.getBoolean("bsdfOnly", false);
+        m_savedSamplesPerPath = props.getInteger("savedSamplesPerPath", 8);
+        m_optimizeAsync = props.getBoolean("optimizeAsync", true);
+        (void)props.getBoolean("flushDenormals", true);   // the device flushes f32 denormals
+        // this port's own
+        m_device = props.getInteger("hipDevice", 0);
+        m_tileSize = props.getInteger("wavefrontTile", 64);
+        if (m_rrDepth <= 0) Log(EError, "'rrDepth' must be set to a value greater than zero!");
+        if (m_maxDepth <= 0 && m_maxDepth != -1)
+            Log(EError, "'maxDepth' must be set to -1 (infinite) or a value greater than zero!");
+        if (m_maxDepth != m_rrDepth) Log(EError, "'maxDepth' must match 'rrDepth' for the SDMM integrator!");
+        if (m_sampleProduct)
+            Log(EError, "'sampleProduct' needs the materials' learned-BSDF tables "
+                        "(sdmm_guide_product_batch); not wired for generic Mitsuba BSDFs");
+    }
+
+    SDMMAmdPathTracer(Stream* stream, InstanceManager* manager) : Integrator(stream, manager) {
+        m_strictNormals = stream->readBool();
+        m_maxDepth = stream->readInt();
+        m_rrDepth = stream->readInt();
+        m_samplesPerIteration = stream->readInt();
+        m_sampleProduct = stream->readBool();
+        m_bsdfOnly = stream->readBool();
+        m_savedSamplesPerPath = stream->readInt();
+        m_optimizeAsync = stream->readBool();
+        m_device = stream->readInt();
+        m_tileSize = stream->readInt();
+    }
+
+    ~SDMMAmdPathTracer() {
+        if (m_guiding) sdmm_guiding_destroy(m_guiding);
+    }
+
+    void serialize(Stream* stream, InstanceManager* manager) const override {
+        Integrator::serialize(stream, manager);
+        stream->writeBool(m_strictNormals);
+        stream->writeInt(m_maxDepth);
+        stream->writeInt(m_rrDepth);
+        stream->writeInt(m_samplesPerIteration);
+        stream->writeBool(m_sampleProduct);
+        stream->writeBool(m_bsdfOnly);
+        stream->writeInt(m_savedSamplesPerPath);
+        stream->writeBool(m_optimizeAsync);
+        stream->writeInt(m_device);
+        stream->writeInt(m_tileSize);
+    }
+
+    bool preprocess(const Scene* scene, RenderQueue* queue, const RenderJob* job, int sceneResID, int sensorResID,
+                    int samplerResID) override {
+        Integrator::preprocess(scene, queue, job, sceneResID, sensorResID, samplerResID);
+        if (scene->getSubsurfaceIntegrators().size() > 0)
+            Log(EError, "Subsurface integrators are not supported by the SDMM path tracer!");
+        return true;
+    }
+
+    void cancel() override { m_cancelled = true; }
+
+    bool render(Scene* scene, RenderQueue* queue, const RenderJob* job, int, int, int) override {
+        ref<Sensor> sensor = scene->getSensor();
+        Film* film = sensor->getFilm();
+        const Vector2i size = film->getCropSize();
+        const size_t sampleCount = scene->getSampler()->getSampleCount();
+        const int nCores = std::max(1, (int)std::thread::hardware_concurrency());
+        if (sampleCount % m_samplesPerIteration != 0)
+            Log(EWarn, "sampleCount %% samplesPerIteration (" SIZE_T_FMT " %% %i) != 0", sampleCount,
+                m_samplesPerIteration);
+        const fs::path outDir = scene->getDestinationFile().parent_path();
+
+        // scene normalisation and the tree box (:375-396)
+        const AABB sceneBox = scene->getAABBWithoutCamera();
+        const Vector extents = sceneBox.getExtents();
+        m_sceneMin = sceneBox.min;
+        m_spatialNorm = std::max(extents[0], std::max(extents[1], extents[2]));
+        {
+            std::ofstream f((outDir / "scene_norm.json").string());
+            f << std::setprecision(9) << "{\n    \"scene_min\": [" << m_sceneMin[0] << ", " << m_sceneMin[1] << ", "
+              << m_sceneMin[2] << "],\n    \"spatial_norm\": " << m_spatialNorm << "\n}\n";
+        }
+        float tmin[3], tmax[3];
+        for (int a = 0; a < 3; ++a) {
+            tmin[a] = -1e-5f;
+            tmax[a] = (float)((sceneBox.max[a] - sceneBox.min[a]) / m_spatialNorm) + 1e-5f;
+        }
+        sdmm_guiding_config cfg;
+        sdmm_guiding_config_default(&cfg);             // K 16, split_to_depth(2), 4000, 2048
+        cfg.saved_per_path = m_savedSamplesPerPath;
+        cfg.optimize_async = m_optimizeAsync ? 1 : 0;
+        check_sdmm(sdmm_guiding_create(tmin, tmax, &cfg, m_device, &m_guiding), "sdmm_guiding_create");
+        m_stream = (hipStream_t)sdmm_stree_get_stream(sdmm_guiding_tree(m_guiding));
+
+        ref<Timer> timer = new Timer();
+        std::ostringstream stats;
+        stats << "[\n";
+        Float totalElapsed = 0;
+        bool success = true;
+        const int nPasses = (int)((sampleCount + m_samplesPerIteration - 1) / m_samplesPerIteration);
+        film->clear();
+        for (int samplesRendered = 0, it = 0; samplesRendered < (int)sampleCount;
+             samplesRendered += m_samplesPerIteration, ++it) {
+            const bool training = !m_bsdfOnly && samplesRendered < (int)sampleCount / 4;   // (:416)
+            timer->reset();
+            std::vector<float> mean(3 * (size_t)size.x * size.y), sqr(mean.size());
+            int64_t pathLength = 0, paths = 0;
+            success = renderPass(scene, sensor.get(), size, it, training, nCores, mean, sqr, pathLength, paths);
+            if (!success) break;
+            // optimize_async_wait_and_update after the pass (:446-448)
+            check_sdmm(sdmm_guiding_update(m_guiding), "sdmm_guiding_update");
+            const Float elapsed = timer->getSeconds();
+            totalElapsed += elapsed;
+            // the film: this pass with weight spp / sampleCount (sdmm_proc.cpp:1142-1158)
+            ref<Bitmap> bmp = new Bitmap(Bitmap::ERGB, Bitmap::EFloat32, size);
+            float* px = bmp->getFloat32Data();
+            const size_t plane = (size_t)size.x * size.y;
+            for (size_t i = 0; i < plane; ++i)
+                for (int ch = 0; ch < 3; ++ch) px[3 * i + ch] = mean[ch * plane + i];
+            film->addBitmap(bmp, (Float)1 / (Float)nPasses);
+            queue->signalRefresh(job);
+            // dumpIndividual (sdmm_wr.cpp:115-146)
+            char name[64];
+            std::snprintf(name, sizeof(name), "iteration%05i.exr", it);
+            check_sdmm(sdmm_write_exr((outDir / name).string().c_str(), size.x, size.y, mean.data(),
+                                      m_samplesPerIteration, it, (float)elapsed),
+                       "sdmm_write_exr");
+            std::snprintf(name, sizeof(name), "iteration_sqr%05i.exr", it);
+            check_sdmm(sdmm_write_exr((outDir / name).string().c_str(), size.x, size.y, sqr.data(),
+                                      m_samplesPerIteration, it, (float)elapsed),
+                       "sdmm_write_exr");
+            // optimize() / optimize_async_run() while training (:495-501)
+            timer->reset();
+            sdmm_guiding_stats gs{};
+            if (training) check_sdmm(sdmm_guiding_optimize(m_guiding, m_samplesPerIteration, &gs), "optimize");
+            const Float trainingSeconds = timer->getSeconds();
+            stats << (it ? ",\n" : "") << "    {\"iteration\": " << it << ", \"elapsed_seconds\": " << elapsed
+                  << ", \"total_elapsed_seconds\": " << totalElapsed << ", \"training_seconds\": " << trainingSeconds
+                  << ", \"mean_path_length\": " << (paths ? (double)pathLength / (double)paths : 0.0)
+                  << ", \"spp\": " << m_samplesPerIteration
+                  << ", \"total_spp\": " << samplesRendered + m_samplesPerIteration
+                  << ", \"leaf_nodes_count\": " << sdmm_stree_leaf_nodes(sdmm_guiding_tree(m_guiding))
+                  << ", \"optimized_nodes_count\": " << (training ? gs.optimized : 0) << "}";
+            if (m_cancelled) { success = false; break; }
+        }
+        check_sdmm(sdmm_guiding_update(m_guiding), "sdmm_guiding_update");
+        stats << "\n]\n";
+        std::ofstream((outDir / "stats.json").string()) << stats.str();
+        saveCheckpoint(outDir, nPasses);
+        return success;
+    }
+
+    MTS_DECLARE_CLASS()
+
+private:
+    // saveCheckpoint (:121-130): checkpoints/model_%05i.asdmm
+    void saveCheckpoint(const fs::path& dir, int iteration) {
+        const fs::path cdir = dir / "checkpoints";
+        if (!fs::exists(cdir)) fs::create_directories(cdir);
+        char name[64];
+        std::snprintf(name, sizeof(name), "model_%05i.asdmm", iteration);
+        sdmm_stree* tree = sdmm_guiding_tree(m_guiding);
+        std::vector<const sdmm_mix*> mix((size_t)sdmm_stree_num_nodes(tree));
+        check_sdmm(sdmm_guiding_node_mixtures(m_guiding, mix.data(), (int)mix.size()), "node_mixtures");
+        check_sdmm(sdmm_save_json(tree, mix.data(), (cdir / name).string().c_str()), "sdmm_save_json");
+    }
+
+    // One render pass over all tiles on nCores threads.
+    bool renderPass(Scene* scene, Sensor* sensor, const Vector2i& size, int iteration, bool training, int nCores,
+                    std::vector<float>& mean, std::vector<float>& sqr, int64_t& pathLength, int64_t& paths) {
+        const int T = m_tileSize;
+        const int tx = (size.x + T - 1) / T, ty = (size.y + T - 1) / T;
+        std::atomic<int> next{0};
+        std::atomic<int64_t> len{0}, cnt{0};
+        const bool guided = sdmm_guiding_trained(m_guiding) > 0;   // m_iteration != 0 (:311-316)
+        auto worker = [&](int wid) {
+            ref<Sampler> sampler = static_cast<Sampler*>(scene->getSampler()->clone().get());
+            Staging st;
+            const int V = std::max(1, m_maxDepth > 0 ? std::min(m_maxDepth - 1, 10) : 10);
+            st.allocate((int64_t)T * T * m_samplesPerIteration, V);
+            for (int t = next++; t < tx * ty && !m_cancelled; t = next++) {
+                const int x0 = (t % tx) * T, y0 = (t / tx) * T;
+                const int w = std::min(T, size.x - x0), h = std::min(T, size.y - y0);
+                int64_t l = 0, c = 0;
+                renderTile(scene, sensor, sampler, st, size, x0, y0, w, h, iteration, training, guided, mean, sqr,
+                           l, c);
+                len += l;
+                cnt += c;
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int i = 0; i < nCores; ++i) pool.emplace_back(worker, i);
+        for (auto& th : pool) th.join();
+        pathLength = len;
+        paths = cnt;
+        return !m_cancelled;
+    }
+
+    // One tile's paths as a wavefront (Li, sdmm_proc.cpp:592-871).  The
+    // bounce loop draws its numbers from the worker's sampler in wavefront
+    // order (every path's bounce b before any path's bounce b+1): use the
+    // independent sampler, as the test suite's scenes do.
+    void renderTile(Scene* scene, Sensor* sensor, Sampler* sampler, Staging& st, const Vector2i& size, int x0,
+                    int y0, int w, int h, int iteration, bool training, bool guided, std::vector<float>& mean,
+                    std::vector<float>& sqr, int64_t& pathLength, int64_t& pathCount) {
+        const int spp = m_samplesPerIteration;
+        const int64_t n = (int64_t)w * h * spp;
+        const int V = st.V;
+        const Float hWeight = 0.5f;                            // heuristicConditionalWeight (:383)
+        std::vector<PathState> P((size_t)n);
+        std::vector<int> nv((size_t)n, 0);
+        // camera rays and the first hit (:641-677)
+        for (int64_t p = 0; p < n; ++p) {
+            const int64_t pix = p / spp;
+            const Point2i xy(x0 + (int)(pix % w), y0 + (int)(pix / w));
+            if (p % spp == 0) sampler->generate(xy);
+            PathState& s = P[(size_t)p];
+            s.samplePos = Point2((Float)xy.x, (Float)xy.y) + sampler->next2D();
+            s.throughput = sensor->sampleRayDifferential(s.ray, s.samplePos, Point2(0.5f), 0.5f);
+            s.Li = Spectrum(0.0f);
+            s.depth = -1;
+            s.query = -1;
+            if (scene->rayIntersect(s.ray, s.its)) {
+                if (s.its.isEmitter()) s.Li += s.throughput * s.its.Le(-s.ray.d);
+                s.depth = 1;
+            } else {
+                s.Li += s.throughput * scene->evalEnvironment(s.ray);
+            }
+            sampler->advance();
+        }
+        std::vector<std::unique_ptr<BSDFSamplingRecord>> brecs((size_t)n);
+        for (int bounce = 0;; ++bounce) {
+            // loop head: depth cap, the BSDF sample, the guide query (:684-421)
+            int64_t nq = 0, live = 0;
+            for (int64_t p = 0; p < n; ++p) {
+                PathState& s = P[(size_t)p];
+                s.query = -1;
+                if (s.depth < 0) continue;
+                if (m_maxDepth >= 0 && s.depth >= m_maxDepth) { s.depth = -1; continue; }
+                const BSDF* bsdf = s.its.getBSDF(s.ray);
+                brecs[(size_t)p].reset(new BSDFSamplingRecord(s.its, sampler, ERadiance));
+                BSDFSamplingRecord& bRec = *brecs[(size_t)p];
+                s.bsdfWeight = bsdf->sample(bRec, s.bsdfPdf, sampler->next2D());
+                const bool smooth = (bsdf->getType() & BSDF::ESmooth) && !(bRec.sampledType & BSDF::EDelta);
+                ++live;
+                if (!guided || !smooth) continue;
+                const Float choice = sampler->next1D();
+                s.pdfMode = choice <= hWeight;
+                const Vector dB = s.its.toWorld(bRec.wo);
+                const int64_t q = nq++;
+                float* in = st.h_in;
+                const Point c((s.its.p - m_sceneMin) / m_spatialNorm);        // createCondition (:263-273)
+                in[0 * n + q] = (float)c.x; in[1 * n + q] = (float)c.y; in[2 * n + q] = (float)c.z;
+                in[3 * n + q] = (float)sampler->next1D();
+                in[4 * n + q] = (float)sampler->next1D();
+                in[5 * n + q] = (float)sampler->next1D();
+                in[6 * n + q] = (float)dB.x; in[7 * n + q] = (float)dB.y; in[8 * n + q] = (float)dB.z;
+                st.h_mode[q] = s.pdfMode ? 1 : 0;
+                s.query = q;
+            }
+            if (live == 0) break;
+            if (nq > 0) guideWavefront(st, n, nq);
+            // shade (:392-507, :759-871)
+            for (int64_t p = 0; p < n; ++p) {
+                PathState& s = P[(size_t)p];
+                if (s.depth < 0) continue;
+                const BSDF* bsdf = s.its.getBSDF(s.ray);
+                BSDFSamplingRecord& bRec = *brecs[(size_t)p];
+                const int32_t comp = s.query >= 0 ? st.h_comp[s.query] : -1;
+                Spectrum weight;
+                Float pdf;
+                if (comp == -1) {                      // BSDF only, h = 1 (:316-323)
+                    weight = s.bsdfWeight;
+                    pdf = s.bsdfPdf;
+                } else {
+                    const Float gmmPdf = st.h_out[3 * n + s.query];
+                    if (!s.pdfMode) {                  // the guide's direction
+                        const Vector d(st.h_out[0 * n + s.query], st.h_out[1 * n + s.query],
+                                       st.h_out[2 * n + s.query]);
+                        bRec.wo = s.its.toLocal(d);
+                    }
+                    const Float bsdfPdf = bsdf->pdf(bRec);
+                    pdf = bsdfPdf > 0 ? hWeight * bsdfPdf + (1 - hWeight) * gmmPdf : 0;   // (:587-589)
+                    weight = pdf > 0 ? bsdf->eval(bRec) / pdf : Spectrum(0.0f);
+                }
+                const Vector wo = s.its.toWorld(bRec.wo);
+                const Float woDotGeoN = dot(s.its.geoFrame.n, wo);
+                if (weight.isZero() || (m_strictNormals && woDotGeoN * Frame::cosTheta(bRec.wo) <= 0)) {
+                    s.depth = -1;                      // (:772-780)
+                    continue;
+                }
+                s.throughput *= weight;
+                // trace and look for an emitter (no NEE: MIS weight 1, :803-819)
+                const Point o = s.its.p;
+                const Normal n_s = s.its.shFrame.n;
+                const Point cnd((o - m_sceneMin) / m_spatialNorm);
+                s.ray = RayDifferential(o, wo, s.ray.time);
+                Spectrum value(0.0f);
+                const bool hit = scene->rayIntersect(s.ray, s.its);
+                if (hit) {
+                    if (s.its.isEmitter()) value = s.its.Le(-s.ray.d);
+                } else {
+                    value = scene->evalEnvironment(s.ray);
+                }
+                int& k = nv[(size_t)p];
+                if (!value.isZero()) {
+                    const Spectrum rad = s.throughput * value;
+                    s.Li += rad;
+                    recordRadiance(st, p, n, k, rad);
+                }
+                if (k < V) {                            // the saved vertex (:821-846)
+                    const Float clamped = std::max(pdf, (Float)0.1f);
+                    Float rgb[3], thr[3];
+                    value.toLinearRGB(rgb[0], rgb[1], rgb[2]);
+                    s.throughput.toLinearRGB(thr[0], thr[1], thr[2]);
+                    for (int ch = 0; ch < 3; ++ch) {
+                        st.rec(ch, k, p, n) = (float)(rgb[ch] / clamped);
+                        st.rec(3 + ch, k, p, n) = (float)thr[ch];
+                    }
+                    st.rec(6, k, p, n) = (float)clamped;
+                    st.rec(7, k, p, n) = (float)cnd.x; st.rec(8, k, p, n) = (float)cnd.y;
+                    st.rec(9, k, p, n) = (float)cnd.z;
+                    st.rec(10, k, p, n) = (float)wo.x; st.rec(11, k, p, n) = (float)wo.y;
+                    st.rec(12, k, p, n) = (float)wo.z;
+                    st.rec(13, k, p, n) = (float)n_s.x; st.rec(14, k, p, n) = (float)n_s.y;
+                    st.rec(15, k, p, n) = (float)n_s.z;
+                    ++k;
+                }
+                if (!hit) { s.depth = -1; continue; }
+                if (s.depth >= m_rrDepth) {             // Russian roulette (:858-868)
+                    const Float qq = std::min(s.throughput.max(), (Float)0.95f);
+                    if (sampler->next1D() >= qq) { s.depth = -1; continue; }
+                    s.throughput /= qq;
+                }
+                ++s.depth;
+            }
+        }
+        // the pixels' pass mean and mean of squares (box filter, sample order)
+        const size_t plane = (size_t)size.x * size.y;
+        for (int64_t pix = 0; pix < (int64_t)w * h; ++pix) {
+            Float acc[3] = {0, 0, 0}, sq[3] = {0, 0, 0};
+            for (int sidx = 0; sidx < spp; ++sidx) {
+                Float rgb[3];
+                P[(size_t)(pix * spp + sidx)].Li.toLinearRGB(rgb[0], rgb[1], rgb[2]);
+                for (int ch = 0; ch < 3; ++ch) { acc[ch] += rgb[ch]; sq[ch] += rgb[ch] * rgb[ch]; }
+            }
+            const size_t o = (size_t)(y0 + pix / w) * size.x + (size_t)(x0 + pix % w);
+            for (int ch = 0; ch < 3; ++ch) {
+                mean[ch * plane + o] = (float)(acc[ch] / spp);
+                sqr[ch * plane + o] = (float)(sq[ch] / spp);
+            }
+        }
+        for (int64_t p = 0; p < n; ++p) pathLength += nv[(size_t)p];
+        pathCount += n;
+        // push_back_data + the jittered neighbour leaves for the tile (:876-965)
+        if (training) {
+            for (int64_t p = 0; p < n; ++p) st.h_nv[p] = nv[(size_t)p];
+            const int64_t path0 = ((int64_t)y0 * size.x + x0) * spp;   // the jitter's counter RNG (tile-unique)
+            std::lock_guard<std::mutex> lock(m_gpuMutex);
+            check_hip(hipMemcpyAsync(st.d_rec, st.h_rec, sizeof(float) * 16 * V * n, hipMemcpyHostToDevice, m_stream),
+                      "upload vertices");
+            check_hip(hipMemcpyAsync(st.d_nv, st.h_nv, sizeof(int32_t) * n, hipMemcpyHostToDevice, m_stream),
+                      "upload vertex counts");
+            sdmm_path_vertices v{n, V, path0, st.d_rec, st.d_nv};
+            check_sdmm(sdmm_guiding_push(m_guiding, &v, 0x5D33u + (uint64_t)iteration), "sdmm_guiding_push");
+        }
+    }
+
+    // recordRadiance (:628-637): every saved vertex of the path gets the
+    // radiance divided by its throughput and sampling pdf
+    static void recordRadiance(Staging& st, int64_t p, int64_t n, int k, const Spectrum& rad) {
+        Float r[3];
+        rad.toLinearRGB(r[0], r[1], r[2]);
+        for (int v = 0; v < k; ++v) {
+            const float pdf = st.rec(6, v, p, n);
+            for (int ch = 0; ch < 3; ++ch) {
+                const float thr = st.rec(3 + ch, v, p, n);
+                if (thr > 1e-4f) st.rec(ch, v, p, n) += (float)(r[ch] / (thr * pdf));
+            }
+        }
+    }
+
+    // One guided bounce of a tile's wavefront: sampleSurface / pdfSurface for
+    // nq queries (query planes of stride n) in one call on the model's stream.
+    void guideWavefront(Staging& st, int64_t n, int64_t nq) {
+        std::lock_guard<std::mutex> lock(m_gpuMutex);
+        for (int f = 0; f < 9; ++f)
+            check_hip(hipMemcpyAsync(st.d_in + f * n, st.h_in + f * n, sizeof(float) * nq, hipMemcpyHostToDevice,
+                                     m_stream), "upload queries");
+        check_hip(hipMemcpyAsync(st.d_mode, st.h_mode, nq, hipMemcpyHostToDevice, m_stream), "upload modes");
+        const float* c[3] = {st.d_in, st.d_in + n, st.d_in + 2 * n};
+        const float* u[3] = {st.d_in + 3 * n, st.d_in + 4 * n, st.d_in + 5 * n};
+        const float* dg[3] = {st.d_in + 6 * n, st.d_in + 7 * n, st.d_in + 8 * n};
+        float* d[3] = {st.d_out, st.d_out + n, st.d_out + 2 * n};
+        check_sdmm(sdmm_guide_pdf_wavefront(sdmm_guiding_tree(m_guiding), nullptr, nq, c, u, dg, st.d_mode, d,
+                                            st.d_out + 3 * n, st.d_comp, nullptr),
+                   "sdmm_guide_pdf_wavefront");
+        for (int f = 0; f < 4; ++f)
+            check_hip(hipMemcpyAsync(st.h_out + f * n, st.d_out + f * n, sizeof(float) * nq, hipMemcpyDeviceToHost,
+                                     m_stream), "download directions");
+        check_hip(hipMemcpyAsync(st.h_comp, st.d_comp, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, m_stream),
+                  "download components");
+        check_hip(hipStreamSynchronize(m_stream), "hipStreamSynchronize");
+    }
+
+    bool m_strictNormals = true;
+    int m_maxDepth = -1, m_rrDepth = 5, m_samplesPerIteration = 8, m_savedSamplesPerPath = 8;
+    bool m_sampleProduct = false, m_bsdfOnly = false, m_optimizeAsync = true;
+    int m_device = 0, m_tileSize = 64;
+    Point m_sceneMin;
+    Float m_spatialNorm = 1;
+    sdmm_guiding* m_guiding = nullptr;
+    hipStream_t m_stream = nullptr;
+    std::mutex m_gpuMutex;
+    std::atomic<bool> m_cancelled{false};
+};
+
+MTS_IMPLEMENT_CLASS_S(SDMMAmdPathTracer, false, Integrator)
+MTS_EXPORT_PLUGIN(SDMMAmdPathTracer, "SDMM volumetric path tracer (MI355X guiding)");
+MTS_NAMESPACE_END
