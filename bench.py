@@ -8,12 +8,13 @@ synthetic batch of N = 2^20 samples against a K = 128 mixture that has been
 through 5 warm EM iterations.  Inputs (SoA fp32 planes) are resident in HBM
 before timing; the N x K fp32 responsibilities are written to HBM.
 
-Multi-GPU (torchrun, one process per GPU): the N samples are sharded
-contiguously across ranks (strong scaling, no data-path collective for the
-E-step); EM steps go through the library's own RCCL communicator
-(sdmm_comm_init_rccl, sdmm_em_step_sharded: the fp64 sufficient statistics are
-all-reduced over xGMI before each M-step).  value = N / max-over-ranks step
-time.
+Multi-GPU (torchrun, one process per GPU): weak scaling -- every rank holds
+its own N = 2^20 samples of one global batch of N x world (independent parts
+of the same synthetic distribution; rank 0's is the single-GPU batch), no
+data-path collective for the E-step; EM steps go through the library's own
+RCCL communicator (sdmm_comm_init_rccl, sdmm_em_step_sharded: the fp64
+sufficient statistics of the global batch are all-reduced over xGMI before
+each M-step).  value = N x world / max-over-ranks step time.
 
 Also reported (same JSON line): the full EM step (E-step + statistics +
 all-reduce + M-step), guided queries/sec (conditional + sample + pdf, Q = 2^20,
@@ -352,14 +353,25 @@ def main():
     synth = importlib.import_module("sdmm_mitsuba_amd.synth")
     K, N = args.K, args.N
 
+    # weak scaling (the samples partition over ranks): every rank
+    # holds its own N samples of one global batch of N x world (rank 0's share
+    # is the single-GPU batch); the E-step needs no exchange, the EM step
+    # all-reduces the statistics of the global batch
     t0 = time.perf_counter()
-    batch = synth.em_batch(N, 128)
+    batch = synth.em_batch(N, 128, part=rank)
     pos, nrm = synth.model_seed_points(batch, K)
+    if world > 1:   # one model for all ranks: rank 0's seed points
+        pn = torch.from_numpy(np.concatenate([pos, nrm]).astype(np.float32))
+        pn = pn.to(dev) if not rehearse else pn
+        dist.broadcast(pn, 0)
+        pn = pn.cpu().numpy()
+        pos, nrm = pn[:len(pos)], pn[len(pos):]
     log(f"[bench] rank {rank}/{world}: synthetic batch N={N} in {time.perf_counter() - t0:.1f}s")
     full = pkg.DeviceSamples.from_numpy(batch["x"], batch["w"], batch["hpdf"], batch["is_diffuse"],
                                         device=dev)
-    shard = full.shard(rank, world) if world > 1 else full
+    shard = full
     n_local = shard.n
+    N_global = N * world
 
     stream = torch.cuda.current_stream(dev)
     mix = pkg.SDMM(K, device=dev.index, stream=stream)
@@ -423,7 +435,7 @@ def main():
         estep()
     wall, kern = timed(estep, args.steps)
     ms_per_step = wall / args.steps * 1e3
-    value = N / (wall / args.steps)
+    value = N_global / (wall / args.steps)
     bytes_per_launch = n_local * (28 + 4 * K)
     flops_per_launch = n_local * K * 66.0
     achieved = bytes_per_launch / kern
@@ -439,13 +451,13 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (BASELINE.md 2: 2^20 samples from a K=128 uniformHemisphereInit "
                 "generator, LogNormal weights with 0.1% zero / 0.01% non-finite; model after 5 EM steps)",
         "config": {"workload": "responsibility E-step, synthetic 5D sample batch (configs[1])",
-                   "K": K, "N": N, "global_batch": N, "samples_per_gpu": n_local,
+                   "K": K, "N": N_global, "global_batch": N_global, "samples_per_gpu": n_local,
                    "parallelism": f"sample-sharded x{world}", "layout": "SoA fp32 in, [N][K] fp32 out"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK, "traffic": None,
@@ -473,10 +485,12 @@ def main():
         # ---- full EM step (E-step stats + reduce + [all-reduce] + M-step) ----
         em_wall, _ = timed(em_step, max(5, args.steps // 2), events=False)
         em_steps = max(5, args.steps // 2)
-        out["em_step"] = {"samples_per_s": N / (em_wall / em_steps), "ms_per_step": em_wall / em_steps * 1e3}
+        out["em_step"] = {"samples_per_s": N_global / (em_wall / em_steps),
+                          "ms_per_step": em_wall / em_steps * 1e3}
         # ---- fused stats kernel alone (per rank) ----
         st_wall, st_kern = timed(lambda: mix.estep_stats(shard, stats), args.steps)
-        out["estep_stats"] = {"ms_per_step": st_wall / args.steps * 1e3, "samples_per_s": N / (st_wall / args.steps)}
+        out["estep_stats"] = {"ms_per_step": st_wall / args.steps * 1e3,
+                              "samples_per_s": N_global / (st_wall / args.steps)}
         # ---- guided queries (replicas: each rank serves Q/world queries) ----
         q_local = args.Q // world
         c, u = synth.sample_queries_near(batch, q_local, seed=synth.SEED_QUERIES + rank)
@@ -526,7 +540,7 @@ def main():
         out["cornell_async"] = cornell_bench(pkg, dev, args, world, optimize_async=1)
 
     if not args.no_extra and not args.no_large_k:
-        out["large_k"] = large_k_bench(pkg, synth, batch, shard, dev, stream, timed, args, world, N, comm)
+        out["large_k"] = large_k_bench(pkg, synth, batch, shard, dev, stream, timed, args, world, N_global, comm)
 
     if rank == 0 and world == 1 and not args.no_cpu:
         try:

@@ -88,12 +88,14 @@ def sample_mixture(g: dict, n: int, rng) -> tuple[np.ndarray, np.ndarray]:
     return out.astype(np.float32), normals.astype(np.float32)
 
 
-def em_batch(n: int, K_gen: int = 128, heuristic: bool = False, guards: bool = True):
-    """Synthetic EM batch: dict with x (6,n), w, hpdf, is_diffuse, normals."""
+def em_batch(n: int, K_gen: int = 128, heuristic: bool = False, guards: bool = True, part: int = 0):
+    """Synthetic EM batch: dict with x (6,n), w, hpdf, is_diffuse, normals.
+    part p > 0: an independent batch of the same distribution (rank p's share
+    of a weak-scaled global batch; part 0 is the single-GPU batch)."""
     g = generator_mixture(K_gen)
-    rng = np.random.default_rng(SEED_SAMPLES)
+    rng = np.random.default_rng(SEED_SAMPLES + 7919 * part)
     x, normals = sample_mixture(g, n, rng)
-    wr = np.random.default_rng(SEED_WEIGHTS)
+    wr = np.random.default_rng(SEED_WEIGHTS + 7919 * part)
     w = wr.lognormal(0.0, 1.0, size=n).astype(np.float32)
     if guards and n >= 16:
         zi = wr.choice(n, size=max(1, n // 1000), replace=False)
