@@ -229,9 +229,10 @@ def wavefront_bench(pkg, synth, batch, shard, tree, dev, stream, ct, ut, gout, t
             "guided_frac": float((comp >= 0).mean()), "scaling": "weak (replicas: queries per rank)"}
 
 
-def cornell_bench(pkg, dev, args, world, optimize_async=0):
+def cornell_bench(pkg, dev, args, world, optimize_async=0, K=16):
     """configs[0] on the device: the test suite's Cornell Box (640x360), K=16
-    per leaf, 64 spp rendered 8 spp per iteration, training (push + optimize)
+    per leaf (K=128: the Torus line's K, configs[2], over the one scene whose
+    geometry the snapshot holds), 64 spp rendered 8 spp per iteration, training (push + optimize)
     while samplesRendered < sampleCount / 4 (volpath_sdmm.cpp:411-507), the
     native guiding model (sdmm_guiding_iteration) with the device Li.  Replicas
     only (each rank renders the whole image; no exchange).  "guided rays/s" =
@@ -245,7 +246,7 @@ def cornell_bench(pkg, dev, args, world, optimize_async=0):
     acc = torch.zeros_like(img)
     its = []
     for rep in range(2):                          # the first run pages in code and scratch (untimed)
-        g = pkg.Guiding(tmin, tmax, device=dev.index, optimize_async=optimize_async)
+        g = pkg.Guiding(tmin, tmax, device=dev.index, optimize_async=optimize_async, K=K)
         acc.zero_()
         its = []
         torch.cuda.synchronize()
@@ -257,13 +258,14 @@ def cornell_bench(pkg, dev, args, world, optimize_async=0):
             acc += img
             torch.cuda.synchronize()
             its.append({"ms": (time.perf_counter() - t) * 1e3, "train": train, "segments": ls["segments"],
+                        "guided_queries": ls["guided_queries"], "fallback_queries": ls["fallback_queries"],
                         "paths": ls["paths"], "leaves": gs["leaves"] if train else None,
                         "optimized": gs["optimized"] if train else None, "trained": g.trained})
         total = time.perf_counter() - t_all
     guided = [x for x in its if not x["train"]]
     seg = sum(x["segments"] for x in guided)
     gms = sum(x["ms"] for x in guided)
-    return {"workload": "Cornell Box 640x360, K=16 per leaf, 64 spp (8 per iteration, training for the first 16)",
+    return {"workload": f"Cornell Box 640x360, K={K} per leaf, 64 spp (8 per iteration, training for the first 16)",
             "total_ms": total * 1e3, "guided_rays_per_s": seg / (gms * 1e-3),
             "guided_paths_per_s": sum(x["paths"] for x in guided) / (gms * 1e-3),
             "trained_leaves": its[-1]["trained"], "iterations": its,

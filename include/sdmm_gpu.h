@@ -545,6 +545,7 @@ typedef struct {
     int64_t paths;           /* paths started (pixels x spp) */
     int64_t segments;        /* bounce rays traced after the camera rays (= saved vertices) */
     int64_t guided_queries;  /* live bounces that queried the guide (compacted wavefront sizes summed) */
+    int64_t fallback_queries;   /* of those, served by the full-K path (the candidate list overflowed) */
 } sdmm_li_stats;
 int sdmm_scene_create(const sdmm_scene_desc* desc, int device, sdmm_scene** out);
 void sdmm_scene_destroy(sdmm_scene* s);

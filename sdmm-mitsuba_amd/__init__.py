@@ -1066,7 +1066,8 @@ class Guiding:
                                             C.c_void_p(image.data_ptr()),
                                             None if image_sqr is None else C.c_void_p(image_sqr.data_ptr()),
                                             C.byref(ls), C.byref(gs)))
-        return image, {"paths": ls.paths, "segments": ls.segments, "guided_queries": ls.guided_queries}, \
+        return image, {"paths": ls.paths, "segments": ls.segments, "guided_queries": ls.guided_queries,
+                       "fallback_queries": ls.fallback_queries}, \
             {"leaves": gs.leaves, "optimized": gs.optimized, "records": gs.records}
 
 
@@ -1105,7 +1106,8 @@ class _PathVertices(C.Structure):
 
 
 class _LiStats(C.Structure):
-    _fields_ = [("paths", C.c_int64), ("segments", C.c_int64), ("guided_queries", C.c_int64)]
+    _fields_ = [("paths", C.c_int64), ("segments", C.c_int64), ("guided_queries", C.c_int64),
+                ("fallback_queries", C.c_int64)]
 
 
 def _hip():
@@ -1193,4 +1195,5 @@ class Scene:
                                     None if image_sqr is None else C.c_void_p(image_sqr.data_ptr()), C.byref(v),
                                     C.byref(st)))
         return image, PathVertices(v, self, self.device), {"paths": st.paths, "segments": st.segments,
-                                                           "guided_queries": st.guided_queries}
+                                                           "guided_queries": st.guided_queries,
+                                                           "fallback_queries": st.fallback_queries}

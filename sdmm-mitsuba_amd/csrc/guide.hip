@@ -292,18 +292,22 @@ struct CandSlots {
 // the same loop, keeps every LIVE component (weight > 0) in the LDS list
 // sorted (weight desc, index asc) by stable insertion, at most `cap` of them.
 // When the list is full a newcomer either displaces the last entry or is
-// dropped; `dropped` is the largest weight ever dropped.  Once totalMass (hence
-// tau) is known, the candidates are the list prefix with w >= tau -- the same
-// sequence the two-pass form built, provided no dropped weight reaches tau
-// (else: fallback).  tau > 0 whenever totalMass > 0, so a weight of exactly 0
-// (all components with q > kMarginalZeroQ, most of K) can never be a candidate
-// and never enters the list.  Validity of the conditionals is only evaluated
-// for the candidates.
+// dropped.  A dropped weight never exceeds the final last entry (the last
+// entry of a full list only grows), and a skipped weight (below the running
+// bound, hence below the final tau) is below every candidate, so the list
+// prefix with w >= tau is exactly the first ncand entries of the reference's
+// selection order.  The cutoff walk runs over it; when it reaches the cutoff
+// inside the list the kept prefix is that of the full-K scan, whatever was
+// dropped.  Only a walk that exhausts the candidates without reaching the
+// cutoff (a full list, or invalid conditionals zeroing kept weights) needs
+// the full-K fallback -- unless the candidates are all K components.  tau > 0
+// whenever totalMass > 0, so a weight of exactly 0 (all components with q >
+// kMarginalZeroQ, most of K) can never be a candidate and never enters the
+// list.  Validity of the conditionals is only evaluated for the candidates.
 __device__ __forceinline__ int build_candidates(const float* gp, int Kp, int K, const float c[3], float* cw,
                                                 unsigned short* ck, int T, int tid, float norm3, int cap,
                                                 float& accum) {
     float total = 0.0f;
-    float dropped = 0.0f;
     int cnt = 0;
     // 0.0089 / K (< the 0.009 / K of the bound below; the float product's
     // rounding, 2^-24 relative, stays far inside the margin): one multiply per
@@ -314,16 +318,12 @@ __device__ __forceinline__ int build_candidates(const float* gp, int Kp, int K, 
         total += w;
         // the float sum of non-negative terms never decreases, so the final
         // tau >= (0.01 total - ulp) 0.999 / K > 0.009 total_so_far / K: a weight
-        // below that is neither a candidate nor a dropped weight that matters
+        // below that is never a candidate
         if (!(w > 0.0f) || w < total * skip_f) continue;
         if (cnt == cap) {
             // full: w joins only if it sorts before the last entry (ties keep
             // the lower index, which arrived first)
-            if (cap == 0 || !(w > cw[(cap - 1) * T + tid])) {
-                dropped = fmaxf(dropped, w);
-                continue;
-            }
-            dropped = fmaxf(dropped, cw[(cap - 1) * T + tid]);
+            if (cap == 0 || !(w > cw[(cap - 1) * T + tid])) continue;
             --cnt;
         }
         int pos = cnt;
@@ -339,7 +339,7 @@ __device__ __forceinline__ int build_candidates(const float* gp, int Kp, int K, 
     if (!__builtin_isfinite(total)) return -1;
     const float cutoff = (float)(0.99 * (double)total);
     const double tau = ((double)total - (double)cutoff) / (double)K * 0.999;
-    if (!(tau > 0.0) || (double)dropped >= tau) return -1;
+    if (!(tau > 0.0)) return -1;
     int ncand = 0;
     while (ncand < cnt && (double)cw[ncand * T + tid] >= tau) ++ncand;
     accum = 0.0f;
@@ -526,24 +526,8 @@ __device__ __forceinline__ float seq_sum(float acc, float x, int n) {
     for (int l = 0; l < n; ++l) acc += rl(x, l);
     return acc;
 }
-__device__ __forceinline__ float wave_max_f(float x) {   // no NaN
-    x = fmaxf(x, dpp<0xB1>(x));
-    x = fmaxf(x, dpp<0x4E>(x));
-    x = fmaxf(x, dpp<0x141>(x));
-    x = fmaxf(x, dpp<0x140>(x));
-    return fmaxf(fmaxf(rl(x, 0), rl(x, 16)), fmaxf(rl(x, 32), rl(x, 48)));
-}
 template <int CTRL>
 __device__ __forceinline__ int dppi(int x) { return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false); }
-__device__ __forceinline__ int wave_min_i(int x) {
-    x = min(x, dppi<0xB1>(x));
-    x = min(x, dppi<0x4E>(x));
-    x = min(x, dppi<0x141>(x));
-    x = min(x, dppi<0x140>(x));
-    return min(min(__builtin_amdgcn_readlane(x, 0), __builtin_amdgcn_readlane(x, 16)),
-               min(__builtin_amdgcn_readlane(x, 32), __builtin_amdgcn_readlane(x, 48)));
-}
-
 constexpr int kWaveKMax = 512;            // components per wave query: 8 per lane
 constexpr int kWaveSlots = kWaveKMax / 64;
 
@@ -572,57 +556,158 @@ __device__ __forceinline__ WaveLds wave_lds(float* lds, int K, float* pscratch =
 }
 static size_t wave_lds_bytes(int K, int M = 0) { return sizeof(float) * (5 * (size_t)K + 20 * (size_t)M) + 16; }
 
+// lane ^ J of a wave-uniform compile-time J (DPP inside rows, ds_bpermute across)
+template <int J>
+__device__ __forceinline__ uint32_t xor_lane_u(uint32_t x) {
+    const int xi = (int)x;
+    if constexpr (J == 1) return (uint32_t)dppi<0xB1>(xi);         // quad_perm [1,0,3,2]
+    else if constexpr (J == 2) return (uint32_t)dppi<0x4E>(xi);    // quad_perm [2,3,0,1]
+    else if constexpr (J == 4) {                                   // row_shl:4 / row_shr:4 by bank
+        int t = __builtin_amdgcn_update_dpp(xi, xi, 0x104, 0xF, 0x5, false);
+        return (uint32_t)__builtin_amdgcn_update_dpp(t, xi, 0x114, 0xF, 0xA, false);
+    } else if constexpr (J == 8) return (uint32_t)dppi<0x128>(xi); // row_ror:8
+    else return (uint32_t)__shfl_xor(xi, J);
+}
+
+// One compare-exchange step of a bitonic network over the wave's 64 S
+// elements e = 64 i + lane, ordered by `before` = (key desc, index asc) -- the
+// order in which the reference's selection scan takes the weights (largest
+// first, the lowest index among equals).  Stage (KS, J): element e pairs with
+// e ^ J and, inside the KS-block of e, the block runs "up" (before-first)
+// when (e & KS) == 0.
+__device__ __forceinline__ bool sel_before(uint32_t ka, uint32_t ia, uint32_t kb, uint32_t ib) {
+    return ka > kb || (ka == kb && ia < ib);
+}
+template <int S, int KS, int J>
+__device__ __forceinline__ void bitonic_step(uint32_t (&key)[S], uint32_t (&idx)[S], int lane) {
+    if constexpr (J >= 64) {
+        constexpr int JJ = J / 64;
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+            if (i & JJ) continue;
+            const int i2 = i | JJ;
+            const bool up = ((64 * i) & KS) == 0;   // lanes do not reach bit KS >= 128
+            const bool b = sel_before(key[i], idx[i], key[i2], idx[i2]);
+            const bool sw = up ? !b : b;
+            const uint32_t k0 = key[i], x0 = idx[i];
+            key[i] = sw ? key[i2] : k0; idx[i] = sw ? idx[i2] : x0;
+            key[i2] = sw ? k0 : key[i2]; idx[i2] = sw ? x0 : idx[i2];
+        }
+    } else {
+        const bool lower = (lane & J) == 0;
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+            const uint32_t ok = xor_lane_u<J>(key[i]), oi = xor_lane_u<J>(idx[i]);
+            const bool up = ((64 * i + lane) & KS) == 0;
+            const bool b = sel_before(key[i], idx[i], ok, oi);
+            const bool keep = (lower == up) ? b : !b;
+            key[i] = keep ? key[i] : ok;
+            idx[i] = keep ? idx[i] : oi;
+        }
+    }
+}
+template <int S, int KS, int J>
+__device__ __forceinline__ void bitonic_stage(uint32_t (&key)[S], uint32_t (&idx)[S], int lane) {
+    bitonic_step<S, KS, J>(key, idx, lane);
+    if constexpr (J > 1) bitonic_stage<S, KS, J / 2>(key, idx, lane);
+}
+template <int S, int KS = 2>
+__device__ __forceinline__ void bitonic_sort(uint32_t (&key)[S], uint32_t (&idx)[S], int lane) {
+    bitonic_stage<S, KS, KS / 2>(key, idx, lane);
+    if constexpr (KS < 64 * S) bitonic_sort<S, 2 * KS>(key, idx, lane);
+}
+
 // The kept prefix of query c's full-K conditional (above): slots
 // i < lastIdx in L.sl / L.fw (raw weight); returns lastIdx and accum.
-__device__ __forceinline__ int build_full_wave(const float* gp, int Kp, int K, const float c[3], const WaveLds& L,
-                                               int lane, float norm3, float& accum) {
-    float wr[kWaveSlots];
+//
+// S = 64-lane slots per component index (K <= 64 S).  Without a NaN weight the
+// selection order is a strict total order -- (weight desc, index asc) -- so the
+// wave sorts all K weights once (a bitonic network in registers: 21..45
+// compare-exchange steps for K = 64..512) and walks the sorted sequence,
+// instead of one wave max + min reduction per kept component (O(K x kept));
+// accum and the cutoff test run in that same order, so lastIdx, the slots and
+// accum are those of the reference's scan bit for bit.  Keys: the weight's bits
+// + 1 (non-negative floats order as unsigned integers; +0.0 -> 1), 0 for an
+// absent entry (sign bit set: never taken).  With a NaN present the scan's
+// choice depends on the order of comparisons, so the scan itself runs.
+template <int S>
+__device__ __forceinline__ int build_full_wave_s(const float* gp, int Kp, int K, const float c[3], const WaveLds& L,
+                                                 int lane, float norm3, float& accum) {
+    float wr[S];
     unsigned vmask = 0;   // bit i: the conditional of component lane + 64 i is valid
+    bool nan_seen = false;
 #pragma unroll
-    for (int i = 0; i < kWaveSlots; ++i) {
+    for (int i = 0; i < S; ++i) {
         const int k = lane + 64 * i;
         wr[i] = -0.0f;    // absent: never a candidate
         if (k < K) {
             wr[i] = gp_ld(gp, Kp, GP_W, k) * marginal_pdf(gp, Kp, k, c, norm3);
             vmask |= (cond_valid(gp, Kp, k, c) ? 1u : 0u) << i;
         }
+        nan_seen |= (wr[i] != wr[i]);
     }
     float total = 0.0f;   // component order
 #pragma unroll
-    for (int i = 0; i < kWaveSlots; ++i)
+    for (int i = 0; i < S; ++i)
         if (64 * i < K) total = seq_sum(total, wr[i], min(64, K - 64 * i));
     const float cutoff = (float)(0.99 * (double)total);
     accum = 0.0f;
     int lastIdx = K;   // the reference leaves it uninitialised if never reached
-    for (int it = 0; it < K; ++it) {
-        float bv = -1.0f;
-        int bi = -1;
-        bool nan_seen = false;
+    if (!__any(nan_seen)) {
+        uint32_t key[S], idx[S];
 #pragma unroll
-        for (int i = 0; i < kWaveSlots; ++i) {
-            const float x = wr[i];
-            if (__builtin_signbit(x)) continue;
-            nan_seen |= (x != x);
-            if (bi < 0 || x > bv) { bv = x; bi = i; }
+        for (int i = 0; i < S; ++i) {
+            key[i] = __builtin_signbit(wr[i]) ? 0u : __builtin_bit_cast(uint32_t, wr[i]) + 1u;
+            idx[i] = (uint32_t)(lane + 64 * i);
         }
+        bitonic_sort<S>(key, idx, lane);
+        // sorted element p = 64 i + lane: its slot record, written by its own
+        // lane, and its term of the kept mass (0 for an invalid conditional)
+        int n_live = 0;   // entries with a weight (sorted first)
+        float term[S];
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+            n_live += __builtin_popcountll(__builtin_amdgcn_ballot_w64(key[i] != 0u));
+            const unsigned vm = (unsigned)__shfl((int)vmask, (int)(idx[i] & 63u));
+            const bool ok = (vm >> (idx[i] >> 6)) & 1u;
+            const float w = __builtin_bit_cast(float, key[i] - 1u);
+            term[i] = ok ? w : 0.0f;
+            if (key[i] != 0u) {
+                L.sl[64 * i + lane] = (int)idx[i] | (ok ? (int)0x80000000 : 0);
+                L.fw[64 * i + lane] = w;
+            }
+        }
+        // accum in the selection order, up to the first slot that reaches the
+        // cutoff; all live entries taken without reaching it: lastIdx = n_live
+        // (the scan finds nothing left), which is K when every weight is live
+        lastIdx = n_live;
+        bool done = false;
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+            if (done) break;
+            const int n = min(64, n_live - 64 * i);
+            for (int l = 0; l < n; ++l) {
+                accum += rl(term[i], l);
+                if (accum >= cutoff) { lastIdx = 64 * i + l + 1; done = true; break; }
+            }
+        }
+        __syncthreads();
+        return lastIdx;
+    }
+    for (int it = 0; it < K; ++it) {
+        // the reference scan itself, in component order (a NaN is present)
         int best = -1;
         float bw = 0.0f;
-        if (__any(nan_seen)) {
-            // the reference scan itself, in component order
 #pragma unroll
-            for (int i = 0; i < kWaveSlots; ++i)
-                for (int l = 0; l < 64 && 64 * i + l < K; ++l) {
-                    const float x = rl(wr[i], l);
-                    if (__builtin_signbit(x)) continue;
-                    if (best < 0 || x > bw) { best = 64 * i + l; bw = x; }
-                }
-        } else {
-            bw = wave_max_f(bi >= 0 ? bv : -1.0f);
-            if (bw >= 0.0f) best = wave_min_i((bi >= 0 && bv == bw) ? lane + 64 * bi : 0x7fffffff);
-        }
+        for (int i = 0; i < S; ++i)
+            for (int l = 0; l < 64 && 64 * i + l < K; ++l) {
+                const float x = rl(wr[i], l);
+                if (__builtin_signbit(x)) continue;
+                if (best < 0 || x > bw) { best = 64 * i + l; bw = x; }
+            }
         if (best < 0) { lastIdx = it; break; }
 #pragma unroll
-        for (int i = 0; i < kWaveSlots; ++i)
+        for (int i = 0; i < S; ++i)
             if (best == lane + 64 * i) wr[i] = -bw;
         const bool ok = ((unsigned)__builtin_amdgcn_readlane((int)vmask, best & 63) >> (best >> 6)) & 1u;
         if (lane == 0) {
@@ -634,6 +719,14 @@ __device__ __forceinline__ int build_full_wave(const float* gp, int Kp, int K, c
     }
     __syncthreads();
     return lastIdx;
+}
+
+__device__ __forceinline__ int build_full_wave(const float* gp, int Kp, int K, const float c[3], const WaveLds& L,
+                                               int lane, float norm3, float& accum) {
+    if (K <= 64) return build_full_wave_s<1>(gp, Kp, K, c, L, lane, norm3, accum);
+    if (K <= 128) return build_full_wave_s<2>(gp, Kp, K, c, L, lane, norm3, accum);
+    if (K <= 256) return build_full_wave_s<4>(gp, Kp, K, c, L, lane, norm3, accum);
+    return build_full_wave_s<kWaveSlots>(gp, Kp, K, c, L, lane, norm3, accum);
 }
 
 __device__ __forceinline__ int slot_comp(const WaveLds& L, int i) { return L.sl[i] & 0x7fffffff; }
@@ -1658,7 +1751,7 @@ hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float*
         perm = sort->idx[1];
     }
     const dim3 grid((unsigned)((nq + T - 1) / T));
-    const int fb_blocks = cus * 8;
+    const int fb_blocks = cus * 16;
     const GuideIO io = make_io(c, u, dgiven, d, pdf, comp);
     cap = cap < K ? cap : K;
     e = dgiven ? launch_cand<true>(cap, grid, st, gp, Kp, K, nq, io, gc, fb_count, fb_list, perm)
@@ -1703,7 +1796,7 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
     const STNodeDev* nd = (const STNodeDev*)nodes;
     const GuideMix* tb = (const GuideMix*)tab;
     const dim3 grid((unsigned)((nq + T - 1) / T));
-    const int fb_blocks = cus * 8;
+    const int fb_blocks = cus * 16;
     const GuideIO io = make_io(c, u, dgiven, d, pdf, comp, pmode);
     if (pmode) dgiven = nullptr;   // mixed: the sampling kernels, pdf queries per pmode
     cap = cap < kmax ? cap : kmax;

@@ -32,6 +32,7 @@ hipError_t launch_li_film(const PathsDev& P, int64_t pix0, int64_t npix, int spp
 namespace sdmm_detail {
 int set_error(int code, const char* msg);
 int tree_stream(sdmm_stree* t, hipStream_t* st);   // sdmm_api.cpp: device nodes uploaded, the tree's stream
+const int* tree_fallback_count(const sdmm_stree* t);   // sdmm_api.cpp
 }  // namespace sdmm_detail
 
 using namespace sdmm;
@@ -53,6 +54,8 @@ struct sdmm_scene {
     int64_t* dsum = nullptr;
     int32_t* dcount = nullptr;   // live guided queries of the current bounce
     int32_t* hcount = nullptr;   // (pinned host copy)
+    int32_t* hfb = nullptr;      // per bounce: fallback queries of its wavefront (pinned)
+    int hfb_cap = 0;
     void* temp = nullptr;
     size_t temp_bytes = 0;
 };
@@ -216,6 +219,7 @@ void sdmm_scene_destroy(sdmm_scene* s) {
     if (s->drad) (void)hipFree(s->drad);
     if (s->buf) (void)hipFree(s->buf);
     if (s->hcount) (void)hipHostFree(s->hcount);
+    if (s->hfb) (void)hipHostFree(s->hfb);
     delete s;
 }
 
@@ -261,6 +265,15 @@ int sdmm_li_render(sdmm_scene* s, sdmm_stree* t, const sdmm_mix* const* node_mix
     const int bounces = p->max_depth > 0 ? p->max_depth - 1 : V;
     int64_t guided_queries = 0;
     if (!s->hcount) HIP_TRY(hipHostMalloc((void**)&s->hcount, sizeof(int32_t), hipHostMallocDefault));
+    if (stats && p->guided && s->hfb_cap < bounces) {
+        if (s->hfb) HIP_TRY(hipHostFree(s->hfb));
+        s->hfb = nullptr;
+        s->hfb_cap = 0;
+        HIP_TRY(hipHostMalloc((void**)&s->hfb, sizeof(int32_t) * (size_t)bounces, hipHostMallocDefault));
+        s->hfb_cap = bounces;
+    }
+    if (stats && p->guided)
+        for (int b = 0; b < bounces; ++b) s->hfb[b] = 0;
     const float h = p->bsdf_fraction;
     for (int b = 0; b < bounces; ++b) {
         HIP_TRY(launch_li_query(s->S, s->P, s->Q, path0, b, p->max_depth > 0 ? p->max_depth : INT32_MAX, p->guided,
@@ -280,6 +293,10 @@ int sdmm_li_render(sdmm_scene* s, sdmm_stree* t, const sdmm_mix* const* node_mix
                 r = sdmm_guide_pdf_wavefront(t, node_mix, nlive, c, u, bd, s->Q.k_mode, d, s->Q.pdf, s->Q.comp,
                                              nullptr);
                 if (r) return r;
+                // (stream-ordered copy, read after the final synchronisation)
+                const int* fb = sdmm_detail::tree_fallback_count(t);
+                if (stats && fb)
+                    HIP_TRY(hipMemcpyAsync(s->hfb + b, fb, sizeof(int32_t), hipMemcpyDeviceToHost, st));
             }
             guided_queries += nlive;
         }
@@ -303,6 +320,9 @@ int sdmm_li_render(sdmm_scene* s, sdmm_stree* t, const sdmm_mix* const* node_mix
         stats->paths = P;
         stats->segments = seg;
         stats->guided_queries = guided_queries;
+        stats->fallback_queries = 0;
+        if (p->guided)
+            for (int b = 0; b < bounces; ++b) stats->fallback_queries += s->hfb[b];
     }
     return SDMM_OK;
 }

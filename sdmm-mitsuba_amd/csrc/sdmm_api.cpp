@@ -2442,6 +2442,8 @@ int tree_stream(sdmm_stree* t, hipStream_t* st) {
     *st = t->stream;
     return SDMM_OK;
 }
+// the device count of full-K (fallback) queries of the tree's last guided call
+const int* tree_fallback_count(const sdmm_stree* t) { return t->guide_fb; }
 }  // namespace sdmm_detail
 
 extern "C" {

@@ -324,12 +324,13 @@ def _em_model(pkg, oracle, synth, K, N, iters):
     return b, mix, m
 
 
-@pytest.mark.parametrize("K,iters,cap", [(16, 3, 40), (128, 4, 40), (128, 4, 4), (128, 4, 0),
-                                         (256, 2, 40), (512, 2, 40), (512, 2, 0)])
+@pytest.mark.parametrize("K,iters,cap", [(16, 3, 40), (16, 3, 0), (72, 3, 0), (128, 4, 40), (128, 4, 4),
+                                         (128, 4, 0), (256, 2, 40), (256, 2, 0), (512, 2, 40), (512, 2, 0)])
 def test_guide_indices_bit_exact(pkg, oracle, synth, gpu, plog, K, iters, cap):
     """Guided bounces vs the oracle.  cap: per-query candidate-list capacity;
     4 sends most K=128 queries and 0 sends all of them down the full-K
-    fallback path, which must give the same bits.  K=512 (the Kitchen
+    fallback path (one wave per query: a bitonic sort of the K weights, 1, 2,
+    4 or 8 per lane by K), which must give the same bits.  K=512 (the Kitchen
     config) runs the fallback with 32-wide workgroups (its K x 64 lists
     would not fit the 160 KB LDS)."""
     import torch

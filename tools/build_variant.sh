@@ -18,5 +18,5 @@ for o in "$PKG"/build/*.o; do
     OBJS+=("$o")
   fi
 done
-/opt/rocm/bin/hipcc $HIPFLAGS -shared -o "$PKG/build_ab/$NAME.so" "${OBJS[@]}"
+/opt/rocm/bin/hipcc $HIPFLAGS -shared -o "$PKG/build_ab/$NAME.so" "${OBJS[@]}" -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo "$PKG/build_ab/$NAME.so"

@@ -12,9 +12,15 @@ spec.loader.exec_module(bench)
 
 if __name__ == "__main__":
     import torch
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--K", type=int, nargs="+", default=[16])
+    ap.add_argument("--modes", type=int, nargs="+", default=[0, 1])
+    a = ap.parse_args()
     pkg = bench.load_pkg()
-    for mode in (0, 1):
-        out = bench.cornell_bench(pkg, torch.device("cuda", 0), None, 1, optimize_async=mode)
-        print(json.dumps({k: v for k, v in out.items() if k != "iterations"}))
+    for K in a.K:
+      for mode in a.modes:
+        out = bench.cornell_bench(pkg, torch.device("cuda", 0), None, 1, optimize_async=mode, K=K)
+        print(json.dumps({k: v for k, v in out.items() if k != "iterations"}), flush=True)
         for it in out["iterations"]:
-            print(json.dumps(it))
+            print(json.dumps(it), flush=True)
