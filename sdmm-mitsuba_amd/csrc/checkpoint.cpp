@@ -23,6 +23,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <string_view>
 #include <vector>
 
 #include "../../include/sdmm_gpu.h"
@@ -164,17 +165,24 @@ int write_file(const char* path, const std::string& s) {
     return SDMM_OK;
 }
 
-// ---- reader: a small JSON DOM (numbers kept as text until their type is known)
+// ---- reader: a small JSON DOM over the file text.  Scalars are views into
+// the text (converted when their type is known); an array of numbers (or of
+// the non-finite strings) is kept as one vector of views, 16 B per element --
+// the per-leaf parameter arrays are almost all of a checkpoint.
 struct Value {
     enum Kind { Null, Bool, Num, Str, Arr, Obj } kind = Null;
-    std::string text;                       // Num / Str
+    std::string_view text;                  // Num / Str
     bool b = false;
-    std::vector<Value> arr;
-    std::map<std::string, Value> obj;
+    std::vector<Value> arr;                 // Arr of objects / arrays
+    std::vector<std::string_view> nums;     // Arr of numbers / strings (views; strings unquoted)
+    std::vector<bool> num_is_str;
+    std::map<std::string, Value, std::less<>> obj;
     const Value* get(const char* k) const {
-        auto it = obj.find(k);
-        return kind == Obj && it != obj.end() ? &it->second : nullptr;
+        if (kind != Obj) return nullptr;
+        auto it = obj.find(std::string_view(k));
+        return it != obj.end() ? &it->second : nullptr;
     }
+    size_t size() const { return arr.empty() ? nums.size() : arr.size(); }
 };
 
 struct Parser {
@@ -191,22 +199,49 @@ struct Parser {
         p += n;
         return true;
     }
-    bool str(std::string& out) {
+    // the writer never escapes: a string is the text between its quotes (an
+    // escape is rejected rather than mis-read)
+    bool str(std::string_view& out) {
         if (p >= end || *p != '"') return fail("expected string");
-        ++p;
+        const char* s = ++p;
         while (p < end && *p != '"') {
-            if (*p == '\\') {   // the writer never escapes; accept the simple escapes anyway
-                if (++p >= end) return fail("bad escape");
-                const char c = *p;
-                out += c == 'n' ? '\n' : c == 't' ? '\t' : c;
-            } else {
-                out += *p;
-            }
+            if (*p == '\\') return fail("escaped strings are not used by this format");
             ++p;
         }
         if (p >= end) return fail("unterminated string");
+        out = std::string_view(s, (size_t)(p - s));
         ++p;
         return true;
+    }
+    bool number(std::string_view& out) {
+        const char* s = p;
+        while (p < end && (std::strchr("+-.eE", *p) || (*p >= '0' && *p <= '9'))) ++p;
+        if (p == s) return fail("unexpected character");
+        out = std::string_view(s, (size_t)(p - s));
+        return true;
+    }
+    bool array(Value& v) {
+        v.kind = Value::Arr;
+        ++p; ws();
+        if (p < end && *p == ']') { ++p; return true; }
+        const bool scalars = p < end && *p != '{' && *p != '[';
+        for (;;) {
+            ws();
+            if (scalars) {
+                std::string_view t;
+                const bool is_str = p < end && *p == '"';
+                if (!(is_str ? str(t) : number(t))) return false;
+                v.nums.push_back(t);
+                v.num_is_str.push_back(is_str);
+            } else {
+                v.arr.emplace_back();
+                if (!value(v.arr.back())) return false;
+            }
+            ws();
+            if (p < end && *p == ',') { ++p; continue; }
+            if (p < end && *p == ']') { ++p; return true; }
+            return fail("expected ',' or ']'");
+        }
     }
     bool value(Value& v) {
         if (++depth > 64) return fail("nesting too deep");
@@ -219,29 +254,19 @@ struct Parser {
             if (p < end && *p == '}') { ++p; --depth; return true; }
             while (ok) {
                 ws();
-                std::string k;
+                std::string_view k;
                 if (!str(k)) return false;
                 ws();
                 if (p >= end || *p != ':') return fail("expected ':'");
                 ++p;
-                if (!value(v.obj[k])) return false;
+                if (!value(v.obj[std::string(k)])) return false;
                 ws();
                 if (p < end && *p == ',') { ++p; continue; }
                 if (p < end && *p == '}') { ++p; break; }
                 return fail("expected ',' or '}'");
             }
         } else if (*p == '[') {
-            v.kind = Value::Arr;
-            ++p; ws();
-            if (p < end && *p == ']') { ++p; --depth; return true; }
-            while (ok) {
-                v.arr.emplace_back();
-                if (!value(v.arr.back())) return false;
-                ws();
-                if (p < end && *p == ',') { ++p; continue; }
-                if (p < end && *p == ']') { ++p; break; }
-                return fail("expected ',' or ']'");
-            }
+            ok = array(v);
         } else if (*p == '"') {
             v.kind = Value::Str;
             ok = str(v.text);
@@ -249,76 +274,90 @@ struct Parser {
         else if (*p == 'f') { v.kind = Value::Bool; ok = lit("false"); }
         else if (*p == 'n') { ok = lit("null"); }
         else {
-            const char* s = p;
-            while (p < end && (std::strchr("+-.eE", *p) || (*p >= '0' && *p <= '9'))) ++p;
-            if (p == s) return fail("unexpected character");
             v.kind = Value::Num;
-            v.text.assign(s, p);
+            ok = number(v.text);
         }
         --depth;
         return ok;
     }
 };
 
-bool num_f64(const Value& v, double& out) {
-    if (v.kind == Value::Str) {
-        if (v.text == "NaN") { out = std::nan(""); return true; }
-        if (v.text == "Infinity") { out = HUGE_VAL; return true; }
-        if (v.text == "-Infinity") { out = -HUGE_VAL; return true; }
+// text -> number through a NUL-terminated copy (numbers are short)
+bool text_f64(std::string_view t, bool is_str, double& out) {
+    if (is_str) {
+        if (t == "NaN") { out = std::nan(""); return true; }
+        if (t == "Infinity") { out = HUGE_VAL; return true; }
+        if (t == "-Infinity") { out = -HUGE_VAL; return true; }
         return false;
     }
-    if (v.kind != Value::Num) return false;
+    char b[64];
+    if (t.empty() || t.size() >= sizeof b) return false;
+    std::memcpy(b, t.data(), t.size());
+    b[t.size()] = 0;
     char* e = nullptr;
-    out = std::strtod(v.text.c_str(), &e);
-    return e && *e == 0;
+    out = std::strtod(b, &e);
+    return e == b + t.size();
 }
-bool num_f32(const Value& v, float& out) {
-    if (v.kind == Value::Str) {
+bool text_f32(std::string_view t, bool is_str, float& out) {
+    if (is_str) {
         double d;
-        if (!num_f64(v, d)) return false;
+        if (!text_f64(t, true, d)) return false;
         out = (float)d;
         return true;
     }
-    if (v.kind != Value::Num) return false;
+    char b[64];
+    if (t.empty() || t.size() >= sizeof b) return false;
+    std::memcpy(b, t.data(), t.size());
+    b[t.size()] = 0;
     char* e = nullptr;
-    out = std::strtof(v.text.c_str(), &e);   // nearest float of the 9-digit text: exact round trip
-    return e && *e == 0;
+    out = std::strtof(b, &e);   // nearest float of the 9-digit text: exact round trip
+    return e == b + t.size();
 }
-bool num_int(const Value& v, long long& out) {
-    if (v.kind != Value::Num) return false;
+bool text_int(std::string_view t, bool is_str, long long& out) {
+    if (is_str) return false;
+    char b[32];
+    if (t.empty() || t.size() >= sizeof b) return false;
+    std::memcpy(b, t.data(), t.size());
+    b[t.size()] = 0;
     char* e = nullptr;
     errno = 0;
-    out = std::strtoll(v.text.c_str(), &e, 10);
-    return e && *e == 0 && errno == 0;
+    out = std::strtoll(b, &e, 10);
+    return e == b + t.size() && errno == 0;
 }
+bool num_f64(const Value& v, double& out) {
+    return (v.kind == Value::Num || v.kind == Value::Str) && text_f64(v.text, v.kind == Value::Str, out);
+}
+bool num_f32(const Value& v, float& out) {
+    return (v.kind == Value::Num || v.kind == Value::Str) && text_f32(v.text, v.kind == Value::Str, out);
+}
+bool num_int(const Value& v, long long& out) { return v.kind == Value::Num && text_int(v.text, false, out); }
 
 template <class T, class F>
 bool read_array(const Value* v, std::vector<T>& out, size_t n, F conv) {
-    if (!v || v->kind != Value::Arr || v->arr.size() != n) return false;
+    if (!v || v->kind != Value::Arr || !v->arr.empty() || v->nums.size() != n) return false;
     out.resize(n);
     for (size_t i = 0; i < n; ++i)
-        if (!conv(v->arr[i], out[i])) return false;
+        if (!conv(v->nums[i], v->num_is_str[i], out[i])) return false;
     return true;
 }
 bool farr(const Value& o, const char* k, std::vector<float>& out, size_t n) {
-    return read_array(o.get(k), out, n, num_f32);
+    return read_array(o.get(k), out, n, text_f32);
 }
 bool darr(const Value& o, const char* k, std::vector<double>& out, size_t n) {
-    return read_array(o.get(k), out, n, num_f64);
+    return read_array(o.get(k), out, n, text_f64);
 }
 bool iarr(const Value& o, const char* k, std::vector<int32_t>& out, size_t n) {
-    return read_array(o.get(k), out, n, [](const Value& v, int32_t& x) {
+    return read_array(o.get(k), out, n, [](std::string_view t, bool is_str, int32_t& x) {
         long long l;
-        if (!num_int(v, l) || l < INT32_MIN || l > INT32_MAX) return false;
+        if (!text_int(t, is_str, l) || l < INT32_MIN || l > INT32_MAX) return false;
         x = (int32_t)l;
         return true;
     });
 }
 
-int read_file(const char* path, Value& root) {
+int read_file(const char* path, std::string& s, Value& root) {
     FILE* fp = std::fopen(path, "rb");
     if (!fp) return err(SDMM_E_INVALID, std::string("cannot open ") + path);
-    std::string s;
     char buf[1 << 16];
     size_t n;
     while ((n = std::fread(buf, 1, sizeof buf, fp)) > 0) s.append(buf, n);
@@ -404,8 +443,9 @@ int sdmm_mix_save_json(const sdmm_mix* m, const char* path) {
 int sdmm_mix_load_json(const char* path, int device, sdmm_mix** out) {
     if (!path || !out) return err(SDMM_E_INVALID, "invalid argument");
     *out = nullptr;
+    std::string text;   // the values below are views into it
     Value root;
-    int r = read_file(path, root);
+    int r = read_file(path, text, root);
     if (r) return r;
     const Value* mv = root.get("mixture");
     if (!mv || mv->kind != Value::Obj) return err(SDMM_E_INVALID, std::string(path) + ": no mixture");
@@ -456,8 +496,9 @@ int sdmm_load_json(const char* path, int device, sdmm_stree** tree_out, sdmm_mix
                    int* num_nodes_out) {
     if (!path) return err(SDMM_E_INVALID, "invalid argument");
     if (tree_out) *tree_out = nullptr;
+    std::string text;   // the values below are views into it
     Value root;
-    int r = read_file(path, root);
+    int r = read_file(path, text, root);
     if (r) return r;
     long long n = 0;
     const Value* nv = root.get("num_nodes");
@@ -476,14 +517,16 @@ int sdmm_load_json(const char* path, int device, sdmm_stree** tree_out, sdmm_mix
     if (!mixes || mixes->kind != Value::Arr) return err(SDMM_E_INVALID, std::string(path) + ": no mixtures array");
     // parse everything before creating device objects: a bad file allocates nothing
     std::vector<std::pair<int, std::unique_ptr<MixImage>>> images;
+    if (!mixes->nums.empty()) return err(SDMM_E_INVALID, std::string(path) + ": mixtures must be objects");
+    std::vector<char> seen(un, 0);
     for (size_t j = 0; j < mixes->arr.size(); ++j) {
         const Value& e = mixes->arr[j];
         long long node = -1;
         const std::string where = std::string(path) + ": mixtures[" + std::to_string(j) + "]";
         if (!e.get("node") || !num_int(*e.get("node"), node) || node < 0 || node >= n)
             return err(SDMM_E_INVALID, where + ": bad node id");
-        for (const auto& pr : images)
-            if (pr.first == node) return err(SDMM_E_INVALID, where + ": duplicate node id");
+        if (seen[(size_t)node]) return err(SDMM_E_INVALID, where + ": duplicate node id");
+        seen[(size_t)node] = 1;
         const Value* mv = e.get("mixture");
         if (!mv) return err(SDMM_E_INVALID, where + ": no mixture");
         std::unique_ptr<MixImage> im(new MixImage());

@@ -291,16 +291,19 @@ def test_guided_render_unbiased_and_trained(pkg, oracle, scenes, gpu, plog):
     assert eg < 0.85 * eu
 
 
-def test_native_guiding_model_equals_host_loop(pkg, scenes, gpu, plog):
+@pytest.mark.parametrize("K", [16, 128])
+def test_native_guiding_model_equals_host_loop(pkg, scenes, gpu, plog, K):
     """sdmm_guiding_* (the C++ model) == the host loop above, bitwise: the
-    tree, every leaf's mixture and EM state, and a guided render."""
+    tree, every leaf's mixture and EM state, and a guided render.  K=128
+    (configs[2]'s K): wide, barely trained leaves, so most guided bounces take
+    the candidate-list overflow / full-K wave path."""
     import torch
     sc = _scene(pkg, scenes, 96, 54)
     T, spp = 4, 8
     tree = _tree(pkg, sc)
-    ref_mix = _train(pkg, sc, tree, T, spp, K=16, seed=1)
+    ref_mix = _train(pkg, sc, tree, T, spp, K=K, seed=1)
     _, _, tmin, tmax = sc.normalization()
-    g = pkg.Guiding(tmin, tmax)
+    g = pkg.Guiding(tmin, tmax, K=K)
     for it in range(T):
         _, _, st = g.iteration(sc, spp, seed=1 + it, push_seed=1 + 1000 + it)
     torch.cuda.synchronize()
@@ -321,10 +324,13 @@ def test_native_guiding_model_equals_host_loop(pkg, scenes, gpu, plog):
         for k in sr:
             np.testing.assert_array_equal(sr[k], sm[k], err_msg=f"node {i} state {k}")
     assert n == g.trained > 0
-    plog("guiding_model_trained_leaves", n, 1, lower=True)
-    img_r = sc.render(tree, ref_mix, spp=4, guided=True, seed=31)[0].clone()
-    img_g = sc.render(g.tree, None, spp=4, guided=True, seed=31)[0]
+    plog(f"guiding_model_trained_leaves_K{K}", n, 1, lower=True)
+    img_r, _, st_r = sc.render(tree, ref_mix, spp=4, guided=True, seed=31)
+    img_r = img_r.clone()
+    img_g, _, st_g = sc.render(g.tree, None, spp=4, guided=True, seed=31)
     assert torch.equal(img_r, img_g)
+    assert st_r["fallback_queries"] == st_g["fallback_queries"]
+    plog(f"guided_render_fallback_fraction_K{K}", st_g["fallback_queries"] / max(1, st_g["guided_queries"]), 1.0)
 
 
 def _assert_same_mixtures(ref, got):
