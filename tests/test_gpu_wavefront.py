@@ -5,9 +5,11 @@ bounces (sdmm_proc.cpp:309-421, :510-590) -- find the query's leaf
 leaf has none (:316-323).
 
 Parity: every query's outputs are BITWISE those of sdmm_guide_batch /
-sdmm_pdf_batch against its own leaf's mixture (themselves bit-exact in the
-component index vs the oracle, test_gpu_parity.py), node ids equal
-sdmm_stree_find's, and queries without a mixture give comp -1, pdf 0."""
+sdmm_pdf_batch against its own leaf's mixture, node ids equal
+sdmm_stree_find's, and queries without a mixture give comp -1, pdf 0; and,
+directly against the oracle, the node ids equal or_stree_find's and every
+query's component index is the oracle's (or_conditional_create + sample on
+its leaf's parameters), direction within 1e-5 and pdf within 1e-4 rel."""
 import numpy as np
 import pytest
 
@@ -55,8 +57,35 @@ def _queries(gpu, nq, seed, lo=-0.05, hi=1.05):
     return c, u, d, tt(c), tt(u), tt(d)
 
 
+def _oracle_check(oracle, t, mixes, c, u, d, node, has, cw, dw, pw, pdw, plog):
+    """The wavefront's outputs against the C oracle: node ids from the
+    oracle's tree find, per leaf the oracle's guide / pdf batch on that leaf's
+    parameters."""
+    aabb, child, _ = t.nodes()
+    np.testing.assert_array_equal(node, oracle.stree_find(aabb, child, c.T.copy()))
+    mism, derr, perr = 0, 0.0, 0.0
+    for v in np.unique(node[has]):
+        sel = np.nonzero(node == v)[0]
+        p = mixes[v].get_params()
+        om = oracle.Mixture(mixes[v].K)
+        om.copy_params_from(p)
+        om.valid[:] = p["valid"]
+        dr, pr, cr, _ = oracle.guide_batch(om, c[:, sel].T.copy(), u[:, sel].T.copy())
+        mism += int((cw[sel] != cr).sum())
+        np.testing.assert_array_equal(cw[sel], cr)
+        np.testing.assert_allclose(dw[:, sel].T, dr, atol=1e-5)
+        np.testing.assert_allclose(pw[sel], pr, rtol=1e-4, atol=1e-7)
+        pdr = oracle.pdf_batch(om, c[:, sel].T.copy(), d[:, sel].T.copy())
+        np.testing.assert_allclose(pdw[sel], pdr, rtol=1e-4, atol=1e-7)
+        derr = max(derr, float(np.abs(dw[:, sel].T - dr).max()))
+        perr = max(perr, float((np.abs(pw[sel] - pr) / (1e-7 + 1e-4 * np.abs(pr))).max()))
+    plog("wavefront_vs_oracle_index_mismatches", mism, 0)
+    plog("wavefront_vs_oracle_dir_abs_err", derr, 1e-5)
+    plog("wavefront_vs_oracle_pdf_err_over_tol", perr, 1.0)
+
+
 @pytest.mark.parametrize("K,nq", [(16, 1 << 15), (16, 3000), (64, 1 << 14)])
-def test_wavefront_equals_per_leaf_guide(pkg, synth, gpu, K, nq):
+def test_wavefront_equals_per_leaf_guide(pkg, oracle, synth, gpu, plog, K, nq):
     import torch
     b, t, mixes, leaves = _tree_and_leaf_mixtures(pkg, synth, K)
     assert sum(m is not None for m in mixes) >= 4 and sum(mixes[v] is None for v in leaves) >= 1
@@ -75,6 +104,7 @@ def test_wavefront_equals_per_leaf_guide(pkg, synth, gpu, K, nq):
     # no mixture (outside the tree, inner/untrained leaf): BSDF only
     assert (cw[~has] == -1).all() and (pw[~has] == 0).all() and (pdw[~has] == 0).all()
     assert (dw[:, ~has] == 0).all()
+    _oracle_check(oracle, t, mixes, c, u, d, node, has, cw, dw, pw, pdw, plog)
     served = 0
     for v in np.unique(node[has]):
         sel = np.nonzero(node == v)[0]
