@@ -879,6 +879,285 @@ guide_tree_fallback_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* 
 }
 
 // ---------------------------------------------------------------------------
+// Full-K queries of SMALL mixtures (K <= 128; the tree's wide leaves), FOUR
+// per wave: a 16-lane group per query, lane l of a group holding components
+// l, l + 16, ... (S slots, K <= 16 S).  Same arithmetic, same order, same
+// bits as serve_full_wave; what changes is that every instruction of the
+// serial float chains (total, the cutoff walk, sum2, the CDF walk, the pdf
+// sum) serves four queries, the per-slot values stay in registers (no LDS),
+// and the sort's cross-lane steps are DPP moves inside the group's row.  A
+// group's broadcasts never leave its own 16 lanes (ds_swizzle, DPP row
+// patterns, bpermute inside the group) and its control flow is uniform
+// across its lanes, so the groups of a wave may diverge freely.  A query
+// with a NaN weight goes to the one-wave kernel (list fb2), whose scan
+// reproduces the reference's order-dependent NaN comparisons.
+constexpr int kGroupKMax = 128;
+
+template <int L>
+__device__ __forceinline__ float gbc_t(float x) {   // lane L of this lane's 16-lane group
+    return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, x), 0x10 | (L << 5)));
+}
+// (l is a constant after unrolling: the switch folds to one swizzle)
+__device__ __forceinline__ float gbc(float x, int l) {
+    switch (l) {
+        case 0: return gbc_t<0>(x);   case 1: return gbc_t<1>(x);   case 2: return gbc_t<2>(x);
+        case 3: return gbc_t<3>(x);   case 4: return gbc_t<4>(x);   case 5: return gbc_t<5>(x);
+        case 6: return gbc_t<6>(x);   case 7: return gbc_t<7>(x);   case 8: return gbc_t<8>(x);
+        case 9: return gbc_t<9>(x);   case 10: return gbc_t<10>(x); case 11: return gbc_t<11>(x);
+        case 12: return gbc_t<12>(x); case 13: return gbc_t<13>(x); case 14: return gbc_t<14>(x);
+        default: return gbc_t<15>(x);
+    }
+}
+// acc += x of this group's elements p = 16 i + l < n, in p order (n uniform
+// inside a group; a skipped term adds -0.0, an exact no-op)
+template <int S>
+__device__ __forceinline__ float gseq_sum(float acc, const float (&x)[S], int n) {
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        if (!__any(16 * i < n)) break;
+#pragma unroll
+        for (int l = 0; l < 16; ++l) {
+            const float b = gbc(x[i], l);
+            acc += (16 * i + l < n) ? b : -0.0f;
+        }
+    }
+    return acc;
+}
+// one compare-exchange stage of the group's bitonic network (elements
+// e = 16 i + gl; cross-lane partners inside the row of 16 by DPP)
+template <int S, int KS, int J>
+__device__ __forceinline__ void gbitonic_step(uint32_t (&key)[S], uint32_t (&idx)[S], int gl) {
+    if constexpr (J >= 16) {
+        constexpr int JJ = J / 16;
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+            if (i & JJ) continue;
+            const int i2 = i | JJ;
+            const bool up = ((16 * i) & KS) == 0;   // lanes do not reach bit KS >= 32
+            const bool b = sel_before(key[i], idx[i], key[i2], idx[i2]);
+            const bool sw = up ? !b : b;
+            const uint32_t k0 = key[i], x0 = idx[i];
+            key[i] = sw ? key[i2] : k0; idx[i] = sw ? idx[i2] : x0;
+            key[i2] = sw ? k0 : key[i2]; idx[i2] = sw ? x0 : idx[i2];
+        }
+    } else {
+        const bool lower = (gl & J) == 0;
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+            const uint32_t ok = xor_lane_u<J>(key[i]), oi = xor_lane_u<J>(idx[i]);
+            const bool up = ((16 * i + gl) & KS) == 0;
+            const bool b = sel_before(key[i], idx[i], ok, oi);
+            const bool keep = (lower == up) ? b : !b;
+            key[i] = keep ? key[i] : ok;
+            idx[i] = keep ? idx[i] : oi;
+        }
+    }
+}
+template <int S, int KS, int J>
+__device__ __forceinline__ void gbitonic_stage(uint32_t (&key)[S], uint32_t (&idx)[S], int gl) {
+    gbitonic_step<S, KS, J>(key, idx, gl);
+    if constexpr (J > 1) gbitonic_stage<S, KS, J / 2>(key, idx, gl);
+}
+template <int S, int KS = 2>
+__device__ __forceinline__ void gbitonic_sort(uint32_t (&key)[S], uint32_t (&idx)[S], int gl) {
+    gbitonic_stage<S, KS, KS / 2>(key, idx, gl);
+    if constexpr (KS < 16 * S) gbitonic_sort<S, 2 * KS>(key, idx, gl);
+}
+
+// One full-K query on this lane's group; false: a NaN weight (the caller
+// hands the query to the one-wave kernel).  Outputs written by group lane 0.
+template <bool PDF_ONLY, int S>
+__device__ __forceinline__ bool serve_full_group(const float* gp, int Kp, int K, const GuideIO& io, int64_t q,
+                                                 int lane, GuideConsts gc) {
+    const int gl = lane & 15;
+    const int gbase = lane & 48;
+    const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
+    float wr[S];
+    unsigned vmask = 0;   // bit i: the conditional of component 16 i + gl is valid
+    bool nan_l = false;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        const int k = 16 * i + gl;
+        wr[i] = -0.0f;    // absent: never a candidate
+        if (k < K) {
+            wr[i] = gp_ld(gp, Kp, GP_W, k) * marginal_pdf(gp, Kp, k, c, gc.norm3);
+            vmask |= (cond_valid(gp, Kp, k, c) ? 1u : 0u) << i;
+        }
+        nan_l |= (wr[i] != wr[i]);
+    }
+    if (((__builtin_amdgcn_ballot_w64(nan_l) >> gbase) & 0xFFFFull) != 0) return false;
+    // totalMass in component order (element k = 16 i + l)
+    const float total = gseq_sum<S>(0.0f, wr, K);
+    const float cutoff = (float)(0.99 * (double)total);
+    // the selection order: (weight desc, index asc), absent entries last
+    uint32_t key[S], idx[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        key[i] = __builtin_signbit(wr[i]) ? 0u : __builtin_bit_cast(uint32_t, wr[i]) + 1u;
+        idx[i] = (uint32_t)(16 * i + gl);
+    }
+    gbitonic_sort<S>(key, idx, gl);
+    int n_live = 0;
+    float w[S];
+    bool ok[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        n_live += __builtin_popcountll((__builtin_amdgcn_ballot_w64(key[i] != 0u) >> gbase) & 0xFFFFull);
+        const unsigned vm = (unsigned)__shfl((int)vmask, gbase | (int)(idx[i] & 15u));
+        ok[i] = (vm >> (idx[i] >> 4)) & 1u;
+        w[i] = __builtin_bit_cast(float, key[i] - 1u);
+    }
+    // the cutoff walk: accum of the valid weights in selection order
+    float accum = 0.0f;
+    int lastIdx = n_live;   // (K when every weight is live and the cutoff is never reached)
+    bool done = false;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        if (!__any(!done && 16 * i < n_live)) break;
+        const float t = ok[i] ? w[i] : 0.0f;
+#pragma unroll
+        for (int l = 0; l < 16; ++l) {
+            const float b = gbc(t, l);
+            const int p = 16 * i + l;
+            if (!done && p < n_live) {
+                accum += b;
+                if (accum >= cutoff) { lastIdx = p + 1; done = true; }
+            }
+        }
+    }
+    // finish_query: slot weights, createCdf, sample / given direction, pdf
+    const float invSum = 1.0f / accum;
+    const bool scaled = __builtin_isfinite(invSum);
+    float f[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        float wi = ok[i] ? w[i] : 0.0f;
+        if (scaled) wi = wi * invSum;
+        f[i] = wi;
+    }
+    const float sum2 = gseq_sum<S>(0.0f, f, lastIdx);
+    bool pdf_q = PDF_ONLY;
+    if constexpr (!PDF_ONLY) pdf_q = io.pmode && io.pmode[q];   // uniform in the group
+    float outd[3] = {0.0f, 0.0f, 0.0f};
+    float outpdf = 0.0f;
+    int outcomp = -1;
+    if (lastIdx > 0 && sum2 != 0.0f) {
+#pragma unroll
+        for (int i = 0; i < S; ++i) f[i] = f[i] / sum2;
+        float dir[3];
+        if (!pdf_q) {
+            // sampleDiscreteCdf: lower_bound == first slot with cdf >= u, else the tie walk
+            const float u0 = io.u0[q], u1 = io.u1[q], u2 = io.u2[q];
+            float cdf = 0.0f, prev = 0.0f;
+            int slot = -1, runStart = 0;
+#pragma unroll
+            for (int i = 0; i < S; ++i) {
+                if (!__any(slot < 0 && 16 * i < lastIdx)) break;
+#pragma unroll
+                for (int l = 0; l < 16; ++l) {
+                    const float b = gbc(f[i], l);
+                    const int p = 16 * i + l;
+                    if (slot < 0 && p < lastIdx) {
+                        cdf += b;
+                        if (p == 0 || cdf != prev) runStart = p;
+                        prev = cdf;
+                        if (cdf >= u0) slot = p;
+                    }
+                }
+            }
+            if (slot < 0) slot = runStart;
+            int mine = 0;
+#pragma unroll
+            for (int i = 0; i < S; ++i) mine = (i == (slot >> 4)) ? (int)idx[i] : mine;
+            const int ksel = __shfl(mine, gbase | (slot & 15));
+            float esel[3];
+            cond_mean_dir(gp, Kp, ksel, c, esel);
+            const float radius = sqrtf(-2.0f * logf(1.0f - u1));
+            const float theta = (float)(2.0 * kPi * (double)u2);
+            float res0, res1;
+            sincosf(theta, &res0, &res1);
+            const float z0 = radius * res0, z1 = radius * res1;
+            const float L00 = gp_ld(gp, Kp, GP_CL00, ksel), L10 = gp_ld(gp, Kp, GP_CL10, ksel);
+            const float L11 = gp_ld(gp, Kp, GP_CL11, ksel);
+            const float v0 = L00 * z0 + 0.0f * z1;
+            const float v1 = L10 * z0 + L11 * z1;
+            float tof[9];
+            coordinates_f(esel, tof);
+            ts_exp_dir(tof, v0, v1, dir);
+            outcomp = ksel;
+        } else {
+            dir[0] = io.e0[q]; dir[1] = io.e1[q]; dir[2] = io.e2[q];
+            outcomp = kCompPdfValid;
+        }
+        // MixtureModel::pdf over the conditional: terms per own slot, summed in slot order
+        float term[S];
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+            term[i] = -0.0f;
+            if (16 * i + gl < lastIdx && f[i] != 0.0f) {
+                float e[3];
+                cond_mean_dir(gp, Kp, (int)idx[i], c, e);
+                term[i] = f[i] * cond_component_pdf(gp, Kp, (int)idx[i], e, dir, gc.norm2);
+            }
+        }
+        outpdf = gseq_sum<S>(0.0f, term, lastIdx);
+        outd[0] = dir[0]; outd[1] = dir[1]; outd[2] = dir[2];
+    }
+    if (gl == 0) {
+        io.pdf[q] = outpdf;
+        if constexpr (!PDF_ONLY) {
+            io.d0[q] = outd[0]; io.d1[q] = outd[1]; io.d2[q] = outd[2];
+            io.comp[q] = outcomp;
+        }
+    }
+    return true;
+}
+
+// The listed full-K queries, a 16-lane group each (grid-stride over groups);
+// TREE: each against its own leaf's mixture.  NaN queries -> fb2 (count at
+// fb2[0], list from fb2 + 1) for the one-wave kernel.
+template <bool PDF_ONLY, bool TREE, int S>
+__global__ void __launch_bounds__(64)
+guide_group_fallback_kernel(const float* __restrict__ gp1, int Kp1, int K1, const STNodeDev* __restrict__ nodes,
+                            const GuideMix* __restrict__ tab, GuideIO io, GuideConsts gc,
+                            const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list,
+                            int* __restrict__ fb2) {
+    const int lane = threadIdx.x;
+    const int count = *fb_count;
+    const int64_t groups = (int64_t)gridDim.x * 4;
+    for (int64_t gi = (int64_t)blockIdx.x * 4 + (lane >> 4); gi < count; gi += groups) {
+        const int64_t q = fb_list[gi];
+        const float* gp = gp1;
+        int Kp = Kp1, K = K1;
+        if constexpr (TREE) {
+            const int node = stree_find_point(nodes, io.c0[q], io.c1[q], io.c2[q]);   // a listed query has a mixture
+            const GuideMix mx = tab[node];
+            gp = mx.gp; Kp = mx.Kp; K = mx.K;
+        }
+        if (!serve_full_group<PDF_ONLY, S>(gp, Kp, K, io, q, lane, gc) && (lane & 15) == 0)
+            fb2[1 + atomicAdd(fb2, 1)] = (int32_t)q;
+    }
+}
+
+template <bool PDF_ONLY, bool TREE>
+static void launch_group_fallback(int kmax, int blocks, hipStream_t st, const float* gp, int Kp, int K,
+                                  const STNodeDev* nd, const GuideMix* tb, const GuideIO& io, GuideConsts gc,
+                                  const int* fb_count, const int32_t* fb_list, int* fb2) {
+    if (kmax <= 16)
+        hipLaunchKernelGGL((guide_group_fallback_kernel<PDF_ONLY, TREE, 1>), dim3(blocks), dim3(64), 0, st, gp, Kp,
+                           K, nd, tb, io, gc, fb_count, fb_list, fb2);
+    else if (kmax <= 32)
+        hipLaunchKernelGGL((guide_group_fallback_kernel<PDF_ONLY, TREE, 2>), dim3(blocks), dim3(64), 0, st, gp, Kp,
+                           K, nd, tb, io, gc, fb_count, fb_list, fb2);
+    else if (kmax <= 64)
+        hipLaunchKernelGGL((guide_group_fallback_kernel<PDF_ONLY, TREE, 4>), dim3(blocks), dim3(64), 0, st, gp, Kp,
+                           K, nd, tb, io, gc, fb_count, fb_list, fb2);
+    else
+        hipLaunchKernelGGL((guide_group_fallback_kernel<PDF_ONLY, TREE, 8>), dim3(blocks), dim3(64), 0, st, gp, Kp,
+                           K, nd, tb, io, gc, fb_count, fb_list, fb2);
+}
+
+// ---------------------------------------------------------------------------
 // Product with a learned BSDF (the plugin's sampleProduct path,
 // sdmm_proc.cpp:327-392, :474-486): MixtureModel::multiply of the query's
 // conditional with a learned-BSDF lobe set (mixture_model.h:345-370,
@@ -1732,7 +2011,7 @@ static hipError_t launch_tree_cand(int cap, dim3 grid, hipStream_t st, const STN
 hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float* const c[3],
                         const float* const u[3], const float* const dgiven[3], float* const d[3], float* pdf,
                         int32_t* comp, float norm2, float norm3, int cap, int* fb_count, int32_t* fb_list,
-                        int cus, hipStream_t st, const GuideSortScratch* sort) {
+                        int cus, hipStream_t st, const GuideSortScratch* sort, int* fb2) {
     if (nq <= 0) return hipSuccess;
     cap = (cap < 0) ? 0 : (cap > kGuideCap ? kGuideCap : cap);
     if (nq > INT32_MAX) return hipErrorInvalidValue;
@@ -1757,6 +2036,21 @@ hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float*
     e = dgiven ? launch_cand<true>(cap, grid, st, gp, Kp, K, nq, io, gc, fb_count, fb_list, perm)
                : launch_cand<false>(cap, grid, st, gp, Kp, K, nq, io, gc, fb_count, fb_list, perm);
     if (e != hipSuccess) return e;
+    if (fb2 && K <= kGroupKMax) {
+        // four full-K queries per wave; the NaN ones (if any) then one per wave
+        e = hipMemsetAsync(fb2, 0, sizeof(int), st);
+        if (e != hipSuccess) return e;
+        if (dgiven)
+            launch_group_fallback<true, false>(K, fb_blocks, st, gp, Kp, K, nullptr, nullptr, io, gc, fb_count,
+                                               fb_list, fb2);
+        else
+            launch_group_fallback<false, false>(K, fb_blocks, st, gp, Kp, K, nullptr, nullptr, io, gc, fb_count,
+                                                fb_list, fb2);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        fb_count = fb2;
+        fb_list = fb2 + 1;
+    }
     if (dgiven)
         hipLaunchKernelGGL(guide_fallback_kernel<true>, dim3(fb_blocks), dim3(Tfb), lds_fb, st, gp, Kp, K, io, gc,
                            fb_count, fb_list);
@@ -1774,7 +2068,7 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
                              const float* const u[3], const float* const dgiven[3], float* const d[3],
                              float* pdf, int32_t* comp, int32_t* node_out, float norm2, float norm3, int cap,
                              int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
-                             const GuideSortScratch* sort, const uint8_t* pmode) {
+                             const GuideSortScratch* sort, const uint8_t* pmode, int* fb2) {
     if (nq <= 0) return hipSuccess;
     cap = (cap < 0) ? 0 : (cap > kGuideCap ? kGuideCap : cap);
     if (nq > INT32_MAX) return hipErrorInvalidValue;
@@ -1803,6 +2097,20 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
     e = dgiven ? launch_tree_cand<true>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_out)
                : launch_tree_cand<false>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_out);
     if (e != hipSuccess) return e;
+    if (fb2 && kmax <= kGroupKMax) {
+        e = hipMemsetAsync(fb2, 0, sizeof(int), st);
+        if (e != hipSuccess) return e;
+        if (dgiven)
+            launch_group_fallback<true, true>(kmax, fb_blocks, st, nullptr, 0, 0, nd, tb, io, gc, fb_count, fb_list,
+                                              fb2);
+        else
+            launch_group_fallback<false, true>(kmax, fb_blocks, st, nullptr, 0, 0, nd, tb, io, gc, fb_count,
+                                               fb_list, fb2);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        fb_count = fb2;
+        fb_list = fb2 + 1;
+    }
     if (dgiven)
         hipLaunchKernelGGL(guide_tree_fallback_kernel<true>, dim3(fb_blocks), dim3(Tfb), lds_fb, st, nd, tb, kmax,
                            io, gc, fb_count, fb_list);

@@ -81,12 +81,12 @@ hipError_t launch_stree_route(const void* nodes, int num_nodes, int key_bits, co
 hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float* const c[3],
                         const float* const u[3], const float* const dgiven[3], float* const d[3], float* pdf,
                         int32_t* comp, float norm2, float norm3, int cap, int* fb_count, int32_t* fb_list,
-                        int cus, hipStream_t st, const GuideSortScratch* sort);
+                        int cus, hipStream_t st, const GuideSortScratch* sort, int* fb2 = nullptr);
 hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64_t nq, const float* const c[3],
                              const float* const u[3], const float* const dgiven[3], float* const d[3],
                              float* pdf, int32_t* comp, int32_t* node_out, float norm2, float norm3, int cap,
                              int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
-                             const GuideSortScratch* sort, const uint8_t* pmode = nullptr);
+                             const GuideSortScratch* sort, const uint8_t* pmode = nullptr, int* fb2 = nullptr);
 hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* condCov, int64_t nq,
                                 const float* const c[3], const float* const u[3], const float* const dgiven[3],
                                 float* const d[3], float* pdf, int32_t* comp, const int32_t* material,
@@ -1685,7 +1685,8 @@ int sdmm_guide_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], con
     int r = ensure_guide_scratch(m, nq);
     if (r) return r;
     HIP_TRY(launch_guide(m->gp, m->Kp, m->K, nq, c, u, nullptr, d, pdf, comp, m->norm2, m->norm3,
-                         m->guide_cap, m->guide_fb, m->guide_fb + 1, m->cus, m->stream, guide_order(m, nq)));
+                         m->guide_cap, m->guide_fb, m->guide_fb + 1, m->cus, m->stream, guide_order(m, nq),
+                         (int*)m->guide_sort.keys[0]));
     return SDMM_OK;
 }
 
@@ -1698,7 +1699,8 @@ int sdmm_pdf_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], const
     int r = ensure_guide_scratch(m, nq);
     if (r) return r;
     HIP_TRY(launch_guide(m->gp, m->Kp, m->K, nq, c, nullptr, d, nullptr, pdf, nullptr, m->norm2, m->norm3,
-                         m->guide_cap, m->guide_fb, m->guide_fb + 1, m->cus, m->stream, guide_order(m, nq)));
+                         m->guide_cap, m->guide_fb, m->guide_fb + 1, m->cus, m->stream, guide_order(m, nq),
+                         (int*)m->guide_sort.keys[0]));
     return SDMM_OK;
 }
 
@@ -2387,7 +2389,7 @@ int st_guide(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const f
     const GuideSortScratch* sort = nq >= (1 << 14) ? &t->guide_sort : nullptr;
     HIP_TRY(launch_guide_tree(t->dnodes, t->dtab, t->tab_kmax, nq, c, u, dgiven, d, pdf, comp, node_out,
                               norm_const(2), norm_const(3), kGuideCapMax, t->guide_fb, t->guide_fb + 1,
-                              cus > 0 ? cus : 256, t->stream, sort, pmode));
+                              cus > 0 ? cus : 256, t->stream, sort, pmode, (int*)t->guide_sort.keys[0]));
     return SDMM_OK;
 }
 
