@@ -579,6 +579,17 @@ copy_many_kernel(const uint4* const* __restrict__ src, uint4* const* __restrict_
     for (size_t i = threadIdx.x; i < words; i += blockDim.x) d[i] = s[i];
 }
 
+// out[i] = *src[i] (one scalar of each of n mixtures: sdmm_iterations_run)
+__global__ void gather_f64_kernel(const double* const* __restrict__ src, int n, double* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = *src[i];
+}
+hipError_t launch_gather_f64(const void* src_tab, int n, double* out, hipStream_t st) {
+    hipLaunchKernelGGL(gather_f64_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                       (const double* const*)src_tab, n, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_copy_many(int n, const void* src_tab, const void* dst_tab, size_t bytes, hipStream_t st) {
     hipLaunchKernelGGL(copy_many_kernel, dim3((unsigned)n), dim3(256), 0, st, (const uint4* const*)src_tab,
                        (uint4* const*)dst_tab, bytes / 16);

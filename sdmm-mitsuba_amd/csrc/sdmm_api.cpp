@@ -59,6 +59,7 @@ hipError_t launch_init_state(int K, const double* scal, const float* bprior, flo
 hipError_t launch_set_all_batched(int n, int K, int Kp, const void* tab, const void* staging, size_t per, float norm5,
                                   hipStream_t st);
 hipError_t launch_copy_many(int n, const void* src_tab, const void* dst_tab, size_t bytes, hipStream_t st);
+hipError_t launch_gather_f64(const void* src_tab, int n, double* out, hipStream_t st);
 struct InitDescHost {
     CanonDev C;
     float *ep, *gp, *bp, *bd;
@@ -1130,20 +1131,30 @@ int sdmm_iterations_run(const sdmm_mix* const* mixes, int n, int* out) {
     for (int i = 0; i < n; ++i)
         if (!mixes[i]) return fail(SDMM_E_INVALID, "NULL handle in mixes");
     HIP_TRY(hipSetDevice(mixes[0]->device));
-    double* pin = nullptr;
-    HIP_TRY(hipHostMalloc((void**)&pin, sizeof(double) * (size_t)n, hipHostMallocDefault));
+    // every mixture's pending work first (its own stream), then ONE gather of
+    // the n counters and one copy back (a copy per leaf cost ~3 us of launch
+    // each: ~10 ms per training pass of a few thousand leaves)
     hipError_t e = hipSuccess;
-    for (int i = 0; i < n && e == hipSuccess; ++i)
-        e = hipMemcpyAsync(pin + i, mixes[i]->S.scalars + SC_IT, sizeof(double), hipMemcpyDeviceToHost,
-                           mixes[i]->stream);
     std::vector<hipStream_t> seen;
     for (int i = 0; i < n && e == hipSuccess; ++i)
         if (std::find(seen.begin(), seen.end(), mixes[i]->stream) == seen.end()) {
             seen.push_back(mixes[i]->stream);
             e = hipStreamSynchronize(mixes[i]->stream);
         }
-    for (int i = 0; i < n && e == hipSuccess; ++i) out[i] = (int)pin[i];
-    (void)hipHostFree(pin);
+    const hipStream_t st = mixes[0]->stream;
+    std::vector<const double*> src((size_t)n);
+    for (int i = 0; i < n; ++i) src[(size_t)i] = mixes[i]->S.scalars + SC_IT;
+    std::vector<double> vals((size_t)n);
+    char* buf = nullptr;
+    const size_t tab_bytes = ((sizeof(void*) * (size_t)n + 255) / 256) * 256;
+    if (e == hipSuccess) e = hipMallocAsync((void**)&buf, tab_bytes + sizeof(double) * (size_t)n, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(buf, src.data(), sizeof(void*) * (size_t)n, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = launch_gather_f64(buf, n, (double*)(buf + tab_bytes), st);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(vals.data(), buf + tab_bytes, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, st);
+    if (buf) (void)hipFreeAsync(buf, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    for (int i = 0; i < n && e == hipSuccess; ++i) out[i] = (int)vals[(size_t)i];
     if (e != hipSuccess) return fail(SDMM_E_HIP, std::string("sdmm_iterations_run: ") + hipGetErrorString(e));
     return SDMM_OK;
 }
