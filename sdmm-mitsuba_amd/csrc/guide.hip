@@ -122,6 +122,44 @@ __device__ __forceinline__ float marginal_pdf(const float* gp, int Kp, int k, co
     return marginal_pdf_q(gp, Kp, k, marginal_q(gp, Kp, k, c), norm3);
 }
 
+// The marginal fields of component k's record (weight, mean, the Cholesky
+// entries the forward substitution reads, detInv, the three exact-division
+// reciprocals), loaded together so that a loop over components can fetch
+// component k + 1's while it evaluates k (the record loads of a per-lane
+// mixture pointer are vector loads with L2 latency).  Same operations as
+// marginal_q / marginal_pdf_q above.
+struct MargRec {
+    float w, mu0, mu1, mu2, ml10, ml20, ml21, mdi;
+    uint32_t r[6];
+};
+__device__ __forceinline__ MargRec load_marg(const float* gp, int k) {
+    const cfloat_p b = (cfloat_p)gp + k * GP_STRIDE;
+    MargRec m;
+    m.w = b[GP_W]; m.mu0 = b[GP_MU0]; m.mu1 = b[GP_MU1]; m.mu2 = b[GP_MU2];
+    m.ml10 = b[GP_ML10]; m.ml20 = b[GP_ML20]; m.ml21 = b[GP_ML21]; m.mdi = b[GP_MDI];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) m.r[i] = __builtin_bit_cast(uint32_t, b[GP_RML00 + i]);
+    return m;
+}
+__device__ __forceinline__ double marg_rcp(const MargRec& m, int i) {
+    return __builtin_bit_cast(double, (uint64_t)m.r[2 * i] | ((uint64_t)m.r[2 * i + 1] << 32));
+}
+__device__ __forceinline__ float marginal_weight_rec(const MargRec& m, const float c[3], float norm3) {
+    float r0 = c[0] - m.mu0;
+    float r1 = c[1] - m.mu1;
+    float r2 = c[2] - m.mu2;
+    float s0 = (float)((double)r0 * marg_rcp(m, 0));   // r0 / ML00
+    r1 = r1 - s0 * m.ml10;
+    r2 = r2 - s0 * m.ml20;
+    float s1 = (float)((double)r1 * marg_rcp(m, 1));   // r1 / ML11
+    r2 = r2 - s1 * m.ml21;
+    float s2 = (float)((double)r2 * marg_rcp(m, 2));   // r2 / ML22
+    const float q = s0 * s0 + s1 * s1 + s2 * s2;
+    float pdf = 0.0f;
+    if (!(q > kMarginalZeroQ)) pdf = (float)((double)norm3 * exp(-0.5 * (double)q)) * m.mdi;
+    return m.w * pdf;
+}
+
 // MVTN::conditional: mean direction of joint component k's conditional at c.
 __device__ __forceinline__ bool cond_mean_dir(const float* gp, int Kp, int k, const float c[3],
                                               float e[3]) {
@@ -313,8 +351,11 @@ __device__ __forceinline__ int build_candidates(const float* gp, int Kp, int K, 
     // rounding, 2^-24 relative, stays far inside the margin): one multiply per
     // component instead of a double division
     const float skip_f = 0.0089f / (float)K;
+    MargRec nx = load_marg(gp, 0);   // (K >= 1)
     for (int k = 0; k < K; ++k) {
-        const float w = gp_ld(gp, Kp, GP_W, k) * marginal_pdf_q(gp, Kp, k, marginal_q(gp, Kp, k, c), norm3);
+        const MargRec rec = nx;
+        if (k + 1 < K) nx = load_marg(gp, k + 1);   // next component's fields in flight
+        const float w = marginal_weight_rec(rec, c, norm3);
         total += w;
         // the float sum of non-negative terms never decreases, so the final
         // tau >= (0.01 total - ulp) 0.999 / K > 0.009 total_so_far / K: a weight

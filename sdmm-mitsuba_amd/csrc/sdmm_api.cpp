@@ -16,6 +16,7 @@
 #include <vector>
 #include <algorithm>
 #include <atomic>
+#include <future>
 #include <thread>
 
 #include "../../include/sdmm_gpu.h"
@@ -1996,14 +1997,17 @@ void st_split_local(std::vector<STNodeHost>& L, int node, std::vector<int64_t>& 
     STNodeHost parent = nd;
     parent.axis = ax;
     STNodeHost ch[2] = {st_child(parent, 0, split), st_child(parent, 1, split)};
+    // both children's members in one pass (a sample on the split plane goes to both)
     std::vector<int64_t> sub[2];
-    for (int c = 0; c < 2; ++c) {
-        for (int64_t i : idx) {
-            const float p[3] = {px[i], py[i], pz[i]};
-            if (st_contains(ch[c], p)) sub[c].push_back(i);
-        }
-        if ((int64_t)sub[c].size() == n) return;   // would not separate the samples
+    sub[0].reserve((size_t)n / 2 + 16);
+    sub[1].reserve((size_t)n / 2 + 16);
+    for (int64_t i : idx) {
+        const float p[3] = {px[i], py[i], pz[i]};
+        if (st_contains(ch[0], p)) sub[0].push_back(i);
+        if (st_contains(ch[1], p)) sub[1].push_back(i);
     }
+    for (int c = 0; c < 2; ++c)
+        if ((int64_t)sub[c].size() == n) return;   // would not separate the samples
     L[(size_t)node].axis = ax;
     for (int c = 0; c < 2; ++c) {
         L[(size_t)node].child[c] = (int)L.size();
@@ -2011,8 +2015,35 @@ void st_split_local(std::vector<STNodeHost>& L, int node, std::vector<int64_t>& 
     }
     idx.clear();
     idx.shrink_to_fit();
-    for (int c = 0; c < 2; ++c)
-        st_split_local(L, L[(size_t)node].child[c], sub[c], px, py, pz, threshold);
+    const int c0 = L[(size_t)node].child[0], c1 = L[(size_t)node].child[1];
+    // Two large children: child 1's subtree on a thread of its own, built as a
+    // local node list and appended after child 0's -- the creation (DFS)
+    // order, hence every node id, is that of the sequential recursion.
+    constexpr int64_t kParallelSplit = 1 << 15;
+    if ((int64_t)sub[0].size() > kParallelSplit && (int64_t)sub[1].size() > kParallelSplit) {
+        std::vector<STNodeHost> L1{L[(size_t)c1]};
+        std::future<void> f1;
+        try {
+            f1 = std::async(std::launch::async, [&] { st_split_local(L1, 0, sub[1], px, py, pz, threshold); });
+        } catch (...) {
+            f1 = std::future<void>();
+        }
+        st_split_local(L, c0, sub[0], px, py, pz, threshold);
+        if (f1.valid())
+            f1.get();
+        else
+            st_split_local(L1, 0, sub[1], px, py, pz, threshold);
+        const int base = (int)L.size() - 1;
+        auto remap = [&](STNodeHost x) {
+            if (x.child[0] >= 0) { x.child[0] = base + x.child[0]; x.child[1] = base + x.child[1]; }
+            return x;
+        };
+        L[(size_t)c1] = remap(L1[0]);
+        for (size_t i = 1; i < L1.size(); ++i) L.push_back(remap(L1[i]));
+        return;
+    }
+    st_split_local(L, c0, sub[0], px, py, pz, threshold);
+    st_split_local(L, c1, sub[1], px, py, pz, threshold);
 }
 
 // L[0] is tree node v after st_split_local; its new nodes get the next ids

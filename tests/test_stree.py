@@ -11,11 +11,14 @@ def _points(synth, n, seed=4):
     return b, b["x"][0:3].copy()
 
 
-@pytest.mark.parametrize("depth,threshold", [(0, 4000), (1, 3000), (2, 20000), (3, 50000)])
-def test_tree_matches_oracle(pkg, oracle, synth, depth, threshold):
+@pytest.mark.parametrize("depth,threshold,n", [(0, 4000, 60000), (1, 3000, 60000), (2, 20000, 60000),
+                                               (3, 50000, 60000), (0, 2000, 400000)])
+def test_tree_matches_oracle(pkg, oracle, synth, depth, threshold, n):
     """split_to_depth + split(threshold) -> identical node arrays (ids, boxes,
-    children, axes) from the library and from the oracle."""
-    b, p = _points(synth, 60000)
+    children, axes) from the library and from the oracle.  n = 400000: the
+    host split recurses into both children of a large node on two threads
+    (> 2^15 samples each) and must still number the nodes in creation order."""
+    b, p = _points(synth, n)
     lo, hi = np.float32([0.0, 0.0, 0.0]), np.float32([1.0, 0.95, 0.9])
     t = pkg.STree(lo, hi)
     t.split_to_depth(depth)

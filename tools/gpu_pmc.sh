@@ -17,7 +17,7 @@ IFS=';' read -r -a GROUP_LIST <<< "${PMC_GROUPS:-$GROUPS_DEFAULT}"
 for group in "${GROUP_LIST[@]}"; do
   i=$((i + 1))
   timeout -k 10 240 rocprofv3 --pmc $group --output-format csv -d "$OUT/p$i" -o run \
-      -- python3 "$GRAFT_REPO_ROOT/tools/prof_kernels.py" "$@" > "$OUT/p$i.log" 2>&1
+      -- python3 "$GRAFT_REPO_ROOT/${PMC_SCRIPT:-tools/prof_kernels.py}" "$@" > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "pass $i ($group) rc=$rc"
   [ $rc -eq 0 ] || { tail -5 "$OUT/p$i.log"; exit $rc; }
