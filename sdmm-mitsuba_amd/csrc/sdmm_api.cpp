@@ -1132,9 +1132,30 @@ int sdmm_iterations_run(const sdmm_mix* const* mixes, int n, int* out) {
     for (int i = 0; i < n; ++i)
         if (!mixes[i]) return fail(SDMM_E_INVALID, "NULL handle in mixes");
     HIP_TRY(hipSetDevice(mixes[0]->device));
-    // every mixture's pending work first (its own stream), then ONE gather of
-    // the n counters and one copy back (a copy per leaf cost ~3 us of launch
-    // each: ~10 ms per training pass of a few thousand leaves)
+    if (n < 64) {
+        // a few mixtures (the plugin's per-leaf worker threads call this with
+        // one): a pinned copy per mixture on its own stream
+        double* pin = nullptr;
+        HIP_TRY(hipHostMalloc((void**)&pin, sizeof(double) * (size_t)n, hipHostMallocDefault));
+        hipError_t e = hipSuccess;
+        for (int i = 0; i < n && e == hipSuccess; ++i)
+            e = hipMemcpyAsync(pin + i, mixes[i]->S.scalars + SC_IT, sizeof(double), hipMemcpyDeviceToHost,
+                               mixes[i]->stream);
+        std::vector<hipStream_t> seen;
+        for (int i = 0; i < n && e == hipSuccess; ++i)
+            if (std::find(seen.begin(), seen.end(), mixes[i]->stream) == seen.end()) {
+                seen.push_back(mixes[i]->stream);
+                e = hipStreamSynchronize(mixes[i]->stream);
+            }
+        for (int i = 0; i < n && e == hipSuccess; ++i) out[i] = (int)pin[i];
+        (void)hipHostFree(pin);
+        if (e != hipSuccess) return fail(SDMM_E_HIP, std::string("sdmm_iterations_run: ") + hipGetErrorString(e));
+        return SDMM_OK;
+    }
+    // many (the guiding model's ready leaves): every mixture's pending work
+    // first (its own stream), then ONE gather of the n counters and one copy
+    // back (a copy per leaf cost ~3 us of launch each: ~10 ms per training
+    // pass of a few thousand leaves)
     hipError_t e = hipSuccess;
     std::vector<hipStream_t> seen;
     for (int i = 0; i < n && e == hipSuccess; ++i)
