@@ -395,6 +395,72 @@ __device__ __forceinline__ int build_candidates(const float* gp, int Kp, int K, 
     return (ncand == K) ? K : -1;
 }
 
+// The same list built in REGISTERS (LCAP entries, static indices): a live
+// weight ripples through the sorted list by compare-and-swap (strictly
+// greater moves ahead: ties keep the earlier, lower index), the entry pushed
+// past slot cap - 1 is the dropped one.  No LDS latency chain per shift; the
+// finished list goes to the LDS slots once for the walk and finish.  Same
+// list, same results.  Measured (A/B, one box): the tree wavefront over
+// K = 128 leaves (wide, long lists) 21.1 -> 17.6 ms per guided pass; the
+// K = 16 leaves and the single trained K = 128 mixture (short lists, where
+// the ripple's fixed LCAP-step cost and its registers outweigh the LDS
+// shifts) 466 -> 489 us and 618 -> 692 us -- so only the tree kernel's
+// LCAP = 40 instance uses it.
+template <int LCAP>
+__device__ __forceinline__ int build_candidates_reg(const float* gp, int Kp, int K, const float c[3], float* cw,
+                                                    unsigned short* ck, int T, int tid, float norm3, int cap,
+                                                    float& accum) {
+    float rw[LCAP];
+    int rk[LCAP];
+#pragma unroll
+    for (int i = 0; i < LCAP; ++i) { rw[i] = -1.0f; rk[i] = 0; }
+    float total = 0.0f;
+    int cnt = 0;
+    const float skip_f = 0.0089f / (float)K;
+    MargRec nx = load_marg(gp, 0);
+    for (int k = 0; k < K; ++k) {
+        const MargRec rec = nx;
+        if (k + 1 < K) nx = load_marg(gp, k + 1);
+        const float w = marginal_weight_rec(rec, c, norm3);
+        total += w;
+        if (!(w > 0.0f) || w < total * skip_f) continue;
+        float x = w;
+        int xk = k;
+#pragma unroll
+        for (int i = 0; i < LCAP; ++i) {
+            const bool sw = (i < cap) && (x > rw[i]);
+            const float tw = rw[i];
+            const int tk = rk[i];
+            rw[i] = sw ? x : tw;
+            rk[i] = sw ? xk : tk;
+            x = sw ? tw : x;
+            xk = sw ? tk : xk;
+        }
+        cnt = min(cnt + 1, cap);
+    }
+#pragma unroll
+    for (int i = 0; i < LCAP; ++i)
+        if (i < cnt) {
+            cw[i * T + tid] = rw[i];
+            ck[i * T + tid] = (unsigned short)rk[i];
+        }
+    if (!__builtin_isfinite(total)) return -1;
+    const float cutoff = (float)(0.99 * (double)total);
+    const double tau = ((double)total - (double)cutoff) / (double)K * 0.999;
+    if (!(tau > 0.0)) return -1;
+    int ncand = 0;
+    while (ncand < cnt && (double)cw[ncand * T + tid] >= tau) ++ncand;
+    accum = 0.0f;
+    for (int i = 0; i < ncand; ++i) {
+        const int k = ck[i * T + tid];
+        const bool ok = cond_valid(gp, Kp, k, c);
+        ck[i * T + tid] = (unsigned short)(k | (ok ? 0x8000 : 0));
+        accum += ok ? cw[i * T + tid] : 0.0f;
+        if (accum >= cutoff) return i + 1;
+    }
+    return (ncand == K) ? K : -1;
+}
+
 // Plane pointers of one guided batch (inputs c, u or given directions e;
 // outputs d, pdf, comp).
 struct GuideIO {
@@ -445,12 +511,13 @@ __device__ __forceinline__ void finish_and_write(const float* gp, int Kp, const 
 
 // Candidate path of query q against one mixture; false: q needs the full-K
 // fallback (appended to fb_list).
-template <bool PDF_ONLY>
+template <bool PDF_ONLY, int LCAP, bool REG = false>
 __device__ __forceinline__ void serve_cand(const float* gp, int Kp, int K, const GuideIO& io, int64_t q,
                                            const float c[3], float* cw, unsigned short* ck, int tid, int cap,
                                            GuideConsts gc, int* fb_count, int32_t* fb_list) {
     float accum = 0.0f;
-    const int lastIdx = build_candidates(gp, Kp, K, c, cw, ck, 64, tid, gc.norm3, cap, accum);
+    const int lastIdx = REG ? build_candidates_reg<LCAP>(gp, Kp, K, c, cw, ck, 64, tid, gc.norm3, cap, accum)
+                            : build_candidates(gp, Kp, K, c, cw, ck, 64, tid, gc.norm3, cap, accum);
     if (lastIdx < 0) {
         fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
         return;
@@ -472,7 +539,7 @@ guide_cand_kernel(const float* __restrict__ gp, int Kp, int K, int64_t nq, Guide
     // coherent order: thread t serves query perm[t] (Morton order of c)
     const int64_t q = perm ? (int64_t)perm[t] : t;
     const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
-    serve_cand<PDF_ONLY>(gp, Kp, K, io, q, c, cw, ck, tid, cap, gc, fb_count, fb_list);
+    serve_cand<PDF_ONLY, LCAP>(gp, Kp, K, io, q, c, cw, ck, tid, cap, gc, fb_count, fb_list);
 }
 
 // Wavefront over the spatial tree's leaves (SDMMRenderer::sampleSurface,
@@ -510,7 +577,8 @@ guide_tree_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __re
             if (mx.K <= 0)
                 write_invalid<PDF_ONLY>(io, q);
             else
-                serve_cand<PDF_ONLY>(mx.gp, mx.Kp, mx.K, io, q, c, cw, ck, tid, cap, gc, fb_count, fb_list);
+                serve_cand<PDF_ONLY, LCAP, (LCAP >= kGuideCap)>(mx.gp, mx.Kp, mx.K, io, q, c, cw, ck, tid, cap, gc,
+                                                                 fb_count, fb_list);
             return;
         }
     }
@@ -521,7 +589,8 @@ guide_tree_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __re
         if (mx.K <= 0)
             write_invalid<PDF_ONLY>(io, q);
         else
-            serve_cand<PDF_ONLY>(mx.gp, mx.Kp, mx.K, io, q, c, cw, ck, tid, cap, gc, fb_count, fb_list);
+            serve_cand<PDF_ONLY, LCAP, (LCAP >= kGuideCap)>(mx.gp, mx.Kp, mx.K, io, q, c, cw, ck, tid, cap, gc,
+                                                             fb_count, fb_list);
         break;
     }
 }
