@@ -679,52 +679,60 @@ __device__ __forceinline__ uint32_t xor_lane_u(uint32_t x) {
     else return (uint32_t)__shfl_xor(xi, J);
 }
 
-// One compare-exchange step of a bitonic network over the wave's 64 S
-// elements e = 64 i + lane, ordered by `before` = (key desc, index asc) -- the
-// order in which the reference's selection scan takes the weights (largest
-// first, the lowest index among equals).  Stage (KS, J): element e pairs with
-// e ^ J and, inside the KS-block of e, the block runs "up" (before-first)
-// when (e & KS) == 0.
-__device__ __forceinline__ bool sel_before(uint32_t ka, uint32_t ia, uint32_t kb, uint32_t ib) {
-    return ka > kb || (ka == kb && ia < ib);
+// Bitonic networks over the 64 S elements of a wave (W = 64) or the 16 S
+// elements of a 16-lane group (W = 16), element e = W i + (lane mod W), in
+// the order the reference's selection scan takes weights: largest first, the
+// lowest index among equals.  One packed 64-bit key per element, (weight key
+// << 32) | (2^32 - 1 - index), makes that order a single unsigned compare
+// (a larger key comes first).  Stage (KS, J): element e pairs with e ^ J; the
+// KS-block of e runs "up" (larger first) when (e & KS) == 0.
+template <int J>
+__device__ __forceinline__ uint64_t xor_lane_u64(uint64_t x) {
+    const uint32_t lo = xor_lane_u<J>((uint32_t)x), hi = xor_lane_u<J>((uint32_t)(x >> 32));
+    return (uint64_t)lo | ((uint64_t)hi << 32);
 }
-template <int S, int KS, int J>
-__device__ __forceinline__ void bitonic_step(uint32_t (&key)[S], uint32_t (&idx)[S], int lane) {
-    if constexpr (J >= 64) {
-        constexpr int JJ = J / 64;
+__device__ __forceinline__ uint64_t sel_key(uint32_t wkey, uint32_t idx) {
+    return ((uint64_t)wkey << 32) | (uint64_t)(0xFFFFFFFFu - idx);
+}
+__device__ __forceinline__ uint32_t sel_idx(uint64_t k) { return 0xFFFFFFFFu - (uint32_t)k; }
+__device__ __forceinline__ uint32_t sel_wkey(uint64_t k) { return (uint32_t)(k >> 32); }
+
+template <int W, int S, int KS, int J>
+__device__ __forceinline__ void bsort_step(uint64_t (&v)[S], int gl) {
+    if constexpr (J >= W) {
+        constexpr int JJ = J / W;
 #pragma unroll
         for (int i = 0; i < S; ++i) {
             if (i & JJ) continue;
             const int i2 = i | JJ;
-            const bool up = ((64 * i) & KS) == 0;   // lanes do not reach bit KS >= 128
-            const bool b = sel_before(key[i], idx[i], key[i2], idx[i2]);
+            const bool up = ((W * i) & KS) == 0;   // lanes do not reach bit KS >= 2W
+            const bool b = v[i] > v[i2];
             const bool sw = up ? !b : b;
-            const uint32_t k0 = key[i], x0 = idx[i];
-            key[i] = sw ? key[i2] : k0; idx[i] = sw ? idx[i2] : x0;
-            key[i2] = sw ? k0 : key[i2]; idx[i2] = sw ? x0 : idx[i2];
+            const uint64_t a = v[i];
+            v[i] = sw ? v[i2] : a;
+            v[i2] = sw ? a : v[i2];
         }
     } else {
-        const bool lower = (lane & J) == 0;
+        const bool lower = (gl & J) == 0;
 #pragma unroll
         for (int i = 0; i < S; ++i) {
-            const uint32_t ok = xor_lane_u<J>(key[i]), oi = xor_lane_u<J>(idx[i]);
-            const bool up = ((64 * i + lane) & KS) == 0;
-            const bool b = sel_before(key[i], idx[i], ok, oi);
+            const uint64_t o = xor_lane_u64<J>(v[i]);
+            const bool up = ((W * i + gl) & KS) == 0;
+            const bool b = v[i] > o;
             const bool keep = (lower == up) ? b : !b;
-            key[i] = keep ? key[i] : ok;
-            idx[i] = keep ? idx[i] : oi;
+            v[i] = keep ? v[i] : o;
         }
     }
 }
-template <int S, int KS, int J>
-__device__ __forceinline__ void bitonic_stage(uint32_t (&key)[S], uint32_t (&idx)[S], int lane) {
-    bitonic_step<S, KS, J>(key, idx, lane);
-    if constexpr (J > 1) bitonic_stage<S, KS, J / 2>(key, idx, lane);
+template <int W, int S, int KS, int J>
+__device__ __forceinline__ void bsort_stage(uint64_t (&v)[S], int gl) {
+    bsort_step<W, S, KS, J>(v, gl);
+    if constexpr (J > 1) bsort_stage<W, S, KS, J / 2>(v, gl);
 }
-template <int S, int KS = 2>
-__device__ __forceinline__ void bitonic_sort(uint32_t (&key)[S], uint32_t (&idx)[S], int lane) {
-    bitonic_stage<S, KS, KS / 2>(key, idx, lane);
-    if constexpr (KS < 64 * S) bitonic_sort<S, 2 * KS>(key, idx, lane);
+template <int W, int S, int KS = 2>
+__device__ __forceinline__ void bsort(uint64_t (&v)[S], int gl) {
+    bsort_stage<W, S, KS, KS / 2>(v, gl);
+    if constexpr (KS < W * S) bsort<W, S, 2 * KS>(v, gl);
 }
 
 // The kept prefix of query c's full-K conditional (above): slots
@@ -765,12 +773,16 @@ __device__ __forceinline__ int build_full_wave_s(const float* gp, int Kp, int K,
     int lastIdx = K;   // the reference leaves it uninitialised if never reached
     if (!__any(nan_seen)) {
         uint32_t key[S], idx[S];
+        {
+            uint64_t v[S];
 #pragma unroll
-        for (int i = 0; i < S; ++i) {
-            key[i] = __builtin_signbit(wr[i]) ? 0u : __builtin_bit_cast(uint32_t, wr[i]) + 1u;
-            idx[i] = (uint32_t)(lane + 64 * i);
+            for (int i = 0; i < S; ++i)
+                v[i] = sel_key(__builtin_signbit(wr[i]) ? 0u : __builtin_bit_cast(uint32_t, wr[i]) + 1u,
+                               (uint32_t)(lane + 64 * i));
+            bsort<64, S>(v, lane);
+#pragma unroll
+            for (int i = 0; i < S; ++i) { key[i] = sel_wkey(v[i]); idx[i] = sel_idx(v[i]); }
         }
-        bitonic_sort<S>(key, idx, lane);
         // sorted element p = 64 i + lane: its slot record, written by its own
         // lane, and its term of the kept mass (0 for an invalid conditional)
         int n_live = 0;   // entries with a weight (sorted first)
@@ -1033,47 +1045,6 @@ __device__ __forceinline__ float gseq_sum(float acc, const float (&x)[S], int n)
     }
     return acc;
 }
-// one compare-exchange stage of the group's bitonic network (elements
-// e = 16 i + gl; cross-lane partners inside the row of 16 by DPP)
-template <int S, int KS, int J>
-__device__ __forceinline__ void gbitonic_step(uint32_t (&key)[S], uint32_t (&idx)[S], int gl) {
-    if constexpr (J >= 16) {
-        constexpr int JJ = J / 16;
-#pragma unroll
-        for (int i = 0; i < S; ++i) {
-            if (i & JJ) continue;
-            const int i2 = i | JJ;
-            const bool up = ((16 * i) & KS) == 0;   // lanes do not reach bit KS >= 32
-            const bool b = sel_before(key[i], idx[i], key[i2], idx[i2]);
-            const bool sw = up ? !b : b;
-            const uint32_t k0 = key[i], x0 = idx[i];
-            key[i] = sw ? key[i2] : k0; idx[i] = sw ? idx[i2] : x0;
-            key[i2] = sw ? k0 : key[i2]; idx[i2] = sw ? x0 : idx[i2];
-        }
-    } else {
-        const bool lower = (gl & J) == 0;
-#pragma unroll
-        for (int i = 0; i < S; ++i) {
-            const uint32_t ok = xor_lane_u<J>(key[i]), oi = xor_lane_u<J>(idx[i]);
-            const bool up = ((16 * i + gl) & KS) == 0;
-            const bool b = sel_before(key[i], idx[i], ok, oi);
-            const bool keep = (lower == up) ? b : !b;
-            key[i] = keep ? key[i] : ok;
-            idx[i] = keep ? idx[i] : oi;
-        }
-    }
-}
-template <int S, int KS, int J>
-__device__ __forceinline__ void gbitonic_stage(uint32_t (&key)[S], uint32_t (&idx)[S], int gl) {
-    gbitonic_step<S, KS, J>(key, idx, gl);
-    if constexpr (J > 1) gbitonic_stage<S, KS, J / 2>(key, idx, gl);
-}
-template <int S, int KS = 2>
-__device__ __forceinline__ void gbitonic_sort(uint32_t (&key)[S], uint32_t (&idx)[S], int gl) {
-    gbitonic_stage<S, KS, KS / 2>(key, idx, gl);
-    if constexpr (KS < 16 * S) gbitonic_sort<S, 2 * KS>(key, idx, gl);
-}
-
 // One full-K query on this lane's group; false: a NaN weight (the caller
 // hands the query to the one-wave kernel).  Outputs written by group lane 0.
 template <bool PDF_ONLY, int S>
@@ -1101,12 +1072,16 @@ __device__ __forceinline__ bool serve_full_group(const float* gp, int Kp, int K,
     const float cutoff = (float)(0.99 * (double)total);
     // the selection order: (weight desc, index asc), absent entries last
     uint32_t key[S], idx[S];
+    {
+        uint64_t v[S];
 #pragma unroll
-    for (int i = 0; i < S; ++i) {
-        key[i] = __builtin_signbit(wr[i]) ? 0u : __builtin_bit_cast(uint32_t, wr[i]) + 1u;
-        idx[i] = (uint32_t)(16 * i + gl);
+        for (int i = 0; i < S; ++i)
+            v[i] = sel_key(__builtin_signbit(wr[i]) ? 0u : __builtin_bit_cast(uint32_t, wr[i]) + 1u,
+                           (uint32_t)(16 * i + gl));
+        bsort<16, S>(v, gl);
+#pragma unroll
+        for (int i = 0; i < S; ++i) { key[i] = sel_wkey(v[i]); idx[i] = sel_idx(v[i]); }
     }
-    gbitonic_sort<S>(key, idx, gl);
     int n_live = 0;
     float w[S];
     bool ok[S];
