@@ -1724,7 +1724,8 @@ guide_product_cand_kernel(const float* __restrict__ gp, int Kp, int K, const flo
     const int64_t q = perm ? (int64_t)perm[t] : t;
     const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
     float accum = 0.0f;
-    const int lastIdx = build_candidates(gp, Kp, K, c, cw, ck, 64, tid, gc.norm3, cap, accum);
+    // (the register list: K = 512 x 8 lobes 10.81 -> 10.61 ms per 2^18 queries)
+    const int lastIdx = build_candidates_reg<LCAP>(gp, Kp, K, c, cw, ck, 64, tid, gc.norm3, cap, accum);
     if (lastIdx < 0) {
         fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
         return;
