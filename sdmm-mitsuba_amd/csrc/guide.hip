@@ -1946,7 +1946,7 @@ __device__ void product_tail_wave(const float* gp, int Kp, const float* condCov,
 // The product path's full-K queries (listed by guide_product_cand_kernel):
 // one wave per query, grid-stride.
 #ifndef SDMM_PRODUCT_WPE
-#define SDMM_PRODUCT_WPE 2   // waves per SIMD the register budget is sized for (A/B knob)
+#define SDMM_PRODUCT_WPE 3   // waves per SIMD the register budget is sized for (A/B: 2: 10.57, 3: 9.93, 4 (spills): 13.4 ms)
 #endif
 template <bool PDF_ONLY>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDMM_PRODUCT_WPE)))
@@ -2254,7 +2254,7 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
     if (e != hipSuccess) return e;
     // the full-K queries' product pairs (up to kProductPairCap per query) live in a
     // stream-ordered scratch for the call: one slice per workgroup
-    const unsigned fblocks = (unsigned)(cus * 8);
+    const unsigned fblocks = (unsigned)(cus * 4 * SDMM_PRODUCT_WPE);
     float* pscratch = nullptr;
     const size_t sbytes = sizeof(float) * kPcStride * (size_t)kProductPairCap * fblocks;
     if (hipMallocAsync((void**)&pscratch, sbytes, st) != hipSuccess) {
