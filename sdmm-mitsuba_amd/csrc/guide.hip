@@ -1201,8 +1201,11 @@ __device__ __forceinline__ bool serve_full_group(const float* gp, int Kp, int K,
 // The listed full-K queries, a 16-lane group each (grid-stride over groups);
 // TREE: each against its own leaf's mixture.  NaN queries -> fb2 (count at
 // fb2[0], list from fb2 + 1) for the one-wave kernel.
+#ifndef SDMM_GROUP_WPE
+#define SDMM_GROUP_WPE 4   // 128 VGPRs, no spill; K=128 guided pass 17.6 -> 15.2 ms (2: 189 VGPRs, 2 waves per SIMD)
+#endif
 template <bool PDF_ONLY, bool TREE, int S>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDMM_GROUP_WPE)))
 guide_group_fallback_kernel(const float* __restrict__ gp1, int Kp1, int K1, const STNodeDev* __restrict__ nodes,
                             const GuideMix* __restrict__ tab, GuideIO io, GuideConsts gc,
                             const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list,
