@@ -2452,7 +2452,10 @@ int st_guide(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const f
     const GuideSortScratch* sort = nq >= (1 << 14) ? &t->guide_sort : nullptr;
     HIP_TRY(launch_guide_tree(t->dnodes, t->dtab, t->tab_kmax, nq, c, u, dgiven, d, pdf, comp, node_out,
                               norm_const(2), norm_const(3), kGuideCapMax, t->guide_fb, t->guide_fb + 1,
-                              cus > 0 ? cus : 256, t->stream, sort, pmode, (int*)t->guide_sort.keys[0]));
+                              cus > 0 ? cus : 256, t->stream, sort, pmode,
+                              // the NaN hand-off list of the group fallback: the
+                              // Morton keys' input buffer, free once the order is built
+                              (int*)t->guide_sort.keys[0]));
     return SDMM_OK;
 }
 
