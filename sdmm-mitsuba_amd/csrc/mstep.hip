@@ -468,13 +468,20 @@ __device__ __forceinline__ void mstep_component(int k, int K, const double* __re
     for (int i = 0; i < 25; ++i) S.sgC[25 * k + i] = gC[i];
 }
 
-__device__ __forceinline__ void mstep_finish(int K, const CanonDev& C, const EmStateDev& S, double* newW) {
+// Thread 0, on LDS: the fp64 weight normalisation, the float weights and
+// createCdf (weights_cdf, the same float operations in the same order) --
+// wl (K floats) and cl (K floats, over newW once it has been read) are LDS, so
+// the serial loops do not wait on a global round trip per element (they did:
+// C.weights / C.cdf may alias, so no load could be hoisted; ~60 of the 73 us
+// of a K = 128 M-step).  The caller copies wl / cl out in parallel.
+__device__ __forceinline__ void mstep_finish(int K, const EmStateDev& S, double* newW, float* wl) {
     double sum = 0.0;
     for (int k = 0; k < K; ++k) sum += newW[k];
     if (sum != 0.0)
         for (int k = 0; k < K; ++k) newW[k] = newW[k] / sum;
-    for (int k = 0; k < K; ++k) C.weights[k] = (float)newW[k];
-    weights_cdf(C.weights, C.cdf, K, true);
+    for (int k = 0; k < K; ++k) wl[k] = (float)newW[k];
+    float* cl = (float*)newW;   // newW is fully consumed above
+    weights_cdf(wl, cl, K, true);
     S.scalars[SC_IT] = S.scalars[SC_IT] + 1.0;
 }
 
@@ -494,7 +501,13 @@ __device__ __forceinline__ void mstep_body(int K, int Kp, const double* __restri
     for (int k = t; k < K; k += blockDim.x)
         if (setk[k]) set_component(k, wmean + 6 * k, wcov + 25 * k, C);
     __syncthreads();
-    if (t == 0) mstep_finish(K, C, S, newW);
+    float* wl = (float*)setk;   // setk is consumed by the loop above
+    if (t == 0) mstep_finish(K, S, newW, wl);
+    __syncthreads();
+    for (int k = t; k < K; k += blockDim.x) {
+        C.weights[k] = wl[k];
+        C.cdf[k] = ((const float*)newW)[k];
+    }
     __syncthreads();
     for (int kk = t; kk < Kp; kk += blockDim.x) pack_component(kk, K, Kp, C, ep, gp, norm5);
 }
