@@ -781,7 +781,7 @@ estep_stats_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, in
         const float thr = nm.fin ? 1e-10f : __builtin_inff();
         // Spatial statistics are accumulated centred on the component's mean
         // position (tp = p - mu_k) and un-centred in fp64 by
-        // finalize_stats_kernel: the M-step's C/W - mu mu^T then does not
+        // uncenter_stats_kernel: the M-step's C/W - mu mu^T then does not
         // amplify fp32 accumulation error by |p|^2 / sigma^2.
 #pragma unroll
         for (int c = 0; c < NP; ++c) {
@@ -1148,7 +1148,7 @@ estep_stats_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
 // vector [H, wsum, W(K), M(5K), Clow(15K)], in two launches so the whole chip
 // takes part: stage 1 = (64-column block) x (row slice) workgroups, each
 // summing its slice in a fixed order into slice[s][col]; stage 2 (inside
-// finalize_stats_kernel) sums the kReduceSlices slices of each column in order.
+// sum_slices_kernel) sums the kReduceSlices slices of each column in order.
 constexpr int kReduceSlices = 16;
 
 __device__ __forceinline__ int partial_col(int o, int Kp, int K) {
@@ -1188,25 +1188,30 @@ reduce_partials_slices_kernel(const float* __restrict__ partials, int rows, int 
 // statistics (fp64):
 //   M_p = M'_p + W mu,  C_pp = C'_pp + M'_p mu^T + mu M'_p^T + W mu mu^T,
 //   C_tp = C'_tp + M_t mu^T   (mu = the float mean the E-step subtracted).
-__global__ void finalize_stats_kernel(const float* __restrict__ ep, int Kp, int K,
-                                      const double* __restrict__ slices, double* __restrict__ stats) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    const int ncols = 2 + ST_FIELDS * K;
-    // stage 2 of the reduction: the slices of each column, in slice order
-    auto col = [&](int o) {
-        double t = 0.0;
+// Stage 2 of the reduction, one thread per stats column (coalesced): the
+// slices of column o summed in slice order, into stats[o].
+__global__ void __launch_bounds__(256)
+sum_slices_kernel(int ncols, const double* __restrict__ slices, double* __restrict__ stats) {
+    const int o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= ncols) return;
+    double t = 0.0;
 #pragma unroll
-        for (int sl = 0; sl < kReduceSlices; ++sl) t += slices[(int64_t)sl * ncols + o];
-        return t;
-    };
-    if (k == 0) { stats[0] = col(0); stats[1] = col(1); }
+    for (int sl = 0; sl < kReduceSlices; ++sl) t += slices[(int64_t)sl * ncols + o];
+    stats[o] = t;
+}
+// Then one thread per component un-centres its own columns in place (the
+// statistics were accumulated about mu_k).  Together: the former one-thread-
+// per-component kernel operation for operation (bitwise), which read its 21 x
+// 16 strided values on 128 threads (19 us of a 0.4 ms K = 128 EM step).
+__global__ void uncenter_stats_kernel(const float* __restrict__ ep, int Kp, int K, double* __restrict__ stats) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= K) return;
     const double mu[3] = {(double)ep[EP_MU0 * Kp + k], (double)ep[EP_MU1 * Kp + k],
                           (double)ep[EP_MU2 * Kp + k]};
-    const double w = col(2 + k);
+    const double w = stats[2 + k];
     double M[5], C[15];   // C: lower triangle, row-major
-    for (int i = 0; i < 5; ++i) M[i] = col(2 + K + 5 * k + i);
-    for (int i = 0; i < 15; ++i) C[i] = col(2 + 6 * K + 15 * k + i);
+    for (int i = 0; i < 5; ++i) M[i] = stats[2 + K + 5 * k + i];
+    for (int i = 0; i < 15; ++i) C[i] = stats[2 + 6 * K + 15 * k + i];
     // C_pp (entries 0..5: (0,0) (1,0) (1,1) (2,0) (2,1) (2,2))
     int e = 0;
     for (int i = 0; i < 3; ++i)
@@ -1218,7 +1223,6 @@ __global__ void finalize_stats_kernel(const float* __restrict__ ep, int Kp, int 
         C[10 + j] += M[4] * mu[j];
     }
     for (int i = 0; i < 3; ++i) M[i] = M[i] + w * mu[i];
-    stats[2 + k] = w;
     for (int i = 0; i < 5; ++i) stats[2 + K + 5 * k + i] = M[i];
     for (int i = 0; i < 15; ++i) stats[2 + 6 * K + 15 * k + i] = C[i];
 }
@@ -1226,7 +1230,7 @@ __global__ void finalize_stats_kernel(const float* __restrict__ ep, int Kp, int 
 // Batched reduction + finalisation: thread (leaf blockIdx.y, component k)
 // reproduces, operation for operation, reduce_partials_slices_kernel (slices
 // of the leaf's rows, four row-interleaved fp64 partials per slice combined as
-// ((b0 + b1) + b2) + b3) followed by finalize_stats_kernel (slices summed in
+// ((b0 + b1) + b2) + b3) followed by sum_slices_kernel + uncenter_stats_kernel (slices summed in
 // order, then the un-centring), so a batched leaf's stats are bitwise those of
 // its single-mixture E-step.
 __device__ __forceinline__ double batched_col(const float* __restrict__ partials, int pstride, int row0, int rows,
@@ -1251,7 +1255,7 @@ __device__ __forceinline__ double batched_col(const float* __restrict__ partials
 // reduced exactly as batched_col / the single-mixture path orders it (16 row
 // slices, four row-interleaved fp64 sums per slice combined as
 // ((b0 + b1) + b2) + b3, slices summed in order) into LDS.  Phase 2: the
-// un-centring of the spatial moments per component, as finalize_stats_kernel.
+// un-centring of the spatial moments per component, as uncenter_stats_kernel.
 // Bitwise equal to the previous thread-per-component form, with 21x more
 // threads in flight (it was latency-bound: 16 busy lanes per leaf): 257 ->
 // ~50 us per 256-leaf K=16 step (a (column, slice) split measured no faster).
@@ -1450,8 +1454,10 @@ hipError_t launch_reduce_partials(const float* partials, int rows, int pstride, 
                        partials, rows, pstride, Kp, K, scratch);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(finalize_stats_kernel, dim3((K + 63) / 64), dim3(64), 0, st, ep_for_finalize, Kp, K,
-                       scratch, stats);
+    hipLaunchKernelGGL(sum_slices_kernel, dim3((ncols + 255) / 256), dim3(256), 0, st, ncols, scratch, stats);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(uncenter_stats_kernel, dim3((K + 63) / 64), dim3(64), 0, st, ep_for_finalize, Kp, K, stats);
     return hipGetLastError();
 }
 
