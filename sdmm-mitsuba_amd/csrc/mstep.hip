@@ -472,8 +472,8 @@ __device__ __forceinline__ void mstep_component(int k, int K, const double* __re
 // createCdf (weights_cdf, the same float operations in the same order) --
 // wl (K floats) and cl (K floats, over newW once it has been read) are LDS, so
 // the serial loops do not wait on a global round trip per element (they did:
-// C.weights / C.cdf may alias, so no load could be hoisted; ~60 of the 73 us
-// of a K = 128 M-step went there: 73 -> 40 us).  The caller copies wl / cl out in parallel.
+// C.weights / C.cdf may alias, so no load could be hoisted: a K = 128 M-step
+// 73 -> 40 us).  The caller copies wl / cl out in parallel.
 __device__ __forceinline__ void mstep_finish(int K, const EmStateDev& S, double* newW, float* wl) {
     double sum = 0.0;
     for (int k = 0; k < K; ++k) sum += newW[k];
