@@ -468,21 +468,74 @@ __device__ __forceinline__ void mstep_component(int k, int K, const double* __re
     for (int i = 0; i < 25; ++i) S.sgC[25 * k + i] = gC[i];
 }
 
-// Thread 0, on LDS: the fp64 weight normalisation, the float weights and
-// createCdf (weights_cdf, the same float operations in the same order) --
-// wl (K floats) and cl (K floats, over newW once it has been read) are LDS, so
-// the serial loops do not wait on a global round trip per element (they did:
-// C.weights / C.cdf may alias, so no load could be hoisted: a K = 128 M-step
-// 73 -> 40 us).  The caller copies wl / cl out in parallel.
-__device__ __forceinline__ void mstep_finish(int K, const EmStateDev& S, double* newW, float* wl) {
+// Wave 0: the fp64 weight normalisation, the float weights and createCdf
+// (weights_cdf's float operations, in its order) with every sequential sum a
+// chain of v_readlane broadcasts and adds over registers -- lane l holds
+// components l, l + 64, ... -- and each prefix captured by the lane that owns
+// the element.  (Thread 0 alone walking C.weights / C.cdf in global memory,
+// which may alias, waited a round trip per element: a K = 128 M-step took
+// 73 us, 40 us once these loops ran on LDS; the rest is the per-component
+// fp64 work of mstep_component.)  Results in wl / cl (LDS); the caller copies
+// them out in parallel.  K <= 512.
+__device__ __forceinline__ double rl_f64(double x, int l) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+    return __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
+}
+__device__ __forceinline__ float rl_f32(float x, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
+}
+__device__ __forceinline__ void mstep_finish_wave(int K, const EmStateDev& S, const double* newW, float* wl,
+                                                  float* cl, int lane) {
+    constexpr int SL = 8;   // 512 / 64
+    double nw[SL];
+    float w[SL], cdf[SL];
+#pragma unroll
+    for (int i = 0; i < SL; ++i) nw[i] = (64 * i + lane < K) ? newW[64 * i + lane] : 0.0;
     double sum = 0.0;
-    for (int k = 0; k < K; ++k) sum += newW[k];
+#pragma unroll
+    for (int i = 0; i < SL; ++i)
+        if (64 * i < K)
+            for (int l = 0; l < 64 && 64 * i + l < K; ++l) sum += rl_f64(nw[i], l);
     if (sum != 0.0)
-        for (int k = 0; k < K; ++k) newW[k] = newW[k] / sum;
-    for (int k = 0; k < K; ++k) wl[k] = (float)newW[k];
-    float* cl = (float*)newW;   // newW is fully consumed above
-    weights_cdf(wl, cl, K, true);
-    S.scalars[SC_IT] = S.scalars[SC_IT] + 1.0;
+#pragma unroll
+        for (int i = 0; i < SL; ++i) nw[i] = nw[i] / sum;
+#pragma unroll
+    for (int i = 0; i < SL; ++i) { w[i] = (float)nw[i]; cdf[i] = 0.0f; }
+    // createCdf(false): the unnormalised prefix (kept if the sum below is 0)
+    float acc = 0.0f;
+#pragma unroll
+    for (int i = 0; i < SL; ++i)
+        if (64 * i < K)
+            for (int l = 0; l < 64 && 64 * i + l < K; ++l) {
+                acc += rl_f32(w[i], l);
+                cdf[i] = (lane == l) ? acc : cdf[i];
+            }
+    float fs = 0.0f;
+#pragma unroll
+    for (int i = 0; i < SL; ++i)
+        if (64 * i < K)
+            for (int l = 0; l < 64 && 64 * i + l < K; ++l) fs += rl_f32(w[i], l);
+    if (fs != 0.0f) {
+#pragma unroll
+        for (int i = 0; i < SL; ++i) w[i] = w[i] / fs;
+        acc = 0.0f;
+#pragma unroll
+        for (int i = 0; i < SL; ++i)
+            if (64 * i < K)
+                for (int l = 0; l < 64 && 64 * i + l < K; ++l) {
+                    acc += rl_f32(w[i], l);
+                    cdf[i] = (lane == l) ? acc : cdf[i];
+                }
+    }
+#pragma unroll
+    for (int i = 0; i < SL; ++i)
+        if (64 * i + lane < K) {
+            wl[64 * i + lane] = w[i];
+            cl[64 * i + lane] = cdf[i];
+        }
+    if (lane == 0) S.scalars[SC_IT] = S.scalars[SC_IT] + 1.0;
 }
 
 // The four phases in one workgroup (the batched per-leaf M-step).
@@ -501,12 +554,14 @@ __device__ __forceinline__ void mstep_body(int K, int Kp, const double* __restri
     for (int k = t; k < K; k += blockDim.x)
         if (setk[k]) set_component(k, wmean + 6 * k, wcov + 25 * k, C);
     __syncthreads();
-    float* wl = (float*)setk;   // setk is consumed by the loop above
-    if (t == 0) mstep_finish(K, S, newW, wl);
+    // dynamic LDS: newW (8K bytes), setk (4K) -- reused as wl --, cl (4K)
+    float* wl = (float*)setk;
+    float* cl = wl + K;
+    if (t < 64) mstep_finish_wave(K, S, newW, wl, cl, t);
     __syncthreads();
     for (int k = t; k < K; k += blockDim.x) {
         C.weights[k] = wl[k];
-        C.cdf[k] = ((const float*)newW)[k];
+        C.cdf[k] = cl[k];
     }
     __syncthreads();
     for (int kk = t; kk < Kp; kk += blockDim.x) pack_component(kk, K, Kp, C, ep, gp, norm5);
@@ -690,7 +745,7 @@ hipError_t launch_mstep(int K, int Kp, const double* stats, int64_t nSamples, co
     // chip in separate launches (K = 128: 0.41 vs 0.46 ms per EM step; K = 512:
     // 1.49 vs 1.62 ms) -- the M-step is launch/latency bound, not throughput bound.
     const int threads = Kp < 64 ? 64 : (Kp > 512 ? 512 : Kp);
-    hipLaunchKernelGGL(mstep_single_kernel, dim3(1), dim3(threads), (sizeof(double) + sizeof(int)) * (size_t)K,
+    hipLaunchKernelGGL(mstep_single_kernel, dim3(1), dim3(threads), (sizeof(double) + sizeof(int) + sizeof(float)) * (size_t)K,
                        st, K, Kp, stats, nSamples, C, S, ep, gp, norm5, wmean, wcov);
     return hipGetLastError();
 }
@@ -698,7 +753,7 @@ hipError_t launch_mstep(int K, int Kp, const double* stats, int64_t nSamples, co
 hipError_t launch_mstep_batched(int K, int Kp, const MixDesc* mixes, int n_mix, float norm5, hipStream_t st) {
     if (n_mix <= 0) return hipSuccess;
     const int threads = Kp < 64 ? 64 : (Kp > 512 ? 512 : Kp);
-    hipLaunchKernelGGL(mstep_batched_kernel, dim3(n_mix), dim3(threads), (sizeof(double) + sizeof(int)) * (size_t)K,
+    hipLaunchKernelGGL(mstep_batched_kernel, dim3(n_mix), dim3(threads), (sizeof(double) + sizeof(int) + sizeof(float)) * (size_t)K,
                        st, K, Kp, mixes, norm5);
     return hipGetLastError();
 }
