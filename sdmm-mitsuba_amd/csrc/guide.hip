@@ -1037,11 +1037,12 @@ __device__ __forceinline__ float gseq_sum(float acc, const float (&x)[S], int n)
 #pragma unroll
     for (int i = 0; i < S; ++i) {
         if (!__any(16 * i < n)) break;
+        // all 16 broadcasts in flight first, then the add chain (one wait)
+        float b[16];
 #pragma unroll
-        for (int l = 0; l < 16; ++l) {
-            const float b = gbc(x[i], l);
-            acc += (16 * i + l < n) ? b : -0.0f;
-        }
+        for (int l = 0; l < 16; ++l) b[l] = gbc(x[i], l);
+#pragma unroll
+        for (int l = 0; l < 16; ++l) acc += (16 * i + l < n) ? b[l] : -0.0f;
     }
     return acc;
 }
@@ -1100,12 +1101,14 @@ __device__ __forceinline__ bool serve_full_group(const float* gp, int Kp, int K,
     for (int i = 0; i < S; ++i) {
         if (!__any(!done && 16 * i < n_live)) break;
         const float t = ok[i] ? w[i] : 0.0f;
+        float bt[16];
+#pragma unroll
+        for (int l = 0; l < 16; ++l) bt[l] = gbc(t, l);
 #pragma unroll
         for (int l = 0; l < 16; ++l) {
-            const float b = gbc(t, l);
             const int p = 16 * i + l;
             if (!done && p < n_live) {
-                accum += b;
+                accum += bt[l];
                 if (accum >= cutoff) { lastIdx = p + 1; done = true; }
             }
         }
@@ -1138,9 +1141,12 @@ __device__ __forceinline__ bool serve_full_group(const float* gp, int Kp, int K,
 #pragma unroll
             for (int i = 0; i < S; ++i) {
                 if (!__any(slot < 0 && 16 * i < lastIdx)) break;
+                float bf[16];
+#pragma unroll
+                for (int l = 0; l < 16; ++l) bf[l] = gbc(f[i], l);
 #pragma unroll
                 for (int l = 0; l < 16; ++l) {
-                    const float b = gbc(f[i], l);
+                    const float b = bf[l];
                     const int p = 16 * i + l;
                     if (slot < 0 && p < lastIdx) {
                         cdf += b;
