@@ -8,13 +8,14 @@ synthetic batch of N = 2^20 samples against a K = 128 mixture that has been
 through 5 warm EM iterations.  Inputs (SoA fp32 planes) are resident in HBM
 before timing; the N x K fp32 responsibilities are written to HBM.
 
-Multi-GPU (torchrun, one process per GPU): weak scaling -- every rank holds
-its own N = 2^20 samples of one global batch of N x world (independent parts
-of the same synthetic distribution; rank 0's is the single-GPU batch), no
-data-path collective for the E-step; EM steps go through the library's own
-RCCL communicator (sdmm_comm_init_rccl, sdmm_em_step_sharded: the fp64
-sufficient statistics of the global batch are all-reduced over xGMI before
-each M-step).  value = N x world / max-over-ranks step time.
+Multi-GPU (torchrun, one process per GPU): STRONG scaling (north_star, SURVEY
+7/8e) -- the fixed N = 2^20 batch is sharded N/world contiguous samples per
+rank (SURVEY 8e partitioning), no data-path collective for the E-step; EM
+steps go through the library's own RCCL communicator (sdmm_comm_init_rccl,
+sdmm_em_step_sharded: the fp64 sufficient statistics of the shards are
+all-reduced over xGMI before each M-step).  value = N / max-over-ranks step
+time.  An extra `weak` line times every rank on its own full N = 2^20 part of
+an N x world batch.
 
 Also reported (same JSON line): the full EM step (E-step + statistics +
 all-reduce + M-step), guided queries/sec (conditional + sample + pdf, Q = 2^20,
@@ -355,25 +356,20 @@ def main():
     synth = importlib.import_module("sdmm_mitsuba_amd.synth")
     K, N = args.K, args.N
 
-    # weak scaling (the samples partition over ranks): every rank
-    # holds its own N samples of one global batch of N x world (rank 0's share
-    # is the single-GPU batch); the E-step needs no exchange, the EM step
-    # all-reduces the statistics of the global batch
+    # strong scaling (the samples partition over ranks): every rank
+    # builds the same N-sample batch (deterministic seeds) and owns the
+    # contiguous shard [rank N/world, (rank+1) N/world); the E-step needs no
+    # exchange, the EM step all-reduces the shards' statistics.  The model is
+    # the same on every rank (the batch's own first samples seed it).
     t0 = time.perf_counter()
-    batch = synth.em_batch(N, 128, part=rank)
+    batch = synth.em_batch(N, 128)
     pos, nrm = synth.model_seed_points(batch, K)
-    if world > 1:   # one model for all ranks: rank 0's seed points
-        pn = torch.from_numpy(np.concatenate([pos, nrm]).astype(np.float32))
-        pn = pn.to(dev) if not rehearse else pn
-        dist.broadcast(pn, 0)
-        pn = pn.cpu().numpy()
-        pos, nrm = pn[:len(pos)], pn[len(pos):]
     log(f"[bench] rank {rank}/{world}: synthetic batch N={N} in {time.perf_counter() - t0:.1f}s")
     full = pkg.DeviceSamples.from_numpy(batch["x"], batch["w"], batch["hpdf"], batch["is_diffuse"],
                                         device=dev)
-    shard = full
+    shard = full.shard(rank, world) if world > 1 else full
     n_local = shard.n
-    N_global = N * world
+    N_global = N
 
     stream = torch.cuda.current_stream(dev)
     mix = pkg.SDMM(K, device=dev.index, stream=stream)
@@ -396,7 +392,7 @@ def main():
         em_step()
     torch.cuda.synchronize()
 
-    resp = torch.empty((n_local, K), dtype=torch.float32, device=dev)
+    resp = torch.empty((max(n_local, full.n if world > 1 else 0), K), dtype=torch.float32, device=dev)
 
     def estep():
         mix.posterior(shard, resp)
@@ -453,14 +449,15 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (BASELINE.md 2: 2^20 samples from a K=128 uniformHemisphereInit "
                 "generator, LogNormal weights with 0.1% zero / 0.01% non-finite; model after 5 EM steps)",
         "config": {"workload": "responsibility E-step, synthetic 5D sample batch (configs[1])",
                    "K": K, "N": N_global, "global_batch": N_global, "samples_per_gpu": n_local,
-                   "parallelism": f"sample-sharded x{world}", "layout": "SoA fp32 in, [N][K] fp32 out"},
+                   "parallelism": f"sample-sharded x{world} (strong: N fixed)",
+                   "layout": "SoA fp32 in, [N][K] fp32 out"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK, "traffic": None,
                      "kernel": mix.kernel_name("resp"),
@@ -489,6 +486,18 @@ def main():
         em_steps = max(5, args.steps // 2)
         out["em_step"] = {"samples_per_s": N_global / (em_wall / em_steps),
                           "ms_per_step": em_wall / em_steps * 1e3}
+        # ---- weak scaling (extra line): every rank its own full N-sample
+        # part of an N x world batch (part 0 = the single-GPU batch) ----
+        if world > 1:
+            wb = synth.em_batch(N, 128, part=rank)
+            wfull = pkg.DeviceSamples.from_numpy(wb["x"], wb["w"], wb["hpdf"], wb["is_diffuse"], device=dev)
+            for _ in range(args.warmup):
+                mix.posterior(wfull, resp)
+            ww, wk = timed(lambda: mix.posterior(wfull, resp), args.steps)
+            out["weak"] = {"metric": out["metric"], "samples_per_s": N * world / (ww / args.steps),
+                           "ms_per_step": ww / args.steps * 1e3, "kernel_us": wk * 1e6,
+                           "N": N * world, "samples_per_gpu": N, "scaling": "weak"}
+            del wfull, wb
         # ---- fused stats kernel alone (per rank) ----
         st_wall, st_kern = timed(lambda: mix.estep_stats(shard, stats), args.steps)
         out["estep_stats"] = {"ms_per_step": st_wall / args.steps * 1e3,

@@ -1,9 +1,12 @@
 /*
- * volpath_sdmm_amd.cpp -- the SDMM volumetric path tracer integrator for
- * Mitsuba 0.6 with its guiding model on an MI355X through the C ABI of
- * include/sdmm_gpu.h.  A maintainer drops this file in place of
- * mitsuba/src/integrators/sdmm/volpath_sdmm.cpp (plus sdmm_proc.{h,cpp},
- * whose roles it takes over) and links libsdmm_amd.so.
+ * volpath_sdmm_amd.cpp -- the `sdmm` integrator plugin (the SDMM volumetric
+ * path tracer of Mitsuba 0.6) with its guiding model on an MI355X through the
+ * C ABI of include/sdmm_gpu.h.  It builds as the plugin named `sdmm` -- the
+ * SharedLibrary('sdmm', ...) entry of mitsuba/src/integrators/SConscript:44-55,
+ * with this one source in place of volpath_sdmm.cpp + sdmm_proc.cpp +
+ * sdmm_wr.cpp + sdmm_wu.cpp -- so scenes that say <integrator type="sdmm">
+ * (test-suite/scenes/_integrators/sdmm.xml:14) load it unchanged; it links
+ * libsdmm_amd.so.
  *
  * NOT COMPILED in this repository: Mitsuba 0.6 and its dependencies are not in
  * the image.  Every guiding call below is exercised by the tests through the
@@ -20,8 +23,14 @@
  *     (SDMMProcess::develop, sdmm_proc.cpp:1142-1158);
  *   - Li (sdmm_proc.cpp:592-871): no NEE, BSDF / guide mixing with
  *     heuristicConditionalWeight 0.5 (:383-392), pdf = h bsdfPdf + (1-h)
- *     gmmPdf (:587-589), saved vertices with clamped pdf (:815-846),
- *     recordRadiance (:615-637), Russian roulette after rrDepth (:858-868).
+ *     gmmPdf (:587-589), saved vertices with clamped pdf only for non-delta
+ *     samples (`cacheable`, :764, :821-846) with the normal flipped to the
+ *     wi side (:765-767), recordRadiance (:615-637), Russian roulette after
+ *     rrDepth with q = min(max(throughput) eta^2, 0.95) (:788, :858-868);
+ *   - bsdfOnly: no training (:416), so no leaf ever holds an initialised
+ *     context and every bounce takes the BSDF-only branch (:316-323); the
+ *     learned-BSDF-only branch (:331, :384, :410-413) is unreachable in the
+ *     reference for the same reason and is not reproduced.
  * What changes:
  *   - the guiding state (tree, per-leaf SDMM + EM, training data, optimize)
  *     lives on the GPU: one sdmm_guiding handle;
@@ -125,6 +134,8 @@ struct PathState {
     Spectrum bsdfWeight;
     Float bsdfPdf;
     bool pdfMode;        // the BSDF was chosen (rnd <= h)
+    bool cacheable;      // !(bRec.sampledType & EDelta): the vertex is saved (:764)
+    Float eta;           // relative IOR along the path (:604, :788)
 };
 
 }  // namespace
@@ -356,6 +367,7 @@ private:
             s.Li = Spectrum(0.0f);
             s.depth = -1;
             s.query = -1;
+            s.eta = 1.0f;
             if (scene->rayIntersect(s.ray, s.its)) {
                 if (s.its.isEmitter()) s.Li += s.throughput * s.its.Le(-s.ray.d);
                 s.depth = 1;
@@ -377,7 +389,8 @@ private:
                 brecs[(size_t)p].reset(new BSDFSamplingRecord(s.its, sampler, ERadiance));
                 BSDFSamplingRecord& bRec = *brecs[(size_t)p];
                 s.bsdfWeight = bsdf->sample(bRec, s.bsdfPdf, sampler->next2D());
-                const bool smooth = (bsdf->getType() & BSDF::ESmooth) && !(bRec.sampledType & BSDF::EDelta);
+                s.cacheable = !(bRec.sampledType & BSDF::EDelta);
+                const bool smooth = (bsdf->getType() & BSDF::ESmooth) && s.cacheable;
                 ++live;
                 if (!guided || !smooth) continue;
                 const Float choice = sampler->next1D();
@@ -426,9 +439,11 @@ private:
                     continue;
                 }
                 s.throughput *= weight;
+                s.eta *= bRec.eta;                     // (:788)
                 // trace and look for an emitter (no NEE: MIS weight 1, :803-819)
                 const Point o = s.its.p;
-                const Normal n_s = s.its.shFrame.n;
+                // the vertex normal on the wi side (:650-651, :765-767)
+                const Normal n_s = Frame::cosTheta(bRec.wi) < 0 ? Normal(-s.its.shFrame.n) : s.its.shFrame.n;
                 const Point cnd((o - m_sceneMin) / m_spatialNorm);
                 s.ray = RayDifferential(o, wo, s.ray.time);
                 Spectrum value(0.0f);
@@ -444,7 +459,7 @@ private:
                     s.Li += rad;
                     recordRadiance(st, p, n, k, rad);
                 }
-                if (k < V) {                            // the saved vertex (:821-846)
+                if (s.cacheable && k < V) {             // the saved vertex: non-delta samples only (:764, :821-846)
                     const Float clamped = std::max(pdf, (Float)0.1f);
                     Float rgb[3], thr[3];
                     value.toLinearRGB(rgb[0], rgb[1], rgb[2]);
@@ -464,7 +479,7 @@ private:
                 }
                 if (!hit) { s.depth = -1; continue; }
                 if (s.depth >= m_rrDepth) {             // Russian roulette (:858-868)
-                    const Float qq = std::min(s.throughput.max(), (Float)0.95f);
+                    const Float qq = std::min(s.throughput.max() * s.eta * s.eta, (Float)0.95f);
                     if (sampler->next1D() >= qq) { s.depth = -1; continue; }
                     s.throughput /= qq;
                 }

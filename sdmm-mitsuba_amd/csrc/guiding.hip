@@ -31,6 +31,7 @@
 #include <cmath>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -169,6 +170,7 @@ struct Pool {
 
 struct sdmm_guiding {
     int device = 0;
+    bool pool_held = false;     // raised the default pool's release threshold (pool_hold)
     sdmm_guiding_config cfg{};
     sdmm_stree* tree = nullptr;
     hipStream_t st = nullptr;
@@ -402,6 +404,39 @@ int update(sdmm_guiding* g) {
     return bind(g);
 }
 
+// The default pool's release threshold, raised while any guiding model on
+// the device lives and restored afterwards (it is shared with every other
+// stream-ordered allocation of the host process).
+struct PoolHold {
+    int users = 0;
+    uint64_t saved = 0;
+    bool have_saved = false;
+};
+std::mutex g_pool_mu;
+PoolHold g_pool_hold[64];
+
+void pool_hold(int device) {
+    if (device < 0 || device >= 64) return;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    PoolHold& h = g_pool_hold[device];
+    if (h.users++ > 0) return;
+    hipMemPool_t pool = nullptr;
+    if (hipDeviceGetDefaultMemPool(&pool, device) != hipSuccess || !pool) return;
+    h.have_saved = hipMemPoolGetAttribute(pool, hipMemPoolAttrReleaseThreshold, &h.saved) == hipSuccess;
+    uint64_t keep = UINT64_MAX;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+}
+
+void pool_release(int device) {
+    if (device < 0 || device >= 64) return;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    PoolHold& h = g_pool_hold[device];
+    if (h.users == 0 || --h.users > 0) return;
+    hipMemPool_t pool = nullptr;
+    if (!h.have_saved || hipDeviceGetDefaultMemPool(&pool, device) != hipSuccess || !pool) return;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &h.saved);
+}
+
 }  // namespace
 
 extern "C" {
@@ -440,11 +475,10 @@ int sdmm_guiding_create(const float tree_min[3], const float tree_max[3], const 
         // device's default pool: keep its memory between synchronisations
         // (the default threshold returns it at every sync, so each new leaf
         // would grow the pool again)
-        hipMemPool_t pool = nullptr;
-        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess && pool) {
-            uint64_t keep = UINT64_MAX;
-            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-        }
+        // -- a process-wide setting: the first live model raises it and the
+        // last one restores the caller's value (pool_hold / pool_release)
+        pool_hold(device);
+        g->pool_held = true;
     }
     if (!r) r = sdmm_stree_set_stream(g->tree, (void*)g->st);
     g->async = cfg->optimize_async != 0;
@@ -486,6 +520,7 @@ void sdmm_guiding_destroy(sdmm_guiding* g) {
     if (g->pinned) (void)hipHostFree(g->pinned);
     if (g->st) (void)hipStreamDestroy(g->st);
     if (g->em_st) (void)hipStreamDestroy(g->em_st);
+    if (g->pool_held) pool_release(g->device);
     delete g;
 }
 

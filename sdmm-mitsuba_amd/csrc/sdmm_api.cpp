@@ -779,7 +779,12 @@ int create_many(int K, const sdmm_em_params* params, int device, hipStream_t st,
         return fail(SDMM_E_HIP, "hipMallocAsync failed");
     }
     int r = SDMM_OK;
+    // fault injection for the cleanup path's test (tests/test_gpu_batched.py):
+    // member SDMM_TEST_FAIL_MEMBER fails as if its creation had
+    const char* inject = std::getenv("SDMM_TEST_FAIL_MEMBER");
+    const int fail_at = inject ? std::atoi(inject) : -1;
     for (int i = 0; i < n && !r; ++i) {
+        if (i == fail_at) { r = fail(SDMM_E_HIP, "create_many: injected failure"); break; }
         r = create_impl(K, params, device, st, true, &out[i], (char*)slab->p + stride * (size_t)i);
         if (!r) { out[i]->slab = slab; ++slab->refs; out[i]->block_async = false; }
     }
@@ -792,8 +797,11 @@ int create_many(int K, const sdmm_em_params* params, int device, hipStream_t st,
                                   m0->S.bPriors, m0->S.bDepth, m0->C, m0->ep, m0->gp, m0->norm5, stride, st);
     }
     if (r || e != hipSuccess) {
+        // hold the slab across the members' destruction: the last member's
+        // sdmm_destroy must not free it under us (it is freed once, below)
+        ++slab->refs;
         for (int i = 0; i < n; ++i) { sdmm_destroy(out[i]); out[i] = nullptr; }
-        if (slab->refs == 0) { (void)hipFreeAsync(slab->p, st); delete slab; }
+        if (--slab->refs == 0) { (void)hipFreeAsync(slab->p, st); delete slab; }
         return r ? r : fail(SDMM_E_HIP, std::string("create_many: ") + hipGetErrorString(e));
     }
     return SDMM_OK;
@@ -810,7 +818,10 @@ void sdmm_destroy(sdmm_mix* m) {
     if (m->stream && m->stream != m->own_stream) (void)hipStreamSynchronize(m->stream);
     if (m->slab) {
         if (--m->slab->refs == 0) {
-            (void)hipFreeAsync(m->slab->p, m->slab->st);
+            // on the destroying handle's current stream (synchronised above):
+            // the slab's creation stream may be gone by now, or no longer be
+            // any member's stream after sdmm_set_stream
+            (void)hipFreeAsync(m->slab->p, m->stream);
             delete m->slab;
         }
     } else if (m->block) {

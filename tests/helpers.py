@@ -18,9 +18,11 @@ def _pdf_ftz(q, di, a, w):
     return _ftz(w * p2)
 
 
-def posterior_f64(mix_params: dict, x: np.ndarray) -> np.ndarray:
+def posterior_f64(mix_params: dict, x: np.ndarray, hpdf=None, is_diffuse=None, h=0.5) -> np.ndarray:
     """posteriorAndLog (mixture_model.h:146-192) in float64 from the float
-    mixture parameters: the 'exact' reference both fp32 paths are judged by."""
+    mixture parameters: the 'exact' reference both fp32 paths are judged by.
+    With is_diffuse: the heuristic mix S' = (1-h) S + h hpdf on those rows,
+    gamma_k = (1-h) q_k / S' (:170-181)."""
     w = np.asarray(mix_params["weights"], np.float64)
     mean = np.asarray(mix_params["mean"], np.float64).reshape(-1, 6)
     to = np.asarray(mix_params["to"], np.float64).reshape(-1, 3, 3)
@@ -41,9 +43,16 @@ def posterior_f64(mix_params: dict, x: np.ndarray) -> np.ndarray:
     post = _pdf_ftz(q, di[None], a, w[None])
     post[bad] = 0
     S = post.sum(1, keepdims=True)
+    if is_diffuse is None:
+        with np.errstate(invalid="ignore", divide="ignore"):
+            return np.where(S > 0, post / S, 0.0)
+    dif = (np.asarray(is_diffuse) != 0)[:, None]
+    hp = np.asarray(hpdf, np.float64)[:, None]
+    S2 = np.where(dif, (1.0 - h) * S + h * hp, S)
     with np.errstate(invalid="ignore", divide="ignore"):
-        out = np.where(S > 0, post / S, 0.0)
-    return out
+        inv = 1.0 / S2
+        scale = np.where(dif, (1.0 - h) * inv, inv)
+        return np.where(np.isfinite(inv) & (S2 > 0), post * scale, 0.0)
 
 
 def estep_f64(mix_params: dict, x, w, hpdf=None, is_diffuse=None, h=0.5, chunk=2048):

@@ -129,3 +129,26 @@ def test_batched_rejects_bad_arguments(pkg, synth, gpu):
     other.init_hemisphere(x[0:3, :4].T.copy(), nrm[:4].copy(), synth.DEPTH_PRIOR, synth.SPATIAL_DISTANCE, 1)
     with pytest.raises(pkg.SDMMError):
         pkg.em_step_batched([mixes[0], other], ds, seg, 1)            # K differs
+
+
+@pytest.mark.parametrize("fail_at", [1, 3])
+def test_create_many_failure_cleanup(pkg, gpu, monkeypatch, fail_at):
+    """A stream-ordered slab whose member fail_at (> 0) fails to be created:
+    the members already carved are destroyed, the slab is freed exactly once
+    (no use after free), the call reports the error, and the next creation
+    from a fresh slab succeeds (create_many's cleanup path)."""
+    import ctypes as C
+    import torch
+    lib = pkg.lib()
+    st = torch.cuda.Stream(gpu)
+    out = (C.c_void_p * 5)()
+    monkeypatch.setenv("SDMM_TEST_FAIL_MEMBER", str(fail_at))
+    rc = lib.sdmm_create_many_on_stream(16, None, gpu.index, C.c_void_p(st.cuda_stream), 5, out)
+    assert rc != 0
+    assert all(v is None for v in out), "failed creation left handles behind"
+    monkeypatch.delenv("SDMM_TEST_FAIL_MEMBER")
+    rc = lib.sdmm_create_many_on_stream(16, None, gpu.index, C.c_void_p(st.cuda_stream), 5, out)
+    assert rc == 0
+    for v in out:
+        lib.sdmm_destroy(C.c_void_p(v))
+    torch.cuda.synchronize()

@@ -91,6 +91,15 @@ def _mp_worker(rank, world, port, out_dir):
         mix.optimize_sharded(comm, ds.shard(rank, world))
     out.update({f"s_{k}": v for k, v in _params(mix).items()})
 
+    # (1b) the Pool config's K = 256 (configs[3]), sample-sharded the same way
+    K2 = 256
+    pos2, nrm2 = synth.model_seed_points(b, K2)
+    mix2 = pkg.SDMM(K2)
+    mix2.init_hemisphere(pos2, nrm2, synth.DEPTH_PRIOR, synth.SPATIAL_DISTANCE, synth.SEED_MODEL)
+    for _ in range(3):
+        mix2.optimize_sharded(comm, ds.shard(rank, world))
+    out.update({f"p_{k}": v for k, v in _params(mix2).items()})
+
     # (2) per-leaf EM, every rank holding half of every leaf's samples
     lb, seg, Kl = _leaves(synth)
     iters = np.array([2, 1, 2, 1, 2, 2], np.int32)
@@ -125,6 +134,11 @@ def _mp_worker(rank, world, port, out_dir):
         for _ in range(3):
             ref.optimize(ds)
         out.update({f"rs_{k}": v for k, v in _params(ref).items()})
+        ref2 = pkg.SDMM(K2)
+        ref2.init_hemisphere(pos2, nrm2, synth.DEPTH_PRIOR, synth.SPATIAL_DISTANCE, synth.SEED_MODEL)
+        for _ in range(3):
+            ref2.optimize(ds)
+        out.update({f"rp_{k}": v for k, v in _params(ref2).items()})
         refs = [_init_leaf(pkg, synth, lb, seg, i, Kl) for i in range(len(seg) - 1)]
         pkg.em_step_batched_iters(refs, full, seg, iters)
         for i, m in enumerate(refs):
@@ -159,6 +173,8 @@ def test_world2_host_transport(tmp_path, pkg, gpu, plog):
     pick = lambda d, p: {k: d[f"{p}_{k}"] for k in ("weights", "cov")}
     assert int(r0["s_it"]) == 3
     _close(pick(r0, "s"), pick(r0, "rs"), plog, "sample_sharded_em")
+    assert int(r0["p_it"]) == 3
+    _close(pick(r0, "p"), pick(r0, "rp"), plog, "sample_sharded_em_K256")
     n_leaves = 6
     for i in range(n_leaves):
         _close(pick(r0, f"b{i}"), pick(r0, f"rb{i}"), plog, f"batched_sharded_leaf{i}")
