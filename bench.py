@@ -230,7 +230,7 @@ def wavefront_bench(pkg, synth, batch, shard, tree, dev, stream, ct, ut, gout, t
             "guided_frac": float((comp >= 0).mean()), "scaling": "weak (replicas: queries per rank)"}
 
 
-def cornell_bench(pkg, dev, args, world, optimize_async=0, K=16):
+def cornell_bench(pkg, dev, args, world, optimize_async=0, K=16, product=False):
     """configs[0] on the device: the test suite's Cornell Box (640x360), K=16
     per leaf (K=128: the Torus line's K, configs[2], over the one scene whose
     geometry the snapshot holds), 64 spp rendered 8 spp per iteration, training (push + optimize)
@@ -240,8 +240,13 @@ def cornell_bench(pkg, dev, args, world, optimize_async=0, K=16):
     bounce rays traced per second in the guided passes."""
     import torch
     scenes = importlib.import_module("sdmm_mitsuba_amd.scenes")
-    sc = pkg.Scene(scenes.cornell_box(640, 360), device=dev.index)
+    desc = scenes.cornell_box(640, 360)
+    sc = pkg.Scene(desc, device=dev.index)
     _, _, tmin, tmax = sc.normalization()
+    table = None
+    if product:   # sampleProduct: every Cornell BSDF is diffuse, one learned lobe each
+        w, m, cov, dif = scenes.diffuse_learned_bsdf(len(desc["reflectance"]) // 3)
+        table = pkg.BsdfTable(w, m, cov, device=dev, diffuse=dif)
     spp_total, spp_it = 64, 8
     img = torch.zeros(3, 360, 640, device=dev)
     acc = torch.zeros_like(img)
@@ -255,7 +260,8 @@ def cornell_bench(pkg, dev, args, world, optimize_async=0, K=16):
         for it, done in enumerate(range(0, spp_total, spp_it)):
             train = done < spp_total // 4
             t = time.perf_counter()
-            _, ls, gs = g.iteration(sc, spp_it, seed=1 + it, push_seed=1001 + it, train=train, image=img)
+            _, ls, gs = g.iteration(sc, spp_it, seed=1 + it, push_seed=1001 + it, train=train, image=img,
+                                    learned_bsdf=table)
             acc += img
             torch.cuda.synchronize()
             its.append({"ms": (time.perf_counter() - t) * 1e3, "train": train, "segments": ls["segments"],
@@ -271,7 +277,7 @@ def cornell_bench(pkg, dev, args, world, optimize_async=0, K=16):
             "guided_paths_per_s": sum(x["paths"] for x in guided) / (gms * 1e-3),
             "trained_leaves": its[-1]["trained"], "iterations": its,
             "image_mean": float((acc / len(its)).mean().item()), "replicas": world,
-            "optimize_async": bool(optimize_async)}
+            "optimize_async": bool(optimize_async), "sample_product": bool(product)}
 
 
 def large_k_bench(pkg, synth, batch, shard, dev, stream, timed, args, world, N, comm):
@@ -553,6 +559,9 @@ def main():
         # on the device): the Torus meshes are LFS pointers in the snapshot, so
         # the same guided renderer runs over the Cornell Box with K=128 leaves
         out["cornell_k128"] = cornell_bench(pkg, dev, args, world, K=128)
+        # sampleProduct (configs[4]'s learned-BSDF product sampling, sdmm_proc.cpp:327-392)
+        # inside the full guided render: the Cornell BSDFs' synthesised diffuse lobes
+        out["cornell_product"] = cornell_bench(pkg, dev, args, world, product=True)
 
     if not args.no_extra and not args.no_large_k:
         out["large_k"] = large_k_bench(pkg, synth, batch, shard, dev, stream, timed, args, world, N_global, comm)

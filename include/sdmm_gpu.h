@@ -105,7 +105,8 @@ const char* sdmm_kernel_name(const sdmm_mix* m, int which);
 /* Guided queries keep a per-query list of at most `cap` candidate components
  * (default and maximum 40); queries that do not fit take the full-K path.
  * Results are identical for every cap; 0 sends every query down the full-K
- * path (a testing knob). */
+ * path (a testing knob).  A tree wavefront uses the smallest cap of the
+ * mixtures bound to it (read when the table is bound / passed). */
 int sdmm_set_guide_capacity(sdmm_mix* m, int cap);
 /* coherent != 0 (default): guided batches of >= 16384 queries are served in
  * Morton order of their condition position (a device radix sort of the
@@ -286,6 +287,11 @@ typedef struct {
     const float* means;
     const float* covs;
     int B, M;
+    /* per material (nullable): 1 = a diffuse BSDF.  The plugin's diffuse case
+     * (sdmm_proc.cpp:335-339) re-centres only slice 0 on the shading normal
+     * (set_mean(normal): mean = F's third column, frame Coordinates(mean));
+     * slices >= 1 are then used as stored, in world coordinates. */
+    const uint8_t* diffuse;
 } sdmm_bsdf_table;
 int sdmm_guide_product_batch(const sdmm_mix* m, int64_t nq, const float* const c[3], const float* const u[3],
                              const sdmm_bsdf_table* bsdf, const int32_t* material, const float* const frame[9],
@@ -425,6 +431,27 @@ int sdmm_guide_pdf_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int
                              const float* const u[3], const float* const dgiven[3], const uint8_t* pdf_mode,
                              float* const d[3], float* pdf, int32_t* comp, int32_t* node_out);
 
+/* Product sampling over the spatial tree's leaves -- sampleSurface /
+ * pdfSurface with sampleProduct for a wavefront of bounces (sdmm_proc.cpp:
+ * 309-392, :474-502): per query, node = STree.find(c), that node's mixture
+ * (node_mix or the table bound by sdmm_stree_bind_mixtures; none: BSDF only,
+ * h = 1, comp -1, pdf 0), then exactly sdmm_guide_product_batch /
+ * sdmm_pdf_product_batch against it (outputs bitwise equal).
+ *   choice (nullable, device): the mixed bounce -- query q's BSDF/guide draw;
+ *          with it, dgiven (device, 3 planes: the BSDF-sampled directions) is
+ *          required and query q becomes a pdf query at dgiven[q] when
+ *          choice[q] <= h[q] (the reference's rRec.nextSample1D() <=
+ *          heuristicConditionalWeight, :392, with h 0.3 for a usable product,
+ *          0.5 for the plain conditional): d = dgiven, pdf = the used
+ *          mixture's pdf there, comp = -2.  Without choice, every query samples.
+ *   heuristic (nullable): per query h (0.3 / 0.5 / 1); node_out (nullable). */
+int sdmm_guide_product_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
+                                 const float* const u[3], const float* choice, const float* const dgiven[3],
+                                 const sdmm_bsdf_table* bsdf, const int32_t* material, const float* const frame[9],
+                                 float* const d[3], float* pdf, int32_t* comp, float* heuristic, int32_t* node_out);
+int sdmm_pdf_product_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
+                               const float* const d[3], const sdmm_bsdf_table* bsdf, const int32_t* material,
+                               const float* const frame[9], float* pdf, float* heuristic);
 /* Checkpoints (.asdmm, JSON; schema in DESIGN.md section 9).
  *   sdmm_save_json      the accelerator: sdmm::save_json(m_accelerator, path),
  *                       volpath_sdmm.cpp:117-126 (model_%05i.asdmm, once per
@@ -528,6 +555,17 @@ typedef struct {
     int saved_vertices;       /* vertex slots per path (>= max_depth - 1; the reference's array holds 10) */
     uint64_t seed;
     int64_t pixel_begin, pixel_end;
+    /* sampleProduct (volpath_sdmm.cpp:60, sdmm_proc.cpp:327-392): guided
+     * bounces sample the product of the leaf's conditional with the hit
+     * material's learned BSDF (learned_bsdf row = the quad's bsdf index; every
+     * BSDF here is diffuse: set diffuse[b], the plugin's slice-0 rule) through
+     * sdmm_guide_product_wavefront, with h = 0.3 (0.5 when the product is
+     * unusable) and the BSDF/guide choice taken against that h.  0: the plain
+     * conditional with bsdf_fraction.  (bsdfOnly never trains, :416, so it
+     * is the guided = 0 render; its learned-BSDF branch, :331/:384/:410, is
+     * unreachable in the reference.) */
+    int sample_product;
+    sdmm_bsdf_table learned_bsdf;   /* device arrays */
 } sdmm_li_params;
 /* Vertex records of the last render (device): field f of vertex v of path p
  * at rec[(f * max_vertices + v) * n_paths + p]; f: 0-2 weight (RGB), 3-5

@@ -90,7 +90,8 @@ def lib():
         L.or_coordinates.argtypes = [_f, _f]
         L.or_component_set.argtypes = [C.c_void_p, C.c_int, _d, _d, C.c_int]
         L.or_guide_product_batch.argtypes = [C.c_void_p, C.c_int64, _f, _f, C.POINTER(C.c_int32), _f, _f, _f,
-                                             _f, C.c_int, _f, _f, _f, C.POINTER(C.c_int32), _f]
+                                             _f, C.c_int, C.POINTER(C.c_uint8), _f, _f, _f, _f,
+                                             C.POINTER(C.c_int32), _f]
         _l = C.POINTER(C.c_int64)
         L.or_kmeanspp_select.argtypes = [_f, _f, _f, _f, _f, _f, _f, C.c_int64, C.c_int, _f, C.c_int, _l]
         L.or_uniform_hemisphere_init_kmeanspp.argtypes = [
@@ -292,11 +293,15 @@ def guide_batch(m: Mixture, c: np.ndarray, u: np.ndarray):
     return d, pdf, comp, slot
 
 
-def guide_product_batch(m: Mixture, c, u, material, frames, bw, bmean, bcov, dgiven=None):
+def guide_product_batch(m: Mixture, c, u, material, frames, bw, bmean, bcov, dgiven=None, diffuse=None,
+                        choice=None):
     """Product sampling with a learned-BSDF table (sdmm_oracle_product.inc).
     c, u: (nq, 3); material: (nq,) int (-1: none); frames: (nq, 9) row-major
     to-world [s t n] columns; bw (B, M), bmean (B, M, 3) local, bcov (B, M, 4).
-    Returns dir (nq, 3), pdf, comp (k * M + j for product samples), h."""
+    diffuse (B,) flags: the plugin's diffuse case (slice 0 on the normal);
+    choice (nq,) with dgiven: the mixed bounce (pdf query where choice <= h).
+    Returns dir (nq, 3), pdf, comp (k * M + j for product samples, -2 for
+    pdf queries of the mixed bounce), h."""
     c = np.ascontiguousarray(c, np.float32)
     u = np.ascontiguousarray(u, np.float32)
     nq = c.shape[0]
@@ -312,9 +317,13 @@ def guide_product_batch(m: Mixture, c, u, material, frames, bw, bmean, bcov, dgi
     h = np.zeros(nq, np.float32)
     I32 = C.POINTER(C.c_int32)
     dg = None if dgiven is None else np.ascontiguousarray(dgiven, np.float32)
+    df = None if diffuse is None else np.ascontiguousarray(diffuse, np.uint8)
+    ch = None if choice is None else np.ascontiguousarray(choice, np.float32)
     lib().or_guide_product_batch(m.ptr, nq, _fp(c), _fp(u), material.ctypes.data_as(I32), _fp(frames), _fp(bw),
-                                 _fp(bmean), _fp(bcov), M, None if dg is None else _fp(dg), _fp(d), _fp(pdf),
-                                 comp.ctypes.data_as(I32), _fp(h))
+                                 _fp(bmean), _fp(bcov), M,
+                                 None if df is None else df.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                 None if ch is None else _fp(ch), None if dg is None else _fp(dg), _fp(d),
+                                 _fp(pdf), comp.ctypes.data_as(I32), _fp(h))
     return d, pdf, comp, h
 
 

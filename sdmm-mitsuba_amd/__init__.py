@@ -220,6 +220,7 @@ EXPORTED_SYMBOLS = [
     "sdmm_init_hemisphere_batched", "sdmm_iterations_run", "sdmm_stree_split_leaf_recurse_many",
     "sdmm_em_step_batched_host_iters", "sdmm_write_exr", "sdmm_clone_many_on_stream", "sdmm_copy_many",
     "sdmm_guiding_update", "sdmm_kmeanspp_select", "sdmm_init_hemisphere_kmeanspp_batched",
+    "sdmm_guide_product_wavefront", "sdmm_pdf_product_wavefront",
 ]
 
 
@@ -747,21 +748,27 @@ class SDMM:
 
 class _BsdfTable(C.Structure):
     _fields_ = [("weights", C.c_void_p), ("means", C.c_void_p), ("covs", C.c_void_p), ("B", C.c_int),
-                ("M", C.c_int)]
+                ("M", C.c_int), ("diffuse", C.c_void_p)]
 
 
 class BsdfTable:
     """Learned-BSDF lobes on the device (sdmm_bsdf_table): weights (B, M),
-    local unit means (B, M, 3), 2x2 covariances (B, M, 4)."""
+    local unit means (B, M, 3), 2x2 covariances (B, M, 4); diffuse (B,)
+    optional per-material flags (the plugin's diffuse case: slice 0 on the
+    shading normal, sdmm_proc.cpp:335-339)."""
 
-    def __init__(self, weights, means, covs, device="cuda"):
+    def __init__(self, weights, means, covs, device="cuda", diffuse=None):
         import torch
         w = np.ascontiguousarray(weights, np.float32)
         self.B, self.M = w.shape
         self.w = torch.from_numpy(w.copy()).to(device)
         self.mean = torch.from_numpy(np.ascontiguousarray(means, np.float32).reshape(self.B, self.M, 3).copy()).to(device)
         self.cov = torch.from_numpy(np.ascontiguousarray(covs, np.float32).reshape(self.B, self.M, 4).copy()).to(device)
-        self.c = _BsdfTable(self.w.data_ptr(), self.mean.data_ptr(), self.cov.data_ptr(), self.B, self.M)
+        self.diffuse = None
+        if diffuse is not None:
+            self.diffuse = torch.from_numpy(np.ascontiguousarray(diffuse, np.uint8).reshape(self.B).copy()).to(device)
+        self.c = _BsdfTable(self.w.data_ptr(), self.mean.data_ptr(), self.cov.data_ptr(), self.B, self.M,
+                            None if self.diffuse is None else self.diffuse.data_ptr())
 
 
 class STree:
@@ -957,6 +964,46 @@ class STree:
                                               comp.data_ptr(), None if node_out is None else node_out.data_ptr()))
         return d, pdf, comp
 
+    def guide_product(self, node_mix, c, u, bsdf, material, frame, choice=None, dgiven=None, node_out=None):
+        """Product sampling over the leaves (sdmm_guide_product_wavefront):
+        per query the leaf's conditional times its material's learned-BSDF
+        lobes; with choice + dgiven the mixed bounce (a pdf query at dgiven
+        where choice <= h, comp -2).  Returns (d planes, pdf, comp, h)."""
+        import torch
+        nq = c[0].numel()
+        tab = self._node_table(node_mix)
+        dev = c[0].device
+        d = [torch.empty(nq, device=dev) for _ in range(3)]
+        pdf = torch.empty(nq, device=dev)
+        comp = torch.empty(nq, device=dev, dtype=torch.int32)
+        h = torch.empty(nq, device=dev)
+        cc = (C.c_void_p * 3)(*[t.data_ptr() for t in c])
+        uu = (C.c_void_p * 3)(*[t.data_ptr() for t in u])
+        dd = (C.c_void_p * 3)(*[t.data_ptr() for t in d])
+        ff = (C.c_void_p * 9)(*[t.data_ptr() for t in frame])
+        gg = None if dgiven is None else (C.c_void_p * 3)(*[t.data_ptr() for t in dgiven])
+        _check(lib().sdmm_guide_product_wavefront(
+            self.h, tab, nq, cc, uu, None if choice is None else C.c_void_p(choice.data_ptr()), gg,
+            C.byref(bsdf.c), C.c_void_p(material.data_ptr()), ff, dd, C.c_void_p(pdf.data_ptr()),
+            C.c_void_p(comp.data_ptr()), C.c_void_p(h.data_ptr()),
+            None if node_out is None else C.c_void_p(node_out.data_ptr())))
+        return d, pdf, comp, h
+
+    def pdf_product(self, node_mix, c, d, bsdf, material, frame):
+        """pdfSurface with sampleProduct per query's leaf (sdmm_pdf_product_wavefront)."""
+        import torch
+        nq = c[0].numel()
+        tab = self._node_table(node_mix)
+        pdf = torch.empty(nq, device=c[0].device)
+        h = torch.empty(nq, device=c[0].device)
+        cc = (C.c_void_p * 3)(*[t.data_ptr() for t in c])
+        dd = (C.c_void_p * 3)(*[t.data_ptr() for t in d])
+        ff = (C.c_void_p * 9)(*[t.data_ptr() for t in frame])
+        _check(lib().sdmm_pdf_product_wavefront(self.h, tab, nq, cc, dd, C.byref(bsdf.c),
+                                                C.c_void_p(material.data_ptr()), ff, C.c_void_p(pdf.data_ptr()),
+                                                C.c_void_p(h.data_ptr())))
+        return pdf, h
+
     def push_training(self, vertices: "PathVertices", saved_per_path: int = 8, seed: int = 0):
         """Training records of Li's tail (sdmm_push_training): dict of device
         tensors x (6 planes), normal (3), w, stats, node, source; seg (host);
@@ -1051,8 +1098,9 @@ class Guiding:
 
     def iteration(self, scene: "Scene", spp: int, seed: int, push_seed: int, train: bool = True,
                   max_depth: int = 10, rr_depth: int = 10, bsdf_fraction: float = 0.5, saved_vertices: int = 9,
-                  image=None, image_sqr=None):
-        """One pass of render()'s loop -> (image, li stats, optimize stats)."""
+                  image=None, image_sqr=None, learned_bsdf: "BsdfTable" = None):
+        """One pass of render()'s loop -> (image, li stats, optimize stats).
+        learned_bsdf: sampleProduct with that table (rows = the scene's BSDFs)."""
         import torch
         if image is None:
             image = torch.zeros(3, scene.height, scene.width, device=torch.device("cuda", self.device))
@@ -1060,6 +1108,8 @@ class Guiding:
         p.spp, p.max_depth, p.rr_depth, p.guided = int(spp), int(max_depth), int(rr_depth), 0
         p.bsdf_fraction, p.saved_vertices, p.seed = float(bsdf_fraction), int(saved_vertices), int(seed)
         p.pixel_begin, p.pixel_end = 0, scene.width * scene.height
+        if learned_bsdf is not None:
+            p.sample_product, p.learned_bsdf = 1, learned_bsdf.c
         ls = _LiStats()
         gs = _GuidingStats()
         _check(lib().sdmm_guiding_iteration(self.h, scene.h, C.byref(p), C.c_uint64(push_seed), int(train),
@@ -1097,7 +1147,8 @@ class _SceneDesc(C.Structure):
 class _LiParams(C.Structure):
     _fields_ = [("spp", C.c_int), ("max_depth", C.c_int), ("rr_depth", C.c_int), ("guided", C.c_int),
                 ("bsdf_fraction", C.c_float), ("saved_vertices", C.c_int), ("seed", C.c_uint64),
-                ("pixel_begin", C.c_int64), ("pixel_end", C.c_int64)]
+                ("pixel_begin", C.c_int64), ("pixel_end", C.c_int64), ("sample_product", C.c_int),
+                ("learned_bsdf", _BsdfTable)]
 
 
 class _PathVertices(C.Structure):
@@ -1178,9 +1229,10 @@ class Scene:
 
     def render(self, tree: "STree", node_mix=None, spp: int = 1, max_depth: int = 10, rr_depth: int = 10,
                guided: bool = False, bsdf_fraction: float = 0.5, saved_vertices: int = 9, seed: int = 0,
-               pixels=None, image=None, image_sqr=None):
+               pixels=None, image=None, image_sqr=None, learned_bsdf: "BsdfTable" = None):
         """One render pass (sdmm_li_render) -> (image (3, H, W) device tensor,
-        PathVertices, stats dict)."""
+        PathVertices, stats dict).  learned_bsdf: sampleProduct with that
+        learned-BSDF table (one row per scene BSDF)."""
         import torch
         if image is None:
             image = torch.zeros(3, self.height, self.width, device=torch.device("cuda", self.device))
@@ -1188,6 +1240,8 @@ class Scene:
         p.spp, p.max_depth, p.rr_depth, p.guided = int(spp), int(max_depth), int(rr_depth), int(guided)
         p.bsdf_fraction, p.saved_vertices, p.seed = float(bsdf_fraction), int(saved_vertices), int(seed)
         p.pixel_begin, p.pixel_end = (0, self.width * self.height) if pixels is None else pixels
+        if learned_bsdf is not None:
+            p.sample_product, p.learned_bsdf = 1, learned_bsdf.c
         v = _PathVertices()
         st = _LiStats()
         tab = None if not guided else tree._node_table(node_mix)

@@ -1265,17 +1265,29 @@ static void launch_group_fallback(int kmax, int blocks, hipStream_t st, const fl
 // sampled direction, each recomputing the pairs (a pair is ~40 small
 // matrix/vector ops; the kept conditional x lobes is tens of pairs).
 
+// heuristicConditionalWeight with a usable product (sdmm_proc.cpp:386-387)
+constexpr float kProductH = 0.3f;
+
 struct BsdfTab {
     const float* w;      // [B][M]
     const float* mean;   // [B][M][3]  local shading frame
     const float* cov;    // [B][M][4]  2x2 in the lobe's own tangent frame
     int B, M;
+    // per material (nullable): a diffuse BSDF -- the plugin's diffuse case
+    // (sdmm_proc.cpp:335-339) only re-centres slice 0 on the shading normal
+    // (set_mean: mean n, frame Coordinates(n)); slices >= 1 are used as stored
+    const uint8_t* diffuse;
 };
 
 struct ProductIO {
     const int32_t* material;   // per query; < 0: no learned BSDF
     const float* F[9];         // per-query to-world frame, row-major [s t n]
     float* h;                  // heuristicConditionalWeight per query
+    // mixed wavefront (nullable; sampling kernels): query q is a pdf query at
+    // its given direction io.e[q] when choice[q] <= h, h being the query's own
+    // heuristic weight (0.3 product / 0.5 conditional), the reference's
+    // rRec.nextSample1D() <= heuristicConditionalWeight (:392)
+    const float* choice;
 };
 
 __device__ __forceinline__ float acos_x(float x) { return (float)acos((double)x); }
@@ -1544,6 +1556,14 @@ __device__ __forceinline__ void bsdf_world(const float F[9], const BsdfTab& bt, 
     wj = bt.w[idx];
     const float ml[3] = {bt.mean[3 * idx], bt.mean[3 * idx + 1], bt.mean[3 * idx + 2]};
     for (int i = 0; i < 4; ++i) cj[i] = bt.cov[4 * idx + i];
+    if (bt.diffuse && bt.diffuse[b]) {
+        // slice 0: mean = the shading normal (F's third column), frame
+        // Coordinates(mean); the other slices as stored (world)
+        if (j == 0) { mw[0] = F[2]; mw[1] = F[5]; mw[2] = F[8]; }
+        else { mw[0] = ml[0]; mw[1] = ml[1]; mw[2] = ml[2]; }
+        coordinates_f(mw, tw);
+        return;
+    }
     float tl[9];
     coordinates_f(ml, tl);
     for (int i = 0; i < 3; ++i) mw[i] = F[3 * i] * ml[0] + F[3 * i + 1] * ml[1] + F[3 * i + 2] * ml[2];
@@ -1599,10 +1619,12 @@ __device__ __forceinline__ float prod_comp_pdf(const ProdComp& pc, const float d
 // Query q after its conditional's kept prefix is known.  Returns false when
 // the product is unusable (no learned BSDF, no pair, zero mass): the caller
 // then serves the plain conditional (h = 0.5).
+// choice: the mixed wavefront's BSDF/guide draw (> 1 when none): a query
+// whose product is usable becomes a pdf query at dir_in when choice <= 0.3.
 template <bool PDF_ONLY, class Slots>
 __device__ bool finish_product(const float* gp, int Kp, const float* condCov, const float c[3], int lastIdx,
                                float accum, const Slots& S, const BsdfTab& bt, int b, const float F[9],
-                               const float* u, const float* dir_in, GuideConsts gc, QueryOut& o) {
+                               const float* u, const float* dir_in, float choice, GuideConsts gc, QueryOut& o) {
     const float invSum = 1.0f / accum;
     const bool scaled = __builtin_isfinite(invSum);
     float sum2 = 0.0f;
@@ -1618,8 +1640,8 @@ __device__ bool finish_product(const float* gp, int Kp, const float* condCov, co
                   [&](int, int, int, float w, const ProdComp&) { total += w; ++P; return false; });
     if (P == 0 || total == 0.0f) return false;
     float dir[3];
-    o.comp = -1;
-    if constexpr (!PDF_ONLY) {
+    o.comp = kCompPdfValid;
+    if (!PDF_ONLY && !(choice <= kProductH)) {
         // pass 2: sampleDiscreteCdf over the normalised weights (lower_bound,
         // then the tie walk), keeping the selected pair
         float cdf = 0.0f, prev = 0.0f;
@@ -1669,6 +1691,8 @@ __device__ __forceinline__ void product_tail(const float* gp, int Kp, const floa
                                              const ProductIO& pio, const BsdfTab& bt, int64_t q, GuideConsts gc) {
     int b = pio.material ? pio.material[q] : -1;
     if (b >= bt.B) b = -1;
+    const bool mixed = !PDF_ONLY && pio.choice != nullptr;
+    const float choice = mixed ? pio.choice[q] : 2.0f;
     // createCdf(true) of the conditional (finish_query's validity test)
     float sum2 = 0.0f;
     {
@@ -1684,26 +1708,21 @@ __device__ __forceinline__ void product_tail(const float* gp, int Kp, const floa
     QueryOut o{{0.0f, 0.0f, 0.0f}, 0.0f, -1};
     float h = 1.0f;                       // no valid conditional: BSDF only
     if (cvalid) {
+        float u[3] = {0.0f, 0.0f, 0.0f}, dg[3] = {0.0f, 0.0f, 0.0f};
+        if (PDF_ONLY || mixed) { dg[0] = io.e0[q]; dg[1] = io.e1[q]; dg[2] = io.e2[q]; }
+        if constexpr (!PDF_ONLY) { u[0] = io.u0[q]; u[1] = io.u1[q]; u[2] = io.u2[q]; }
         bool used = false;
         if (b >= 0 && bt.M > 0) {
             float F[9];
             for (int i = 0; i < 9; ++i) F[i] = pio.F[i][q];
-            float u[3] = {0.0f, 0.0f, 0.0f}, dg[3] = {0.0f, 0.0f, 0.0f};
-            if constexpr (PDF_ONLY) { dg[0] = io.e0[q]; dg[1] = io.e1[q]; dg[2] = io.e2[q]; }
-            else { u[0] = io.u0[q]; u[1] = io.u1[q]; u[2] = io.u2[q]; }
-            used = finish_product<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, accum, S, bt, b, F, u, dg, gc, o);
+            used = finish_product<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, accum, S, bt, b, F, u, dg, choice, gc, o);
         }
         if (used) {
-            h = 0.3f;
+            h = kProductH;
         } else {
             h = 0.5f;
-            if constexpr (PDF_ONLY) {
-                const float dir[3] = {io.e0[q], io.e1[q], io.e2[q]};
-                o = finish_query(gp, Kp, c, nullptr, lastIdx, accum, S, dir, gc);
-            } else {
-                const float u[3] = {io.u0[q], io.u1[q], io.u2[q]};
-                o = finish_query(gp, Kp, c, u, lastIdx, accum, S, nullptr, gc);
-            }
+            const bool pdfq = PDF_ONLY || choice <= 0.5f;
+            o = finish_query(gp, Kp, c, pdfq ? nullptr : u, lastIdx, accum, S, pdfq ? dg : nullptr, gc);
         }
     }
     if constexpr (PDF_ONLY) {
@@ -1796,7 +1815,7 @@ __device__ __forceinline__ bool pair_eval(const float* condCov, const WaveLds& L
 template <bool PDF_ONLY>
 __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCov, const float c[3], int lastIdx,
                                     const WaveLds& L, const BsdfTab& bt, int b, const float F[9], const float* u,
-                                    const float* dir_in, int lane, GuideConsts gc, QueryOut& o) {
+                                    const float* dir_in, float choice, int lane, GuideConsts gc, QueryOut& o) {
     const int M = bt.M;
     const int NP = lastIdx * M;
     const bool keep = NP <= L.pcap;
@@ -1827,8 +1846,8 @@ __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCo
     __syncthreads();
     if (P == 0 || total == 0.0f) return false;
     float dir[3];
-    o.comp = -1;
-    if constexpr (!PDF_ONLY) {
+    o.comp = kCompPdfValid;
+    if (!PDF_ONLY && !(choice <= kProductH)) {
         // pass 2: sampleDiscreteCdf over w / total (lower_bound + tie walk)
         float cdf = 0.0f, prev = 0.0f;
         int p = 0, run_f = -1, sel_f = -1;
@@ -1919,25 +1938,32 @@ __device__ void product_tail_wave(const float* gp, int Kp, const float* condCov,
                                   const BsdfTab& bt, int64_t q, int lane, GuideConsts gc) {
     int b = pio.material ? pio.material[q] : -1;
     if (b >= bt.B) b = -1;
+    const bool mixed = !PDF_ONLY && pio.choice != nullptr;
+    const float choice = mixed ? pio.choice[q] : 2.0f;
     const float sum2 = wave_slot_weights(lastIdx, accum, L, lane);
     const bool cvalid = lastIdx > 0 && sum2 != 0.0f;
     QueryOut o{{0.0f, 0.0f, 0.0f}, 0.0f, -1};
     float h = 1.0f;                       // no valid conditional: BSDF only
     float u[3] = {0.0f, 0.0f, 0.0f}, dg[3] = {0.0f, 0.0f, 0.0f};
-    if constexpr (PDF_ONLY) { dg[0] = io.e0[q]; dg[1] = io.e1[q]; dg[2] = io.e2[q]; }
-    else { u[0] = io.u0[q]; u[1] = io.u1[q]; u[2] = io.u2[q]; }
+    if (PDF_ONLY || mixed) { dg[0] = io.e0[q]; dg[1] = io.e1[q]; dg[2] = io.e2[q]; }
+    if constexpr (!PDF_ONLY) { u[0] = io.u0[q]; u[1] = io.u1[q]; u[2] = io.u2[q]; }
     if (cvalid) {
         bool used = false;
         if (b >= 0 && bt.M > 0) {
             float F[9];
             for (int i = 0; i < 9; ++i) F[i] = pio.F[i][q];
-            used = finish_product_wave<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, L, bt, b, F, u, dg, lane, gc, o);
+            used = finish_product_wave<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, L, bt, b, F, u, dg, choice, lane, gc,
+                                                 o);
         }
         if (used) {
-            h = 0.3f;
+            h = kProductH;
         } else {
             h = 0.5f;
-            o = finish_query_wave<PDF_ONLY>(gp, Kp, c, u, dg, lastIdx, sum2, L, lane, gc);
+            // uniform: one query per wave
+            if (PDF_ONLY || choice <= 0.5f)
+                o = finish_query_wave<true>(gp, Kp, c, u, dg, lastIdx, sum2, L, lane, gc);
+            else
+                o = finish_query_wave<false>(gp, Kp, c, u, dg, lastIdx, sum2, L, lane, gc);
         }
     }
     if (lane == 0) {
@@ -1972,6 +1998,91 @@ guide_product_wave_kernel(const float* __restrict__ gp, int Kp, int K, const flo
         float accum = 0.0f;
         const int lastIdx = build_full_wave(gp, Kp, K, c, L, lane, gc.norm3, accum);
         product_tail_wave<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, accum, L, io, pio, bt, q, lane, gc);
+        __syncthreads();   // the LDS is reused by the next query
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Product sampling over the spatial tree's leaves (sampleSurface with
+// sampleProduct for a wavefront of bounces, sdmm_proc.cpp:309-392): per query,
+// node = STree.find(c) (:314), that node's mixture (none: BSDF only, h = 1,
+// :316-323), then exactly what guide_product_cand_kernel /
+// guide_product_wave_kernel do against that one mixture.  cctab[node] is the
+// node mixture's conditional covariances (condCov).
+template <bool PDF_ONLY, int LCAP>
+__device__ __forceinline__ void serve_product_cand(const float* gp, int Kp, int K, const float* condCov,
+                                                   const GuideIO& io, const ProductIO& pio, const BsdfTab& bt,
+                                                   int64_t q, const float c[3], float* cw, unsigned short* ck,
+                                                   int tid, int cap, GuideConsts gc, int* fb_count,
+                                                   int32_t* fb_list) {
+    float accum = 0.0f;
+    const int lastIdx = build_candidates_reg<LCAP>(gp, Kp, K, c, cw, ck, 64, tid, gc.norm3, cap, accum);
+    if (lastIdx < 0) {
+        fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
+        return;
+    }
+    product_tail<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, accum, CandSlots{cw, ck, 64, tid}, io, pio, bt, q, gc);
+}
+
+template <bool PDF_ONLY>
+__device__ __forceinline__ void product_invalid(const GuideIO& io, const ProductIO& pio, int64_t q) {
+    write_invalid<PDF_ONLY>(io, q);
+    if (pio.h) pio.h[q] = 1.0f;
+}
+
+template <bool PDF_ONLY, int LCAP>
+__global__ void __launch_bounds__(64)
+guide_tree_product_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __restrict__ tab,
+                               const float* const* __restrict__ cctab, int64_t nq, GuideIO io, ProductIO pio,
+                               BsdfTab bt, GuideConsts gc, int cap, int* __restrict__ fb_count,
+                               int32_t* __restrict__ fb_list, const int32_t* __restrict__ perm,
+                               int32_t* __restrict__ node_out) {
+    __shared__ float cw[LCAP * 64];
+    __shared__ unsigned short ck[LCAP * 64];
+    const int tid = threadIdx.x;
+    const int64_t t = (int64_t)blockIdx.x * 64 + tid;
+    if (t >= nq) return;
+    const int64_t q = perm ? (int64_t)perm[t] : t;
+    const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
+    const int node = stree_find_point(nodes, c[0], c[1], c[2]);
+    if (node_out) node_out[q] = node;
+    // one leaf for the whole wave (the Morton-ordered common case): uniform
+    // control flow; else one distinct leaf per trip (waterfall)
+    const int n0 = __builtin_amdgcn_readfirstlane(node);
+    const bool uniform = __builtin_amdgcn_ballot_w64(node != n0) == 0;
+    for (;;) {
+        const int nw = uniform ? n0 : __builtin_amdgcn_readfirstlane(node);
+        if (node != nw) continue;
+        const GuideMix mx = (nw >= 0) ? tab[nw] : GuideMix{nullptr, 0, 0};
+        if (mx.K <= 0)
+            product_invalid<PDF_ONLY>(io, pio, q);
+        else
+            serve_product_cand<PDF_ONLY, LCAP>(mx.gp, mx.Kp, mx.K, cctab[nw], io, pio, bt, q, c, cw, ck, tid, cap,
+                                               gc, fb_count, fb_list);
+        break;
+    }
+}
+
+// the tree product path's full-K queries, one wave per query (grid-stride);
+// kmax sizes the LDS
+template <bool PDF_ONLY>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDMM_PRODUCT_WPE)))
+guide_tree_product_wave_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __restrict__ tab,
+                               const float* const* __restrict__ cctab, int kmax, GuideIO io, ProductIO pio,
+                               BsdfTab bt, GuideConsts gc, float* __restrict__ pscratch, int pcap,
+                               const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int lane = threadIdx.x;
+    const WaveLds L = wave_lds(lds, kmax, pscratch, pcap, bt.M);
+    const int n = *fb_count;
+    for (int idx = blockIdx.x; idx < n; idx += gridDim.x) {
+        const int64_t q = fb_list[idx];
+        const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
+        const int node = stree_find_point(nodes, c[0], c[1], c[2]);   // uniform: a listed query has a mixture
+        const GuideMix mx = tab[node];
+        float accum = 0.0f;
+        const int lastIdx = build_full_wave(mx.gp, mx.Kp, mx.K, c, L, lane, gc.norm3, accum);
+        product_tail_wave<PDF_ONLY>(mx.gp, mx.Kp, cctab[node], c, lastIdx, accum, L, io, pio, bt, q, lane, gc);
         __syncthreads();   // the LDS is reused by the next query
     }
 }
@@ -2221,8 +2332,9 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
                                 const float* const c[3], const float* const u[3], const float* const dgiven[3],
                                 float* const d[3], float* pdf, int32_t* comp, const int32_t* material,
                                 const float* const frame[9], float* h, const float* bw, const float* bmean,
-                                const float* bcov, int B, int M, float norm2, float norm3, int cap, int* fb_count,
-                                int32_t* fb_list, int cus, hipStream_t st, const GuideSortScratch* sort) {
+                                const float* bcov, const uint8_t* diffuse, int B, int M, float norm2, float norm3,
+                                int cap, int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
+                                const GuideSortScratch* sort) {
     if (nq <= 0) return hipSuccess;
     if (nq > INT32_MAX) return hipErrorInvalidValue;
     if (K > kWaveKMax || M > 64) return hipErrorInvalidValue;
@@ -2235,7 +2347,7 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
     pio.material = material;
     for (int i = 0; i < 9; ++i) pio.F[i] = frame[i];
     pio.h = h;
-    const BsdfTab bt{bw, bmean, bcov, B, M};
+    const BsdfTab bt{bw, bmean, bcov, B, M, diffuse};
     hipError_t e = hipMemsetAsync(fb_count, 0, sizeof(int), st);
     if (e != hipSuccess) return e;
     const int32_t* perm = nullptr;
@@ -2276,6 +2388,93 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
     else
         hipLaunchKernelGGL(guide_product_wave_kernel<false>, dim3(fblocks), dim3(64), lds, st, gp, Kp, K, condCov,
                            io, pio, bt, gc, pscratch, kProductPairCap, fb_count, fb_list);
+    e = hipGetLastError();
+    if (pscratch) {
+        const hipError_t f = hipFreeAsync(pscratch, st);
+        if (e == hipSuccess) e = f;
+    }
+    return e;
+}
+
+// The product wavefront over the tree (tab / cctab per node, kmax the largest
+// K): candidate pass, then the full-K queries one per wave.  Modes: sampling
+// (dgiven null), pdf only (dgiven, no choice), mixed (dgiven + choice: a pdf
+// query where choice <= the query's h).
+hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const void* cctab, int kmax, int64_t nq,
+                                     const float* const c[3], const float* const u[3], const float* choice,
+                                     const float* const dgiven[3], float* const d[3], float* pdf, int32_t* comp,
+                                     int32_t* node_out, const int32_t* material, const float* const frame[9],
+                                     float* h, const float* bw, const float* bmean, const float* bcov,
+                                     const uint8_t* diffuse, int B, int M, float norm2, float norm3, int cap,
+                                     int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
+                                     const GuideSortScratch* sort) {
+    if (nq <= 0) return hipSuccess;
+    if (nq > INT32_MAX) return hipErrorInvalidValue;
+    if (kmax < 1) kmax = 1;
+    if (kmax > kWaveKMax || M > 64) return hipErrorInvalidValue;
+    const size_t lds = wave_lds_bytes(kmax, M);
+    cap = (cap < 0) ? 0 : (cap > kGuideCap ? kGuideCap : cap);
+    cap = cap < kmax ? cap : kmax;
+    GuideConsts gc{norm2, norm3};
+    const bool pdf_only = dgiven != nullptr && choice == nullptr;
+    // mixed: the sampling kernels also read the given directions (io.e);
+    // the per-query mode comes from pio.choice, not io.pmode
+    GuideIO iox{};
+    iox.c0 = c[0]; iox.c1 = c[1]; iox.c2 = c[2];
+    if (dgiven) { iox.e0 = dgiven[0]; iox.e1 = dgiven[1]; iox.e2 = dgiven[2]; }
+    if (!pdf_only) {
+        iox.u0 = u[0]; iox.u1 = u[1]; iox.u2 = u[2];
+        iox.d0 = d[0]; iox.d1 = d[1]; iox.d2 = d[2];
+        iox.comp = comp;
+    }
+    iox.pdf = pdf;
+    ProductIO pio{};
+    pio.material = material;
+    for (int i = 0; i < 9; ++i) pio.F[i] = frame[i];
+    pio.h = h;
+    pio.choice = choice;
+    const BsdfTab bt{bw, bmean, bcov, B, M, diffuse};
+    hipError_t e = hipMemsetAsync(fb_count, 0, sizeof(int), st);
+    if (e != hipSuccess) return e;
+    const int32_t* perm = nullptr;
+    if (sort) {
+        e = coherent_order(c, (int)nq, sort->keys[0], sort->keys[1], sort->idx[0], sort->idx[1], sort->temp,
+                           sort->temp_bytes, st);
+        if (e != hipSuccess) return e;
+        perm = sort->idx[1];
+    }
+    const STNodeDev* nd = (const STNodeDev*)nodes;
+    const GuideMix* tb = (const GuideMix*)tab;
+    const float* const* cc = (const float* const*)cctab;
+    const dim3 grid((unsigned)((nq + 63) / 64));
+#define SDMM_TREE_PRODUCT_CAND(P, L)                                                                         \
+    hipLaunchKernelGGL((guide_tree_product_cand_kernel<P, L>), grid, dim3(64), 0, st, nd, tb, cc, nq, iox, pio, \
+                       bt, gc, cap, fb_count, fb_list, perm, node_out)
+    if (pdf_only) {
+        if (cap <= 16) SDMM_TREE_PRODUCT_CAND(true, 16);
+        else if (cap <= 24) SDMM_TREE_PRODUCT_CAND(true, 24);
+        else SDMM_TREE_PRODUCT_CAND(true, kGuideCap);
+    } else {
+        if (cap <= 16) SDMM_TREE_PRODUCT_CAND(false, 16);
+        else if (cap <= 24) SDMM_TREE_PRODUCT_CAND(false, 24);
+        else SDMM_TREE_PRODUCT_CAND(false, kGuideCap);
+    }
+#undef SDMM_TREE_PRODUCT_CAND
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const unsigned fblocks = (unsigned)(cus * 4 * SDMM_PRODUCT_WPE);
+    float* pscratch = nullptr;
+    const size_t sbytes = sizeof(float) * kPcStride * (size_t)kProductPairCap * fblocks;
+    if (hipMallocAsync((void**)&pscratch, sbytes, st) != hipSuccess) {
+        (void)hipGetLastError();
+        pscratch = nullptr;   // no scratch: the pairs are recomputed (same results)
+    }
+    if (pdf_only)
+        hipLaunchKernelGGL(guide_tree_product_wave_kernel<true>, dim3(fblocks), dim3(64), lds, st, nd, tb, cc, kmax,
+                           iox, pio, bt, gc, pscratch, kProductPairCap, fb_count, fb_list);
+    else
+        hipLaunchKernelGGL(guide_tree_product_wave_kernel<false>, dim3(fblocks), dim3(64), lds, st, nd, tb, cc,
+                           kmax, iox, pio, bt, gc, pscratch, kProductPairCap, fb_count, fb_list);
     e = hipGetLastError();
     if (pscratch) {
         const hipError_t f = hipFreeAsync(pscratch, st);

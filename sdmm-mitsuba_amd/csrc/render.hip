@@ -200,12 +200,18 @@ li_query_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, i
     Q.u0[i] = rng_uniform(seed, gp, stream, 3);
     Q.u1[i] = rng_uniform(seed, gp, stream, 4);
     Q.u2[i] = rng_uniform(seed, gp, stream, 5);
-    Q.mode[i] = (!guided || rng_uniform(seed, gp, stream, 2) <= h) ? 1 : 0;
+    const float choice = rng_uniform(seed, gp, stream, 2);
+    Q.ch[i] = choice;
+    Q.mode[i] = (!guided || choice <= h) ? 1 : 0;
 }
 
-// the live guided queries, compacted: query j serves path idx[j]
+// the live guided queries, compacted: query j serves path idx[j].  With
+// product sampling also the query's shading frame F = [s t n] (Frame(n) of
+// the hit quad), its material (the quad's BSDF: its learned-BSDF table row;
+// diffuse here, so getDMM succeeds for every live path, cosTheta(wi) > 0,
+// bsdfs/diffuse.cpp:86-92) and the BSDF/guide draw.
 __global__ void __launch_bounds__(256)
-li_compact_kernel(QueryDev Q, const int32_t* __restrict__ count) {
+li_compact_kernel(SceneDev S, PathsDev P, QueryDev Q, const int32_t* __restrict__ count, int product) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= *count) return;
     const int i = Q.idx[j];
@@ -214,13 +220,30 @@ li_compact_kernel(QueryDev Q, const int32_t* __restrict__ count) {
     Q.k_b0[j] = Q.b0[i]; Q.k_b1[j] = Q.b1[i]; Q.k_b2[j] = Q.b2[i];
     Q.k_mode[j] = Q.mode[i];
     Q.slot[i] = j;
+    if (product) {
+        const QuadDev& QD = S.quads[P.quad[i]];
+        float s[3], t[3];
+        frame_of(QD.n, s, t);
+        for (int r = 0; r < 3; ++r) {
+            Q.k_F[3 * r][j] = s[r];
+            Q.k_F[3 * r + 1][j] = t[r];
+            Q.k_F[3 * r + 2][j] = QD.n[r];
+        }
+        Q.k_mat[j] = QD.bsdf;
+        Q.k_ch[j] = Q.ch[i];
+    }
 }
 
 // ---------------------------------------------------------------------------
 // The rest of the bounce (:392-507, :759-871).
+// product: the query's own heuristicConditionalWeight (0.3 with a usable
+// product, 0.5 for the plain conditional, sdmm_proc.cpp:383-392) replaces h.
+// The wavefront marks a query whose BSDF sample was chosen comp == -2 (valid
+// conditional) -- the plain bounce's pdf_mode and the product bounce's
+// choice <= h alike.
 __global__ void __launch_bounds__(256)
 li_shade_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, int rr_depth, float h,
-                uint64_t seed) {
+                uint64_t seed, int product) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.P) return;
     int depth = P.depth[i];
@@ -232,6 +255,7 @@ li_shade_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, i
     const int j = Q.slot[i];            // the path's guided query (-1: none, BSDF only)
     const int comp = j >= 0 ? Q.comp[j] : -1;
     const bool valid = comp != -1;      // validConditional (:368)
+    if (product && valid) h = Q.hq[j];
     float wo[3], weight[3], mis_pdf;
     if (!valid) {
         // BSDF only, h = 1 (:316-323, :392-405): weight = rho, pdf = bsdfPdf
@@ -239,7 +263,7 @@ li_shade_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, i
         const float cos_o = dot3(wo, n);
         mis_pdf = kInvPi * cos_o;
         for (int ch = 0; ch < 3; ++ch) weight[ch] = rho[ch];
-    } else if (Q.mode[i]) {
+    } else if (comp == -2) {
         // BSDF chosen: (bsdf weight * bsdfPdf) / (h bsdfPdf + (1 - h) gmmPdf) (:393-407, :587-589)
         wo[0] = Q.b0[i]; wo[1] = Q.b1[i]; wo[2] = Q.b2[i];
         const float bsdf_pdf = kInvPi * dot3(wo, n);
@@ -466,18 +490,20 @@ size_t li_select_temp_bytes(int64_t n) {
     return b;
 }
 // live guided queries -> compact planes; *count_dev = their number
-hipError_t launch_li_compact(const QueryDev& Q, int64_t n, int32_t* count_dev, void* temp, size_t temp_bytes,
-                             hipStream_t st) {
+hipError_t launch_li_compact(const SceneDev& S, const PathsDev& P, const QueryDev& Q, int64_t n, int32_t* count_dev,
+                             void* temp, size_t temp_bytes, int product, hipStream_t st) {
     hipError_t e = hipcub::DeviceSelect::Flagged(temp, temp_bytes, hipcub::CountingInputIterator<int32_t>(0), Q.live,
                                                  Q.idx, count_dev, (int)n, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(li_compact_kernel, grid_for(n), dim3(256), 0, st, Q, (const int32_t*)count_dev);
+    hipLaunchKernelGGL(li_compact_kernel, grid_for(n), dim3(256), 0, st, S, P, Q, (const int32_t*)count_dev,
+                       product);
     return hipGetLastError();
 }
 
 hipError_t launch_li_shade(const SceneDev& S, const PathsDev& P, const QueryDev& Q, int64_t path0, int bounce,
-                           int rr_depth, float h, uint64_t seed, hipStream_t st) {
-    hipLaunchKernelGGL(li_shade_kernel, grid_for(P.P), dim3(256), 0, st, S, P, Q, path0, bounce, rr_depth, h, seed);
+                           int rr_depth, float h, uint64_t seed, int product, hipStream_t st) {
+    hipLaunchKernelGGL(li_shade_kernel, grid_for(P.P), dim3(256), 0, st, S, P, Q, path0, bounce, rr_depth, h, seed,
+                       product);
     return hipGetLastError();
 }
 hipError_t launch_li_film(const PathsDev& P, int64_t pix0, int64_t npix, int spp, int64_t plane, float* image,

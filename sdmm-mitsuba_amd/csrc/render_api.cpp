@@ -21,10 +21,10 @@ hipError_t launch_li_camera(const SceneDev& S, const PathsDev& P, int64_t path0,
 hipError_t launch_li_query(const SceneDev& S, const PathsDev& P, const QueryDev& Q, int64_t path0, int bounce,
                            int max_depth, int guided, float h, uint64_t seed, hipStream_t st);
 hipError_t launch_li_shade(const SceneDev& S, const PathsDev& P, const QueryDev& Q, int64_t path0, int bounce,
-                           int rr_depth, float h, uint64_t seed, hipStream_t st);
+                           int rr_depth, float h, uint64_t seed, int product, hipStream_t st);
 size_t li_select_temp_bytes(int64_t n);
-hipError_t launch_li_compact(const QueryDev& Q, int64_t n, int32_t* count_dev, void* temp, size_t temp_bytes,
-                             hipStream_t st);
+hipError_t launch_li_compact(const SceneDev& S, const PathsDev& P, const QueryDev& Q, int64_t n, int32_t* count_dev,
+                             void* temp, size_t temp_bytes, int product, hipStream_t st);
 hipError_t launch_li_film(const PathsDev& P, int64_t pix0, int64_t npix, int spp, int64_t plane, float* image,
                           float* image_sqr, hipStream_t st);
 }  // namespace sdmm
@@ -89,7 +89,8 @@ int grow(sdmm_scene* s, int64_t P, int V, hipStream_t st) {
     size_t tb = 0;
     (void)hipcub::DeviceReduce::Sum(nullptr, tb, (const int32_t*)nullptr, (int64_t*)nullptr, (int)cap);
     tb = std::max(tb, li_select_temp_bytes(cap));
-    const size_t need = 12 * f + 3 * i4 + recb + 13 * f + u1 + i4 + 256 + al(tb) + 9 * f + 2 * u1 + 3 * i4;
+    const size_t need = 12 * f + 3 * i4 + recb + 13 * f + u1 + i4 + 256 + al(tb) + 9 * f + 2 * u1 + 3 * i4 +
+                        (1 + 1 + 9 + 1) * f + i4;
     HIP_TRY(hipStreamSynchronize(st));
     if (s->buf) HIP_TRY(hipFree(s->buf));
     s->buf = nullptr;
@@ -122,6 +123,11 @@ int grow(sdmm_scene* s, int64_t P, int V, hipStream_t st) {
     s->Q.idx = (int32_t*)take(i4);
     s->Q.slot = (int32_t*)take(i4);
     s->dcount = (int32_t*)take(i4);
+    s->Q.ch = (float*)take(f);
+    s->Q.k_ch = (float*)take(f);
+    for (int i = 0; i < 9; ++i) s->Q.k_F[i] = (float*)take(f);
+    s->Q.hq = (float*)take(f);
+    s->Q.k_mat = (int32_t*)take(i4);
     return SDMM_OK;
 }
 
@@ -246,6 +252,12 @@ int sdmm_li_render(sdmm_scene* s, sdmm_stree* t, const sdmm_mix* const* node_mix
         return fail(SDMM_E_INVALID, "sdmm_li_render: saved_vertices < max_depth - 1");
     if (p->guided && !(p->bsdf_fraction >= 0.0f && p->bsdf_fraction <= 1.0f))
         return fail(SDMM_E_INVALID, "sdmm_li_render: bsdf_fraction outside [0, 1]");
+    const int product = p->sample_product ? 1 : 0;
+    if (product) {
+        const sdmm_bsdf_table& lb = p->learned_bsdf;
+        if (lb.M < 1 || lb.M > 64 || lb.B < 1 || !lb.weights || !lb.means || !lb.covs)
+            return fail(SDMM_E_INVALID, "sdmm_li_render: sample_product needs a learned-BSDF table (B >= 1, 1 <= M <= 64)");
+    }
     const int64_t npix = p->pixel_end - p->pixel_begin;
     const int64_t P = npix * p->spp;
     if (P > INT32_MAX) return fail(SDMM_E_INVALID, "sdmm_li_render: at most 2^31 - 1 paths per call");
@@ -281,7 +293,7 @@ int sdmm_li_render(sdmm_scene* s, sdmm_stree* t, const sdmm_mix* const* node_mix
         if (p->guided) {
             // only the live paths query the guide: compact them (the order of
             // the compact queries does not change any query's outputs)
-            HIP_TRY(launch_li_compact(s->Q, P, s->dcount, s->temp, s->temp_bytes, st));
+            HIP_TRY(launch_li_compact(s->S, s->P, s->Q, P, s->dcount, s->temp, s->temp_bytes, product, st));
             HIP_TRY(hipMemcpyAsync(s->hcount, s->dcount, sizeof(int32_t), hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
             const int64_t nlive = *s->hcount;
@@ -290,8 +302,19 @@ int sdmm_li_render(sdmm_scene* s, sdmm_stree* t, const sdmm_mix* const* node_mix
             const float* bd[3] = {s->Q.k_b0, s->Q.k_b1, s->Q.k_b2};
             float* d[3] = {s->Q.d0, s->Q.d1, s->Q.d2};
             if (nlive > 0) {
-                r = sdmm_guide_pdf_wavefront(t, node_mix, nlive, c, u, bd, s->Q.k_mode, d, s->Q.pdf, s->Q.comp,
-                                             nullptr);
+                if (product) {
+                    // sampleSurface with sampleProduct (:327-392): the product
+                    // of the leaf's conditional and the material's learned
+                    // BSDF, h = 0.3 (0.5 without a usable product), the BSDF /
+                    // guide choice taken against the query's own h
+                    const float* F[9];
+                    for (int i = 0; i < 9; ++i) F[i] = s->Q.k_F[i];
+                    r = sdmm_guide_product_wavefront(t, node_mix, nlive, c, u, s->Q.k_ch, bd, &p->learned_bsdf,
+                                                     s->Q.k_mat, F, d, s->Q.pdf, s->Q.comp, s->Q.hq, nullptr);
+                } else {
+                    r = sdmm_guide_pdf_wavefront(t, node_mix, nlive, c, u, bd, s->Q.k_mode, d, s->Q.pdf,
+                                                 s->Q.comp, nullptr);
+                }
                 if (r) return r;
                 // (stream-ordered copy, read after the final synchronisation)
                 const int* fb = sdmm_detail::tree_fallback_count(t);
@@ -300,7 +323,7 @@ int sdmm_li_render(sdmm_scene* s, sdmm_stree* t, const sdmm_mix* const* node_mix
             }
             guided_queries += nlive;
         }
-        HIP_TRY(launch_li_shade(s->S, s->P, s->Q, path0, b, p->rr_depth, h, p->seed, st));
+        HIP_TRY(launch_li_shade(s->S, s->P, s->Q, path0, b, p->rr_depth, h, p->seed, product && p->guided, st));
     }
     HIP_TRY(launch_li_film(s->P, p->pixel_begin, npix, p->spp, npix_all, image, image_sqr, st));
     if (vout) {

@@ -70,6 +70,14 @@ struct QueryDev {
     int32_t* slot;
     float *k_c0, *k_c1, *k_c2, *k_u0, *k_u1, *k_u2, *k_b0, *k_b1, *k_b2;
     uint8_t* k_mode;
+    // product sampling (sampleProduct): the BSDF/guide draw per path (the
+    // wavefront decides with the query's own h), and per compact query the
+    // shading frame (row-major, columns s t n), the material and h out
+    float* ch;
+    float* k_ch;
+    float* k_F[9];
+    int32_t* k_mat;
+    float* hq;
 };
 
 }  // namespace sdmm

@@ -93,8 +93,17 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
                                 const float* const c[3], const float* const u[3], const float* const dgiven[3],
                                 float* const d[3], float* pdf, int32_t* comp, const int32_t* material,
                                 const float* const frame[9], float* h, const float* bw, const float* bmean,
-                                const float* bcov, int B, int M, float norm2, float norm3, int cap, int* fb_count,
-                                int32_t* fb_list, int cus, hipStream_t st, const GuideSortScratch* sort);
+                                const float* bcov, const uint8_t* diffuse, int B, int M, float norm2, float norm3,
+                                int cap, int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
+                                const GuideSortScratch* sort);
+hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const void* cctab, int kmax, int64_t nq,
+                                     const float* const c[3], const float* const u[3], const float* choice,
+                                     const float* const dgiven[3], float* const d[3], float* pdf, int32_t* comp,
+                                     int32_t* node_out, const int32_t* material, const float* const frame[9],
+                                     float* h, const float* bw, const float* bmean, const float* bcov,
+                                     const uint8_t* diffuse, int B, int M, float norm2, float norm3, int cap,
+                                     int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
+                                     const GuideSortScratch* sort);
 #ifndef SDMM_GUIDE_CAP_MAX
 #define SDMM_GUIDE_CAP_MAX 40
 #endif
@@ -1769,7 +1778,8 @@ int sdmm_guide_product_batch(const sdmm_mix* m, int64_t nq, const float* const c
     if (r) return r;
     if ((r = ensure_guide_scratch(m, nq))) return r;
     HIP_TRY(launch_guide_product(m->gp, m->Kp, m->K, m->C.condCov, nq, c, u, nullptr, d, pdf, comp, material,
-                                 frame, heuristic, bsdf->weights, bsdf->means, bsdf->covs, bsdf->B, bsdf->M,
+                                 frame, heuristic, bsdf->weights, bsdf->means, bsdf->covs, bsdf->diffuse, bsdf->B,
+                                 bsdf->M,
                                  m->norm2, m->norm3, m->guide_cap, m->guide_fb, m->guide_fb + 1, m->cus, m->stream,
                                  guide_order(m, nq)));
     return SDMM_OK;
@@ -1786,8 +1796,8 @@ int sdmm_pdf_product_batch(const sdmm_mix* m, int64_t nq, const float* const c[3
     if (r) return r;
     if ((r = ensure_guide_scratch(m, nq))) return r;
     HIP_TRY(launch_guide_product(m->gp, m->Kp, m->K, m->C.condCov, nq, c, nullptr, d, nullptr, pdf, nullptr,
-                                 material, frame, heuristic, bsdf->weights, bsdf->means, bsdf->covs, bsdf->B,
-                                 bsdf->M, m->norm2, m->norm3, m->guide_cap, m->guide_fb, m->guide_fb + 1, m->cus,
+                                 material, frame, heuristic, bsdf->weights, bsdf->means, bsdf->covs, bsdf->diffuse,
+                                 bsdf->B, bsdf->M, m->norm2, m->norm3, m->guide_cap, m->guide_fb, m->guide_fb + 1, m->cus,
                                  m->stream, guide_order(m, nq)));
     return SDMM_OK;
 }
@@ -1946,9 +1956,12 @@ struct sdmm_stree {
     // guided wavefront: per-node mixture table (device + the host copy it
     // was uploaded from) and the guided-batch scratch
     std::vector<GuideMixHost> tab_host;
-    void* dtab = nullptr;
+    std::vector<const float*> cc_host;   // per node: the mixture's condCov (product wavefront)
+    void* dtab = nullptr;                // [nn] GuideMix, then [nn] condCov pointers (dcctab)
+    void* dcctab = nullptr;
     size_t dtab_cap = 0;
     int tab_kmax = 0;
+    int tab_cap = kGuideCapMax; // candidate capacity: the smallest of the bound mixtures' (sdmm_set_guide_capacity)
     bool tab_valid = false;     // bound table matches the current nodes
     int* guide_fb = nullptr;
     int64_t guide_fb_cap = 0;
@@ -2402,7 +2415,8 @@ namespace {
 int st_upload_table(sdmm_stree* t, const sdmm_mix* const* node_mix) {
     const size_t nn = t->nodes.size();
     std::vector<GuideMixHost> tab(nn);
-    int kmax = 0;
+    std::vector<const float*> cc(nn, nullptr);
+    int kmax = 0, cap = kGuideCapMax;
     t->mix_streams.clear();
     for (size_t i = 0; i < nn; ++i) {
         const sdmm_mix* m = node_mix[i];
@@ -2410,7 +2424,9 @@ int st_upload_table(sdmm_stree* t, const sdmm_mix* const* node_mix) {
         if (!m || !m->initialised) continue;
         if (m->device != t->device) return fail(SDMM_E_INVALID, "wavefront: mixture on another device");
         tab[i] = GuideMixHost{m->gp, m->Kp, m->K};
+        cc[i] = m->C.condCov;
         kmax = std::max(kmax, m->K);
+        cap = std::min(cap, m->guide_cap);
         if (m->stream != t->stream &&
             std::find(t->mix_streams.begin(), t->mix_streams.end(), m->stream) == t->mix_streams.end())
             t->mix_streams.push_back(m->stream);
@@ -2420,28 +2436,35 @@ int st_upload_table(sdmm_stree* t, const sdmm_mix* const* node_mix) {
         HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         t->mix_events.push_back(e);
     }
-    bool same = tab.size() == t->tab_host.size();
+    bool same = tab.size() == t->tab_host.size() && cc == t->cc_host;
     for (size_t i = 0; same && i < nn; ++i) same = !(tab[i] != t->tab_host[i]);
     t->tab_kmax = kmax;
+    t->tab_cap = cap;
     t->tab_valid = true;
     if (same && t->dtab) return SDMM_OK;
     HIP_TRY(hipStreamSynchronize(t->stream));   // the previous copy may still read tab_host
-    const size_t bytes = sizeof(GuideMixHost) * (nn ? nn : 1);
+    const size_t nb = nn ? nn : 1;
+    const size_t bytes = (sizeof(GuideMixHost) + sizeof(const float*)) * nb;
     if (bytes > t->dtab_cap) {
         if (t->dtab) HIP_TRY(hipFree(t->dtab));
         t->dtab = nullptr;
         HIP_TRY(hipMalloc(&t->dtab, bytes));
         t->dtab_cap = bytes;
     }
+    t->dcctab = (char*)t->dtab + sizeof(GuideMixHost) * nb;
     t->tab_host.swap(tab);
+    t->cc_host.swap(cc);
     HIP_TRY(hipMemcpyAsync(t->dtab, t->tab_host.data(), sizeof(GuideMixHost) * nn, hipMemcpyHostToDevice,
+                           t->stream));
+    HIP_TRY(hipMemcpyAsync(t->dcctab, t->cc_host.data(), sizeof(const float*) * nn, hipMemcpyHostToDevice,
                            t->stream));
     return SDMM_OK;
 }
 
-int st_guide(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
-             const float* const u[3], const float* const dgiven[3], float* const d[3], float* pdf, int32_t* comp,
-             int32_t* node_out, const uint8_t* pmode = nullptr) {
+// The wavefronts' common prologue: device nodes and mixture table current,
+// scratch for nq queries, the tree's stream ordered after the mixtures'
+// pending work on their own streams.  *cus: the device's CUs.
+int st_prepare(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, int* cus) {
     HIP_TRY(hipSetDevice(t->device));
     int r = st_upload(t);
     if (r) return r;
@@ -2453,20 +2476,44 @@ int st_guide(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const f
     }
     r = grow_guide_scratch(t->guide_fb, t->guide_fb_cap, t->guide_sort, t->stream, nq);
     if (r) return r;
-    // order the wavefront after the mixtures' pending work on their own streams
     for (size_t i = 0; i < t->mix_streams.size(); ++i) {
         HIP_TRY(hipEventRecord(t->mix_events[i], t->mix_streams[i]));
         HIP_TRY(hipStreamWaitEvent(t->stream, t->mix_events[i], 0));
     }
+    *cus = 256;
+    (void)hipDeviceGetAttribute(cus, hipDeviceAttributeMultiprocessorCount, t->device);
+    if (*cus <= 0) *cus = 256;
+    return SDMM_OK;
+}
+
+int st_guide(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
+             const float* const u[3], const float* const dgiven[3], float* const d[3], float* pdf, int32_t* comp,
+             int32_t* node_out, const uint8_t* pmode = nullptr) {
     int cus = 256;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, t->device);
+    const int r = st_prepare(t, node_mix, nq, &cus);
+    if (r) return r;
     const GuideSortScratch* sort = nq >= (1 << 14) ? &t->guide_sort : nullptr;
     HIP_TRY(launch_guide_tree(t->dnodes, t->dtab, t->tab_kmax, nq, c, u, dgiven, d, pdf, comp, node_out,
-                              norm_const(2), norm_const(3), kGuideCapMax, t->guide_fb, t->guide_fb + 1,
-                              cus > 0 ? cus : 256, t->stream, sort, pmode,
+                              norm_const(2), norm_const(3), t->tab_cap, t->guide_fb, t->guide_fb + 1,
+                              cus, t->stream, sort, pmode,
                               // the NaN hand-off list of the group fallback: the
                               // Morton keys' input buffer, free once the order is built
                               (int*)t->guide_sort.keys[0]));
+    return SDMM_OK;
+}
+
+int st_guide_product(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
+                     const float* const u[3], const float* choice, const float* const dgiven[3],
+                     const sdmm_bsdf_table* bsdf, const int32_t* material, const float* const frame[9],
+                     float* const d[3], float* pdf, int32_t* comp, float* heuristic, int32_t* node_out) {
+    int cus = 256;
+    const int r = st_prepare(t, node_mix, nq, &cus);
+    if (r) return r;
+    const GuideSortScratch* sort = nq >= (1 << 14) ? &t->guide_sort : nullptr;
+    HIP_TRY(launch_guide_product_tree(t->dnodes, t->dtab, t->dcctab, t->tab_kmax, nq, c, u, choice, dgiven, d, pdf,
+                                      comp, node_out, material, frame, heuristic, bsdf->weights, bsdf->means,
+                                      bsdf->covs, bsdf->diffuse, bsdf->B, bsdf->M, norm_const(2), norm_const(3),
+                                      t->tab_cap, t->guide_fb, t->guide_fb + 1, cus, t->stream, sort));
     return SDMM_OK;
 }
 
@@ -2506,6 +2553,31 @@ int sdmm_pdf_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t n
     if (nq == 0) return SDMM_OK;
     if (!c || !d || !pdf) return fail(SDMM_E_INVALID, "invalid argument");
     return st_guide(t, node_mix, nq, c, nullptr, d, nullptr, pdf, nullptr, nullptr);
+}
+
+int sdmm_guide_product_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
+                                 const float* const u[3], const float* choice, const float* const dgiven[3],
+                                 const sdmm_bsdf_table* bsdf, const int32_t* material, const float* const frame[9],
+                                 float* const d[3], float* pdf, int32_t* comp, float* heuristic, int32_t* node_out) {
+    if (!t || nq < 0) return fail(SDMM_E_INVALID, "invalid argument");
+    if (nq == 0) return SDMM_OK;
+    if (!c || !u || !d || !pdf || !comp || (choice && !dgiven)) return fail(SDMM_E_INVALID, "invalid argument");
+    const int r = check_bsdf(bsdf, material, frame);
+    if (r) return r;
+    return st_guide_product(t, node_mix, nq, c, u, choice, choice ? dgiven : nullptr, bsdf, material, frame, d, pdf,
+                            comp, heuristic, node_out);
+}
+
+int sdmm_pdf_product_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
+                               const float* const d[3], const sdmm_bsdf_table* bsdf, const int32_t* material,
+                               const float* const frame[9], float* pdf, float* heuristic) {
+    if (!t || nq < 0) return fail(SDMM_E_INVALID, "invalid argument");
+    if (nq == 0) return SDMM_OK;
+    if (!c || !d || !pdf) return fail(SDMM_E_INVALID, "invalid argument");
+    const int r = check_bsdf(bsdf, material, frame);
+    if (r) return r;
+    return st_guide_product(t, node_mix, nq, c, nullptr, nullptr, d, bsdf, material, frame, nullptr, pdf, nullptr,
+                            heuristic, nullptr);
 }
 
 }  // extern "C"

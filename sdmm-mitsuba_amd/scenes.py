@@ -133,3 +133,20 @@ def cornell_box(width=640, height=360):
         "width": width,
         "height": height,
     }
+
+
+def diffuse_learned_bsdf(n_bsdfs: int, sigma: float = 0.65):
+    """Learned-BSDF tables for diffuse materials (the plugin's sampleProduct
+    path; the suite's `diffuse.sdmm` files are LFS pointers, so the table is
+    synthesised): per BSDF ONE directional lobe -- the plugin's diffuse case
+    re-centres only slice 0 on the shading normal (sdmm_proc.cpp:335-339), so
+    a diffuse learned BSDF is one lobe around the normal.  sigma: the lobe's
+    tangent-space standard deviation (0.65 rad ~ the spread of a cosine lobe).
+    Returns (weights (B, 1), local means (B, 1, 3), covs (B, 1, 4), diffuse (B,))."""
+    B = int(n_bsdfs)
+    w = np.ones((B, 1), np.float32)
+    m = np.zeros((B, 1, 3), np.float32)
+    m[..., 2] = 1.0
+    cov = np.zeros((B, 1, 4), np.float32)
+    cov[..., 0] = cov[..., 3] = sigma * sigma
+    return w, m, cov, np.ones(B, np.uint8)

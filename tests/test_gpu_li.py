@@ -291,6 +291,50 @@ def test_guided_render_unbiased_and_trained(pkg, oracle, scenes, gpu, plog):
     assert eg < 0.85 * eu
 
 
+def test_product_render_unbiased(pkg, oracle, scenes, gpu, plog):
+    """sampleProduct in the device Li (sdmm_proc.cpp:327-392): guided bounces
+    sample the product of the leaf's conditional with the diffuse material's
+    learned lobe (h = 0.3, 0.5 without a usable product), the BSDF/guide choice
+    against that h.  The image is unbiased against BSDF-only sampling, most
+    guided bounces use the product, and the training producer on a product
+    render still equals the host-routed oracle bitwise."""
+    import torch
+    sc = _scene(pkg, scenes, 160, 90)
+    tree = _tree(pkg, sc)
+    node_mix = _train(pkg, sc, tree, 6, 8)
+    desc = scenes.cornell_box(160, 90)
+    w, m, cov, dif = scenes.diffuse_learned_bsdf(len(desc["reflectance"]) // 3)
+    table = pkg.BsdfTable(w, m, cov, device=gpu, diffuse=dif)
+    img, verts, st = sc.render(tree, node_mix, spp=4, guided=True, seed=77, learned_bsdf=table)
+    assert np.isfinite(img.cpu().numpy()).all() and st["guided_queries"] > 0
+    _check_producer(pkg, oracle, tree, verts, 8, 0xABD, plog, "product")
+    spp = 64
+    lum = lambda im: im.cpu().numpy().mean(0).reshape(-1)
+    g = lum(sc.render(tree, node_mix, spp=spp, guided=True, seed=2345, learned_bsdf=table)[0])
+    u = lum(sc.render(tree, None, spp=spp, guided=False, seed=4321)[0])
+    mg, mu = g.mean(), u.mean()
+    se = np.sqrt(g.var() / g.size + u.var() / u.size)
+    plog("li_product_vs_unguided_mean_sigma", float(abs(mg - mu) / se), 4.0, product=float(mg), unguided=float(mu))
+    assert abs(mg - mu) < 4.0 * se, (mg, mu, se)
+    # the heuristic weights the wavefront chose: the product is usable for most
+    # trained-leaf bounces (a direct product-wavefront call on one bounce's queries)
+    nq = 4096
+    rng = np.random.default_rng(3)
+    c = rng.uniform(0.05, 0.95, size=(3, nq)).astype(np.float32)
+    uu = rng.uniform(0, 1, size=(3, nq)).astype(np.float32)
+    n = rng.normal(size=(nq, 3))
+    n /= np.linalg.norm(n, axis=1, keepdims=True)
+    F = np.stack([np.eye(3)] * nq).astype(np.float32)
+    F[:, :, 2] = n
+    tt = lambda a: [torch.from_numpy(np.ascontiguousarray(a[i])).to(gpu) for i in range(a.shape[0])]
+    mat = torch.zeros(nq, dtype=torch.int32, device=gpu)
+    _, _, comp, h = tree.guide_product(node_mix, tt(c), tt(uu), table, mat, tt(F.reshape(nq, 9).T))
+    h = h.cpu().numpy()
+    guided = h < 1.0
+    plog("li_product_usable_frac", float((h[guided] == np.float32(0.3)).mean()), 0.5, lower=True)
+    assert guided.sum() > nq // 4 and (h[guided] == np.float32(0.3)).mean() > 0.5
+
+
 @pytest.mark.parametrize("K", [16, 128])
 def test_native_guiding_model_equals_host_loop(pkg, scenes, gpu, plog, K):
     """sdmm_guiding_* (the C++ model) == the host loop above, bitwise: the
