@@ -27,6 +27,13 @@
  *     samples (`cacheable`, :764, :821-846) with the normal flipped to the
  *     wi side (:765-767), recordRadiance (:615-637), Russian roulette after
  *     rrDepth with q = min(max(throughput) eta^2, 0.95) (:788, :858-868);
+ *   - sampleProduct (:327-392): the BSDF's learned DMM (getDMM, :327-329;
+ *     the diffuse case re-centres slice 0 on the wi-side normal, :335-339,
+ *     otherwise rotate_to_wo(wi), :341-354 -- sdmm-lib calls the maintainer's
+ *     build keeps) is handed to sdmm_guide_product_wavefront as one table row
+ *     per query (lobes in the local frame, the shading frame per query),
+ *     which multiplies it with the leaf's conditional, picks h = 0.3 (0.5
+ *     without a usable product) and the BSDF/guide choice against that h;
  *   - bsdfOnly: no training (:416), so no leaf ever holds an initialised
  *     context and every bounce takes the BSDF-only branch (:316-323); the
  *     learned-BSDF-only branch (:331, :384, :410-413) is unreachable in the
@@ -62,6 +69,10 @@
 
 MTS_NAMESPACE_BEGIN
 
+// learned-BSDF lobes per product query (a row of the per-tile table); a
+// learned DMM with more slices is an error
+constexpr int kMaxLobes = 32;
+
 namespace {
 
 void check_sdmm(int rc, const char* what) {
@@ -85,16 +96,46 @@ struct Staging {
     uint8_t* d_mode = nullptr;
     float* d_out = nullptr;
     int32_t* d_comp = nullptr;
+    // sampleProduct: per query its learned-BSDF row (weights, local means,
+    // 2x2 covs, diffuse flag), material = its own row (-1: none), the
+    // shading frame (9 planes), the BSDF/guide draw, and h out
+    float* h_bw = nullptr;
+    float* h_bmean = nullptr;
+    float* h_bcov = nullptr;
+    uint8_t* h_bdiff = nullptr;
+    int32_t* h_mat = nullptr;
+    float* h_pf = nullptr;       // frame 9 planes, choice, h
+    float* d_bw = nullptr;
+    float* d_bmean = nullptr;
+    float* d_bcov = nullptr;
+    uint8_t* d_bdiff = nullptr;
+    int32_t* d_mat = nullptr;
+    float* d_pf = nullptr;
     // saved-vertex records of the tile's paths (sdmm_path_vertices layout)
     float* h_rec = nullptr;
     int32_t* h_nv = nullptr;
     float* d_rec = nullptr;
     int32_t* d_nv = nullptr;
 
-    void allocate(int64_t n, int vslots) {
+    void allocate(int64_t n, int vslots, bool product) {
         release();
         cap = n;
         V = vslots;
+        if (product) {
+            const size_t L = (size_t)n * kMaxLobes;
+            check_hip(hipHostMalloc((void**)&h_bw, sizeof(float) * L, hipHostMallocDefault), "hipHostMalloc");
+            check_hip(hipHostMalloc((void**)&h_bmean, sizeof(float) * 3 * L, hipHostMallocDefault), "hipHostMalloc");
+            check_hip(hipHostMalloc((void**)&h_bcov, sizeof(float) * 4 * L, hipHostMallocDefault), "hipHostMalloc");
+            check_hip(hipHostMalloc((void**)&h_bdiff, n, hipHostMallocDefault), "hipHostMalloc");
+            check_hip(hipHostMalloc((void**)&h_mat, sizeof(int32_t) * n, hipHostMallocDefault), "hipHostMalloc");
+            check_hip(hipHostMalloc((void**)&h_pf, sizeof(float) * 11 * n, hipHostMallocDefault), "hipHostMalloc");
+            check_hip(hipMalloc((void**)&d_bw, sizeof(float) * L), "hipMalloc");
+            check_hip(hipMalloc((void**)&d_bmean, sizeof(float) * 3 * L), "hipMalloc");
+            check_hip(hipMalloc((void**)&d_bcov, sizeof(float) * 4 * L), "hipMalloc");
+            check_hip(hipMalloc((void**)&d_bdiff, n), "hipMalloc");
+            check_hip(hipMalloc((void**)&d_mat, sizeof(int32_t) * n), "hipMalloc");
+            check_hip(hipMalloc((void**)&d_pf, sizeof(float) * 11 * n), "hipMalloc");
+        }
         check_hip(hipHostMalloc((void**)&h_in, sizeof(float) * 9 * n, hipHostMallocDefault), "hipHostMalloc");
         check_hip(hipHostMalloc((void**)&h_mode, n, hipHostMallocDefault), "hipHostMalloc");
         check_hip(hipHostMalloc((void**)&h_out, sizeof(float) * 4 * n, hipHostMallocDefault), "hipHostMalloc");
@@ -109,10 +150,15 @@ struct Staging {
         check_hip(hipMalloc((void**)&d_nv, sizeof(int32_t) * n), "hipMalloc");
     }
     void release() {
-        for (void* p : {(void*)h_in, (void*)h_mode, (void*)h_out, (void*)h_comp, (void*)h_rec, (void*)h_nv})
+        for (void* p : {(void*)h_in, (void*)h_mode, (void*)h_out, (void*)h_comp, (void*)h_rec, (void*)h_nv,
+                        (void*)h_bw, (void*)h_bmean, (void*)h_bcov, (void*)h_bdiff, (void*)h_mat, (void*)h_pf})
             if (p) (void)hipHostFree(p);
-        for (void* p : {(void*)d_in, (void*)d_mode, (void*)d_out, (void*)d_comp, (void*)d_rec, (void*)d_nv})
+        for (void* p : {(void*)d_in, (void*)d_mode, (void*)d_out, (void*)d_comp, (void*)d_rec, (void*)d_nv,
+                        (void*)d_bw, (void*)d_bmean, (void*)d_bcov, (void*)d_bdiff, (void*)d_mat, (void*)d_pf})
             if (p) (void)hipFree(p);
+        h_bw = h_bmean = h_bcov = h_pf = d_bw = d_bmean = d_bcov = d_pf = nullptr;
+        h_bdiff = d_bdiff = nullptr;
+        h_mat = d_mat = nullptr;
         h_in = h_out = d_in = d_out = h_rec = d_rec = nullptr;
         h_mode = d_mode = nullptr;
         h_comp = d_comp = h_nv = d_nv = nullptr;
@@ -133,7 +179,7 @@ struct PathState {
     // the BSDF sample drawn before the query (its direction is the pdf query's)
     Spectrum bsdfWeight;
     Float bsdfPdf;
-    bool pdfMode;        // the BSDF was chosen (rnd <= h)
+    bool pdfMode;        // the BSDF was chosen (rnd <= h; with sampleProduct the wavefront decides, comp -2)
     bool cacheable;      // !(bRec.sampledType & EDelta): the vertex is saved (:764)
     Float eta;           // relative IOR along the path (:604, :788)
 };
@@ -160,9 +206,6 @@ public:
         if (m_maxDepth <= 0 && m_maxDepth != -1)
             Log(EError, "'maxDepth' must be set to -1 (infinite) or a value greater than zero!");
         if (m_maxDepth != m_rrDepth) Log(EError, "'maxDepth' must match 'rrDepth' for the SDMM integrator!");
-        if (m_sampleProduct)
-            Log(EError, "'sampleProduct' needs the materials' learned-BSDF tables "
-                        "(sdmm_guide_product_batch); not wired for generic Mitsuba BSDFs");
     }
 
     SDMMAmdPathTracer(Stream* stream, InstanceManager* manager) : Integrator(stream, manager) {
@@ -324,7 +367,7 @@ private:
             ref<Sampler> sampler = static_cast<Sampler*>(scene->getSampler()->clone().get());
             Staging st;
             const int V = std::max(1, m_maxDepth > 0 ? std::min(m_maxDepth - 1, 10) : 10);
-            st.allocate((int64_t)T * T * m_samplesPerIteration, V);
+            st.allocate((int64_t)T * T * m_samplesPerIteration, V, m_sampleProduct && !m_bsdfOnly);
             for (int t = next++; t < tx * ty && !m_cancelled; t = next++) {
                 const int x0 = (t % tx) * T, y0 = (t / tx) * T;
                 const int w = std::min(T, size.x - x0), h = std::min(T, size.y - y0);
@@ -397,6 +440,7 @@ private:
                 s.pdfMode = choice <= hWeight;
                 const Vector dB = s.its.toWorld(bRec.wo);
                 const int64_t q = nq++;
+                if (st.h_mat) learnedRow(st, bsdf, bRec, s.its, q, n, (float)choice);
                 float* in = st.h_in;
                 const Point c((s.its.p - m_sceneMin) / m_spatialNorm);        // createCondition (:263-273)
                 in[0 * n + q] = (float)c.x; in[1 * n + q] = (float)c.y; in[2 * n + q] = (float)c.z;
@@ -409,6 +453,7 @@ private:
             }
             if (live == 0) break;
             if (nq > 0) guideWavefront(st, n, nq);
+            const bool productBounce = nq > 0 && st.h_mat != nullptr;
             // shade (:392-507, :759-871)
             for (int64_t p = 0; p < n; ++p) {
                 PathState& s = P[(size_t)p];
@@ -423,13 +468,16 @@ private:
                     pdf = s.bsdfPdf;
                 } else {
                     const Float gmmPdf = st.h_out[3 * n + s.query];
+                    // h: 0.5, or the product query's own 0.3 / 0.5 (:383-392)
+                    const Float hq = productBounce ? (Float)st.h_pf[10 * n + s.query] : hWeight;
+                    s.pdfMode = comp == -2;            // the BSDF sample was chosen (:392)
                     if (!s.pdfMode) {                  // the guide's direction
                         const Vector d(st.h_out[0 * n + s.query], st.h_out[1 * n + s.query],
                                        st.h_out[2 * n + s.query]);
                         bRec.wo = s.its.toLocal(d);
                     }
                     const Float bsdfPdf = bsdf->pdf(bRec);
-                    pdf = bsdfPdf > 0 ? hWeight * bsdfPdf + (1 - hWeight) * gmmPdf : 0;   // (:587-589)
+                    pdf = bsdfPdf > 0 ? hq * bsdfPdf + (1 - hq) * gmmPdf : 0;   // (:587-589)
                     weight = pdf > 0 ? bsdf->eval(bRec) / pdf : Spectrum(0.0f);
                 }
                 const Vector wo = s.its.toWorld(bRec.wo);
@@ -531,6 +579,45 @@ private:
         }
     }
 
+    // sampleProduct: query q's learned-BSDF row (:327-356).  getDMM / the
+    // diffuse re-centring / rotate_to_wo are the BSDF's and sdmm-lib's calls
+    // (the maintainer's build has both); the lobes go over in the local
+    // shading frame with the frame F = [s t n] per query -- the kernel forms
+    // mean F m and frame Coordinates(m) F^T (:348-355).  A diffuse BSDF keeps
+    // its lobes as loaded and is flagged: the kernel re-centres slice 0 on
+    // F's third column (the shading normal; getDMM fails from the back side,
+    // so no flip is needed) exactly as set_mean does (:335-339).
+    void learnedRow(Staging& st, const BSDF* bsdf, BSDFSamplingRecord& bRec, const Intersection& its, int64_t q,
+                    int64_t n, float choice) {
+        st.h_mat[q] = -1;
+        for (int f = 0; f < 3; ++f)
+            for (int c = 0; c < 3; ++c) {
+                const Vector col = c == 0 ? its.shFrame.s : (c == 1 ? its.shFrame.t : its.shFrame.n);
+                st.h_pf[(size_t)(3 * f + c) * n + q] = (float)col[f];
+            }
+        st.h_pf[9 * n + q] = choice;
+        BSDF::DMM learned;
+        if (!bsdf->getDMM(bRec, learned)) return;          // no learned BSDF: the plain conditional (h 0.5)
+        const auto type = bsdf->getType();
+        const bool diffuse = (type & BSDF::EDiffuseReflection) == (type & BSDF::EAll);
+        if (!diffuse) enoki::packet(learned.tangent_space, 0).rotate_to_wo({bRec.wi[0], bRec.wi[1], bRec.wi[2]});
+        const size_t M = enoki::slices(learned);
+        if (M > (size_t)kMaxLobes) Log(EError, "learned BSDF with %i lobes (max %i)", (int)M, kMaxLobes);
+        float* w = st.h_bw + (size_t)q * kMaxLobes;
+        float* mean = st.h_bmean + (size_t)q * kMaxLobes * 3;
+        float* cov = st.h_bcov + (size_t)q * kMaxLobes * 4;
+        for (int j = 0; j < kMaxLobes; ++j) {
+            w[j] = (size_t)j < M ? (float)enoki::slice(learned.weight.pmf, j) : 0.0f;   // 0: skipped
+            if ((size_t)j >= M) continue;
+            auto lobe = enoki::slice(learned.tangent_space, j);
+            for (int a = 0; a < 3; ++a) mean[3 * j + a] = (float)lobe.mean(a);
+            auto c2 = enoki::slice(learned.cov, j);
+            for (int a = 0; a < 4; ++a) cov[4 * j + a] = (float)c2(a / 2, a % 2);
+        }
+        st.h_bdiff[q] = diffuse ? 1 : 0;
+        st.h_mat[q] = (int32_t)q;
+    }
+
     // One guided bounce of a tile's wavefront: sampleSurface / pdfSurface for
     // nq queries (query planes of stride n) in one call on the model's stream.
     void guideWavefront(Staging& st, int64_t n, int64_t nq) {
@@ -543,9 +630,34 @@ private:
         const float* u[3] = {st.d_in + 3 * n, st.d_in + 4 * n, st.d_in + 5 * n};
         const float* dg[3] = {st.d_in + 6 * n, st.d_in + 7 * n, st.d_in + 8 * n};
         float* d[3] = {st.d_out, st.d_out + n, st.d_out + 2 * n};
-        check_sdmm(sdmm_guide_pdf_wavefront(sdmm_guiding_tree(m_guiding), nullptr, nq, c, u, dg, st.d_mode, d,
-                                            st.d_out + 3 * n, st.d_comp, nullptr),
-                   "sdmm_guide_pdf_wavefront");
+        if (st.h_mat) {
+            // sampleProduct: the per-query table rows, frames and draws
+            const size_t L = (size_t)nq * kMaxLobes;
+            check_hip(hipMemcpyAsync(st.d_bw, st.h_bw, sizeof(float) * L, hipMemcpyHostToDevice, m_stream), "upload");
+            check_hip(hipMemcpyAsync(st.d_bmean, st.h_bmean, sizeof(float) * 3 * L, hipMemcpyHostToDevice, m_stream),
+                      "upload");
+            check_hip(hipMemcpyAsync(st.d_bcov, st.h_bcov, sizeof(float) * 4 * L, hipMemcpyHostToDevice, m_stream),
+                      "upload");
+            check_hip(hipMemcpyAsync(st.d_bdiff, st.h_bdiff, nq, hipMemcpyHostToDevice, m_stream), "upload");
+            check_hip(hipMemcpyAsync(st.d_mat, st.h_mat, sizeof(int32_t) * nq, hipMemcpyHostToDevice, m_stream),
+                      "upload");
+            for (int f = 0; f < 10; ++f)
+                check_hip(hipMemcpyAsync(st.d_pf + f * n, st.h_pf + f * n, sizeof(float) * nq, hipMemcpyHostToDevice,
+                                         m_stream), "upload");
+            const sdmm_bsdf_table tab{st.d_bw, st.d_bmean, st.d_bcov, (int)nq, kMaxLobes, st.d_bdiff};
+            const float* F[9];
+            for (int f = 0; f < 9; ++f) F[f] = st.d_pf + f * n;
+            check_sdmm(sdmm_guide_product_wavefront(sdmm_guiding_tree(m_guiding), nullptr, nq, c, u, st.d_pf + 9 * n,
+                                                    dg, &tab, st.d_mat, F, d, st.d_out + 3 * n, st.d_comp,
+                                                    st.d_pf + 10 * n, nullptr),
+                       "sdmm_guide_product_wavefront");
+            check_hip(hipMemcpyAsync(st.h_pf + 10 * n, st.d_pf + 10 * n, sizeof(float) * nq, hipMemcpyDeviceToHost,
+                                     m_stream), "download h");
+        } else {
+            check_sdmm(sdmm_guide_pdf_wavefront(sdmm_guiding_tree(m_guiding), nullptr, nq, c, u, dg, st.d_mode, d,
+                                                st.d_out + 3 * n, st.d_comp, nullptr),
+                       "sdmm_guide_pdf_wavefront");
+        }
         for (int f = 0; f < 4; ++f)
             check_hip(hipMemcpyAsync(st.h_out + f * n, st.d_out + f * n, sizeof(float) * nq, hipMemcpyDeviceToHost,
                                      m_stream), "download directions");
