@@ -230,7 +230,45 @@ def wavefront_bench(pkg, synth, batch, shard, tree, dev, stream, ct, ut, gout, t
             "guided_frac": float((comp >= 0).mean()), "scaling": "weak (replicas: queries per rank)"}
 
 
-def cornell_bench(pkg, dev, args, world, optimize_async=0, K=16, product=False):
+def cornell_cpu_baseline(pkg, g, desc, spp, seed, threads, learned=None, budget_s=6.0):
+    """The CPU restatement of Li (oracle/sdmm_oracle_li.inc) rendering the same
+    guided pass (the trained model's leaves as oracle mixtures, the same tree,
+    seed and spp) over a bounded slice of the image on `threads` host threads:
+    guided rays/s = bounce rays traced / wall time (the reference's CPU Li
+    cannot run here: no Mitsuba)."""
+    sys.path.insert(0, str(ROOT))
+    from oracle import oracle as orc
+    orc.build()
+    mixes = []
+    for m in g.node_mixtures():
+        if m is None:
+            mixes.append(None)
+            continue
+        p = m.get_params()
+        om = orc.Mixture(m.K)
+        om.copy_params_from(p)
+        om.valid[:] = p["valid"]
+        mixes.append(om)
+    aabb, child, _ = g.tree.nodes()
+    npix = desc["width"] * desc["height"]
+    kw = dict(node_mix=mixes, guided=True, spp=spp, seed=seed, learned=learned, threads=threads)
+    t = time.perf_counter()
+    r = orc.li_render(desc, aabb, child, pixels=(0, 512), **kw)          # probe
+    dt = time.perf_counter() - t
+    n = int(min(npix, max(512, 512 * budget_s / max(dt, 1e-3))))
+    t = time.perf_counter()
+    r = orc.li_render(desc, aabb, child, pixels=(0, n), **kw)
+    dt = time.perf_counter() - t
+    rays = int(r["nv"].sum())
+    return {"value": rays / dt, "unit": "rays/s", "cores": threads, "kind": "port",
+            "sample": f"guided pass of the trained model, first {n} of {npix} pixels x {spp} spp "
+                      f"({n * spp} paths, {rays} bounce rays): oracle or_li_render (CPU restatement of "
+                      f"SDMMRenderer::Li with the oracle's conditional{' and product' if learned else ''}) "
+                      f"on {threads} host threads",
+            "seconds": dt}
+
+
+def cornell_bench(pkg, dev, args, world, optimize_async=0, K=16, product=False, cpu=False):
     """configs[0] on the device: the test suite's Cornell Box (640x360), K=16
     per leaf (K=128: the Torus line's K, configs[2], over the one scene whose
     geometry the snapshot holds), 64 spp rendered 8 spp per iteration, training (push + optimize)
@@ -243,10 +281,10 @@ def cornell_bench(pkg, dev, args, world, optimize_async=0, K=16, product=False):
     desc = scenes.cornell_box(640, 360)
     sc = pkg.Scene(desc, device=dev.index)
     _, _, tmin, tmax = sc.normalization()
-    table = None
+    table = learned = None
     if product:   # sampleProduct: every Cornell BSDF is diffuse, one learned lobe each
-        w, m, cov, dif = scenes.diffuse_learned_bsdf(len(desc["reflectance"]) // 3)
-        table = pkg.BsdfTable(w, m, cov, device=dev, diffuse=dif)
+        learned = scenes.diffuse_learned_bsdf(len(desc["reflectance"]) // 3)
+        table = pkg.BsdfTable(*learned[:3], device=dev, diffuse=learned[3])
     spp_total, spp_it = 64, 8
     img = torch.zeros(3, 360, 640, device=dev)
     acc = torch.zeros_like(img)
@@ -272,12 +310,19 @@ def cornell_bench(pkg, dev, args, world, optimize_async=0, K=16, product=False):
     guided = [x for x in its if not x["train"]]
     seg = sum(x["segments"] for x in guided)
     gms = sum(x["ms"] for x in guided)
-    return {"workload": f"Cornell Box 640x360, K={K} per leaf, 64 spp (8 per iteration, training for the first 16)",
+    res = {"workload": f"Cornell Box 640x360, K={K} per leaf, 64 spp (8 per iteration, training for the first 16)",
             "total_ms": total * 1e3, "guided_rays_per_s": seg / (gms * 1e-3),
             "guided_paths_per_s": sum(x["paths"] for x in guided) / (gms * 1e-3),
             "trained_leaves": its[-1]["trained"], "iterations": its,
             "image_mean": float((acc / len(its)).mean().item()), "replicas": world,
             "optimize_async": bool(optimize_async), "sample_product": bool(product)}
+    if cpu:
+        try:
+            res["cpu_baseline"] = cornell_cpu_baseline(pkg, g, desc, spp_it, 1 + len(its) - 1, host_threads(),
+                                                       learned)
+        except Exception as e:  # reported, never required
+            res["cpu_baseline"] = {"value": None, "error": repr(e)}
+    return res
 
 
 def large_k_bench(pkg, synth, batch, shard, dev, stream, timed, args, world, N, comm):
@@ -553,15 +598,16 @@ def main():
                                                  timed, args, world)
 
     if not args.no_extra:
-        out["cornell"] = cornell_bench(pkg, dev, args, world)
+        cpu = rank == 0 and world == 1 and not args.no_cpu
+        out["cornell"] = cornell_bench(pkg, dev, args, world, cpu=cpu)
         out["cornell_async"] = cornell_bench(pkg, dev, args, world, optimize_async=1)
         # configs[2]'s K (Torus, K=128 guided path tracing with Li/sampleSurface
         # on the device): the Torus meshes are LFS pointers in the snapshot, so
         # the same guided renderer runs over the Cornell Box with K=128 leaves
-        out["cornell_k128"] = cornell_bench(pkg, dev, args, world, K=128)
+        out["cornell_k128"] = cornell_bench(pkg, dev, args, world, K=128, cpu=cpu)
         # sampleProduct (configs[4]'s learned-BSDF product sampling, sdmm_proc.cpp:327-392)
         # inside the full guided render: the Cornell BSDFs' synthesised diffuse lobes
-        out["cornell_product"] = cornell_bench(pkg, dev, args, world, product=True)
+        out["cornell_product"] = cornell_bench(pkg, dev, args, world, product=True, cpu=cpu)
 
     if not args.no_extra and not args.no_large_k:
         out["large_k"] = large_k_bench(pkg, synth, batch, shard, dev, stream, timed, args, world, N_global, comm)

@@ -455,3 +455,56 @@ def push_training(aabb, child, rec, nv, V, path0, saved, seed):
     assert n <= cap
     return {"node": node[:n].copy(), "source": src[:n].copy(), "stats": st[:n].copy(), "w": w[:n].copy(),
             "lost": int(lost.value)}
+
+
+def li_render(desc: dict, aabb, child, node_mix=None, guided=False, spp=1, max_depth=10, rr_depth=10, h=0.5,
+              V=9, seed=0, pixels=None, learned=None, threads=1):
+    """SDMMRenderer::Li restated on the CPU (sdmm_oracle_li.inc) for a
+    scene description (scenes.cornell_box() fields), the tree (aabb (n, 6),
+    child (n, 2)) and per-node oracle Mixtures (None: no trained context).
+    learned: (weights (B, M), means (B, M, 3), covs (B, M, 4), diffuse (B,))
+    for sampleProduct.  Returns dict image (3, H, W), image_sqr, rec
+    (16, V, P), nv (P,), comps (bounces, P)."""
+    W, H = int(desc["width"]), int(desc["height"])
+    lo, hi = (0, W * H) if pixels is None else pixels
+    P = (hi - lo) * spp
+    f32 = lambda a: np.ascontiguousarray(a, np.float32)
+    i32 = lambda a: np.ascontiguousarray(a, np.int32)
+    quads, flip, bsdf = f32(desc["quads"]), i32(desc["flip_normals"]), i32(desc["bsdf"])
+    refl, em, rad = f32(desc["reflectance"]), i32(desc["emitter"]), f32(desc["radiance"])
+    cam = f32(desc["camera_to_world"])
+    mn = np.ascontiguousarray(np.asarray(aabb)[:, :3].reshape(-1), np.float32)
+    mx = np.ascontiguousarray(np.asarray(aabb)[:, 3:].reshape(-1), np.float32)
+    ch = np.ascontiguousarray(np.asarray(child).reshape(-1), np.int32)
+    nn = len(mn) // 3
+    tab = (C.c_void_p * nn)()
+    kmax = 1
+    if node_mix is not None:
+        for i, m in enumerate(node_mix):
+            if m is not None:
+                tab[i] = C.cast(m.ptr, C.c_void_p)
+                kmax = max(kmax, m.K)
+    image = np.zeros((3, H, W), np.float32)
+    image_sqr = np.zeros((3, H, W), np.float32)
+    rec = np.zeros((16, V, P), np.float32)
+    nv = np.zeros(P, np.int32)
+    bounces = max_depth - 1 if max_depth > 0 else V
+    comps = np.full((bounces, P), -9, np.int32)
+    if learned is not None:
+        bw, bm, bc, bd = f32(learned[0]), f32(learned[1]), f32(learned[2]), np.ascontiguousarray(learned[3], np.uint8)
+        M = bw.shape[1]
+    else:
+        bw = bm = bc = np.zeros(1, np.float32)
+        bd = np.zeros(1, np.uint8)
+        M = 0
+    f = lib().or_li_render
+    f.restype = C.c_int
+    vp = lambda a: a.ctypes.data_as(C.c_void_p)
+    rc = f(vp(quads), vp(flip), vp(bsdf), C.c_int(len(bsdf)), vp(refl), vp(em), vp(rad), vp(cam),
+           C.c_float(desc["fov_x_deg"]), C.c_float(desc["near_clip"]), C.c_int(W), C.c_int(H), vp(mn), vp(mx),
+           vp(ch), tab, C.c_int(int(guided)), C.c_int(spp), C.c_int(max_depth), C.c_int(rr_depth), C.c_float(h),
+           C.c_int(V), C.c_uint64(seed), C.c_int64(lo), C.c_int64(hi), C.c_int(1 if learned is not None else 0),
+           vp(bw), vp(bm), vp(bc), vp(bd), C.c_int(M), C.c_int(kmax), vp(image), vp(image_sqr), vp(rec), vp(nv),
+           vp(comps), C.c_int(threads))
+    assert rc == 0, "or_li_render failed"
+    return {"image": image, "image_sqr": image_sqr, "rec": rec, "nv": nv, "comps": comps}

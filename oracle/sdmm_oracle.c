@@ -856,3 +856,4 @@ void or_pdf_batch(const or_mixture* m, int64_t nq, const float* c, const float* 
 }
 
 #include "sdmm_oracle_product.inc"
+#include "sdmm_oracle_li.inc"

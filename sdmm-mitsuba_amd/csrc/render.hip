@@ -92,8 +92,11 @@ __device__ __forceinline__ void cosine_hemisphere(float u0, float u1, float w[3]
     } else {
         r = r2; phi = (float)(kPi / 2.0) - (r1 / r2) * (float)(kPi / 4.0);
     }
-    float sp, cp;
-    sincosf(phi, &sp, &cp);
+    // sin / cos in double, rounded: the float values the CPU restatement
+    // (oracle/sdmm_oracle_li.inc) forms with the C library
+    double sd, cd;
+    sincos((double)phi, &sd, &cd);
+    const float sp = (float)sd, cp = (float)cd;
     w[0] = r * cp;
     w[1] = r * sp;
     float z = sqrtf(fmaxf(0.0f, 1.0f - w[0] * w[0] - w[1] * w[1]));

@@ -15,6 +15,10 @@
 #include "../../include/sdmm_gpu.h"
 #include "render_device.h"
 
+// the scene's derived quad data in plain IEEE float (no FMA contraction), as
+// the CPU restatement of Li forms it (oracle/sdmm_oracle_li.inc)
+#pragma clang fp contract(off)
+
 namespace sdmm {
 hipError_t launch_li_camera(const SceneDev& S, const PathsDev& P, int64_t path0, int spp, uint64_t seed,
                             hipStream_t st);

@@ -54,6 +54,12 @@ def synth(pkg):
     return importlib.import_module("sdmm_mitsuba_amd.synth")
 
 
+@pytest.fixture(scope="session")
+def scenes(pkg):
+    import importlib
+    return importlib.import_module("sdmm_mitsuba_amd.scenes")
+
+
 @pytest.fixture
 def plog(request):
     """record(quantity, realized, bound): append the realized max error of a
