@@ -309,6 +309,11 @@ struct sdmm_mix {
     // batched per-leaf EM tables (this handle as mixes[0]): device + pinned host
     void* batch_dev = nullptr;
     void* batch_host = nullptr;
+    // sdmm_iterations_run's gather scratch (this handle as mixes[0]): the
+    // pointer table + the counters, device and pinned host, grown on demand
+    mutable void* it_dev = nullptr;
+    mutable void* it_host = nullptr;
+    mutable size_t it_cap = 0;
     size_t batch_bytes = 0;
     hipEvent_t batch_copied = nullptr;   // the last table upload has completed
     hipEvent_t batch_done = nullptr;     // the last batch's kernels have completed
@@ -842,6 +847,8 @@ void sdmm_destroy(sdmm_mix* m) {
     if (m->staging) (void)hipFree(m->staging);
     if (m->batch_dev) (void)hipFree(m->batch_dev);
     if (m->batch_host) (void)hipHostFree(m->batch_host);
+    if (m->it_dev) (void)hipFree(m->it_dev);
+    if (m->it_host) (void)hipHostFree(m->it_host);
     if (m->shard_stats) (void)hipFree(m->shard_stats);
     if (m->batch_copied) (void)hipEventDestroy(m->batch_copied);
     if (m->batch_done) (void)hipEventDestroy(m->batch_done);
@@ -1151,53 +1158,49 @@ int sdmm_iterations_run(const sdmm_mix* const* mixes, int n, int* out) {
     if (n == 0) return SDMM_OK;
     for (int i = 0; i < n; ++i)
         if (!mixes[i]) return fail(SDMM_E_INVALID, "NULL handle in mixes");
-    HIP_TRY(hipSetDevice(mixes[0]->device));
-    if (n < 64) {
-        // a few mixtures (the plugin's per-leaf worker threads call this with
-        // one): a pinned copy per mixture on its own stream
-        double* pin = nullptr;
-        HIP_TRY(hipHostMalloc((void**)&pin, sizeof(double) * (size_t)n, hipHostMallocDefault));
-        hipError_t e = hipSuccess;
-        for (int i = 0; i < n && e == hipSuccess; ++i)
-            e = hipMemcpyAsync(pin + i, mixes[i]->S.scalars + SC_IT, sizeof(double), hipMemcpyDeviceToHost,
-                               mixes[i]->stream);
-        std::vector<hipStream_t> seen;
-        for (int i = 0; i < n && e == hipSuccess; ++i)
-            if (std::find(seen.begin(), seen.end(), mixes[i]->stream) == seen.end()) {
-                seen.push_back(mixes[i]->stream);
-                e = hipStreamSynchronize(mixes[i]->stream);
-            }
-        for (int i = 0; i < n && e == hipSuccess; ++i) out[i] = (int)pin[i];
-        (void)hipHostFree(pin);
-        if (e != hipSuccess) return fail(SDMM_E_HIP, std::string("sdmm_iterations_run: ") + hipGetErrorString(e));
-        return SDMM_OK;
-    }
-    // many (the guiding model's ready leaves): every mixture's pending work
-    // first (its own stream), then ONE gather of the n counters and one copy
-    // back (a copy per leaf cost ~3 us of launch each: ~10 ms per training
-    // pass of a few thousand leaves)
-    hipError_t e = hipSuccess;
+    const sdmm_mix* m0 = mixes[0];
+    HIP_TRY(hipSetDevice(m0->device));
+    // every mixture's pending work first (its own stream), then ONE gather of
+    // the n counters and one copy back on mixes[0]'s stream (a copy per leaf
+    // cost ~3 us of launch each: ~10 ms per training pass of a few thousand
+    // leaves).  The scratch is mixes[0]'s own, device + pinned, allocated
+    // once and reused: no stream-ordered allocation and no pageable copy in
+    // the call.  (Round 2's version took hipMallocAsync / hipFreeAsync from the
+    // device's default pool and pageable hipMemcpyAsync both ways; called from
+    // the plugin's per-leaf worker threads at once it hung -- the one place
+    // where pool allocations on many streams (release threshold 0: the pool
+    // trims at each synchronisation) met other threads' hipMalloc / hipFree
+    // (device-wide synchronisations) and staged pageable copies.  Calls on one
+    // handle are serialised by the caller (the ABI's rule), so mixes[0]'s
+    // scratch needs no lock.)
     std::vector<hipStream_t> seen;
-    for (int i = 0; i < n && e == hipSuccess; ++i)
+    for (int i = 0; i < n; ++i)
         if (std::find(seen.begin(), seen.end(), mixes[i]->stream) == seen.end()) {
             seen.push_back(mixes[i]->stream);
-            e = hipStreamSynchronize(mixes[i]->stream);
+            HIP_TRY(hipStreamSynchronize(mixes[i]->stream));
         }
-    const hipStream_t st = mixes[0]->stream;
-    std::vector<const double*> src((size_t)n);
-    for (int i = 0; i < n; ++i) src[(size_t)i] = mixes[i]->S.scalars + SC_IT;
-    std::vector<double> vals((size_t)n);
-    char* buf = nullptr;
+    const hipStream_t st = m0->stream;
     const size_t tab_bytes = ((sizeof(void*) * (size_t)n + 255) / 256) * 256;
-    if (e == hipSuccess) e = hipMallocAsync((void**)&buf, tab_bytes + sizeof(double) * (size_t)n, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(buf, src.data(), sizeof(void*) * (size_t)n, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = launch_gather_f64(buf, n, (double*)(buf + tab_bytes), st);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(vals.data(), buf + tab_bytes, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, st);
-    if (buf) (void)hipFreeAsync(buf, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    for (int i = 0; i < n && e == hipSuccess; ++i) out[i] = (int)vals[(size_t)i];
-    if (e != hipSuccess) return fail(SDMM_E_HIP, std::string("sdmm_iterations_run: ") + hipGetErrorString(e));
+    const size_t need = tab_bytes + sizeof(double) * (size_t)n;
+    if (need > m0->it_cap) {
+        if (m0->it_dev) HIP_TRY(hipFree(m0->it_dev));
+        if (m0->it_host) HIP_TRY(hipHostFree(m0->it_host));
+        m0->it_dev = m0->it_host = nullptr;
+        m0->it_cap = 0;
+        const size_t cap = std::max<size_t>(need, 4096);
+        HIP_TRY(hipMalloc(&m0->it_dev, cap));
+        HIP_TRY(hipHostMalloc(&m0->it_host, cap, hipHostMallocDefault));
+        m0->it_cap = cap;
+    }
+    const double** src = (const double**)m0->it_host;
+    for (int i = 0; i < n; ++i) src[i] = mixes[i]->S.scalars + SC_IT;
+    char* db = (char*)m0->it_dev;
+    double* vals = (double*)((char*)m0->it_host + tab_bytes);
+    HIP_TRY(hipMemcpyAsync(db, src, sizeof(void*) * (size_t)n, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_gather_f64(db, n, (double*)(db + tab_bytes), st));
+    HIP_TRY(hipMemcpyAsync(vals, db + tab_bytes, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int i = 0; i < n; ++i) out[i] = (int)vals[i];
     return SDMM_OK;
 }
 

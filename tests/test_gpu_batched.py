@@ -152,3 +152,49 @@ def test_create_many_failure_cleanup(pkg, gpu, monkeypatch, fail_at):
     for v in out:
         lib.sdmm_destroy(C.c_void_p(v))
     torch.cuda.synchronize()
+
+
+def test_iterations_run_concurrent_threads(pkg, synth, gpu):
+    """sdmm_iterations_run with >= 64 mixtures from 4 host threads at once --
+    the plugin's per-leaf worker threads (volpath_sdmm.cpp:287-311) calling it
+    beside each other's mixture creation / EM steps / destruction (hipMalloc /
+    hipFree) -- completes and returns every mixture's count.  (Round 2's
+    version with stream-ordered pool allocations and pageable copies hung in
+    this pattern; DESIGN.md, training passes.)"""
+    import ctypes as C
+    import threading
+    import torch
+    lib = pkg.lib()
+    b = synth.em_batch(4096, 128)
+    pos, nrm = synth.model_seed_points(b, 16)
+    ds = pkg.DeviceSamples.from_numpy(b["x"], b["w"])
+    errors, counts = [], {}
+
+    def worker(t):
+        try:
+            mixes = [pkg.SDMM(16, device=gpu.index) for _ in range(64 + 8 * t)]
+            for m in mixes:
+                m.init_hemisphere(pos[:2], nrm[:2], synth.DEPTH_PRIOR, synth.SPATIAL_DISTANCE, 3 + t)
+            for j in range(t + 1):
+                mixes[j].optimize(ds, 1 + j % 3)
+            tab = (C.c_void_p * len(mixes))(*[m.h.value for m in mixes])
+            out = (C.c_int * len(mixes))()
+            for rep in range(20):
+                assert lib.sdmm_iterations_run(tab, len(mixes), out) == 0
+                extra = pkg.SDMM(16, device=gpu.index)      # a creation + destruction beside it
+                del extra
+            counts[t] = list(out)
+        except Exception as e:   # surfaced below
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=90)
+    assert not any(th.is_alive() for th in ths), "sdmm_iterations_run did not complete"
+    assert not errors, errors
+    torch.cuda.synchronize()
+    for t in range(4):
+        expect = [1 + j % 3 for j in range(t + 1)] + [0] * (64 + 8 * t - t - 1)
+        assert counts[t] == expect, (t, counts[t][:8])
