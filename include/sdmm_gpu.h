@@ -387,6 +387,14 @@ int sdmm_stree_split_leaves(sdmm_stree* t, const float* const p[3], int64_t n, i
  * threads, the new nodes numbered exactly as n sequential calls would. */
 int sdmm_stree_split_leaf_recurse_many(sdmm_stree* t, int n, const int32_t* nodes, const float* const* p,
                                        const int64_t* counts, int threshold);
+/* The same on DEVICE-resident positions: node i's counts[i] positions are
+ * entries [starts[i], starts[i] + counts[i]) of the device planes p[0..2].
+ * The recursion runs on the device level by level (fp64 sums in the same
+ * fixed order as the host split's, the per-node decisions on the host, a
+ * stable partition per level); the node arrays are identical to
+ * sdmm_stree_split_leaf_recurse_many's.  On the tree's stream; synchronous. */
+int sdmm_stree_split_leaf_recurse_device(sdmm_stree* t, int n, const int32_t* nodes, const float* const p[3],
+                                         const int64_t* starts, const int64_t* counts, int threshold);
 /* aabb[6 * i] = min(3), max(3); child[2 * i] = children (-1, -1 for a leaf);
  * axis[i]: split axis.  Any output may be NULL. */
 int sdmm_stree_get_nodes(const sdmm_stree* t, float* aabb, int32_t* child, int32_t* axis);

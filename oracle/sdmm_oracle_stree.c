@@ -25,6 +25,7 @@
  */
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 typedef struct {
     float* mn;
@@ -101,14 +102,44 @@ int or_stree_find(const float* mn, const float* mx, const int* child, const floa
     return st_find_rec(&t, 0, p);
 }
 
+/* The split's fp64 sums over a node's samples in the library's one fixed
+ * order (sdmm_api.cpp split_sums_host, stree.hip split_sums_kernel): chunks
+ * of 4096 consecutive samples; in a chunk lane t of 256 sums samples t,
+ * t + 256, ... in order (products separately rounded); the lane sums fold
+ * pairwise (stride 128 .. 1); the chunk sums are added in chunk order.  jmm
+ * itself sums in float in an unspecified (Eigen) order. */
+static void st_sums(const int64_t* idx, int64_t n, const float* px, const float* py, const float* pz,
+                    double mean[3], double sq[3]) {
+    static const int64_t C = 4096;
+    double lane[256][6];
+    for (int a = 0; a < 3; ++a) { mean[a] = 0.0; sq[a] = 0.0; }
+    for (int64_t c0 = 0; c0 < n; c0 += C) {
+        const int64_t len = (n - c0 < C) ? n - c0 : C;
+        memset(lane, 0, sizeof(lane));
+        for (int64_t j = 0; j < len; ++j) {
+            double* a = lane[j % 256];
+            const int64_t i = idx[c0 + j];
+            const double p[3] = {px[i], py[i], pz[i]};
+            for (int k = 0; k < 3; ++k) {
+                a[k] = a[k] + p[k];
+                a[3 + k] = a[3 + k] + p[k] * p[k];
+            }
+        }
+        for (int st = 128; st > 0; st >>= 1)
+            for (int tt = 0; tt < st; ++tt)
+                for (int k = 0; k < 6; ++k) lane[tt][k] = lane[tt][k] + lane[tt + st][k];
+        for (int k = 0; k < 3; ++k) {
+            mean[k] = mean[k] + lane[0][k];
+            sq[k] = sq[k] + lane[0][3 + k];
+        }
+    }
+}
+
 static int st_split(st_tree* t, int i, int64_t* idx, int64_t n, const float* px, const float* py,
                     const float* pz, int threshold) {
     if (n <= threshold) return 0;
-    double mean[3] = {0, 0, 0}, sq[3] = {0, 0, 0};
-    for (int64_t j = 0; j < n; ++j) {
-        const double p[3] = {px[idx[j]], py[idx[j]], pz[idx[j]]};
-        for (int a = 0; a < 3; ++a) { mean[a] += p[a]; sq[a] += p[a] * p[a]; }
-    }
+    double mean[3], sq[3];
+    st_sums(idx, n, px, py, pz, mean, sq);
     float m[3], var[3];
     for (int a = 0; a < 3; ++a) {
         const double mu = mean[a] / (double)n;

@@ -220,7 +220,7 @@ EXPORTED_SYMBOLS = [
     "sdmm_init_hemisphere_batched", "sdmm_iterations_run", "sdmm_stree_split_leaf_recurse_many",
     "sdmm_em_step_batched_host_iters", "sdmm_write_exr", "sdmm_clone_many_on_stream", "sdmm_copy_many",
     "sdmm_guiding_update", "sdmm_kmeanspp_select", "sdmm_init_hemisphere_kmeanspp_batched",
-    "sdmm_guide_product_wavefront", "sdmm_pdf_product_wavefront",
+    "sdmm_guide_product_wavefront", "sdmm_pdf_product_wavefront", "sdmm_stree_split_leaf_recurse_device",
 ]
 
 
@@ -846,6 +846,27 @@ class STree:
         arr = (C.c_void_p * 3)(*[x.ctypes.data for x in p])
         _check(lib().sdmm_stree_split_leaf_recurse(self.h, int(node), arr, C.c_int64(p[0].shape[0]),
                                                    int(threshold)))
+
+    def split_leaf_recurse_many(self, nodes, positions, threshold: int):
+        """split_leaf_recurse for several leaves (increasing ids), leaf i with
+        its own host positions positions[i] (3, n_i) (sdmm_stree_split_leaf_recurse_many)."""
+        ps = [[np.ascontiguousarray(pp[i], np.float32) for i in range(3)] for pp in positions]
+        arr = (C.c_void_p * (3 * len(ps)))(*[x.ctypes.data for pp in ps for x in pp])
+        nd = np.ascontiguousarray(nodes, np.int32)
+        cnt = np.array([pp[0].shape[0] for pp in ps], np.int64)
+        _check(lib().sdmm_stree_split_leaf_recurse_many(self.h, len(ps), nd.ctypes.data_as(C.c_void_p), arr,
+                                                        cnt.ctypes.data_as(C.c_void_p), int(threshold)))
+
+    def split_leaf_recurse_device(self, nodes, planes, starts, counts, threshold: int):
+        """The same on device planes (3 tensors): leaf i's positions are
+        entries [starts[i], starts[i] + counts[i]) (sdmm_stree_split_leaf_recurse_device)."""
+        nd = np.ascontiguousarray(nodes, np.int32)
+        st = np.ascontiguousarray(starts, np.int64)
+        cn = np.ascontiguousarray(counts, np.int64)
+        arr = (C.c_void_p * 3)(*[t.data_ptr() for t in planes])
+        _check(lib().sdmm_stree_split_leaf_recurse_device(self.h, len(nd), nd.ctypes.data_as(C.c_void_p), arr,
+                                                          st.ctypes.data_as(C.c_void_p),
+                                                          cn.ctypes.data_as(C.c_void_p), int(threshold)))
 
     def split_leaves(self, positions, threshold: int = 4000, max_leaf_nodes: int = 2048):
         """The built plugin's splitting block (volpath_sdmm.cpp:253-260)."""

@@ -626,29 +626,13 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
             starts.push_back(a);
         }
         if (!nodes.empty()) {
-            // the positions of the splitting leaves (one span of the sorted pool)
-            const int64_t lo = starts.front(), hi = starts.back() + counts.back(), m = hi - lo;
-            if (3 * (size_t)m > g->pinned_floats) {
-                if (g->pinned) HIP_TRY(hipHostFree(g->pinned));
-                g->pinned = nullptr;
-                g->pinned_floats = 0;
-                const size_t want = 3 * (size_t)m + 3 * (size_t)m / 2;
-                HIP_TRY(hipHostMalloc((void**)&g->pinned, sizeof(float) * want, hipHostMallocDefault));
-                g->pinned_floats = want;
-            }
-            float* host = g->pinned;
-            for (int f = 0; f < 3; ++f)
-                HIP_TRY(hipMemcpyAsync(host + (size_t)f * (size_t)m, S.plane(f) + lo, sizeof(float) * (size_t)m,
-                                       hipMemcpyDeviceToHost, g->st));
-            HIP_TRY(hipStreamSynchronize(g->st));
-            std::vector<const float*> pp;
-            for (size_t i = 0; i < nodes.size(); ++i) {
-                const size_t o = (size_t)(starts[i] - lo);
-                pp.insert(pp.end(), {host + o, host + (size_t)m + o, host + 2 * (size_t)m + o});
-            }
-            clk.lap("split:copy");
-            SDMM_TRY(sdmm_stree_split_leaf_recurse_many(g->tree, (int)nodes.size(), nodes.data(), pp.data(),
-                                                        counts.data(), g->cfg.split_threshold));
+            // the splitting leaves' stats positions stay on the device: the
+            // split runs there (sdmm_stree_split_leaf_recurse_device, node
+            // arrays identical to the host split's)
+            clk.lap("split:order");
+            const float* planes[3] = {S.plane(0), S.plane(1), S.plane(2)};
+            SDMM_TRY(sdmm_stree_split_leaf_recurse_device(g->tree, (int)nodes.size(), nodes.data(), planes,
+                                                          starts.data(), counts.data(), g->cfg.split_threshold));
         }
     }
     clk.lap("split");

@@ -108,6 +108,17 @@ hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const v
 #define SDMM_GUIDE_CAP_MAX 40
 #endif
 constexpr int kGuideCapMax = SDMM_GUIDE_CAP_MAX;
+hipError_t launch_split_load(const float* const p[3], const int64_t* src_start, const int64_t* dst_start, int n_items,
+                             int64_t total, float* ox, float* oy, float* oz, int32_t* oitem, hipStream_t st);
+hipError_t launch_split_sums(const float* x, const float* y, const float* z, const void* chunks, int n_chunks,
+                             double* partial, hipStream_t st);
+hipError_t launch_split_count(const float* x, const float* y, const float* z, const int32_t* item, int64_t n,
+                              const void* cand, unsigned long long* counts, hipStream_t st);
+hipError_t launch_split_partition(const float* x, const float* y, const float* z, const int32_t* item, int64_t n,
+                                  const void* cand, int32_t* flags, int64_t* rank, void* temp, size_t temp_bytes,
+                                  float* ox, float* oy, float* oz, int32_t* oitem, hipStream_t st);
+size_t split_scan_temp_bytes(int64_t n);
+int split_chunk_samples();
 hipError_t launch_sample_cdf(const float* cdf, int n, const float* u, int64_t nq, int32_t* out,
                              hipStream_t st);
 hipError_t launch_produce_count(const void* nodes, const PathsDev& P, int64_t path0, int saved, uint64_t seed,
@@ -2020,28 +2031,68 @@ void st_split_depth(sdmm_stree* t, int node, int depth, int max_depth) {
 // px/py/pz owned by node.  Works on a LOCAL list so that independent leaves
 // can split in parallel; st_merge_local then appends the new nodes to the
 // tree in the order a sequential split would have created them.
+// The split's fp64 sums over a node's samples (sum p, then sum p^2, per axis)
+// in ONE fixed order, the order the device reduction forms them
+// (stree.hip split_sums_kernel): chunks of split_chunk_samples() consecutive
+// samples; within a chunk lane t of 256 sums samples t, t + 256, ... in order,
+// products separately rounded; the 256 lane sums fold pairwise (stride 128,
+// 64, .., 1); the chunk sums are added in chunk order to 0.  (jmm sums in
+// float in an unspecified order; oracle/sdmm_oracle_stree.c mirrors this.)
+void split_sums_host(const std::vector<int64_t>& idx, const float* px, const float* py, const float* pz,
+                     double out[6]) {
+#pragma clang fp contract(off)
+    const int64_t n = (int64_t)idx.size(), C = split_chunk_samples();
+    for (int k = 0; k < 6; ++k) out[k] = 0.0;
+    std::vector<double> lane(256 * 6);
+    for (int64_t c0 = 0; c0 < n; c0 += C) {
+        const int64_t len = std::min(C, n - c0);
+        std::fill(lane.begin(), lane.end(), 0.0);
+        for (int64_t j = 0; j < len; ++j) {
+            double* a = &lane[(size_t)(j % 256) * 6];
+            const int64_t i = idx[(size_t)(c0 + j)];
+            const double p[3] = {px[i], py[i], pz[i]};
+            for (int k = 0; k < 3; ++k) {
+                a[k] = a[k] + p[k];
+                const double sq = p[k] * p[k];
+                a[3 + k] = a[3 + k] + sq;
+            }
+        }
+        for (int st = 128; st > 0; st >>= 1)
+            for (int t = 0; t < st; ++t)
+                for (int k = 0; k < 6; ++k) lane[(size_t)t * 6 + k] = lane[(size_t)t * 6 + k] + lane[(size_t)(t + st) * 6 + k];
+        for (int k = 0; k < 6; ++k) out[k] = out[k] + lane[k];
+    }
+}
+
+// sntree.h:235-283's choice from the sums: the mean along the axis of largest
+// variance (the first of equals); false when the split position is not
+// strictly inside the node (zero variance / outside: the reference would
+// recurse forever)
+bool split_decide(const STNodeHost& nd, const double sums[6], int64_t n, int& ax, float& split) {
+    float m[3], var[3];
+    for (int a = 0; a < 3; ++a) {
+        const double mu = sums[a] / (double)n;
+        m[a] = (float)mu;
+        var[a] = (float)(sums[3 + a] / (double)n - mu * mu);
+    }
+    ax = 0;
+    for (int a = 0; a < 3; ++a)
+        if (var[a] > var[ax]) ax = a;
+    split = (m[ax] - nd.mn[ax]) / (nd.mx[ax] - nd.mn[ax]);
+    return split > 0.0f && split < 1.0f;
+}
+
 void st_split_local(std::vector<STNodeHost>& L, int node, std::vector<int64_t>& idx, const float* px,
                     const float* py, const float* pz, int threshold) {
     if (L[(size_t)node].child[0] >= 0) return;   // (inner nodes are routed by the caller)
     const int64_t n = (int64_t)idx.size();
     if (n <= threshold) return;
-    double mean[3] = {0, 0, 0}, sq[3] = {0, 0, 0};
-    for (int64_t i : idx) {
-        const double p[3] = {px[i], py[i], pz[i]};
-        for (int a = 0; a < 3; ++a) { mean[a] += p[a]; sq[a] += p[a] * p[a]; }
-    }
-    float m[3], var[3];
-    for (int a = 0; a < 3; ++a) {
-        const double mu = mean[a] / (double)n;
-        m[a] = (float)mu;
-        var[a] = (float)(sq[a] / (double)n - mu * mu);
-    }
+    double sums[6];
+    split_sums_host(idx, px, py, pz, sums);
     int ax = 0;
-    for (int a = 0; a < 3; ++a)
-        if (var[a] > var[ax]) ax = a;
+    float split = 0.0f;
+    if (!split_decide(L[(size_t)node], sums, n, ax, split)) return;   // degenerate (zero variance / outside)
     const STNodeHost& nd = L[(size_t)node];
-    const float split = (m[ax] - nd.mn[ax]) / (nd.mx[ax] - nd.mn[ax]);
-    if (!(split > 0.0f && split < 1.0f)) return;   // degenerate (zero variance / outside)
     STNodeHost parent = nd;
     parent.axis = ax;
     STNodeHost ch[2] = {st_child(parent, 0, split), st_child(parent, 1, split)};
@@ -2264,6 +2315,285 @@ int sdmm_stree_split_leaf_recurse(sdmm_stree* t, int node, const float* const p[
     t->dirty = true;
     t->tab_valid = false;
     return SDMM_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// split_leaf_recurse of many leaves on device-resident positions: the
+// recursion level by level (every item = a node being split + its samples,
+// contiguous in a level buffer in the parent's order); per level ONE sums
+// launch (canonical fp64 order, split_sums_host), the decisions on the host
+// (split_decide), one count launch (a split that would not separate its
+// samples is dropped, as in st_split_local), one stable partition into the
+// next level.  Each leaf's new nodes are collected breadth first and
+// renumbered to the sequential recursion's creation order (depth first,
+// both children at a split, child 0's subtree first) before merging.
+struct DevSplitBuf {
+    float* x = nullptr;
+    float* y = nullptr;
+    float* z = nullptr;
+    int32_t* item = nullptr;
+};
+
+int st_split_device(sdmm_stree* t, const std::vector<int>& leaves, const float* const p[3],
+                    const std::vector<int64_t>& src_start, const std::vector<int64_t>& counts, int threshold,
+                    hipStream_t st) {
+    const int nl = (int)leaves.size();
+    struct Local { std::vector<STNodeHost> nodes; };   // BFS: [0] = the leaf
+    std::vector<Local> L((size_t)nl);
+    for (int i = 0; i < nl; ++i) L[(size_t)i].nodes.push_back(t->nodes[(size_t)leaves[(size_t)i]]);
+    struct Item { int leaf, local; int64_t start, n; };
+    std::vector<Item> items;
+    std::vector<int64_t> dst_start;
+    int64_t total = 0;
+    for (int i = 0; i < nl; ++i) {
+        items.push_back({i, 0, total, counts[(size_t)i]});
+        dst_start.push_back(total);
+        total += counts[(size_t)i];
+    }
+    // device buffers (one allocation, regrown when a level outgrows it)
+    int64_t cap = 0;
+    void* mem = nullptr;
+    DevSplitBuf buf[2];
+    int32_t* flags = nullptr;
+    int64_t* rank = nullptr;
+    void* temp = nullptr;
+    size_t temp_bytes = 0;
+    auto release = [&]() { if (mem) (void)hipFree(mem); mem = nullptr; };
+    auto grow = [&](int64_t need, int keep) -> int {   // keep: the buffer set holding live data
+        if (need <= cap) return SDMM_OK;
+        const int64_t nc = need + need / 4 + 1024;
+        const size_t plane = ((sizeof(float) * (size_t)nc + 255) / 256) * 256;
+        const size_t tb = ((split_scan_temp_bytes(2 * nc) + 255) / 256) * 256;
+        const size_t bytes = 8 * plane + ((sizeof(int32_t) * 2 * (size_t)nc + 255) / 256) * 256 +
+                             sizeof(int64_t) * 2 * (size_t)nc + tb;
+        void* nm = nullptr;
+        HIP_TRY(hipMalloc(&nm, bytes));
+        char* b = (char*)nm;
+        DevSplitBuf nb[2];
+        for (int k = 0; k < 2; ++k) {
+            nb[k].x = (float*)b; b += plane;
+            nb[k].y = (float*)b; b += plane;
+            nb[k].z = (float*)b; b += plane;
+            nb[k].item = (int32_t*)b; b += plane;
+        }
+        int32_t* nflags = (int32_t*)b; b += ((sizeof(int32_t) * 2 * (size_t)nc + 255) / 256) * 256;
+        int64_t* nrank = (int64_t*)b; b += sizeof(int64_t) * 2 * (size_t)nc;
+        if (keep >= 0 && cap > 0) {   // move the live level over
+            HIP_TRY(hipMemcpyAsync(nb[keep].x, buf[keep].x, sizeof(float) * (size_t)cap, hipMemcpyDeviceToDevice, st));
+            HIP_TRY(hipMemcpyAsync(nb[keep].y, buf[keep].y, sizeof(float) * (size_t)cap, hipMemcpyDeviceToDevice, st));
+            HIP_TRY(hipMemcpyAsync(nb[keep].z, buf[keep].z, sizeof(float) * (size_t)cap, hipMemcpyDeviceToDevice, st));
+            HIP_TRY(hipMemcpyAsync(nb[keep].item, buf[keep].item, sizeof(int32_t) * (size_t)cap,
+                                   hipMemcpyDeviceToDevice, st));
+            HIP_TRY(hipStreamSynchronize(st));
+        }
+        release();
+        mem = nm;
+        buf[0] = nb[0];
+        buf[1] = nb[1];
+        flags = nflags;
+        rank = nrank;
+        temp = b;
+        temp_bytes = tb;
+        cap = nc;
+        return SDMM_OK;
+    };
+    int rc = SDMM_OK;
+    void* small = nullptr;       // per-level tables (chunks, partials, candidates, counts)
+    size_t small_cap = 0;
+    auto run = [&]() -> int {
+        int r = grow(total, -1);
+        if (r) return r;
+        int cur = 0;
+        {
+            int64_t* tabs = nullptr;
+            HIP_TRY(hipMallocAsync((void**)&tabs, sizeof(int64_t) * 2 * (size_t)nl, st));
+            HIP_TRY(hipMemcpyAsync(tabs, src_start.data(), sizeof(int64_t) * (size_t)nl, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemcpyAsync(tabs + nl, dst_start.data(), sizeof(int64_t) * (size_t)nl, hipMemcpyHostToDevice,
+                                   st));
+            HIP_TRY(launch_split_load(p, tabs, tabs + nl, nl, total, buf[0].x, buf[0].y, buf[0].z, buf[0].item, st));
+            HIP_TRY(hipFreeAsync(tabs, st));
+        }
+        const int C = split_chunk_samples();
+        while (!items.empty()) {
+            const int ni = (int)items.size();
+            // (1) sums of the items above the threshold, chunked
+            std::vector<SplitChunkDev> chunks;
+            std::vector<int> chunk_item;
+            for (int i = 0; i < ni; ++i) {
+                if (items[(size_t)i].n <= threshold) continue;
+                for (int64_t c0 = 0; c0 < items[(size_t)i].n; c0 += C) {
+                    SplitChunkDev c{};
+                    c.start = items[(size_t)i].start + c0;
+                    c.len = (int32_t)std::min<int64_t>(C, items[(size_t)i].n - c0);
+                    chunks.push_back(c);
+                    chunk_item.push_back(i);
+                }
+            }
+            if (chunks.empty()) break;
+            const size_t nch = chunks.size();
+            const size_t need = sizeof(SplitChunkDev) * nch + sizeof(double) * 6 * nch + sizeof(SplitCandDev) * ni +
+                                sizeof(unsigned long long) * 2 * ni + 4 * 256;
+            if (need > small_cap) {
+                if (small) HIP_TRY(hipFree(small));
+                small = nullptr;
+                small_cap = need + need / 2;
+                HIP_TRY(hipMalloc(&small, small_cap));
+            }
+            auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+            char* sb = (char*)small;
+            SplitChunkDev* dch = (SplitChunkDev*)sb; sb += al(sizeof(SplitChunkDev) * nch);
+            double* dpart = (double*)sb; sb += al(sizeof(double) * 6 * nch);
+            SplitCandDev* dcand = (SplitCandDev*)sb; sb += al(sizeof(SplitCandDev) * (size_t)ni);
+            unsigned long long* dcnt = (unsigned long long*)sb;
+            DevSplitBuf& B = buf[cur];
+            HIP_TRY(hipMemcpyAsync(dch, chunks.data(), sizeof(SplitChunkDev) * nch, hipMemcpyHostToDevice, st));
+            HIP_TRY(launch_split_sums(B.x, B.y, B.z, dch, (int)nch, dpart, st));
+            std::vector<double> part(6 * nch);
+            HIP_TRY(hipMemcpyAsync(part.data(), dpart, sizeof(double) * 6 * nch, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            std::vector<double> sums(6 * (size_t)ni, 0.0);
+            for (size_t c = 0; c < nch; ++c)
+                for (int k = 0; k < 6; ++k) {
+                    double& a = sums[6 * (size_t)chunk_item[c] + (size_t)k];
+                    a = a + part[6 * c + (size_t)k];
+                }
+            // (2) candidate splits
+            std::vector<SplitCandDev> cand((size_t)ni);
+            std::vector<int> axes((size_t)ni, 0);
+            std::vector<STNodeHost> kids(2 * (size_t)ni);
+            int n_active = 0;
+            for (int i = 0; i < ni; ++i) {
+                SplitCandDev& c = cand[(size_t)i];
+                std::memset(&c, 0, sizeof(c));
+                const Item& it = items[(size_t)i];
+                c.start = it.start;
+                c.n = it.n;
+                if (it.n <= threshold) continue;
+                const STNodeHost& nd = L[(size_t)it.leaf].nodes[(size_t)it.local];
+                int ax = 0;
+                float split = 0.0f;
+                if (!split_decide(nd, &sums[6 * (size_t)i], it.n, ax, split)) continue;
+                STNodeHost parent = nd;
+                parent.axis = ax;
+                for (int k = 0; k < 2; ++k) kids[2 * (size_t)i + (size_t)k] = st_child(parent, k, split);
+                for (int a = 0; a < 3; ++a) {
+                    c.mn0[a] = kids[2 * (size_t)i].mn[a]; c.mx0[a] = kids[2 * (size_t)i].mx[a];
+                    c.mn1[a] = kids[2 * (size_t)i + 1].mn[a]; c.mx1[a] = kids[2 * (size_t)i + 1].mx[a];
+                }
+                c.active = 1;
+                axes[(size_t)i] = ax;
+                ++n_active;
+            }
+            if (n_active == 0) break;
+            // (3) children's counts; a split that would not separate is dropped
+            HIP_TRY(hipMemcpyAsync(dcand, cand.data(), sizeof(SplitCandDev) * (size_t)ni, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemsetAsync(dcnt, 0, sizeof(unsigned long long) * 2 * (size_t)ni, st));
+            const int64_t lvl_n = items.back().start + items.back().n;
+            HIP_TRY(launch_split_count(B.x, B.y, B.z, B.item, lvl_n, dcand, dcnt, st));
+            std::vector<unsigned long long> cnt(2 * (size_t)ni);
+            HIP_TRY(hipMemcpyAsync(cnt.data(), dcnt, sizeof(unsigned long long) * 2 * (size_t)ni,
+                                   hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            std::vector<Item> next;
+            int64_t ntotal = 0;
+            for (int i = 0; i < ni; ++i) {
+                SplitCandDev& c = cand[(size_t)i];
+                if (!c.active) continue;
+                const Item& it = items[(size_t)i];
+                if ((int64_t)cnt[2 * (size_t)i] == it.n || (int64_t)cnt[2 * (size_t)i + 1] == it.n) {
+                    c.active = 0;   // would not separate the samples
+                    continue;
+                }
+                auto& ln = L[(size_t)it.leaf].nodes;
+                ln[(size_t)it.local].axis = axes[(size_t)i];
+                for (int k = 0; k < 2; ++k) {
+                    ln[(size_t)it.local].child[k] = (int)ln.size();
+                    ln.push_back(kids[2 * (size_t)i + (size_t)k]);
+                    c.child_item[k] = (int32_t)next.size();
+                    c.out[k] = ntotal;
+                    next.push_back({it.leaf, (int)ln.size() - 1, ntotal, (int64_t)cnt[2 * (size_t)i + (size_t)k]});
+                    ntotal += (int64_t)cnt[2 * (size_t)i + (size_t)k];
+                }
+            }
+            if (next.empty()) break;
+            // (4) the stable partition into the next level
+            r = grow(std::max(ntotal, lvl_n), cur);
+            if (r) return r;
+            HIP_TRY(hipMemcpyAsync(dcand, cand.data(), sizeof(SplitCandDev) * (size_t)ni, hipMemcpyHostToDevice, st));
+            DevSplitBuf& O = buf[1 - cur];
+            DevSplitBuf& I = buf[cur];
+            HIP_TRY(launch_split_partition(I.x, I.y, I.z, I.item, lvl_n, dcand, flags, rank, temp, temp_bytes, O.x,
+                                           O.y, O.z, O.item, st));
+            items.swap(next);
+            cur = 1 - cur;
+        }
+        HIP_TRY(hipStreamSynchronize(st));
+        return SDMM_OK;
+    };
+    rc = run();
+    if (small) (void)hipFree(small);
+    release();
+    if (rc) return rc;
+    // renumber each leaf's breadth-first nodes to the creation (depth-first) order
+    for (int i = 0; i < nl; ++i) {
+        const auto& Bn = L[(size_t)i].nodes;
+        std::vector<STNodeHost> D;
+        D.push_back(Bn[0]);
+        D[0].child[0] = D[0].child[1] = -1;
+        std::vector<std::pair<int, int>> stack{{0, 0}};   // (BFS index, D index)
+        // depth first, child 0's subtree before child 1's: a node's children are
+        // numbered when it is visited; the visit order is a pre-order
+        while (!stack.empty()) {
+            const auto [b, d] = stack.back();
+            stack.pop_back();
+            if (Bn[(size_t)b].child[0] < 0) continue;
+            D[(size_t)d].axis = Bn[(size_t)b].axis;
+            int ids[2];
+            for (int k = 0; k < 2; ++k) {
+                STNodeHost c = Bn[(size_t)Bn[(size_t)b].child[k]];
+                c.child[0] = c.child[1] = -1;
+                ids[k] = (int)D.size();
+                D.push_back(c);
+                D[(size_t)d].child[k] = ids[k];
+            }
+            stack.push_back({Bn[(size_t)b].child[1], ids[1]});
+            stack.push_back({Bn[(size_t)b].child[0], ids[0]});
+        }
+        st_merge_local(t, leaves[(size_t)i], D);
+    }
+    t->dirty = true;
+    t->tab_valid = false;
+    return SDMM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sdmm_stree_split_leaf_recurse_device(sdmm_stree* t, int n, const int32_t* nodes, const float* const p[3],
+                                         const int64_t* starts, const int64_t* counts, int threshold) {
+    if (!t || n < 0 || threshold < 1 || (n > 0 && (!nodes || !p || !p[0] || !p[1] || !p[2] || !starts || !counts)))
+        return fail(SDMM_E_INVALID, "invalid argument");
+    std::vector<int> leaves;
+    std::vector<int64_t> st0, cn;
+    for (int i = 0; i < n; ++i) {
+        const int v = nodes[i];
+        if (v < 0 || v >= (int)t->nodes.size() || counts[i] < 0 || starts[i] < 0)
+            return fail(SDMM_E_INVALID, "invalid argument");
+        if (i > 0 && v <= nodes[i - 1]) return fail(SDMM_E_INVALID, "nodes must be increasing");
+        if (t->nodes[(size_t)v].child[0] >= 0 || counts[i] <= threshold) continue;
+        leaves.push_back(v);
+        st0.push_back(starts[i]);
+        cn.push_back(counts[i]);
+    }
+    if (leaves.empty()) return SDMM_OK;
+    HIP_TRY(hipSetDevice(t->device));
+    int r = st_upload(t);
+    if (r) return r;
+    return st_split_device(t, leaves, p, st0, cn, threshold, t->stream);
 }
 
 int sdmm_stree_split_leaf_recurse_many(sdmm_stree* t, int n, const int32_t* nodes, const float* const* p,

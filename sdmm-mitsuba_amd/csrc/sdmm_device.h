@@ -153,6 +153,24 @@ struct GuideSortScratch {
 
 // ---- spatial tree node (stree.hip, guide.hip) ------------------------------
 // min[3], max[3], child0, child1 (-1 for a leaf).
+// device split of the spatial tree (stree.hip, sdmm_stree_split_leaf_recurse_device)
+struct SplitChunkDev {
+    int64_t start;   // level-buffer index of the chunk's first sample
+    int32_t len;
+    int32_t pad;
+};
+
+// per item: the candidate children's boxes (child 0 = the upper part), or
+// inactive (the item is a final leaf: its samples leave the recursion)
+struct SplitCandDev {
+    float mn0[3], mx0[3], mn1[3], mx1[3];
+    int32_t active;
+    int32_t child_item[2];   // next-level item ids (final pass)
+    int32_t pad;
+    int64_t start, n;        // the item's range in the level buffer
+    int64_t out[2];          // the children's first index in the next level buffer
+};
+
 struct STNodeDev {
     float mn[3], mx[3];
     int c0, c1;

@@ -103,3 +103,184 @@ hipError_t launch_stree_route(const void* nodes, int num_nodes, int key_bits, co
 }
 
 }  // namespace sdmm
+
+// ---------------------------------------------------------------------------
+// split_leaf_recurse on device-resident positions (sdmm_stree_split_leaf_
+// recurse_device; jmm SNTree::split, sntree.h:235-283, as the library's host
+// split restates it).  The recursion runs level by level over "items" (a node
+// being split with its samples, contiguous in a level buffer, in the parent's
+// sample order); the host makes every per-node decision from the sums these
+// kernels return, so the node arrays are those of the sequential recursion
+// (renumbered to its creation order on the host).
+namespace sdmm {
+
+constexpr int kSplitChunk = 4096;   // samples per reduction chunk (= the host's split_sums)
+
+
+
+// per chunk: the fp64 sums (p0, p1, p2, p0^2, p1^2, p2^2) in the canonical
+// order: lane t sums samples t, t + 256, ... ; the 256 lane sums fold by a
+// binary tree (stride 128 .. 1).  Products are separately rounded (no FMA),
+// as on the host.
+__global__ void __launch_bounds__(256)
+split_sums_kernel(const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ z,
+                  const SplitChunkDev* __restrict__ chunks, double* __restrict__ partial) {
+#pragma clang fp contract(off)
+    __shared__ double red[6][256];
+    const SplitChunkDev c = chunks[blockIdx.x];
+    const int t = threadIdx.x;
+    double a[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int j = t; j < c.len; j += 256) {
+        const double p[3] = {(double)x[c.start + j], (double)y[c.start + j], (double)z[c.start + j]};
+        for (int k = 0; k < 3; ++k) {
+            a[k] = a[k] + p[k];
+            const double sq = p[k] * p[k];
+            a[3 + k] = a[3 + k] + sq;
+        }
+    }
+    for (int k = 0; k < 6; ++k) red[k][t] = a[k];
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (t < s)
+            for (int k = 0; k < 6; ++k) red[k][t] = red[k][t] + red[k][t + s];
+        __syncthreads();
+    }
+    if (t < 6) partial[6 * (int64_t)blockIdx.x + t] = red[t][0];
+}
+
+
+
+__device__ __forceinline__ bool split_in(const float* mn, const float* mx, float a, float b, float c) {
+    return mn[0] <= a && a <= mx[0] && mn[1] <= b && b <= mx[1] && mn[2] <= c && c <= mx[2];
+}
+
+// children's sample counts of the candidate splits (integer atomics: order free)
+__global__ void __launch_bounds__(256)
+split_count_kernel(const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ z,
+                   const int32_t* __restrict__ item, int64_t n, const SplitCandDev* __restrict__ cand,
+                   unsigned long long* __restrict__ counts) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int it = item[i];
+    const SplitCandDev& c = cand[it];
+    if (!c.active) return;
+    const float a = x[i], b = y[i], d = z[i];
+    if (split_in(c.mn0, c.mx0, a, b, d)) atomicAdd(&counts[2 * it], 1ull);
+    if (split_in(c.mn1, c.mx1, a, b, d)) atomicAdd(&counts[2 * it + 1], 1ull);
+}
+
+// stable partition into the next level: item it's child-0 members then its
+// child-1 members, each in the item's sample order.  flags[2 start + j] (c0),
+// flags[2 start + n + j] (c1): the layout the exclusive scan turns into ranks.
+__global__ void __launch_bounds__(256)
+split_flags_kernel(const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ z,
+                   const int32_t* __restrict__ item, int64_t n, const SplitCandDev* __restrict__ cand,
+                   int32_t* __restrict__ flags) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const SplitCandDev& c = cand[item[i]];
+    const int64_t j = i - c.start;
+    int f0 = 0, f1 = 0;
+    if (c.active) {
+        const float a = x[i], b = y[i], d = z[i];
+        f0 = split_in(c.mn0, c.mx0, a, b, d) ? 1 : 0;
+        f1 = split_in(c.mn1, c.mx1, a, b, d) ? 1 : 0;
+    }
+    flags[2 * c.start + j] = f0;
+    flags[2 * c.start + c.n + j] = f1;
+}
+
+// rank[] = exclusive scan of flags; the child's members land at its out
+// offset + (rank - the item's rank at the child's first flag)
+__global__ void __launch_bounds__(256)
+split_scatter_kernel(const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ z,
+                     const int32_t* __restrict__ item, int64_t n, const SplitCandDev* __restrict__ cand,
+                     const int32_t* __restrict__ flags, const int64_t* __restrict__ rank, float* __restrict__ ox,
+                     float* __restrict__ oy, float* __restrict__ oz, int32_t* __restrict__ oitem) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int it = item[i];
+    const SplitCandDev& c = cand[it];
+    if (!c.active) return;
+    const int64_t j = i - c.start;
+    const int64_t e0 = 2 * c.start + j, e1 = 2 * c.start + c.n + j;
+    const int64_t b0 = rank[2 * c.start], b1 = rank[2 * c.start + c.n];
+    if (flags[e0]) {
+        const int64_t o = c.out[0] + (rank[e0] - b0);
+        ox[o] = x[i]; oy[o] = y[i]; oz[o] = z[i]; oitem[o] = c.child_item[0];
+    }
+    if (flags[e1]) {
+        const int64_t o = c.out[1] + (rank[e1] - b1);
+        ox[o] = x[i]; oy[o] = y[i]; oz[o] = z[i]; oitem[o] = c.child_item[1];
+    }
+}
+
+// gather the splitting leaves' positions into the first level buffer
+__global__ void __launch_bounds__(256)
+split_load_kernel(const float* __restrict__ px, const float* __restrict__ py, const float* __restrict__ pz,
+                  const int64_t* __restrict__ src_start, const int64_t* __restrict__ dst_start, int n_items,
+                  int64_t total, float* __restrict__ ox, float* __restrict__ oy, float* __restrict__ oz,
+                  int32_t* __restrict__ oitem) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    int lo = 0, hi = n_items - 1;        // last item with dst_start <= i
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (dst_start[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    const int64_t s = src_start[lo] + (i - dst_start[lo]);
+    ox[i] = px[s]; oy[i] = py[s]; oz[i] = pz[s]; oitem[i] = lo;
+}
+
+size_t split_scan_temp_bytes(int64_t n) {
+    size_t b = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const int32_t*)nullptr, (int64_t*)nullptr, (int)n);
+    return b;
+}
+
+static inline dim3 split_grid(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+
+hipError_t launch_split_load(const float* const p[3], const int64_t* src_start, const int64_t* dst_start, int n_items,
+                             int64_t total, float* ox, float* oy, float* oz, int32_t* oitem, hipStream_t st) {
+    if (total <= 0) return hipSuccess;
+    hipLaunchKernelGGL(split_load_kernel, split_grid(total), dim3(256), 0, st, p[0], p[1], p[2], src_start, dst_start,
+                       n_items, total, ox, oy, oz, oitem);
+    return hipGetLastError();
+}
+
+hipError_t launch_split_sums(const float* x, const float* y, const float* z, const void* chunks, int n_chunks,
+                             double* partial, hipStream_t st) {
+    if (n_chunks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(split_sums_kernel, dim3((unsigned)n_chunks), dim3(256), 0, st, x, y, z,
+                       (const SplitChunkDev*)chunks, partial);
+    return hipGetLastError();
+}
+
+hipError_t launch_split_count(const float* x, const float* y, const float* z, const int32_t* item, int64_t n,
+                              const void* cand, unsigned long long* counts, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(split_count_kernel, split_grid(n), dim3(256), 0, st, x, y, z, item, n,
+                       (const SplitCandDev*)cand, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_split_partition(const float* x, const float* y, const float* z, const int32_t* item, int64_t n,
+                                  const void* cand, int32_t* flags, int64_t* rank, void* temp, size_t temp_bytes,
+                                  float* ox, float* oy, float* oz, int32_t* oitem, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(split_flags_kernel, split_grid(n), dim3(256), 0, st, x, y, z, item, n,
+                       (const SplitCandDev*)cand, flags);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, flags, rank, (int)(2 * n), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(split_scatter_kernel, split_grid(n), dim3(256), 0, st, x, y, z, item, n,
+                       (const SplitCandDev*)cand, flags, rank, ox, oy, oz, oitem);
+    return hipGetLastError();
+}
+
+size_t split_cand_bytes() { return sizeof(SplitCandDev); }
+size_t split_chunk_bytes() { return sizeof(SplitChunkDev); }
+int split_chunk_samples() { return kSplitChunk; }
+
+}  // namespace sdmm

@@ -195,3 +195,38 @@ def test_device_find_backtracks(pkg, oracle, gpu):
     q, expect = _gap_queries()
     got = t.find([torch.from_numpy(q[:, i].copy()).to(gpu) for i in range(3)]).cpu().numpy()
     np.testing.assert_array_equal(got, expect)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,threshold,grid", [(400000, 2000, 0), (120000, 3000, 64), (60000, 500, 0)])
+def test_device_split_equals_host_split(pkg, oracle, synth, gpu, n, threshold, grid):
+    """sdmm_stree_split_leaf_recurse_device (the split on device-resident
+    positions, level by level) builds node arrays IDENTICAL to the host
+    split_leaf_recurse_many and to the oracle's recursion, for several leaves
+    at once; grid > 0 snaps the points to a lattice so many lie exactly on
+    split planes (they go to both children)."""
+    import torch
+    b, p = _points(synth, n)
+    if grid:
+        p = np.floor(p * grid) / grid
+    lo, hi = np.float32([0, 0, 0]), np.float32([1, 1, 1])
+    th, td = pkg.STree(lo, hi), pkg.STree(lo, hi)
+    for t in (th, td):
+        t.split_to_depth(1)
+    aabb, child, _ = th.nodes()
+    ids = oracle.stree_find(aabb, child, p.T)
+    leaves = [v for v in range(len(child)) if child[v, 0] < 0 and (ids == v).sum() > threshold]
+    per = [p[:, ids == v] for v in leaves]
+    th.split_leaf_recurse_many(leaves, per, threshold)
+    cat = np.concatenate(per, axis=1)
+    counts = np.array([x.shape[1] for x in per], np.int64)
+    starts = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
+    planes = [torch.from_numpy(np.ascontiguousarray(cat[i])).to(gpu) for i in range(3)]
+    td.split_leaf_recurse_device(leaves, planes, starts, counts, threshold)
+    for a, c in zip(th.nodes(), td.nodes()):
+        np.testing.assert_array_equal(a, c)
+    assert td.num_nodes > len(child) + 10
+    # and the oracle's sequential recursion from the same leaves
+    oa, oc, ox = oracle.stree_build(lo, hi, 1, p, threshold)
+    np.testing.assert_array_equal(td.nodes()[1], oc)
+    np.testing.assert_array_equal(td.nodes()[0], oa)
