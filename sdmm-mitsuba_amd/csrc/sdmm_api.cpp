@@ -112,11 +112,12 @@ hipError_t launch_split_load(const float* const p[3], const int64_t* src_start, 
                              int64_t total, float* ox, float* oy, float* oz, int32_t* oitem, hipStream_t st);
 hipError_t launch_split_sums(const float* x, const float* y, const float* z, const void* chunks, int n_chunks,
                              double* partial, hipStream_t st);
-hipError_t launch_split_count(const float* x, const float* y, const float* z, const int32_t* item, int64_t n,
-                              const void* cand, unsigned long long* counts, hipStream_t st);
-hipError_t launch_split_partition(const float* x, const float* y, const float* z, const int32_t* item, int64_t n,
-                                  const void* cand, int32_t* flags, int64_t* rank, void* temp, size_t temp_bytes,
-                                  float* ox, float* oy, float* oz, int32_t* oitem, hipStream_t st);
+hipError_t launch_split_flags(const float* x, const float* y, const float* z, const int32_t* item, int64_t n,
+                              const void* cand, int n_items, int32_t* flags, int64_t* rank, void* temp,
+                              size_t temp_bytes, long long* counts, hipStream_t st);
+hipError_t launch_split_scatter(const float* x, const float* y, const float* z, const int32_t* item, int64_t n,
+                                const void* cand, const int32_t* flags, const int64_t* rank, float* ox, float* oy,
+                                float* oz, int32_t* oitem, hipStream_t st);
 size_t split_scan_temp_bytes(int64_t n);
 int split_chunk_samples();
 hipError_t launch_sample_cdf(const float* cdf, int n, const float* u, int64_t nq, int32_t* out,
@@ -1985,6 +1986,12 @@ struct sdmm_stree {
     // their pending work (EM steps) through one event per stream
     std::vector<hipStream_t> mix_streams;
     std::vector<hipEvent_t> mix_events;
+    // device split scratch (level buffers, flags / ranks, scan temp; per-level
+    // tables), kept across calls
+    void* split_mem = nullptr;
+    int64_t split_cap = 0;
+    void* split_small = nullptr;
+    size_t split_small_cap = 0;
 };
 
 namespace {
@@ -2255,6 +2262,8 @@ void sdmm_stree_destroy(sdmm_stree* t) {
     if (t->dnodes) (void)hipFree(t->dnodes);
     if (t->scratch) (void)hipFree(t->scratch);
     if (t->dtab) (void)hipFree(t->dtab);
+    if (t->split_mem) (void)hipFree(t->split_mem);
+    if (t->split_small) (void)hipFree(t->split_small);
     if (t->guide_fb) (void)hipFree(t->guide_fb);
     for (hipEvent_t e : t->mix_events) (void)hipEventDestroy(e);
     if (t->stream && t->own_stream) (void)hipStreamDestroy(t->stream);
@@ -2337,215 +2346,232 @@ struct DevSplitBuf {
     int32_t* item = nullptr;
 };
 
-int st_split_device(sdmm_stree* t, const std::vector<int>& leaves, const float* const p[3],
-                    const std::vector<int64_t>& src_start, const std::vector<int64_t>& counts, int threshold,
-                    hipStream_t st) {
-    const int nl = (int)leaves.size();
-    struct Local { std::vector<STNodeHost> nodes; };   // BFS: [0] = the leaf
-    std::vector<Local> L((size_t)nl);
-    for (int i = 0; i < nl; ++i) L[(size_t)i].nodes.push_back(t->nodes[(size_t)leaves[(size_t)i]]);
-    struct Item { int leaf, local; int64_t start, n; };
-    std::vector<Item> items;
-    std::vector<int64_t> dst_start;
-    int64_t total = 0;
-    for (int i = 0; i < nl; ++i) {
-        items.push_back({i, 0, total, counts[(size_t)i]});
-        dst_start.push_back(total);
-        total += counts[(size_t)i];
-    }
-    // device buffers (one allocation, regrown when a level outgrows it)
-    int64_t cap = 0;
-    void* mem = nullptr;
+// the split scratch of t for levels of up to `need` samples (contents kept
+// only by the caller's own copies: grown before a level is loaded / written)
+struct DevSplitScratch {
     DevSplitBuf buf[2];
     int32_t* flags = nullptr;
     int64_t* rank = nullptr;
     void* temp = nullptr;
     size_t temp_bytes = 0;
-    auto release = [&]() { if (mem) (void)hipFree(mem); mem = nullptr; };
-    auto grow = [&](int64_t need, int keep) -> int {   // keep: the buffer set holding live data
-        if (need <= cap) return SDMM_OK;
-        const int64_t nc = need + need / 4 + 1024;
-        const size_t plane = ((sizeof(float) * (size_t)nc + 255) / 256) * 256;
-        const size_t tb = ((split_scan_temp_bytes(2 * nc) + 255) / 256) * 256;
-        const size_t bytes = 8 * plane + ((sizeof(int32_t) * 2 * (size_t)nc + 255) / 256) * 256 +
-                             sizeof(int64_t) * 2 * (size_t)nc + tb;
-        void* nm = nullptr;
-        HIP_TRY(hipMalloc(&nm, bytes));
-        char* b = (char*)nm;
-        DevSplitBuf nb[2];
-        for (int k = 0; k < 2; ++k) {
-            nb[k].x = (float*)b; b += plane;
-            nb[k].y = (float*)b; b += plane;
-            nb[k].z = (float*)b; b += plane;
-            nb[k].item = (int32_t*)b; b += plane;
-        }
-        int32_t* nflags = (int32_t*)b; b += ((sizeof(int32_t) * 2 * (size_t)nc + 255) / 256) * 256;
-        int64_t* nrank = (int64_t*)b; b += sizeof(int64_t) * 2 * (size_t)nc;
-        if (keep >= 0 && cap > 0) {   // move the live level over
-            HIP_TRY(hipMemcpyAsync(nb[keep].x, buf[keep].x, sizeof(float) * (size_t)cap, hipMemcpyDeviceToDevice, st));
-            HIP_TRY(hipMemcpyAsync(nb[keep].y, buf[keep].y, sizeof(float) * (size_t)cap, hipMemcpyDeviceToDevice, st));
-            HIP_TRY(hipMemcpyAsync(nb[keep].z, buf[keep].z, sizeof(float) * (size_t)cap, hipMemcpyDeviceToDevice, st));
-            HIP_TRY(hipMemcpyAsync(nb[keep].item, buf[keep].item, sizeof(int32_t) * (size_t)cap,
-                                   hipMemcpyDeviceToDevice, st));
-            HIP_TRY(hipStreamSynchronize(st));
-        }
-        release();
-        mem = nm;
-        buf[0] = nb[0];
-        buf[1] = nb[1];
-        flags = nflags;
-        rank = nrank;
-        temp = b;
-        temp_bytes = tb;
-        cap = nc;
+};
+
+DevSplitScratch split_layout(void* mem, int64_t nc) {
+    const size_t plane = ((sizeof(float) * (size_t)nc + 255) / 256) * 256;
+    const size_t fl = ((sizeof(int32_t) * (2 * (size_t)nc + 1) + 255) / 256) * 256;
+    const size_t rk = ((sizeof(int64_t) * (2 * (size_t)nc + 1) + 255) / 256) * 256;
+    DevSplitScratch S;
+    char* b = (char*)mem;
+    for (int k = 0; k < 2; ++k) {
+        S.buf[k].x = (float*)b; b += plane;
+        S.buf[k].y = (float*)b; b += plane;
+        S.buf[k].z = (float*)b; b += plane;
+        S.buf[k].item = (int32_t*)b; b += plane;
+    }
+    S.flags = (int32_t*)b; b += fl;
+    S.rank = (int64_t*)b; b += rk;
+    S.temp = b;
+    S.temp_bytes = ((split_scan_temp_bytes(2 * nc + 1) + 255) / 256) * 256;
+    return S;
+}
+size_t split_mem_bytes(int64_t nc) {
+    const size_t plane = ((sizeof(float) * (size_t)nc + 255) / 256) * 256;
+    const size_t fl = ((sizeof(int32_t) * (2 * (size_t)nc + 1) + 255) / 256) * 256;
+    const size_t rk = ((sizeof(int64_t) * (2 * (size_t)nc + 1) + 255) / 256) * 256;
+    return 8 * plane + fl + rk + ((split_scan_temp_bytes(2 * nc + 1) + 255) / 256) * 256;
+}
+
+// grow t's split scratch to `need` samples per level; keep >= 0: the buffer
+// set whose first `live` entries are copied over
+int split_grow(sdmm_stree* t, int64_t need, int keep, int64_t live, hipStream_t st, DevSplitScratch& S) {
+    if (need <= t->split_cap && t->split_mem) {
+        S = split_layout(t->split_mem, t->split_cap);
         return SDMM_OK;
-    };
-    int rc = SDMM_OK;
-    void* small = nullptr;       // per-level tables (chunks, partials, candidates, counts)
-    size_t small_cap = 0;
-    auto run = [&]() -> int {
-        int r = grow(total, -1);
+    }
+    const int64_t nc = need + need / 4 + 4096;
+    void* nm = nullptr;
+    HIP_TRY(hipMalloc(&nm, split_mem_bytes(nc)));
+    DevSplitScratch N = split_layout(nm, nc);
+    if (keep >= 0 && t->split_mem && live > 0) {
+        const DevSplitScratch O = split_layout(t->split_mem, t->split_cap);
+        HIP_TRY(hipMemcpyAsync(N.buf[keep].x, O.buf[keep].x, sizeof(float) * (size_t)live, hipMemcpyDeviceToDevice, st));
+        HIP_TRY(hipMemcpyAsync(N.buf[keep].y, O.buf[keep].y, sizeof(float) * (size_t)live, hipMemcpyDeviceToDevice, st));
+        HIP_TRY(hipMemcpyAsync(N.buf[keep].z, O.buf[keep].z, sizeof(float) * (size_t)live, hipMemcpyDeviceToDevice, st));
+        HIP_TRY(hipMemcpyAsync(N.buf[keep].item, O.buf[keep].item, sizeof(int32_t) * (size_t)live,
+                               hipMemcpyDeviceToDevice, st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    if (t->split_mem) HIP_TRY(hipFree(t->split_mem));
+    t->split_mem = nm;
+    t->split_cap = nc;
+    S = N;
+    return SDMM_OK;
+}
+
+int split_small(sdmm_stree* t, size_t need) {
+    if (need <= t->split_small_cap && t->split_small) return SDMM_OK;
+    if (t->split_small) HIP_TRY(hipFree(t->split_small));
+    t->split_small = nullptr;
+    t->split_small_cap = 0;
+    const size_t cap = need + need / 2 + 4096;
+    HIP_TRY(hipMalloc(&t->split_small, cap));
+    t->split_small_cap = cap;
+    return SDMM_OK;
+}
+
+int st_split_device(sdmm_stree* t, const std::vector<int>& leaves, const float* const p[3],
+                    const std::vector<int64_t>& src_start, const std::vector<int64_t>& counts, int threshold,
+                    hipStream_t st) {
+    const int nl = (int)leaves.size();
+    std::vector<std::vector<STNodeHost>> L((size_t)nl);   // per leaf, breadth first: [0] = the leaf
+    for (int i = 0; i < nl; ++i) L[(size_t)i].push_back(t->nodes[(size_t)leaves[(size_t)i]]);
+    struct Item { int leaf, local; int64_t start, n; };
+    std::vector<Item> items;
+    std::vector<int64_t> tabs;   // src starts, then dst starts
+    int64_t total = 0;
+    for (int i = 0; i < nl; ++i) {
+        items.push_back({i, 0, total, counts[(size_t)i]});
+        total += counts[(size_t)i];
+    }
+    for (int i = 0; i < nl; ++i) tabs.push_back(src_start[(size_t)i]);
+    for (int i = 0; i < nl; ++i) tabs.push_back(items[(size_t)i].start);
+    DevSplitScratch S;
+    int r = split_grow(t, total, -1, 0, st, S);
+    if (r) return r;
+    const int C = split_chunk_samples();
+    auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+    // level 0: gather the leaves' positions
+    {
+        r = split_small(t, al(sizeof(int64_t) * tabs.size()));
         if (r) return r;
-        int cur = 0;
-        {
-            int64_t* tabs = nullptr;
-            HIP_TRY(hipMallocAsync((void**)&tabs, sizeof(int64_t) * 2 * (size_t)nl, st));
-            HIP_TRY(hipMemcpyAsync(tabs, src_start.data(), sizeof(int64_t) * (size_t)nl, hipMemcpyHostToDevice, st));
-            HIP_TRY(hipMemcpyAsync(tabs + nl, dst_start.data(), sizeof(int64_t) * (size_t)nl, hipMemcpyHostToDevice,
-                                   st));
-            HIP_TRY(launch_split_load(p, tabs, tabs + nl, nl, total, buf[0].x, buf[0].y, buf[0].z, buf[0].item, st));
-            HIP_TRY(hipFreeAsync(tabs, st));
+        int64_t* dt = (int64_t*)t->split_small;
+        HIP_TRY(hipMemcpyAsync(dt, tabs.data(), sizeof(int64_t) * tabs.size(), hipMemcpyHostToDevice, st));
+        HIP_TRY(launch_split_load(p, dt, dt + nl, nl, total, S.buf[0].x, S.buf[0].y, S.buf[0].z, S.buf[0].item, st));
+    }
+    int cur = 0;
+    while (!items.empty()) {
+        const int ni = (int)items.size();
+        const int64_t lvl_n = items.back().start + items.back().n;
+        // (1) fp64 sums of the items above the threshold, by chunks
+        std::vector<SplitChunkDev> chunks;
+        std::vector<int> chunk_item;
+        for (int i = 0; i < ni; ++i) {
+            if (items[(size_t)i].n <= threshold) continue;
+            for (int64_t c0 = 0; c0 < items[(size_t)i].n; c0 += C) {
+                SplitChunkDev c{};
+                c.start = items[(size_t)i].start + c0;
+                c.len = (int32_t)std::min<int64_t>(C, items[(size_t)i].n - c0);
+                chunks.push_back(c);
+                chunk_item.push_back(i);
+            }
         }
-        const int C = split_chunk_samples();
-        while (!items.empty()) {
-            const int ni = (int)items.size();
-            // (1) sums of the items above the threshold, chunked
-            std::vector<SplitChunkDev> chunks;
-            std::vector<int> chunk_item;
-            for (int i = 0; i < ni; ++i) {
-                if (items[(size_t)i].n <= threshold) continue;
-                for (int64_t c0 = 0; c0 < items[(size_t)i].n; c0 += C) {
-                    SplitChunkDev c{};
-                    c.start = items[(size_t)i].start + c0;
-                    c.len = (int32_t)std::min<int64_t>(C, items[(size_t)i].n - c0);
-                    chunks.push_back(c);
-                    chunk_item.push_back(i);
-                }
-            }
-            if (chunks.empty()) break;
-            const size_t nch = chunks.size();
-            const size_t need = sizeof(SplitChunkDev) * nch + sizeof(double) * 6 * nch + sizeof(SplitCandDev) * ni +
-                                sizeof(unsigned long long) * 2 * ni + 4 * 256;
-            if (need > small_cap) {
-                if (small) HIP_TRY(hipFree(small));
-                small = nullptr;
-                small_cap = need + need / 2;
-                HIP_TRY(hipMalloc(&small, small_cap));
-            }
-            auto al = [](size_t b) { return (b + 255) / 256 * 256; };
-            char* sb = (char*)small;
-            SplitChunkDev* dch = (SplitChunkDev*)sb; sb += al(sizeof(SplitChunkDev) * nch);
-            double* dpart = (double*)sb; sb += al(sizeof(double) * 6 * nch);
-            SplitCandDev* dcand = (SplitCandDev*)sb; sb += al(sizeof(SplitCandDev) * (size_t)ni);
-            unsigned long long* dcnt = (unsigned long long*)sb;
-            DevSplitBuf& B = buf[cur];
-            HIP_TRY(hipMemcpyAsync(dch, chunks.data(), sizeof(SplitChunkDev) * nch, hipMemcpyHostToDevice, st));
-            HIP_TRY(launch_split_sums(B.x, B.y, B.z, dch, (int)nch, dpart, st));
-            std::vector<double> part(6 * nch);
-            HIP_TRY(hipMemcpyAsync(part.data(), dpart, sizeof(double) * 6 * nch, hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipStreamSynchronize(st));
-            std::vector<double> sums(6 * (size_t)ni, 0.0);
-            for (size_t c = 0; c < nch; ++c)
-                for (int k = 0; k < 6; ++k) {
-                    double& a = sums[6 * (size_t)chunk_item[c] + (size_t)k];
-                    a = a + part[6 * c + (size_t)k];
-                }
-            // (2) candidate splits
-            std::vector<SplitCandDev> cand((size_t)ni);
-            std::vector<int> axes((size_t)ni, 0);
-            std::vector<STNodeHost> kids(2 * (size_t)ni);
-            int n_active = 0;
-            for (int i = 0; i < ni; ++i) {
-                SplitCandDev& c = cand[(size_t)i];
-                std::memset(&c, 0, sizeof(c));
-                const Item& it = items[(size_t)i];
-                c.start = it.start;
-                c.n = it.n;
-                if (it.n <= threshold) continue;
-                const STNodeHost& nd = L[(size_t)it.leaf].nodes[(size_t)it.local];
-                int ax = 0;
-                float split = 0.0f;
-                if (!split_decide(nd, &sums[6 * (size_t)i], it.n, ax, split)) continue;
-                STNodeHost parent = nd;
-                parent.axis = ax;
-                for (int k = 0; k < 2; ++k) kids[2 * (size_t)i + (size_t)k] = st_child(parent, k, split);
-                for (int a = 0; a < 3; ++a) {
-                    c.mn0[a] = kids[2 * (size_t)i].mn[a]; c.mx0[a] = kids[2 * (size_t)i].mx[a];
-                    c.mn1[a] = kids[2 * (size_t)i + 1].mn[a]; c.mx1[a] = kids[2 * (size_t)i + 1].mx[a];
-                }
-                c.active = 1;
-                axes[(size_t)i] = ax;
-                ++n_active;
-            }
-            if (n_active == 0) break;
-            // (3) children's counts; a split that would not separate is dropped
-            HIP_TRY(hipMemcpyAsync(dcand, cand.data(), sizeof(SplitCandDev) * (size_t)ni, hipMemcpyHostToDevice, st));
-            HIP_TRY(hipMemsetAsync(dcnt, 0, sizeof(unsigned long long) * 2 * (size_t)ni, st));
-            const int64_t lvl_n = items.back().start + items.back().n;
-            HIP_TRY(launch_split_count(B.x, B.y, B.z, B.item, lvl_n, dcand, dcnt, st));
-            std::vector<unsigned long long> cnt(2 * (size_t)ni);
-            HIP_TRY(hipMemcpyAsync(cnt.data(), dcnt, sizeof(unsigned long long) * 2 * (size_t)ni,
-                                   hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipStreamSynchronize(st));
-            std::vector<Item> next;
-            int64_t ntotal = 0;
-            for (int i = 0; i < ni; ++i) {
-                SplitCandDev& c = cand[(size_t)i];
-                if (!c.active) continue;
-                const Item& it = items[(size_t)i];
-                if ((int64_t)cnt[2 * (size_t)i] == it.n || (int64_t)cnt[2 * (size_t)i + 1] == it.n) {
-                    c.active = 0;   // would not separate the samples
-                    continue;
-                }
-                auto& ln = L[(size_t)it.leaf].nodes;
-                ln[(size_t)it.local].axis = axes[(size_t)i];
-                for (int k = 0; k < 2; ++k) {
-                    ln[(size_t)it.local].child[k] = (int)ln.size();
-                    ln.push_back(kids[2 * (size_t)i + (size_t)k]);
-                    c.child_item[k] = (int32_t)next.size();
-                    c.out[k] = ntotal;
-                    next.push_back({it.leaf, (int)ln.size() - 1, ntotal, (int64_t)cnt[2 * (size_t)i + (size_t)k]});
-                    ntotal += (int64_t)cnt[2 * (size_t)i + (size_t)k];
-                }
-            }
-            if (next.empty()) break;
-            // (4) the stable partition into the next level
-            r = grow(std::max(ntotal, lvl_n), cur);
-            if (r) return r;
-            HIP_TRY(hipMemcpyAsync(dcand, cand.data(), sizeof(SplitCandDev) * (size_t)ni, hipMemcpyHostToDevice, st));
-            DevSplitBuf& O = buf[1 - cur];
-            DevSplitBuf& I = buf[cur];
-            HIP_TRY(launch_split_partition(I.x, I.y, I.z, I.item, lvl_n, dcand, flags, rank, temp, temp_bytes, O.x,
-                                           O.y, O.z, O.item, st));
-            items.swap(next);
-            cur = 1 - cur;
-        }
+        if (chunks.empty()) break;
+        const size_t nch = chunks.size();
+        r = split_small(t, al(sizeof(SplitChunkDev) * nch) + al(sizeof(double) * 6 * nch) +
+                               al(sizeof(SplitCandDev) * (size_t)ni) + al(sizeof(long long) * 2 * (size_t)ni));
+        if (r) return r;
+        char* sb = (char*)t->split_small;
+        SplitChunkDev* dch = (SplitChunkDev*)sb; sb += al(sizeof(SplitChunkDev) * nch);
+        double* dpart = (double*)sb; sb += al(sizeof(double) * 6 * nch);
+        SplitCandDev* dcand = (SplitCandDev*)sb; sb += al(sizeof(SplitCandDev) * (size_t)ni);
+        long long* dcnt = (long long*)sb;
+        const DevSplitBuf I = S.buf[cur];
+        HIP_TRY(hipMemcpyAsync(dch, chunks.data(), sizeof(SplitChunkDev) * nch, hipMemcpyHostToDevice, st));
+        HIP_TRY(launch_split_sums(I.x, I.y, I.z, dch, (int)nch, dpart, st));
+        std::vector<double> part(6 * nch);
+        HIP_TRY(hipMemcpyAsync(part.data(), dpart, sizeof(double) * 6 * nch, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
-        return SDMM_OK;
-    };
-    rc = run();
-    if (small) (void)hipFree(small);
-    release();
-    if (rc) return rc;
+        std::vector<double> sums(6 * (size_t)ni, 0.0);
+        for (size_t c = 0; c < nch; ++c)
+            for (int k = 0; k < 6; ++k) {
+                double& a = sums[6 * (size_t)chunk_item[c] + (size_t)k];
+                a = a + part[6 * c + (size_t)k];
+            }
+        // (2) the candidate splits (split_decide), their children's counts
+        std::vector<SplitCandDev> cand((size_t)ni);
+        std::vector<int> axes((size_t)ni, 0);
+        std::vector<STNodeHost> kids(2 * (size_t)ni);
+        int n_active = 0;
+        for (int i = 0; i < ni; ++i) {
+            SplitCandDev& c = cand[(size_t)i];
+            std::memset(&c, 0, sizeof(c));
+            const Item& it = items[(size_t)i];
+            c.start = it.start;
+            c.n = it.n;
+            if (it.n <= threshold) continue;
+            const STNodeHost& nd = L[(size_t)it.leaf][(size_t)it.local];
+            int ax = 0;
+            float split = 0.0f;
+            if (!split_decide(nd, &sums[6 * (size_t)i], it.n, ax, split)) continue;
+            STNodeHost parent = nd;
+            parent.axis = ax;
+            for (int k = 0; k < 2; ++k) kids[2 * (size_t)i + (size_t)k] = st_child(parent, k, split);
+            for (int a = 0; a < 3; ++a) {
+                c.mn0[a] = kids[2 * (size_t)i].mn[a]; c.mx0[a] = kids[2 * (size_t)i].mx[a];
+                c.mn1[a] = kids[2 * (size_t)i + 1].mn[a]; c.mx1[a] = kids[2 * (size_t)i + 1].mx[a];
+            }
+            c.active = 1;
+            axes[(size_t)i] = ax;
+            ++n_active;
+        }
+        if (n_active == 0) break;
+        HIP_TRY(hipMemcpyAsync(dcand, cand.data(), sizeof(SplitCandDev) * (size_t)ni, hipMemcpyHostToDevice, st));
+        HIP_TRY(launch_split_flags(I.x, I.y, I.z, I.item, lvl_n, dcand, ni, S.flags, S.rank, S.temp, S.temp_bytes,
+                                   dcnt, st));
+        std::vector<long long> cnt(2 * (size_t)ni);
+        HIP_TRY(hipMemcpyAsync(cnt.data(), dcnt, sizeof(long long) * 2 * (size_t)ni, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        // (3) accept the splits that separate their samples (st_split_local)
+        std::vector<Item> next;
+        int64_t ntotal = 0;
+        for (int i = 0; i < ni; ++i) {
+            SplitCandDev& c = cand[(size_t)i];
+            if (!c.active) continue;
+            const Item& it = items[(size_t)i];
+            if (cnt[2 * (size_t)i] == it.n || cnt[2 * (size_t)i + 1] == it.n) {
+                c.active = 0;
+                continue;
+            }
+            auto& ln = L[(size_t)it.leaf];
+            ln[(size_t)it.local].axis = axes[(size_t)i];
+            for (int k = 0; k < 2; ++k) {
+                ln[(size_t)it.local].child[k] = (int)ln.size();
+                ln.push_back(kids[2 * (size_t)i + (size_t)k]);
+                c.child_item[k] = (int32_t)next.size();
+                c.out[k] = ntotal;
+                next.push_back({it.leaf, (int)ln.size() - 1, ntotal, (int64_t)cnt[2 * (size_t)i + (size_t)k]});
+                ntotal += (int64_t)cnt[2 * (size_t)i + (size_t)k];
+            }
+        }
+        if (next.empty()) break;
+        if (ntotal > t->split_cap) {
+            // rare (many samples on split planes): the current level and its
+            // flags / ranks move to a larger scratch, recomputed there
+            r = split_grow(t, ntotal, cur, lvl_n, st, S);
+            if (r) return r;
+            HIP_TRY(hipMemcpyAsync(dcand, cand.data(), sizeof(SplitCandDev) * (size_t)ni, hipMemcpyHostToDevice,
+                                   st));
+            HIP_TRY(launch_split_flags(S.buf[cur].x, S.buf[cur].y, S.buf[cur].z, S.buf[cur].item, lvl_n, dcand, ni,
+                                       S.flags, S.rank, S.temp, S.temp_bytes, dcnt, st));
+        }
+        // (4) the stable partition into the next level (rejected items: inactive)
+        HIP_TRY(hipMemcpyAsync(dcand, cand.data(), sizeof(SplitCandDev) * (size_t)ni, hipMemcpyHostToDevice, st));
+        const DevSplitBuf In = S.buf[cur], O = S.buf[1 - cur];
+        HIP_TRY(launch_split_scatter(In.x, In.y, In.z, In.item, lvl_n, dcand, S.flags, S.rank, O.x, O.y, O.z,
+                                     O.item, st));
+        items.swap(next);
+        cur = 1 - cur;
+    }
+    HIP_TRY(hipStreamSynchronize(st));
     // renumber each leaf's breadth-first nodes to the creation (depth-first) order
     for (int i = 0; i < nl; ++i) {
-        const auto& Bn = L[(size_t)i].nodes;
+        const auto& Bn = L[(size_t)i];
         std::vector<STNodeHost> D;
         D.push_back(Bn[0]);
         D[0].child[0] = D[0].child[1] = -1;
+        // pre-order: a node's two children are numbered when it is visited,
+        // child 0's subtree before child 1's
         std::vector<std::pair<int, int>> stack{{0, 0}};   // (BFS index, D index)
-        // depth first, child 0's subtree before child 1's: a node's children are
-        // numbered when it is visited; the visit order is a pre-order
         while (!stack.empty()) {
             const auto [b, d] = stack.back();
             stack.pop_back();

@@ -154,19 +154,17 @@ __device__ __forceinline__ bool split_in(const float* mn, const float* mx, float
     return mn[0] <= a && a <= mx[0] && mn[1] <= b && b <= mx[1] && mn[2] <= c && c <= mx[2];
 }
 
-// children's sample counts of the candidate splits (integer atomics: order free)
-__global__ void __launch_bounds__(256)
-split_count_kernel(const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ z,
-                   const int32_t* __restrict__ item, int64_t n, const SplitCandDev* __restrict__ cand,
-                   unsigned long long* __restrict__ counts) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int it = item[i];
+// children's sample counts of the candidate splits from the flags' exclusive
+// scan: item it's child c holds rank[2 start + (c + 1) n] - rank[2 start + c n]
+// (rank has 2 n_level + 1 entries: the last is the total)
+__global__ void split_counts_kernel(const SplitCandDev* __restrict__ cand, int n_items,
+                                    const int64_t* __restrict__ rank, long long* __restrict__ counts) {
+    const int it = blockIdx.x * blockDim.x + threadIdx.x;
+    if (it >= n_items) return;
     const SplitCandDev& c = cand[it];
-    if (!c.active) return;
-    const float a = x[i], b = y[i], d = z[i];
-    if (split_in(c.mn0, c.mx0, a, b, d)) atomicAdd(&counts[2 * it], 1ull);
-    if (split_in(c.mn1, c.mx1, a, b, d)) atomicAdd(&counts[2 * it + 1], 1ull);
+    const int64_t b = 2 * c.start;
+    counts[2 * it] = (long long)(rank[b + c.n] - rank[b]);
+    counts[2 * it + 1] = (long long)(rank[b + 2 * c.n] - rank[b + c.n]);
 }
 
 // stable partition into the next level: item it's child-0 members then its
@@ -188,6 +186,7 @@ split_flags_kernel(const float* __restrict__ x, const float* __restrict__ y, con
     }
     flags[2 * c.start + j] = f0;
     flags[2 * c.start + c.n + j] = f1;
+    if (i == n - 1) flags[2 * n] = 0;   // the scan's last entry: the total
 }
 
 // rank[] = exclusive scan of flags; the child's members land at its out
@@ -256,24 +255,27 @@ hipError_t launch_split_sums(const float* x, const float* y, const float* z, con
     return hipGetLastError();
 }
 
-hipError_t launch_split_count(const float* x, const float* y, const float* z, const int32_t* item, int64_t n,
-                              const void* cand, unsigned long long* counts, hipStream_t st) {
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(split_count_kernel, split_grid(n), dim3(256), 0, st, x, y, z, item, n,
-                       (const SplitCandDev*)cand, counts);
-    return hipGetLastError();
-}
-
-hipError_t launch_split_partition(const float* x, const float* y, const float* z, const int32_t* item, int64_t n,
-                                  const void* cand, int32_t* flags, int64_t* rank, void* temp, size_t temp_bytes,
-                                  float* ox, float* oy, float* oz, int32_t* oitem, hipStream_t st) {
+// flags + exclusive scan (2 n + 1 entries) + the children's counts per item
+hipError_t launch_split_flags(const float* x, const float* y, const float* z, const int32_t* item, int64_t n,
+                              const void* cand, int n_items, int32_t* flags, int64_t* rank, void* temp,
+                              size_t temp_bytes, long long* counts, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(split_flags_kernel, split_grid(n), dim3(256), 0, st, x, y, z, item, n,
                        (const SplitCandDev*)cand, flags);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, flags, rank, (int)(2 * n), st);
+    e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, flags, rank, (int)(2 * n + 1), st);
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(split_counts_kernel, split_grid(n_items), dim3(256), 0, st, (const SplitCandDev*)cand,
+                       n_items, rank, counts);
+    return hipGetLastError();
+}
+
+// the stable partition of the accepted splits into the next level
+hipError_t launch_split_scatter(const float* x, const float* y, const float* z, const int32_t* item, int64_t n,
+                                const void* cand, const int32_t* flags, const int64_t* rank, float* ox, float* oy,
+                                float* oz, int32_t* oitem, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(split_scatter_kernel, split_grid(n), dim3(256), 0, st, x, y, z, item, n,
                        (const SplitCandDev*)cand, flags, rank, ox, oy, oz, oitem);
     return hipGetLastError();
