@@ -1265,6 +1265,23 @@ static void launch_group_fallback(int kmax, int blocks, hipStream_t st, const fl
 // sampled direction, each recomputing the pairs (a pair is ~40 small
 // matrix/vector ops; the kept conditional x lobes is tens of pairs).
 
+// Per-query cache of the product pairs formed by the mass pass (pass 1), so
+// the CDF walk and the pdf pass read them instead of re-forming every pair
+// (each ~40 small ops with fp64-rounded transcendentals).  Pair p of the
+// query in cache column `col`: fields f (weight, slot | lobe << 16, mean 3,
+// Linv 4, detInv) at base[(p * kPairFields + f) * stride + col] -- coalesced
+// across a wave's queries.  A query with more than cap pairs re-forms them.
+constexpr int kPairFields = 10;
+#ifndef SDMM_PAIR_CACHE
+#define SDMM_PAIR_CACHE 16
+#endif
+constexpr int kPairCacheCap = SDMM_PAIR_CACHE;
+struct PairCacheDev {
+    float* base;
+    int64_t stride;
+    int cap;
+};
+
 // heuristicConditionalWeight with a usable product (sdmm_proc.cpp:386-387)
 constexpr float kProductH = 0.3f;
 
@@ -1288,6 +1305,7 @@ struct ProductIO {
     // heuristic weight (0.3 product / 0.5 conditional), the reference's
     // rRec.nextSample1D() <= heuristicConditionalWeight (:392)
     const float* choice;
+    PairCacheDev cache;        // the thread path's pair cache (base null: none)
 };
 
 __device__ __forceinline__ float acos_x(float x) { return (float)acos((double)x); }
@@ -1573,7 +1591,7 @@ __device__ __forceinline__ void bsdf_world(const float F[9], const BsdfTab& bt, 
 }
 
 // Walk the product pairs in the reference's order (slot i asc, lobe j asc)
-// calling fn(pair_index, k, j, weight, comp) for every kept pair.
+// calling fn(pair_index, slot, k, j, weight, comp) for every kept pair.
 template <class Slots, class Fn>
 __device__ __forceinline__ void for_each_pair(const float* gp, int Kp, const float* condCov, const float c[3],
                                               int lastIdx, float invSum, bool scaled, float sum2,
@@ -1597,11 +1615,34 @@ __device__ __forceinline__ void for_each_pair(const float* gp, int Kp, const flo
             if (e[0] * mw[0] + e[1] * mw[1] + e[2] * mw[2] < 0.0f) continue;
             ProdComp pc;
             const float nw = mvtn_multiply(e, to_i, ci, mw, tw, cj, norm2, pc, lazy);
-            if (fn(p, k, j, wi * wj * nw, pc)) return;
+            if (fn(p, i, k, j, wi * wj * nw, pc)) return;
             ++p;
         }
     }
 }
+
+// Product pair (slot i, lobe j) evaluated on its own, exactly as
+// for_each_pair forms it (the same expressions): its weight wi * wj * nw and
+// component.  Used to re-form the one pair a cached walk selected.
+template <class Slots>
+__device__ __forceinline__ float eval_pair(const float* gp, int Kp, const float* condCov, const float c[3],
+                                           float invSum, bool scaled, float sum2, const Slots& S, int i,
+                                           const BsdfTab& bt, int b, int j, const float F[9], float norm2,
+                                           ProdComp& pc) {
+    float wi = S.valid(i) ? S.weight(i) : 0.0f;
+    if (scaled) wi = wi * invSum;
+    wi = wi / sum2;
+    const int k = S.comp(i);
+    float e[3], to_i[9], ci[4];
+    cond_mean_dir_x(gp, Kp, k, c, e);
+    coordinates_f(e, to_i);
+    for (int l = 0; l < 4; ++l) ci[l] = condCov[4 * k + l];
+    float mw[3], tw[9], cj[4], wj;
+    bsdf_world(F, bt, b, j, mw, tw, cj, wj);
+    const float nw = mvtn_multiply(e, to_i, ci, mw, tw, cj, norm2, pc, false);
+    return wi * wj * nw;
+}
+
 
 // MVTN<3,3>::pdf of a product component at d
 __device__ __forceinline__ float prod_comp_pdf(const ProdComp& pc, const float d[3], float norm2) {
@@ -1624,7 +1665,8 @@ __device__ __forceinline__ float prod_comp_pdf(const ProdComp& pc, const float d
 template <bool PDF_ONLY, class Slots>
 __device__ bool finish_product(const float* gp, int Kp, const float* condCov, const float c[3], int lastIdx,
                                float accum, const Slots& S, const BsdfTab& bt, int b, const float F[9],
-                               const float* u, const float* dir_in, float choice, GuideConsts gc, QueryOut& o) {
+                               const float* u, const float* dir_in, float choice, GuideConsts gc, QueryOut& o,
+                               const PairCacheDev& pcd, int64_t col) {
     const float invSum = 1.0f / accum;
     const bool scaled = __builtin_isfinite(invSum);
     float sum2 = 0.0f;
@@ -1633,11 +1675,30 @@ __device__ bool finish_product(const float* gp, int Kp, const float* condCov, co
         if (scaled) wi = wi * invSum;
         sum2 += wi;
     }
-    // pass 1: the product mass (createCdf(true)'s sum)
+    // pass 1: the product mass (createCdf(true)'s sum), each pair cached
     float total = 0.0f;
     int P = 0;
+    bool cached = pcd.base != nullptr;
+    auto cf = [&](int p, int f) -> float& { return pcd.base[((int64_t)p * kPairFields + f) * pcd.stride + col]; };
     for_each_pair(gp, Kp, condCov, c, lastIdx, invSum, scaled, sum2, S, bt, b, F, gc.norm2, true,
-                  [&](int, int, int, float w, const ProdComp&) { total += w; ++P; return false; });
+                  [&](int p, int i, int, int j, float w, const ProdComp& pc) {
+                      total += w;
+                      ++P;
+                      if (cached) {
+                          if (p >= pcd.cap) {
+                              cached = false;
+                          } else {
+                              cf(p, 0) = w;
+                              cf(p, 1) = __builtin_bit_cast(float, i | (j << 16));
+                              if (w != 0.0f) {   // (a zero-weight pair is never read back)
+                                  cf(p, 2) = pc.mean[0]; cf(p, 3) = pc.mean[1]; cf(p, 4) = pc.mean[2];
+                                  cf(p, 5) = pc.Linv[0]; cf(p, 6) = pc.Linv[1]; cf(p, 7) = pc.Linv[2];
+                                  cf(p, 8) = pc.Linv[3]; cf(p, 9) = pc.detInv;
+                              }
+                          }
+                      }
+                      return false;
+                  });
     if (P == 0 || total == 0.0f) return false;
     float dir[3];
     o.comp = kCompPdfValid;
@@ -1647,15 +1708,30 @@ __device__ bool finish_product(const float* gp, int Kp, const float* condCov, co
         float cdf = 0.0f, prev = 0.0f;
         int runStart = 0, sel = -1, selComp = -1, runComp = -1;
         ProdComp pcs{}, runPc{};
-        for_each_pair(gp, Kp, condCov, c, lastIdx, invSum, scaled, sum2, S, bt, b, F, gc.norm2, false,
-                      [&](int p, int k, int j, float w, const ProdComp& pc) {
-                          cdf += w / total;
-                          if (p == 0 || cdf != prev) { runStart = p; runComp = k * bt.M + j; runPc = pc; }
-                          prev = cdf;
-                          if (cdf >= u[0]) { sel = p; selComp = k * bt.M + j; pcs = pc; return true; }
-                          return false;
-                      });
-        if (sel < 0) { sel = runStart; selComp = runComp; pcs = runPc; }
+        if (cached) {
+            int selCode = -1, runCode = -1;
+            for (int p = 0; p < P; ++p) {
+                cdf += cf(p, 0) / total;
+                const int code = __builtin_bit_cast(int, cf(p, 1));
+                if (p == 0 || cdf != prev) { runStart = p; runCode = code; }
+                prev = cdf;
+                if (cdf >= u[0]) { sel = p; selCode = code; break; }
+            }
+            if (sel < 0) selCode = runCode;
+            const int si = selCode & 0xffff, sj = selCode >> 16;
+            (void)eval_pair(gp, Kp, condCov, c, invSum, scaled, sum2, S, si, bt, b, sj, F, gc.norm2, pcs);
+            selComp = S.comp(si) * bt.M + sj;
+        } else {
+            for_each_pair(gp, Kp, condCov, c, lastIdx, invSum, scaled, sum2, S, bt, b, F, gc.norm2, false,
+                          [&](int p, int, int k, int j, float w, const ProdComp& pc) {
+                              cdf += w / total;
+                              if (p == 0 || cdf != prev) { runStart = p; runComp = k * bt.M + j; runPc = pc; }
+                              prev = cdf;
+                              if (cdf >= u[0]) { sel = p; selComp = k * bt.M + j; pcs = pc; return true; }
+                              return false;
+                          });
+            if (sel < 0) { sel = runStart; selComp = runComp; pcs = runPc; }
+        }
         const float radius = sqrtf(-2.0f * log_x(1.0f - u[1]));
         const float theta = (float)(2.0 * kPi * (double)u[2]);
         const float z0 = radius * sin_x(theta), z1 = radius * cos_x(theta);
@@ -1670,12 +1746,24 @@ __device__ bool finish_product(const float* gp, int Kp, const float* condCov, co
     }
     // pass 3: the product mixture pdf at dir
     float acc = 0.0f;
-    for_each_pair(gp, Kp, condCov, c, lastIdx, invSum, scaled, sum2, S, bt, b, F, gc.norm2, true,
-                  [&](int, int, int, float w, const ProdComp& pc) {
-                      const float wn = w / total;
-                      if (wn != 0.0f) acc += wn * prod_comp_pdf(pc, dir, gc.norm2);
-                      return false;
-                  });
+    if (cached) {
+        for (int p = 0; p < P; ++p) {
+            const float wn = cf(p, 0) / total;
+            if (wn == 0.0f) continue;
+            ProdComp pc{};
+            pc.mean[0] = cf(p, 2); pc.mean[1] = cf(p, 3); pc.mean[2] = cf(p, 4);
+            pc.Linv[0] = cf(p, 5); pc.Linv[1] = cf(p, 6); pc.Linv[2] = cf(p, 7); pc.Linv[3] = cf(p, 8);
+            pc.detInv = cf(p, 9);
+            acc += wn * prod_comp_pdf(pc, dir, gc.norm2);
+        }
+    } else {
+        for_each_pair(gp, Kp, condCov, c, lastIdx, invSum, scaled, sum2, S, bt, b, F, gc.norm2, true,
+                      [&](int, int, int, int, float w, const ProdComp& pc) {
+                          const float wn = w / total;
+                          if (wn != 0.0f) acc += wn * prod_comp_pdf(pc, dir, gc.norm2);
+                          return false;
+                      });
+    }
     o.d[0] = dir[0]; o.d[1] = dir[1]; o.d[2] = dir[2];
     o.pdf = acc;
     return true;
@@ -1688,7 +1776,8 @@ __device__ bool finish_product(const float* gp, int Kp, const float* condCov, co
 template <bool PDF_ONLY, class Slots>
 __device__ __forceinline__ void product_tail(const float* gp, int Kp, const float* condCov, const float c[3],
                                              int lastIdx, float accum, const Slots& S, const GuideIO& io,
-                                             const ProductIO& pio, const BsdfTab& bt, int64_t q, GuideConsts gc) {
+                                             const ProductIO& pio, const BsdfTab& bt, int64_t q, GuideConsts gc,
+                                             int64_t col) {
     int b = pio.material ? pio.material[q] : -1;
     if (b >= bt.B) b = -1;
     const bool mixed = !PDF_ONLY && pio.choice != nullptr;
@@ -1715,7 +1804,8 @@ __device__ __forceinline__ void product_tail(const float* gp, int Kp, const floa
         if (b >= 0 && bt.M > 0) {
             float F[9];
             for (int i = 0; i < 9; ++i) F[i] = pio.F[i][q];
-            used = finish_product<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, accum, S, bt, b, F, u, dg, choice, gc, o);
+            used = finish_product<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, accum, S, bt, b, F, u, dg, choice, gc, o,
+                                            pio.cache, col);
         }
         if (used) {
             h = kProductH;
@@ -1758,7 +1848,7 @@ guide_product_cand_kernel(const float* __restrict__ gp, int Kp, int K, const flo
         fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
         return;
     }
-    product_tail<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, accum, CandSlots{cw, ck, 64, tid}, io, pio, bt, q, gc);
+    product_tail<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, accum, CandSlots{cw, ck, 64, tid}, io, pio, bt, q, gc, t);
 }
 
 // ---------------------------------------------------------------------------
@@ -2014,14 +2104,14 @@ __device__ __forceinline__ void serve_product_cand(const float* gp, int Kp, int 
                                                    const GuideIO& io, const ProductIO& pio, const BsdfTab& bt,
                                                    int64_t q, const float c[3], float* cw, unsigned short* ck,
                                                    int tid, int cap, GuideConsts gc, int* fb_count,
-                                                   int32_t* fb_list) {
+                                                   int32_t* fb_list, int64_t t) {
     float accum = 0.0f;
     const int lastIdx = build_candidates_reg<LCAP>(gp, Kp, K, c, cw, ck, 64, tid, gc.norm3, cap, accum);
     if (lastIdx < 0) {
         fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
         return;
     }
-    product_tail<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, accum, CandSlots{cw, ck, 64, tid}, io, pio, bt, q, gc);
+    product_tail<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, accum, CandSlots{cw, ck, 64, tid}, io, pio, bt, q, gc, t);
 }
 
 template <bool PDF_ONLY>
@@ -2058,7 +2148,7 @@ guide_tree_product_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideM
             product_invalid<PDF_ONLY>(io, pio, q);
         else
             serve_product_cand<PDF_ONLY, LCAP>(mx.gp, mx.Kp, mx.K, cctab[nw], io, pio, bt, q, c, cw, ck, tid, cap,
-                                               gc, fb_count, fb_list);
+                                               gc, fb_count, fb_list, t);
         break;
     }
 }
@@ -2326,6 +2416,22 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
     return hipGetLastError();
 }
 
+// the thread path's pair cache for `threads` query columns (stream ordered;
+// none when the allocation fails: the pairs are then re-formed, same results)
+static PairCacheDev pair_cache_alloc(int64_t threads, hipStream_t st) {
+    PairCacheDev pc{nullptr, threads, kPairCacheCap};
+    if (kPairCacheCap <= 0) return pc;
+    if (hipMallocAsync((void**)&pc.base, sizeof(float) * kPairFields * (size_t)kPairCacheCap * (size_t)threads, st) !=
+        hipSuccess) {
+        (void)hipGetLastError();
+        pc.base = nullptr;
+    }
+    return pc;
+}
+static void pair_cache_free(const PairCacheDev& pc, hipStream_t st) {
+    if (pc.base) (void)hipFreeAsync(pc.base, st);
+}
+
 // Product sampling (or its pdf, dgiven != null) against one mixture: the
 // candidate kernel (thread per query), then its full-K queries one per wave.
 hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* condCov, int64_t nq,
@@ -2358,6 +2464,7 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
         perm = sort->idx[1];
     }
     const dim3 grid((unsigned)((nq + 63) / 64));
+    pio.cache = pair_cache_alloc((int64_t)grid.x * 64, st);
 #define SDMM_PRODUCT_CAND(P, L)                                                                           \
     hipLaunchKernelGGL((guide_product_cand_kernel<P, L>), grid, dim3(64), 0, st, gp, Kp, K, condCov, nq, io, pio, \
                        bt, gc, cap, fb_count, fb_list, perm)
@@ -2372,6 +2479,7 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
     }
 #undef SDMM_PRODUCT_CAND
     e = hipGetLastError();
+    pair_cache_free(pio.cache, st);
     if (e != hipSuccess) return e;
     // the full-K queries' product pairs (up to kProductPairCap per query) live in a
     // stream-ordered scratch for the call: one slice per workgroup
@@ -2447,6 +2555,7 @@ hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const v
     const GuideMix* tb = (const GuideMix*)tab;
     const float* const* cc = (const float* const*)cctab;
     const dim3 grid((unsigned)((nq + 63) / 64));
+    pio.cache = pair_cache_alloc((int64_t)grid.x * 64, st);
 #define SDMM_TREE_PRODUCT_CAND(P, L)                                                                         \
     hipLaunchKernelGGL((guide_tree_product_cand_kernel<P, L>), grid, dim3(64), 0, st, nd, tb, cc, nq, iox, pio, \
                        bt, gc, cap, fb_count, fb_list, perm, node_out)
@@ -2461,6 +2570,7 @@ hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const v
     }
 #undef SDMM_TREE_PRODUCT_CAND
     e = hipGetLastError();
+    pair_cache_free(pio.cache, st);
     if (e != hipSuccess) return e;
     const unsigned fblocks = (unsigned)(cus * 4 * SDMM_PRODUCT_WPE);
     float* pscratch = nullptr;
