@@ -226,7 +226,9 @@ def wavefront_bench(pkg, synth, batch, shard, tree, dev, stream, ct, ut, gout, t
     comp = gout[2].cpu().numpy()
     q = ct[0].numel()
     return {"queries_per_s": q * world / (w_wall / steps), "Q": q * world, "ms_per_step": w_wall / steps * 1e3,
-            "kernel_us": w_kern * 1e6, "leaves_with_mixture": len(live), "nodes": nn, "K": K,
+            "kernel_us": w_kern * 1e6, "fp32_frac": q * 22.0 * K / w_kern / FP32_PEAK,
+            "flops_per_query_lower_bound": 22 * K, "hbm_frac": q * 48.0 / w_kern / HBM_PEAK,
+            "leaves_with_mixture": len(live), "nodes": nn, "K": K,
             "guided_frac": float((comp >= 0).mean()), "scaling": "weak (replicas: queries per rank)"}
 
 
@@ -551,8 +553,12 @@ def main():
             del wfull, wb
         # ---- fused stats kernel alone (per rank) ----
         st_wall, st_kern = timed(lambda: mix.estep_stats(shard, stats), args.steps)
+        # the fused E-step + statistics is compute-bound: SURVEY 8(d)'s ~113
+        # FP32 flops per (sample, component) pair (E-step 66 + rank-1 stats 47)
         out["estep_stats"] = {"ms_per_step": st_wall / args.steps * 1e3,
-                              "samples_per_s": N_global / (st_wall / args.steps)}
+                              "samples_per_s": N_global / (st_wall / args.steps),
+                              "kernel_us": st_kern * 1e6, "flops_per_pair": 113,
+                              "fp32_frac": n_local * K * 113.0 / st_kern / FP32_PEAK}
         # ---- guided queries (replicas: each rank serves Q/world queries) ----
         q_local = args.Q // world
         c, u = synth.sample_queries_near(batch, q_local, seed=synth.SEED_QUERIES + rank)
@@ -563,9 +569,15 @@ def main():
         mix.guide(ct, ut, gout)
         g_steps = max(3, args.steps // 4)
         g_wall, g_kern = timed(lambda: mix.guide(ct, ut, gout), g_steps)
+        # FP32 fraction of the guided queries, counted from below: the K
+        # marginal weights every query forms (3x3 triangular solve, squared
+        # norm, scaling: ~22 flops per component; the exp and the kept
+        # components' conditional / sample / pdf work not counted)
         out["guide"] = {"queries_per_s": q_local * world / (g_wall / g_steps), "Q": q_local * world,
                         "ms_per_step": g_wall / g_steps * 1e3, "bytes_per_query": 48,
-                        "kernel_us": g_kern * 1e6}
+                        "kernel_us": g_kern * 1e6, "flops_per_query_lower_bound": 22 * K,
+                        "fp32_frac": q_local * 22.0 * K / g_kern / FP32_PEAK,
+                        "hbm_frac": q_local * 48.0 / g_kern / HBM_PEAK}
         # ---- batched per-leaf EM: the plugin's tree leaves,
         # each its own K=16 mixture over its own samples (volpath_sdmm.cpp:287-311);
         # leaves shard across ranks with no exchange (weak scaling per rank) ----
