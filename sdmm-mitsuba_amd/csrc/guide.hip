@@ -512,7 +512,7 @@ __device__ __forceinline__ void finish_and_write(const float* gp, int Kp, const 
 // Candidate path of query q against one mixture; false: q needs the full-K
 // fallback (appended to fb_list).
 template <bool PDF_ONLY, int LCAP, bool REG = false>
-__device__ __forceinline__ bool serve_cand(const float* gp, int Kp, int K, const GuideIO& io, int64_t q,
+__device__ __forceinline__ void serve_cand(const float* gp, int Kp, int K, const GuideIO& io, int64_t q,
                                            const float c[3], float* cw, unsigned short* ck, int tid, int cap,
                                            GuideConsts gc, int* fb_count, int32_t* fb_list) {
     float accum = 0.0f;
@@ -520,42 +520,9 @@ __device__ __forceinline__ bool serve_cand(const float* gp, int Kp, int K, const
                             : build_candidates(gp, Kp, K, c, cw, ck, 64, tid, gc.norm3, cap, accum);
     if (lastIdx < 0) {
         fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
-        return false;
+        return;
     }
     finish_and_write<PDF_ONLY>(gp, Kp, c, lastIdx, accum, CandSlots{cw, ck, 64, tid}, io, q, gc);
-    return true;
-}
-
-// Wide leaves (the tree wavefront's K > cap leaves whose queries mostly
-// overflow the candidate list): per node, the queries the candidate pass saw
-// and how many of them went to the full-K path (nstat[2 v], nstat[2 v + 1]),
-// and skip[v] set from them between calls; a query of a skipped leaf goes to
-// the full-K path directly.  Both paths give the same bits, so the routing
-// changes only the cost.
-struct WideRoute {
-    const uint8_t* skip;   // nullable
-    unsigned* nstat;       // nullable
-};
-__device__ __forceinline__ void route_count(const WideRoute& wr, int node, bool uniform, bool overflowed) {
-    if (!wr.nstat || node < 0) return;
-    if (uniform) {
-        const uint64_t all = __builtin_amdgcn_ballot_w64(true);
-        const uint64_t ov = __builtin_amdgcn_ballot_w64(overflowed);
-        if ((int)__builtin_amdgcn_mbcnt_hi((uint32_t)(all >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)all, 0u)) == 0) {
-            atomicAdd(&wr.nstat[2 * node], (unsigned)__builtin_popcountll(all));
-            if (ov) atomicAdd(&wr.nstat[2 * node + 1], (unsigned)__builtin_popcountll(ov));
-        }
-    } else {
-        atomicAdd(&wr.nstat[2 * node], 1u);
-        if (overflowed) atomicAdd(&wr.nstat[2 * node + 1], 1u);
-    }
-}
-// skip[v] = at least 64 queries seen, more than half of them full-K
-__global__ void route_update_kernel(const unsigned* __restrict__ nstat, uint8_t* __restrict__ skip, int nn) {
-    const int v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= nn) return;
-    const unsigned q = nstat[2 * v], ov = nstat[2 * v + 1];
-    skip[v] = (q >= 64u && 2u * ov > q) ? 1 : 0;
 }
 
 // LDS list capacity LCAP (24 or 40): the lists are 6 B per entry per thread,
@@ -587,7 +554,7 @@ __global__ void __launch_bounds__(64)
 guide_tree_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __restrict__ tab, int64_t nq,
                        GuideIO io, GuideConsts gc, int cap, int* __restrict__ fb_count,
                        int32_t* __restrict__ fb_list, const int32_t* __restrict__ perm,
-                       int32_t* __restrict__ node_out, WideRoute wr) {
+                       int32_t* __restrict__ node_out) {
     __shared__ float cw[LCAP * 64];
     __shared__ unsigned short ck[LCAP * 64];
     const int tid = threadIdx.x;
@@ -607,17 +574,11 @@ guide_tree_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __re
         const int n0 = __builtin_amdgcn_readfirstlane(node);
         if (__builtin_amdgcn_ballot_w64(node != n0) == 0) {
             const GuideMix mx = (n0 >= 0) ? tab[n0] : GuideMix{nullptr, 0, 0};
-            if (mx.K <= 0) {
+            if (mx.K <= 0)
                 write_invalid<PDF_ONLY>(io, q);
-            } else if (wr.skip && wr.skip[n0]) {
-                // a wide leaf: straight to the full-K path
-                fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
-                route_count(wr, n0, true, true);
-            } else {
-                const bool ok = serve_cand<PDF_ONLY, LCAP, (LCAP >= kGuideCap)>(mx.gp, mx.Kp, mx.K, io, q, c, cw, ck,
-                                                                                tid, cap, gc, fb_count, fb_list);
-                route_count(wr, n0, true, !ok);
-            }
+            else
+                serve_cand<PDF_ONLY, LCAP, (LCAP >= kGuideCap)>(mx.gp, mx.Kp, mx.K, io, q, c, cw, ck, tid, cap, gc,
+                                                                 fb_count, fb_list);
             return;
         }
     }
@@ -625,16 +586,11 @@ guide_tree_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __re
         const int n0 = __builtin_amdgcn_readfirstlane(node);
         if (node != n0) continue;
         const GuideMix mx = (n0 >= 0) ? tab[n0] : GuideMix{nullptr, 0, 0};
-        if (mx.K <= 0) {
+        if (mx.K <= 0)
             write_invalid<PDF_ONLY>(io, q);
-        } else if (wr.skip && wr.skip[n0]) {
-            fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
-            route_count(wr, n0, false, true);
-        } else {
-            const bool ok = serve_cand<PDF_ONLY, LCAP, (LCAP >= kGuideCap)>(mx.gp, mx.Kp, mx.K, io, q, c, cw, ck,
-                                                                            tid, cap, gc, fb_count, fb_list);
-            route_count(wr, n0, false, !ok);
-        }
+        else
+            serve_cand<PDF_ONLY, LCAP, (LCAP >= kGuideCap)>(mx.gp, mx.Kp, mx.K, io, q, c, cw, ck, tid, cap, gc,
+                                                             fb_count, fb_list);
         break;
     }
 }
@@ -2332,16 +2288,16 @@ static hipError_t launch_cand(int cap, dim3 grid, hipStream_t st, const float* g
 template <bool PDF_ONLY>
 static hipError_t launch_tree_cand(int cap, dim3 grid, hipStream_t st, const STNodeDev* nd, const GuideMix* tb,
                                    int64_t nq, const GuideIO& io, GuideConsts gc, int* fb_count, int32_t* fb_list,
-                                   const int32_t* perm, int32_t* node_out, WideRoute wr) {
+                                   const int32_t* perm, int32_t* node_out) {
     if (cap <= 16)
         hipLaunchKernelGGL((guide_tree_cand_kernel<PDF_ONLY, 16>), grid, dim3(64), 0, st, nd, tb, nq, io, gc, cap,
-                           fb_count, fb_list, perm, node_out, wr);
+                           fb_count, fb_list, perm, node_out);
     else if (cap <= 24)
         hipLaunchKernelGGL((guide_tree_cand_kernel<PDF_ONLY, 24>), grid, dim3(64), 0, st, nd, tb, nq, io, gc, cap,
-                           fb_count, fb_list, perm, node_out, wr);
+                           fb_count, fb_list, perm, node_out);
     else
         hipLaunchKernelGGL((guide_tree_cand_kernel<PDF_ONLY, kGuideCap>), grid, dim3(64), 0, st, nd, tb, nq, io,
-                           gc, cap, fb_count, fb_list, perm, node_out, wr);
+                           gc, cap, fb_count, fb_list, perm, node_out);
     return hipGetLastError();
 }
 
@@ -2408,8 +2364,7 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
                              const float* const u[3], const float* const dgiven[3], float* const d[3],
                              float* pdf, int32_t* comp, int32_t* node_out, float norm2, float norm3, int cap,
                              int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
-                             const GuideSortScratch* sort, const uint8_t* pmode, int* fb2, uint8_t* route_skip,
-                             unsigned* route_stat, int num_nodes) {
+                             const GuideSortScratch* sort, const uint8_t* pmode, int* fb2) {
     if (nq <= 0) return hipSuccess;
     cap = (cap < 0) ? 0 : (cap > kGuideCap ? kGuideCap : cap);
     if (nq > INT32_MAX) return hipErrorInvalidValue;
@@ -2435,18 +2390,9 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
     const GuideIO io = make_io(c, u, dgiven, d, pdf, comp, pmode);
     if (pmode) dgiven = nullptr;   // mixed: the sampling kernels, pdf queries per pmode
     cap = cap < kmax ? cap : kmax;
-    // the wide-leaf routing only where a list can overflow (some K > cap)
-    const WideRoute wr = (kmax > cap && route_skip && route_stat) ? WideRoute{route_skip, route_stat}
-                                                                  : WideRoute{nullptr, nullptr};
-    e = dgiven ? launch_tree_cand<true>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_out, wr)
-               : launch_tree_cand<false>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_out, wr);
+    e = dgiven ? launch_tree_cand<true>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_out)
+               : launch_tree_cand<false>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_out);
     if (e != hipSuccess) return e;
-    if (wr.nstat && num_nodes > 0) {
-        hipLaunchKernelGGL(route_update_kernel, dim3((unsigned)((num_nodes + 255) / 256)), dim3(256), 0, st,
-                           (const unsigned*)route_stat, route_skip, num_nodes);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
     if (fb2 && kmax <= kGroupKMax) {
         e = hipMemsetAsync(fb2, 0, sizeof(int), st);
         if (e != hipSuccess) return e;

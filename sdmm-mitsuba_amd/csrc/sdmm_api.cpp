@@ -88,8 +88,7 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
                              const float* const u[3], const float* const dgiven[3], float* const d[3],
                              float* pdf, int32_t* comp, int32_t* node_out, float norm2, float norm3, int cap,
                              int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
-                             const GuideSortScratch* sort, const uint8_t* pmode = nullptr, int* fb2 = nullptr,
-                             uint8_t* route_skip = nullptr, unsigned* route_stat = nullptr, int num_nodes = 0);
+                             const GuideSortScratch* sort, const uint8_t* pmode = nullptr, int* fb2 = nullptr);
 hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* condCov, int64_t nq,
                                 const float* const c[3], const float* const u[3], const float* const dgiven[3],
                                 float* const d[3], float* pdf, int32_t* comp, const int32_t* material,
@@ -1973,10 +1972,8 @@ struct sdmm_stree {
     // was uploaded from) and the guided-batch scratch
     std::vector<GuideMixHost> tab_host;
     std::vector<const float*> cc_host;   // per node: the mixture's condCov (product wavefront)
-    void* dtab = nullptr;                // [nn] GuideMix, [nn] condCov pointers (dcctab), route stats / skips
+    void* dtab = nullptr;                // [nn] GuideMix, then [nn] condCov pointers (dcctab)
     void* dcctab = nullptr;
-    unsigned* droute_stat = nullptr;     // per node: queries, full-K queries (guide.hip WideRoute)
-    uint8_t* droute_skip = nullptr;
     size_t dtab_cap = 0;
     int tab_kmax = 0;
     int tab_cap = kGuideCapMax; // candidate capacity: the smallest of the bound mixtures' (sdmm_set_guide_capacity)
@@ -2806,7 +2803,7 @@ int st_upload_table(sdmm_stree* t, const sdmm_mix* const* node_mix) {
     if (same && t->dtab) return SDMM_OK;
     HIP_TRY(hipStreamSynchronize(t->stream));   // the previous copy may still read tab_host
     const size_t nb = nn ? nn : 1;
-    const size_t bytes = (sizeof(GuideMixHost) + sizeof(const float*) + 2 * sizeof(unsigned) + 1) * nb;
+    const size_t bytes = (sizeof(GuideMixHost) + sizeof(const float*)) * nb;
     if (bytes > t->dtab_cap) {
         if (t->dtab) HIP_TRY(hipFree(t->dtab));
         t->dtab = nullptr;
@@ -2814,10 +2811,6 @@ int st_upload_table(sdmm_stree* t, const sdmm_mix* const* node_mix) {
         t->dtab_cap = bytes;
     }
     t->dcctab = (char*)t->dtab + sizeof(GuideMixHost) * nb;
-    t->droute_stat = (unsigned*)((char*)t->dcctab + sizeof(const float*) * nb);
-    t->droute_skip = (uint8_t*)(t->droute_stat + 2 * nb);
-    // a new table: the wide-leaf routing starts over (every query tries its list)
-    HIP_TRY(hipMemsetAsync(t->droute_stat, 0, (2 * sizeof(unsigned) + 1) * nb, t->stream));
     t->tab_host.swap(tab);
     t->cc_host.swap(cc);
     HIP_TRY(hipMemcpyAsync(t->dtab, t->tab_host.data(), sizeof(GuideMixHost) * nn, hipMemcpyHostToDevice,
@@ -2864,8 +2857,7 @@ int st_guide(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const f
                               cus, t->stream, sort, pmode,
                               // the NaN hand-off list of the group fallback: the
                               // Morton keys' input buffer, free once the order is built
-                              (int*)t->guide_sort.keys[0], t->droute_skip, t->droute_stat,
-                              (int)t->nodes.size()));
+                              (int*)t->guide_sort.keys[0]));
     return SDMM_OK;
 }
 

@@ -228,33 +228,3 @@ def test_wavefront_orders_after_em_on_other_streams(pkg, synth, gpu):
     a, r = run(False), run(True)
     for x, y in zip(a, r):
         np.testing.assert_array_equal(x, y)
-
-
-def test_wide_leaf_routing_is_bitwise_neutral(pkg, synth, gpu):
-    """K = 128 leaves after one EM step are wide: most queries overflow the
-    candidate list.  After a call has counted that per leaf, later calls on
-    the same bound table send those leaves' queries straight to the full-K
-    path (guide.hip WideRoute) -- same bits as the first call and as the
-    per-leaf single-mixture guide."""
-    import torch
-    b, t, mixes, leaves = _tree_and_leaf_mixtures(pkg, synth, 128, skip_every=1000, iters=1)
-    nq = 1 << 15
-    c, u, d, ct, ut, dt = _queries(gpu, nq, 17, 0.0, 1.0)
-    t.bind(mixes)
-    runs = [t.guide(None, ct, ut) for _ in range(3)]
-    pdfs = [t.pdf(None, ct, dt) for _ in range(2)]
-    torch.cuda.synchronize()
-    for r in runs[1:]:
-        for a, x in zip((runs[0][0][0], runs[0][0][1], runs[0][0][2], runs[0][1], runs[0][2]),
-                        (r[0][0], r[0][1], r[0][2], r[1], r[2])):
-            np.testing.assert_array_equal(a.cpu().numpy(), x.cpu().numpy())
-    np.testing.assert_array_equal(pdfs[0].cpu().numpy(), pdfs[1].cpu().numpy())
-    node = t.find(ct).cpu().numpy()
-    for v in np.unique(node)[:6]:
-        if v < 0 or mixes[v] is None:
-            continue
-        idx = torch.from_numpy(np.nonzero(node == v)[0]).to(gpu)
-        dr, pr, cr = mixes[v].guide([x[idx] for x in ct], [x[idx] for x in ut])
-        torch.cuda.synchronize()
-        np.testing.assert_array_equal(runs[2][2][idx].cpu().numpy(), cr.cpu().numpy())
-        np.testing.assert_array_equal(runs[2][1][idx].cpu().numpy(), pr.cpu().numpy())
