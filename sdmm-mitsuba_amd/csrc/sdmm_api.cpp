@@ -45,6 +45,11 @@ hipError_t launch_estep_resp_mfma(int variant, const float* ep, int Kp, int K, c
                                   int64_t chunk, float* resp, hipStream_t st);
 hipError_t estep_resp_mfma_occupancy(int variant, int Kp, int* blocks_per_cu);
 const char* estep_resp_mfma_name(int variant, int Kp);
+bool estep_resp_split_supported(int Kp);
+hipError_t launch_estep_resp_split(int variant, const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
+                                   int64_t resident_waves, float* resp, hipStream_t st);
+hipError_t estep_resp_split_occupancy(int variant, int Kp, int* waves_per_cu);
+const char* estep_resp_split_name(int variant, int Kp);
 hipError_t launch_estep_stats_tile(int variant, const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
                                    int64_t chunk, int blocks, float* partials, int pstride, hipStream_t st,
                                    const LeafDesc* leaves = nullptr, const int2* items = nullptr);
@@ -281,6 +286,7 @@ struct sdmm_mix {
     int rcpl = 2, rlps = 64;                 // responsibility E-step layout (same Kp)
     int rtile = 0;                           // 1: estep_resp_tile_kernel (64 < K <= 128)
                                              // 2: estep_resp_mfma_kernel (every K)
+                                             // 3: estep_resp_split_kernel (bf16x3 MFMA forms, Kp <= 128)
     int rvariant = 4;                        // tile kernel variant (SDMM_RESP_VARIANT): KT=8, 3 waves/SIMD
     int stile = 0;                           // 1: estep_stats_tile_kernel (64 < K <= 128)
                                              // 2: its GROUP form (128 < K <= 512: Kp / 128 waves per chunk)
@@ -656,10 +662,10 @@ void constructor_scalars(const sdmm_mix* m, double* scal) {
     scal[SC_CUT] = 32.0;
 }
 
-// E-step occupancy per K (the layout choice depends on K and the process's
-// environment only): queried once
+// E-step occupancy per K and kernel choice (the layout depends on K and the
+// process's environment only): queried once per combination
 struct OccCache {
-    int K = -1, resp = 0, stats = 0;
+    int K = -1, kern = -1, resp = 0, stats = 0;
 };
 
 int create_impl(int K, const sdmm_em_params* params, int device, hipStream_t ordered, bool on_stream,
@@ -691,20 +697,29 @@ int create_impl(int K, const sdmm_em_params* params, int device, hipStream_t ord
     m->rcpl = cpl;
     m->rlps = lps;
     if (K > 64 && K <= 128) { m->rcpl = 4; m->rlps = 32; }
-    // 64 < K <= 128: the tiled kernel (one packed pair per lane, 16-sample
-    // tiles, transposed normaliser reduction); SDMM_RESP_KERNEL=legacy keeps
-    // estep_resp_kernel<4,32> (A/B measurements)
+    // 64 < K <= 128 (Kp = 128): the bf16x3 split-MFMA kernel (estep_split.hip:
+    // the eight linear forms on the matrix cores, the rest packed f32; 186 vs
+    // 204 us per 2^20 samples).  SDMM_RESP_KERNEL selects
+    // the others for A/B measurements: tile (estep_resp_tile_kernel, the VALU
+    // form), mfma (f32 matrix cores, estep_mfma.hip), legacy
+    // (estep_resp_kernel<4,32>); split also for other K with Kp / 16 in {1, 2, 4}.
     {
         const char* ev = std::getenv("SDMM_RESP_KERNEL");
         const bool legacy = ev && std::strcmp(ev, "legacy") == 0;
         const bool mfma = ev && std::strcmp(ev, "mfma") == 0;
-        if (K > 64 && K <= 128 && !legacy && !mfma) { m->rtile = 1; m->rcpl = 2; m->rlps = 64; }
-        // SDMM_RESP_KERNEL=mfma: the linear forms on the f32 matrix cores
-        // (estep_mfma.hip); measured slower on gfx950 (no VALU/MFMA co-execution
-        // for f32 MFMA), kept as a tested alternative
+        const bool tile = ev && std::strcmp(ev, "tile") == 0;
+        const bool split = ev && std::strcmp(ev, "split") == 0;
+        if (K > 64 && K <= 128 && !legacy && !mfma) {
+            m->rtile = 1;
+            m->rcpl = 2;
+            m->rlps = 64;
+            if (!tile && estep_resp_split_supported(m->Kp)) m->rtile = 3;
+        }
         if (mfma) m->rtile = 2;
+        if (split && estep_resp_split_supported(m->Kp)) m->rtile = 3;
         const char* vv = std::getenv("SDMM_RESP_VARIANT");
         if (vv) m->rvariant = std::atoi(vv);
+        if (m->rtile == 3) m->rvariant = vv ? std::atoi(vv) : 0;
         const char* sv = std::getenv("SDMM_STATS_KERNEL");
         if (K > 64 && K <= 128 && !(sv && std::strcmp(sv, "legacy") == 0)) m->stile = 1;
         if (K > 128 && K <= 512 && !(sv && std::strcmp(sv, "legacy") == 0)) m->stile = 2;
@@ -713,7 +728,8 @@ int create_impl(int K, const sdmm_em_params* params, int device, hipStream_t ord
     }
     static thread_local OccCache occ[8];
     OccCache& oc = occ[(K * 7 + device) & 7];
-    if (oc.K == K * 64 + device) {
+    const int kern = ((m->rtile * 16 + m->rvariant) * 16 + m->stile) * 16 + m->svariant;
+    if (oc.K == K * 64 + device && oc.kern == kern) {
         m->resp_blocks = oc.resp;
         m->stats_blocks = oc.stats;
     } else {
@@ -723,11 +739,18 @@ int create_impl(int K, const sdmm_em_params* params, int device, hipStream_t ord
             return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
         if (m->rtile == 2 && estep_resp_mfma_occupancy(m->rvariant, m->Kp, &m->resp_blocks) != hipSuccess)
             return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
+        if (m->rtile == 3) {
+            int wpc = 0;
+            if (estep_resp_split_occupancy(m->rvariant, m->Kp, &wpc) != hipSuccess)
+                return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
+            m->resp_blocks = wpc;   // resident waves per CU (split kernel)
+        }
         if (m->rtile == 1 && estep_resp_tile_occupancy(m->rvariant, &m->resp_blocks) != hipSuccess)
             return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
         if (m->stile && estep_stats_tile_occupancy(m->svariant, m->Kp, &m->stats_blocks) != hipSuccess)
             return cleanup(fail(SDMM_E_HIP, "E-step occupancy query failed"));
         oc.K = K * 64 + device;
+        oc.kern = kern;
         oc.resp = m->resp_blocks;
         oc.stats = m->stats_blocks;
     }
@@ -991,7 +1014,10 @@ const char* sdmm_kernel_name(const sdmm_mix* m, int which) {
     if (!m) return "";
     static thread_local char buf[64];
     if (which == 0) {
-        if (m->rtile == 2) {
+        if (m->rtile == 3) {
+            std::snprintf(buf, sizeof buf, "%s", estep_resp_split_name(m->rvariant, m->Kp));
+            return buf;
+        } else if (m->rtile == 2) {
             std::snprintf(buf, sizeof buf, "%s", estep_resp_mfma_name(m->rvariant, m->Kp));
             return buf;
         } else if (m->rtile) {
@@ -1719,6 +1745,11 @@ int sdmm_responsibilities(sdmm_mix* m, const sdmm_samples* s, float* resp) {
     int r = check_samples(s);
     if (r) return r;
     if (s->n == 0) return SDMM_OK;
+    if (m->rtile == 3) {
+        const int64_t resident = (int64_t)m->cus * (m->resp_blocks > 0 ? m->resp_blocks : 1);
+        HIP_TRY(launch_estep_resp_split(m->rvariant, m->ep, m->Kp, m->K, to_dev(s), s->n, resident, resp, m->stream));
+        return SDMM_OK;
+    }
     if (m->rtile == 2) {
         // chunks of whole 16-sample tiles, ~3 rounds of resident waves
         const int64_t resident = (int64_t)m->cus * 4 * (m->resp_blocks > 0 ? m->resp_blocks : 1);

@@ -394,6 +394,7 @@ def test_sample_discrete_cdf_bit_exact(pkg, oracle, gpu):
 
 
 @pytest.mark.parametrize("kernel,K", [("mfma", 128), ("mfma", 72), ("mfma", 16), ("mfma", 256), ("mfma", 512),
+                                      ("split", 128), ("split", 72), ("split", 32), ("split", 16),
                                       ("tile", 128), ("legacy", 128), ("legacy", 256)])
 def test_responsibilities_fitted_each_kernel(pkg, oracle, synth, gpu, monkeypatch, kernel, K):
     """Every responsibility kernel (SDMM_RESP_KERNEL) on a FITTED mixture (4 EM
@@ -406,7 +407,7 @@ def test_responsibilities_fitted_each_kernel(pkg, oracle, synth, gpu, monkeypatc
     N = 3001
     b, mix, m = _em_model(pkg, oracle, synth, K, N, 4)
     name = mix.kernel_name("resp")
-    assert {"mfma": "mfma", "tile": "tile", "legacy": "estep_resp_kernel"}[kernel] in name, name
+    assert {"mfma": "mfma", "split": "split", "tile": "tile", "legacy": "estep_resp_kernel"}[kernel] in name, name
     ds = pkg.DeviceSamples.from_numpy(b["x"], b["w"], b["hpdf"], b["is_diffuse"])
     resp = torch.full((N, K), -1.0, device=gpu)
     mix.posterior(ds, resp)
