@@ -77,25 +77,36 @@ __device__ __forceinline__ unsigned pk(float lo, float hi) {
 __device__ __forceinline__ float hi_of(unsigned d) { return __builtin_bit_cast(float, d & 0xFFFF0000u); }
 __device__ __forceinline__ float lo_of(unsigned d) { return __builtin_bit_cast(float, d << 16); }
 
-// A fragment of one lane: feature x of its sample, entries [h h m h l m e6 e7]
-__device__ __forceinline__ bf8 a_frag(float x, unsigned e67) {
-    const unsigned d0 = pk(x, x);            // (h, h)
-    const float r1 = x - hi_of(d0);          // exact
-    const unsigned d1 = pk(r1, x);           // (m, h)
-    const float r2 = r1 - lo_of(d1);         // exact, <= 8 significant bits
-    const unsigned d2 = pk(r2, r1);          // (l, m)
-    return __builtin_bit_cast(bf8, u4{d0, d1, d2, e67});
+// Split x into (h, m, l) bf16 parts as floats' dwords: see the header.
+// Sample fragment of one lane (K layout in the header): lane group g < 3 holds
+// the small products of feature g, [h m h l m e5 e6 0]; group 3 holds the
+// three large ones and the constant's largest part, [0 0 0 0 x0h x1h x2h e7].
+// x: the sample's three features; spatial: the forms with the constant NC.
+__device__ __forceinline__ bf8 a_frag(const float (&x)[3], int g, bool spatial) {
+    const float xg = g == 0 ? x[0] : (g == 1 ? x[1] : x[2]);   // (g < 3)
+    const unsigned t = pk(xg, xg);
+    const float r1 = xg - hi_of(t);               // exact
+    const unsigned d0 = pk(xg, r1);               // (h, m)
+    const float r2 = r1 - hi_of(d0);              // exact, <= 8 significant bits
+    const unsigned d1 = pk(xg, r2);               // (h, l)
+    const bool cst = spatial && g == 0;
+    const unsigned d2 = pk(r1, cst ? 1.0f : 0.0f);   // (m, e5)
+    const unsigned d3 = cst ? 0x3F80u : 0u;          // (e6, 0)
+    const unsigned q2 = pk(x[0], x[1]);              // (x0h, x1h)
+    const unsigned q3 = pk(x[2], spatial ? 1.0f : 0.0f);   // (x2h, e7)
+    return __builtin_bit_cast(bf8, g < 3 ? u4{d0, d1, d2, d3} : u4{0u, 0u, q2, q3});
 }
 
-// B fragment entries [hc mc hc lc hc mc X6 X7] of coefficient c
-__device__ __forceinline__ u4 b_frag(float c, unsigned x67) {
+// (h, m, l) of an fp32 value as bf16 bit patterns
+__device__ __forceinline__ void split3(float c, unsigned& h, unsigned& m, unsigned& l) {
     const unsigned hh = pk(c, c);
     const float r1 = c - hi_of(hh);
     const unsigned mm = pk(r1, r1);
     const float r2 = r1 - lo_of(mm);
     const unsigned ll = pk(r2, r2);
-    const unsigned h = hh & 0xFFFFu, m = mm & 0xFFFFu, l = ll & 0xFFFFu;
-    return u4{h | (m << 16), h | (l << 16), h | (m << 16), x67};
+    h = hh & 0xFFFFu;
+    m = mm & 0xFFFFu;
+    l = ll & 0xFFFFu;
 }
 
 // sqrt(log2(e) / 2): the rows of u (spatial forms, ad, bd) are pre-scaled by
@@ -118,7 +129,16 @@ __device__ __forceinline__ int lrow(int m) { return EP_L00 + m * (m + 1) / 2; }
 // components the two terms stay small for the samples whose pdfs matter (the
 // MFMA accumulation error scales with them; a single scene-centre origin left
 // the heuristic row sums at 1.2e-5 of the fp64 evaluation instead of 4e-6).
+#ifdef SDMM_SPLIT_BLOCKORIGIN
+constexpr bool kBlockOrigin = true;
+#else
+constexpr bool kBlockOrigin = false;
+#endif
 __device__ __forceinline__ void block_origin(const float* __restrict__ ep, int Kp, int r, float* o) {
+    if (!kBlockOrigin) {
+        o[0] = o[1] = o[2] = kOrigin;
+        return;
+    }
     double acc[3] = {0.0, 0.0, 0.0};
     int cnt = 0;
     for (int i = 0; i < 16; ++i) {
@@ -133,38 +153,45 @@ __device__ __forceinline__ void block_origin(const float* __restrict__ ep, int K
     for (int j = 0; j < 3; ++j) o[j] = cnt ? (float)(acc[j] / cnt) : kOrigin;
 }
 
-// B fragment of block r, form f, lane l.  Forms: 0 c (R2), 1 ad (A), 2 bd (B),
-// 3 + m the spatial row m (L_m0..L_m2 of L^-1, constant NC_m(o_r) =
-// -sum_j L_mj (mu_j - o_r) in fp64).
+// Coefficient fragment of block r, form f, lane l (the A operand of the
+// MFMA; K layout in the header): lane group g < 3 pairs feature g's small
+// products, [cm ch cl ch cm X5 X6 0] with X5, X6 = NC's l, m parts in group 0
+// of the spatial forms; group 3 holds [0 0 0 0 c0h c1h c2h X7], X7 = NC's h
+// part.  Forms: 0 c (R2), 1 ad (A), 2 bd (B), 3 + m the spatial row m
+// (L_m0..L_m2 of L^-1, constant NC_m(o) = -sum_j L_mj (mu_j - o) in fp64).
 __device__ __forceinline__ u4 coef_frag(const float* __restrict__ ep, int Kp, int r, int f, int l,
                                         const float* __restrict__ o) {
     const int k = 16 * r + (l & 15);
     const int g = l >> 4;
-    if (g == 3) return u4{0u, 0u, 0u, 0u};
-    float c;
-    unsigned x67 = 0u;
+    float c[3];
+    unsigned nh = 0u, nm = 0u, nl = 0u;
     if (f < 3) {
         const int base = f == 0 ? EP_R20 : (f == 1 ? EP_A0 : EP_B0);
-        c = ep[(base + g) * Kp + k];
-        if (f > 0) c = (float)((double)c * kRowScale);
+        for (int j = 0; j < 3; ++j) {
+            c[j] = ep[(base + j) * Kp + k];
+            if (f > 0) c[j] = (float)((double)c[j] * kRowScale);
+        }
     } else {
         const int m = f - 3;
-        c = (m <= 2 && g > m) ? 0.0f : (float)((double)ep[(lrow(m) + g) * Kp + k] * kRowScale);
-        if (g < 2) {
-            double acc = 0.0;
-            const int jn = m < 3 ? m + 1 : 3;
-            for (int j = 0; j < jn; ++j)
-                acc += (double)ep[(lrow(m) + j) * Kp + k] * ((double)ep[(EP_MU0 + j) * Kp + k] - (double)o[j]);
-            const float nc = (float)(-acc * kRowScale);
-            const unsigned hh = pk(nc, nc);
-            const float r1 = nc - hi_of(hh);
-            const unsigned mm = pk(r1, r1);
-            const float r2 = r1 - lo_of(mm);
-            const unsigned ll = pk(r2, r2);
-            x67 = g == 0 ? ((hh & 0xFFFFu) | (mm << 16)) : (ll & 0xFFFFu);
+        double acc = 0.0;
+        for (int j = 0; j < 3; ++j) {
+            const bool z = m <= 2 && j > m;
+            c[j] = z ? 0.0f : (float)((double)ep[(lrow(m) + j) * Kp + k] * kRowScale);
+            if (!z) acc += (double)ep[(lrow(m) + j) * Kp + k] * ((double)ep[(EP_MU0 + j) * Kp + k] - (double)o[j]);
         }
+        split3((float)(-acc * kRowScale), nh, nm, nl);
     }
-    return b_frag(c, x67);
+    if (g < 3) {
+        unsigned h, m, lo;
+        split3(c[g], h, m, lo);
+        const unsigned x5 = g == 0 ? nl : 0u, x6 = g == 0 ? nm : 0u;
+        return u4{m | (h << 16), lo | (h << 16), m | (x5 << 16), x6};
+    }
+    unsigned h0, h1, h2, t1, t2;
+    split3(c[0], h0, t1, t2);
+    split3(c[1], h1, t1, t2);
+    split3(c[2], h2, t1, t2);
+    return u4{0u, 0u, h0 | (h1 << 16), h2 | (nh << 16)};
 }
 
 // sum over the 16 lanes of a DPP row; every lane of the row gets the sum
@@ -298,26 +325,23 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
     // D gives lane (g, col) components 16 r + 4 g + j (j = 0..3) of sample col
     const int g = lane >> 4;
     const int col = lane & 15;
-    const int gf = g < 3 ? g : 2;
-    const float* pp = s.x[gf];
-    const float* pd = s.x[3 + gf];
-    // sample-fragment dword 3 of the spatial forms: the constant feature 1
-    // (group 0: two entries, group 1: one) against NC_m's split
-    const unsigned e67 = g == 0 ? 0x3F803F80u : (g == 1 ? 0x00003F80u : 0u);
     const bool has_h = s.hpdf != nullptr, has_d = s.isDiffuse != nullptr;
 
-    // the lane's sample col of tile t: feature g (position - o, direction) and,
-    // when present, the heuristic pdf and the diffuse flag (its dword)
+    // sample col of tile t: position and direction coordinate g (lane group 3
+    // loads coordinate 0 and gathers all three from groups 0..2 when the
+    // fragments are built) and, when present, the heuristic pdf and the
+    // diffuse flag (its dword)
+    const int gf = g < 3 ? g : 0;
     struct Feat {
-        float fs, fd, hp;
+        float p, d, hp;
         int dw;
     };
     auto load_feat = [&](int64_t t) {
         int64_t i = t + col;
         i = (i < s1) ? i : s1 - 1;
         Feat f;
-        f.fs = __builtin_nontemporal_load(pp + i);
-        f.fd = __builtin_nontemporal_load(pd + i);
+        f.p = __builtin_nontemporal_load(s.x[gf] + i);
+        f.d = __builtin_nontemporal_load(s.x[3 + gf] + i);
         // optional planes: always load (from a valid plane when absent), select after
         const float* hpp = has_h ? s.hpdf : s.x[0];
         const uint8_t* dpp = has_d ? s.isDiffuse : (const uint8_t*)s.x[0];
@@ -325,13 +349,21 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
         f.dw = *(const __attribute__((address_space(1))) int*)((uintptr_t)(dpp + i) & ~(uintptr_t)3);
         return f;
     };
-    // block r's coefficient fragments, detInv pi of the lane's four
-    // components and coordinate g of the block's spatial origin
-    auto frags = [&](int r, bf8 (&F)[8], f4& dp, float& og) __attribute__((always_inline)) {
+    // the three coordinates of sample col from lane groups 0..2
+    auto gather3 = [&](float v, float (&x)[3]) __attribute__((always_inline)) {
+        x[0] = __shfl(v, col);
+        x[1] = __shfl(v, 16 + col);
+        x[2] = __shfl(v, 32 + col);
+    };
+    auto pfrag = [&](const float (&p3)[3], const float* o) __attribute__((always_inline)) {
+        const float x[3] = {p3[0] - o[0], p3[1] - o[1], p3[2] - o[2]};
+        return a_frag(x, g, true);
+    };
+    // block r's coefficient fragments and detInv pi of the lane's four components
+    auto frags = [&](int r, bf8 (&F)[8], f4& dp) __attribute__((always_inline)) {
 #pragma unroll
         for (int f = 0; f < 8; ++f) F[f] = __builtin_bit_cast(bf8, cimg[(r * 8 + f) * 64 + lane]);
         dp = dimg[r * 4 + g];
-        og = borig[r][gf];
     };
     auto forms = [&](const bf8 (&F)[8], bf8 bs, bf8 bd, f4 (&D)[8]) __attribute__((always_inline)) {
         const f4 z = f4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -399,14 +431,16 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
     Feat nf = load_feat(s0);
     for (int64_t t = s0; t < s1; t += 16) {
         const Feat cf = nf;
-        const float fd = (g < 3) ? cf.fd : 0.0f;
+        float P3[3], D3[3];
+        gather3(cf.p, P3);
+        gather3(cf.d, D3);
         // d == 0 fails every log map (mvtn.h:152-154)
-        const uint64_t zb = __builtin_amdgcn_ballot_w64(g < 3 && fd == 0.0f);
-        const bool dzero = ((zb & (zb >> 16) & (zb >> 32)) >> col) & 1u;
+        const bool dzero = D3[0] == 0.0f && D3[1] == 0.0f && D3[2] == 0.0f;
         const bool dif = has_d && ((cf.dw >> (8 * (int)((uintptr_t)(s.isDiffuse + ((t + col < s1) ? t + col : s1 - 1)) & 3))) & 0xff) != 0;
         const float hp = has_h ? cf.hp : 0.0f;
-        // spatial sample fragments are built per block (its origin), below
-        const bf8 Bd = a_frag(fd, 0u);
+        const bf8 Bd = a_frag(D3, g, false);
+        const float o0[3] = {kOrigin, kOrigin, kOrigin};
+        const bf8 Bs0 = pfrag(P3, o0);   // one origin for every block unless kBlockOrigin
         __builtin_amdgcn_sched_barrier(0);
         flush();                          // tile t - 16's rows
         __builtin_amdgcn_sched_barrier(0);
@@ -438,18 +472,20 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
         {
             // pipelined over the blocks: block r + 1's fragments are read from
             // LDS while block r's pair math runs
-            bf8 F[2][8];
+            bf8 F[2][8], BS[2];
             f4 dp[2];
-            float og[2];
-            frags(0, F[0], dp[0], og[0]);
+            frags(0, F[0], dp[0]);
+            BS[0] = kBlockOrigin ? pfrag(P3, borig[0]) : Bs0;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 f4 D[8];
-                forms(F[r & 1], a_frag(g < 3 ? cf.fs - og[r & 1] : 0.0f, e67), Bd, D);
+                forms(F[r & 1], BS[r & 1], Bd, D);
                 __builtin_amdgcn_sched_barrier(0);
-                if (r + 1 < R) frags(r + 1, F[(r + 1) & 1], dp[(r + 1) & 1], og[(r + 1) & 1]);
+                if (r + 1 < R) frags(r + 1, F[(r + 1) & 1], dp[(r + 1) & 1]);
                 __builtin_amdgcn_sched_barrier(0);
                 pair_math(r, Tag<false>{}, D, dp[r & 1]);
+                // the next block's spatial sample fragment, off the MFMA issue path
+                if (r + 1 < R) BS[(r + 1) & 1] = kBlockOrigin ? pfrag(P3, borig[r + 1]) : Bs0;
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -464,17 +500,15 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
 #else
         if (__builtin_amdgcn_ballot_w64(odd) != 0) {
 #endif
-            bf8 bd2 = Bd;
-            float ps2 = cf.fs;
-            asm volatile("" : "+v"(ps2), "+v"(bd2));
+            bf8 bd2 = Bd, bs2 = Bs0;
+            asm volatile("" : "+v"(bd2), "+v"(bs2));
             acc = f2{0.0f, 0.0f};
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 bf8 F[8];
                 f4 dp, D[8];
-                float o1;
-                frags(r, F, dp, o1);
-                forms(F, a_frag(g < 3 ? ps2 - o1 : 0.0f, e67), bd2, D);
+                frags(r, F, dp);
+                forms(F, kBlockOrigin ? pfrag(P3, borig[r]) : bs2, bd2, D);
                 pair_math(r, Tag<true>{}, D, dp);
             }
         }
@@ -500,15 +534,17 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
 // The B image takes R x 8 KB of LDS per workgroup.
 #define SDMM_SPLIT_CONFIGS(X) X(1, 4, 4) X(2, 4, 4) X(4, 4, 4) X(8, 4, 2) X(8, 8, 2) X(8, 12, 3)
 
-// R = 8 (K = 128): variant 0 = 12 waves per workgroup at 3 per SIMD (one
-// workgroup per CU), 1 = two 4-wave workgroups, 2 = one 8-wave workgroup
+// R = 8 (K = 128): variant 0 = one 8-wave workgroup per CU at 2 waves per
+// SIMD (256 VGPRs: double-buffered fragments, no spill; 189 us at N = 2^20),
+// 1 = two 4-wave workgroups, 2 = 12 waves at 3 per SIMD (168 VGPRs, spills;
+// 199 us)
 static void split_cfg(int R, int variant, int* wpb, int* occ) {
     *wpb = 4;
     *occ = 4;
     if (R == 8) {
-        *wpb = 12; *occ = 3;
+        *wpb = 8; *occ = 2;
         if (variant == 1) { *wpb = 4; *occ = 2; }
-        if (variant == 2) { *wpb = 8; *occ = 2; }
+        if (variant == 2) { *wpb = 12; *occ = 3; }
     }
 }
 
