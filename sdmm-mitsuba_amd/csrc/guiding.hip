@@ -40,6 +40,10 @@
 
 namespace sdmm_detail {
 int set_error(int code, const char* msg);
+int push_training_ex(sdmm_stree* t, const sdmm_path_vertices* v, int saved_per_path, uint64_t seed,
+                     const sdmm_training_out* out, int64_t* n_out, int64_t* seg, int64_t* lost, bool reuse_counts,
+                     int64_t known_count);
+void destroy_many(sdmm_mix* const* ms, int n);
 }  // namespace sdmm_detail
 
 namespace {
@@ -199,7 +203,9 @@ namespace {
 
 int grow_pool(sdmm_guiding* g, Pool& P, int64_t need) {
     if (need <= P.cap) return SDMM_OK;
-    int64_t cap = std::max<int64_t>(need, P.cap * 2);
+    // headroom for the next passes' records (every regrowth copies and
+    // synchronises; HBM is plentiful)
+    int64_t cap = std::max<int64_t>(need + need / 2, P.cap * 2);
     cap = std::max<int64_t>(cap, 1 << 16);
     float* np[2] = {nullptr, nullptr};
     int32_t* nn[2] = {nullptr, nullptr};
@@ -296,6 +302,7 @@ int relabel(sdmm_guiding* g, Pool& P, const uint8_t* dsplit, const int32_t* dpar
 // leaf move to its new leaves.  A new node's split leaf is its first ancestor
 // that existed before (new nodes are numbered after every old one).
 int redistribute(sdmm_guiding* g, int old_nodes) {
+    PhaseClock clk(g->st);
     const int nn = sdmm_stree_num_nodes(g->tree);
     std::vector<int32_t> child(2 * (size_t)nn), parent((size_t)nn, -1);
     SDMM_TRY(sdmm_stree_get_nodes(g->tree, nullptr, child.data(), nullptr));
@@ -326,11 +333,16 @@ int redistribute(sdmm_guiding* g, int old_nodes) {
         SDMM_TRY(sdmm_clone_many(src.data(), (int)src.size(), made.data()));   // (on the model's stream)
         for (size_t i = 0; i < dst.size(); ++i) g->mix[(size_t)dst[i]] = made[i];
     }
-    for (int v = 0; v < old_nodes; ++v)
-        if (was_split[(size_t)v] && g->mix[(size_t)v]) {
-            sdmm_destroy(g->mix[(size_t)v]);
-            g->mix[(size_t)v] = nullptr;
-        }
+    clk.lap("redis:clone");
+    {
+        std::vector<sdmm_mix*> gone;
+        for (int v = 0; v < old_nodes; ++v)
+            if (was_split[(size_t)v] && g->mix[(size_t)v]) {
+                gone.push_back(g->mix[(size_t)v]);
+                g->mix[(size_t)v] = nullptr;
+            }
+        sdmm_detail::destroy_many(gone.data(), (int)gone.size());
+    }
     if (g->async) {   // the conditioners follow their mixtures
         g->cond.resize((size_t)nn, nullptr);
         std::vector<const sdmm_mix*> src;
@@ -344,12 +356,15 @@ int redistribute(sdmm_guiding* g, int old_nodes) {
         std::vector<sdmm_mix*> made(src.size(), nullptr);
         SDMM_TRY(sdmm_clone_many_on_stream(src.data(), (int)src.size(), (void*)g->st, made.data()));
         for (size_t i = 0; i < dst.size(); ++i) g->cond[(size_t)dst[i]] = made[i];
+        std::vector<sdmm_mix*> gone;
         for (int v = 0; v < old_nodes; ++v)
             if (was_split[(size_t)v] && g->cond[(size_t)v]) {
-                sdmm_destroy(g->cond[(size_t)v]);
+                gone.push_back(g->cond[(size_t)v]);
                 g->cond[(size_t)v] = nullptr;
             }
+        sdmm_detail::destroy_many(gone.data(), (int)gone.size());
     }
+    clk.lap("redis:destroy");
     // records and stats positions: relabelled on the device (order kept)
     uint8_t* dsplit = nullptr;
     int32_t* dparent = nullptr;
@@ -554,12 +569,19 @@ int sdmm_guiding_push(sdmm_guiding* g, const sdmm_path_vertices* v, uint64_t see
     if (!g || !v) return fail(SDMM_E_INVALID, "invalid argument");
     HIP_TRY(hipSetDevice(g->device));
     PhaseClock clk(g->st);
+    // the producer's count pass once (its offsets are reused by the write);
+    // the pools are sized before anything is read back, so a push costs two
+    // synchronisations: the record count and the stats count
     int64_t count = 0;
-    SDMM_TRY(sdmm_push_training(g->tree, v, g->cfg.saved_per_path, seed, nullptr, &count, nullptr, nullptr));
+    SDMM_TRY(sdmm_detail::push_training_ex(g->tree, v, g->cfg.saved_per_path, seed, nullptr, &count, nullptr, nullptr,
+                                           false, -1));
+    clk.lap("push:count");
     if (count == 0) return SDMM_OK;
     if (count > INT32_MAX) return fail(SDMM_E_INVALID, "sdmm_guiding_push: too many records");
     Pool& R = g->rec;
+    Pool& S = g->stat;
     SDMM_TRY(grow_pool(g, R, R.n + count));
+    SDMM_TRY(grow_pool(g, S, S.n + count));   // the stats entries are a subset of the records
     size_t tb = 0;
     (void)hipcub::DeviceSelect::Flagged(nullptr, tb, hipcub::CountingInputIterator<int32_t>(0),
                                         (const uint8_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, (int)count);
@@ -577,19 +599,19 @@ int sdmm_guiding_push(sdmm_guiding* g, const sdmm_path_vertices* v, uint64_t see
     o.node = R.nodes() + R.n;
     o.capacity = count;
     int64_t got = 0;
-    SDMM_TRY(sdmm_push_training(g->tree, v, g->cfg.saved_per_path, seed, &o, &got, nullptr, nullptr));
+    SDMM_TRY(sdmm_detail::push_training_ex(g->tree, v, g->cfg.saved_per_path, seed, &o, &got, nullptr, nullptr, true,
+                                           count));
+    clk.lap("push:write");
     // the stats entries in record order (leaf order, producer order inside)
     HIP_TRY(hipcub::DeviceSelect::Flagged(tmp + fb + sb + 256, tb, hipcub::CountingInputIterator<int32_t>(0), dstats,
                                           sel, dcount, (int)count, g->st));
-    int32_t ns = 0;
-    HIP_TRY(hipMemcpyAsync(&ns, dcount, sizeof(int32_t), hipMemcpyDeviceToHost, g->st));
-    HIP_TRY(hipStreamSynchronize(g->st));
-    Pool& S = g->stat;
-    SDMM_TRY(grow_pool(g, S, S.n + ns));
     hipLaunchKernelGGL(stats_append_kernel, grid_for(count), dim3(256), 0, g->st, sel, dcount, R.plane(0) + R.n, R.cap,
                        R.nodes() + R.n, S.plane(0) + S.n, S.cap, S.nodes() + S.n);
     HIP_TRY(hipGetLastError());
+    int32_t ns = 0;
+    HIP_TRY(hipMemcpyAsync(&ns, dcount, sizeof(int32_t), hipMemcpyDeviceToHost, g->st));
     HIP_TRY(hipFreeAsync(tmp, g->st));
+    HIP_TRY(hipStreamSynchronize(g->st));
     R.n += count;
     S.n += ns;
     clk.lap("push");

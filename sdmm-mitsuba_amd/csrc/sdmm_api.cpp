@@ -18,6 +18,7 @@
 #include <atomic>
 #include <future>
 #include <thread>
+#include <mutex>
 
 #include "../../include/sdmm_gpu.h"
 #include "sdmm_device.h"
@@ -153,6 +154,8 @@ int fail(int code, const std::string& msg) {
 // the error slot for the library's other host translation units (checkpoint.cpp)
 namespace sdmm_detail {
 int set_error(int code, const char* msg) { return fail(code, msg); }
+void destroy_impl(sdmm_mix* m, bool sync);
+void destroy_many(sdmm_mix* const* ms, int n);
 }  // namespace sdmm_detail
 
 namespace {
@@ -860,11 +863,16 @@ int create_many(int K, const sdmm_em_params* params, int device, hipStream_t st,
 
 extern "C" {
 
-void sdmm_destroy(sdmm_mix* m) {
+void sdmm_destroy(sdmm_mix* m) { sdmm_detail::destroy_impl(m, true); }
+
+}  // extern "C"
+
+// synced: the caller has synchronised the handle's streams (destroy_many)
+void sdmm_detail::destroy_impl(sdmm_mix* m, bool sync) {
     if (!m) return;
     (void)hipSetDevice(m->device);
-    if (m->own_stream) (void)hipStreamSynchronize(m->own_stream);
-    if (m->stream && m->stream != m->own_stream) (void)hipStreamSynchronize(m->stream);
+    if (sync && m->own_stream) (void)hipStreamSynchronize(m->own_stream);
+    if (sync && m->stream && m->stream != m->own_stream) (void)hipStreamSynchronize(m->stream);
     if (m->slab) {
         if (--m->slab->refs == 0) {
             // on the destroying handle's current stream (synchronised above):
@@ -890,6 +898,25 @@ void sdmm_destroy(sdmm_mix* m) {
     if (m->own_stream) (void)hipStreamDestroy(m->own_stream);
     delete m;
 }
+
+// many handles: each distinct stream synchronised once (a training pass
+// destroys the mixtures of every split leaf: ~1 us of synchronisation each)
+void sdmm_detail::destroy_many(sdmm_mix* const* ms, int n) {
+    std::vector<hipStream_t> seen;
+    for (int i = 0; i < n; ++i) {
+        const sdmm_mix* m = ms[i];
+        if (!m) continue;
+        for (hipStream_t st : {m->own_stream, m->stream})
+            if (st && std::find(seen.begin(), seen.end(), st) == seen.end()) {
+                (void)hipSetDevice(m->device);
+                (void)hipStreamSynchronize(st);
+                seen.push_back(st);
+            }
+    }
+    for (int i = 0; i < n; ++i) destroy_impl(ms[i], false);
+}
+
+extern "C" {
 
 int sdmm_create_many_on_stream(int K, const sdmm_em_params* params, int device, void* hip_stream, int n,
                                sdmm_mix** out) {
@@ -1150,22 +1177,53 @@ static int init_hemisphere_batched_impl(sdmm_mix* const* mixes, int n, const flo
     // per mixture: weights K, means 6K (f64), covs 25K (f64), bPriors 25K, bDepth 9K
     const size_t Kz = (size_t)K;
     const size_t per = 4 * Kz + 8 * 6 * Kz + 8 * 25 * Kz + 4 * 25 * Kz + 4 * 9 * Kz;
-    char* pin = nullptr;
-    HIP_TRY(hipHostMalloc((void**)&pin, (per * (size_t)n + 255) / 256 * 256 + sizeof(InitDescHost) * (size_t)n,
-                          hipHostMallocDefault));
-    std::vector<float> w(Kz), mean(6 * Kz), cov(25 * Kz);
+    // pinned staging: one grow-only buffer per device, held for the call (a
+    // fresh hipHostMalloc of ~10 MB per training pass pinned pages each time)
+    struct Staging {
+        std::mutex mu;
+        char* p = nullptr;
+        size_t cap = 0;
+    };
+    static Staging staging[64];
+    const int dev_i = mixes[0]->device;
+    if (dev_i < 0 || dev_i >= 64) return fail(SDMM_E_INVALID, "device index out of range");
+    Staging& sg = staging[dev_i];
+    std::lock_guard<std::mutex> hold(sg.mu);
+    const size_t want = (per * (size_t)n + 255) / 256 * 256 + sizeof(InitDescHost) * (size_t)n;
+    if (want > sg.cap) {
+        if (sg.p) HIP_TRY(hipHostFree(sg.p));
+        sg.p = nullptr;
+        sg.cap = 0;
+        const size_t cap = std::max<size_t>(want + want / 2, 1 << 20);
+        HIP_TRY(hipHostMalloc((void**)&sg.p, cap, hipHostMallocDefault));
+        sg.cap = cap;
+    }
+    char* pin = sg.p;
     int r = SDMM_OK;
-    for (int i = 0; i < n && !r; ++i) {
-        char* b = pin + per * (size_t)i;
-        float* pw = (float*)b;
-        double* pm = (double*)(b + 4 * Kz);
-        double* pc = (double*)(b + 4 * Kz + 48 * Kz);
-        float* pb = (float*)(b + 4 * Kz + 48 * Kz + 200 * Kz);
-        float* pd = (float*)(b + 4 * Kz + 48 * Kz + 200 * Kz + 100 * Kz);
-        hemisphere_init(positions + 3 * (size_t)npos * i, normals + 3 * (size_t)npos * i, npos, depth_prior,
-                        min_spatial_distance[i], seeds[i], pw, mean.data(), cov.data(), pb, pd, skip);
-        for (size_t j = 0; j < 6 * Kz; ++j) pm[j] = (double)mean[j];
-        for (size_t j = 0; j < 25 * Kz; ++j) pc[j] = (double)cov[j];
+    // the host fp64 initialisations, in parallel over the mixtures (each is
+    // independent and writes its own staging slice: bitwise as sequential)
+    auto init_range = [&](int i0, int i1) {
+        std::vector<float> mean(6 * Kz), cov(25 * Kz);
+        for (int i = i0; i < i1; ++i) {
+            char* b = pin + per * (size_t)i;
+            float* pw = (float*)b;
+            double* pm = (double*)(b + 4 * Kz);
+            double* pc = (double*)(b + 4 * Kz + 48 * Kz);
+            float* pb = (float*)(b + 4 * Kz + 48 * Kz + 200 * Kz);
+            float* pd = (float*)(b + 4 * Kz + 48 * Kz + 200 * Kz + 100 * Kz);
+            hemisphere_init(positions + 3 * (size_t)npos * i, normals + 3 * (size_t)npos * i, npos, depth_prior,
+                            min_spatial_distance[i], seeds[i], pw, mean.data(), cov.data(), pb, pd, skip);
+            for (size_t j = 0; j < 6 * Kz; ++j) pm[j] = (double)mean[j];
+            for (size_t j = 0; j < 25 * Kz; ++j) pc[j] = (double)cov[j];
+        }
+    };
+    {
+        const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+        const int nt = std::max(1, std::min({16, hw, n / 64}));
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back(init_range, (int)((int64_t)n * t / nt), (int)((int64_t)n * (t + 1) / nt));
+        init_range(0, (int)((int64_t)n / nt));
+        for (auto& x : th) x.join();
     }
     // one upload of the staging block + the per-mixture pointer table, one
     // kernel (a workgroup per mixture: copy in, MVTN::set, CDF, pack)
@@ -1183,8 +1241,7 @@ static int init_hemisphere_batched_impl(sdmm_mix* const* mixes, int n, const flo
         e0 = launch_set_all_batched(n, K, mixes[0]->Kp, (char*)dev + tab_off, dev, per, mixes[0]->norm5, st);
     if (dev) (void)hipFreeAsync(dev, st);
     if (!r && e0 != hipSuccess) r = fail(SDMM_E_HIP, std::string("init_hemisphere_batched: ") + hipGetErrorString(e0));
-    const hipError_t e = hipStreamSynchronize(st);   // the pinned staging is freed below
-    (void)hipHostFree(pin);
+    const hipError_t e = hipStreamSynchronize(st);   // the pinned staging is reused by the next call
     if (r) return r;
     if (e != hipSuccess) return fail(SDMM_E_HIP, std::string("init_hemisphere_batched: ") + hipGetErrorString(e));
     for (int i = 0; i < n; ++i) mixes[i]->initialised = true;
@@ -2989,8 +3046,34 @@ const int* tree_fallback_count(const sdmm_stree* t) { return t->guide_fb; }
 
 extern "C" {
 
+}  // extern "C"
+
+namespace sdmm_detail {
+// sdmm_push_training with reuse_counts: the call directly follows a count-only
+// call with the same tree, paths, saved_per_path and seed, so the per-path
+// record offsets still in the tree's scratch are reused (no second producer
+// count pass, no second synchronisation).  Without seg and lost nothing is read
+// back: the call returns with the writes in flight on the tree's stream.
+int push_training_ex(sdmm_stree* t, const sdmm_path_vertices* v, int saved_per_path, uint64_t seed,
+                     const sdmm_training_out* out, int64_t* n_out, int64_t* seg, int64_t* lost, bool reuse_counts,
+                     int64_t known_count);
+}  // namespace sdmm_detail
+
+extern "C" {
+
 int sdmm_push_training(sdmm_stree* t, const sdmm_path_vertices* v, int saved_per_path, uint64_t seed,
                        const sdmm_training_out* out, int64_t* n_out, int64_t* seg, int64_t* lost) {
+    int64_t hl = 0;
+    const int r = sdmm_detail::push_training_ex(t, v, saved_per_path, seed, out, n_out, seg, &hl, false, -1);
+    if (lost) *lost = hl;
+    return r;
+}
+
+}  // extern "C"
+
+int sdmm_detail::push_training_ex(sdmm_stree* t, const sdmm_path_vertices* v, int saved_per_path, uint64_t seed,
+                                  const sdmm_training_out* out, int64_t* n_out, int64_t* seg, int64_t* lost,
+                                  bool reuse_counts, int64_t known_count) {
     if (!t || !v || !n_out || saved_per_path < 1 || v->n_paths < 0 || v->max_vertices < 1 ||
         (v->n_paths > 0 && (!v->rec || !v->nv)))
         return fail(SDMM_E_INVALID, "invalid argument");
@@ -3030,11 +3113,14 @@ int sdmm_push_training(sdmm_stree* t, const sdmm_path_vertices* v, int saved_per
     int64_t* count = (int64_t*)b;
     int64_t* offs = (int64_t*)(b + cb);
     void* temp = b + 2 * cb;
-    HIP_TRY(hipMemsetAsync(count + P, 0, sizeof(int64_t), t->stream));
-    HIP_TRY(launch_produce_count(t->dnodes, PD, v->path0, saved_per_path, seed, count, offs, temp, tb, t->stream));
-    int64_t n_rec = 0;
-    HIP_TRY(hipMemcpyAsync(&n_rec, offs + P, sizeof(int64_t), hipMemcpyDeviceToHost, t->stream));
-    HIP_TRY(hipStreamSynchronize(t->stream));
+    int64_t n_rec = known_count;
+    if (!reuse_counts || known_count < 0) {
+        HIP_TRY(hipMemsetAsync(count + P, 0, sizeof(int64_t), t->stream));
+        HIP_TRY(launch_produce_count(t->dnodes, PD, v->path0, saved_per_path, seed, count, offs, temp, tb,
+                                     t->stream));
+        HIP_TRY(hipMemcpyAsync(&n_rec, offs + P, sizeof(int64_t), hipMemcpyDeviceToHost, t->stream));
+        HIP_TRY(hipStreamSynchronize(t->stream));
+    }
     *n_out = n_rec;
     if (!out) return SDMM_OK;   // count only
     if (n_rec > out->capacity) return fail(SDMM_E_INVALID, "push_training: output capacity too small");
@@ -3074,6 +3160,7 @@ int sdmm_push_training(sdmm_stree* t, const sdmm_path_vertices* v, int saved_per
     HIP_TRY(launch_produce_records(t->dnodes, nn, key_bits, PD, v->path0, saved_per_path, seed, offs, n_rec, k0, k1,
                                    q0, q1, temp, tb, sdev, dlost, ox, out->normal[0] ? on : nullptr, out->w,
                                    out->stats, out->node, out->source, t->stream));
+    if (!seg && !lost) return SDMM_OK;   // writes in flight on the tree's stream
     int hl = 0;
     if (seg) HIP_TRY(hipMemcpyAsync(seg, sdev, sizeof(int64_t) * (size_t)(nn + 1), hipMemcpyDeviceToHost, t->stream));
     HIP_TRY(hipMemcpyAsync(&hl, dlost, sizeof(int), hipMemcpyDeviceToHost, t->stream));
@@ -3081,5 +3168,3 @@ int sdmm_push_training(sdmm_stree* t, const sdmm_path_vertices* v, int saved_per
     if (lost) *lost = hl;
     return SDMM_OK;
 }
-
-}  // extern "C"
