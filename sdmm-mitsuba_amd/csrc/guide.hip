@@ -25,6 +25,7 @@
 // direction and the mixture pdf (tolerances 1e-5 / 1e-4) use the float
 // transcendentals.
 #include "sdmm_device.h"
+#include <cstdlib>
 
 #include <hipcub/hipcub.hpp>
 
@@ -2214,18 +2215,31 @@ __device__ __forceinline__ uint32_t spread3(uint32_t v) {   // 10 bits -> every 
     v = (v | (v << 2)) & 0x09249249u;
     return v;
 }
-__device__ __forceinline__ uint32_t quant10(float x) {
+// bits per axis (<= 10): the key has 3 * bits bits
+__device__ __forceinline__ uint32_t quantb(float x, int bits) {
     x = fminf(fmaxf(x, 0.0f), 1.0f);                          // NaN -> 0
-    const uint32_t q = (uint32_t)(x * 1024.0f);
-    return q > 1023u ? 1023u : q;
+    const uint32_t m = (1u << bits) - 1u;
+    const uint32_t q = (uint32_t)(x * (float)(1u << bits));
+    return q > m ? m : q;
 }
 __global__ void morton_keys_kernel(const float* __restrict__ c0, const float* __restrict__ c1,
-                                   const float* __restrict__ c2, int n, uint32_t* __restrict__ keys,
+                                   const float* __restrict__ c2, int n, int bits, uint32_t* __restrict__ keys,
                                    int32_t* __restrict__ idx) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= n) return;
-    keys[q] = spread3(quant10(c0[q])) | (spread3(quant10(c1[q])) << 1) | (spread3(quant10(c2[q])) << 2);
+    keys[q] = spread3(quantb(c0[q], bits)) | (spread3(quantb(c1[q], bits)) << 1) |
+              (spread3(quantb(c2[q], bits)) << 2);
     idx[q] = q;
+}
+
+// SDMM_MORTON_BITS (A/B): bits per axis of the coherent order's key
+static int morton_bits() {
+    static const int b = [] {
+        const char* e = std::getenv("SDMM_MORTON_BITS");
+        const int v = e ? std::atoi(e) : 10;
+        return v < 1 ? 1 : (v > 10 ? 10 : v);
+    }();
+    return b;
 }
 
 size_t guide_sort_temp_bytes(int n) {
@@ -2239,11 +2253,13 @@ size_t guide_sort_temp_bytes(int n) {
 static hipError_t coherent_order(const float* const c[3], int n, uint32_t* keys_in, uint32_t* keys_out,
                                  int32_t* idx_in, int32_t* idx_out, void* temp, size_t temp_bytes,
                                  hipStream_t st) {
+    const int bits = morton_bits();
     hipLaunchKernelGGL(morton_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, c[0], c[1], c[2], n,
-                       keys_in, idx_in);
+                       bits, keys_in, idx_in);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, idx_in, idx_out, n, 0, 30, st);
+    return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, idx_in, idx_out, n, 0, 3 * bits,
+                                              st);
 }
 
 static GuideIO make_io(const float* const c[3], const float* const u[3], const float* const dgiven[3],
