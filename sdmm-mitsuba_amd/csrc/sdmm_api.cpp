@@ -2933,13 +2933,23 @@ int st_prepare(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, int* 
     return SDMM_OK;
 }
 
+// SDMM_TREE_ORDER=0 (A/B): the tree wavefronts serve queries in the given
+// order (no Morton sort of the batch)
+bool tree_order_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("SDMM_TREE_ORDER");
+        return !(e && std::strcmp(e, "0") == 0);
+    }();
+    return on;
+}
+
 int st_guide(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
              const float* const u[3], const float* const dgiven[3], float* const d[3], float* pdf, int32_t* comp,
              int32_t* node_out, const uint8_t* pmode = nullptr) {
     int cus = 256;
     const int r = st_prepare(t, node_mix, nq, &cus);
     if (r) return r;
-    const GuideSortScratch* sort = nq >= (1 << 14) ? &t->guide_sort : nullptr;
+    const GuideSortScratch* sort = (nq >= (1 << 14) && tree_order_on()) ? &t->guide_sort : nullptr;
     HIP_TRY(launch_guide_tree(t->dnodes, t->dtab, t->tab_kmax, nq, c, u, dgiven, d, pdf, comp, node_out,
                               norm_const(2), norm_const(3), t->tab_cap, t->guide_fb, t->guide_fb + 1,
                               cus, t->stream, sort, pmode,
@@ -2956,7 +2966,7 @@ int st_guide_product(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq,
     int cus = 256;
     const int r = st_prepare(t, node_mix, nq, &cus);
     if (r) return r;
-    const GuideSortScratch* sort = nq >= (1 << 14) ? &t->guide_sort : nullptr;
+    const GuideSortScratch* sort = (nq >= (1 << 14) && tree_order_on()) ? &t->guide_sort : nullptr;
     HIP_TRY(launch_guide_product_tree(t->dnodes, t->dtab, t->dcctab, t->tab_kmax, nq, c, u, choice, dgiven, d, pdf,
                                       comp, node_out, material, frame, heuristic, bsdf->weights, bsdf->means,
                                       bsdf->covs, bsdf->diffuse, bsdf->B, bsdf->M, norm_const(2), norm_const(3),
