@@ -623,6 +623,12 @@ def main():
 
     if not args.no_extra and not args.no_large_k:
         out["large_k"] = large_k_bench(pkg, synth, batch, shard, dev, stream, timed, args, world, N_global, comm)
+        # configs[4] as a full guided render: K=512 leaves (the Kitchen's K) with
+        # sampleProduct, over the Cornell Box (the Kitchen meshes are LFS
+        # pointers; the device Li's BSDFs are diffuse, so the learned lobes are
+        # the diffuse slice rule's).  No CPU baseline: the CPU Li at K=512 x
+        # product runs minutes for a useful sample.
+        out["cornell_k512_product"] = cornell_bench(pkg, dev, args, world, K=512, product=True)
 
     if rank == 0 and world == 1 and not args.no_cpu:
         try:

@@ -291,17 +291,19 @@ def test_guided_render_unbiased_and_trained(pkg, oracle, scenes, gpu, plog):
     assert eg < 0.85 * eu
 
 
-def test_product_render_unbiased(pkg, oracle, scenes, gpu, plog):
+@pytest.mark.parametrize("K", [16, 512])
+def test_product_render_unbiased(pkg, oracle, scenes, gpu, plog, K):
     """sampleProduct in the device Li (sdmm_proc.cpp:327-392): guided bounces
     sample the product of the leaf's conditional with the diffuse material's
     learned lobe (h = 0.3, 0.5 without a usable product), the BSDF/guide choice
     against that h.  The image is unbiased against BSDF-only sampling, most
     guided bounces use the product, and the training producer on a product
-    render still equals the host-routed oracle bitwise."""
+    render still equals the host-routed oracle bitwise.  K = 512: the
+    Kitchen's K (configs[4]) over the same scene."""
     import torch
     sc = _scene(pkg, scenes, 160, 90)
     tree = _tree(pkg, sc)
-    node_mix = _train(pkg, sc, tree, 6, 8)
+    node_mix = _train(pkg, sc, tree, 6, 8, K=K)
     desc = scenes.cornell_box(160, 90)
     w, m, cov, dif = scenes.diffuse_learned_bsdf(len(desc["reflectance"]) // 3)
     table = pkg.BsdfTable(w, m, cov, device=gpu, diffuse=dif)
