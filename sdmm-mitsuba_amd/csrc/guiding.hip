@@ -34,6 +34,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <numeric>
 #include <vector>
 
 #include "../../include/sdmm_gpu.h"
@@ -126,6 +127,32 @@ __global__ void pool_relabel_kernel(int32_t* __restrict__ node, const int32_t* _
 }
 
 inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+
+// entries per leaf of a pool (dropped entries, node < 0, not counted): a
+// block-private LDS histogram when the node count fits, else global atomics
+constexpr int kCountBins = 16384;
+constexpr int kCountPer = 16;   // entries per thread
+__global__ void __launch_bounds__(256) pool_count_kernel(const int32_t* __restrict__ node, int64_t n, int nn,
+                                                         unsigned long long* __restrict__ counts) {
+    __shared__ unsigned h[kCountBins];
+    const bool lds = nn <= kCountBins;
+    if (lds)
+        for (int i = threadIdx.x; i < nn; i += 256) h[i] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * 256 * kCountPer;
+    for (int k = 0; k < kCountPer; ++k) {
+        const int64_t i = base + (int64_t)k * 256 + threadIdx.x;
+        if (i >= n) break;
+        const int v = node[i];
+        if (v < 0 || v >= nn) continue;
+        if (lds) atomicAdd(&h[v], 1u);
+        else atomicAdd(&counts[v], 1ull);
+    }
+    __syncthreads();
+    if (lds)
+        for (int i = threadIdx.x; i < nn; i += 256)
+            if (h[i]) atomicAdd(&counts[i], (unsigned long long)h[i]);
+}
 
 // out[(i * npos + j) * 6 + f]: point (f < 3) / normal (f >= 3) of record starts[i] + j
 __global__ void init_gather_kernel(const float* __restrict__ pool, int64_t cap, const int64_t* __restrict__ starts,
@@ -283,6 +310,33 @@ int order_pool(sdmm_guiding* g, Pool& P, const std::vector<uint8_t>& ready) {
     return SDMM_OK;
 }
 
+// entries per leaf of the record and stats pools (rc, sc: nn each) without
+// reordering them: the one stable sort by `ready` that follows gives every
+// leaf's entries the order a leaf sort before it would have kept
+int pool_counts(sdmm_guiding* g, const Pool& R, const Pool& S, int nn, std::vector<int64_t>& rc,
+                std::vector<int64_t>& sc) {
+    rc.assign((size_t)nn, 0);
+    sc.assign((size_t)nn, 0);
+    if (nn == 0) return SDMM_OK;
+    SDMM_TRY(grow_scratch(g, sizeof(int64_t) * 2 * (size_t)nn));
+    unsigned long long* d = (unsigned long long*)g->scratch;
+    HIP_TRY(hipMemsetAsync(d, 0, sizeof(int64_t) * 2 * (size_t)nn, g->st));
+    const Pool* P[2] = {&R, &S};
+    for (int q = 0; q < 2; ++q) {
+        if (P[q]->n == 0) continue;
+        const int64_t per = 256 * (int64_t)kCountPer;
+        hipLaunchKernelGGL(pool_count_kernel, dim3((unsigned)((P[q]->n + per - 1) / per)), dim3(256), 0, g->st,
+                           P[q]->nodes(), P[q]->n, nn, d + (size_t)q * nn);
+        HIP_TRY(hipGetLastError());
+    }
+    std::vector<int64_t> h(2 * (size_t)nn);
+    HIP_TRY(hipMemcpyAsync(h.data(), d, sizeof(int64_t) * h.size(), hipMemcpyDeviceToHost, g->st));
+    HIP_TRY(hipStreamSynchronize(g->st));
+    std::copy(h.begin(), h.begin() + nn, rc.begin());
+    std::copy(h.begin() + nn, h.end(), sc.begin());
+    return SDMM_OK;
+}
+
 // entries of split leaves: the leaf found in the new tree if it descends from
 // the split leaf, else dropped
 int relabel(sdmm_guiding* g, Pool& P, const uint8_t* dsplit, const int32_t* dparent) {
@@ -319,51 +373,44 @@ int redistribute(sdmm_guiding* g, int old_nodes) {
         origin[(size_t)c] = a;
     }
     g->mix.resize((size_t)nn, nullptr);
-    // mixtures: a copy of the split leaf's in each of its new leaves (one slab)
-    {
+    // mixtures: the split leaf's own handle moves to its first new leaf and
+    // the others get copies (one slab); a split leaf whose mixture has no new
+    // leaf to go to is destroyed.  Applied to the conditioners too (async).
+    auto hand_down = [&](std::vector<sdmm_mix*>& tab, bool on_model_stream) -> int {
+        tab.resize((size_t)nn, nullptr);
         std::vector<const sdmm_mix*> src;
         std::vector<int> dst;
+        std::vector<uint8_t> moved((size_t)old_nodes, 0);
         for (int c = old_nodes; c < nn; ++c) {
             const int v = origin[(size_t)c];
-            if (child[2 * (size_t)c] >= 0 || v < 0 || !g->mix[(size_t)v]) continue;
-            src.push_back(g->mix[(size_t)v]);
+            if (child[2 * (size_t)c] >= 0 || v < 0 || !tab[(size_t)v]) continue;
+            if (!moved[(size_t)v]) {
+                moved[(size_t)v] = 1;
+                tab[(size_t)c] = tab[(size_t)v];
+                continue;
+            }
+            src.push_back(tab[(size_t)v]);
             dst.push_back(c);
         }
         std::vector<sdmm_mix*> made(src.size(), nullptr);
-        SDMM_TRY(sdmm_clone_many(src.data(), (int)src.size(), made.data()));   // (on the model's stream)
-        for (size_t i = 0; i < dst.size(); ++i) g->mix[(size_t)dst[i]] = made[i];
-    }
+        if (on_model_stream) {
+            SDMM_TRY(sdmm_clone_many(src.data(), (int)src.size(), made.data()));
+        } else {
+            SDMM_TRY(sdmm_clone_many_on_stream(src.data(), (int)src.size(), (void*)g->st, made.data()));
+        }
+        for (size_t i = 0; i < dst.size(); ++i) tab[(size_t)dst[i]] = made[i];
+        std::vector<sdmm_mix*> gone;
+        for (int v = 0; v < old_nodes; ++v)
+            if (was_split[(size_t)v] && tab[(size_t)v]) {
+                if (!moved[(size_t)v]) gone.push_back(tab[(size_t)v]);
+                tab[(size_t)v] = nullptr;
+            }
+        sdmm_detail::destroy_many(gone.data(), (int)gone.size());
+        return SDMM_OK;
+    };
+    SDMM_TRY(hand_down(g->mix, true));
     clk.lap("redis:clone");
-    {
-        std::vector<sdmm_mix*> gone;
-        for (int v = 0; v < old_nodes; ++v)
-            if (was_split[(size_t)v] && g->mix[(size_t)v]) {
-                gone.push_back(g->mix[(size_t)v]);
-                g->mix[(size_t)v] = nullptr;
-            }
-        sdmm_detail::destroy_many(gone.data(), (int)gone.size());
-    }
-    if (g->async) {   // the conditioners follow their mixtures
-        g->cond.resize((size_t)nn, nullptr);
-        std::vector<const sdmm_mix*> src;
-        std::vector<int> dst;
-        for (int c = old_nodes; c < nn; ++c) {
-            const int v = origin[(size_t)c];
-            if (child[2 * (size_t)c] >= 0 || v < 0 || !g->cond[(size_t)v]) continue;
-            src.push_back(g->cond[(size_t)v]);
-            dst.push_back(c);
-        }
-        std::vector<sdmm_mix*> made(src.size(), nullptr);
-        SDMM_TRY(sdmm_clone_many_on_stream(src.data(), (int)src.size(), (void*)g->st, made.data()));
-        for (size_t i = 0; i < dst.size(); ++i) g->cond[(size_t)dst[i]] = made[i];
-        std::vector<sdmm_mix*> gone;
-        for (int v = 0; v < old_nodes; ++v)
-            if (was_split[(size_t)v] && g->cond[(size_t)v]) {
-                gone.push_back(g->cond[(size_t)v]);
-                g->cond[(size_t)v] = nullptr;
-            }
-        sdmm_detail::destroy_many(gone.data(), (int)gone.size());
-    }
+    if (g->async) SDMM_TRY(hand_down(g->cond, false));   // the conditioners follow their mixtures
     clk.lap("redis:destroy");
     // records and stats positions: relabelled on the device (order kept)
     uint8_t* dsplit = nullptr;
@@ -664,14 +711,15 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
     std::vector<float> aabb(6 * (size_t)nn);
     std::vector<int32_t> child(2 * (size_t)nn);
     SDMM_TRY(sdmm_stree_get_nodes(g->tree, aabb.data(), child.data(), nullptr));
-    // (2) records and stats per leaf (both pools ordered by leaf, nothing ready yet)
+    // (2) records and stats per leaf: counted in place (the pools are reordered
+    // once, by readiness, below; the stats pool at the next split)
     std::vector<uint8_t> ready((size_t)nn, 0);
-    SDMM_TRY(order_pool(g, R, ready));
-    SDMM_TRY(order_pool(g, S, ready));
+    std::vector<int64_t> rcount, scount;
+    SDMM_TRY(pool_counts(g, R, S, nn, rcount, scount));
     int n_ready = 0;
     for (int v = 0; v < nn; ++v) {
-        const int64_t n_data = R.seg[(size_t)(nn + v + 1)] - R.seg[(size_t)(nn + v)];
-        const int64_t n_stats = S.seg[(size_t)(nn + v + 1)] - S.seg[(size_t)(nn + v)];
+        const int64_t n_data = rcount[(size_t)v];
+        const int64_t n_stats = scount[(size_t)v];
         if ((g->total_spp > 12 || n_data > 1000) && child[2 * (size_t)v] < 0 && n_stats >= 64 && n_data >= 8) {
             ready[(size_t)v] = 1;
             ++n_ready;
@@ -682,7 +730,7 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
     if (out) {
         out->leaves = sdmm_stree_leaf_nodes(g->tree);
         out->optimized = n_ready;
-        out->records = R.n;
+        out->records = std::accumulate(rcount.begin(), rcount.end(), (int64_t)0);   // dropped ones not counted
     }
     ++g->iteration;
     if (n_ready == 0) return bind(g);
