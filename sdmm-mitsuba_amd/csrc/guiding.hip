@@ -232,7 +232,9 @@ int grow_pool(sdmm_guiding* g, Pool& P, int64_t need) {
     if (need <= P.cap) return SDMM_OK;
     // headroom for the next passes' records (every regrowth copies and
     // synchronises; HBM is plentiful)
-    int64_t cap = std::max<int64_t>(need + need / 2, P.cap * 2);
+    // (the first pass's pool takes 3x: the second pass adds as many records
+    // again beside the first pass's untrained ones)
+    int64_t cap = P.cap == 0 ? 3 * need : std::max<int64_t>(need + need / 2, P.cap * 2);
     cap = std::max<int64_t>(cap, 1 << 16);
     float* np[2] = {nullptr, nullptr};
     int32_t* nn[2] = {nullptr, nullptr};

@@ -369,10 +369,20 @@ li_film_kernel(PathsDev P, int64_t pix0, int64_t npix, int spp, int64_t plane, f
 // leaf (equal box min) retried while fewer than 8 draws failed.  Pass 0 counts
 // a path's records, pass 1 writes (leaf, code) at its offset; code =
 // ((path * V + d) << 1) | stats.  Records keep (path, push) order.
+// a record staged in path order (48 B, one or two cache lines) for the
+// leaf-order gather: point + wo, normal, average weight, code
+struct alignas(16) ProducedRec {
+    float x[6];
+    float n[3];
+    float w;
+    int64_t code;
+};
+static_assert(sizeof(ProducedRec) == 48, "ProducedRec layout");
+
 template <bool WRITE>
 __device__ __forceinline__ int produce_path(const STNodeDev* __restrict__ nodes, const PathsDev& P, int64_t p,
                                             int64_t path0, int saved, uint64_t seed, uint32_t* keys,
-                                            int64_t* codes, int64_t off, int* lost) {
+                                            int64_t* codes, ProducedRec* recs, int64_t off, int* lost) {
     const int nv = P.nv[p];
     const int first = nv - saved > 0 ? nv - saved : 0;
     int cnt = 0;
@@ -387,8 +397,24 @@ __device__ __forceinline__ int produce_path(const STNodeDev* __restrict__ nodes,
         const float avg = (vrec(P, 0, d, p) + vrec(P, 1, d, p) + vrec(P, 2, d, p)) * (1.0f / 3.0f);
         const bool ok = __builtin_isfinite(avg);
         const int64_t code = ((int64_t)p * P.V + d) << 1;
+        ProducedRec r{};
+        if (WRITE && ok) {
+            for (int a = 0; a < 3; ++a) {
+                r.x[a] = pos[a];
+                r.x[3 + a] = vrec(P, 10 + a, d, p);
+                r.n[a] = vrec(P, 13 + a, d, p);
+            }
+            r.w = avg;
+        }
+        auto put = [&](uint32_t key, int64_t c) {
+            const int64_t at = off + cnt;
+            keys[at] = key;
+            codes[at] = at;   // the sort's payload: the staged record's slot
+            r.code = c;
+            recs[at] = r;
+        };
         if (ok) {
-            if (WRITE) { keys[off + cnt] = (uint32_t)leaf; codes[off + cnt] = code | 1; }
+            if (WRITE) put((uint32_t)leaf, code | 1);
             ++cnt;
         }
         int jitters = (d >= nv - 1 ? 1 : 0) + (avg > 1000.0f ? 1 : 0);
@@ -412,7 +438,7 @@ __device__ __forceinline__ int produce_path(const STNodeDev* __restrict__ nodes,
                 continue;
             }
             if (ok) {
-                if (WRITE) { keys[off + cnt] = (uint32_t)nb; codes[off + cnt] = code; }
+                if (WRITE) put((uint32_t)nb, code);
                 ++cnt;
             }
         }
@@ -425,36 +451,34 @@ produce_count_kernel(const STNodeDev* __restrict__ nodes, PathsDev P, int64_t pa
                      int64_t* __restrict__ count) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P.P) return;
-    count[p] = produce_path<false>(nodes, P, p, path0, saved, seed, nullptr, nullptr, 0, nullptr);
+    count[p] = produce_path<false>(nodes, P, p, path0, saved, seed, nullptr, nullptr, nullptr, 0, nullptr);
 }
 
 __global__ void __launch_bounds__(256)
 produce_write_kernel(const STNodeDev* __restrict__ nodes, PathsDev P, int64_t path0, int saved, uint64_t seed,
                      const int64_t* __restrict__ offset, uint32_t* __restrict__ keys, int64_t* __restrict__ codes,
-                     int* __restrict__ lost) {
+                     ProducedRec* __restrict__ recs, int* __restrict__ lost) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P.P) return;
-    (void)produce_path<true>(nodes, P, p, path0, saved, seed, keys, codes, offset[p], lost);
+    (void)produce_path<true>(nodes, P, p, path0, saved, seed, keys, codes, recs, offset[p], lost);
 }
 
-// leaf-contiguous records -> training planes
+// leaf-contiguous records -> training planes (slot: the staged record of
+// sorted position j)
 __global__ void __launch_bounds__(256)
-produce_gather_kernel(PathsDev P, const int64_t* __restrict__ codes, int64_t n, float* x0, float* x1, float* x2,
-                      float* x3, float* x4, float* x5, float* n0, float* n1, float* n2, float* w,
-                      uint8_t* stats, const uint32_t* __restrict__ keys, int32_t* node, int64_t* source) {
+produce_gather_kernel(const ProducedRec* __restrict__ recs, const int64_t* __restrict__ slot, int64_t n, float* x0,
+                      float* x1, float* x2, float* x3, float* x4, float* x5, float* n0, float* n1, float* n2,
+                      float* w, uint8_t* stats, const uint32_t* __restrict__ keys, int32_t* node, int64_t* source) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
-    const int64_t code = codes[j];
-    const int64_t pv = code >> 1;
-    const int64_t p = pv / P.V;
-    const int d = (int)(pv % P.V);
-    x0[j] = vrec(P, 7, d, p); x1[j] = vrec(P, 8, d, p); x2[j] = vrec(P, 9, d, p);
-    x3[j] = vrec(P, 10, d, p); x4[j] = vrec(P, 11, d, p); x5[j] = vrec(P, 12, d, p);
-    if (n0) { n0[j] = vrec(P, 13, d, p); n1[j] = vrec(P, 14, d, p); n2[j] = vrec(P, 15, d, p); }
-    w[j] = (vrec(P, 0, d, p) + vrec(P, 1, d, p) + vrec(P, 2, d, p)) * (1.0f / 3.0f);
-    if (stats) stats[j] = (uint8_t)(code & 1);
+    const ProducedRec r = recs[slot[j]];
+    x0[j] = r.x[0]; x1[j] = r.x[1]; x2[j] = r.x[2];
+    x3[j] = r.x[3]; x4[j] = r.x[4]; x5[j] = r.x[5];
+    if (n0) { n0[j] = r.n[0]; n1[j] = r.n[1]; n2[j] = r.n[2]; }
+    w[j] = r.w;
+    if (stats) stats[j] = (uint8_t)(r.code & 1);
     if (node) node[j] = (int32_t)keys[j];
-    if (source) source[j] = pv;   // p * V + d
+    if (source) source[j] = r.code >> 1;   // p * V + d
 }
 
 // seg[v] = first sorted position with key >= v, v = 0..num_nodes
@@ -536,11 +560,12 @@ hipError_t launch_produce_count(const void* nodes, const PathsDev& P, int64_t pa
 
 hipError_t launch_produce_records(const void* nodes, int num_nodes, int key_bits, const PathsDev& P, int64_t path0,
                                   int saved, uint64_t seed, const int64_t* offsets, int64_t n_rec, uint32_t* keys0,
-                                  uint32_t* keys1, int64_t* codes0, int64_t* codes1, void* temp, size_t temp_bytes,
-                                  int64_t* seg_dev, int* lost, float* const x[6], float* const nrm[3], float* w,
-                                  uint8_t* stats, int32_t* node, int64_t* source, hipStream_t st) {
+                                  uint32_t* keys1, int64_t* codes0, int64_t* codes1, void* recs, void* temp,
+                                  size_t temp_bytes, int64_t* seg_dev, int* lost, float* const x[6],
+                                  float* const nrm[3], float* w, uint8_t* stats, int32_t* node, int64_t* source,
+                                  hipStream_t st) {
     hipLaunchKernelGGL(produce_write_kernel, grid_for(P.P), dim3(256), 0, st, (const STNodeDev*)nodes, P, path0,
-                       saved, seed, offsets, keys0, codes0, lost);
+                       saved, seed, offsets, keys0, codes0, (ProducedRec*)recs, lost);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || n_rec == 0) return e;
     // stable: a leaf's records stay in (path, push) order
@@ -551,7 +576,8 @@ hipError_t launch_produce_records(const void* nodes, int num_nodes, int key_bits
                        seg_dev);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(produce_gather_kernel, grid_for(n_rec), dim3(256), 0, st, P, codes1, n_rec, x[0], x[1], x[2],
+    hipLaunchKernelGGL(produce_gather_kernel, grid_for(n_rec), dim3(256), 0, st, (const ProducedRec*)recs, codes1,
+                       n_rec, x[0], x[1], x[2],
                        x[3], x[4], x[5], nrm ? nrm[0] : nullptr, nrm ? nrm[1] : nullptr, nrm ? nrm[2] : nullptr, w,
                        stats, keys1, node, source);
     return hipGetLastError();

@@ -132,9 +132,10 @@ hipError_t launch_produce_count(const void* nodes, const PathsDev& P, int64_t pa
                                 int64_t* count, int64_t* offsets, void* temp, size_t temp_bytes, hipStream_t st);
 hipError_t launch_produce_records(const void* nodes, int num_nodes, int key_bits, const PathsDev& P, int64_t path0,
                                   int saved, uint64_t seed, const int64_t* offsets, int64_t n_rec, uint32_t* keys0,
-                                  uint32_t* keys1, int64_t* codes0, int64_t* codes1, void* temp, size_t temp_bytes,
-                                  int64_t* seg_dev, int* lost, float* const x[6], float* const nrm[3], float* w,
-                                  uint8_t* stats, int32_t* node, int64_t* source, hipStream_t st);
+                                  uint32_t* keys1, int64_t* codes0, int64_t* codes1, void* recs, void* temp,
+                                  size_t temp_bytes, int64_t* seg_dev, int* lost, float* const x[6],
+                                  float* const nrm[3], float* w, uint8_t* stats, int32_t* node, int64_t* source,
+                                  hipStream_t st);
 size_t produce_temp_bytes(int64_t n_paths, int64_t n_records, int key_bits);
 }  // namespace sdmm
 
@@ -3142,7 +3143,8 @@ int sdmm_detail::push_training_ex(sdmm_stree* t, const sdmm_path_vertices* v, in
     const size_t kb = al(sizeof(uint32_t) * (size_t)std::max<int64_t>(n_rec, 1));
     const size_t qb = al(sizeof(int64_t) * (size_t)std::max<int64_t>(n_rec, 1));
     const size_t sb = al(sizeof(int64_t) * (size_t)(nn + 2));
-    const size_t need = 2 * cb + tb + 2 * kb + 2 * qb + sb + 256;
+    const size_t rb = al((size_t)48 * (size_t)std::max<int64_t>(n_rec, 1));   // staged records (render.hip)
+    const size_t need = 2 * cb + tb + 2 * kb + 2 * qb + sb + 256 + rb;
     if (need > t->scratch_bytes) {
         // keep the offsets: copy them out through a fresh buffer
         void* nb = nullptr;
@@ -3162,13 +3164,14 @@ int sdmm_detail::push_training_ex(sdmm_stree* t, const sdmm_path_vertices* v, in
     int64_t* q1 = (int64_t*)(b + 2 * cb + tb + 2 * kb + qb);
     int64_t* sdev = (int64_t*)(b + 2 * cb + tb + 2 * kb + 2 * qb);
     int* dlost = (int*)(b + 2 * cb + tb + 2 * kb + 2 * qb + sb);
+    void* recs = b + 2 * cb + tb + 2 * kb + 2 * qb + sb + 256;
     HIP_TRY(hipMemsetAsync(dlost, 0, sizeof(int), t->stream));
     if (n_rec == 0) HIP_TRY(hipMemsetAsync(sdev, 0, sizeof(int64_t) * (size_t)(nn + 1), t->stream));
     float* ox[6];
     for (int i = 0; i < 6; ++i) ox[i] = out->x[i];
     float* on[3] = {out->normal[0], out->normal[1], out->normal[2]};
     HIP_TRY(launch_produce_records(t->dnodes, nn, key_bits, PD, v->path0, saved_per_path, seed, offs, n_rec, k0, k1,
-                                   q0, q1, temp, tb, sdev, dlost, ox, out->normal[0] ? on : nullptr, out->w,
+                                   q0, q1, recs, temp, tb, sdev, dlost, ox, out->normal[0] ? on : nullptr, out->w,
                                    out->stats, out->node, out->source, t->stream));
     if (!seg && !lost) return SDMM_OK;   // writes in flight on the tree's stream
     int hl = 0;
