@@ -274,6 +274,17 @@ size_t al(size_t b) { return (b + 255) / 256 * 256; }
 
 // Stable reorder of a pool by key (ready leaves first, then the other
 // leaves, dropped entries last); P.seg over keys 0 .. 2 * num_nodes.
+// order_pool's scratch for n entries over nn nodes
+size_t order_scratch_bytes(int64_t n, int nn, int bits) {
+    size_t tb = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                             (const int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, bits);
+    const size_t kb = al(sizeof(uint32_t) * (size_t)n);
+    const size_t sb = al(sizeof(int64_t) * (size_t)(2 * nn + 1));
+    const size_t rb = al((size_t)std::max(nn, 1));
+    return 4 * kb + sb + rb + al(tb);
+}
+
 int order_pool(sdmm_guiding* g, Pool& P, const std::vector<uint8_t>& ready) {
     const int nn = sdmm_stree_num_nodes(g->tree);
     const int nk = 2 * nn;
@@ -631,6 +642,14 @@ int sdmm_guiding_push(sdmm_guiding* g, const sdmm_path_vertices* v, uint64_t see
     Pool& S = g->stat;
     SDMM_TRY(grow_pool(g, R, R.n + count));
     SDMM_TRY(grow_pool(g, S, S.n + count));   // the stats entries are a subset of the records
+    {
+        // the reorders' scratch sized with the pools (a regrowth inside
+        // optimize() would free and synchronise there): the record pool's
+        // capacity over the node count the leaf cap allows (x2 for the split's
+        // overshoot), 17-bit keys
+        const int nn_cap = std::max(sdmm_stree_num_nodes(g->tree), 4 * g->cfg.max_leaf_nodes + 64);
+        SDMM_TRY(grow_scratch(g, order_scratch_bytes(R.cap, nn_cap, 17)));
+    }
     size_t tb = 0;
     (void)hipcub::DeviceSelect::Flagged(nullptr, tb, hipcub::CountingInputIterator<int32_t>(0),
                                         (const uint8_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, (int)count);
@@ -738,6 +757,7 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
     if (n_ready == 0) return bind(g);
     // (3) the ready leaves' records as one prefix, in leaf order
     SDMM_TRY(order_pool(g, R, ready));
+    clk.lap("init:order");
     std::vector<sdmm_mix*> mixes;
     std::vector<int64_t> bseg{0};
     const int K = g->cfg.K, npos = K / 8;
@@ -768,6 +788,7 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
         HIP_TRY(hipFreeAsync(dstart, g->st));
         HIP_TRY(hipFreeAsync(dinit, g->st));
         HIP_TRY(hipStreamSynchronize(g->st));
+        clk.lap("init:gather");
         std::vector<float> pos(3 * (size_t)npos * (size_t)nf), nrm(3 * (size_t)npos * (size_t)nf), dist((size_t)nf);
         std::vector<uint64_t> seeds((size_t)nf);
         std::vector<sdmm_mix*> made((size_t)nf, nullptr);
@@ -775,6 +796,7 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
         sdmm_em_params_default(&ep);
         int r = sdmm_create_many_on_stream(K, &ep, g->device, (void*)(g->async ? g->em_st : g->st), nf, made.data());
         if (r) return r;
+        clk.lap("init:create");
         for (int i = 0; i < nf; ++i) {
             const int v = fresh[(size_t)i];
             for (int j = 0; j < npos; ++j)
@@ -799,6 +821,7 @@ int sdmm_guiding_optimize(sdmm_guiding* g, int spp, sdmm_guiding_stats* out) {
             return r;
         }
         for (int i = 0; i < nf; ++i) g->mix[(size_t)fresh[(size_t)i]] = made[(size_t)i];
+        clk.lap("init:hemi");
     }
     for (int v = 0; v < nn; ++v) {
         if (!ready[(size_t)v]) continue;
