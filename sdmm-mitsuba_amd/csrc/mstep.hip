@@ -601,9 +601,10 @@ __global__ void init_state_kernel(int K, InitScalars a, float eps, double* __res
     for (int i = 0; i < 9; ++i) bd[9 * k + i] = (i % 4 == 0) ? eps : 0.0f;
 }
 
-// Batched initialisation: mixture b takes its weights (K f32), means (6K f64),
-// covs (25K f64), bPriors (25K f32), bDepth (9K f32) from a device staging
-// block and runs set_all (MVTN::set per component, CDF, packing).
+// Batched initialisation: mixture b takes its weights (K f32), means (6K f32),
+// covs (25K f32), bPriors (25K f32), bDepth (9K f32) from a device staging
+// block and runs set_all (MVTN::set per component on the fp64-widened mean
+// and covariance, CDF, packing).
 struct InitDesc {
     CanonDev C;
     float *ep, *gp, *bp, *bd;
@@ -615,16 +616,21 @@ set_all_batched_kernel(int K, int Kp, const InitDesc* __restrict__ tab, const ch
     const InitDesc d = tab[blockIdx.x];
     const char* b = staging + per * (size_t)blockIdx.x;
     const float* w = (const float*)b;
-    const double* mean = (const double*)(b + 4 * (size_t)K);
-    const double* cov = (const double*)(b + 52 * (size_t)K);
-    const float* bp = (const float*)(b + 252 * (size_t)K);
-    const float* bd = (const float*)(b + 352 * (size_t)K);
+    const float* mean = (const float*)(b + 4 * (size_t)K);
+    const float* cov = (const float*)(b + 28 * (size_t)K);
+    const float* bp = (const float*)(b + 128 * (size_t)K);
+    const float* bd = (const float*)(b + 228 * (size_t)K);
     const int t = threadIdx.x;
     for (int i = t; i < K; i += blockDim.x) d.C.weights[i] = w[i];
     for (int i = t; i < 25 * K; i += blockDim.x) d.bp[i] = bp[i];
     for (int i = t; i < 9 * K; i += blockDim.x) d.bd[i] = bd[i];
     __syncthreads();
-    for (int k = t; k < K; k += blockDim.x) set_component(k, mean + 6 * k, cov + 25 * k, d.C);
+    for (int k = t; k < K; k += blockDim.x) {
+        double m[6], c[25];
+        for (int i = 0; i < 6; ++i) m[i] = (double)mean[6 * k + i];
+        for (int i = 0; i < 25; ++i) c[i] = (double)cov[25 * k + i];
+        set_component(k, m, c, d.C);
+    }
     __syncthreads();
     if (t == 0) weights_cdf(d.C.weights, d.C.cdf, K, false);
     __syncthreads();

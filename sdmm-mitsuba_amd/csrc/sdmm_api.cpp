@@ -124,6 +124,8 @@ hipError_t launch_split_flags(const float* x, const float* y, const float* z, co
 hipError_t launch_split_scatter(const float* x, const float* y, const float* z, const int32_t* item, int64_t n,
                                 const void* cand, const int32_t* flags, const int64_t* rank, float* ox, float* oy,
                                 float* oz, int32_t* oitem, hipStream_t st);
+hipError_t launch_split_decide(const void* items, int n_items, const double* partial, int threshold, void* cand,
+                               void* dec, hipStream_t st);
 size_t split_scan_temp_bytes(int64_t n);
 int split_chunk_samples();
 hipError_t launch_sample_cdf(const float* cdf, int n, const float* u, int64_t nq, int32_t* out,
@@ -1175,9 +1177,11 @@ static int init_hemisphere_batched_impl(sdmm_mix* const* mixes, int n, const flo
     const hipStream_t st = mixes[0]->stream;
     for (int i = 1; i < n; ++i)
         if (mixes[i]->stream != st) HIP_TRY(hipStreamSynchronize(mixes[i]->stream));
-    // per mixture: weights K, means 6K (f64), covs 25K (f64), bPriors 25K, bDepth 9K
+    // per mixture: weights K, means 6K, covs 25K, bPriors 25K, bDepth 9K, all
+    // f32 (the initial means and covariances are float values: the kernel
+    // widens them to the fp64 MVTN::set takes)
     const size_t Kz = (size_t)K;
-    const size_t per = 4 * Kz + 8 * 6 * Kz + 8 * 25 * Kz + 4 * 25 * Kz + 4 * 9 * Kz;
+    const size_t per = 4 * Kz + 4 * 6 * Kz + 4 * 25 * Kz + 4 * 25 * Kz + 4 * 9 * Kz;
     // pinned staging: one grow-only buffer per device, held for the call (a
     // fresh hipHostMalloc of ~10 MB per training pass pinned pages each time)
     struct Staging {
@@ -1204,18 +1208,15 @@ static int init_hemisphere_batched_impl(sdmm_mix* const* mixes, int n, const flo
     // the host fp64 initialisations, in parallel over the mixtures (each is
     // independent and writes its own staging slice: bitwise as sequential)
     auto init_range = [&](int i0, int i1) {
-        std::vector<float> mean(6 * Kz), cov(25 * Kz);
         for (int i = i0; i < i1; ++i) {
             char* b = pin + per * (size_t)i;
             float* pw = (float*)b;
-            double* pm = (double*)(b + 4 * Kz);
-            double* pc = (double*)(b + 4 * Kz + 48 * Kz);
-            float* pb = (float*)(b + 4 * Kz + 48 * Kz + 200 * Kz);
-            float* pd = (float*)(b + 4 * Kz + 48 * Kz + 200 * Kz + 100 * Kz);
+            float* pm = (float*)(b + 4 * Kz);
+            float* pc = (float*)(b + 28 * Kz);
+            float* pb = (float*)(b + 128 * Kz);
+            float* pd = (float*)(b + 228 * Kz);
             hemisphere_init(positions + 3 * (size_t)npos * i, normals + 3 * (size_t)npos * i, npos, depth_prior,
-                            min_spatial_distance[i], seeds[i], pw, mean.data(), cov.data(), pb, pd, skip);
-            for (size_t j = 0; j < 6 * Kz; ++j) pm[j] = (double)mean[j];
-            for (size_t j = 0; j < 25 * Kz; ++j) pc[j] = (double)cov[j];
+                            min_spatial_distance[i], seeds[i], pw, pm, pc, pb, pd, skip);
         }
     };
     {
@@ -2541,42 +2542,54 @@ int st_split_device(sdmm_stree* t, const std::vector<int>& leaves, const float* 
     while (!items.empty()) {
         const int ni = (int)items.size();
         const int64_t lvl_n = items.back().start + items.back().n;
-        // (1) fp64 sums of the items above the threshold, by chunks
+        // (1) fp64 sums of the items above the threshold, by chunks; (2) the
+        // decisions (split_decide) and the children's counts, on the device:
+        // one round trip per level
         std::vector<SplitChunkDev> chunks;
-        std::vector<int> chunk_item;
+        std::vector<SplitItemDev> idesc((size_t)ni);
         for (int i = 0; i < ni; ++i) {
-            if (items[(size_t)i].n <= threshold) continue;
-            for (int64_t c0 = 0; c0 < items[(size_t)i].n; c0 += C) {
+            const Item& it = items[(size_t)i];
+            const STNodeHost& nd = L[(size_t)it.leaf][(size_t)it.local];
+            SplitItemDev& d = idesc[(size_t)i];
+            for (int a = 0; a < 3; ++a) { d.mn[a] = nd.mn[a]; d.mx[a] = nd.mx[a]; }
+            d.start = it.start;
+            d.n = it.n;
+            d.c0 = d.c1 = (int32_t)chunks.size();
+            if (it.n <= threshold) continue;
+            for (int64_t c0 = 0; c0 < it.n; c0 += C) {
                 SplitChunkDev c{};
-                c.start = items[(size_t)i].start + c0;
-                c.len = (int32_t)std::min<int64_t>(C, items[(size_t)i].n - c0);
+                c.start = it.start + c0;
+                c.len = (int32_t)std::min<int64_t>(C, it.n - c0);
                 chunks.push_back(c);
-                chunk_item.push_back(i);
             }
+            d.c1 = (int32_t)chunks.size();
         }
         if (chunks.empty()) break;
         const size_t nch = chunks.size();
         r = split_small(t, al(sizeof(SplitChunkDev) * nch) + al(sizeof(double) * 6 * nch) +
-                               al(sizeof(SplitCandDev) * (size_t)ni) + al(sizeof(long long) * 2 * (size_t)ni));
+                               al(sizeof(SplitCandDev) * (size_t)ni) + al(sizeof(long long) * 2 * (size_t)ni) +
+                               al(sizeof(SplitItemDev) * (size_t)ni) + al(sizeof(SplitDecisionDev) * (size_t)ni));
         if (r) return r;
         char* sb = (char*)t->split_small;
         SplitChunkDev* dch = (SplitChunkDev*)sb; sb += al(sizeof(SplitChunkDev) * nch);
         double* dpart = (double*)sb; sb += al(sizeof(double) * 6 * nch);
         SplitCandDev* dcand = (SplitCandDev*)sb; sb += al(sizeof(SplitCandDev) * (size_t)ni);
-        long long* dcnt = (long long*)sb;
+        long long* dcnt = (long long*)sb; sb += al(sizeof(long long) * 2 * (size_t)ni);
+        SplitItemDev* ditem = (SplitItemDev*)sb; sb += al(sizeof(SplitItemDev) * (size_t)ni);
+        SplitDecisionDev* ddec = (SplitDecisionDev*)sb;
         const DevSplitBuf I = S.buf[cur];
         HIP_TRY(hipMemcpyAsync(dch, chunks.data(), sizeof(SplitChunkDev) * nch, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(ditem, idesc.data(), sizeof(SplitItemDev) * (size_t)ni, hipMemcpyHostToDevice, st));
         HIP_TRY(launch_split_sums(I.x, I.y, I.z, dch, (int)nch, dpart, st));
-        std::vector<double> part(6 * nch);
-        HIP_TRY(hipMemcpyAsync(part.data(), dpart, sizeof(double) * 6 * nch, hipMemcpyDeviceToHost, st));
+        HIP_TRY(launch_split_decide(ditem, ni, dpart, threshold, dcand, ddec, st));
+        HIP_TRY(launch_split_flags(I.x, I.y, I.z, I.item, lvl_n, dcand, ni, S.flags, S.rank, S.temp, S.temp_bytes,
+                                   dcnt, st));
+        std::vector<long long> cnt(2 * (size_t)ni);
+        std::vector<SplitDecisionDev> dec((size_t)ni);
+        HIP_TRY(hipMemcpyAsync(cnt.data(), dcnt, sizeof(long long) * 2 * (size_t)ni, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(dec.data(), ddec, sizeof(SplitDecisionDev) * (size_t)ni, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
-        std::vector<double> sums(6 * (size_t)ni, 0.0);
-        for (size_t c = 0; c < nch; ++c)
-            for (int k = 0; k < 6; ++k) {
-                double& a = sums[6 * (size_t)chunk_item[c] + (size_t)k];
-                a = a + part[6 * c + (size_t)k];
-            }
-        // (2) the candidate splits (split_decide), their children's counts
+        // the candidates as the device formed them (st_child of its decision)
         std::vector<SplitCandDev> cand((size_t)ni);
         std::vector<int> axes((size_t)ni, 0);
         std::vector<STNodeHost> kids(2 * (size_t)ni);
@@ -2587,29 +2600,19 @@ int st_split_device(sdmm_stree* t, const std::vector<int>& leaves, const float* 
             const Item& it = items[(size_t)i];
             c.start = it.start;
             c.n = it.n;
-            if (it.n <= threshold) continue;
-            const STNodeHost& nd = L[(size_t)it.leaf][(size_t)it.local];
-            int ax = 0;
-            float split = 0.0f;
-            if (!split_decide(nd, &sums[6 * (size_t)i], it.n, ax, split)) continue;
-            STNodeHost parent = nd;
-            parent.axis = ax;
-            for (int k = 0; k < 2; ++k) kids[2 * (size_t)i + (size_t)k] = st_child(parent, k, split);
+            if (!dec[(size_t)i].active) continue;
+            STNodeHost parent = L[(size_t)it.leaf][(size_t)it.local];
+            parent.axis = dec[(size_t)i].axis;
+            for (int k = 0; k < 2; ++k) kids[2 * (size_t)i + (size_t)k] = st_child(parent, k, dec[(size_t)i].split);
             for (int a = 0; a < 3; ++a) {
                 c.mn0[a] = kids[2 * (size_t)i].mn[a]; c.mx0[a] = kids[2 * (size_t)i].mx[a];
                 c.mn1[a] = kids[2 * (size_t)i + 1].mn[a]; c.mx1[a] = kids[2 * (size_t)i + 1].mx[a];
             }
             c.active = 1;
-            axes[(size_t)i] = ax;
+            axes[(size_t)i] = dec[(size_t)i].axis;
             ++n_active;
         }
         if (n_active == 0) break;
-        HIP_TRY(hipMemcpyAsync(dcand, cand.data(), sizeof(SplitCandDev) * (size_t)ni, hipMemcpyHostToDevice, st));
-        HIP_TRY(launch_split_flags(I.x, I.y, I.z, I.item, lvl_n, dcand, ni, S.flags, S.rank, S.temp, S.temp_bytes,
-                                   dcnt, st));
-        std::vector<long long> cnt(2 * (size_t)ni);
-        HIP_TRY(hipMemcpyAsync(cnt.data(), dcnt, sizeof(long long) * 2 * (size_t)ni, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
         // (3) accept the splits that separate their samples (st_split_local)
         std::vector<Item> next;
         int64_t ntotal = 0;

@@ -171,6 +171,20 @@ struct SplitCandDev {
     int64_t out[2];          // the children's first index in the next level buffer
 };
 
+// per item of a split level, for the decision on the device: the node's box,
+// its range in the level buffer and its chunks [c0, c1) of the level's sums
+struct SplitItemDev {
+    float mn[3], mx[3];
+    int64_t start, n;
+    int32_t c0, c1;
+};
+// the decision per item (active 0: at most threshold samples, or degenerate)
+struct SplitDecisionDev {
+    int32_t active, axis;
+    float split;
+    int32_t pad;
+};
+
 struct STNodeDev {
     float mn[3], mx[3];
     int c0, c1;

@@ -150,6 +150,60 @@ split_sums_kernel(const float* __restrict__ x, const float* __restrict__ y, cons
 
 
 
+// split_decide (the library's host split, sdmm_api.cpp) per item on the
+// device: the chunk partials folded in chunk order from 0, the mean along the
+// axis of largest variance (the first of equals), the children's boxes as
+// st_child forms them.  IEEE fp64 / fp32 division, no contraction: bitwise
+// the host's decision.
+__global__ void __launch_bounds__(256)
+split_decide_kernel(const SplitItemDev* __restrict__ items, int n_items, const double* __restrict__ partial,
+                    int threshold, SplitCandDev* __restrict__ cand, SplitDecisionDev* __restrict__ dec) {
+#pragma clang fp contract(off)
+    const int it = blockIdx.x * blockDim.x + threadIdx.x;
+    if (it >= n_items) return;
+    const SplitItemDev I = items[it];
+    SplitCandDev c;
+    for (int a = 0; a < 3; ++a) c.mn0[a] = c.mx0[a] = c.mn1[a] = c.mx1[a] = 0.0f;
+    c.active = 0;
+    c.child_item[0] = c.child_item[1] = 0;
+    c.pad = 0;
+    c.start = I.start;
+    c.n = I.n;
+    c.out[0] = c.out[1] = 0;
+    SplitDecisionDev d{0, 0, 0.0f, 0};
+    if (I.n > threshold) {
+        double s[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        for (int ch = I.c0; ch < I.c1; ++ch)
+            for (int k = 0; k < 6; ++k) s[k] = s[k] + partial[6 * (int64_t)ch + k];
+        float m[3], var[3];
+        for (int a = 0; a < 3; ++a) {
+            const double mu = s[a] / (double)I.n;
+            m[a] = (float)mu;
+            const double sq = mu * mu;
+            var[a] = (float)(s[3 + a] / (double)I.n - sq);
+        }
+        int ax = 0;
+        for (int a = 0; a < 3; ++a)
+            if (var[a] > var[ax]) ax = a;
+        const float split = (m[ax] - I.mn[ax]) / (I.mx[ax] - I.mn[ax]);
+        if (split > 0.0f && split < 1.0f) {
+            for (int a = 0; a < 3; ++a) {
+                c.mn0[a] = c.mn1[a] = I.mn[a];
+                c.mx0[a] = c.mx1[a] = I.mx[a];
+            }
+            const float diag = I.mx[ax] - I.mn[ax];
+            const float d0 = split * diag;
+            c.mn0[ax] = I.mn[ax] + d0;
+            const float d1 = (1.0f - split) * diag;
+            c.mx1[ax] = I.mx[ax] - d1;
+            c.active = 1;
+            d = SplitDecisionDev{1, ax, split, 0};
+        }
+    }
+    cand[it] = c;
+    dec[it] = d;
+}
+
 __device__ __forceinline__ bool split_in(const float* mn, const float* mx, float a, float b, float c) {
     return mn[0] <= a && a <= mx[0] && mn[1] <= b && b <= mx[1] && mn[2] <= c && c <= mx[2];
 }
@@ -268,6 +322,14 @@ hipError_t launch_split_flags(const float* x, const float* y, const float* z, co
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(split_counts_kernel, split_grid(n_items), dim3(256), 0, st, (const SplitCandDev*)cand,
                        n_items, rank, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_split_decide(const void* items, int n_items, const double* partial, int threshold, void* cand,
+                               void* dec, hipStream_t st) {
+    if (n_items <= 0) return hipSuccess;
+    hipLaunchKernelGGL(split_decide_kernel, split_grid(n_items), dim3(256), 0, st, (const SplitItemDev*)items,
+                       n_items, partial, threshold, (SplitCandDev*)cand, (SplitDecisionDev*)dec);
     return hipGetLastError();
 }
 
