@@ -553,6 +553,16 @@ typedef struct {
     float fov_x_deg;
     float near_clip;
     int width, height;
+    /* nullable (every BSDF diffuse): 8 floats per BSDF -- [0] kind (0
+     * diffuse, 1 smooth plastic: bsdfs/plastic.cpp, its diffuseReflectance in
+     * `reflectance`), [1..3] specularReflectance, [4] eta = intIOR / extIOR,
+     * [5] 1 / eta^2, [6] fdrInt (the internal diffuse Fresnel reflectance,
+     * fresnelDiffuseReflectance(1 / eta)), [7] the specular sampling weight
+     * sAvg / (dAvg + sAvg) (plastic.cpp:188-196).  A plastic bounce queries
+     * the guide like any BSDF with a smooth lobe; a delta lobe chosen by the
+     * BSDF sample returns weight / h with pdf * h and saves no vertex
+     * (sdmm_proc.cpp:297, :383-409, :764). */
+    const float* bsdf_params;
 } sdmm_scene_desc;
 typedef struct {
     int spp;
@@ -589,7 +599,7 @@ typedef struct {
 } sdmm_path_vertices;
 typedef struct {
     int64_t paths;           /* paths started (pixels x spp) */
-    int64_t segments;        /* bounce rays traced after the camera rays (= saved vertices) */
+    int64_t segments;        /* bounce rays traced after the camera rays (a delta lobe's saves no vertex) */
     int64_t guided_queries;  /* live bounces that queried the guide (compacted wavefront sizes summed) */
     int64_t fallback_queries;   /* of those, served by the full-K path (the candidate list overflowed) */
 } sdmm_li_stats;

@@ -500,7 +500,9 @@ def li_render(desc: dict, aabb, child, node_mix=None, guided=False, spp=1, max_d
     f = lib().or_li_render
     f.restype = C.c_int
     vp = lambda a: a.ctypes.data_as(C.c_void_p)
-    rc = f(vp(quads), vp(flip), vp(bsdf), C.c_int(len(bsdf)), vp(refl), vp(em), vp(rad), vp(cam),
+    bpar = f32(desc["bsdf_params"]) if "bsdf_params" in desc else None
+    rc = f(vp(quads), vp(flip), vp(bsdf), C.c_int(len(bsdf)), vp(refl), vp(bpar) if bpar is not None else None,
+           vp(em), vp(rad), vp(cam),
            C.c_float(desc["fov_x_deg"]), C.c_float(desc["near_clip"]), C.c_int(W), C.c_int(H), vp(mn), vp(mx),
            vp(ch), tab, C.c_int(int(guided)), C.c_int(spp), C.c_int(max_depth), C.c_int(rr_depth), C.c_float(h),
            C.c_int(V), C.c_uint64(seed), C.c_int64(lo), C.c_int64(hi), C.c_int(1 if learned is not None else 0),

@@ -21,12 +21,19 @@
  *     per-pass iteration%05i.exr dumps, stats.json, the final checkpoint;
  *   - the film: each pass added with weight spp / sampleCount
  *     (SDMMProcess::develop, sdmm_proc.cpp:1142-1158);
- *   - Li (sdmm_proc.cpp:592-871): no NEE, BSDF / guide mixing with
- *     heuristicConditionalWeight 0.5 (:383-392), pdf = h bsdfPdf + (1-h)
- *     gmmPdf (:587-589), saved vertices with clamped pdf only for non-delta
- *     samples (`cacheable`, :764, :821-846) with the normal flipped to the
- *     wi side (:765-767), recordRadiance (:615-637), Russian roulette after
- *     rrDepth with q = min(max(throughput) eta^2, 0.95) (:788, :858-868);
+ *   - Li (sdmm_proc.cpp:592-871): no NEE; the guide is queried for every
+ *     BSDF that is not all-delta (:297) and the BSDF/guide choice is taken
+ *     first with heuristicConditionalWeight 0.5 (:383-392); a BSDF-chosen
+ *     delta lobe returns weight / h with pdf * h (:401-405), a smooth one
+ *     (weight * pdf) / pdfSurface, the guide's direction eval / pdfSurface
+ *     with pdf = h bsdfPdf + (1-h) gmmPdf (:587-589); saved vertices with
+ *     clamped pdf only for non-delta samples (`cacheable`, :764, :821-846)
+ *     with the normal flipped to the wi side (:765-767); recordRadiance
+ *     (:615-637); strict normals on wi and wo (:688-691, :777-780); medium
+ *     transitions, index-matched (ENull) passes and
+ *     rayIntersectAndLookForEmitter's transmittance through null surfaces
+ *     (:788-800, :988-1050); Russian roulette after rrDepth with q =
+ *     min(max(throughput) eta^2, 0.95) (:788, :858-868);
  *   - sampleProduct (:327-392): the BSDF's learned DMM (getDMM, :327-329;
  *     the diffuse case re-centres slice 0 on the wi-side normal, :335-339,
  *     otherwise rotate_to_wo(wi), :341-354 -- sdmm-lib calls the maintainer's
@@ -180,8 +187,10 @@ struct PathState {
     Spectrum bsdfWeight;
     Float bsdfPdf;
     bool pdfMode;        // the BSDF was chosen (rnd <= h; with sampleProduct the wavefront decides, comp -2)
-    bool cacheable;      // !(bRec.sampledType & EDelta): the vertex is saved (:764)
     Float eta;           // relative IOR along the path (:604, :788)
+    const Medium* medium;   // rRec.medium (:788-790)
+    bool emission;       // rRec.type still has EEmittedRadiance (camera ray, or index-matched passes before a scatter)
+    bool scattered;      // (:645, :870)
 };
 
 }  // namespace
@@ -411,32 +420,62 @@ private:
             s.depth = -1;
             s.query = -1;
             s.eta = 1.0f;
+            s.medium = sensor->getMedium();
+            s.emission = true;
+            s.scattered = false;
             if (scene->rayIntersect(s.ray, s.its)) {
                 if (s.its.isEmitter()) s.Li += s.throughput * s.its.Le(-s.ray.d);
                 s.depth = 1;
-            } else {
-                s.Li += s.throughput * scene->evalEnvironment(s.ray);
+            } else {                               // (:653-665): attenuated by the camera's medium
+                Spectrum v = s.throughput * scene->evalEnvironment(s.ray);
+                if (s.medium) v *= s.medium->evalTransmittance(s.ray, sampler);
+                s.Li += v;
             }
             sampler->advance();
         }
         std::vector<std::unique_ptr<BSDFSamplingRecord>> brecs((size_t)n);
         for (int bounce = 0;; ++bounce) {
-            // loop head: depth cap, the BSDF sample, the guide query (:684-421)
+            // loop head (:649-691): emission / environment after index-matched
+            // passes, the depth cap, strict normals on wi; then sampleSurface's
+            // first half (:275-392): the guide is queried for every BSDF that is
+            // not all-delta (:297); the BSDF sample is drawn up front (its
+            // direction is the pdf query's when the BSDF is chosen, and it is
+            // the whole answer when the leaf has no valid conditional)
             int64_t nq = 0, live = 0;
             for (int64_t p = 0; p < n; ++p) {
                 PathState& s = P[(size_t)p];
                 s.query = -1;
                 if (s.depth < 0) continue;
+                if (!s.its.isValid()) {                // (:653-665), only reached after an index-matched pass
+                    if (s.emission) {
+                        Spectrum v = s.throughput * scene->evalEnvironment(s.ray);
+                        if (s.medium) v *= s.medium->evalTransmittance(s.ray, sampler);
+                        s.Li += v;
+                        recordRadiance(st, p, n, nv[(size_t)p], v);
+                    }
+                    s.depth = -1;
+                    continue;
+                }
+                if (bounce > 0 && s.emission && s.its.isEmitter()) {   // (:668-672)
+                    const Spectrum v = s.throughput * s.its.Le(-s.ray.d);
+                    s.Li += v;
+                    recordRadiance(st, p, n, nv[(size_t)p], v);
+                }
                 if (m_maxDepth >= 0 && s.depth >= m_maxDepth) { s.depth = -1; continue; }
+                const Float wiDotGeoN = -dot(s.its.geoFrame.n, s.ray.d), wiDotShN = Frame::cosTheta(s.its.wi);
+                if (wiDotGeoN * wiDotShN < 0 && m_strictNormals) { s.depth = -1; continue; }   // (:688-691)
                 const BSDF* bsdf = s.its.getBSDF(s.ray);
                 brecs[(size_t)p].reset(new BSDFSamplingRecord(s.its, sampler, ERadiance));
                 BSDFSamplingRecord& bRec = *brecs[(size_t)p];
-                s.bsdfWeight = bsdf->sample(bRec, s.bsdfPdf, sampler->next2D());
-                s.cacheable = !(bRec.sampledType & BSDF::EDelta);
-                const bool smooth = (bsdf->getType() & BSDF::ESmooth) && s.cacheable;
+                const unsigned type = bsdf->getType();
+                const bool allDelta = (type & BSDF::EDelta) == (type & BSDF::EAll);
                 ++live;
-                if (!guided || !smooth) continue;
-                const Float choice = sampler->next1D();
+                if (!guided || allDelta) {              // (:297-302, :316-323)
+                    s.bsdfWeight = bsdf->sample(bRec, s.bsdfPdf, sampler->next2D());
+                    continue;
+                }
+                const Float choice = sampler->next1D();    // rRec.nextSample1D() (:383)
+                s.bsdfWeight = bsdf->sample(bRec, s.bsdfPdf, sampler->next2D());
                 s.pdfMode = choice <= hWeight;
                 const Vector dB = s.its.toWorld(bRec.wo);
                 const int64_t q = nq++;
@@ -454,60 +493,87 @@ private:
             if (live == 0) break;
             if (nq > 0) guideWavefront(st, n, nq);
             const bool productBounce = nq > 0 && st.h_mat != nullptr;
-            // shade (:392-507, :759-871)
+            // sampleSurface's second half (:392-507) and the loop body (:759-871)
             for (int64_t p = 0; p < n; ++p) {
                 PathState& s = P[(size_t)p];
                 if (s.depth < 0) continue;
                 const BSDF* bsdf = s.its.getBSDF(s.ray);
                 BSDFSamplingRecord& bRec = *brecs[(size_t)p];
                 const int32_t comp = s.query >= 0 ? st.h_comp[s.query] : -1;
-                Spectrum weight;
-                Float pdf;
-                if (comp == -1) {                      // BSDF only, h = 1 (:316-323)
+                Spectrum weight(0.0f);
+                Float pdf = 0;
+                if (comp == -1) {
+                    // BSDF only, h = 1 (:298-302, :316-323, :392-405)
                     weight = s.bsdfWeight;
                     pdf = s.bsdfPdf;
                 } else {
                     const Float gmmPdf = st.h_out[3 * n + s.query];
                     // h: 0.5, or the product query's own 0.3 / 0.5 (:383-392)
                     const Float hq = productBounce ? (Float)st.h_pf[10 * n + s.query] : hWeight;
-                    s.pdfMode = comp == -2;            // the BSDF sample was chosen (:392)
-                    if (!s.pdfMode) {                  // the guide's direction
+                    if (comp == -2) {
+                        // the BSDF sample was chosen (:392-407)
+                        if (!s.bsdfWeight.isZero()) {
+                            if (bRec.sampledType & BSDF::EDelta) {
+                                // a delta lobe: gmmPdf = 0, pdf *= h, weight / h (:401-405)
+                                pdf = s.bsdfPdf * hq;
+                                weight = s.bsdfWeight / hq;
+                            } else {
+                                const Float bsdfPdf = bsdf->pdf(bRec);   // pdfSurface (:510-534, :587-589)
+                                pdf = (bsdfPdf > 0 && std::isfinite(bsdfPdf)) ? hq * bsdfPdf + (1 - hq) * gmmPdf : 0;
+                                if (pdf != 0) weight = (s.bsdfWeight * s.bsdfPdf) / pdf;
+                            }
+                        }
+                    } else {
+                        // the guide's direction: a fresh record's lobe state
+                        // (nothing was sampled, :410-463) and bsdf->eval / pdfSurface
+                        bRec.sampledType = 0;
+                        bRec.sampledComponent = -1;
+                        bRec.eta = 1.0f;
                         const Vector d(st.h_out[0 * n + s.query], st.h_out[1 * n + s.query],
                                        st.h_out[2 * n + s.query]);
-                        bRec.wo = s.its.toLocal(d);
+                        if (!d.isZero()) {
+                            bRec.wo = s.its.toLocal(d);
+                            const Float bsdfPdf = bsdf->pdf(bRec);
+                            pdf = (bsdfPdf > 0 && std::isfinite(bsdfPdf)) ? hq * bsdfPdf + (1 - hq) * gmmPdf : 0;
+                            if (pdf != 0) weight = bsdf->eval(bRec) / pdf;
+                        }
                     }
-                    const Float bsdfPdf = bsdf->pdf(bRec);
-                    pdf = bsdfPdf > 0 ? hq * bsdfPdf + (1 - hq) * gmmPdf : 0;   // (:587-589)
-                    weight = pdf > 0 ? bsdf->eval(bRec) / pdf : Spectrum(0.0f);
                 }
+                const bool cacheable = !(bRec.sampledType & BSDF::EDelta);   // (:764)
+                if (weight.isZero() || !weight.isValid()) { s.depth = -1; continue; }   // (:759-774)
                 const Vector wo = s.its.toWorld(bRec.wo);
                 const Float woDotGeoN = dot(s.its.geoFrame.n, wo);
-                if (weight.isZero() || (m_strictNormals && woDotGeoN * Frame::cosTheta(bRec.wo) <= 0)) {
-                    s.depth = -1;                      // (:772-780)
-                    continue;
-                }
-                s.throughput *= weight;
-                s.eta *= bRec.eta;                     // (:788)
-                // trace and look for an emitter (no NEE: MIS weight 1, :803-819)
-                const Point o = s.its.p;
+                if (woDotGeoN * Frame::cosTheta(bRec.wo) <= 0 && m_strictNormals) { s.depth = -1; continue; }
                 // the vertex normal on the wi side (:650-651, :765-767)
                 const Normal n_s = Frame::cosTheta(bRec.wi) < 0 ? Normal(-s.its.shFrame.n) : s.its.shFrame.n;
+                const Point o = s.its.p;
                 const Point cnd((o - m_sceneMin) / m_spatialNorm);
                 s.ray = RayDifferential(o, wo, s.ray.time);
-                Spectrum value(0.0f);
-                const bool hit = scene->rayIntersect(s.ray, s.its);
-                if (hit) {
-                    if (s.its.isEmitter()) value = s.its.Le(-s.ray.d);
-                } else {
-                    value = scene->evalEnvironment(s.ray);
+                s.throughput *= weight;
+                s.eta *= bRec.eta;                     // (:788)
+                if (s.its.isMediumTransition()) s.medium = s.its.getTargetMedium(s.ray.d);   // (:789-790)
+                if (bRec.sampledType == BSDF::ENull) {
+                    // an index-matched medium transition (:792-800): continue
+                    // through it, no vertex, no roulette; emission is seen
+                    // again only if the path has not scattered yet
+                    s.emission = !s.scattered;
+                    scene->rayIntersect(s.ray, s.its);
+                    ++s.depth;
+                    continue;
                 }
+                // trace and look for an emitter through index-matched surfaces
+                // (rayIntersectAndLookForEmitter, :803, :988-1050); no NEE: MIS
+                // weight 1 (:811-816)
+                Spectrum value(0.0f);
+                const int maxInteractions = m_maxDepth >= 0 ? m_maxDepth - s.depth - 1 : -1;
+                const bool hit = lookForEmitter(scene, sampler, s.medium, maxInteractions, s.ray, s.its, value);
                 int& k = nv[(size_t)p];
                 if (!value.isZero()) {
                     const Spectrum rad = s.throughput * value;
                     s.Li += rad;
                     recordRadiance(st, p, n, k, rad);
                 }
-                if (s.cacheable && k < V) {             // the saved vertex: non-delta samples only (:764, :821-846)
+                if (cacheable && k < V) {             // the saved vertex (:821-846)
                     const Float clamped = std::max(pdf, (Float)0.1f);
                     Float rgb[3], thr[3];
                     value.toLinearRGB(rgb[0], rgb[1], rgb[2]);
@@ -525,13 +591,15 @@ private:
                     st.rec(15, k, p, n) = (float)n_s.z;
                     ++k;
                 }
-                if (!hit) { s.depth = -1; continue; }
+                s.emission = false;                    // rRec.type = ERadianceNoEmission (:850)
+                if (!hit) { s.depth = -1; continue; }   // the next loop head would end it (:653-665)
                 if (s.depth >= m_rrDepth) {             // Russian roulette (:858-868)
                     const Float qq = std::min(s.throughput.max() * s.eta * s.eta, (Float)0.95f);
                     if (sampler->next1D() >= qq) { s.depth = -1; continue; }
                     s.throughput /= qq;
                 }
                 ++s.depth;
+                s.scattered = true;
             }
         }
         // the pixels' pass mean and mean of squares (box filter, sample order)
@@ -563,6 +631,47 @@ private:
             sdmm_path_vertices v{n, V, path0, st.d_rec, st.d_nv};
             check_sdmm(sdmm_guiding_push(m_guiding, &v, 0x5D33u + (uint64_t)iteration), "sdmm_guiding_push");
         }
+    }
+
+    // rayIntersectAndLookForEmitter (sdmm_proc.cpp:988-1050): intersect, and
+    // through a chain of index-matched (ENull) surfaces keep tracing while
+    // accumulating the medium transmittance and the null BSDFs' discrete
+    // eval, until an occluder, a light source or maxInteractions; value gets
+    // the attenuated emission of an emitter (or the environment on a miss).
+    // _its receives the FIRST surface hit (the path continues from there).
+    // Returns whether a surface was hit.
+    static bool lookForEmitter(const Scene* scene, Sampler* sampler, const Medium* medium, int maxInteractions,
+                               Ray ray, Intersection& _its, Spectrum& value) {
+        Intersection its2, *its = &_its;
+        Spectrum transmittance(1.0f);
+        bool surface = false, first = true, firstHit = false;
+        int interactions = 0;
+        while (true) {
+            surface = scene->rayIntersect(ray, *its);
+            if (first) { firstHit = surface; first = false; }
+            if (medium) transmittance *= medium->evalTransmittance(Ray(ray, 0, its->t), sampler);
+            if (surface && (interactions == maxInteractions || !(its->getBSDF()->getType() & BSDF::ENull) ||
+                            its->isEmitter()))
+                break;                              // an occluder or a light source
+            if (!surface) break;
+            if (transmittance.isZero()) return firstHit;
+            if (its->isMediumTransition()) medium = its->getTargetMedium(ray.d);
+            const Vector wo = its->shFrame.toLocal(ray.d);
+            BSDFSamplingRecord bRec(*its, -wo, wo, ERadiance);
+            bRec.typeMask = BSDF::ENull;
+            transmittance *= its->getBSDF()->eval(bRec, EDiscrete);
+            ray.o = ray(its->t);
+            ray.mint = Epsilon;
+            its = &its2;
+            if (++interactions > 100) return firstHit;   // round-off guard (:1035-1038)
+        }
+        if (surface) {
+            if (its->isEmitter()) value = transmittance * its->Le(-ray.d);
+        } else {
+            const Emitter* env = scene->getEnvironmentEmitter();
+            if (env) value = transmittance * env->evalEnvironment(RayDifferential(ray));
+        }
+        return firstHit;
     }
 
     // recordRadiance (:628-637): every saved vertex of the path gets the

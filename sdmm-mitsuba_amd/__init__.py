@@ -1162,7 +1162,8 @@ class _SceneDesc(C.Structure):
     _fields_ = [("n_quads", C.c_int), ("quads", C.c_void_p), ("flip_normals", C.c_void_p), ("bsdf", C.c_void_p),
                 ("n_bsdfs", C.c_int), ("reflectance", C.c_void_p), ("emitter", C.c_void_p),
                 ("n_emitters", C.c_int), ("radiance", C.c_void_p), ("camera_to_world", C.c_float * 16),
-                ("fov_x_deg", C.c_float), ("near_clip", C.c_float), ("width", C.c_int), ("height", C.c_int)]
+                ("fov_x_deg", C.c_float), ("near_clip", C.c_float), ("width", C.c_int), ("height", C.c_int),
+                ("bsdf_params", C.c_void_p)]
 
 
 class _LiParams(C.Structure):
@@ -1228,6 +1229,9 @@ class Scene:
         d.fov_x_deg = float(desc["fov_x_deg"])
         d.near_clip = float(desc.get("near_clip", 1e-2))
         d.width, d.height = int(desc["width"]), int(desc["height"])
+        if "bsdf_params" in self._keep:
+            self._keep["bsdf_params"] = np.ascontiguousarray(self._keep["bsdf_params"], np.float32)
+            d.bsdf_params = self._keep["bsdf_params"].ctypes.data
         self.width, self.height, self.device = d.width, d.height, device
         h = C.c_void_p()
         _check(lib().sdmm_scene_create(C.byref(d), int(device), C.byref(h)))

@@ -130,6 +130,9 @@ __device__ __forceinline__ int lrow(int m) { return EP_L00 + m * (m + 1) / 2; }
 // MFMA accumulation error scales with them; a single scene-centre origin left
 // the heuristic row sums at 1.2e-5 of the fp64 evaluation instead of 4e-6).
 #ifdef SDMM_SPLIT_BLOCKORIGIN
+#ifdef SDMM_SPLIT_PIPE
+#error "SDMM_SPLIT_PIPE uses the one scene-centre origin"
+#endif
 constexpr bool kBlockOrigin = true;
 #else
 constexpr bool kBlockOrigin = false;
@@ -342,11 +345,11 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
         Feat f;
         f.p = __builtin_nontemporal_load(s.x[gf] + i);
         f.d = __builtin_nontemporal_load(s.x[3 + gf] + i);
-        // optional planes: always load (from a valid plane when absent), select after
-        const float* hpp = has_h ? s.hpdf : s.x[0];
-        const uint8_t* dpp = has_d ? s.isDiffuse : (const uint8_t*)s.x[0];
-        f.hp = __builtin_nontemporal_load(hpp + i);
-        f.dw = *(const __attribute__((address_space(1))) int*)((uintptr_t)(dpp + i) & ~(uintptr_t)3);
+        // optional planes: loaded only when present (a wave-uniform branch)
+        f.hp = 0.0f;
+        f.dw = 0;
+        if (has_h) f.hp = __builtin_nontemporal_load(s.hpdf + i);
+        if (has_d) f.dw = *(const __attribute__((address_space(1))) int*)((uintptr_t)(s.isDiffuse + i) & ~(uintptr_t)3);
         return f;
     };
     // the three coordinates of sample col from lane groups 0..2
@@ -469,6 +472,46 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
             pdf[r][3] = p[1].y;
             acc = padd(acc, padd(p[0], p[1]));
         };
+#if defined(SDMM_SPLIT_DIAG_STOREONLY)
+        // diagnostic ceiling (tools/build_variant.sh): the same loads, row
+        // staging and stores with no matrix or pair math; the rows are not
+        // responsibilities
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                pdf[r][j] = P3[j & 1] + D3[j >> 1] + (float)(16 * r + j);
+                acc.x += pdf[r][j];
+            }
+#elif defined(SDMM_SPLIT_PIPE)
+        {
+            // software-pipelined over the blocks: block r + 1's eight MFMAs are
+            // issued before block r's pair math and interleaved with it
+            // (sched_group_barrier), block r + 2's fragments are read from LDS
+            // meanwhile; the matrix pipe works while the VALU does
+            bf8 F[R][8];
+            f4 dp[R], D[R][8];
+            frags(0, F[0], dp[0]);
+            forms(F[0], Bs0, Bd, D[0]);
+            if (R > 1) frags(1, F[1], dp[1]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (r + 1 < R) forms(F[r + 1], Bs0, Bd, D[r + 1]);
+                if (r + 2 < R) frags(r + 2, F[r + 2], dp[r + 2]);
+                pair_math(r, Tag<false>{}, D[r], dp[r]);
+                if (r + 1 < R) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);              // one MFMA
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);              // one LDS read
+                        __builtin_amdgcn_sched_group_barrier(0x002, SDMM_SPLIT_PIPE, 0);  // VALU
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#else
         {
             // pipelined over the blocks: block r + 1's fragments are read from
             // LDS while block r's pair math runs
@@ -489,6 +532,7 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
+#endif
         // rare angle case anywhere in the tile (c < -0.9999995; its bits,
         // unsigned, exceed those of -0.9999995f) or a NaN: redo the tile with
         // the reference's quirks (wave-uniform, a few tiles per launch)

@@ -20,8 +20,10 @@
 // film kernel averages each pixel's samples in sample order (box filter).
 //
 // Scene: parallelograms (Mitsuba rectangles; a cube is six), diffuse BSDFs
-// (diffuse.cpp: cosine-hemisphere sampling, f = rho / pi), one-sided area
-// emitters (area.cpp: Le = radiance on the normal side).  No NEE (the plugin's
+// (diffuse.cpp: cosine-hemisphere sampling, f = rho / pi) and smooth plastic
+// (plastic.cpp: a delta specular lobe with the dielectric Fresnel reflectance
+// over a diffuse base, the lobe chosen by Fresnel-weighted probability), one-
+// sided area emitters (area.cpp: Le = radiance on the normal side).  No NEE (the plugin's
 // NEE block is compiled out, :700-734; emitterPdf = 0, MIS weight 1, :811-816).
 //
 // Random numbers: counter-based (rng_uniform below), one fixed slot per
@@ -104,6 +106,24 @@ __device__ __forceinline__ void cosine_hemisphere(float u0, float u1, float w[3]
     w[2] = z;
 }
 
+// fresnelDielectricExt (libcore/util.cpp:651-681): the unpolarised
+// reflectance at cos(theta_i) for the relative index eta
+__device__ __forceinline__ float fresnel_dielectric(float cos_i, float eta) {
+    if (eta == 1.0f) return 0.0f;
+    const float scale = cos_i > 0.0f ? 1.0f / eta : eta;
+    const float ct2 = 1.0f - (1.0f - cos_i * cos_i) * (scale * scale);
+    if (ct2 <= 0.0f) return 1.0f;
+    const float ci = fabsf(cos_i), ct = sqrtf(ct2);
+    const float rs = (ci - eta * ct) / (ci + eta * ct);
+    const float rp = (eta * ci - ct) / (eta * ci + ct);
+    return 0.5f * (rs * rs + rp * rp);
+}
+
+// SmoothPlastic's specular sampling probability (plastic.cpp:339-342)
+__device__ __forceinline__ float plastic_prob_specular(float Fi, float ssw) {
+    return (Fi * ssw) / (Fi * ssw + (1.0f - Fi) * (1.0f - ssw));
+}
+
 __device__ __forceinline__ float& vrec(const PathsDev& P, int f, int v, int64_t p) {
     return P.rec[((int64_t)f * P.V + v) * P.P + p];
 }
@@ -146,6 +166,7 @@ li_camera_kernel(SceneDev S, PathsDev P, int64_t path0, int spp, uint64_t seed) 
     const int q = intersect(S, o, d, S.near_clip / l[2], INFINITY, t);
     P.tr[i] = 1.0f; P.tg[i] = 1.0f; P.tb[i] = 1.0f;
     P.nv[i] = 0;
+    P.nray[i] = 0;
     P.dx[i] = d[0]; P.dy[i] = d[1]; P.dz[i] = d[2];
     float L[3] = {0.0f, 0.0f, 0.0f};
     if (q >= 0) {
@@ -178,9 +199,11 @@ li_query_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, i
         n[0] = QD.n[0]; n[1] = QD.n[1]; n[2] = QD.n[2];
         wi[0] = -P.dx[i]; wi[1] = -P.dy[i]; wi[2] = -P.dz[i];
         const float* rho = S.refl + 3 * QD.bsdf;
-        // diffuse: no reflection from the back side or with rho = 0 (the
+        const float* bp = S.bpar ? S.bpar + kBsdfParams * QD.bsdf : nullptr;
+        const bool zero_spec = !bp || bp[0] != (float)kBsdfPlastic || (bp[1] == 0.0f && bp[2] == 0.0f && bp[3] == 0.0f);
+        // no reflection from the back side or with zero reflectances (the
         // light's BSDF): sample and eval are 0, the path ends (:772-774)
-        if (!(dot3(wi, n) > 0.0f) || (rho[0] == 0.0f && rho[1] == 0.0f && rho[2] == 0.0f)) live = false;
+        if (!(dot3(wi, n) > 0.0f) || (rho[0] == 0.0f && rho[1] == 0.0f && rho[2] == 0.0f && zero_spec)) live = false;
     }
     Q.live[i] = (uint8_t)((live && guided) ? 1 : 0);
     Q.slot[i] = -1;
@@ -196,7 +219,40 @@ li_query_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, i
     Q.c2[i] = (p[2] - S.smin[2]) / S.snorm;
     float s[3], t[3], w[3];
     frame_of(n, s, t);
-    cosine_hemisphere(rng_uniform(seed, gp, stream, 0), rng_uniform(seed, gp, stream, 1), w);
+    const float* bp = S.bpar ? S.bpar + kBsdfParams * S.quads[q].bsdf : nullptr;
+    uint8_t delta = 0;
+    if (bp && bp[0] == (float)kBsdfPlastic) {
+        // SmoothPlastic::sample(bRec, pdf, sample) (plastic.cpp:378-420): the
+        // delta mirror lobe with probability probSpecular, else the cosine
+        // hemisphere on the rescaled first coordinate; weight and pdf for the
+        // shade kernel (a mixture bounce keeps the sampled lobe, :392-407)
+        const float* rho = S.refl + 3 * S.quads[q].bsdf;
+        const float wl[3] = {dot3(wi, s), dot3(wi, t), dot3(wi, n)};   // Frame::toLocal
+        const float Fi = fresnel_dielectric(wl[2], bp[4]);
+        const float ps = plastic_prob_specular(Fi, bp[7]);
+        const float u0 = rng_uniform(seed, gp, stream, 0), u1 = rng_uniform(seed, gp, stream, 1);
+        if (u0 < ps) {
+            delta = 1;
+            w[0] = -wl[0]; w[1] = -wl[1]; w[2] = wl[2];
+            // Spectrum * Fi / probSpecular (TSpectrum::operator/: times the reciprocal)
+            const float rs = 1.0f / ps;
+            Q.bw0[i] = bp[1] * Fi * rs; Q.bw1[i] = bp[2] * Fi * rs; Q.bw2[i] = bp[3] * Fi * rs;
+            Q.bpdf[i] = ps;
+        } else {
+            cosine_hemisphere((u0 - ps) / (1.0f - ps), u1, w);
+            const float Fo = fresnel_dielectric(w[2], bp[4]);
+            // diff /= 1 - fdrInt; diff * (invEta2 (1 - Fi) (1 - Fo) / (1 - probSpecular))
+            const float rd = 1.0f / (1.0f - bp[6]);
+            const float k = bp[5] * (1.0f - Fi) * (1.0f - Fo) / (1.0f - ps);
+            Q.bw0[i] = rho[0] * rd * k;
+            Q.bw1[i] = rho[1] * rd * k;
+            Q.bw2[i] = rho[2] * rd * k;
+            Q.bpdf[i] = (1.0f - ps) * (kInvPi * w[2]);
+        }
+    } else {
+        cosine_hemisphere(rng_uniform(seed, gp, stream, 0), rng_uniform(seed, gp, stream, 1), w);
+    }
+    Q.bdelta[i] = delta;
     Q.b0[i] = s[0] * w[0] + t[0] * w[1] + n[0] * w[2];
     Q.b1[i] = s[1] * w[0] + t[1] * w[1] + n[1] * w[2];
     Q.b2[i] = s[2] * w[0] + t[2] * w[1] + n[2] * w[2];
@@ -260,7 +316,53 @@ li_shade_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, i
     const bool valid = comp != -1;      // validConditional (:368)
     if (product && valid) h = Q.hq[j];
     float wo[3], weight[3], mis_pdf;
-    if (!valid) {
+    const float* bp = S.bpar ? S.bpar + kBsdfParams * QD.bsdf : nullptr;
+    bool cacheable = true;
+    if (bp && bp[0] == (float)kBsdfPlastic) {
+        // smooth plastic (plastic.cpp): the loop head's sample (weight, pdf,
+        // lobe) or the guide's direction under eval / pdf, the smooth part only
+        const float wi[3] = {-P.dx[i], -P.dy[i], -P.dz[i]};
+        const float Fi = fresnel_dielectric(dot3(wi, n), bp[4]);
+        const float ps = plastic_prob_specular(Fi, bp[7]);
+        const bool delta = Q.bdelta[i] != 0;
+        const float bw[3] = {Q.bw0[i], Q.bw1[i], Q.bw2[i]};
+        if (!valid || comp == -2) {
+            wo[0] = Q.b0[i]; wo[1] = Q.b1[i]; wo[2] = Q.b2[i];
+            cacheable = !delta;                 // :764
+            if (!valid) {
+                // BSDF only, h = 1 (:316-323, :392-405)
+                mis_pdf = Q.bpdf[i];
+                for (int ch = 0; ch < 3; ++ch) weight[ch] = bw[ch];
+            } else if (delta) {
+                // a delta lobe of the chosen BSDF sample: gmmPdf = 0, pdf *= h,
+                // weight / h (:401-405)
+                mis_pdf = Q.bpdf[i] * h;
+                const float rh = 1.0f / h;
+                for (int ch = 0; ch < 3; ++ch) weight[ch] = bw[ch] * rh;
+            } else {
+                // (bsdfWeight * bsdfPdf) / pdfSurface (:407, :531-534, :587-589)
+                const float bsdf_pdf = Q.bpdf[i];
+                mis_pdf = bsdf_pdf > 0.0f ? h * bsdf_pdf + (1.0f - h) * Q.pdf[j] : 0.0f;
+                for (int ch = 0; ch < 3; ++ch) weight[ch] = mis_pdf == 0.0f ? 0.0f : (bw[ch] * bsdf_pdf) / mis_pdf;
+            }
+        } else {
+            // the guide's direction: bsdf->eval (smooth lobe, ESolidAngle) / pdfSurface (:456-507)
+            wo[0] = Q.d0[j]; wo[1] = Q.d1[j]; wo[2] = Q.d2[j];
+            const float cos_o = dot3(wo, n);
+            const bool zero = (wo[0] == 0.0f && wo[1] == 0.0f && wo[2] == 0.0f) || !__builtin_isfinite(cos_o);
+            const bool up = !zero && cos_o > 0.0f;
+            const float cpdf = kInvPi * cos_o;   // warp::squareToCosineHemispherePdf
+            const float bsdf_pdf = up ? cpdf * (1.0f - ps) : 0.0f;
+            mis_pdf = bsdf_pdf > 0.0f ? h * bsdf_pdf + (1.0f - h) * Q.pdf[j] : 0.0f;
+            const float Fo = up ? fresnel_dielectric(cos_o, bp[4]) : 0.0f;
+            const float rd = 1.0f / (1.0f - bp[6]);
+            const float k = cpdf * bp[5] * (1.0f - Fi) * (1.0f - Fo);
+            for (int ch = 0; ch < 3; ++ch) {
+                const float f = up ? S.refl[3 * QD.bsdf + ch] * rd * k : 0.0f;
+                weight[ch] = mis_pdf == 0.0f ? 0.0f : f / mis_pdf;
+            }
+        }
+    } else if (!valid) {
         // BSDF only, h = 1 (:316-323, :392-405): weight = rho, pdf = bsdfPdf
         wo[0] = Q.b0[i]; wo[1] = Q.b1[i]; wo[2] = Q.b2[i];
         const float cos_o = dot3(wo, n);
@@ -305,8 +407,9 @@ li_shade_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, i
         P.lr[i] += rad[0]; P.lg[i] += rad[1]; P.lb[i] += rad[2];
         record_radiance(P, i, nv, rad);
     }
-    // the saved vertex (cacheable: diffuse, :821-845)
-    if (nv < P.V) {
+    P.nray[i] += 1;
+    // the saved vertex (cacheable: not a delta lobe, :764, :821-845)
+    if (cacheable && nv < P.V) {
         const float clamped = fmaxf(mis_pdf, 0.1f);
         const float inv_pdf = 1.0f / clamped;
         for (int ch = 0; ch < 3; ++ch) {

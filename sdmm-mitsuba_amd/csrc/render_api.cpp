@@ -46,6 +46,7 @@ struct sdmm_scene {
     SceneDev S{};
     QuadDev* dquads = nullptr;
     float* drefl = nullptr;
+    float* dbpar = nullptr;
     float* drad = nullptr;
     float smin[3] = {0, 0, 0}, snorm = 1.0f, tmin[3] = {0, 0, 0}, tmax[3] = {0, 0, 0};
     // per-render buffers (grown)
@@ -93,8 +94,8 @@ int grow(sdmm_scene* s, int64_t P, int V, hipStream_t st) {
     size_t tb = 0;
     (void)hipcub::DeviceReduce::Sum(nullptr, tb, (const int32_t*)nullptr, (int64_t*)nullptr, (int)cap);
     tb = std::max(tb, li_select_temp_bytes(cap));
-    const size_t need = 12 * f + 3 * i4 + recb + 13 * f + u1 + i4 + 256 + al(tb) + 9 * f + 2 * u1 + 3 * i4 +
-                        (1 + 1 + 9 + 1) * f + i4;
+    const size_t need = 12 * f + 4 * i4 + recb + 13 * f + u1 + i4 + 256 + al(tb) + 9 * f + 2 * u1 + 3 * i4 +
+                        (1 + 1 + 9 + 1) * f + i4 + u1 + 4 * f;
     HIP_TRY(hipStreamSynchronize(st));
     if (s->buf) HIP_TRY(hipFree(s->buf));
     s->buf = nullptr;
@@ -110,6 +111,7 @@ int grow(sdmm_scene* s, int64_t P, int V, hipStream_t st) {
     s->P.depth = (int*)take(i4);
     s->P.quad = (int*)take(i4);
     s->P.nv = (int*)take(i4);
+    s->P.nray = (int*)take(i4);
     s->P.rec = (float*)take(recb);
     float** qf[13] = {&s->Q.c0, &s->Q.c1, &s->Q.c2, &s->Q.u0, &s->Q.u1, &s->Q.u2, &s->Q.b0,
                       &s->Q.b1, &s->Q.b2, &s->Q.d0, &s->Q.d1, &s->Q.d2, &s->Q.pdf};
@@ -132,6 +134,9 @@ int grow(sdmm_scene* s, int64_t P, int V, hipStream_t st) {
     for (int i = 0; i < 9; ++i) s->Q.k_F[i] = (float*)take(f);
     s->Q.hq = (float*)take(f);
     s->Q.k_mat = (int32_t*)take(i4);
+    s->Q.bdelta = (uint8_t*)take(u1);
+    float** bf[4] = {&s->Q.bw0, &s->Q.bw1, &s->Q.bw2, &s->Q.bpdf};
+    for (float** q : bf) *q = (float*)take(f);
     return SDMM_OK;
 }
 
@@ -145,6 +150,14 @@ int sdmm_scene_create(const sdmm_scene_desc* d, int device, sdmm_scene** out) {
         return fail(SDMM_E_INVALID, "sdmm_scene_create: invalid description");
     if (d->emitter && (d->n_emitters < 1 || !d->radiance))
         return fail(SDMM_E_INVALID, "sdmm_scene_create: emitters without radiance");
+    if (d->bsdf_params)
+        for (int b = 0; b < d->n_bsdfs; ++b) {
+            const float* bp = d->bsdf_params + kBsdfParams * b;
+            const bool ok = bp[0] == (float)kBsdfDiffuse ||
+                            (bp[0] == (float)kBsdfPlastic && bp[4] > 0.0f && bp[5] > 0.0f && bp[6] < 1.0f &&
+                             bp[7] >= 0.0f && bp[7] < 1.0f);
+            if (!ok) return fail(SDMM_E_INVALID, "sdmm_scene_create: invalid bsdf_params");
+        }
     *out = nullptr;
     std::vector<QuadDev> qs((size_t)d->n_quads);
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -193,6 +206,11 @@ int sdmm_scene_create(const sdmm_scene_desc* d, int device, sdmm_scene** out) {
     if (e == hipSuccess) e = hipMalloc(&s->dquads, sizeof(QuadDev) * qs.size());
     if (e == hipSuccess) e = hipMalloc(&s->drefl, sizeof(float) * 3 * (size_t)d->n_bsdfs);
     if (e == hipSuccess && d->emitter) e = hipMalloc(&s->drad, sizeof(float) * 3 * (size_t)d->n_emitters);
+    if (e == hipSuccess && d->bsdf_params)
+        e = hipMalloc(&s->dbpar, sizeof(float) * kBsdfParams * (size_t)d->n_bsdfs);
+    if (e == hipSuccess && d->bsdf_params)
+        e = hipMemcpy(s->dbpar, d->bsdf_params, sizeof(float) * kBsdfParams * (size_t)d->n_bsdfs,
+                      hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(s->dquads, qs.data(), sizeof(QuadDev) * qs.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipMemcpy(s->drefl, d->reflectance, sizeof(float) * 3 * (size_t)d->n_bsdfs, hipMemcpyHostToDevice);
@@ -206,6 +224,7 @@ int sdmm_scene_create(const sdmm_scene_desc* d, int device, sdmm_scene** out) {
     S.quads = s->dquads;
     S.n_quads = d->n_quads;
     S.refl = s->drefl;
+    S.bpar = s->dbpar;
     S.rad = s->drad;
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 4; ++c) S.cam[4 * r + c] = d->camera_to_world[4 * r + c];
@@ -226,6 +245,7 @@ void sdmm_scene_destroy(sdmm_scene* s) {
     (void)hipDeviceSynchronize();
     if (s->dquads) (void)hipFree(s->dquads);
     if (s->drefl) (void)hipFree(s->drefl);
+    if (s->dbpar) (void)hipFree(s->dbpar);
     if (s->drad) (void)hipFree(s->drad);
     if (s->buf) (void)hipFree(s->buf);
     if (s->hcount) (void)hipHostFree(s->hcount);
@@ -338,9 +358,9 @@ int sdmm_li_render(sdmm_scene* s, sdmm_stree* t, const sdmm_mix* const* node_mix
         vout->nv = s->P.nv;
     }
     if (stats) {
-        // every traced bounce ray saves a vertex (all BSDFs here are cacheable)
+        // traced bounce rays (a delta lobe's ray saves no vertex)
         size_t tb = s->temp_bytes;
-        HIP_TRY(hipcub::DeviceReduce::Sum(s->temp, tb, (const int32_t*)s->P.nv, s->dsum, (int)P, st));
+        HIP_TRY(hipcub::DeviceReduce::Sum(s->temp, tb, (const int32_t*)s->P.nray, s->dsum, (int)P, st));
         int64_t seg = 0;
         HIP_TRY(hipMemcpyAsync(&seg, s->dsum, sizeof(int64_t), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));

@@ -31,10 +31,20 @@ struct QuadDev {
     int bsdf, emitter;           // emitter -1: none
 };
 
+// Per-BSDF parameters beside the diffuse reflectance (kBsdfParams floats per
+// BSDF): [0] kind (0 diffuse, 1 smooth plastic), [1..3] specular reflectance,
+// [4] eta = intIOR / extIOR, [5] 1 / eta^2, [6] the internal diffuse Fresnel
+// reflectance fdrInt, [7] the specular sampling weight sAvg / (dAvg + sAvg)
+// (bsdfs/plastic.cpp:159-200)
+constexpr int kBsdfParams = 8;
+constexpr int kBsdfDiffuse = 0;
+constexpr int kBsdfPlastic = 1;
+
 struct SceneDev {
     const QuadDev* quads;
     int n_quads;
-    const float* refl;    // 3 per BSDF
+    const float* refl;    // 3 per BSDF (plastic: its diffuseReflectance)
+    const float* bpar;    // kBsdfParams per BSDF; null: every BSDF diffuse
     const float* rad;     // 3 per emitter
     float cam[12];        // camera-to-world 3x4 (row major)
     float tanx, aspect, near_clip;
@@ -50,6 +60,7 @@ struct PathsDev {
     int* depth;              // rRec.depth; -1 once the path has ended
     int* quad;               // hit quad
     int* nv;                 // saved vertices
+    int* nray;               // traced bounce rays (a delta bounce saves no vertex)
     float* rec;              // vertex records: rec[(f * V + v) * P + p]
     int V;
     int64_t P;
@@ -78,6 +89,10 @@ struct QueryDev {
     float* k_F[9];
     int32_t* k_mat;
     float* hq;
+    // the loop head's BSDF sample for the shade kernel (non-diffuse BSDFs):
+    // sampled lobe delta (1) or smooth (0), its weight (RGB) and pdf
+    uint8_t* bdelta;
+    float *bw0, *bw1, *bw2, *bpdf;
 };
 
 }  // namespace sdmm

@@ -106,8 +106,48 @@ def _cube_faces(M):
     return faces
 
 
-def cornell_box(width=640, height=360):
-    """sdmm_scene_desc fields for the Cornell Box (numpy arrays)."""
+def _fresnel_dielectric(cos_i, eta):
+    """fresnelDielectricExt (libcore/util.cpp:651-681), reflectance only (float64)."""
+    if eta == 1.0:
+        return 0.0
+    scale = 1.0 / eta if cos_i > 0 else eta
+    ct2 = 1.0 - (1.0 - cos_i * cos_i) * scale * scale
+    if ct2 <= 0.0:
+        return 1.0
+    ci, ct = abs(cos_i), np.sqrt(ct2)
+    rs = (ci - eta * ct) / (ci + eta * ct)
+    rp = (eta * ci - ct) / (eta * ci + ct)
+    return 0.5 * (rs * rs + rp * rp)
+
+
+def plastic_params(diffuse_rgb, specular_rgb=(1.0, 1.0, 1.0), int_ior=1.49, ext_ior=1.000277):
+    """The 8 bsdf_params floats of a smooth plastic (bsdfs/plastic.cpp:148-200;
+    include/sdmm_gpu.h sdmm_scene_desc): kind 1, specularReflectance, eta =
+    intIOR / extIOR (polypropylene / air, the plugin's defaults), 1 / eta^2,
+    fdrInt = fresnelDiffuseReflectance(1 / eta) (the integral over xi of
+    F(sqrt(xi)), here by adaptive quadrature in double where Mitsuba runs a
+    Gauss-Lobatto rule: the constant may differ in its last float bits), and
+    the specular sampling weight sAvg / (dAvg + sAvg) from the luminances."""
+    from scipy.integrate import quad
+    f32 = np.float32
+    eta = f32(f32(int_ior) / f32(ext_ior))
+    inv_eta2 = f32(f32(1.0) / f32(eta * eta))
+    fdr_int, _ = quad(lambda xi: _fresnel_dielectric(np.sqrt(xi), 1.0 / float(eta)), 0.0, 1.0,
+                      epsabs=1e-12, epsrel=1e-12, limit=200)
+
+    def lum(c):
+        c = [f32(x) for x in c]
+        return f32(f32(f32(c[0] * f32(0.212671)) + f32(c[1] * f32(0.715160))) + f32(c[2] * f32(0.072169)))
+    d_avg, s_avg = lum(diffuse_rgb), lum(specular_rgb)
+    ssw = f32(s_avg / f32(d_avg + s_avg))
+    return np.array([1.0, *specular_rgb, eta, inv_eta2, fdr_int, ssw], np.float32)
+
+
+def cornell_box(width=640, height=360, plastic=()):
+    """sdmm_scene_desc fields for the Cornell Box (numpy arrays).  plastic:
+    names of BSDFs (e.g. "TallBox", "ShortBox", "Floor") rendered as smooth
+    plastic over their diffuse reflectance (a delta specular lobe beside a
+    smooth one, like the Kitchen's `plastic` materials, kitchen.xml)."""
     names = list(_BSDFS)
     quads, bsdf, flip, emitter = [], [], [], []
     for m, name, fl in _RECTS:
@@ -120,7 +160,17 @@ def cornell_box(width=640, height=360):
     quads.append(np.concatenate(_rect(_mat(_LIGHT))))
     bsdf.append(names.index("Light")); flip.append(0); emitter.append(0)
     cam = np.array([float(x) for x in _CAMERA.split()], np.float32)
-    return {
+    extra = {}
+    if plastic:
+        unknown = set(plastic) - set(names)
+        if unknown:
+            raise ValueError(f"unknown BSDFs {sorted(unknown)}")
+        bp = np.zeros((len(names), 8), np.float32)
+        for i, nm in enumerate(names):
+            if nm in plastic:
+                bp[i] = plastic_params(_BSDFS[nm])
+        extra["bsdf_params"] = bp.reshape(-1)
+    return {**extra,
         "quads": np.asarray(quads, np.float32).reshape(-1),
         "flip_normals": np.asarray(flip, np.int32),
         "bsdf": np.asarray(bsdf, np.int32),

@@ -18,11 +18,12 @@ def _pdf_ftz(q, di, a, w):
     return _ftz(w * p2)
 
 
-def posterior_f64(mix_params: dict, x: np.ndarray, hpdf=None, is_diffuse=None, h=0.5) -> np.ndarray:
+def posterior_f64(mix_params: dict, x: np.ndarray, hpdf=None, is_diffuse=None, h=0.5, return_qc=False):
     """posteriorAndLog (mixture_model.h:146-192) in float64 from the float
     mixture parameters: the 'exact' reference both fp32 paths are judged by.
     With is_diffuse: the heuristic mix S' = (1-h) S + h hpdf on those rows,
-    gamma_k = (1-h) q_k / S' (:170-181)."""
+    gamma_k = (1-h) q_k / S' (:170-181).  return_qc: also the (N, K)
+    Mahalanobis distances q and cosines c = cos(theta) of each pair."""
     w = np.asarray(mix_params["weights"], np.float64)
     mean = np.asarray(mix_params["mean"], np.float64).reshape(-1, 6)
     to = np.asarray(mix_params["to"], np.float64).reshape(-1, 3, 3)
@@ -43,6 +44,8 @@ def posterior_f64(mix_params: dict, x: np.ndarray, hpdf=None, is_diffuse=None, h
     post = _pdf_ftz(q, di[None], a, w[None])
     post[bad] = 0
     S = post.sum(1, keepdims=True)
+    if return_qc:
+        return posterior_f64(mix_params, x, hpdf, is_diffuse, h), q, c
     if is_diffuse is None:
         with np.errstate(invalid="ignore", divide="ignore"):
             return np.where(S > 0, post / S, 0.0)
@@ -53,6 +56,18 @@ def posterior_f64(mix_params: dict, x: np.ndarray, hpdf=None, is_diffuse=None, h
         inv = 1.0 / S2
         scale = np.where(dif, (1.0 - h) * inv, inv)
         return np.where(np.isfinite(inv) & (S2 > 0), post * scale, 0.0)
+
+
+def explained_rows(post, q, c, qmax=100.0, cmin=1e-2, pmin=1e-7):
+    """Rows the mixture explains with well-conditioned fp32 arithmetic: the
+    fp64 max posterior sits at q < qmax, and no component with posterior
+    > pmin is near-antipodal (1 + c < cmin: there theta/sin(theta) amplifies
+    the fp32 rounding of c, and both fp32 paths -- the reference's and the
+    GPU's -- carry up to ~4e-3 of absolute error in such rows)."""
+    n = post.shape[0]
+    qm = q[np.arange(n), post.argmax(1)]
+    cond = ~((post > pmin) & (1.0 + c < cmin)).any(1)
+    return (qm < qmax) & (post.sum(1) > 0) & cond
 
 
 def estep_f64(mix_params: dict, x, w, hpdf=None, is_diffuse=None, h=0.5, chunk=2048):

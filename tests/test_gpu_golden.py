@@ -5,6 +5,7 @@ import numpy as np
 import pytest
 
 from helpers import estep_f64, posterior_f64
+from test_gpu_parity import check_explained
 
 pytestmark = pytest.mark.gpu
 GOLDEN = Path(__file__).resolve().parent / "golden"
@@ -29,12 +30,16 @@ def test_gpu_estep_vs_golden(pkg, gpu, plog, K):
     mix.posterior(ds, resp)
     got = resp.cpu().numpy()
     # the golden responsibilities (fp32 oracle) and the GPU's, both judged by
-    # the fp64 evaluation of the same float parameters (test_gpu_parity._check_resp)
-    exact = posterior_f64(p, g["x"])
+    # the fp64 evaluation of the same float parameters with the fixture's
+    # heuristic mix on its diffuse rows (test_gpu_parity._check_resp)
+    exact, q, c = posterior_f64(p, g["x"], g["hpdf"], g["is_diffuse"], return_qc=True)
     live = (g["resp"].sum(1) > 0) & (got.sum(1) > 0)
     eg = np.abs(got[live] - exact[live]).max()
     eo = np.abs(g["resp"][live] - exact[live]).max()
     plog("golden_resp_abs_err_vs_fp64", eg, 4 * eo + 1e-5, golden_fp32_err=eo)
+    # the flat 2e-5 bound on the explained, well-conditioned rows, against the
+    # fp64 evaluation and against the committed fixture
+    check_explained(got, g["resp"], exact, q, c, plog, tag=f"golden_K{K}")
     # and against the committed fixture itself: 1e-4 absolute (both evaluate the
     # same float parameters in fp32; where the fp64 evaluation departs from both
     # -- different FTZ flush points of tiny densities -- they still agree)

@@ -291,6 +291,29 @@ def test_guided_render_unbiased_and_trained(pkg, oracle, scenes, gpu, plog):
     assert eg < 0.85 * eu
 
 
+def test_plastic_render_unbiased(pkg, oracle, scenes, gpu, plog):
+    """Guided rendering over a delta + smooth BSDF (smooth plastic boxes and
+    floor) is unbiased against BSDF-only sampling: the guide is queried on
+    every plastic bounce and a BSDF-chosen delta lobe carries weight / h
+    (sdmm_proc.cpp:297, :383-409) -- the estimator the plugin now follows."""
+    desc = scenes.cornell_box(160, 90, plastic=("TallBox", "ShortBox", "Floor"))
+    sc = pkg.Scene(desc)
+    tree = _tree(pkg, sc)
+    node_mix = _train(pkg, sc, tree, 6, 8)
+    assert sum(m is not None for m in node_mix) >= 4
+    img, verts, st = sc.render(tree, node_mix, spp=4, guided=True, seed=78)
+    assert np.isfinite(img.cpu().numpy()).all()
+    _check_producer(pkg, oracle, tree, verts, 8, 0xABE, plog, "plastic")
+    spp = 64
+    lum = lambda im: im.cpu().numpy().mean(0).reshape(-1)
+    g = lum(sc.render(tree, node_mix, spp=spp, guided=True, seed=3456)[0])
+    u = lum(sc.render(tree, None, spp=spp, guided=False, seed=4321)[0])
+    mg, mu = g.mean(), u.mean()
+    se = np.sqrt(g.var() / g.size + u.var() / u.size)
+    plog("li_plastic_vs_unguided_mean_sigma", float(abs(mg - mu) / se), 4.0, guided=float(mg), unguided=float(mu))
+    assert abs(mg - mu) < 4.0 * se, (mg, mu, se)
+
+
 @pytest.mark.parametrize("K", [16, 512])
 def test_product_render_unbiased(pkg, oracle, scenes, gpu, plog, K):
     """sampleProduct in the device Li (sdmm_proc.cpp:327-392): guided bounces

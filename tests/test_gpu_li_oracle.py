@@ -80,16 +80,20 @@ def _compare_guided(oracle, plog, tag, img, rec, nv, r):
     assert abs(m1 - m2) <= 5e-3 * m2
 
 
-def test_guided_li_matches_oracle(pkg, oracle, scenes, gpu, plog):
+@pytest.mark.parametrize("K", [16, 128])
+def test_guided_li_matches_oracle(pkg, oracle, scenes, gpu, plog, K):
+    """K = 128: configs[2]'s leaf size (the Torus meshes are LFS pointers; the
+    Cornell Box stands in), through the tree wavefront's K = 128 kernels."""
     desc = scenes.cornell_box(128, 72)
     sc = pkg.Scene(desc)
     tree = _tree(pkg, sc)
-    node_mix = _train(pkg, sc, tree, 4, 8)
+    node_mix = _train(pkg, sc, tree, 4, 8, K=K)
+    assert any(m is not None and m.K == K for m in node_mix)
     img, rec, nv, _ = _device(sc, tree, node_mix, True)
     aabb, child, _ = tree.nodes()
     r = oracle.li_render(desc, aabb, child, node_mix=_oracle_mixes(oracle, node_mix), guided=True, spp=SPP,
                          seed=SEED, threads=16)
-    _compare_guided(oracle, plog, "li_guided", img, rec, nv, r)
+    _compare_guided(oracle, plog, f"li_guided_K{K}", img, rec, nv, r)
 
 
 def test_product_li_matches_oracle(pkg, oracle, scenes, gpu, plog):
@@ -104,3 +108,34 @@ def test_product_li_matches_oracle(pkg, oracle, scenes, gpu, plog):
     r = oracle.li_render(desc, aabb, child, node_mix=_oracle_mixes(oracle, node_mix), guided=True, spp=SPP,
                          seed=SEED, learned=learned, threads=16)
     _compare_guided(oracle, plog, "li_product", img, rec, nv, r)
+
+
+PLASTIC = ("TallBox", "ShortBox", "Floor")
+
+
+def test_plastic_li_matches_oracle(pkg, oracle, scenes, gpu, plog):
+    """A delta + smooth BSDF (smooth plastic on the boxes and the floor, the
+    Kitchen's `plastic`) through the device Li and the CPU Li: unguided
+    bitwise (records, vertex counts -- a delta bounce saves none -- image);
+    guided with trained K = 16 leaves >= 99 % of the paths (the guide is
+    queried on every plastic bounce, a BSDF-chosen delta lobe returns
+    weight / h with pdf * h: sdmm_proc.cpp:297, :383-409)."""
+    desc = scenes.cornell_box(128, 72, plastic=PLASTIC)
+    sc = pkg.Scene(desc)
+    tree = _tree(pkg, sc)
+    img, rec, nv, st = _device(sc, tree, None, False)
+    aabb, child, _ = tree.nodes()
+    r = oracle.li_render(desc, aabb, child, spp=SPP, seed=SEED, threads=8)
+    np.testing.assert_array_equal(nv, r["nv"])
+    sel = np.arange(rec.shape[1])[:, None] < nv[None, :]
+    plog("li_plastic_unguided_rec_max_abs_diff", float(np.abs(rec - r["rec"])[:, sel].max()), 0.0)
+    np.testing.assert_array_equal(rec[:, sel], r["rec"][:, sel])
+    np.testing.assert_array_equal(img, r["image"])
+    # delta bounces trace a ray but save no vertex
+    assert st["segments"] > int(nv.sum())
+    node_mix = _train(pkg, sc, tree, 4, 8)
+    img, rec, nv, _ = _device(sc, tree, node_mix, True)
+    aabb, child, _ = tree.nodes()
+    r = oracle.li_render(desc, aabb, child, node_mix=_oracle_mixes(oracle, node_mix), guided=True, spp=SPP,
+                         seed=SEED, threads=16)
+    _compare_guided(oracle, plog, "li_plastic_guided", img, rec, nv, r)

@@ -84,11 +84,19 @@ def _oracle_check(oracle, t, mixes, c, u, d, node, has, cw, dw, pw, pdw, plog):
     plog("wavefront_vs_oracle_pdf_err_over_tol", perr, 1.0)
 
 
-@pytest.mark.parametrize("K,nq", [(16, 1 << 15), (16, 3000), (64, 1 << 14)])
-def test_wavefront_equals_per_leaf_guide(pkg, oracle, synth, gpu, plog, K, nq):
+@pytest.mark.parametrize("K,nq,cap", [(16, 1 << 15, 40), (16, 3000, 40), (64, 1 << 14, 40),
+                                      (128, 1 << 14, 40), (128, 1 << 14, 4), (128, 1 << 14, 0)])
+def test_wavefront_equals_per_leaf_guide(pkg, oracle, synth, gpu, plog, K, nq, cap):
+    """K = 128 is configs[2]'s leaf size: the tree kernels' candidate pass
+    (capacity 40), the 16-lane group fallback most queries take at capacity 4,
+    and every query on the full-K path at capacity 0 -- indices bit-exact
+    against the oracle per leaf (sdmm_proc.cpp:275-590 at K = 128 leaves)."""
     import torch
     b, t, mixes, leaves = _tree_and_leaf_mixtures(pkg, synth, K)
     assert sum(m is not None for m in mixes) >= 4 and sum(mixes[v] is None for v in leaves) >= 1
+    for m in mixes:
+        if m is not None:
+            m.set_guide_capacity(cap)
     c, u, d, ct, ut, dt = _queries(gpu, nq, 5)
     node = torch.empty(nq, dtype=torch.int32, device=gpu)
     dw, pw, cw = t.guide(mixes, ct, ut, node_out=node)

@@ -81,3 +81,56 @@ def test_pixel_range_is_a_slice(oracle, scenes):
     part = oracle.li_render(d, aabb, child, spp=2, seed=11, pixels=(100, 300), threads=2)
     np.testing.assert_array_equal(full["image"].reshape(3, -1)[:, 100:300], part["image"].reshape(3, -1)[:, 100:300])
     np.testing.assert_array_equal(full["rec"][:, :, 200:600], part["rec"])
+
+
+def _plastic_albedo(cos_i, bp, rho):
+    """Directional albedo of SmoothPlastic (plastic.cpp:250-290): Fi spec +
+    (1 - Fi) invEta2 rho / (1 - fdrInt) * int (1 - F(cos_o)) cos_o / pi dw,
+    the integral 1 - int_0^1 F(sqrt(xi)) dxi (fdrExt) by quadrature."""
+    from scipy.integrate import quad
+    import importlib
+    scenes = importlib.import_module("sdmm_mitsuba_amd.scenes")
+    eta, inv_eta2, fdr_int = float(bp[4]), float(bp[5]), float(bp[6])
+    fdr_ext, _ = quad(lambda xi: scenes._fresnel_dielectric(np.sqrt(xi), eta), 0.0, 1.0, epsabs=1e-12, limit=200)
+    fi = np.array([scenes._fresnel_dielectric(c, eta) for c in cos_i])
+    return fi * float(bp[1]) + (1 - fi) * inv_eta2 * rho / (1 - fdr_int) * (1 - fdr_ext)
+
+
+def test_plastic_albedo_known_answer(oracle, scenes):
+    """The plastic bounce (delta specular lobe + Fresnel-weighted diffuse
+    base) against its closed-form directional albedo: a box whose far face is
+    plastic and whose other faces are black emitters (Le = 1); with one
+    scatter (maxDepth 2) a pixel's expected radiance is the albedo at its
+    camera ray's incidence angle -- both lobes are exercised (the delta lobe
+    saves no vertex, the diffuse one does)."""
+    d = _furnace(0.0, 1.0, w=24, h=16)
+    rho = 0.6
+    bp = scenes.plastic_params((rho, rho, rho))
+    far = 5                                           # axis 2, sgn +1: the face the camera looks at
+    d["bsdf"] = np.zeros(6, np.int32)
+    d["bsdf"][far] = 1
+    d["reflectance"] = np.float32([0.0, 0.0, 0.0, rho, rho, rho])
+    d["bsdf_params"] = np.concatenate([np.zeros(8, np.float32), bp])
+    d["emitter"] = np.zeros(6, np.int32)
+    d["emitter"][far] = -1
+    aabb = np.float32([[0, 0, 0, 1, 1, 1]])
+    child = np.int32([[-1, -1]])
+    spp = 256
+    r = oracle.li_render(d, aabb, child, spp=spp, max_depth=2, rr_depth=2, V=1, seed=5, threads=4)
+    # camera rays through the pixel centres: cos(theta_i) = d_z (the face normal is -z)
+    W, H = d["width"], d["height"]
+    tanx = np.tan(np.radians(35.0))
+    sx = (np.arange(W) + 0.5) / W
+    sy = (np.arange(H) + 0.5) / H
+    lx = (1 - 2 * sx)[None, :] * tanx
+    ly = (1 - 2 * sy)[:, None] * tanx / (W / H)
+    cos_i = 1 / np.sqrt(lx ** 2 + ly ** 2 + 1)
+    want = _plastic_albedo(cos_i.reshape(-1), bp, rho).reshape(H, W)
+    img = r["image"][0]
+    var = (r["image_sqr"][0] - img ** 2) / spp                         # per-pixel variance of the mean
+    err = abs(img.mean() - want.mean())
+    sig = np.sqrt(var.sum()) / img.size
+    print("plastic albedo", img.mean(), want.mean(), sig)
+    assert err <= 4 * sig + 2e-4, (img.mean(), want.mean(), sig)
+    # both lobes taken: vertices saved for the diffuse lobe only
+    assert 0 < (r["nv"] == 1).mean() < 1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of the headline responsibility E-step: library builds (SDMM_LIB_PATH) x
-# tile variants (SDMM_RESP_VARIANT), each a short bench.py --no-extra run.
-# Usage: bash tools/gpu_resp_ab.sh "lib1.so lib2.so" "4 0 2"
+# split variants (SDMM_RESP_VARIANT), each a short bench.py --no-extra run.
+# Usage: bash tools/gpu_resp_ab.sh "lib1.so lib2.so" "0 1"
 OUT=gpurun_out; mkdir -p $OUT
 for lib in $1; do
   for v in $2; do
