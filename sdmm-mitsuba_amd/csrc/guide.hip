@@ -2432,20 +2432,32 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
     return hipGetLastError();
 }
 
-// the thread path's pair cache for `threads` query columns (stream ordered;
-// none when the allocation fails: the pairs are then re-formed, same results)
-static PairCacheDev pair_cache_alloc(int64_t threads, hipStream_t st) {
-    PairCacheDev pc{nullptr, threads, kPairCacheCap};
-    if (kPairCacheCap <= 0) return pc;
-    if (hipMallocAsync((void**)&pc.base, sizeof(float) * kPairFields * (size_t)kPairCacheCap * (size_t)threads, st) !=
-        hipSuccess) {
-        (void)hipGetLastError();
-        pc.base = nullptr;
+// The product launches' scratch in the handle's grow-only buffer: the thread
+// path's pair cache for `threads` query columns, then the wave kernel's pair
+// slices (fblocks workgroups).  Regrowth frees the old buffer in stream order
+// (every earlier use is on the same stream) and allocates the larger one; an
+// allocation failure is an error (no silent uncached path).
+static hipError_t product_scratch(ProductScratch* ps, int64_t threads, unsigned fblocks, hipStream_t st,
+                                  PairCacheDev* pc, float** pairs) {
+    const size_t cb = kPairCacheCap > 0 ? sizeof(float) * kPairFields * (size_t)kPairCacheCap * (size_t)threads : 0;
+    const size_t ca = (cb + 255) / 256 * 256;
+    const size_t need = ca + sizeof(float) * kPcStride * (size_t)kProductPairCap * fblocks;
+    if (!ps) return hipErrorInvalidValue;
+    if (ps->bytes < need) {
+        if (ps->base) {
+            const hipError_t f = hipFreeAsync(ps->base, st);
+            if (f != hipSuccess) return f;
+        }
+        ps->base = nullptr;
+        ps->bytes = 0;
+        const size_t grown = need + need / 4;
+        const hipError_t e = hipMallocAsync((void**)&ps->base, grown, st);
+        if (e != hipSuccess) return e;
+        ps->bytes = grown;
     }
-    return pc;
-}
-static void pair_cache_free(const PairCacheDev& pc, hipStream_t st) {
-    if (pc.base) (void)hipFreeAsync(pc.base, st);
+    *pc = PairCacheDev{kPairCacheCap > 0 ? ps->base : nullptr, threads, kPairCacheCap};
+    *pairs = (float*)((char*)ps->base + ca);
+    return hipSuccess;
 }
 
 // Product sampling (or its pdf, dgiven != null) against one mixture: the
@@ -2456,7 +2468,7 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
                                 const float* const frame[9], float* h, const float* bw, const float* bmean,
                                 const float* bcov, const uint8_t* diffuse, int B, int M, float norm2, float norm3,
                                 int cap, int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
-                                const GuideSortScratch* sort) {
+                                const GuideSortScratch* sort, ProductScratch* scratch) {
     if (nq <= 0) return hipSuccess;
     if (nq > INT32_MAX) return hipErrorInvalidValue;
     if (K > kWaveKMax || M > 64) return hipErrorInvalidValue;
@@ -2480,7 +2492,12 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
         perm = sort->idx[1];
     }
     const dim3 grid((unsigned)((nq + 63) / 64));
-    pio.cache = pair_cache_alloc((int64_t)grid.x * 64, st);
+    // the full-K queries' product pairs (up to kProductPairCap per query): one
+    // scratch slice per workgroup of the wave kernel
+    const unsigned fblocks = (unsigned)(cus * 4 * SDMM_PRODUCT_WPE);
+    float* pscratch = nullptr;
+    e = product_scratch(scratch, (int64_t)grid.x * 64, fblocks, st, &pio.cache, &pscratch);
+    if (e != hipSuccess) return e;
 #define SDMM_PRODUCT_CAND(P, L)                                                                           \
     hipLaunchKernelGGL((guide_product_cand_kernel<P, L>), grid, dim3(64), 0, st, gp, Kp, K, condCov, nq, io, pio, \
                        bt, gc, cap, fb_count, fb_list, perm)
@@ -2495,29 +2512,14 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
     }
 #undef SDMM_PRODUCT_CAND
     e = hipGetLastError();
-    pair_cache_free(pio.cache, st);
     if (e != hipSuccess) return e;
-    // the full-K queries' product pairs (up to kProductPairCap per query) live in a
-    // stream-ordered scratch for the call: one slice per workgroup
-    const unsigned fblocks = (unsigned)(cus * 4 * SDMM_PRODUCT_WPE);
-    float* pscratch = nullptr;
-    const size_t sbytes = sizeof(float) * kPcStride * (size_t)kProductPairCap * fblocks;
-    if (hipMallocAsync((void**)&pscratch, sbytes, st) != hipSuccess) {
-        (void)hipGetLastError();
-        pscratch = nullptr;   // no scratch: the pairs are recomputed (same results)
-    }
     if (dgiven)
         hipLaunchKernelGGL(guide_product_wave_kernel<true>, dim3(fblocks), dim3(64), lds, st, gp, Kp, K, condCov, io,
                            pio, bt, gc, pscratch, kProductPairCap, fb_count, fb_list);
     else
         hipLaunchKernelGGL(guide_product_wave_kernel<false>, dim3(fblocks), dim3(64), lds, st, gp, Kp, K, condCov,
                            io, pio, bt, gc, pscratch, kProductPairCap, fb_count, fb_list);
-    e = hipGetLastError();
-    if (pscratch) {
-        const hipError_t f = hipFreeAsync(pscratch, st);
-        if (e == hipSuccess) e = f;
-    }
-    return e;
+    return hipGetLastError();
 }
 
 // The product wavefront over the tree (tab / cctab per node, kmax the largest
@@ -2531,7 +2533,7 @@ hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const v
                                      float* h, const float* bw, const float* bmean, const float* bcov,
                                      const uint8_t* diffuse, int B, int M, float norm2, float norm3, int cap,
                                      int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
-                                     const GuideSortScratch* sort) {
+                                     const GuideSortScratch* sort, ProductScratch* scratch) {
     if (nq <= 0) return hipSuccess;
     if (nq > INT32_MAX) return hipErrorInvalidValue;
     if (kmax < 1) kmax = 1;
@@ -2571,7 +2573,10 @@ hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const v
     const GuideMix* tb = (const GuideMix*)tab;
     const float* const* cc = (const float* const*)cctab;
     const dim3 grid((unsigned)((nq + 63) / 64));
-    pio.cache = pair_cache_alloc((int64_t)grid.x * 64, st);
+    const unsigned fblocks = (unsigned)(cus * 4 * SDMM_PRODUCT_WPE);
+    float* pscratch = nullptr;
+    e = product_scratch(scratch, (int64_t)grid.x * 64, fblocks, st, &pio.cache, &pscratch);
+    if (e != hipSuccess) return e;
 #define SDMM_TREE_PRODUCT_CAND(P, L)                                                                         \
     hipLaunchKernelGGL((guide_tree_product_cand_kernel<P, L>), grid, dim3(64), 0, st, nd, tb, cc, nq, iox, pio, \
                        bt, gc, cap, fb_count, fb_list, perm, node_out)
@@ -2586,27 +2591,14 @@ hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const v
     }
 #undef SDMM_TREE_PRODUCT_CAND
     e = hipGetLastError();
-    pair_cache_free(pio.cache, st);
     if (e != hipSuccess) return e;
-    const unsigned fblocks = (unsigned)(cus * 4 * SDMM_PRODUCT_WPE);
-    float* pscratch = nullptr;
-    const size_t sbytes = sizeof(float) * kPcStride * (size_t)kProductPairCap * fblocks;
-    if (hipMallocAsync((void**)&pscratch, sbytes, st) != hipSuccess) {
-        (void)hipGetLastError();
-        pscratch = nullptr;   // no scratch: the pairs are recomputed (same results)
-    }
     if (pdf_only)
         hipLaunchKernelGGL(guide_tree_product_wave_kernel<true>, dim3(fblocks), dim3(64), lds, st, nd, tb, cc, kmax,
                            iox, pio, bt, gc, pscratch, kProductPairCap, fb_count, fb_list);
     else
         hipLaunchKernelGGL(guide_tree_product_wave_kernel<false>, dim3(fblocks), dim3(64), lds, st, nd, tb, cc,
                            kmax, iox, pio, bt, gc, pscratch, kProductPairCap, fb_count, fb_list);
-    e = hipGetLastError();
-    if (pscratch) {
-        const hipError_t f = hipFreeAsync(pscratch, st);
-        if (e == hipSuccess) e = f;
-    }
-    return e;
+    return hipGetLastError();
 }
 
 hipError_t launch_sample_cdf(const float* cdf, int n, const float* u, int64_t nq, int32_t* out,

@@ -101,7 +101,7 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
                                 const float* const frame[9], float* h, const float* bw, const float* bmean,
                                 const float* bcov, const uint8_t* diffuse, int B, int M, float norm2, float norm3,
                                 int cap, int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
-                                const GuideSortScratch* sort);
+                                const GuideSortScratch* sort, ProductScratch* scratch);
 hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const void* cctab, int kmax, int64_t nq,
                                      const float* const c[3], const float* const u[3], const float* choice,
                                      const float* const dgiven[3], float* const d[3], float* pdf, int32_t* comp,
@@ -109,7 +109,7 @@ hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const v
                                      float* h, const float* bw, const float* bmean, const float* bcov,
                                      const uint8_t* diffuse, int B, int M, float norm2, float norm3, int cap,
                                      int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
-                                     const GuideSortScratch* sort);
+                                     const GuideSortScratch* sort, ProductScratch* scratch);
 #ifndef SDMM_GUIDE_CAP_MAX
 #define SDMM_GUIDE_CAP_MAX 40
 #endif
@@ -169,6 +169,22 @@ namespace {
         if (e_ != hipSuccess)                                                             \
             return fail(SDMM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
     } while (0)
+
+// release a scratch buffer before regrowing it: the pointer is cleared first,
+// so an error return can never leave it dangling for a second free (the free
+// itself is not checked, as in destroy)
+template <class T>
+void release_dev(T*& p) {
+    void* q = (void*)p;
+    p = nullptr;
+    if (q) (void)hipFree(q);
+}
+template <class T>
+void release_host(T*& p) {
+    void* q = (void*)p;
+    p = nullptr;
+    if (q) (void)hipHostFree(q);
+}
 
 // (float) pow((double)(float)INV_SQRT_TWO_PI, d) -- mvtn.h:351-352
 float norm_const(int d) {
@@ -305,6 +321,7 @@ struct sdmm_mix {
     mutable int* guide_fb = nullptr;
     mutable int64_t guide_fb_cap = 0;
     mutable GuideSortScratch guide_sort{};
+    mutable ProductScratch product_scratch{};   // grow-only (guide.hip product_scratch)
     int guide_order = 1;            // 1: serve large batches in Morton order of c (sdmm_set_guide_order)
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
@@ -371,7 +388,7 @@ int nccl_fail(ncclResult_t r, const char* what) {
 
 int comm_pinned(sdmm_comm* c, size_t bytes) {
     if (bytes <= c->pinned_bytes) return SDMM_OK;
-    if (c->pinned) HIP_TRY(hipHostFree(c->pinned));
+    release_host(c->pinned);
     c->pinned = nullptr;
     c->pinned_bytes = 0;
     HIP_TRY(hipHostMalloc(&c->pinned, bytes, hipHostMallocDefault));
@@ -473,7 +490,7 @@ int check_samples(const sdmm_samples* s) {
 
 int ensure_partials(sdmm_mix* m, int rows) {
     if (rows <= m->partial_rows) return SDMM_OK;
-    if (m->partials) HIP_TRY(hipFree(m->partials));
+    release_dev(m->partials);
     m->partials = nullptr;
     int cap = rows < 1024 ? 1024 : rows;
     HIP_TRY(hipMalloc(&m->partials, sizeof(float) * (size_t)cap * m->pstride));
@@ -489,7 +506,7 @@ int grow_guide_scratch(int*& fb, int64_t& fb_cap, GuideSortScratch& sort, hipStr
     if (nq + 1 <= fb_cap) return SDMM_OK;
     if (fb) {
         HIP_TRY(hipStreamSynchronize(st));
-        HIP_TRY(hipFree(fb));
+        release_dev(fb);
         fb = nullptr;
         fb_cap = 0;
     }
@@ -834,10 +851,15 @@ int create_many(int K, const sdmm_em_params* params, int device, hipStream_t st,
         return fail(SDMM_E_HIP, "hipMallocAsync failed");
     }
     int r = SDMM_OK;
-    // fault injection for the cleanup path's test (tests/test_gpu_batched.py):
-    // member SDMM_TEST_FAIL_MEMBER fails as if its creation had
-    const char* inject = std::getenv("SDMM_TEST_FAIL_MEMBER");
-    const int fail_at = inject ? std::atoi(inject) : -1;
+    // fault injection for the cleanup path's test (tests/test_gpu_batched.py),
+    // behind the explicit debug switch SDMM_DEBUG_FAULT_INJECTION=1 (README):
+    // member SDMM_TEST_FAIL_MEMBER then fails as if its creation had
+    int fail_at = -1;
+    if (const char* dbg = std::getenv("SDMM_DEBUG_FAULT_INJECTION"); dbg && std::strcmp(dbg, "1") == 0) {
+        const char* inject = std::getenv("SDMM_TEST_FAIL_MEMBER");
+        fail_at = inject ? std::atoi(inject) : -1;
+        if (fail_at >= 0) std::fprintf(stderr, "sdmm: debug fault injection at create_many member %d\n", fail_at);
+    }
     for (int i = 0; i < n && !r; ++i) {
         if (i == fail_at) { r = fail(SDMM_E_HIP, "create_many: injected failure"); break; }
         r = create_impl(K, params, device, st, true, &out[i], (char*)slab->p + stride * (size_t)i);
@@ -890,6 +912,9 @@ void sdmm_detail::destroy_impl(sdmm_mix* m, bool sync) {
     }
     if (m->partials) (void)hipFree(m->partials);
     if (m->guide_fb) (void)hipFree(m->guide_fb);
+    // stream ordered after the handle's last product launch (allocated on
+    // its stream; streams are synchronised above or by destroy_many)
+    if (m->product_scratch.base) (void)hipFreeAsync(m->product_scratch.base, m->stream);
     if (m->staging) (void)hipFree(m->staging);
     if (m->batch_dev) (void)hipFree(m->batch_dev);
     if (m->batch_host) (void)hipHostFree(m->batch_host);
@@ -1196,7 +1221,7 @@ static int init_hemisphere_batched_impl(sdmm_mix* const* mixes, int n, const flo
     std::lock_guard<std::mutex> hold(sg.mu);
     const size_t want = (per * (size_t)n + 255) / 256 * 256 + sizeof(InitDescHost) * (size_t)n;
     if (want > sg.cap) {
-        if (sg.p) HIP_TRY(hipHostFree(sg.p));
+        release_host(sg.p);
         sg.p = nullptr;
         sg.cap = 0;
         const size_t cap = std::max<size_t>(want + want / 2, 1 << 20);
@@ -1223,7 +1248,16 @@ static int init_hemisphere_batched_impl(sdmm_mix* const* mixes, int n, const flo
         const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
         const int nt = std::max(1, std::min({16, hw, n / 64}));
         std::vector<std::thread> th;
-        for (int t = 1; t < nt; ++t) th.emplace_back(init_range, (int)((int64_t)n * t / nt), (int)((int64_t)n * (t + 1) / nt));
+        for (int t = 1; t < nt; ++t) {
+            const int a = (int)((int64_t)n * t / nt), b = (int)((int64_t)n * (t + 1) / nt);
+            // a thread that cannot be started (std::system_error must not leave
+            // this extern "C" call): its range runs here instead
+            try {
+                th.emplace_back(init_range, a, b);
+            } catch (...) {
+                init_range(a, b);
+            }
+        }
         init_range(0, (int)((int64_t)n / nt));
         for (auto& x : th) x.join();
     }
@@ -1280,10 +1314,14 @@ int sdmm_iterations_run(const sdmm_mix* const* mixes, int n, int* out) {
     const size_t tab_bytes = ((sizeof(void*) * (size_t)n + 255) / 256) * 256;
     const size_t need = tab_bytes + sizeof(double) * (size_t)n;
     if (need > m0->it_cap) {
-        if (m0->it_dev) HIP_TRY(hipFree(m0->it_dev));
-        if (m0->it_host) HIP_TRY(hipHostFree(m0->it_host));
+        // pointers cleared before any error can return (destroy must not free
+        // them twice); free errors are ignored as in destroy
+        void* od = m0->it_dev;
+        void* oh = m0->it_host;
         m0->it_dev = m0->it_host = nullptr;
         m0->it_cap = 0;
+        if (od) (void)hipFree(od);
+        if (oh) (void)hipHostFree(oh);
         const size_t cap = std::max<size_t>(need, 4096);
         HIP_TRY(hipMalloc(&m0->it_dev, cap));
         HIP_TRY(hipHostMalloc(&m0->it_host, cap, hipHostMallocDefault));
@@ -1622,8 +1660,8 @@ int batched_iteration(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* s, 
     HIP_TRY(hipEventSynchronize(m0->batch_copied));   // the pinned tables are free again
     if (need > m0->batch_bytes) {
         HIP_TRY(hipStreamSynchronize(st));
-        if (m0->batch_dev) HIP_TRY(hipFree(m0->batch_dev));
-        if (m0->batch_host) HIP_TRY(hipHostFree(m0->batch_host));
+        release_dev(m0->batch_dev);
+        release_host(m0->batch_host);
         m0->batch_dev = m0->batch_host = nullptr;
         m0->batch_bytes = 0;
         const size_t cap = need < (1u << 16) ? (1u << 16) : need + need / 2;
@@ -1637,7 +1675,7 @@ int batched_iteration(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* s, 
         const size_t sbytes = sizeof(double) * (len + 1) * (size_t)n_mix;
         if (sbytes > m0->shard_bytes) {
             HIP_TRY(hipStreamSynchronize(st));
-            if (m0->shard_stats) HIP_TRY(hipFree(m0->shard_stats));
+            release_dev(m0->shard_stats);
             m0->shard_stats = nullptr;
             m0->shard_bytes = 0;
             HIP_TRY(hipMalloc((void**)&m0->shard_stats, sbytes));
@@ -1699,7 +1737,7 @@ static int stage_host_samples(sdmm_mix* m, const sdmm_samples* s, sdmm_samples* 
     const size_t need = n * (7 * 4 + 4 + 1) + 64;
     if (need > m->staging_bytes) {
         HIP_TRY(hipStreamSynchronize(m->stream));
-        if (m->staging) HIP_TRY(hipFree(m->staging));
+        release_dev(m->staging);
         m->staging = nullptr;
         HIP_TRY(hipMalloc(&m->staging, need));
         m->staging_bytes = need;
@@ -1769,7 +1807,7 @@ int sdmm_em_step_host(sdmm_mix* m, const sdmm_samples* s, int iterations) {
     const size_t n = (size_t)s->n;
     const size_t need = n * (7 * 4 + 4 + 1) + 64;
     if (need > m->staging_bytes) {
-        if (m->staging) HIP_TRY(hipFree(m->staging));
+        release_dev(m->staging);
         m->staging = nullptr;
         HIP_TRY(hipMalloc(&m->staging, need));
         m->staging_bytes = need;
@@ -1886,7 +1924,7 @@ int sdmm_guide_product_batch(const sdmm_mix* m, int64_t nq, const float* const c
                                  frame, heuristic, bsdf->weights, bsdf->means, bsdf->covs, bsdf->diffuse, bsdf->B,
                                  bsdf->M,
                                  m->norm2, m->norm3, m->guide_cap, m->guide_fb, m->guide_fb + 1, m->cus, m->stream,
-                                 guide_order(m, nq)));
+                                 guide_order(m, nq), &m->product_scratch));
     return SDMM_OK;
 }
 
@@ -1903,7 +1941,7 @@ int sdmm_pdf_product_batch(const sdmm_mix* m, int64_t nq, const float* const c[3
     HIP_TRY(launch_guide_product(m->gp, m->Kp, m->K, m->C.condCov, nq, c, nullptr, d, nullptr, pdf, nullptr,
                                  material, frame, heuristic, bsdf->weights, bsdf->means, bsdf->covs, bsdf->diffuse,
                                  bsdf->B, bsdf->M, m->norm2, m->norm3, m->guide_cap, m->guide_fb, m->guide_fb + 1, m->cus,
-                                 m->stream, guide_order(m, nq)));
+                                 m->stream, guide_order(m, nq), &m->product_scratch));
     return SDMM_OK;
 }
 
@@ -2071,6 +2109,7 @@ struct sdmm_stree {
     int* guide_fb = nullptr;
     int64_t guide_fb_cap = 0;
     GuideSortScratch guide_sort{};
+    ProductScratch product_scratch{};
     bool stream_set = false;    // sdmm_stree_set_stream called (NULL then means the null stream)
     // the bound mixtures' streams other than the tree's: a wavefront waits for
     // their pending work (EM steps) through one event per stream
@@ -2272,7 +2311,11 @@ void st_split_many(sdmm_stree* t, int n, const int* leaves, std::vector<int64_t>
         work();
     } else {
         std::vector<std::thread> th;
-        for (unsigned k = 0; k < nt; ++k) th.emplace_back(work);
+        try {
+            for (unsigned k = 0; k < nt; ++k) th.emplace_back(work);
+        } catch (...) {
+            work();   // the shared counter hands this thread what is left
+        }
         for (auto& x : th) x.join();
     }
     for (int i = 0; i < n; ++i) st_merge_local(t, leaves[i], L[(size_t)i]);
@@ -2303,7 +2346,7 @@ int st_upload(sdmm_stree* t) {
     const size_t bytes = 32 * t->nodes.size();
     if (bytes > t->dnodes_cap) {
         HIP_TRY(hipStreamSynchronize(t->stream));
-        if (t->dnodes) HIP_TRY(hipFree(t->dnodes));
+        release_dev(t->dnodes);
         t->dnodes = nullptr;
         const size_t cap = bytes * 2 > 4096 ? bytes * 2 : 4096;
         HIP_TRY(hipMalloc(&t->dnodes, cap));
@@ -2355,6 +2398,10 @@ void sdmm_stree_destroy(sdmm_stree* t) {
     if (t->split_mem) (void)hipFree(t->split_mem);
     if (t->split_small) (void)hipFree(t->split_small);
     if (t->guide_fb) (void)hipFree(t->guide_fb);
+    if (t->product_scratch.base) {
+        (void)hipFreeAsync(t->product_scratch.base, t->stream);
+        (void)hipStreamSynchronize(t->stream);
+    }
     for (hipEvent_t e : t->mix_events) (void)hipEventDestroy(e);
     if (t->stream && t->own_stream) (void)hipStreamDestroy(t->stream);
     delete t;
@@ -2471,6 +2518,9 @@ size_t split_mem_bytes(int64_t nc) {
     return 8 * plane + fl + rk + ((split_scan_temp_bytes(2 * nc + 1) + 255) / 256) * 256;
 }
 
+// the flag scan covers 2 n + 1 entries of a level as an int item count
+constexpr int64_t kSplitLevelMax = (INT32_MAX - 1) / 2;
+
 // grow t's split scratch to `need` samples per level; keep >= 0: the buffer
 // set whose first `live` entries are copied over
 int split_grow(sdmm_stree* t, int64_t need, int keep, int64_t live, hipStream_t st, DevSplitScratch& S) {
@@ -2478,7 +2528,11 @@ int split_grow(sdmm_stree* t, int64_t need, int keep, int64_t live, hipStream_t 
         S = split_layout(t->split_mem, t->split_cap);
         return SDMM_OK;
     }
-    const int64_t nc = need + need / 4 + 4096;
+    // SDMM_SPLIT_TIGHT=1 (a test knob): no headroom, so that duplicates on
+    // split planes take the regrowth path below (tests/test_stree.py)
+    const char* tight = std::getenv("SDMM_SPLIT_TIGHT");
+    const int64_t nc = (tight && std::strcmp(tight, "1") == 0) ? need : need + need / 4 + 4096;
+    if (nc > kSplitLevelMax) return fail(SDMM_E_INVALID, "device split: a level exceeds 2^30 samples");
     void* nm = nullptr;
     HIP_TRY(hipMalloc(&nm, split_mem_bytes(nc)));
     DevSplitScratch N = split_layout(nm, nc);
@@ -2491,7 +2545,7 @@ int split_grow(sdmm_stree* t, int64_t need, int keep, int64_t live, hipStream_t 
                                hipMemcpyDeviceToDevice, st));
     }
     HIP_TRY(hipStreamSynchronize(st));
-    if (t->split_mem) HIP_TRY(hipFree(t->split_mem));
+    release_dev(t->split_mem);
     t->split_mem = nm;
     t->split_cap = nc;
     S = N;
@@ -2500,7 +2554,7 @@ int split_grow(sdmm_stree* t, int64_t need, int keep, int64_t live, hipStream_t 
 
 int split_small(sdmm_stree* t, size_t need) {
     if (need <= t->split_small_cap && t->split_small) return SDMM_OK;
-    if (t->split_small) HIP_TRY(hipFree(t->split_small));
+    release_dev(t->split_small);
     t->split_small = nullptr;
     t->split_small_cap = 0;
     const size_t cap = need + need / 2 + 4096;
@@ -2819,7 +2873,7 @@ int sdmm_stree_route(sdmm_stree* t, const sdmm_samples* in, const sdmm_samples* 
     const size_t need = 4 * kb + sb + tb + 256;
     if (need > t->scratch_bytes) {
         HIP_TRY(hipStreamSynchronize(t->stream));
-        if (t->scratch) HIP_TRY(hipFree(t->scratch));
+        release_dev(t->scratch);
         t->scratch = nullptr;
         HIP_TRY(hipMalloc(&t->scratch, need));
         t->scratch_bytes = need;
@@ -2897,7 +2951,7 @@ int st_upload_table(sdmm_stree* t, const sdmm_mix* const* node_mix) {
     const size_t nb = nn ? nn : 1;
     const size_t bytes = (sizeof(GuideMixHost) + sizeof(const float*)) * nb;
     if (bytes > t->dtab_cap) {
-        if (t->dtab) HIP_TRY(hipFree(t->dtab));
+        release_dev(t->dtab);
         t->dtab = nullptr;
         HIP_TRY(hipMalloc(&t->dtab, bytes));
         t->dtab_cap = bytes;
@@ -2974,7 +3028,8 @@ int st_guide_product(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq,
     HIP_TRY(launch_guide_product_tree(t->dnodes, t->dtab, t->dcctab, t->tab_kmax, nq, c, u, choice, dgiven, d, pdf,
                                       comp, node_out, material, frame, heuristic, bsdf->weights, bsdf->means,
                                       bsdf->covs, bsdf->diffuse, bsdf->B, bsdf->M, norm_const(2), norm_const(3),
-                                      t->tab_cap, t->guide_fb, t->guide_fb + 1, cus, t->stream, sort));
+                                      t->tab_cap, t->guide_fb, t->guide_fb + 1, cus, t->stream, sort,
+                                      &t->product_scratch));
     return SDMM_OK;
 }
 
@@ -3113,7 +3168,7 @@ int sdmm_detail::push_training_ex(sdmm_stree* t, const sdmm_path_vertices* v, in
     const size_t need0 = 2 * cb + tb + al(sizeof(int64_t) * (size_t)(nn + 2)) + 256;
     if (need0 > t->scratch_bytes) {
         HIP_TRY(hipStreamSynchronize(t->stream));
-        if (t->scratch) HIP_TRY(hipFree(t->scratch));
+        release_dev(t->scratch);
         t->scratch = nullptr;
         HIP_TRY(hipMalloc(&t->scratch, need0));
         t->scratch_bytes = need0;
@@ -3154,7 +3209,7 @@ int sdmm_detail::push_training_ex(sdmm_stree* t, const sdmm_path_vertices* v, in
         HIP_TRY(hipMalloc(&nb, need));
         HIP_TRY(hipMemcpyAsync(nb, t->scratch, 2 * cb, hipMemcpyDeviceToDevice, t->stream));
         HIP_TRY(hipStreamSynchronize(t->stream));
-        HIP_TRY(hipFree(t->scratch));
+        release_dev(t->scratch);
         t->scratch = nb;
         t->scratch_bytes = need;
     }

@@ -151,6 +151,14 @@ struct GuideSortScratch {
     size_t temp_bytes;
 };
 
+// grow-only scratch of the product wavefronts (guide.hip): the thread path's
+// per-query pair cache and the full-K wave kernel's per-workgroup pair slices;
+// owned by the mixture / tree handle, released with it
+struct ProductScratch {
+    float* base;
+    size_t bytes;
+};
+
 // ---- spatial tree node (stree.hip, guide.hip) ------------------------------
 // min[3], max[3], child0, child1 (-1 for a leaf).
 // device split of the spatial tree (stree.hip, sdmm_stree_split_leaf_recurse_device)

@@ -144,6 +144,11 @@ def test_create_many_failure_cleanup(pkg, gpu, monkeypatch, fail_at):
     out = (C.c_void_p * 5)()
     monkeypatch.setenv("SDMM_TEST_FAIL_MEMBER", str(fail_at))
     rc = lib.sdmm_create_many_on_stream(16, None, gpu.index, C.c_void_p(st.cuda_stream), 5, out)
+    assert rc == 0, "the injection must need the explicit debug switch"
+    for v in out:
+        lib.sdmm_destroy(C.c_void_p(v))
+    monkeypatch.setenv("SDMM_DEBUG_FAULT_INJECTION", "1")
+    rc = lib.sdmm_create_many_on_stream(16, None, gpu.index, C.c_void_p(st.cuda_stream), 5, out)
     assert rc != 0
     assert all(v is None for v in out), "failed creation left handles behind"
     monkeypatch.delenv("SDMM_TEST_FAIL_MEMBER")

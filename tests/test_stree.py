@@ -198,14 +198,20 @@ def test_device_find_backtracks(pkg, oracle, gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,threshold,grid", [(400000, 2000, 0), (120000, 3000, 64), (60000, 500, 0)])
-def test_device_split_equals_host_split(pkg, oracle, synth, gpu, n, threshold, grid):
+@pytest.mark.parametrize("n,threshold,grid,tight", [(400000, 2000, 0, False), (120000, 3000, 64, False),
+                                                    (60000, 500, 0, False), (120000, 3000, 64, True),
+                                                    (60000, 800, 16, True)])
+def test_device_split_equals_host_split(pkg, oracle, synth, gpu, monkeypatch, n, threshold, grid, tight):
     """sdmm_stree_split_leaf_recurse_device (the split on device-resident
     positions, level by level) builds node arrays IDENTICAL to the host
     split_leaf_recurse_many and to the oracle's recursion, for several leaves
     at once; grid > 0 snaps the points to a lattice so many lie exactly on
-    split planes (they go to both children)."""
+    split planes (they go to both children).  tight: SDMM_SPLIT_TIGHT=1
+    sizes the level scratch without headroom, so the duplicated plane samples
+    take the regrowth branch (split_grow re-layout)."""
     import torch
+    if tight:
+        monkeypatch.setenv("SDMM_SPLIT_TIGHT", "1")
     b, p = _points(synth, n)
     if grid:
         p = np.floor(p * grid) / grid
