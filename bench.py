@@ -232,7 +232,7 @@ def wavefront_bench(pkg, synth, batch, shard, tree, dev, stream, ct, ut, gout, t
             "guided_frac": float((comp >= 0).mean()), "scaling": "weak (replicas: queries per rank)"}
 
 
-def cornell_cpu_baseline(pkg, g, desc, spp, seed, threads, learned=None, budget_s=6.0):
+def cornell_cpu_baseline(pkg, g, desc, spp, seed, threads, learned=None, budget_s=6.0, probe_px=512):
     """The CPU restatement of Li (oracle/sdmm_oracle_li.inc) rendering the same
     guided pass (the trained model's leaves as oracle mixtures, the same tree,
     seed and spp) over a bounded slice of the image on `threads` host threads:
@@ -255,9 +255,9 @@ def cornell_cpu_baseline(pkg, g, desc, spp, seed, threads, learned=None, budget_
     npix = desc["width"] * desc["height"]
     kw = dict(node_mix=mixes, guided=True, spp=spp, seed=seed, learned=learned, threads=threads)
     t = time.perf_counter()
-    r = orc.li_render(desc, aabb, child, pixels=(0, 512), **kw)          # probe
+    r = orc.li_render(desc, aabb, child, pixels=(0, probe_px), **kw)     # probe
     dt = time.perf_counter() - t
-    n = int(min(npix, max(512, 512 * budget_s / max(dt, 1e-3))))
+    n = int(min(npix, max(probe_px, probe_px * budget_s / max(dt, 1e-3))))
     t = time.perf_counter()
     r = orc.li_render(desc, aabb, child, pixels=(0, n), **kw)
     dt = time.perf_counter() - t
@@ -270,7 +270,8 @@ def cornell_cpu_baseline(pkg, g, desc, spp, seed, threads, learned=None, budget_
             "seconds": dt}
 
 
-def cornell_bench(pkg, dev, args, world, optimize_async=0, K=16, product=False, cpu=False):
+def cornell_bench(pkg, dev, args, world, optimize_async=0, K=16, product=False, cpu=False, cpu_probe_px=512,
+                  cpu_budget_s=6.0):
     """configs[0] on the device: the test suite's Cornell Box (640x360), K=16
     per leaf (K=128: the Torus line's K, configs[2], over the one scene whose
     geometry the snapshot holds), 64 spp rendered 8 spp per iteration, training (push + optimize)
@@ -321,7 +322,7 @@ def cornell_bench(pkg, dev, args, world, optimize_async=0, K=16, product=False, 
     if cpu:
         try:
             res["cpu_baseline"] = cornell_cpu_baseline(pkg, g, desc, spp_it, 1 + len(its) - 1, host_threads(),
-                                                       learned)
+                                                       learned, budget_s=cpu_budget_s, probe_px=cpu_probe_px)
         except Exception as e:  # reported, never required
             res["cpu_baseline"] = {"value": None, "error": repr(e)}
     return res
@@ -626,9 +627,12 @@ def main():
         # configs[4] as a full guided render: K=512 leaves (the Kitchen's K) with
         # sampleProduct, over the Cornell Box (the Kitchen meshes are LFS
         # pointers; the device Li's BSDFs are diffuse, so the learned lobes are
-        # the diffuse slice rule's).  No CPU baseline: the CPU Li at K=512 x
-        # product runs minutes for a useful sample.
-        out["cornell_k512_product"] = cornell_bench(pkg, dev, args, world, K=512, product=True)
+        # the diffuse slice rule's).  CPU baseline on a bounded pixel slice (a
+        # 16-pixel probe sizes a ~10 s sample: the CPU Li at K=512 x product is
+        # slow per path)
+        cpu = rank == 0 and world == 1 and not args.no_cpu
+        out["cornell_k512_product"] = cornell_bench(pkg, dev, args, world, K=512, product=True, cpu=cpu,
+                                                    cpu_probe_px=16, cpu_budget_s=10.0)
 
     if rank == 0 and world == 1 and not args.no_cpu:
         try:

@@ -546,19 +546,27 @@ __device__ __forceinline__ void mstep_body(int K, int Kp, const double* __restri
     extern __shared__ double newW[];
     int* setk = (int*)(newW + K);
     const int t = threadIdx.x;
+// SDMM_MSTEP_STOP=n (diagnostic builds, tools/build_variant.sh): return after
+// phase n, for a phase breakdown by subtraction (not results)
+#ifndef SDMM_MSTEP_STOP
+#define SDMM_MSTEP_STOP 99
+#endif
     if (t == 0) mstep_scalars(stats, nSamples, K, S, sh);
     __syncthreads();
-    if (sh[0] == 0.0) return;  // optimize() returns early when weightSum == 0
+    if (sh[0] == 0.0 || SDMM_MSTEP_STOP <= 1) return;  // optimize() returns early when weightSum == 0
     for (int k = t; k < K; k += blockDim.x) mstep_component(k, K, stats, C, S, sh, newW, setk, wmean, wcov);
     __syncthreads();
+    if (SDMM_MSTEP_STOP <= 2) return;
     for (int k = t; k < K; k += blockDim.x)
         if (setk[k]) set_component(k, wmean + 6 * k, wcov + 25 * k, C);
     __syncthreads();
+    if (SDMM_MSTEP_STOP <= 3) return;
     // dynamic LDS: newW (8K bytes), setk (4K) -- reused as wl --, cl (4K)
     float* wl = (float*)setk;
     float* cl = wl + K;
     if (t < 64) mstep_finish_wave(K, S, newW, wl, cl, t);
     __syncthreads();
+    if (SDMM_MSTEP_STOP <= 4) return;
     for (int k = t; k < K; k += blockDim.x) {
         C.weights[k] = wl[k];
         C.cdf[k] = cl[k];

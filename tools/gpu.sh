@@ -4,7 +4,7 @@
 # Honours gpurun's "retry in Ns" back-off hint.
 # Usage: tools/gpu.sh TIMEOUT 'command'
 T=$1; shift
-for attempt in 1 2 3 4 5 6 7 8; do
+for attempt in $(seq 1 ${GPU_ATTEMPTS:-8}); do
   rm -f gpurun_out/.last_call.json
   /usr/local/graft/bin/gpurun --timeout "$T" -- "$@" > /tmp/gpurun_last.out 2>&1
   rc=$?
