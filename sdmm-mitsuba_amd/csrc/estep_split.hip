@@ -291,24 +291,44 @@ __device__ __forceinline__ void pdf_quad(const f4& C, const f4& AD, const f4& BD
 
 }  // namespace
 
+// SDMM_SPLIT_LDSROWS (K = 128): each block's unnormalised pdfs go to the
+// wave's LDS row stage as soon as they are formed (whole rows, 8 KB per wave)
+// instead of living in 32 VGPRs until the tile's normaliser is known; the
+// flush scales them on the way out.  The freed registers allow 3 waves per
+// SIMD (12-wave workgroups: 96 KB of stage + the 64 KB coefficient image fill
+// the 160 KB LDS, so detInv pi is then read from the E-step record instead).
+#ifdef SDMM_SPLIT_LDSROWS
+constexpr bool kLdsRowsOn = true;
+#else
+constexpr bool kLdsRowsOn = false;
+#endif
+
 template <int R, int WPB, int OCC>
 __global__ void __launch_bounds__(64 * WPB, OCC)
 estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, int64_t n, int64_t nwaves,
                         float* __restrict__ resp) {
+    constexpr bool LR = kLdsRowsOn && R == 8;
+    constexpr bool DIMG = !LR || (WPB * 16 * 32 * 16 + R * 8 * 64 * 16 + R * 4 * 16 <= 163840);
     // coefficient fragments (R blocks x 8 forms x 64 lanes) and detInv pi of
     // components 16 r + 4 g .. +3 (the D rows of lane group g)
-    __shared__ u4 cimg[R * 8 * 64];
-    __shared__ f4 dimg[R * 4];
-    __shared__ f4 stage[WPB][16 * 16];   // per wave: 16 rows x 256 B (half rows of the store)
-    __shared__ float borig[R][4];
-    if (threadIdx.x < R) block_origin(ep, Kp, threadIdx.x, borig[threadIdx.x]);
+    // one LDS block carved into the coefficient image, the per-wave row
+    // stages (16 rows x 512 B with LR, else 256-B half rows), detInv pi and
+    // the block origins (only the parts the configuration uses)
+    constexpr int NC = R * 8 * 64, NS = LR ? 16 * 32 : 16 * 16, ND = DIMG ? R * 4 : 0, NB = kBlockOrigin ? R : 0;
+    __shared__ u4 smem[NC + WPB * NS + ND + NB];
+    u4* const cimg = smem;
+    f4* const stage0 = (f4*)(smem + NC);
+    f4* const dimg = (f4*)(smem + NC + WPB * NS);
+    float (*const borig)[4] = (float (*)[4])(smem + NC + WPB * NS + ND);
+    if (kBlockOrigin && threadIdx.x < R) block_origin(ep, Kp, threadIdx.x, borig[threadIdx.x]);
     __syncthreads();
     for (int idx = threadIdx.x; idx < R * 8 * 64; idx += 64 * WPB)
-        cimg[idx] = coef_frag(ep, Kp, idx >> 9, (idx >> 6) & 7, idx & 63, borig[idx >> 9]);
-    for (int i = threadIdx.x; i < R * 4; i += 64 * WPB) {
-        const float* d = ep + EP_DIPI * Kp + 4 * i;
-        dimg[i] = f4{d[0], d[1], d[2], d[3]};
-    }
+        cimg[idx] = coef_frag(ep, Kp, idx >> 9, (idx >> 6) & 7, idx & 63, borig[kBlockOrigin ? idx >> 9 : 0]);
+    if constexpr (DIMG)
+        for (int i = threadIdx.x; i < R * 4; i += 64 * WPB) {
+            const float* d = ep + EP_DIPI * Kp + 4 * i;
+            dimg[i] = f4{d[0], d[1], d[2], d[3]};
+        }
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
@@ -366,7 +386,10 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
     auto frags = [&](int r, bf8 (&F)[8], f4& dp) __attribute__((always_inline)) {
 #pragma unroll
         for (int f = 0; f < 8; ++f) F[f] = __builtin_bit_cast(bf8, cimg[(r * 8 + f) * 64 + lane]);
-        dp = dimg[r * 4 + g];
+        if constexpr (DIMG)
+            dp = dimg[r * 4 + g];
+        else
+            dp = *(const f4*)(ep + EP_DIPI * Kp + 16 * r + 4 * g);
     };
     auto forms = [&](const bf8 (&F)[8], bf8 bs, bf8 bd, f4 (&D)[8]) __attribute__((always_inline)) {
         const f4 z = f4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -379,13 +402,43 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
     // were issued before pending stores is a wait for those stores (the
     // compiler emits vmcnt(0) on mixed pending events).  In this order the
     // wait for tile t + 1's loads only covers stores issued a tile earlier.
-    float pdf[R][4];
+    float pdf[LR ? 1 : R][4];
+    f4* const st = stage0 + wid * NS;
     float gsc_p = 0.0f;
     bool full_p = false;
     int64_t tp = -1;
     auto flush = [&]() __attribute__((always_inline)) {
         if (tp < 0) return;
         float* row = resp + (tp + col) * (int64_t)K + 4 * g;
+        if constexpr (LR) {
+            if (full_p) {
+                // whole unnormalised rows in the stage: lane (g, col) scales and
+                // stores 16-B chunk 16 h + col of rows g + 4 i (four contiguous
+                // 256-B half rows per store instruction)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int rw = g + 4 * i;
+                    const float sc = __shfl(gsc_p, rw);   // row rw's normaliser (lane rw holds it)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int ch = 16 * h + col;
+                        const f4 v = st[rw * 32 + (ch ^ rw)];
+                        __builtin_nontemporal_store(v * sc, (f4*)(resp + (tp + rw) * (int64_t)K + 4 * ch));
+                    }
+                }
+            } else if (tp + col < s1) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const f4 v = st[col * 32 + ((4 * r + g) ^ col)];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float o = gsc_p != 0.0f ? v[j] * gsc_p : 0.0f;
+                        if (16 * r + 4 * g + j < K) __builtin_nontemporal_store(o, row + 16 * r + j);
+                    }
+                }
+            }
+            return;
+        }
         if (full_p && R != 8) {
             // one 16-B store per block: a sample's 64-B row segment per 4 lanes
 #pragma unroll
@@ -401,7 +454,6 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
             // whole lines); staged, every store writes four contiguous 256-B
             // half rows.  16-B chunk c of row i sits at chunk c ^ i (conflict-
             // free writes and reads).
-            f4* st = stage[wid];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -466,10 +518,14 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
 #else
             pdf_quad<RARE>(D[0], D[1], D[2], D[3], D[4], D[5], D[6], D[7], dp, p);
 #endif
-            pdf[r][0] = p[0].x;
-            pdf[r][1] = p[0].y;
-            pdf[r][2] = p[1].x;
-            pdf[r][3] = p[1].y;
+            if constexpr (LR) {
+                st[col * 32 + ((4 * r + g) ^ col)] = f4{p[0].x, p[0].y, p[1].x, p[1].y};   // row col, chunk 4 r + g
+            } else {
+                pdf[r][0] = p[0].x;
+                pdf[r][1] = p[0].y;
+                pdf[r][2] = p[1].x;
+                pdf[r][3] = p[1].y;
+            }
             acc = padd(acc, padd(p[0], p[1]));
         };
 #if defined(SDMM_SPLIT_DIAG_STOREONLY)
@@ -524,9 +580,15 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
                 f4 D[8];
                 forms(F[r & 1], BS[r & 1], Bd, D);
                 __builtin_amdgcn_sched_barrier(0);
+#ifndef SDMM_SPLIT_NOPREFETCH
                 if (r + 1 < R) frags(r + 1, F[(r + 1) & 1], dp[(r + 1) & 1]);
                 __builtin_amdgcn_sched_barrier(0);
+#endif
                 pair_math(r, Tag<false>{}, D, dp[r & 1]);
+#ifdef SDMM_SPLIT_NOPREFETCH
+                // (3 waves per SIMD: the other waves cover the fragment reads)
+                if (r + 1 < R) frags(r + 1, F[(r + 1) & 1], dp[(r + 1) & 1]);
+#endif
                 // the next block's spatial sample fragment, off the MFMA issue path
                 if (r + 1 < R) BS[(r + 1) & 1] = kBlockOrigin ? pfrag(P3, borig[r + 1]) : Bs0;
                 __builtin_amdgcn_sched_barrier(0);
