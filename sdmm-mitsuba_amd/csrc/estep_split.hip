@@ -334,13 +334,15 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t wave = (int64_t)blockIdx.x * WPB + wid;
-    // the launch's 16-sample tiles spread evenly over its waves (one round of
-    // resident waves: each workgroup builds the coefficient image once)
-    const int64_t tiles = (n + 15) / 16;
-    const int64_t s0 = 16 * (wave * tiles / nwaves);
+    // the launch's 16-sample tiles dealt round robin over its waves (one round
+    // of resident waves: each workgroup builds the coefficient image once):
+    // wave w serves tiles w, w + nwaves, ..., so the waves running at one time
+    // write neighbouring 8-KB row blocks.  (A contiguous range per wave put the
+    // 2048 waves' concurrent rows 256 KB apart -- the same HBM channel bits --
+    // and one configuration ran 170-190 or 340-370 us per launch depending on
+    // where the output buffer landed.)
+    const int64_t s0 = 16 * wave, step = 16 * nwaves, s1 = n;
     if (wave >= nwaves || s0 >= n) return;
-    int64_t s1 = 16 * ((wave + 1) * tiles / nwaves);
-    s1 = (s1 < n) ? s1 : n;
 
     // MFMA D[component][sample] = A[component][k] . B[k][sample]: A = the
     // coefficient fragment (lane: component 16 r + (lane & 15), k group
@@ -484,7 +486,7 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
     };
 
     Feat nf = load_feat(s0);
-    for (int64_t t = s0; t < s1; t += 16) {
+    for (int64_t t = s0; t < s1; t += step) {
         const Feat cf = nf;
         float P3[3], D3[3];
         gather3(cf.p, P3);
@@ -499,7 +501,7 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
         __builtin_amdgcn_sched_barrier(0);
         flush();                          // tile t - 16's rows
         __builtin_amdgcn_sched_barrier(0);
-        nf = load_feat(t + 16);           // next tile in flight (clamped past the end)
+        nf = load_feat(t + step);         // next tile in flight (clamped past the end)
         __builtin_amdgcn_sched_barrier(0);
 
         f2 acc = f2{0.0f, 0.0f};
@@ -539,6 +541,42 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
                 pdf[r][j] = P3[j & 1] + D3[j >> 1] + (float)(16 * r + j);
                 acc.x += pdf[r][j];
             }
+#elif defined(SDMM_SPLIT_PAIR2)
+        {
+            // two blocks per step: their 16 MFMAs back to back, then both
+            // blocks' pair math with no fence between them, so the scheduler
+            // interleaves four independent packed chains (the pair math is
+            // dependency-bound at two); the next pair's fragments are read
+            // from LDS meanwhile
+          if constexpr (R % 2 != 0) {
+            bf8 F[8];
+            f4 dp, D[8];
+            frags(0, F, dp);
+            forms(F, Bs0, Bd, D);
+            pair_math(0, Tag<false>{}, D, dp);
+          } else {
+            bf8 F[2][8], G[2][8];
+            f4 dp[2], dq[2];
+            frags(0, F[0], dp[0]);
+            frags(1, G[0], dq[0]);
+#pragma unroll
+            for (int r = 0; r < R; r += 2) {
+                const int b = (r >> 1) & 1;
+                f4 D0[8], D1[8];
+                forms(F[b], Bs0, Bd, D0);
+                forms(G[b], Bs0, Bd, D1);
+                __builtin_amdgcn_sched_barrier(0);
+                if (r + 2 < R) {
+                    frags(r + 2, F[b ^ 1], dp[b ^ 1]);
+                    frags(r + 3, G[b ^ 1], dq[b ^ 1]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                pair_math(r, Tag<false>{}, D0, dp[b]);
+                pair_math(r + 1, Tag<false>{}, D1, dq[b]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+        }
 #elif defined(SDMM_SPLIT_PIPE)
         {
             // software-pipelined over the blocks: block r + 1's eight MFMAs are

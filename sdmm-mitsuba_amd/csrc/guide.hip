@@ -407,12 +407,6 @@ __device__ __forceinline__ int build_candidates(const float* gp, int Kp, int K, 
 // the ripple's fixed LCAP-step cost and its registers outweigh the LDS
 // shifts) 466 -> 489 us and 618 -> 692 us -- so only the tree kernel's
 // LCAP = 40 instance uses it.
-#ifdef SDMM_GUIDE_TWOPASS
-constexpr bool kGuideTwoPass = true;
-#else
-constexpr bool kGuideTwoPass = false;
-#endif
-
 template <int LCAP>
 __device__ __forceinline__ int build_candidates_reg(const float* gp, int Kp, int K, const float c[3], float* cw,
                                                     unsigned short* ck, int T, int tid, float norm3, int cap,
@@ -424,34 +418,13 @@ __device__ __forceinline__ int build_candidates_reg(const float* gp, int Kp, int
     float total = 0.0f;
     int cnt = 0;
     const float skip_f = 0.0089f / (float)K;
-    // SDMM_GUIDE_TWOPASS: a first pass forms totalMass alone, so the list
-    // pass can filter with the final tau (only candidates ripple through the
-    // list, not every live weight that passes the running bound); the second
-    // pass re-forms the same weights (same expression, same bits)
-    double tau2 = 0.0;
-    if constexpr (kGuideTwoPass) {
-        MargRec nx = load_marg(gp, 0);
-        for (int k = 0; k < K; ++k) {
-            const MargRec rec = nx;
-            if (k + 1 < K) nx = load_marg(gp, k + 1);
-            total += marginal_weight_rec(rec, c, norm3);
-        }
-        if (!__builtin_isfinite(total)) return -1;
-        const float cut2 = (float)(0.99 * (double)total);
-        tau2 = ((double)total - (double)cut2) / (double)K * 0.999;
-        if (!(tau2 > 0.0)) return -1;
-    }
     MargRec nx = load_marg(gp, 0);
     for (int k = 0; k < K; ++k) {
         const MargRec rec = nx;
         if (k + 1 < K) nx = load_marg(gp, k + 1);
         const float w = marginal_weight_rec(rec, c, norm3);
-        if constexpr (kGuideTwoPass) {
-            if (!((double)w >= tau2)) continue;
-        } else {
-            total += w;
-            if (!(w > 0.0f) || w < total * skip_f) continue;
-        }
+        total += w;
+        if (!(w > 0.0f) || w < total * skip_f) continue;
         float x = w;
         int xk = k;
 #pragma unroll

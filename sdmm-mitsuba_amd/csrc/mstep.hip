@@ -357,8 +357,14 @@ __device__ __forceinline__ void mstep_scalars(const double* __restrict__ stats, 
         S.scalars[SC_NORM] = (double)(float)((1.0 - eta) * norm + eta * weightSum / (double)nSamples);
         const int cutoff = (int)S.scalars[SC_CUT];
         const int cut = (cutoff < it) ? cutoff : it;
-        const double invGlobal = 1.0 / pow(3.0, (double)cut);
-        const double invMix = 1.0 / pow(2.0, (double)cut);
+        // 3^cut and 2^cut are exact in fp64 for cut <= 33 (the trainingCutoff
+        // is 32), so the products equal any correctly rounded pow (the
+        // oracle's libm pow); a serial fp64 pow was ~2 us each of the M-step
+        double p3 = 1.0;
+        for (int i = 0; i < cut && cut <= 33; ++i) p3 *= 3.0;
+        if (cut > 33) p3 = pow(3.0, (double)cut);
+        const double invGlobal = 1.0 / p3;
+        const double invMix = 1.0 / ldexp(1.0, cut);
         sh[1] = eta;
         sh[2] = weightSum;
         sh[3] = 1.0 / hTW;
@@ -538,11 +544,76 @@ __device__ __forceinline__ void mstep_finish_wave(int K, const EmStateDev& S, co
     if (lane == 0) S.scalars[SC_IT] = S.scalars[SC_IT] + 1.0;
 }
 
+// The same results as mstep_finish_wave from the whole workgroup: the three
+// order-dependent sums (the fp64 total of newW, the float prefix of the
+// weights -- whose last value is also their float total --, the float prefix
+// of the normalised weights) are each ONE thread's sequential chain over LDS
+// (loads batched ahead of the adds), the elementwise divisions and roundings
+// run on every thread between them.  The readlane chains above took ~16 us of
+// a K = 128 M-step (tools/em_phases.py with SDMM_MSTEP_STOP builds).
+// wl, cl: LDS, K floats each; sh2: 2 doubles of LDS.
+__device__ __forceinline__ void mstep_finish_block(int K, const EmStateDev& S, const double* newW, float* wl,
+                                                   float* cl, double* sh2) {
+    const int t = threadIdx.x;
+    if (t == 0) {
+        double sum = 0.0;
+        int k = 0;
+        for (; k + 8 <= K; k += 8) {
+            double v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = newW[k + i];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) sum += v[i];
+        }
+        for (; k < K; ++k) sum += newW[k];
+        sh2[0] = sum;
+    }
+    __syncthreads();
+    const double sum = sh2[0];
+    for (int k = t; k < K; k += blockDim.x) {
+        double nw = newW[k];
+        if (sum != 0.0) nw = nw / sum;
+        wl[k] = (float)nw;
+    }
+    __syncthreads();
+    // createCdf(false): the unnormalised prefix (kept if the total is 0); its
+    // last value is the float total fs
+    auto prefix = [&]() {
+        float acc = 0.0f;
+        int k = 0;
+        for (; k + 8 <= K; k += 8) {
+            float v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = wl[k + i];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                acc += v[i];
+                cl[k + i] = acc;
+            }
+        }
+        for (; k < K; ++k) {
+            acc += wl[k];
+            cl[k] = acc;
+        }
+        return acc;
+    };
+    if (t == 0) sh2[1] = (double)prefix();
+    __syncthreads();
+    const float fs = (float)sh2[1];
+    if (fs != 0.0f) {
+        for (int k = t; k < K; k += blockDim.x) wl[k] = wl[k] / fs;
+        __syncthreads();
+        if (t == 0) (void)prefix();
+    }
+    if (t == 0) S.scalars[SC_IT] = S.scalars[SC_IT] + 1.0;
+}
+
 // The four phases in one workgroup (the batched per-leaf M-step).
 __device__ __forceinline__ void mstep_body(int K, int Kp, const double* __restrict__ stats, int64_t nSamples,
                                            CanonDev C, EmStateDev S, float* ep, float* gp, float norm5,
                                            double* __restrict__ wmean, double* __restrict__ wcov) {
     __shared__ double sh[8];
+    __shared__ double sh2[2];
     extern __shared__ double newW[];
     int* setk = (int*)(newW + K);
     const int t = threadIdx.x;
@@ -564,7 +635,11 @@ __device__ __forceinline__ void mstep_body(int K, int Kp, const double* __restri
     // dynamic LDS: newW (8K bytes), setk (4K) -- reused as wl --, cl (4K)
     float* wl = (float*)setk;
     float* cl = wl + K;
+#ifdef SDMM_MSTEP_FINISH_WAVE
     if (t < 64) mstep_finish_wave(K, S, newW, wl, cl, t);
+#else
+    mstep_finish_block(K, S, newW, wl, cl, sh2);
+#endif
     __syncthreads();
     if (SDMM_MSTEP_STOP <= 4) return;
     for (int k = t; k < K; k += blockDim.x) {

@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Per-launch times of the responsibility E-step on the bench workload
+(K = 128, N = 2^20, 5 warm EM steps): one event pair per launch, so a
+bimodal / drifting kernel shows up (SDMM_RESP_KERNEL / SDMM_RESP_VARIANT /
+SDMM_LIB_PATH select the build and configuration)."""
+import importlib
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+
+
+def main():
+    import torch
+    from conftest import load_pkg
+    pkg = load_pkg()
+    synth = importlib.import_module("sdmm_mitsuba_amd.synth")
+    dev = torch.device("cuda:0")
+    K, N = 128, 1 << 20
+    b = synth.em_batch(N, 128)
+    pos, nrm = synth.model_seed_points(b, K)
+    mix = pkg.SDMM(K)
+    mix.init_hemisphere(pos, nrm, synth.DEPTH_PRIOR, synth.SPATIAL_DISTANCE, synth.SEED_MODEL)
+    ds = pkg.DeviceSamples.from_numpy(b["x"], b["w"], b["hpdf"], b["is_diffuse"], device=dev)
+    for _ in range(5):
+        mix.optimize(ds)
+    resp = torch.empty((N, K), device=dev)
+    ts = []
+    for i in range(40):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        mix.posterior(ds, resp)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(round(e0.elapsed_time(e1) * 1000, 1))
+    r = resp[::4096].cpu().numpy()
+    print(json.dumps({"kernel": mix.kernel_name("resp"), "us": ts, "finite": bool(torch.isfinite(resp).all()),
+                      "rowsum_dev_max": float(abs(r.sum(1) - 1).max())}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
