@@ -291,13 +291,15 @@ __device__ __forceinline__ void pdf_quad(const f4& C, const f4& AD, const f4& BD
 
 }  // namespace
 
-// SDMM_SPLIT_LDSROWS (K = 128): each block's unnormalised pdfs go to the
+// LDS rows (K = 128): each block's unnormalised pdfs go to the
 // wave's LDS row stage as soon as they are formed (whole rows, 8 KB per wave)
 // instead of living in 32 VGPRs until the tile's normaliser is known; the
 // flush scales them on the way out.  The freed registers allow 3 waves per
 // SIMD (12-wave workgroups: 96 KB of stage + the 64 KB coefficient image fill
 // the 160 KB LDS, so detInv pi is then read from the E-step record instead).
-#ifdef SDMM_SPLIT_LDSROWS
+// (the default since round 4; SDMM_SPLIT_REGROWS: the pdfs in registers
+// until the flush, as in round 3)
+#ifndef SDMM_SPLIT_REGROWS
 constexpr bool kLdsRowsOn = true;
 #else
 constexpr bool kLdsRowsOn = false;
@@ -618,13 +620,15 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
                 f4 D[8];
                 forms(F[r & 1], BS[r & 1], Bd, D);
                 __builtin_amdgcn_sched_barrier(0);
-#ifndef SDMM_SPLIT_NOPREFETCH
+#ifdef SDMM_SPLIT_PREFETCH
+                // (A/B: block r + 1's fragments read while block r's pair math runs)
                 if (r + 1 < R) frags(r + 1, F[(r + 1) & 1], dp[(r + 1) & 1]);
                 __builtin_amdgcn_sched_barrier(0);
 #endif
                 pair_math(r, Tag<false>{}, D, dp[r & 1]);
-#ifdef SDMM_SPLIT_NOPREFETCH
-                // (3 waves per SIMD: the other waves cover the fragment reads)
+#ifndef SDMM_SPLIT_PREFETCH
+                // fragments read after the pair math (32 VGPRs fewer: 3 waves
+                // per SIMD fit, and the other waves cover the reads)
                 if (r + 1 < R) frags(r + 1, F[(r + 1) & 1], dp[(r + 1) & 1]);
 #endif
                 // the next block's spatial sample fragment, off the MFMA issue path
@@ -678,17 +682,21 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
 // The B image takes R x 8 KB of LDS per workgroup.
 #define SDMM_SPLIT_CONFIGS(X) X(1, 4, 4) X(2, 4, 4) X(4, 4, 4) X(8, 4, 2) X(8, 8, 2) X(8, 12, 3)
 
-// R = 8 (K = 128): variant 0 = one 8-wave workgroup per CU at 2 waves per
-// SIMD (256 VGPRs: double-buffered fragments, no spill; 189 us at N = 2^20),
-// 1 = two 4-wave workgroups, 2 = 12 waves at 3 per SIMD (168 VGPRs, spills;
-// 199 us)
+// R = 8 (K = 128): variants 0 and 2 = one 12-wave workgroup per CU at 3 waves
+// per SIMD (the 96-KB row stage + the 64-KB coefficient image fill the LDS),
+// 1 = two 4-wave workgroups at 2 per SIMD, 3 = one 8-wave workgroup at 2 per
+// SIMD (round 3's default)
 static void split_cfg(int R, int variant, int* wpb, int* occ) {
     *wpb = 4;
     *occ = 4;
     if (R == 8) {
-        *wpb = 8; *occ = 2;
+        // default: 12-wave workgroups at 3 waves per SIMD (LDS rows, 153
+        // VGPRs; round 4: median 176 us per launch against 186-189 us for the
+        // round-3 configuration, variant 3, which also ran 340-370 us in some
+        // processes -- see DESIGN.md section 4)
+        *wpb = 12; *occ = 3;
         if (variant == 1) { *wpb = 4; *occ = 2; }
-        if (variant == 2) { *wpb = 12; *occ = 3; }
+        if (variant == 3) { *wpb = 8; *occ = 2; }
     }
 }
 
