@@ -324,8 +324,11 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
     float (*const borig)[4] = (float (*)[4])(smem + NC + WPB * NS + ND);
     if (kBlockOrigin && threadIdx.x < R) block_origin(ep, Kp, threadIdx.x, borig[threadIdx.x]);
     __syncthreads();
+    // (without per-block origins every block's spatial forms use the one
+    // scene-centre origin kOrigin; borig then has no storage)
+    const float o_scene[3] = {kOrigin, kOrigin, kOrigin};
     for (int idx = threadIdx.x; idx < R * 8 * 64; idx += 64 * WPB)
-        cimg[idx] = coef_frag(ep, Kp, idx >> 9, (idx >> 6) & 7, idx & 63, borig[kBlockOrigin ? idx >> 9 : 0]);
+        cimg[idx] = coef_frag(ep, Kp, idx >> 9, (idx >> 6) & 7, idx & 63, kBlockOrigin ? borig[idx >> 9] : o_scene);
     if constexpr (DIMG)
         for (int i = threadIdx.x; i < R * 4; i += 64 * WPB) {
             const float* d = ep + EP_DIPI * Kp + 4 * i;
@@ -620,17 +623,29 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
                 f4 D[8];
                 forms(F[r & 1], BS[r & 1], Bd, D);
                 __builtin_amdgcn_sched_barrier(0);
-#ifdef SDMM_SPLIT_PREFETCH
-                // (A/B: block r + 1's fragments read while block r's pair math runs)
-                if (r + 1 < R) frags(r + 1, F[(r + 1) & 1], dp[(r + 1) & 1]);
-                __builtin_amdgcn_sched_barrier(0);
-#endif
-                pair_math(r, Tag<false>{}, D, dp[r & 1]);
 #ifndef SDMM_SPLIT_PREFETCH
-                // fragments read after the pair math (32 VGPRs fewer: 3 waves
-                // per SIMD fit, and the other waves cover the reads)
-                if (r + 1 < R) frags(r + 1, F[(r + 1) & 1], dp[(r + 1) & 1]);
+#define SDMM_SPLIT_PREFETCH 0
 #endif
+                // SDMM_SPLIT_PREFETCH = n (A/B): block r + 1's first n fragments
+                // are read while block r's pair math runs, the rest after it
+                // (default 0: 32 VGPRs fewer, 3 waves per SIMD fit, and the
+                // other waves cover the reads)
+                if (r + 1 < R && SDMM_SPLIT_PREFETCH > 0) {
+#pragma unroll
+                    for (int f = 0; f < SDMM_SPLIT_PREFETCH; ++f)
+                        F[(r + 1) & 1][f] = __builtin_bit_cast(bf8, cimg[((r + 1) * 8 + f) * 64 + lane]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                pair_math(r, Tag<false>{}, D, dp[r & 1]);
+                if (r + 1 < R) {
+#pragma unroll
+                    for (int f = SDMM_SPLIT_PREFETCH; f < 8; ++f)
+                        F[(r + 1) & 1][f] = __builtin_bit_cast(bf8, cimg[((r + 1) * 8 + f) * 64 + lane]);
+                    if constexpr (DIMG)
+                        dp[(r + 1) & 1] = dimg[(r + 1) * 4 + g];
+                    else
+                        dp[(r + 1) & 1] = *(const f4*)(ep + EP_DIPI * Kp + 16 * (r + 1) + 4 * g);
+                }
                 // the next block's spatial sample fragment, off the MFMA issue path
                 if (r + 1 < R) BS[(r + 1) & 1] = kBlockOrigin ? pfrag(P3, borig[r + 1]) : Bs0;
                 __builtin_amdgcn_sched_barrier(0);
