@@ -103,7 +103,7 @@ int sdmm_layout(const sdmm_mix* m, int* resp_cpl, int* resp_lps, int* stats_cpl,
  * (which = 0) or statistics (which = 1) E-step; "" for a NULL handle. */
 const char* sdmm_kernel_name(const sdmm_mix* m, int which);
 /* Guided queries keep a per-query list of at most `cap` candidate components
- * (default and maximum 40); queries that do not fit take the full-K path.
+ * (default 40, maximum 64); queries that do not fit take the full-K path.
  * Results are identical for every cap; 0 sends every query down the full-K
  * path (a testing knob).  A tree wavefront uses the smallest cap of the
  * mixtures bound to it (read when the table is bound / passed). */

@@ -630,7 +630,7 @@ class SDMM:
         _check(lib().sdmm_restore_params(self.h, C.byref(o)))
 
     def set_guide_capacity(self, cap: int):
-        """Per-query candidate-list capacity of the guided-query kernel (0..40)."""
+        """Per-query candidate-list capacity of the guided-query kernel (0..64, default 40)."""
         _check(lib().sdmm_set_guide_capacity(self.h, cap))
 
     def guide_fallback_count(self) -> int:

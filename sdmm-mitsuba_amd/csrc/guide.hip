@@ -311,9 +311,11 @@ __device__ __forceinline__ QueryOut finish_query(const float* gp, int Kp, const 
 // when invalid conditionals zero out kept weights).  With K = 128 the list
 // holds a median of ~10 and a 99th percentile of ~34 entries.
 #ifndef SDMM_GUIDE_CAP_MAX
-#define SDMM_GUIDE_CAP_MAX 40
+#define SDMM_GUIDE_CAP_MAX 64
 #endif
 constexpr int kGuideCap = SDMM_GUIDE_CAP_MAX;
+// lists of at least this capacity are built in registers (build_candidates_reg)
+constexpr int kGuideRegCap = 40;
 
 struct CandSlots {
     const float* cw;
@@ -408,7 +410,7 @@ __device__ __forceinline__ int build_candidates(const float* gp, int Kp, int K, 
 // shifts) 466 -> 489 us and 618 -> 692 us -- so only the tree kernel's
 // LCAP = 40 instance uses it.
 template <int LCAP>
-__device__ __forceinline__ int build_candidates_reg(const float* gp, int Kp, int K, const float c[3], float* cw,
+__device__ __forceinline__ int build_candidates_cas(const float* gp, int Kp, int K, const float c[3], float* cw,
                                                     unsigned short* ck, int T, int tid, float norm3, int cap,
                                                     float& accum) {
     float rw[LCAP];
@@ -462,6 +464,93 @@ __device__ __forceinline__ int build_candidates_reg(const float* gp, int Kp, int
     return (ncand == K) ? K : -1;
 }
 
+// The register list again, with each (weight, index) entry one orderable
+// 64-bit key held as a double: bits 63..32 = the weight's bits + 1 (weights
+// here are positive normal floats, so the pattern is a positive normal double
+// and the doubles order as the keys), bits 31..0 = 2^32 - 1 - index (a larger
+// key comes first: weight desc, index asc -- the selection order; keys are
+// unique).  0 marks an empty slot.  One insertion step is then
+// slot' = max(slot, x), x' = min(slot, x): full-rate f64 operations (three
+// with the compiler's canonicalising max of the loop-carried slot; inline asm
+// saves nothing, the in-place update then costs a move) instead of the
+// compare and four selects of the (weight, index) pair ripple (287 VALU per
+// live weight for LCAP = 40).  The list is walked in chunks of
+// eight slots, and a chunk none of whose slots can change in any lane (x not
+// above its smallest slot: x sorts after it, or nothing left to carry) is
+// skipped on a wave-uniform branch.  The list is the top LCAP live weights
+// seen; a capacity cap < LCAP is its first cap entries (the top cap), so the
+// results are those of the cap-entry list above.
+__device__ __forceinline__ double cand_key(float w, int k) {
+    const uint64_t b = ((uint64_t)(__builtin_bit_cast(uint32_t, w) + 1u) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)k);
+    return __builtin_bit_cast(double, b);
+}
+template <int LCAP>
+__device__ __forceinline__ int build_candidates_key(const float* gp, int Kp, int K, const float c[3], float* cw,
+                                                    unsigned short* ck, int T, int tid, float norm3, int cap,
+                                                    float& accum) {
+    static_assert(LCAP % 8 == 0, "chunks of eight slots");
+    double L[LCAP];
+#pragma unroll
+    for (int i = 0; i < LCAP; ++i) L[i] = 0.0;
+    float total = 0.0f;
+    const float skip_f = 0.0089f / (float)K;
+    MargRec nx = load_marg(gp, 0);
+    for (int k = 0; k < K; ++k) {
+        const MargRec rec = nx;
+        if (k + 1 < K) nx = load_marg(gp, k + 1);
+        const float w = marginal_weight_rec(rec, c, norm3);
+        total += w;
+        if (!(w > 0.0f) || w < total * skip_f) continue;
+        double x = cand_key(w, k);
+#pragma unroll
+        for (int c0 = 0; c0 < LCAP; c0 += 8) {
+            if (!__any(x > L[c0 + 7])) continue;
+#pragma unroll
+            for (int i = c0; i < c0 + 8; ++i) {
+                const double hi = __builtin_fmax(L[i], x);
+                x = __builtin_fmin(L[i], x);
+                L[i] = hi;
+            }
+        }
+    }
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < LCAP; ++i) {
+        const uint64_t b = __builtin_bit_cast(uint64_t, L[i]);
+        if (i < cap && b != 0) {
+            cw[i * T + tid] = __builtin_bit_cast(float, (uint32_t)(b >> 32) - 1u);
+            ck[i * T + tid] = (unsigned short)(0xFFFFFFFFu - (uint32_t)b);
+            cnt = i + 1;
+        }
+    }
+    if (!__builtin_isfinite(total)) return -1;
+    const float cutoff = (float)(0.99 * (double)total);
+    const double tau = ((double)total - (double)cutoff) / (double)K * 0.999;
+    if (!(tau > 0.0)) return -1;
+    int ncand = 0;
+    while (ncand < cnt && (double)cw[ncand * T + tid] >= tau) ++ncand;
+    accum = 0.0f;
+    for (int i = 0; i < ncand; ++i) {
+        const int k = ck[i * T + tid];
+        const bool ok = cond_valid(gp, Kp, k, c);
+        ck[i * T + tid] = (unsigned short)(k | (ok ? 0x8000 : 0));
+        accum += ok ? cw[i * T + tid] : 0.0f;
+        if (accum >= cutoff) return i + 1;
+    }
+    return (ncand == K) ? K : -1;
+}
+
+template <int LCAP>
+__device__ __forceinline__ int build_candidates_reg(const float* gp, int Kp, int K, const float c[3], float* cw,
+                                                    unsigned short* ck, int T, int tid, float norm3, int cap,
+                                                    float& accum) {
+#ifdef SDMM_GUIDE_RIPPLE_CAS
+    return build_candidates_cas<LCAP>(gp, Kp, K, c, cw, ck, T, tid, norm3, cap, accum);
+#else
+    return build_candidates_key<LCAP>(gp, Kp, K, c, cw, ck, T, tid, norm3, cap, accum);
+#endif
+}
+
 // Plane pointers of one guided batch (inputs c, u or given directions e;
 // outputs d, pdf, comp).
 struct GuideIO {
@@ -510,10 +599,10 @@ __device__ __forceinline__ void finish_and_write(const float* gp, int Kp, const 
     }
 }
 
-// Candidate path of query q against one mixture; false: q needs the full-K
+// Candidate path of query q against one mixture; true: q needs the full-K
 // fallback (appended to fb_list).
 template <bool PDF_ONLY, int LCAP, bool REG = false>
-__device__ __forceinline__ void serve_cand(const float* gp, int Kp, int K, const GuideIO& io, int64_t q,
+__device__ __forceinline__ bool serve_cand(const float* gp, int Kp, int K, const GuideIO& io, int64_t q,
                                            const float c[3], float* cw, unsigned short* ck, int tid, int cap,
                                            GuideConsts gc, int* fb_count, int32_t* fb_list) {
     float accum = 0.0f;
@@ -521,9 +610,54 @@ __device__ __forceinline__ void serve_cand(const float* gp, int Kp, int K, const
                             : build_candidates(gp, Kp, K, c, cw, ck, 64, tid, gc.norm3, cap, accum);
     if (lastIdx < 0) {
         fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
-        return;
+        return true;
     }
     finish_and_write<PDF_ONLY>(gp, Kp, c, lastIdx, accum, CandSlots{cw, ck, 64, tid}, io, q, gc);
+    return false;
+}
+
+// Per-node routing of the tree wavefronts.  stats[3 n] counts the queries of
+// node n the candidate kernel served (uniform-leaf waves), stats[3 n + 1] how
+// many of them still needed the full-K path, and stats[3 n + 2] = 1 sends
+// node n's queries straight to the full-K path: guide_route_kernel sets it
+// before each candidate launch once more than two thirds of a node's served
+// queries fell back (routing pays when the fallback fraction p exceeds
+// 1 - c / F, c and F the per-query costs of the candidate and full-K paths:
+// 1.2 / 3.2 ns at K = 128, 10 / 32 ns for the K = 512 product).  A routed
+// query is served by the full-K path, whose result is the candidate path's
+// bit for bit, so routing changes the cost of a query, never its result.  The
+// counts start from zero whenever a different mixture table is bound.
+struct NodeRoute {
+    uint32_t* stats;   // 3 x nodes, or null: no routing
+    int nn;
+};
+constexpr uint32_t kRouteMinQueries = 256;
+__global__ void guide_route_kernel(uint32_t* __restrict__ stats, int nn) {
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= nn) return;
+    uint32_t q = stats[3 * n], f = stats[3 * n + 1];
+    if (q >= (1u << 31)) {   // keep the counts far from wrapping
+        q >>= 1;
+        f >>= 1;
+        stats[3 * n] = q;
+        stats[3 * n + 1] = f;
+    }
+    stats[3 * n + 2] = (q >= kRouteMinQueries && (uint64_t)f * 3 > (uint64_t)q * 2) ? 1u : 0u;
+}
+static hipError_t launch_route(const NodeRoute& rt, hipStream_t st) {
+    if (!rt.stats || rt.nn <= 0) return hipSuccess;
+    hipLaunchKernelGGL(guide_route_kernel, dim3((unsigned)((rt.nn + 255) / 256)), dim3(256), 0, st, rt.stats, rt.nn);
+    return hipGetLastError();
+}
+// a uniform-leaf wave's counts: its queries and those that fell back
+__device__ __forceinline__ void route_count(const NodeRoute& rt, int n, bool fell) {
+    const uint64_t act = __builtin_amdgcn_ballot_w64(true);
+    const uint64_t fb = __builtin_amdgcn_ballot_w64(fell);
+    const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+    if (below == 0) {
+        atomicAdd(&rt.stats[3 * n], (uint32_t)__builtin_popcountll(act));
+        if (fb) atomicAdd(&rt.stats[3 * n + 1], (uint32_t)__builtin_popcountll(fb));
+    }
 }
 
 // LDS list capacity LCAP (24 or 40): the lists are 6 B per entry per thread,
@@ -555,7 +689,7 @@ __global__ void __launch_bounds__(64)
 guide_tree_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __restrict__ tab, int64_t nq,
                        GuideIO io, GuideConsts gc, int cap, int* __restrict__ fb_count,
                        int32_t* __restrict__ fb_list, const int32_t* __restrict__ perm,
-                       int32_t* __restrict__ node_out) {
+                       int32_t* __restrict__ node_out, NodeRoute rt) {
     __shared__ float cw[LCAP * 64];
     __shared__ unsigned short ck[LCAP * 64];
     const int tid = threadIdx.x;
@@ -575,11 +709,15 @@ guide_tree_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __re
         const int n0 = __builtin_amdgcn_readfirstlane(node);
         if (__builtin_amdgcn_ballot_w64(node != n0) == 0) {
             const GuideMix mx = (n0 >= 0) ? tab[n0] : GuideMix{nullptr, 0, 0};
-            if (mx.K <= 0)
+            if (mx.K <= 0) {
                 write_invalid<PDF_ONLY>(io, q);
-            else
-                serve_cand<PDF_ONLY, LCAP, (LCAP >= kGuideCap)>(mx.gp, mx.Kp, mx.K, io, q, c, cw, ck, tid, cap, gc,
-                                                                 fb_count, fb_list);
+            } else if (rt.stats && rt.stats[3 * n0 + 2]) {
+                fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;   // routed: the full-K path serves it
+            } else {
+                const bool fell = serve_cand<PDF_ONLY, LCAP, (LCAP >= kGuideRegCap)>(
+                    mx.gp, mx.Kp, mx.K, io, q, c, cw, ck, tid, cap, gc, fb_count, fb_list);
+                if (rt.stats) route_count(rt, n0, fell);
+            }
             return;
         }
     }
@@ -590,7 +728,7 @@ guide_tree_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __re
         if (mx.K <= 0)
             write_invalid<PDF_ONLY>(io, q);
         else
-            serve_cand<PDF_ONLY, LCAP, (LCAP >= kGuideCap)>(mx.gp, mx.Kp, mx.K, io, q, c, cw, ck, tid, cap, gc,
+            serve_cand<PDF_ONLY, LCAP, (LCAP >= kGuideRegCap)>(mx.gp, mx.Kp, mx.K, io, q, c, cw, ck, tid, cap, gc,
                                                              fb_count, fb_list);
         break;
     }
@@ -1205,22 +1343,233 @@ __device__ __forceinline__ bool serve_full_group(const float* gp, int Kp, int K,
     return true;
 }
 
-// The listed full-K queries, a 16-lane group each (grid-stride over groups);
+// ---------------------------------------------------------------------------
+// The same full-K query on a G-lane group, G = 4 (an A/B option) or 16: lane l
+// of a group holds components l, l + G, ... (S slots, K <= G S).  Same
+// arithmetic and order as serve_full_group (G = 16 reproduces it); with G = 4
+// sixteen queries share every instruction of the serial float chains (four
+// times as many as with 16-lane groups), the broadcasts inside a group are
+// DPP quad permutes (no LDS pipe), and the sort's cross-lane steps are the
+// two quad steps (J = 1, 2) -- the rest of the bitonic network is
+// compare-exchange inside a lane's registers.  The per-slot values stay in
+// registers as keys (weight bits + 1, index) plus a validity bit mask; the
+// slot weights and pdf terms are re-derived from them where consumed.
+template <int G>
+__device__ __forceinline__ float gbcast(float x, int l) {   // lane l of this lane's G-lane group
+    if constexpr (G == 16) {
+        return gbc(x, l);
+    } else {
+        static_assert(G == 4, "groups of 4 or 16 lanes");
+        const int xi = __builtin_bit_cast(int, x);
+        int r;
+        switch (l) {   // quad_perm [l, l, l, l]
+            case 0: r = dppi<0x00>(xi); break;
+            case 1: r = dppi<0x55>(xi); break;
+            case 2: r = dppi<0xAA>(xi); break;
+            default: r = dppi<0xFF>(xi); break;
+        }
+        return __builtin_bit_cast(float, r);
+    }
+}
+// acc += v(i) of this group's elements p = G i + l < n, in p order (n uniform
+// inside a group; a skipped term adds -0.0, an exact no-op); v(i) is this
+// lane's value of slot i
+template <int G, int S, class V>
+__device__ __forceinline__ float gseq_stream(float acc, int n, V&& v) {
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        if (!__any(G * i < n)) break;
+        const float x = v(i);
+        float b[G];
+#pragma unroll
+        for (int l = 0; l < G; ++l) b[l] = gbcast<G>(x, l);
+#pragma unroll
+        for (int l = 0; l < G; ++l) acc += (G * i + l < n) ? b[l] : -0.0f;
+    }
+    return acc;
+}
+
+template <bool PDF_ONLY, int G, int S>
+__device__ __forceinline__ bool serve_full_group_g(const float* gp, int Kp, int K, const GuideIO& io, int64_t q,
+                                                   int lane, GuideConsts gc) {
+    static_assert(S <= 32, "validity masks are 32-bit");
+    constexpr uint64_t GM = (1ull << G) - 1;
+    const int gl = lane & (G - 1);
+    const int gbase = lane & ~(G - 1);
+    const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
+    uint32_t key[S], idx[S];
+    uint32_t vmask = 0;   // bit i: the conditional of component G i + gl is valid
+    float total;
+    {
+        float wr[S];
+        bool nan_l = false;
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+            const int k = G * i + gl;
+            wr[i] = -0.0f;    // absent: never a candidate
+            if (k < K) {
+                wr[i] = gp_ld(gp, Kp, GP_W, k) * marginal_pdf(gp, Kp, k, c, gc.norm3);
+                vmask |= (cond_valid(gp, Kp, k, c) ? 1u : 0u) << i;
+            }
+            nan_l |= (wr[i] != wr[i]);
+        }
+        if (((__builtin_amdgcn_ballot_w64(nan_l) >> gbase) & GM) != 0) return false;
+        // totalMass in component order (element k = G i + l)
+        total = gseq_stream<G, S>(0.0f, K, [&](int i) { return wr[i]; });
+        // the selection order: (weight desc, index asc), absent entries last
+        uint64_t v[S];
+#pragma unroll
+        for (int i = 0; i < S; ++i)
+            v[i] = sel_key(__builtin_signbit(wr[i]) ? 0u : __builtin_bit_cast(uint32_t, wr[i]) + 1u,
+                           (uint32_t)(G * i + gl));
+        bsort<G, S>(v, gl);
+#pragma unroll
+        for (int i = 0; i < S; ++i) { key[i] = sel_wkey(v[i]); idx[i] = sel_idx(v[i]); }
+    }
+    const float cutoff = (float)(0.99 * (double)total);
+    int n_live = 0;
+    uint32_t okm = 0;   // bit i: sorted element G i + gl has a valid conditional
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        n_live += __builtin_popcountll((__builtin_amdgcn_ballot_w64(key[i] != 0u) >> gbase) & GM);
+        const unsigned vm = (unsigned)__shfl((int)vmask, gbase | (int)(idx[i] & (G - 1)));
+        okm |= ((vm >> (idx[i] / G)) & 1u) << i;
+    }
+    auto wk = [&](int i) { return __builtin_bit_cast(float, key[i] - 1u); };
+    auto kept = [&](int i) { return ((okm >> i) & 1u) ? wk(i) : 0.0f; };
+    // the cutoff walk: accum of the valid weights in selection order
+    float accum = 0.0f;
+    int lastIdx = n_live;   // (K when every weight is live and the cutoff is never reached)
+    bool done = false;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        if (!__any(!done && G * i < n_live)) break;
+        const float t = kept(i);
+        float bt[G];
+#pragma unroll
+        for (int l = 0; l < G; ++l) bt[l] = gbcast<G>(t, l);
+#pragma unroll
+        for (int l = 0; l < G; ++l) {
+            const int p = G * i + l;
+            if (!done && p < n_live) {
+                accum += bt[l];
+                if (accum >= cutoff) { lastIdx = p + 1; done = true; }
+            }
+        }
+    }
+    // finish_query: slot weights, createCdf, sample / given direction, pdf
+    const float invSum = 1.0f / accum;
+    const bool scaled = __builtin_isfinite(invSum);
+    auto fs = [&](int i) {   // the slot weight before the sum2 normalisation
+        float wi = kept(i);
+        if (scaled) wi = wi * invSum;
+        return wi;
+    };
+    const float sum2 = gseq_stream<G, S>(0.0f, lastIdx, fs);
+    bool pdf_q = PDF_ONLY;
+    if constexpr (!PDF_ONLY) pdf_q = io.pmode && io.pmode[q];   // uniform in the group
+    float outd[3] = {0.0f, 0.0f, 0.0f};
+    float outpdf = 0.0f;
+    int outcomp = -1;
+    if (lastIdx > 0 && sum2 != 0.0f) {
+        auto f = [&](int i) { return fs(i) / sum2; };
+        float dir[3];
+        if (!pdf_q) {
+            // sampleDiscreteCdf: lower_bound == first slot with cdf >= u, else the tie walk
+            const float u0 = io.u0[q], u1 = io.u1[q], u2 = io.u2[q];
+            float cdf = 0.0f, prev = 0.0f;
+            int slot = -1, runStart = 0;
+#pragma unroll
+            for (int i = 0; i < S; ++i) {
+                if (!__any(slot < 0 && G * i < lastIdx)) break;
+                const float fi = f(i);
+                float bf[G];
+#pragma unroll
+                for (int l = 0; l < G; ++l) bf[l] = gbcast<G>(fi, l);
+#pragma unroll
+                for (int l = 0; l < G; ++l) {
+                    const float b = bf[l];
+                    const int p = G * i + l;
+                    if (slot < 0 && p < lastIdx) {
+                        cdf += b;
+                        if (p == 0 || cdf != prev) runStart = p;
+                        prev = cdf;
+                        if (cdf >= u0) slot = p;
+                    }
+                }
+            }
+            if (slot < 0) slot = runStart;
+            int mine = 0;
+#pragma unroll
+            for (int i = 0; i < S; ++i) mine = (i == slot / G) ? (int)idx[i] : mine;
+            const int ksel = __shfl(mine, gbase | (slot & (G - 1)));
+            float esel[3];
+            cond_mean_dir(gp, Kp, ksel, c, esel);
+            const float radius = sqrtf(-2.0f * logf(1.0f - u1));
+            const float theta = (float)(2.0 * kPi * (double)u2);
+            float res0, res1;
+            sincosf(theta, &res0, &res1);
+            const float z0 = radius * res0, z1 = radius * res1;
+            const float L00 = gp_ld(gp, Kp, GP_CL00, ksel), L10 = gp_ld(gp, Kp, GP_CL10, ksel);
+            const float L11 = gp_ld(gp, Kp, GP_CL11, ksel);
+            const float v0 = L00 * z0 + 0.0f * z1;
+            const float v1 = L10 * z0 + L11 * z1;
+            float tof[9];
+            coordinates_f(esel, tof);
+            ts_exp_dir(tof, v0, v1, dir);
+            outcomp = ksel;
+        } else {
+            dir[0] = io.e0[q]; dir[1] = io.e1[q]; dir[2] = io.e2[q];
+            outcomp = kCompPdfValid;
+        }
+        // MixtureModel::pdf over the conditional: terms per own slot, summed in slot order
+        outpdf = gseq_stream<G, S>(0.0f, lastIdx, [&](int i) {
+            float term = -0.0f;
+            const float fi = f(i);
+            if (G * i + gl < lastIdx && fi != 0.0f) {
+                float e[3];
+                cond_mean_dir(gp, Kp, (int)idx[i], c, e);
+                term = fi * cond_component_pdf(gp, Kp, (int)idx[i], e, dir, gc.norm2);
+            }
+            return term;
+        });
+        outd[0] = dir[0]; outd[1] = dir[1]; outd[2] = dir[2];
+    }
+    if (gl == 0) {
+        io.pdf[q] = outpdf;
+        if constexpr (!PDF_ONLY) {
+            io.d0[q] = outd[0]; io.d1[q] = outd[1]; io.d2[q] = outd[2];
+            io.comp[q] = outcomp;
+        }
+    }
+    return true;
+}
+
+// The listed full-K queries, a G-lane group each (grid-stride over groups);
 // TREE: each against its own leaf's mixture.  NaN queries -> fb2 (count at
 // fb2[0], list from fb2 + 1) for the one-wave kernel.
-#ifndef SDMM_GROUP_WPE
-#define SDMM_GROUP_WPE 4   // 128 VGPRs, no spill; K=128 guided pass 17.6 -> 15.2 ms (2: 189 VGPRs, 2 waves per SIMD)
+// 16 (default) or 4 lanes per query.  Round 4 A/B, Cornell K=128 tree
+// wavefront: 12.4 ms per guided pass with 16-lane groups, 13.1 ms with 4-lane
+// groups (32 slots per lane: 256 VGPRs with a spill, 2 waves per SIMD)
+#ifndef SDMM_GROUP_LANES
+#define SDMM_GROUP_LANES 16
 #endif
+constexpr int kGroupLanes = SDMM_GROUP_LANES;
+#ifndef SDMM_GROUP_WPE
+#define SDMM_GROUP_WPE 4   // 16-lane groups: 128 VGPRs, no spill; K=128 guided pass 17.6 -> 15.2 ms (2: 189 VGPRs)
+#endif
+// (4-lane groups with 16 or 32 slots: 256 VGPRs, 2 waves per SIMD, no spill)
 template <bool PDF_ONLY, bool TREE, int S>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDMM_GROUP_WPE)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(S >= 16 ? 2 : SDMM_GROUP_WPE)))
 guide_group_fallback_kernel(const float* __restrict__ gp1, int Kp1, int K1, const STNodeDev* __restrict__ nodes,
                             const GuideMix* __restrict__ tab, GuideIO io, GuideConsts gc,
                             const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list,
                             int* __restrict__ fb2) {
+    constexpr int G = kGroupLanes, GPW = 64 / G;
     const int lane = threadIdx.x;
     const int count = *fb_count;
-    const int64_t groups = (int64_t)gridDim.x * 4;
-    for (int64_t gi = (int64_t)blockIdx.x * 4 + (lane >> 4); gi < count; gi += groups) {
+    const int64_t groups = (int64_t)gridDim.x * GPW;
+    for (int64_t gi = (int64_t)blockIdx.x * GPW + lane / G; gi < count; gi += groups) {
         const int64_t q = fb_list[gi];
         const float* gp = gp1;
         int Kp = Kp1, K = K1;
@@ -1229,28 +1578,41 @@ guide_group_fallback_kernel(const float* __restrict__ gp1, int Kp1, int K1, cons
             const GuideMix mx = tab[node];
             gp = mx.gp; Kp = mx.Kp; K = mx.K;
         }
-        if (!serve_full_group<PDF_ONLY, S>(gp, Kp, K, io, q, lane, gc) && (lane & 15) == 0)
-            fb2[1 + atomicAdd(fb2, 1)] = (int32_t)q;
+        bool ok;
+        if constexpr (G == 16) ok = serve_full_group<PDF_ONLY, S>(gp, Kp, K, io, q, lane, gc);
+        else ok = serve_full_group_g<PDF_ONLY, G, S>(gp, Kp, K, io, q, lane, gc);
+        if (!ok && (lane & (G - 1)) == 0) fb2[1 + atomicAdd(fb2, 1)] = (int32_t)q;
     }
 }
 
+// S = slots per lane: kmax <= G S
 template <bool PDF_ONLY, bool TREE>
 static void launch_group_fallback(int kmax, int blocks, hipStream_t st, const float* gp, int Kp, int K,
                                   const STNodeDev* nd, const GuideMix* tb, const GuideIO& io, GuideConsts gc,
                                   const int* fb_count, const int32_t* fb_list, int* fb2) {
-    if (kmax <= 16)
+    constexpr int G = kGroupLanes;
+    if (kmax <= G)
         hipLaunchKernelGGL((guide_group_fallback_kernel<PDF_ONLY, TREE, 1>), dim3(blocks), dim3(64), 0, st, gp, Kp,
                            K, nd, tb, io, gc, fb_count, fb_list, fb2);
-    else if (kmax <= 32)
+    else if (kmax <= 2 * G)
         hipLaunchKernelGGL((guide_group_fallback_kernel<PDF_ONLY, TREE, 2>), dim3(blocks), dim3(64), 0, st, gp, Kp,
                            K, nd, tb, io, gc, fb_count, fb_list, fb2);
-    else if (kmax <= 64)
+    else if (kmax <= 4 * G)
         hipLaunchKernelGGL((guide_group_fallback_kernel<PDF_ONLY, TREE, 4>), dim3(blocks), dim3(64), 0, st, gp, Kp,
                            K, nd, tb, io, gc, fb_count, fb_list, fb2);
-    else
+    else if (kmax <= 8 * G)
         hipLaunchKernelGGL((guide_group_fallback_kernel<PDF_ONLY, TREE, 8>), dim3(blocks), dim3(64), 0, st, gp, Kp,
                            K, nd, tb, io, gc, fb_count, fb_list, fb2);
+    else if constexpr (G < 16) {
+        if (kmax <= 16 * G)
+            hipLaunchKernelGGL((guide_group_fallback_kernel<PDF_ONLY, TREE, 16>), dim3(blocks), dim3(64), 0, st, gp,
+                               Kp, K, nd, tb, io, gc, fb_count, fb_list, fb2);
+        else
+            hipLaunchKernelGGL((guide_group_fallback_kernel<PDF_ONLY, TREE, 32>), dim3(blocks), dim3(64), 0, st, gp,
+                               Kp, K, nd, tb, io, gc, fb_count, fb_list, fb2);
+    }
 }
+static_assert(kGroupKMax <= 32 * kGroupLanes || kGroupLanes == 16, "group slots");
 
 // ---------------------------------------------------------------------------
 // Product with a learned BSDF (the plugin's sampleProduct path,
@@ -2101,7 +2463,7 @@ guide_product_wave_kernel(const float* __restrict__ gp, int Kp, int K, const flo
 // guide_product_wave_kernel do against that one mixture.  cctab[node] is the
 // node mixture's conditional covariances (condCov).
 template <bool PDF_ONLY, int LCAP>
-__device__ __forceinline__ void serve_product_cand(const float* gp, int Kp, int K, const float* condCov,
+__device__ __forceinline__ bool serve_product_cand(const float* gp, int Kp, int K, const float* condCov,
                                                    const GuideIO& io, const ProductIO& pio, const BsdfTab& bt,
                                                    int64_t q, const float c[3], float* cw, unsigned short* ck,
                                                    int tid, int cap, GuideConsts gc, int* fb_count,
@@ -2110,9 +2472,10 @@ __device__ __forceinline__ void serve_product_cand(const float* gp, int Kp, int 
     const int lastIdx = build_candidates_reg<LCAP>(gp, Kp, K, c, cw, ck, 64, tid, gc.norm3, cap, accum);
     if (lastIdx < 0) {
         fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
-        return;
+        return true;
     }
     product_tail<PDF_ONLY>(gp, Kp, condCov, c, lastIdx, accum, CandSlots{cw, ck, 64, tid}, io, pio, bt, q, gc, t);
+    return false;
 }
 
 template <bool PDF_ONLY>
@@ -2127,7 +2490,7 @@ guide_tree_product_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideM
                                const float* const* __restrict__ cctab, int64_t nq, GuideIO io, ProductIO pio,
                                BsdfTab bt, GuideConsts gc, int cap, int* __restrict__ fb_count,
                                int32_t* __restrict__ fb_list, const int32_t* __restrict__ perm,
-                               int32_t* __restrict__ node_out) {
+                               int32_t* __restrict__ node_out, NodeRoute rt) {
     __shared__ float cw[LCAP * 64];
     __shared__ unsigned short ck[LCAP * 64];
     const int tid = threadIdx.x;
@@ -2141,6 +2504,21 @@ guide_tree_product_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideM
     // control flow; else one distinct leaf per trip (waterfall)
     const int n0 = __builtin_amdgcn_readfirstlane(node);
     const bool uniform = __builtin_amdgcn_ballot_w64(node != n0) == 0;
+    if (uniform && rt.stats && n0 >= 0) {
+        // uniform-leaf wave with routing: routed to the full-K path, or served
+        // here and counted (see NodeRoute)
+        const GuideMix mx = tab[n0];
+        if (mx.K > 0) {
+            if (rt.stats[3 * n0 + 2]) {
+                fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
+            } else {
+                const bool fell = serve_product_cand<PDF_ONLY, LCAP>(mx.gp, mx.Kp, mx.K, cctab[n0], io, pio, bt, q, c,
+                                                                     cw, ck, tid, cap, gc, fb_count, fb_list, t);
+                route_count(rt, n0, fell);
+            }
+            return;
+        }
+    }
     for (;;) {
         const int nw = uniform ? n0 : __builtin_amdgcn_readfirstlane(node);
         if (node != nw) continue;
@@ -2296,6 +2674,9 @@ static hipError_t launch_cand(int cap, dim3 grid, hipStream_t st, const float* g
     else if (cap <= 24)
         hipLaunchKernelGGL((guide_cand_kernel<PDF_ONLY, 24>), grid, dim3(64), 0, st, gp, Kp, K, nq, io, gc, cap,
                            fb_count, fb_list, perm);
+    else if (cap <= 40)
+        hipLaunchKernelGGL((guide_cand_kernel<PDF_ONLY, 40>), grid, dim3(64), 0, st, gp, Kp, K, nq, io, gc, cap,
+                           fb_count, fb_list, perm);
     else
         hipLaunchKernelGGL((guide_cand_kernel<PDF_ONLY, kGuideCap>), grid, dim3(64), 0, st, gp, Kp, K, nq, io, gc,
                            cap, fb_count, fb_list, perm);
@@ -2304,16 +2685,19 @@ static hipError_t launch_cand(int cap, dim3 grid, hipStream_t st, const float* g
 template <bool PDF_ONLY>
 static hipError_t launch_tree_cand(int cap, dim3 grid, hipStream_t st, const STNodeDev* nd, const GuideMix* tb,
                                    int64_t nq, const GuideIO& io, GuideConsts gc, int* fb_count, int32_t* fb_list,
-                                   const int32_t* perm, int32_t* node_out) {
+                                   const int32_t* perm, int32_t* node_out, const NodeRoute& rt) {
     if (cap <= 16)
         hipLaunchKernelGGL((guide_tree_cand_kernel<PDF_ONLY, 16>), grid, dim3(64), 0, st, nd, tb, nq, io, gc, cap,
-                           fb_count, fb_list, perm, node_out);
+                           fb_count, fb_list, perm, node_out, rt);
     else if (cap <= 24)
         hipLaunchKernelGGL((guide_tree_cand_kernel<PDF_ONLY, 24>), grid, dim3(64), 0, st, nd, tb, nq, io, gc, cap,
-                           fb_count, fb_list, perm, node_out);
+                           fb_count, fb_list, perm, node_out, rt);
+    else if (cap <= 40)
+        hipLaunchKernelGGL((guide_tree_cand_kernel<PDF_ONLY, 40>), grid, dim3(64), 0, st, nd, tb, nq, io, gc, cap,
+                           fb_count, fb_list, perm, node_out, rt);
     else
         hipLaunchKernelGGL((guide_tree_cand_kernel<PDF_ONLY, kGuideCap>), grid, dim3(64), 0, st, nd, tb, nq, io,
-                           gc, cap, fb_count, fb_list, perm, node_out);
+                           gc, cap, fb_count, fb_list, perm, node_out, rt);
     return hipGetLastError();
 }
 
@@ -2380,7 +2764,8 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
                              const float* const u[3], const float* const dgiven[3], float* const d[3],
                              float* pdf, int32_t* comp, int32_t* node_out, float norm2, float norm3, int cap,
                              int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
-                             const GuideSortScratch* sort, const uint8_t* pmode, int* fb2) {
+                             const GuideSortScratch* sort, const uint8_t* pmode, int* fb2, uint32_t* route,
+                             int nn) {
     if (nq <= 0) return hipSuccess;
     cap = (cap < 0) ? 0 : (cap > kGuideCap ? kGuideCap : cap);
     if (nq > INT32_MAX) return hipErrorInvalidValue;
@@ -2406,8 +2791,11 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
     const GuideIO io = make_io(c, u, dgiven, d, pdf, comp, pmode);
     if (pmode) dgiven = nullptr;   // mixed: the sampling kernels, pdf queries per pmode
     cap = cap < kmax ? cap : kmax;
-    e = dgiven ? launch_tree_cand<true>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_out)
-               : launch_tree_cand<false>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_out);
+    const NodeRoute rt{route, nn};
+    e = launch_route(rt, st);
+    if (e != hipSuccess) return e;
+    e = dgiven ? launch_tree_cand<true>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_out, rt)
+               : launch_tree_cand<false>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_out, rt);
     if (e != hipSuccess) return e;
     if (fb2 && kmax <= kGroupKMax) {
         e = hipMemsetAsync(fb2, 0, sizeof(int), st);
@@ -2504,10 +2892,12 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
     if (dgiven) {
         if (cap <= 16) SDMM_PRODUCT_CAND(true, 16);
         else if (cap <= 24) SDMM_PRODUCT_CAND(true, 24);
+        else if (cap <= 40) SDMM_PRODUCT_CAND(true, 40);
         else SDMM_PRODUCT_CAND(true, kGuideCap);
     } else {
         if (cap <= 16) SDMM_PRODUCT_CAND(false, 16);
         else if (cap <= 24) SDMM_PRODUCT_CAND(false, 24);
+        else if (cap <= 40) SDMM_PRODUCT_CAND(false, 40);
         else SDMM_PRODUCT_CAND(false, kGuideCap);
     }
 #undef SDMM_PRODUCT_CAND
@@ -2533,7 +2923,8 @@ hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const v
                                      float* h, const float* bw, const float* bmean, const float* bcov,
                                      const uint8_t* diffuse, int B, int M, float norm2, float norm3, int cap,
                                      int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
-                                     const GuideSortScratch* sort, ProductScratch* scratch) {
+                                     const GuideSortScratch* sort, ProductScratch* scratch, uint32_t* route,
+                                     int nn) {
     if (nq <= 0) return hipSuccess;
     if (nq > INT32_MAX) return hipErrorInvalidValue;
     if (kmax < 1) kmax = 1;
@@ -2577,16 +2968,21 @@ hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const v
     float* pscratch = nullptr;
     e = product_scratch(scratch, (int64_t)grid.x * 64, fblocks, st, &pio.cache, &pscratch);
     if (e != hipSuccess) return e;
+    const NodeRoute rt{route, nn};
+    e = launch_route(rt, st);
+    if (e != hipSuccess) return e;
 #define SDMM_TREE_PRODUCT_CAND(P, L)                                                                         \
     hipLaunchKernelGGL((guide_tree_product_cand_kernel<P, L>), grid, dim3(64), 0, st, nd, tb, cc, nq, iox, pio, \
-                       bt, gc, cap, fb_count, fb_list, perm, node_out)
+                       bt, gc, cap, fb_count, fb_list, perm, node_out, rt)
     if (pdf_only) {
         if (cap <= 16) SDMM_TREE_PRODUCT_CAND(true, 16);
         else if (cap <= 24) SDMM_TREE_PRODUCT_CAND(true, 24);
+        else if (cap <= 40) SDMM_TREE_PRODUCT_CAND(true, 40);
         else SDMM_TREE_PRODUCT_CAND(true, kGuideCap);
     } else {
         if (cap <= 16) SDMM_TREE_PRODUCT_CAND(false, 16);
         else if (cap <= 24) SDMM_TREE_PRODUCT_CAND(false, 24);
+        else if (cap <= 40) SDMM_TREE_PRODUCT_CAND(false, 40);
         else SDMM_TREE_PRODUCT_CAND(false, kGuideCap);
     }
 #undef SDMM_TREE_PRODUCT_CAND

@@ -94,7 +94,8 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
                              const float* const u[3], const float* const dgiven[3], float* const d[3],
                              float* pdf, int32_t* comp, int32_t* node_out, float norm2, float norm3, int cap,
                              int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
-                             const GuideSortScratch* sort, const uint8_t* pmode = nullptr, int* fb2 = nullptr);
+                             const GuideSortScratch* sort, const uint8_t* pmode = nullptr, int* fb2 = nullptr,
+                             uint32_t* route = nullptr, int nn = 0);
 hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* condCov, int64_t nq,
                                 const float* const c[3], const float* const u[3], const float* const dgiven[3],
                                 float* const d[3], float* pdf, int32_t* comp, const int32_t* material,
@@ -109,11 +110,20 @@ hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const v
                                      float* h, const float* bw, const float* bmean, const float* bcov,
                                      const uint8_t* diffuse, int B, int M, float norm2, float norm3, int cap,
                                      int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
-                                     const GuideSortScratch* sort, ProductScratch* scratch);
+                                     const GuideSortScratch* sort, ProductScratch* scratch, uint32_t* route = nullptr,
+                                     int nn = 0);
 #ifndef SDMM_GUIDE_CAP_MAX
-#define SDMM_GUIDE_CAP_MAX 40
+#define SDMM_GUIDE_CAP_MAX 64
 #endif
 constexpr int kGuideCapMax = SDMM_GUIDE_CAP_MAX;
+// default capacity: 40 (round 4 A/B, Cornell K=128 tree wavefront: 12.3 ms per
+// guided pass at 40 against 13.3 ms at 64 -- a third of the fallback queries
+// but 2 instead of 3 waves per SIMD; K=512 product 92.2 vs 91.4 ms; the single
+// K=128 mixture 613 vs 816 us)
+#ifndef SDMM_GUIDE_CAP_DEFAULT
+#define SDMM_GUIDE_CAP_DEFAULT 40
+#endif
+constexpr int kGuideCapDefault = SDMM_GUIDE_CAP_DEFAULT;
 hipError_t launch_split_load(const float* const p[3], const int64_t* src_start, const int64_t* dst_start, int n_items,
                              int64_t total, float* ox, float* oy, float* oz, int32_t* oitem, hipStream_t st);
 hipError_t launch_split_sums(const float* x, const float* y, const float* z, const void* chunks, int n_chunks,
@@ -317,7 +327,7 @@ struct sdmm_mix {
     int cus = 256;
     int resp_blocks = 2, stats_blocks = 2;   // resident 256-thread WGs per CU
     // guided-query scratch: fallback counter + list of fallback query indices
-    int guide_cap = kGuideCapMax;   // candidate-list capacity (sdmm_set_guide_capacity)
+    int guide_cap = kGuideCapDefault;   // candidate-list capacity (sdmm_set_guide_capacity)
     mutable int* guide_fb = nullptr;
     mutable int64_t guide_fb_cap = 0;
     mutable GuideSortScratch guide_sort{};
@@ -1041,7 +1051,7 @@ int sdmm_set_guide_order(sdmm_mix* m, int coherent) {
 
 int sdmm_set_guide_capacity(sdmm_mix* m, int cap) {
     if (!m) return fail(SDMM_E_INVALID, "null handle");
-    if (cap < 0 || cap > kGuideCapMax) return fail(SDMM_E_INVALID, "guide capacity must be in [0, 40]");
+    if (cap < 0 || cap > kGuideCapMax) return fail(SDMM_E_INVALID, "guide capacity must be in [0, 64]");
     m->guide_cap = cap;
     return SDMM_OK;
 }
@@ -2104,7 +2114,9 @@ struct sdmm_stree {
     void* dcctab = nullptr;
     size_t dtab_cap = 0;
     int tab_kmax = 0;
-    int tab_cap = kGuideCapMax; // candidate capacity: the smallest of the bound mixtures' (sdmm_set_guide_capacity)
+    int tab_cap = kGuideCapDefault; // candidate capacity: the smallest of the bound mixtures' (sdmm_set_guide_capacity)
+    uint32_t* droute = nullptr;     // [3 nn] per-node routing counts of the wavefronts (guide.hip NodeRoute)
+    size_t droute_cap = 0;          // entries allocated
     bool tab_valid = false;     // bound table matches the current nodes
     int* guide_fb = nullptr;
     int64_t guide_fb_cap = 0;
@@ -2395,6 +2407,7 @@ void sdmm_stree_destroy(sdmm_stree* t) {
     if (t->dnodes) (void)hipFree(t->dnodes);
     if (t->scratch) (void)hipFree(t->scratch);
     if (t->dtab) (void)hipFree(t->dtab);
+    if (t->droute) (void)hipFree(t->droute);
     if (t->split_mem) (void)hipFree(t->split_mem);
     if (t->split_small) (void)hipFree(t->split_small);
     if (t->guide_fb) (void)hipFree(t->guide_fb);
@@ -2921,7 +2934,7 @@ int st_upload_table(sdmm_stree* t, const sdmm_mix* const* node_mix) {
     const size_t nn = t->nodes.size();
     std::vector<GuideMixHost> tab(nn);
     std::vector<const float*> cc(nn, nullptr);
-    int kmax = 0, cap = kGuideCapMax;
+    int kmax = 0, cap = kGuideCapMax;   // (lowered to the bound mixtures' capacities)
     t->mix_streams.clear();
     for (size_t i = 0; i < nn; ++i) {
         const sdmm_mix* m = node_mix[i];
@@ -2947,6 +2960,15 @@ int st_upload_table(sdmm_stree* t, const sdmm_mix* const* node_mix) {
     t->tab_cap = cap;
     t->tab_valid = true;
     if (same && t->dtab) return SDMM_OK;
+    // a different table: the routing counts start again (grow-only buffer)
+    if (3 * nn > t->droute_cap) {
+        release_dev(t->droute);
+        t->droute = nullptr;
+        t->droute_cap = 0;
+        HIP_TRY(hipMalloc(&t->droute, sizeof(uint32_t) * 3 * nn));
+        t->droute_cap = 3 * nn;
+    }
+    if (nn) HIP_TRY(hipMemsetAsync(t->droute, 0, sizeof(uint32_t) * 3 * nn, t->stream));
     HIP_TRY(hipStreamSynchronize(t->stream));   // the previous copy may still read tab_host
     const size_t nb = nn ? nn : 1;
     const size_t bytes = (sizeof(GuideMixHost) + sizeof(const float*)) * nb;
@@ -3001,6 +3023,15 @@ bool tree_order_on() {
     return on;
 }
 
+// SDMM_GUIDE_ROUTE=0 (A/B): no per-node routing of the wavefronts
+uint32_t* route_stats(sdmm_stree* t) {
+    static const bool on = [] {
+        const char* e = std::getenv("SDMM_GUIDE_ROUTE");
+        return !(e && std::strcmp(e, "0") == 0);
+    }();
+    return (on && t->droute && t->droute_cap >= 3 * t->nodes.size()) ? t->droute : nullptr;
+}
+
 int st_guide(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
              const float* const u[3], const float* const dgiven[3], float* const d[3], float* pdf, int32_t* comp,
              int32_t* node_out, const uint8_t* pmode = nullptr) {
@@ -3013,7 +3044,7 @@ int st_guide(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const f
                               cus, t->stream, sort, pmode,
                               // the NaN hand-off list of the group fallback: the
                               // Morton keys' input buffer, free once the order is built
-                              (int*)t->guide_sort.keys[0]));
+                              (int*)t->guide_sort.keys[0], route_stats(t), (int)t->nodes.size()));
     return SDMM_OK;
 }
 
@@ -3029,7 +3060,7 @@ int st_guide_product(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq,
                                       comp, node_out, material, frame, heuristic, bsdf->weights, bsdf->means,
                                       bsdf->covs, bsdf->diffuse, bsdf->B, bsdf->M, norm_const(2), norm_const(3),
                                       t->tab_cap, t->guide_fb, t->guide_fb + 1, cus, t->stream, sort,
-                                      &t->product_scratch));
+                                      &t->product_scratch, route_stats(t), (int)t->nodes.size()));
     return SDMM_OK;
 }
 

@@ -345,8 +345,8 @@ def _em_model(pkg, oracle, synth, K, N, iters):
     return b, mix, m
 
 
-@pytest.mark.parametrize("K,iters,cap", [(16, 3, 40), (16, 3, 0), (72, 3, 0), (128, 4, 40), (128, 4, 4),
-                                         (128, 4, 0), (256, 2, 40), (256, 2, 0), (512, 2, 40), (512, 2, 0)])
+@pytest.mark.parametrize("K,iters,cap", [(16, 3, 40), (16, 3, 0), (72, 3, 0), (128, 4, 64), (128, 4, 40), (128, 4, 4),
+                                         (128, 4, 0), (256, 2, 40), (256, 2, 0), (512, 2, 64), (512, 2, 40), (512, 2, 0)])
 def test_guide_indices_bit_exact(pkg, oracle, synth, gpu, plog, K, iters, cap):
     """Guided bounces vs the oracle.  cap: per-query candidate-list capacity;
     4 sends most K=128 queries and 0 sends all of them down the full-K

@@ -36,7 +36,7 @@ def _model(pkg, oracle, synth, K, iters, N=8192):
 @pytest.mark.parametrize("K,iters,B,M,cap,nq", [(16, 3, 3, 4, 40, 3000), (128, 4, 2, 6, 40, 3000),
                                                 (64, 2, 1, 1, 40, 3000),
                                                 # the Kitchen config: K=512 x 8 materials x 8 lobes
-                                                (512, 2, 8, 8, 40, 2000),
+                                                (512, 2, 8, 8, 64, 2000), (512, 2, 8, 8, 40, 2000),
                                                 # candidate capacity 0: every query through the
                                                 # full-K fallback kernel of the product path
                                                 (128, 4, 2, 6, 0, 1500), (512, 2, 8, 8, 0, 1000)])

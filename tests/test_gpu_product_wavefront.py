@@ -41,7 +41,8 @@ def _check(plog, tag, hg, hr, cg, cr, dg, dr, pg, pr):
 
 
 @pytest.mark.parametrize("K,B,M,cap,nq", [(16, 4, 3, 40, 1 << 14), (16, 4, 3, 0, 3000),
-                                          (512, 8, 8, 40, 2000), (512, 8, 8, 0, 1000)])
+                                          (512, 8, 8, 64, 2000), (512, 8, 8, 40, 2000),
+                                          (512, 8, 8, 0, 1000)])
 def test_product_wavefront_matches_oracle(pkg, oracle, synth, gpu, plog, K, B, M, cap, nq):
     import torch
     b, t, mixes, leaves = _tree_and_leaf_mixtures(pkg, synth, K, iters=2 if K <= 64 else 1)

@@ -85,7 +85,7 @@ def _oracle_check(oracle, t, mixes, c, u, d, node, has, cw, dw, pw, pdw, plog):
 
 
 @pytest.mark.parametrize("K,nq,cap", [(16, 1 << 15, 40), (16, 3000, 40), (64, 1 << 14, 40),
-                                      (128, 1 << 14, 40), (128, 1 << 14, 4), (128, 1 << 14, 0)])
+                                      (128, 1 << 14, 64), (128, 1 << 14, 40), (128, 1 << 14, 4), (128, 1 << 14, 0)])
 def test_wavefront_equals_per_leaf_guide(pkg, oracle, synth, gpu, plog, K, nq, cap):
     """K = 128 is configs[2]'s leaf size: the tree kernels' candidate pass
     (capacity 40), the 16-lane group fallback most queries take at capacity 4,

@@ -12,7 +12,9 @@ OBJS=()
 for o in "$PKG"/build/*.o; do
   src=csrc/$(basename "$o" .o)
   if printf '%s\n' "$@" | grep -qx "$src"; then
-    /opt/rocm/bin/hipcc $HIPFLAGS $FLAGS -x hip -c "$PKG/$src" -o "$OUT/$(basename "$o")"
+    EXTRA=""   # the Makefile's E-step rule: no SLP re-packing
+    case "$src" in csrc/estep*.hip) EXTRA="-fno-slp-vectorize";; esac
+    /opt/rocm/bin/hipcc $HIPFLAGS $EXTRA $FLAGS -x hip -c "$PKG/$src" -o "$OUT/$(basename "$o")"
     OBJS+=("$OUT/$(basename "$o")")
   else
     OBJS+=("$o")
