@@ -569,6 +569,17 @@ struct GuideMix {
     int Kp, K;
 };
 static_assert(sizeof(GuideMix) == 16, "GuideMix");
+// A mixture record known wave-uniform (a uniform-leaf wave): its fields moved
+// to SGPRs, so that the record loads of a uniform component index compile to
+// scalar loads (the compiler cannot see the uniformity through the table
+// load and the branch structure).
+__device__ __forceinline__ GuideMix uniform_mix(const GuideMix& m) {
+    const uint64_t p = (uint64_t)(uintptr_t)m.gp;
+    const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)p);
+    const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(p >> 32));
+    return GuideMix{(const float*)(uintptr_t)(lo | (hi << 32)), __builtin_amdgcn_readfirstlane(m.Kp),
+                    __builtin_amdgcn_readfirstlane(m.K)};
+}
 
 // Query q with no valid conditional: the reference falls back to BSDF
 // sampling (comp -1, gmmPdf 0).
@@ -708,7 +719,7 @@ guide_tree_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __re
         // see DESIGN.md, guided wavefront.
         const int n0 = __builtin_amdgcn_readfirstlane(node);
         if (__builtin_amdgcn_ballot_w64(node != n0) == 0) {
-            const GuideMix mx = (n0 >= 0) ? tab[n0] : GuideMix{nullptr, 0, 0};
+            const GuideMix mx = uniform_mix((n0 >= 0) ? tab[n0] : GuideMix{nullptr, 0, 0});
             if (mx.K <= 0) {
                 write_invalid<PDF_ONLY>(io, q);
             } else if (rt.stats && rt.stats[3 * n0 + 2]) {
@@ -1125,7 +1136,7 @@ template <bool PDF_ONLY>
 __global__ void __launch_bounds__(64)
 guide_tree_fallback_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __restrict__ tab, int kmax,
                            GuideIO io, GuideConsts gc, const int* __restrict__ fb_count,
-                           const int32_t* __restrict__ fb_list) {
+                           const int32_t* __restrict__ fb_list, const int32_t* __restrict__ node_of) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x;
     const int count = *fb_count;
@@ -1133,8 +1144,9 @@ guide_tree_fallback_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* 
     for (int idx = blockIdx.x; idx < count; idx += gridDim.x) {
         const int64_t q = fb_list[idx];
         const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
-        const int node = stree_find_point(nodes, c[0], c[1], c[2]);   // uniform: a listed query has a mixture
-        const GuideMix mx = tab[node];
+        // uniform: a listed query has a mixture; node_of: the candidate kernel's find
+        const int node = node_of ? node_of[q] : stree_find_point(nodes, c[0], c[1], c[2]);
+        const GuideMix mx = uniform_mix(tab[node]);   // (one query per wave: uniform)
         serve_full_wave<PDF_ONLY>(mx.gp, mx.Kp, mx.K, io, q, c, L, lane, gc);
     }
 }
@@ -1564,7 +1576,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(S >= 16
 guide_group_fallback_kernel(const float* __restrict__ gp1, int Kp1, int K1, const STNodeDev* __restrict__ nodes,
                             const GuideMix* __restrict__ tab, GuideIO io, GuideConsts gc,
                             const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list,
-                            int* __restrict__ fb2) {
+                            int* __restrict__ fb2, const int32_t* __restrict__ node_of) {
     constexpr int G = kGroupLanes, GPW = 64 / G;
     const int lane = threadIdx.x;
     const int count = *fb_count;
@@ -1574,7 +1586,8 @@ guide_group_fallback_kernel(const float* __restrict__ gp1, int Kp1, int K1, cons
         const float* gp = gp1;
         int Kp = Kp1, K = K1;
         if constexpr (TREE) {
-            const int node = stree_find_point(nodes, io.c0[q], io.c1[q], io.c2[q]);   // a listed query has a mixture
+            // a listed query has a mixture; node_of: the candidate kernel's find
+            const int node = node_of ? node_of[q] : stree_find_point(nodes, io.c0[q], io.c1[q], io.c2[q]);
             const GuideMix mx = tab[node];
             gp = mx.gp; Kp = mx.Kp; K = mx.K;
         }
@@ -1589,27 +1602,28 @@ guide_group_fallback_kernel(const float* __restrict__ gp1, int Kp1, int K1, cons
 template <bool PDF_ONLY, bool TREE>
 static void launch_group_fallback(int kmax, int blocks, hipStream_t st, const float* gp, int Kp, int K,
                                   const STNodeDev* nd, const GuideMix* tb, const GuideIO& io, GuideConsts gc,
-                                  const int* fb_count, const int32_t* fb_list, int* fb2) {
+                                  const int* fb_count, const int32_t* fb_list, int* fb2,
+                                  const int32_t* node_of = nullptr) {
     constexpr int G = kGroupLanes;
     if (kmax <= G)
         hipLaunchKernelGGL((guide_group_fallback_kernel<PDF_ONLY, TREE, 1>), dim3(blocks), dim3(64), 0, st, gp, Kp,
-                           K, nd, tb, io, gc, fb_count, fb_list, fb2);
+                           K, nd, tb, io, gc, fb_count, fb_list, fb2, node_of);
     else if (kmax <= 2 * G)
         hipLaunchKernelGGL((guide_group_fallback_kernel<PDF_ONLY, TREE, 2>), dim3(blocks), dim3(64), 0, st, gp, Kp,
-                           K, nd, tb, io, gc, fb_count, fb_list, fb2);
+                           K, nd, tb, io, gc, fb_count, fb_list, fb2, node_of);
     else if (kmax <= 4 * G)
         hipLaunchKernelGGL((guide_group_fallback_kernel<PDF_ONLY, TREE, 4>), dim3(blocks), dim3(64), 0, st, gp, Kp,
-                           K, nd, tb, io, gc, fb_count, fb_list, fb2);
+                           K, nd, tb, io, gc, fb_count, fb_list, fb2, node_of);
     else if (kmax <= 8 * G)
         hipLaunchKernelGGL((guide_group_fallback_kernel<PDF_ONLY, TREE, 8>), dim3(blocks), dim3(64), 0, st, gp, Kp,
-                           K, nd, tb, io, gc, fb_count, fb_list, fb2);
+                           K, nd, tb, io, gc, fb_count, fb_list, fb2, node_of);
     else if constexpr (G < 16) {
         if (kmax <= 16 * G)
             hipLaunchKernelGGL((guide_group_fallback_kernel<PDF_ONLY, TREE, 16>), dim3(blocks), dim3(64), 0, st, gp,
-                               Kp, K, nd, tb, io, gc, fb_count, fb_list, fb2);
+                               Kp, K, nd, tb, io, gc, fb_count, fb_list, fb2, node_of);
         else
             hipLaunchKernelGGL((guide_group_fallback_kernel<PDF_ONLY, TREE, 32>), dim3(blocks), dim3(64), 0, st, gp,
-                               Kp, K, nd, tb, io, gc, fb_count, fb_list, fb2);
+                               Kp, K, nd, tb, io, gc, fb_count, fb_list, fb2, node_of);
     }
 }
 static_assert(kGroupKMax <= 32 * kGroupLanes || kGroupLanes == 16, "group slots");
@@ -2504,23 +2518,23 @@ guide_tree_product_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideM
     // control flow; else one distinct leaf per trip (waterfall)
     const int n0 = __builtin_amdgcn_readfirstlane(node);
     const bool uniform = __builtin_amdgcn_ballot_w64(node != n0) == 0;
-    if (uniform && rt.stats && n0 >= 0) {
-        // uniform-leaf wave with routing: routed to the full-K path, or served
-        // here and counted (see NodeRoute)
-        const GuideMix mx = tab[n0];
-        if (mx.K > 0) {
-            if (rt.stats[3 * n0 + 2]) {
-                fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
-            } else {
-                const bool fell = serve_product_cand<PDF_ONLY, LCAP>(mx.gp, mx.Kp, mx.K, cctab[n0], io, pio, bt, q, c,
-                                                                     cw, ck, tid, cap, gc, fb_count, fb_list, t);
-                route_count(rt, n0, fell);
-            }
-            return;
+    if (uniform) {
+        // uniform-leaf wave: the record in SGPRs (scalar record loads); with
+        // routing, routed to the full-K path or served here and counted
+        const GuideMix mx = uniform_mix((n0 >= 0) ? tab[n0] : GuideMix{nullptr, 0, 0});
+        if (mx.K <= 0) {
+            product_invalid<PDF_ONLY>(io, pio, q);
+        } else if (rt.stats && rt.stats[3 * n0 + 2]) {
+            fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
+        } else {
+            const bool fell = serve_product_cand<PDF_ONLY, LCAP>(mx.gp, mx.Kp, mx.K, cctab[n0], io, pio, bt, q, c, cw,
+                                                                 ck, tid, cap, gc, fb_count, fb_list, t);
+            if (rt.stats) route_count(rt, n0, fell);
         }
+        return;
     }
     for (;;) {
-        const int nw = uniform ? n0 : __builtin_amdgcn_readfirstlane(node);
+        const int nw = __builtin_amdgcn_readfirstlane(node);
         if (node != nw) continue;
         const GuideMix mx = (nw >= 0) ? tab[nw] : GuideMix{nullptr, 0, 0};
         if (mx.K <= 0)
@@ -2539,7 +2553,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDMM_PR
 guide_tree_product_wave_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __restrict__ tab,
                                const float* const* __restrict__ cctab, int kmax, GuideIO io, ProductIO pio,
                                BsdfTab bt, GuideConsts gc, float* __restrict__ pscratch, int pcap,
-                               const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list) {
+                               const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list,
+                               const int32_t* __restrict__ node_of) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x;
     const WaveLds L = wave_lds(lds, kmax, pscratch, pcap, bt.M);
@@ -2547,8 +2562,9 @@ guide_tree_product_wave_kernel(const STNodeDev* __restrict__ nodes, const GuideM
     for (int idx = blockIdx.x; idx < n; idx += gridDim.x) {
         const int64_t q = fb_list[idx];
         const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
-        const int node = stree_find_point(nodes, c[0], c[1], c[2]);   // uniform: a listed query has a mixture
-        const GuideMix mx = tab[node];
+        // uniform: a listed query has a mixture; node_of: the candidate kernel's find
+        const int node = node_of ? node_of[q] : stree_find_point(nodes, c[0], c[1], c[2]);
+        const GuideMix mx = uniform_mix(tab[node]);   // (one query per wave: uniform)
         float accum = 0.0f;
         const int lastIdx = build_full_wave(mx.gp, mx.Kp, mx.K, c, L, lane, gc.norm3, accum);
         product_tail_wave<PDF_ONLY>(mx.gp, mx.Kp, cctab[node], c, lastIdx, accum, L, io, pio, bt, q, lane, gc);
@@ -2794,18 +2810,22 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
     const NodeRoute rt{route, nn};
     e = launch_route(rt, st);
     if (e != hipSuccess) return e;
-    e = dgiven ? launch_tree_cand<true>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_out, rt)
-               : launch_tree_cand<false>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_out, rt);
+    // every query's node as the candidate kernel finds it (the caller's
+    // node_out, else the sorted-keys buffer, free once the order is built):
+    // the fallback kernels read it instead of walking the tree again
+    int32_t* const node_of = node_out ? node_out : (sort ? (int32_t*)sort->keys[1] : nullptr);
+    e = dgiven ? launch_tree_cand<true>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_of, rt)
+               : launch_tree_cand<false>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_of, rt);
     if (e != hipSuccess) return e;
     if (fb2 && kmax <= kGroupKMax) {
         e = hipMemsetAsync(fb2, 0, sizeof(int), st);
         if (e != hipSuccess) return e;
         if (dgiven)
             launch_group_fallback<true, true>(kmax, fb_blocks, st, nullptr, 0, 0, nd, tb, io, gc, fb_count, fb_list,
-                                              fb2);
+                                              fb2, node_of);
         else
             launch_group_fallback<false, true>(kmax, fb_blocks, st, nullptr, 0, 0, nd, tb, io, gc, fb_count,
-                                               fb_list, fb2);
+                                               fb_list, fb2, node_of);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
         fb_count = fb2;
@@ -2813,10 +2833,10 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
     }
     if (dgiven)
         hipLaunchKernelGGL(guide_tree_fallback_kernel<true>, dim3(fb_blocks), dim3(Tfb), lds_fb, st, nd, tb, kmax,
-                           io, gc, fb_count, fb_list);
+                           io, gc, fb_count, fb_list, node_of);
     else
         hipLaunchKernelGGL(guide_tree_fallback_kernel<false>, dim3(fb_blocks), dim3(Tfb), lds_fb, st, nd, tb,
-                           kmax, io, gc, fb_count, fb_list);
+                           kmax, io, gc, fb_count, fb_list, node_of);
     return hipGetLastError();
 }
 
@@ -2971,9 +2991,11 @@ hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const v
     const NodeRoute rt{route, nn};
     e = launch_route(rt, st);
     if (e != hipSuccess) return e;
+    // every query's node from the candidate kernel (see launch_guide_tree)
+    int32_t* const node_of = node_out ? node_out : (sort ? (int32_t*)sort->keys[1] : nullptr);
 #define SDMM_TREE_PRODUCT_CAND(P, L)                                                                         \
     hipLaunchKernelGGL((guide_tree_product_cand_kernel<P, L>), grid, dim3(64), 0, st, nd, tb, cc, nq, iox, pio, \
-                       bt, gc, cap, fb_count, fb_list, perm, node_out, rt)
+                       bt, gc, cap, fb_count, fb_list, perm, node_of, rt)
     if (pdf_only) {
         if (cap <= 16) SDMM_TREE_PRODUCT_CAND(true, 16);
         else if (cap <= 24) SDMM_TREE_PRODUCT_CAND(true, 24);
@@ -2990,10 +3012,10 @@ hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const v
     if (e != hipSuccess) return e;
     if (pdf_only)
         hipLaunchKernelGGL(guide_tree_product_wave_kernel<true>, dim3(fblocks), dim3(64), lds, st, nd, tb, cc, kmax,
-                           iox, pio, bt, gc, pscratch, kProductPairCap, fb_count, fb_list);
+                           iox, pio, bt, gc, pscratch, kProductPairCap, fb_count, fb_list, node_of);
     else
         hipLaunchKernelGGL(guide_tree_product_wave_kernel<false>, dim3(fblocks), dim3(64), lds, st, nd, tb, cc,
-                           kmax, iox, pio, bt, gc, pscratch, kProductPairCap, fb_count, fb_list);
+                           kmax, iox, pio, bt, gc, pscratch, kProductPairCap, fb_count, fb_list, node_of);
     return hipGetLastError();
 }
 

@@ -3023,11 +3023,14 @@ bool tree_order_on() {
     return on;
 }
 
-// SDMM_GUIDE_ROUTE=0 (A/B): no per-node routing of the wavefronts
+// SDMM_GUIDE_ROUTE=1 (A/B, off by default): per-node routing of the
+// wavefronts (guide.hip NodeRoute).  Measured round 4 on the Cornell K=128 and
+// K=512 product lines: no gain -- the fallback queries are spread over the
+// leaves (hardly any node passes the two-thirds threshold).
 uint32_t* route_stats(sdmm_stree* t) {
     static const bool on = [] {
         const char* e = std::getenv("SDMM_GUIDE_ROUTE");
-        return !(e && std::strcmp(e, "0") == 0);
+        return e && std::strcmp(e, "1") == 0;
     }();
     return (on && t->droute && t->droute_cap >= 3 * t->nodes.size()) ? t->droute : nullptr;
 }
