@@ -327,6 +327,9 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
     // (without per-block origins every block's spatial forms use the one
     // scene-centre origin kOrigin; borig then has no storage)
     const float o_scene[3] = {kOrigin, kOrigin, kOrigin};
+#ifdef SDMM_SPLIT_DIAG_NOIMAGE   // (diagnostic: a zero coefficient image -- results are not responsibilities)
+    for (int idx = threadIdx.x; idx < NC + WPB * NS + ND; idx += 64 * WPB) smem[idx] = u4{0u, 0u, 0u, 0u};
+#else
     for (int idx = threadIdx.x; idx < R * 8 * 64; idx += 64 * WPB)
         cimg[idx] = coef_frag(ep, Kp, idx >> 9, (idx >> 6) & 7, idx & 63, kBlockOrigin ? borig[idx >> 9] : o_scene);
     if constexpr (DIMG)
@@ -334,6 +337,7 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
             const float* d = ep + EP_DIPI * Kp + 4 * i;
             dimg[i] = f4{d[0], d[1], d[2], d[3]};
         }
+#endif
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
@@ -540,12 +544,19 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
         // staging and stores with no matrix or pair math; the rows are not
         // responsibilities
 #pragma unroll
-        for (int r = 0; r < R; ++r)
+        for (int r = 0; r < R; ++r) {
+            f4 v;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                pdf[r][j] = P3[j & 1] + D3[j >> 1] + (float)(16 * r + j);
-                acc.x += pdf[r][j];
+                v[j] = P3[j & 1] + D3[j >> 1] + (float)(16 * r + j);
+                acc.x += v[j];
             }
+            if constexpr (LR)
+                st[col * 32 + ((4 * r + g) ^ col)] = v;
+            else
+#pragma unroll
+                for (int j = 0; j < 4; ++j) pdf[r][j] = v[j];
+        }
 #elif defined(SDMM_SPLIT_PAIR2)
         {
             // two blocks per step: their 16 MFMAs back to back, then both

@@ -1,0 +1,7 @@
+#!/bin/bash
+# Round-4 session 7: cost of the rare-angle tile redo on the bench batch.
+B=sdmm-mitsuba_amd/build_ab; L=sdmm-mitsuba_amd/lib/libsdmm_amd.so
+export TMPDIR=/tmp
+run() { SDMM_LIB_PATH=$PWD/$1 SDMM_RESP_VARIANT=$2 timeout -k 10 120 python tools/resp_diag.py | \
+        python3 -c "import json,sys,statistics as s; d=json.loads(sys.stdin.read()); print('$1 v$2', d['kernel'], 'median', s.median(d['us']), 'min', min(d['us']), 'max', max(d['us']))"; }
+for i in 1 2; do run $L 0 || exit 1; run $B/noredo.so 0 || exit 1; run $B/noimg.so 0 || exit 1; done
