@@ -297,9 +297,10 @@ __device__ __forceinline__ void pdf_quad(const f4& C, const f4& AD, const f4& BD
 // flush scales them on the way out.  The freed registers allow 3 waves per
 // SIMD (12-wave workgroups: 96 KB of stage + the 64 KB coefficient image fill
 // the 160 KB LDS, so detInv pi is then read from the E-step record instead).
-// (the default since round 4; SDMM_SPLIT_REGROWS: the pdfs in registers
-// until the flush, as in round 3)
-#ifndef SDMM_SPLIT_REGROWS
+// (an option, SDMM_SPLIT_LDSROWS; round 4, four processes each on one box:
+// 177.5-180.6 us per launch against 175.7-176.9 us with the pdfs in registers
+// until the flush at the same 12-wave / 3-per-SIMD configuration, the default)
+#ifdef SDMM_SPLIT_LDSROWS
 constexpr bool kLdsRowsOn = true;
 #else
 constexpr bool kLdsRowsOn = false;
@@ -716,10 +717,10 @@ static void split_cfg(int R, int variant, int* wpb, int* occ) {
     *wpb = 4;
     *occ = 4;
     if (R == 8) {
-        // default: 12-wave workgroups at 3 waves per SIMD (LDS rows, 153
-        // VGPRs; round 4: median 176 us per launch against 186-189 us for the
-        // round-3 configuration, variant 3, which also ran 340-370 us in some
-        // processes -- see DESIGN.md section 4)
+        // default: 12-wave workgroups at 3 waves per SIMD (round 4: 176 us
+        // per launch against 180-188 us for the round-3 configuration,
+        // variant 3, which also ran 340-370 us in some processes -- see
+        // DESIGN.md section 4)
         *wpb = 12; *occ = 3;
         if (variant == 1) { *wpb = 4; *occ = 2; }
         if (variant == 3) { *wpb = 8; *occ = 2; }
