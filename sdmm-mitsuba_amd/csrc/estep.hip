@@ -29,6 +29,8 @@
 //     non-temporal vector stores).
 #include "sdmm_device.h"
 
+#include <cstdlib>
+
 namespace sdmm {
 
 // log2(NORMALIZATION) of mvtn.h:351-352, NORMALIZATION = (float)pow(0.39894228f, 5)
@@ -1199,6 +1201,20 @@ sum_slices_kernel(int ncols, const double* __restrict__ slices, double* __restri
     for (int sl = 0; sl < kReduceSlices; ++sl) t += slices[(int64_t)sl * ncols + o];
     stats[o] = t;
 }
+// The un-centring of one component's spatial statistics (fp64, in place).
+__device__ __forceinline__ void uncenter_component(const double mu[3], double w, double M[5], double C[15]) {
+    // C_pp (entries 0..5: (0,0) (1,0) (1,1) (2,0) (2,1) (2,2))
+    int e = 0;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j <= i; ++j, ++e)
+            C[e] += M[i] * mu[j] + mu[i] * M[j] + w * mu[i] * mu[j];
+    // C_tp: rows 3, 4 (entries 6..8 and 10..12)
+    for (int j = 0; j < 3; ++j) {
+        C[6 + j] += M[3] * mu[j];
+        C[10 + j] += M[4] * mu[j];
+    }
+    for (int i = 0; i < 3; ++i) M[i] = M[i] + w * mu[i];
+}
 // Then one thread per component un-centres its own columns in place (the
 // statistics were accumulated about mu_k).  Together: the former one-thread-
 // per-component kernel operation for operation (bitwise), which read its 21 x
@@ -1212,19 +1228,61 @@ __global__ void uncenter_stats_kernel(const float* __restrict__ ep, int Kp, int 
     double M[5], C[15];   // C: lower triangle, row-major
     for (int i = 0; i < 5; ++i) M[i] = stats[2 + K + 5 * k + i];
     for (int i = 0; i < 15; ++i) C[i] = stats[2 + 6 * K + 15 * k + i];
-    // C_pp (entries 0..5: (0,0) (1,0) (1,1) (2,0) (2,1) (2,2))
-    int e = 0;
-    for (int i = 0; i < 3; ++i)
-        for (int j = 0; j <= i; ++j, ++e)
-            C[e] += M[i] * mu[j] + mu[i] * M[j] + w * mu[i] * mu[j];
-    // C_tp: rows 3, 4 (entries 6..8 and 10..12)
-    for (int j = 0; j < 3; ++j) {
-        C[6 + j] += M[3] * mu[j];
-        C[10 + j] += M[4] * mu[j];
-    }
-    for (int i = 0; i < 3; ++i) M[i] = M[i] + w * mu[i];
+    uncenter_component(mu, w, M, C);
     for (int i = 0; i < 5; ++i) stats[2 + K + 5 * k + i] = M[i];
     for (int i = 0; i < 15; ++i) stats[2 + 6 * K + 15 * k + i] = C[i];
+}
+
+// sum_slices_kernel + uncenter_stats_kernel in ONE launch (the default;
+// SDMM_REDUCE_SPLIT=1 keeps the two launches): workgroup b owns components
+// kSumCB b .. kSumCB b + kSumCB - 1, one thread per column of theirs (their W,
+// M and C columns are three contiguous runs of the compact vector) sums the
+// slices in slice order into LDS, then one thread per component un-centres
+// from LDS and writes the final columns.  Workgroup 0 also sums H and wsum.
+// The same operations in the same order as the two kernels: bitwise equal.
+constexpr int kSumCB = 8;
+__global__ void __launch_bounds__(256)
+sum_uncenter_kernel(int ncols, const double* __restrict__ slices, const float* __restrict__ ep, int Kp, int K,
+                    double* __restrict__ stats) {
+    __shared__ double col[21 * kSumCB];
+    const int k0 = blockIdx.x * kSumCB;
+    const int t = threadIdx.x;
+    auto column = [&](int i) {   // compact index of this workgroup's column i (< 21 kSumCB), or -1
+        int k, o;
+        if (i < kSumCB) { k = k0 + i; o = 2 + k; }
+        else if (i < 6 * kSumCB) { k = k0 + (i - kSumCB) / 5; o = 2 + K + 5 * k0 + (i - kSumCB); }
+        else { k = k0 + (i - 6 * kSumCB) / 15; o = 2 + 6 * K + 15 * k0 + (i - 6 * kSumCB); }
+        return k < K ? o : -1;
+    };
+    if (t < 21 * kSumCB) {
+        const int o = column(t);
+        if (o >= 0) {
+            double v = 0.0;
+#pragma unroll
+            for (int sl = 0; sl < kReduceSlices; ++sl) v += slices[(int64_t)sl * ncols + o];
+            col[t] = v;
+        }
+    } else if (blockIdx.x == 0 && t < 21 * kSumCB + 2) {
+        const int o = t - 21 * kSumCB;   // H, wsum
+        double v = 0.0;
+#pragma unroll
+        for (int sl = 0; sl < kReduceSlices; ++sl) v += slices[(int64_t)sl * ncols + o];
+        stats[o] = v;
+    }
+    __syncthreads();
+    if (t < kSumCB && k0 + t < K) {
+        const int k = k0 + t;
+        const double mu[3] = {(double)ep[EP_MU0 * Kp + k], (double)ep[EP_MU1 * Kp + k],
+                              (double)ep[EP_MU2 * Kp + k]};
+        const double w = col[t];
+        double M[5], C[15];
+        for (int i = 0; i < 5; ++i) M[i] = col[kSumCB + 5 * t + i];
+        for (int i = 0; i < 15; ++i) C[i] = col[6 * kSumCB + 15 * t + i];
+        uncenter_component(mu, w, M, C);
+        stats[2 + k] = w;
+        for (int i = 0; i < 5; ++i) stats[2 + K + 5 * k + i] = M[i];
+        for (int i = 0; i < 15; ++i) stats[2 + 6 * K + 15 * k + i] = C[i];
+    }
 }
 
 // Batched reduction + finalisation: thread (leaf blockIdx.y, component k)
@@ -1280,15 +1338,7 @@ reduce_finalize_batched_kernel(const float* __restrict__ partials, int pstride, 
         double M[5], C[15];
         for (int i = 0; i < 5; ++i) M[i] = red[2 + K + 5 * k + i];
         for (int i = 0; i < 15; ++i) C[i] = red[2 + 6 * K + 15 * k + i];
-        int e = 0;
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j <= i; ++j, ++e)
-                C[e] += M[i] * mu[j] + mu[i] * M[j] + w * mu[i] * mu[j];
-        for (int j = 0; j < 3; ++j) {
-            C[6 + j] += M[3] * mu[j];
-            C[10 + j] += M[4] * mu[j];
-        }
-        for (int i = 0; i < 3; ++i) M[i] = M[i] + w * mu[i];
+        uncenter_component(mu, w, M, C);
         stats[2 + k] = w;
         for (int i = 0; i < 5; ++i) stats[2 + K + 5 * k + i] = M[i];
         for (int i = 0; i < 15; ++i) stats[2 + 6 * K + 15 * k + i] = C[i];
@@ -1454,6 +1504,15 @@ hipError_t launch_reduce_partials(const float* partials, int rows, int pstride, 
                        partials, rows, pstride, Kp, K, scratch);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    static const bool split = [] {
+        const char* v = std::getenv("SDMM_REDUCE_SPLIT");
+        return v && v[0] == '1';
+    }();
+    if (!split) {
+        hipLaunchKernelGGL(sum_uncenter_kernel, dim3((K + kSumCB - 1) / kSumCB), dim3(256), 0, st, ncols, scratch,
+                           ep_for_finalize, Kp, K, stats);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(sum_slices_kernel, dim3((ncols + 255) / 256), dim3(256), 0, st, ncols, scratch, stats);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
