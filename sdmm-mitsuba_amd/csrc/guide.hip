@@ -1581,15 +1581,50 @@ guide_group_fallback_kernel(const float* __restrict__ gp1, int Kp1, int K1, cons
     const int lane = threadIdx.x;
     const int count = *fb_count;
     const int64_t groups = (int64_t)gridDim.x * GPW;
-    for (int64_t gi = (int64_t)blockIdx.x * GPW + lane / G; gi < count; gi += groups) {
-        const int64_t q = fb_list[gi];
+    const int64_t g0 = (int64_t)blockIdx.x * GPW + lane / G;
+    // With node_of (tree wavefront), the chain list entry -> node -> mixture
+    // record of a query is fetched in a three-stage pipeline across this
+    // group's iterations (entry three ahead, node two ahead, record one
+    // ahead), so no iteration starts by waiting on three dependent loads.
+#ifdef SDMM_GROUP_NOPIPE   // (A/B: the chain fetched at the top of every iteration)
+    const bool piped = false;
+#else
+    const bool piped = TREE && node_of != nullptr;
+#endif
+    int64_t qa = 0, qb = 0, qc = 0;   // entries of iterations i + 1, i + 2 (and i + 3 in flight)
+    int nb = 0;                       // node of iteration i + 1
+    GuideMix mc{gp1, Kp1, K1};        // record of iteration i
+    if (piped) {
+        if (g0 < count) {
+            const int64_t q0 = fb_list[g0];
+            mc = tab[node_of[q0]];
+            qc = q0;
+        }
+        if (g0 + groups < count) { qa = fb_list[g0 + groups]; nb = node_of[qa]; }
+        if (g0 + 2 * groups < count) qb = fb_list[g0 + 2 * groups];
+    }
+    for (int64_t gi = g0; gi < count; gi += groups) {
+        int64_t q;
         const float* gp = gp1;
         int Kp = Kp1, K = K1;
-        if constexpr (TREE) {
-            // a listed query has a mixture; node_of: the candidate kernel's find
-            const int node = node_of ? node_of[q] : stree_find_point(nodes, io.c0[q], io.c1[q], io.c2[q]);
-            const GuideMix mx = tab[node];
-            gp = mx.gp; Kp = mx.Kp; K = mx.K;
+        if (piped) {
+            q = qc;
+            gp = mc.gp; Kp = mc.Kp; K = mc.K;
+            // advance the pipeline: record of i + 1, node of i + 2, entry of i + 3
+            const bool h1 = gi + groups < count, h2 = gi + 2 * groups < count, h3 = gi + 3 * groups < count;
+            if (h1) mc = tab[nb];
+            qc = qa;
+            if (h2) nb = node_of[qb];
+            qa = qb;
+            if (h3) qb = fb_list[gi + 3 * groups];
+        } else {
+            q = fb_list[gi];
+            if constexpr (TREE) {
+                // a listed query has a mixture
+                const int node = stree_find_point(nodes, io.c0[q], io.c1[q], io.c2[q]);
+                const GuideMix mx = tab[node];
+                gp = mx.gp; Kp = mx.Kp; K = mx.K;
+            }
         }
         bool ok;
         if constexpr (G == 16) ok = serve_full_group<PDF_ONLY, S>(gp, Kp, K, io, q, lane, gc);
