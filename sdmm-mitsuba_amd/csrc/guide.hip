@@ -326,6 +326,15 @@ struct CandSlots {
     __device__ bool valid(int i) const { return (ck[i * T + tid] >> 15) != 0; }
 };
 
+// A query whose marginal weights are all exactly zero (totalMass 0, e.g. a
+// point far from every component of a narrow, young mixture): the
+// reference's scan takes one zero weight (accum 0 >= cutoff 0), createCdf
+// then fails on the zero sum and the bounce is BSDF only -- what the full-K
+// path computes for it too.  The candidate kernels answer it directly
+// (round 4: optimizeAsync's guided passes sent 99-145 K such queries per pass
+// down the full-K path).
+constexpr int kNoMass = -2;
+
 // returns lastIdx >= 0, or -1: needs the full-K fallback.
 //
 // ONE pass over the components: it forms totalMass exactly as the reference
@@ -381,6 +390,7 @@ __device__ __forceinline__ int build_candidates(const float* gp, int Kp, int K, 
         ++cnt;
     }
     if (!__builtin_isfinite(total)) return -1;
+    if (total == 0.0f) return kNoMass;   // every marginal weight zero: BSDF only (below)
     const float cutoff = (float)(0.99 * (double)total);
     const double tau = ((double)total - (double)cutoff) / (double)K * 0.999;
     if (!(tau > 0.0)) return -1;
@@ -448,6 +458,7 @@ __device__ __forceinline__ int build_candidates_cas(const float* gp, int Kp, int
             ck[i * T + tid] = (unsigned short)rk[i];
         }
     if (!__builtin_isfinite(total)) return -1;
+    if (total == 0.0f) return kNoMass;   // every marginal weight zero: BSDF only (below)
     const float cutoff = (float)(0.99 * (double)total);
     const double tau = ((double)total - (double)cutoff) / (double)K * 0.999;
     if (!(tau > 0.0)) return -1;
@@ -524,6 +535,7 @@ __device__ __forceinline__ int build_candidates_key(const float* gp, int Kp, int
         }
     }
     if (!__builtin_isfinite(total)) return -1;
+    if (total == 0.0f) return kNoMass;   // every marginal weight zero: BSDF only (below)
     const float cutoff = (float)(0.99 * (double)total);
     const double tau = ((double)total - (double)cutoff) / (double)K * 0.999;
     if (!(tau > 0.0)) return -1;
@@ -619,6 +631,10 @@ __device__ __forceinline__ bool serve_cand(const float* gp, int Kp, int K, const
     float accum = 0.0f;
     const int lastIdx = REG ? build_candidates_reg<LCAP>(gp, Kp, K, c, cw, ck, 64, tid, gc.norm3, cap, accum)
                             : build_candidates(gp, Kp, K, c, cw, ck, 64, tid, gc.norm3, cap, accum);
+    if (lastIdx == kNoMass) {
+        write_invalid<PDF_ONLY>(io, q);
+        return false;
+    }
     if (lastIdx < 0) {
         fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
         return true;
@@ -2237,6 +2253,13 @@ __device__ __forceinline__ void product_tail(const float* gp, int Kp, const floa
     if (pio.h) pio.h[q] = h;
 }
 
+// no valid conditional: BSDF only, h = 1 (sdmm_proc.cpp:316-323)
+template <bool PDF_ONLY>
+__device__ __forceinline__ void product_invalid(const GuideIO& io, const ProductIO& pio, int64_t q) {
+    write_invalid<PDF_ONLY>(io, q);
+    if (pio.h) pio.h[q] = 1.0f;
+}
+
 // Candidate path (as guide_cand_kernel: the kept prefix from the per-query LDS
 // list, bit-identical to the full-K selection); queries the list cannot serve
 // exactly go to fb_list for guide_product_wave_kernel.  perm: coherent order.
@@ -2256,6 +2279,10 @@ guide_product_cand_kernel(const float* __restrict__ gp, int Kp, int K, const flo
     float accum = 0.0f;
     // (the register list: K = 512 x 8 lobes 10.81 -> 10.61 ms per 2^18 queries)
     const int lastIdx = build_candidates_reg<LCAP>(gp, Kp, K, c, cw, ck, 64, tid, gc.norm3, cap, accum);
+    if (lastIdx == kNoMass) {   // every marginal weight zero: BSDF only, as the full-K path finds
+        product_invalid<PDF_ONLY>(io, pio, q);
+        return;
+    }
     if (lastIdx < 0) {
         fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
         return;
@@ -2519,6 +2546,10 @@ __device__ __forceinline__ bool serve_product_cand(const float* gp, int Kp, int 
                                                    int32_t* fb_list, int64_t t) {
     float accum = 0.0f;
     const int lastIdx = build_candidates_reg<LCAP>(gp, Kp, K, c, cw, ck, 64, tid, gc.norm3, cap, accum);
+    if (lastIdx == kNoMass) {   // every marginal weight zero: BSDF only, as the full-K path finds
+        product_invalid<PDF_ONLY>(io, pio, q);
+        return false;
+    }
     if (lastIdx < 0) {
         fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
         return true;
@@ -2527,11 +2558,6 @@ __device__ __forceinline__ bool serve_product_cand(const float* gp, int Kp, int 
     return false;
 }
 
-template <bool PDF_ONLY>
-__device__ __forceinline__ void product_invalid(const GuideIO& io, const ProductIO& pio, int64_t q) {
-    write_invalid<PDF_ONLY>(io, q);
-    if (pio.h) pio.h[q] = 1.0f;
-}
 
 template <bool PDF_ONLY, int LCAP>
 __global__ void __launch_bounds__(64)

@@ -380,6 +380,38 @@ def test_guide_indices_bit_exact(pkg, oracle, synth, gpu, plog, K, iters, cap):
     np.testing.assert_allclose(np.linalg.norm(dg[ok], axis=1), 1.0, atol=1e-5)
 
 
+@pytest.mark.parametrize("K,cap", [(16, 40), (128, 40), (128, 0)])
+def test_guide_zero_mass_queries(pkg, oracle, synth, gpu, plog, K, cap):
+    """Queries far from every component: every marginal weight underflows to
+    exactly 0 (totalMass 0).  The reference's scan then takes one zero weight,
+    createCdf fails and the bounce is BSDF only; the candidate kernel answers
+    these directly (round 4) -- the same bits as the oracle and as the full-K
+    path (cap 0), with no query on the fallback list."""
+    import torch
+    b, mix, om = _em_model(pkg, oracle, synth, K, 8192, 3)
+    mix.set_guide_capacity(cap)
+    nq = 2048
+    c, u = synth.sample_queries_near(b, nq)
+    c = (c + 40.0).astype(np.float32)      # far outside the sample box: zero marginal mass
+    c[:, ::2] = synth.sample_queries_near(b, nq)[0][:, ::2]   # interleaved with ordinary queries
+    ct = [torch.from_numpy(c[i].copy()).to(gpu) for i in range(3)]
+    ut = [torch.from_numpy(u[i].copy()).to(gpu) for i in range(3)]
+    d, pdf, comp = mix.guide(ct, ut)
+    torch.cuda.synchronize()
+    dg = np.stack([t.cpu().numpy() for t in d], 1)
+    pg, cg = pdf.cpu().numpy(), comp.cpu().numpy()
+    dr, pr, cr, sr = oracle.guide_batch(om, c.T, u.T)
+    far = np.arange(nq) % 2 == 1
+    assert (cr[far] == -1).all() and (pr[far] == 0).all()   # the reference's answer for them
+    np.testing.assert_array_equal(cg, cr)
+    np.testing.assert_allclose(dg, dr, atol=1e-5)
+    np.testing.assert_allclose(pg, pr, rtol=1e-4, atol=1e-7)
+    if cap > 0:
+        # the far queries never reach the fallback list (only near ones may)
+        plog(f"guide_zero_mass_fallbacks_K{K}", mix.guide_fallback_count(), int((~far).sum()))
+        assert mix.guide_fallback_count() <= int((~far).sum())
+
+
 @pytest.mark.parametrize("cap", [40, 0])
 def test_pdf_batch_matches_oracle(pkg, oracle, synth, gpu, cap):
     import torch
