@@ -3013,6 +3013,17 @@ int st_prepare(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, int* 
     return SDMM_OK;
 }
 
+// smallest tree wavefront served in Morton order (SDMM_TREE_ORDER_MIN, A/B):
+// below it the batch is served as given -- the sort's ~10 launches cost more
+// than the coherence they buy on a small batch
+int64_t tree_order_min() {
+    static const int64_t v = [] {
+        const char* e = std::getenv("SDMM_TREE_ORDER_MIN");
+        return e ? (int64_t)std::atoll(e) : (int64_t)(1 << 14);
+    }();
+    return v;
+}
+
 // SDMM_TREE_ORDER=0 (A/B): the tree wavefronts serve queries in the given
 // order (no Morton sort of the batch)
 bool tree_order_on() {
@@ -3041,7 +3052,7 @@ int st_guide(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const f
     int cus = 256;
     const int r = st_prepare(t, node_mix, nq, &cus);
     if (r) return r;
-    const GuideSortScratch* sort = (nq >= (1 << 14) && tree_order_on()) ? &t->guide_sort : nullptr;
+    const GuideSortScratch* sort = (nq >= tree_order_min() && tree_order_on()) ? &t->guide_sort : nullptr;
     HIP_TRY(launch_guide_tree(t->dnodes, t->dtab, t->tab_kmax, nq, c, u, dgiven, d, pdf, comp, node_out,
                               norm_const(2), norm_const(3), t->tab_cap, t->guide_fb, t->guide_fb + 1,
                               cus, t->stream, sort, pmode,
@@ -3058,7 +3069,7 @@ int st_guide_product(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq,
     int cus = 256;
     const int r = st_prepare(t, node_mix, nq, &cus);
     if (r) return r;
-    const GuideSortScratch* sort = (nq >= (1 << 14) && tree_order_on()) ? &t->guide_sort : nullptr;
+    const GuideSortScratch* sort = (nq >= tree_order_min() && tree_order_on()) ? &t->guide_sort : nullptr;
     HIP_TRY(launch_guide_product_tree(t->dnodes, t->dtab, t->dcctab, t->tab_kmax, nq, c, u, choice, dgiven, d, pdf,
                                       comp, node_out, material, frame, heuristic, bsdf->weights, bsdf->means,
                                       bsdf->covs, bsdf->diffuse, bsdf->B, bsdf->M, norm_const(2), norm_const(3),
