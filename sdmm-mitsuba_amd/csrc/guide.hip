@@ -716,7 +716,7 @@ __global__ void __launch_bounds__(64)
 guide_tree_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __restrict__ tab, int64_t nq,
                        GuideIO io, GuideConsts gc, int cap, int* __restrict__ fb_count,
                        int32_t* __restrict__ fb_list, const int32_t* __restrict__ perm,
-                       int32_t* __restrict__ node_out, NodeRoute rt) {
+                       int32_t* __restrict__ node_out, NodeRoute rt, const uint32_t* __restrict__ skeys, int mb) {
     __shared__ float cw[LCAP * 64];
     __shared__ unsigned short ck[LCAP * 64];
     const int tid = threadIdx.x;
@@ -724,7 +724,8 @@ guide_tree_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __re
     if (t >= nq) return;
     const int64_t q = perm ? (int64_t)perm[t] : t;
     const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
-    const int node = stree_find_point(nodes, c[0], c[1], c[2]);
+    // leaf-major order: the sorted key holds the node (tree_keys_kernel)
+    const int node = skeys ? (int)(skeys[t] >> mb) - 1 : stree_find_point(nodes, c[0], c[1], c[2]);
     if (node_out) node_out[q] = node;
     {
         // the common case (Morton order): every lane of the wave in one leaf,
@@ -2565,7 +2566,8 @@ guide_tree_product_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideM
                                const float* const* __restrict__ cctab, int64_t nq, GuideIO io, ProductIO pio,
                                BsdfTab bt, GuideConsts gc, int cap, int* __restrict__ fb_count,
                                int32_t* __restrict__ fb_list, const int32_t* __restrict__ perm,
-                               int32_t* __restrict__ node_out, NodeRoute rt) {
+                               int32_t* __restrict__ node_out, NodeRoute rt, const uint32_t* __restrict__ skeys,
+                               int mb) {
     __shared__ float cw[LCAP * 64];
     __shared__ unsigned short ck[LCAP * 64];
     const int tid = threadIdx.x;
@@ -2573,7 +2575,8 @@ guide_tree_product_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideM
     if (t >= nq) return;
     const int64_t q = perm ? (int64_t)perm[t] : t;
     const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
-    const int node = stree_find_point(nodes, c[0], c[1], c[2]);
+    // leaf-major order: the sorted key holds the node (tree_keys_kernel)
+    const int node = skeys ? (int)(skeys[t] >> mb) - 1 : stree_find_point(nodes, c[0], c[1], c[2]);
     if (node_out) node_out[q] = node;
     // one leaf for the whole wave (the Morton-ordered common case): uniform
     // control flow; else one distinct leaf per trip (waterfall)
@@ -2700,7 +2703,7 @@ static int morton_bits() {
 size_t guide_sort_temp_bytes(int n) {
     size_t bytes = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                             (const int32_t*)nullptr, (int32_t*)nullptr, n, 0, 30);
+                                             (const int32_t*)nullptr, (int32_t*)nullptr, n, 0, 32);
     return bytes;
 }
 
@@ -2715,6 +2718,51 @@ static hipError_t coherent_order(const float* const c[3], int n, uint32_t* keys_
     if (e != hipSuccess) return e;
     return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, idx_in, idx_out, n, 0, 3 * bits,
                                               st);
+}
+
+// Leaf-major coherent order for the tree wavefronts: key = (node + 1) in the
+// high bits, the Morton code of c (mb / 3 bits per axis) in the low ones, so
+// a wave's queries share ONE leaf except at the seams between leaves (plain
+// Morton runs cross leaf boxes, whose planes sit at sample means, wherever
+// the Z-curve does).  The sorted keys then carry every query's node: the
+// candidate kernel reads node = (key >> mb) - 1 instead of walking the tree.
+__global__ void tree_keys_kernel(const STNodeDev* __restrict__ nodes, const float* __restrict__ c0,
+                                 const float* __restrict__ c1, const float* __restrict__ c2, int n, int mb,
+                                 uint32_t* __restrict__ keys, int32_t* __restrict__ idx) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const float x = c0[q], y = c1[q], z = c2[q];
+    const int node = stree_find_point(nodes, x, y, z);
+    const int b = mb / 3;
+    const uint32_t m = spread3(quantb(x, b)) | (spread3(quantb(y, b)) << 1) | (spread3(quantb(z, b)) << 2);
+    keys[q] = ((uint32_t)(node + 1) << mb) | m;
+    idx[q] = q;
+}
+// node bits for a tree of nn nodes (node + 1 < 2^nb); 0: no leaf-major order
+static int leaf_key_bits(int nn) {
+    int nb = 1;
+    while (nb < 32 && (1ll << nb) <= (long long)nn) ++nb;
+    return nb <= 20 ? nb : 0;
+}
+static hipError_t leaf_order(const STNodeDev* nodes, int nn, const float* const c[3], int n, uint32_t* keys_in,
+                             uint32_t* keys_out, int32_t* idx_in, int32_t* idx_out, void* temp, size_t temp_bytes,
+                             hipStream_t st, int* mb_out) {
+    const int nb = leaf_key_bits(nn);
+    const int mb = 32 - nb;
+    *mb_out = mb;
+    hipLaunchKernelGGL(tree_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nodes, c[0], c[1], c[2],
+                       n, mb, keys_in, idx_in);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, idx_in, idx_out, n, 0, 32, st);
+}
+// SDMM_LEAF_ORDER=0 (A/B): the tree wavefronts keep the plain Morton order
+static bool leaf_order_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("SDMM_LEAF_ORDER");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 static GuideIO make_io(const float* const c[3], const float* const u[3], const float* const dgiven[3],
@@ -2762,19 +2810,20 @@ static hipError_t launch_cand(int cap, dim3 grid, hipStream_t st, const float* g
 template <bool PDF_ONLY>
 static hipError_t launch_tree_cand(int cap, dim3 grid, hipStream_t st, const STNodeDev* nd, const GuideMix* tb,
                                    int64_t nq, const GuideIO& io, GuideConsts gc, int* fb_count, int32_t* fb_list,
-                                   const int32_t* perm, int32_t* node_out, const NodeRoute& rt) {
+                                   const int32_t* perm, int32_t* node_out, const NodeRoute& rt,
+                                   const uint32_t* skeys, int mb) {
     if (cap <= 16)
         hipLaunchKernelGGL((guide_tree_cand_kernel<PDF_ONLY, 16>), grid, dim3(64), 0, st, nd, tb, nq, io, gc, cap,
-                           fb_count, fb_list, perm, node_out, rt);
+                           fb_count, fb_list, perm, node_out, rt, skeys, mb);
     else if (cap <= 24)
         hipLaunchKernelGGL((guide_tree_cand_kernel<PDF_ONLY, 24>), grid, dim3(64), 0, st, nd, tb, nq, io, gc, cap,
-                           fb_count, fb_list, perm, node_out, rt);
+                           fb_count, fb_list, perm, node_out, rt, skeys, mb);
     else if (cap <= 40)
         hipLaunchKernelGGL((guide_tree_cand_kernel<PDF_ONLY, 40>), grid, dim3(64), 0, st, nd, tb, nq, io, gc, cap,
-                           fb_count, fb_list, perm, node_out, rt);
+                           fb_count, fb_list, perm, node_out, rt, skeys, mb);
     else
         hipLaunchKernelGGL((guide_tree_cand_kernel<PDF_ONLY, kGuideCap>), grid, dim3(64), 0, st, nd, tb, nq, io,
-                           gc, cap, fb_count, fb_list, perm, node_out, rt);
+                           gc, cap, fb_count, fb_list, perm, node_out, rt, skeys, mb);
     return hipGetLastError();
 }
 
@@ -2854,14 +2903,22 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
     GuideConsts gc{norm2, norm3};
     hipError_t e = hipMemsetAsync(fb_count, 0, sizeof(int), st);
     if (e != hipSuccess) return e;
+    const STNodeDev* nd = (const STNodeDev*)nodes;
     const int32_t* perm = nullptr;
+    const uint32_t* skeys = nullptr;   // leaf-major sorted keys (node in the high bits)
+    int mb = 0;
     if (sort) {
-        e = coherent_order(c, (int)nq, sort->keys[0], sort->keys[1], sort->idx[0], sort->idx[1], sort->temp,
-                           sort->temp_bytes, st);
+        if (leaf_order_on() && leaf_key_bits(nn) > 0) {
+            e = leaf_order(nd, nn, c, (int)nq, sort->keys[0], sort->keys[1], sort->idx[0], sort->idx[1], sort->temp,
+                           sort->temp_bytes, st, &mb);
+            skeys = sort->keys[1];
+        } else {
+            e = coherent_order(c, (int)nq, sort->keys[0], sort->keys[1], sort->idx[0], sort->idx[1], sort->temp,
+                               sort->temp_bytes, st);
+        }
         if (e != hipSuccess) return e;
         perm = sort->idx[1];
     }
-    const STNodeDev* nd = (const STNodeDev*)nodes;
     const GuideMix* tb = (const GuideMix*)tab;
     const dim3 grid((unsigned)((nq + T - 1) / T));
     const int fb_blocks = cus * 16;
@@ -2872,11 +2929,15 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
     e = launch_route(rt, st);
     if (e != hipSuccess) return e;
     // every query's node as the candidate kernel finds it (the caller's
-    // node_out, else the sorted-keys buffer, free once the order is built):
-    // the fallback kernels read it instead of walking the tree again
-    int32_t* const node_of = node_out ? node_out : (sort ? (int32_t*)sort->keys[1] : nullptr);
-    e = dgiven ? launch_tree_cand<true>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_of, rt)
-               : launch_tree_cand<false>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_of, rt);
+    // node_out, else a sort buffer free once the order is built: the sorted
+    // keys with the plain Morton order, the sort's index input with the
+    // leaf-major one): the fallback kernels read it instead of walking the tree
+    int32_t* const node_of = node_out ? node_out
+                                      : (sort ? (skeys ? sort->idx[0] : (int32_t*)sort->keys[1]) : nullptr);
+    e = dgiven ? launch_tree_cand<true>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_of, rt,
+                                        skeys, mb)
+               : launch_tree_cand<false>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_of, rt,
+                                         skeys, mb);
     if (e != hipSuccess) return e;
     if (fb2 && kmax <= kGroupKMax) {
         e = hipMemsetAsync(fb2, 0, sizeof(int), st);
@@ -3034,14 +3095,22 @@ hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const v
     const BsdfTab bt{bw, bmean, bcov, B, M, diffuse};
     hipError_t e = hipMemsetAsync(fb_count, 0, sizeof(int), st);
     if (e != hipSuccess) return e;
+    const STNodeDev* nd = (const STNodeDev*)nodes;
     const int32_t* perm = nullptr;
+    const uint32_t* skeys = nullptr;   // leaf-major sorted keys (see launch_guide_tree)
+    int mb = 0;
     if (sort) {
-        e = coherent_order(c, (int)nq, sort->keys[0], sort->keys[1], sort->idx[0], sort->idx[1], sort->temp,
-                           sort->temp_bytes, st);
+        if (leaf_order_on() && leaf_key_bits(nn) > 0) {
+            e = leaf_order(nd, nn, c, (int)nq, sort->keys[0], sort->keys[1], sort->idx[0], sort->idx[1], sort->temp,
+                           sort->temp_bytes, st, &mb);
+            skeys = sort->keys[1];
+        } else {
+            e = coherent_order(c, (int)nq, sort->keys[0], sort->keys[1], sort->idx[0], sort->idx[1], sort->temp,
+                               sort->temp_bytes, st);
+        }
         if (e != hipSuccess) return e;
         perm = sort->idx[1];
     }
-    const STNodeDev* nd = (const STNodeDev*)nodes;
     const GuideMix* tb = (const GuideMix*)tab;
     const float* const* cc = (const float* const*)cctab;
     const dim3 grid((unsigned)((nq + 63) / 64));
@@ -3053,10 +3122,11 @@ hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const v
     e = launch_route(rt, st);
     if (e != hipSuccess) return e;
     // every query's node from the candidate kernel (see launch_guide_tree)
-    int32_t* const node_of = node_out ? node_out : (sort ? (int32_t*)sort->keys[1] : nullptr);
+    int32_t* const node_of = node_out ? node_out
+                                      : (sort ? (skeys ? sort->idx[0] : (int32_t*)sort->keys[1]) : nullptr);
 #define SDMM_TREE_PRODUCT_CAND(P, L)                                                                         \
     hipLaunchKernelGGL((guide_tree_product_cand_kernel<P, L>), grid, dim3(64), 0, st, nd, tb, cc, nq, iox, pio, \
-                       bt, gc, cap, fb_count, fb_list, perm, node_of, rt)
+                       bt, gc, cap, fb_count, fb_list, perm, node_of, rt, skeys, mb)
     if (pdf_only) {
         if (cap <= 16) SDMM_TREE_PRODUCT_CAND(true, 16);
         else if (cap <= 24) SDMM_TREE_PRODUCT_CAND(true, 24);
