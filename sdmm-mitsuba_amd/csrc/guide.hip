@@ -2726,6 +2726,17 @@ static hipError_t coherent_order(const float* const c[3], int n, uint32_t* keys_
 // Morton runs cross leaf boxes, whose planes sit at sample means, wherever
 // the Z-curve does).  The sorted keys then carry every query's node: the
 // candidate kernel reads node = (key >> mb) - 1 instead of walking the tree.
+// A/B: total key bits of the leaf-major order (0: 32, the Morton code at
+// (32 - node bits) / 3 bits per axis) and, when set, which 30-bit Morton
+// levels fill the low bits
+#ifndef SDMM_LEAF_KEY_BITS
+#define SDMM_LEAF_KEY_BITS 0
+#endif
+#ifndef SDMM_LEAF_MORTON_SHIFT
+#define SDMM_LEAF_MORTON_SHIFT -1
+#endif
+constexpr int kLeafKeyBits = SDMM_LEAF_KEY_BITS;
+constexpr int kLeafMortonShift = SDMM_LEAF_MORTON_SHIFT;
 __global__ void tree_keys_kernel(const STNodeDev* __restrict__ nodes, const float* __restrict__ c0,
                                  const float* __restrict__ c1, const float* __restrict__ c2, int n, int mb,
                                  uint32_t* __restrict__ keys, int32_t* __restrict__ idx) {
@@ -2733,8 +2744,16 @@ __global__ void tree_keys_kernel(const STNodeDev* __restrict__ nodes, const floa
     if (q >= n) return;
     const float x = c0[q], y = c1[q], z = c2[q];
     const int node = stree_find_point(nodes, x, y, z);
-    const int b = mb / 3;
-    const uint32_t m = spread3(quantb(x, b)) | (spread3(quantb(y, b)) << 1) | (spread3(quantb(z, b)) << 2);
+    uint32_t m;
+    if (kLeafMortonShift >= 0) {
+        // mb bits of the 30-bit Morton code starting at kLeafMortonShift: the
+        // levels that vary inside a leaf (the top ones are constant there)
+        const uint32_t m30 = spread3(quantb(x, 10)) | (spread3(quantb(y, 10)) << 1) | (spread3(quantb(z, 10)) << 2);
+        m = (m30 >> kLeafMortonShift) & ((1u << mb) - 1u);
+    } else {
+        const int b = mb / 3;
+        m = spread3(quantb(x, b)) | (spread3(quantb(y, b)) << 1) | (spread3(quantb(z, b)) << 2);
+    }
     keys[q] = ((uint32_t)(node + 1) << mb) | m;
     idx[q] = q;
 }
@@ -2748,13 +2767,14 @@ static hipError_t leaf_order(const STNodeDev* nodes, int nn, const float* const 
                              uint32_t* keys_out, int32_t* idx_in, int32_t* idx_out, void* temp, size_t temp_bytes,
                              hipStream_t st, int* mb_out) {
     const int nb = leaf_key_bits(nn);
-    const int mb = 32 - nb;
+    const int mb = kLeafKeyBits > nb ? kLeafKeyBits - nb : 32 - nb;
     *mb_out = mb;
     hipLaunchKernelGGL(tree_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nodes, c[0], c[1], c[2],
                        n, mb, keys_in, idx_in);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, idx_in, idx_out, n, 0, 32, st);
+    return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, idx_in, idx_out, n, 0, nb + mb,
+                                              st);
 }
 // SDMM_LEAF_ORDER=0 (A/B): the tree wavefronts keep the plain Morton order
 static bool leaf_order_on() {
