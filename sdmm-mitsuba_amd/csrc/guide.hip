@@ -499,7 +499,11 @@ template <int LCAP>
 __device__ __forceinline__ int build_candidates_key(const float* gp, int Kp, int K, const float c[3], float* cw,
                                                     unsigned short* ck, int T, int tid, float norm3, int cap,
                                                     float& accum) {
-    static_assert(LCAP % 8 == 0, "chunks of eight slots");
+#ifndef SDMM_RIPPLE_CHUNK
+#define SDMM_RIPPLE_CHUNK 8   // slots per skippable chunk (A/B)
+#endif
+    constexpr int CH = (LCAP % SDMM_RIPPLE_CHUNK == 0) ? SDMM_RIPPLE_CHUNK : 8;
+    static_assert(LCAP % CH == 0, "whole chunks");
     double L[LCAP];
 #pragma unroll
     for (int i = 0; i < LCAP; ++i) L[i] = 0.0;
@@ -514,10 +518,10 @@ __device__ __forceinline__ int build_candidates_key(const float* gp, int Kp, int
         if (!(w > 0.0f) || w < total * skip_f) continue;
         double x = cand_key(w, k);
 #pragma unroll
-        for (int c0 = 0; c0 < LCAP; c0 += 8) {
-            if (!__any(x > L[c0 + 7])) continue;
+        for (int c0 = 0; c0 < LCAP; c0 += CH) {
+            if (!__any(x > L[c0 + CH - 1])) continue;
 #pragma unroll
-            for (int i = c0; i < c0 + 8; ++i) {
+            for (int i = c0; i < c0 + CH; ++i) {
                 const double hi = __builtin_fmax(L[i], x);
                 x = __builtin_fmin(L[i], x);
                 L[i] = hi;
