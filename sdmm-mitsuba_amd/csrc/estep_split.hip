@@ -306,6 +306,13 @@ constexpr bool kLdsRowsOn = true;
 constexpr bool kLdsRowsOn = false;
 #endif
 
+// the default block loop's scheduling fences (SDMM_SPLIT_NOFENCE, A/B: the
+// compiler schedules the MFMAs, the fragment reads and the pair math freely)
+#ifdef SDMM_SPLIT_NOFENCE
+#define SPLIT_FENCE() ((void)0)
+#else
+#define SPLIT_FENCE() __builtin_amdgcn_sched_barrier(0)
+#endif
 template <int R, int WPB, int OCC>
 __global__ void __launch_bounds__(64 * WPB, OCC)
 estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, int64_t n, int64_t nwaves,
@@ -634,7 +641,7 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
             for (int r = 0; r < R; ++r) {
                 f4 D[8];
                 forms(F[r & 1], BS[r & 1], Bd, D);
-                __builtin_amdgcn_sched_barrier(0);
+                SPLIT_FENCE();
 #ifndef SDMM_SPLIT_PREFETCH
 #define SDMM_SPLIT_PREFETCH 0
 #endif
@@ -647,7 +654,7 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
                     for (int f = 0; f < SDMM_SPLIT_PREFETCH; ++f)
                         F[(r + 1) & 1][f] = __builtin_bit_cast(bf8, cimg[((r + 1) * 8 + f) * 64 + lane]);
                 }
-                __builtin_amdgcn_sched_barrier(0);
+                SPLIT_FENCE();
                 pair_math(r, Tag<false>{}, D, dp[r & 1]);
                 if (r + 1 < R) {
 #pragma unroll
@@ -660,7 +667,7 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
                 }
                 // the next block's spatial sample fragment, off the MFMA issue path
                 if (r + 1 < R) BS[(r + 1) & 1] = kBlockOrigin ? pfrag(P3, borig[r + 1]) : Bs0;
-                __builtin_amdgcn_sched_barrier(0);
+                SPLIT_FENCE();
             }
         }
 #endif
