@@ -100,6 +100,16 @@ __device__ __forceinline__ float div_exact(float x, const float* gp, int f, int 
     return (float)((double)x * r);
 }
 
+// x / d for many x and one d, bit for bit as the float division (the same
+// argument as div_exact: RN64(1 / d) once, then one double product per
+// quotient rounded to float; FTZ flushes a denormal quotient in both).  The
+// float division is ~10 instructions with two denormal-mode switches.
+struct DivBy {
+    double r;
+    __device__ explicit DivBy(float d) : r(1.0 / (double)d) {}
+    __device__ float operator()(float x) const { return (float)((double)x * r); }
+};
+
 // MVN<3,3>::pdf with the forward substitution of LLT::matrixL().solve:
 // marginal_q is the squared Mahalanobis distance, marginal_pdf_q the pdf.
 __device__ __forceinline__ float marginal_q(const float* gp, int Kp, int k, const float c[3]) {
@@ -240,10 +250,11 @@ __device__ __forceinline__ QueryOut finish_query(const float* gp, int Kp, const 
         sum2 += wi;
     }
     if (lastIdx == 0 || sum2 == 0.0f) return o;   // createCdf(true) fails: BSDF only
+    const DivBy by_sum2(sum2);
     auto slot_w = [&](int i) {
         float wi = S.valid(i) ? S.weight(i) : 0.0f;
         if (scaled) wi = wi * invSum;
-        return wi / sum2;
+        return by_sum2(wi);
     };
     float dir[3];
     if (!dir_in) {
@@ -1040,8 +1051,10 @@ __device__ __forceinline__ float wave_slot_weights(int lastIdx, float accum, con
         }
         sum2 = seq_sum(sum2, wi, min(64, lastIdx - base));
     }
-    if (lastIdx > 0 && sum2 != 0.0f)
-        for (int i = lane; i < lastIdx; i += 64) L.fw[i] = L.fw[i] / sum2;
+    if (lastIdx > 0 && sum2 != 0.0f) {
+        const DivBy by_sum2(sum2);
+        for (int i = lane; i < lastIdx; i += 64) L.fw[i] = by_sum2(L.fw[i]);
+    }
     __syncthreads();
     return sum2;
 }
@@ -1302,8 +1315,9 @@ __device__ __forceinline__ bool serve_full_group(const float* gp, int Kp, int K,
     float outpdf = 0.0f;
     int outcomp = -1;
     if (lastIdx > 0 && sum2 != 0.0f) {
+        const DivBy by_sum2(sum2);
 #pragma unroll
-        for (int i = 0; i < S; ++i) f[i] = f[i] / sum2;
+        for (int i = 0; i < S; ++i) f[i] = by_sum2(f[i]);
         float dir[3];
         if (!pdf_q) {
             // sampleDiscreteCdf: lower_bound == first slot with cdf >= u, else the tie walk
@@ -1505,7 +1519,8 @@ __device__ __forceinline__ bool serve_full_group_g(const float* gp, int Kp, int 
     float outpdf = 0.0f;
     int outcomp = -1;
     if (lastIdx > 0 && sum2 != 0.0f) {
-        auto f = [&](int i) { return fs(i) / sum2; };
+        const DivBy by_sum2(sum2);
+        auto f = [&](int i) { return by_sum2(fs(i)); };
         float dir[3];
         if (!pdf_q) {
             // sampleDiscreteCdf: lower_bound == first slot with cdf >= u, else the tie walk
@@ -2031,10 +2046,11 @@ __device__ __forceinline__ void for_each_pair(const float* gp, int Kp, const flo
                                               const Slots& S, const BsdfTab& bt, int b, const float F[9],
                                               float norm2, bool lazy, Fn&& fn) {
     int p = 0;
+    const DivBy by_sum2(sum2);
     for (int i = 0; i < lastIdx; ++i) {
         float wi = S.valid(i) ? S.weight(i) : 0.0f;
         if (scaled) wi = wi * invSum;
-        wi = wi / sum2;
+        wi = by_sum2(wi);
         if (wi == 0.0f) continue;
         const int k = S.comp(i);
         float e[3], to_i[9], ci[4];
@@ -2064,7 +2080,7 @@ __device__ __forceinline__ float eval_pair(const float* gp, int Kp, const float*
                                            ProdComp& pc) {
     float wi = S.valid(i) ? S.weight(i) : 0.0f;
     if (scaled) wi = wi * invSum;
-    wi = wi / sum2;
+    wi = DivBy(sum2)(wi);
     const int k = S.comp(i);
     float e[3], to_i[9], ci[4];
     cond_mean_dir_x(gp, Kp, k, c, e);
@@ -2753,7 +2769,7 @@ __global__ void tree_keys_kernel(const STNodeDev* __restrict__ nodes, const floa
         // mb bits of the 30-bit Morton code starting at kLeafMortonShift: the
         // levels that vary inside a leaf (the top ones are constant there)
         const uint32_t m30 = spread3(quantb(x, 10)) | (spread3(quantb(y, 10)) << 1) | (spread3(quantb(z, 10)) << 2);
-        m = (m30 >> kLeafMortonShift) & ((1u << mb) - 1u);
+        m = (m30 >> (kLeafMortonShift >= 0 ? kLeafMortonShift : 0)) & ((1u << mb) - 1u);
     } else {
         const int b = mb / 3;
         m = spread3(quantb(x, b)) | (spread3(quantb(y, b)) << 1) | (spread3(quantb(z, b)) << 2);
