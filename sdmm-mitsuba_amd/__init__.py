@@ -97,6 +97,8 @@ def lib():
         L.sdmm_synchronize.argtypes = [C.c_void_p]
         L.sdmm_init_hemisphere.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_float,
                                            C.c_float, C.c_uint64]
+        L.sdmm_init_hemisphere_batched.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_float,
+                                                   C.c_void_p, C.c_void_p]
         L.sdmm_hemisphere_init_host.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_float, C.c_float,
                                                 C.c_uint64] + [C.c_void_p] * 5
         L.sdmm_em_step.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
@@ -258,6 +260,21 @@ def kmeanspp_select(samples, normals, seg, n_pos, uniforms, stream=None):
                                       nl, n_pos, u.ctypes.data, dev, st, idx.ctypes.data, pos.ctypes.data,
                                       nrm.ctypes.data))
     return idx, pos, nrm
+
+
+def init_hemisphere_batched(mixes, positions, normals, depth_prior, min_spatial_distance, seeds):
+    """uniformHemisphereInit for many mixtures of one K (the guiding model's
+    new leaves): mixture i from positions / normals [i] (K/8 x 3 each), its
+    spatial distance and seed; the staging block is generated on the device."""
+    n = len(mixes)
+    K = mixes[0].K if n else 0
+    pos = np.ascontiguousarray(positions, np.float32).reshape(n, K // 8, 3)
+    nrm = np.ascontiguousarray(normals, np.float32).reshape(n, K // 8, 3)
+    dist = np.ascontiguousarray(np.broadcast_to(np.asarray(min_spatial_distance, np.float32), (n,)))
+    sd = np.ascontiguousarray(np.broadcast_to(np.asarray(seeds, np.uint64), (n,)))
+    hs = (C.c_void_p * max(n, 1))(*[m.h for m in mixes])
+    _check(lib().sdmm_init_hemisphere_batched(hs, n, pos.ctypes.data, nrm.ctypes.data, depth_prior,
+                                              dist.ctypes.data, sd.ctypes.data))
 
 
 def init_hemisphere_kmeanspp_batched(mixes, samples, normals, seg, depth_prior, min_spatial_distance, seeds):

@@ -720,6 +720,133 @@ set_all_batched_kernel(int K, int Kp, const InitDesc* __restrict__ tab, const ch
     for (int kk = t; kk < Kp; kk += blockDim.x) pack_component(kk, K, Kp, d.C, d.ep, d.gp, norm5);
 }
 
+// uniformHemisphereInit (mixture_model_init.h:79-242, the kMeansPlusPlus ==
+// false branch; :130-138 the k-means++ draws skipped) on the device: mixture
+// b's staging block, in the layout set_all_batched_kernel reads, from its npos
+// positions / normals, spatial distance and PCG32 seed.  The host version
+// (sdmm_api.cpp hemisphere_init) wrote ~35 KB per K = 128 mixture into pinned
+// memory for an upload; here only the inputs travel.  Same float and double
+// operations in the same order (contraction off; the float square root taken
+// through the correctly rounded double one, as the host's std::sqrt(float)
+// rounds), so the results are the host's bit for bit except where the
+// device's double cos / sin and the host libm's round to different floats.
+struct HemiGenArgs {
+    const float* pos;      // [n][npos][3]
+    const float* nrm;      // [n][npos][3]
+    const float* dist;     // [n] minimum spatial distance
+    const uint64_t* seed;  // [n]
+    int skip;              // draws already taken from each stream
+    float depth_prior;
+};
+struct Pcg32Dev {
+    uint64_t state, inc;
+    __device__ void seed(uint64_t initstate, uint64_t initseq) {
+        state = 0u;
+        inc = (initseq << 1u) | 1u;
+        next_uint();
+        state += initstate;
+        next_uint();
+    }
+    __device__ uint32_t next_uint() {
+        const uint64_t old = state;
+        state = old * 0x5851f42d4c957f2dULL + inc;
+        const uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        const uint32_t rot = (uint32_t)(old >> 59u);
+        return (xs >> rot) | (xs << ((~rot + 1u) & 31));
+    }
+    __device__ float next_float() {
+        return __builtin_bit_cast(float, (next_uint() >> 9) | 0x3f800000u) - 1.0f;
+    }
+};
+__device__ static void coordinates_fl(const float n[3], float to[9]) {
+    float sign = copysignf(1.0f, n[2]);
+    const float a = -1.0f / (sign + n[2]);
+    const float b = n[0] * n[1] * a;
+    to[0] = 1.0f + sign * n[0] * n[0] * a; to[1] = sign * b; to[2] = -sign * n[0];
+    to[3] = b; to[4] = sign + n[1] * n[1] * a; to[5] = -n[1];
+    to[6] = n[0]; to[7] = n[1]; to[8] = n[2];
+}
+__global__ void __launch_bounds__(256)
+hemi_gen_batched_kernel(int K, HemiGenArgs a, char* __restrict__ staging, size_t per) {
+    extern __shared__ float u[];   // the stream's 10 draws per position, in draw order
+    const int npos = K / 8;
+    const int b = blockIdx.x;
+    if (threadIdx.x == 0) {
+        Pcg32Dev rng;
+        rng.seed(a.seed[b], 0xda3e39cb94b95bdbULL);
+        for (int i = 0; i < a.skip; ++i) (void)rng.next_uint();
+        for (int i = 0; i < 10 * npos; ++i) u[i] = rng.next_float();
+    }
+    __syncthreads();
+    const double PI = 3.14159265358979323846;
+    char* blk = staging + per * (size_t)b;
+    float* pw = (float*)blk;
+    float* pm = (float*)(blk + 4 * (size_t)K);
+    float* pc = (float*)(blk + 28 * (size_t)K);
+    float* pb = (float*)(blk + 128 * (size_t)K);
+    float* pd = (float*)(blk + 228 * (size_t)K);
+    const float maxRadiusSqr = (float)10.644640675668422;   // chi2(6).quantile(0.9)
+    const float minDist = a.dist[b];
+    const float widthVarSqr = (float)(0.5 * (double)minDist * (double)minDist / (double)maxRadiusSqr);
+    const float depthVarSqr = a.depth_prior * a.depth_prior / maxRadiusSqr;
+    const float nThetas = 2.0f, nPhis = 4.0f;
+    const float directionalInit = 1.0f / (nThetas * nPhis);
+    const float dcov = (float)(2.0 * PI * (double)directionalInit);
+    for (int k = threadIdx.x; k < K; k += blockDim.x) {
+        const int pi = k >> 3, ti = (k >> 2) & 1, fi = k & 3;
+        const float* p = a.pos + 3 * ((size_t)npos * b + pi);
+        const float* n = a.nrm + 3 * ((size_t)npos * b + pi);
+        float to[9];
+        coordinates_fl(n, to);
+        const float* s = to;
+        const float* t = to + 3;
+        const float* ud = u + 10 * pi + 5 * ti;   // theta draw, then the four phi draws
+        float theta = 0.0f;
+        for (int j = 0; j <= ti; ++j) {
+            const float rn = (float)(((double)u[10 * pi + 5 * j] - 0.5) * 2e-1);
+            theta = (float)((double)theta + (0.5 * PI / (double)(nThetas + 1.0f) + (double)rn));
+        }
+        const float cosTheta = (float)cos((double)theta);
+        const float sinTheta = (float)sqrt((double)(1.0f - cosTheta * cosTheta));
+        float phi = 0.0f;
+        for (int j = 0; j <= fi; ++j) {
+            const float rn = (float)(((double)ud[1 + j] - 0.5) * 1e-1);
+            phi = (float)((double)phi + (2.0 * PI / (double)nPhis + (double)rn));
+        }
+        const float sinPhi = (float)sin((double)phi), cosPhi = (float)cos((double)phi);
+        const float dl0 = sinTheta * cosPhi, dl1 = sinTheta * sinPhi, dl2 = cosTheta;
+        float* mean = pm + 6 * k;
+        for (int i = 0; i < 3; ++i) mean[i] = p[i];
+        for (int i = 0; i < 3; ++i) mean[3 + i] = (s[i] * dl0 + t[i] * dl1) + n[i] * dl2;
+        float* cov = pc + 25 * k;
+        float* bp = pb + 25 * k;
+        for (int i = 0; i < 25; ++i) {
+            cov[i] = (i % 6 == 0) ? 1.0f : 0.0f;
+            bp[i] = (i % 6 == 0) ? 1.0f : 0.0f;
+        }
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {
+                cov[5 * i + j] = (s[i] * s[j] * widthVarSqr + t[i] * t[j] * widthVarSqr) + n[i] * n[j] * depthVarSqr;
+                bp[5 * i + j] = s[i] * s[j] * 1e-4f + t[i] * t[j] * 1e-4f + n[i] * n[j] * 1e-4f;
+            }
+        cov[18] = dcov; cov[24] = dcov;
+        bp[18] = 1e-5f; bp[24] = 1e-5f;
+        pw[k] = (float)(1.0 / (double)K);   // 1.0f / (float)K, correctly rounded
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) pd[9 * k + 3 * i + j] = n[i] * n[j] * 1e-6f;
+    }
+}
+
+hipError_t launch_hemi_gen_batched(int n, int K, const float* pos, const float* nrm, const float* dist,
+                                   const uint64_t* seed, int skip, float depth_prior, void* staging, size_t per,
+                                   hipStream_t st) {
+    const HemiGenArgs a{pos, nrm, dist, seed, skip, depth_prior};
+    const int threads = K < 64 ? 64 : (K > 256 ? 256 : K);
+    hipLaunchKernelGGL(hemi_gen_batched_kernel, dim3((unsigned)n), dim3(threads), sizeof(float) * 10 * (size_t)(K / 8),
+                       st, K, a, (char*)staging, per);
+    return hipGetLastError();
+}
+
 hipError_t launch_set_all_batched(int n, int K, int Kp, const void* tab, const void* staging, size_t per, float norm5,
                                   hipStream_t st) {
     const int threads = Kp < 64 ? 64 : (Kp > 512 ? 512 : Kp);

@@ -63,6 +63,9 @@ hipError_t launch_pack_all(int K, int Kp, const CanonDev& C, float* ep, float* g
                            hipStream_t st);
 hipError_t launch_init_state(int K, const double* scal, const float* bprior, float eps, double* sc, float* bp,
                              float* bd, hipStream_t st);
+hipError_t launch_hemi_gen_batched(int n, int K, const float* pos, const float* nrm, const float* dist,
+                                   const uint64_t* seed, int skip, float depth_prior, void* staging, size_t per,
+                                   hipStream_t st);
 hipError_t launch_set_all_batched(int n, int K, int Kp, const void* tab, const void* staging, size_t per, float norm5,
                                   hipStream_t st);
 hipError_t launch_copy_many(int n, const void* src_tab, const void* dst_tab, size_t bytes, hipStream_t st);
@@ -1144,24 +1147,20 @@ static int upload_and_set(sdmm_mix* m, const float* weights, const float* means,
     return SDMM_OK;
 }
 
+static int init_hemisphere_batched_impl(sdmm_mix* const* mixes, int n, const float* positions,
+                                        const float* normals, float depth_prior, const float* min_spatial_distance,
+                                        const uint64_t* seeds, int skip);
+
 int sdmm_init_hemisphere(sdmm_mix* m, const float* positions, const float* normals, int n_pos,
                          float depth_prior, float min_spatial_distance, uint64_t seed) {
     if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
     HIP_TRY(hipSetDevice(m->device));
     if (n_pos * 8 != m->K) return fail(SDMM_E_INVALID, "K must equal 8 * n_pos");
-    const size_t K = (size_t)m->K;
-    std::vector<float> w(K), mean(6 * K), cov(25 * K), bp(25 * K), bd(9 * K);
-    int r = sdmm_hemisphere_init_host(positions, normals, n_pos, depth_prior, min_spatial_distance, seed,
-                                      w.data(), mean.data(), cov.data(), bp.data(), bd.data());
-    if (r) return r;
-    HIP_TRY(hipMemcpyAsync(m->S.bPriors, bp.data(), 4 * 25 * K, hipMemcpyHostToDevice, m->stream));
-    HIP_TRY(hipMemcpyAsync(m->S.bDepth, bd.data(), 4 * 9 * K, hipMemcpyHostToDevice, m->stream));
-    return upload_and_set(m, w.data(), mean.data(), cov.data());
+    if (!positions || !normals) return fail(SDMM_E_INVALID, "invalid argument to sdmm_init_hemisphere");
+    // the batched path with one mixture: the same device generator
+    return init_hemisphere_batched_impl(&m, 1, positions, normals, depth_prior, &min_spatial_distance, &seed, 0);
 }
 
-static int init_hemisphere_batched_impl(sdmm_mix* const* mixes, int n, const float* positions,
-                                        const float* normals, float depth_prior, const float* min_spatial_distance,
-                                        const uint64_t* seeds, int skip);
 
 int sdmm_init_hemisphere_batched(sdmm_mix* const* mixes, int n, const float* positions, const float* normals,
                                  float depth_prior, const float* min_spatial_distance, const uint64_t* seeds) {
@@ -1229,7 +1228,19 @@ static int init_hemisphere_batched_impl(sdmm_mix* const* mixes, int n, const flo
     if (dev_i < 0 || dev_i >= 64) return fail(SDMM_E_INVALID, "device index out of range");
     Staging& sg = staging[dev_i];
     std::lock_guard<std::mutex> hold(sg.mu);
-    const size_t want = (per * (size_t)n + 255) / 256 * 256 + sizeof(InitDescHost) * (size_t)n;
+    // the staging block is generated on the device (hemi_gen_batched_kernel):
+    // only the inputs and the pointer table travel.  SDMM_HEMI_HOST=1 runs the
+    // host generator into pinned memory and uploads the whole block instead.
+    static const bool host_gen = [] {
+        const char* e = std::getenv("SDMM_HEMI_HOST");
+        return e && std::atoi(e) != 0;
+    }();
+    const size_t stage_bytes = (per * (size_t)n + 255) / 256 * 256;
+    const size_t tab_bytes = (sizeof(InitDescHost) * (size_t)n + 255) / 256 * 256;
+    const size_t pn_bytes = sizeof(float) * 3 * (size_t)npos * (size_t)n;   // positions, then normals
+    const size_t in_bytes = host_gen ? 0 : 2 * pn_bytes + sizeof(float) * (size_t)n + sizeof(uint64_t) * (size_t)n + 16;
+    const size_t up_off = host_gen ? 0 : stage_bytes;   // device offset of what is uploaded
+    const size_t want = (host_gen ? stage_bytes : 0) + tab_bytes + in_bytes;
     if (want > sg.cap) {
         release_host(sg.p);
         sg.p = nullptr;
@@ -1238,23 +1249,23 @@ static int init_hemisphere_batched_impl(sdmm_mix* const* mixes, int n, const flo
         HIP_TRY(hipHostMalloc((void**)&sg.p, cap, hipHostMallocDefault));
         sg.cap = cap;
     }
-    char* pin = sg.p;
+    char* pin = sg.p;   // pinned image of device bytes [up_off, stage_bytes + tab_bytes + in_bytes)
     int r = SDMM_OK;
-    // the host fp64 initialisations, in parallel over the mixtures (each is
-    // independent and writes its own staging slice: bitwise as sequential)
-    auto init_range = [&](int i0, int i1) {
-        for (int i = i0; i < i1; ++i) {
-            char* b = pin + per * (size_t)i;
-            float* pw = (float*)b;
-            float* pm = (float*)(b + 4 * Kz);
-            float* pc = (float*)(b + 28 * Kz);
-            float* pb = (float*)(b + 128 * Kz);
-            float* pd = (float*)(b + 228 * Kz);
-            hemisphere_init(positions + 3 * (size_t)npos * i, normals + 3 * (size_t)npos * i, npos, depth_prior,
-                            min_spatial_distance[i], seeds[i], pw, pm, pc, pb, pd, skip);
-        }
-    };
-    {
+    if (host_gen) {
+        // the host fp64 initialisations, in parallel over the mixtures (each is
+        // independent and writes its own staging slice: bitwise as sequential)
+        auto init_range = [&](int i0, int i1) {
+            for (int i = i0; i < i1; ++i) {
+                char* b = pin + per * (size_t)i;
+                float* pw = (float*)b;
+                float* pm = (float*)(b + 4 * Kz);
+                float* pc = (float*)(b + 28 * Kz);
+                float* pb = (float*)(b + 128 * Kz);
+                float* pd = (float*)(b + 228 * Kz);
+                hemisphere_init(positions + 3 * (size_t)npos * i, normals + 3 * (size_t)npos * i, npos, depth_prior,
+                                min_spatial_distance[i], seeds[i], pw, pm, pc, pb, pd, skip);
+            }
+        };
         const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
         const int nt = std::max(1, std::min({16, hw, n / 64}));
         std::vector<std::thread> th;
@@ -1271,20 +1282,34 @@ static int init_hemisphere_batched_impl(sdmm_mix* const* mixes, int n, const flo
         init_range(0, (int)((int64_t)n / nt));
         for (auto& x : th) x.join();
     }
-    // one upload of the staging block + the per-mixture pointer table, one
-    // kernel (a workgroup per mixture: copy in, MVTN::set, CDF, pack)
-    const size_t tab_off = (per * (size_t)n + 255) / 256 * 256;
-    InitDescHost* tab = (InitDescHost*)(pin + tab_off);
+    InitDescHost* tab = (InitDescHost*)(pin + stage_bytes - up_off);
     for (int i = 0; i < n; ++i) {
         sdmm_mix* m = mixes[i];
         tab[i] = InitDescHost{m->C, m->ep, m->gp, m->S.bPriors, m->S.bDepth, m->tmp_mean, m->tmp_cov};
     }
+    const size_t in_off = stage_bytes + tab_bytes;   // device offsets of the inputs
+    const size_t dist_off = in_off + 2 * pn_bytes;
+    const size_t seed_off = (dist_off + sizeof(float) * (size_t)n + 7) / 8 * 8;
+    if (!host_gen) {
+        std::memcpy(pin + in_off - up_off, positions, pn_bytes);
+        std::memcpy(pin + in_off - up_off + pn_bytes, normals, pn_bytes);
+        std::memcpy(pin + dist_off - up_off, min_spatial_distance, sizeof(float) * (size_t)n);
+        std::memcpy(pin + seed_off - up_off, seeds, sizeof(uint64_t) * (size_t)n);
+    }
+    // one upload, then (device generation) one kernel filling the staging
+    // block and one kernel (a workgroup per mixture: copy in, MVTN::set, CDF,
+    // pack)
     void* dev = nullptr;
-    const size_t total = tab_off + sizeof(InitDescHost) * (size_t)n;
+    const size_t total = stage_bytes + tab_bytes + in_bytes;
     hipError_t e0 = r ? hipSuccess : hipMallocAsync(&dev, total, st);
-    if (!r && e0 == hipSuccess) e0 = hipMemcpyAsync(dev, pin, total, hipMemcpyHostToDevice, st);
+    char* d = (char*)dev;
+    if (!r && e0 == hipSuccess) e0 = hipMemcpyAsync(d + up_off, pin, total - up_off, hipMemcpyHostToDevice, st);
+    if (!r && e0 == hipSuccess && !host_gen)
+        e0 = launch_hemi_gen_batched(n, K, (const float*)(d + in_off), (const float*)(d + in_off + pn_bytes),
+                                     (const float*)(d + dist_off), (const uint64_t*)(d + seed_off), skip, depth_prior,
+                                     d, per, st);
     if (!r && e0 == hipSuccess)
-        e0 = launch_set_all_batched(n, K, mixes[0]->Kp, (char*)dev + tab_off, dev, per, mixes[0]->norm5, st);
+        e0 = launch_set_all_batched(n, K, mixes[0]->Kp, d + stage_bytes, d, per, mixes[0]->norm5, st);
     if (dev) (void)hipFreeAsync(dev, st);
     if (!r && e0 != hipSuccess) r = fail(SDMM_E_HIP, std::string("init_hemisphere_batched: ") + hipGetErrorString(e0));
     const hipError_t e = hipStreamSynchronize(st);   // the pinned staging is reused by the next call

@@ -119,6 +119,33 @@ def test_init_params_match_oracle(pkg, oracle, synth, gpu, K):
     assert (p["valid"] == 1).all()
 
 
+@pytest.mark.parametrize("K", [16, 128, 512])
+def test_device_hemisphere_init_equals_host_generator(pkg, synth, gpu, K):
+    """The device generator of the initial staging block (hemi_gen_batched_kernel)
+    against the host one (bitwise equal to the oracle, test_abi): every mixture
+    parameter and the bPriors / bDepth priors equal bit for bit, through the
+    single-mixture and the batched entry points."""
+    b = synth.em_batch(4096, 128)
+    pos, nrm = synth.model_seed_points(b, K)
+    seeds = [0x1A17 + K, 7, 123456789]
+    dists = [synth.SPATIAL_DISTANCE, 0.05, 0.3]
+    hosts = [pkg.hemisphere_init_host(pos, nrm, synth.DEPTH_PRIOR, d, s) for d, s in zip(dists, seeds)]
+    single = pkg.SDMM(K)
+    single.init_hemisphere(pos, nrm, synth.DEPTH_PRIOR, dists[0], seeds[0])
+    batched = [pkg.SDMM(K) for _ in seeds]
+    pkg.init_hemisphere_batched(batched, np.stack([pos] * 3), np.stack([nrm] * 3), synth.DEPTH_PRIOR,
+                                np.array(dists, np.float32), np.array(seeds, np.uint64))
+    for m, h in [(single, hosts[0])] + list(zip(batched, hosts)):
+        ref = pkg.SDMM(K)
+        ref.set_params(h["weights"], h["mean"], h["cov"])
+        got, want = m.get_params(), ref.get_params()
+        for name, v in want.items():
+            np.testing.assert_array_equal(got[name], v, err_msg=name)
+        st = m.get_state()
+        np.testing.assert_array_equal(st["bpriors"], h["bpriors"].reshape(-1))
+        np.testing.assert_array_equal(st["bdepth"], h["bdepth"].reshape(-1))
+
+
 @pytest.mark.parametrize("K,N", [(16, 4099), (32, 2048), (64, 3000), (128, 4096), (128, 1001), (72, 777),
                                  (120, 2050), (256, 1500), (512, 700)])
 def test_responsibilities_match_oracle(pkg, oracle, synth, gpu, plog, K, N):
