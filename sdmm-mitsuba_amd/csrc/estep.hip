@@ -1308,6 +1308,55 @@ __device__ __forceinline__ double batched_col(const float* __restrict__ partials
     return t;
 }
 
+// batched_col with the column's rows fetched eight at a time as independent
+// loads (batched_col's loops of data-dependent trip count issue one load per
+// iteration, so a thread waits out one memory latency per row), then summed in
+// row order into the same per-slice sums: row r of slice sl adds to
+// b[(r - r0(sl)) & 3]; every slice, an empty one too, adds its
+// ((b0 + b1) + b2) + b3 to t in slice order.  The same additions in the same
+// order: bitwise equal.  (A b only ever starts at +0.0, so the selects below
+// never need to add a zero.)
+__device__ __forceinline__ double batched_col_mlp(const float* __restrict__ partials, int pstride, int row0,
+                                                  int rows, int col) {
+    constexpr int B = 8;
+    double t = 0.0, b0 = 0.0, b1 = 0.0, b2 = 0.0, b3 = 0.0;
+    int sl = 0, r0 = 0, r1 = (int)((int64_t)rows / kReduceSlices);
+    const float* p = partials + (int64_t)row0 * pstride + col;
+    for (int base = 0; base < rows; base += B) {
+        float v[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) v[j] = (base + j < rows) ? p[(int64_t)(base + j) * pstride] : 0.0f;
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            const int r = base + j;
+            if (r >= rows) break;
+            while (r >= r1) {   // close slice sl (and any empty ones after it)
+                t += ((b0 + b1) + b2) + b3;
+                b0 = b1 = b2 = b3 = 0.0;
+                ++sl;
+                r0 = r1;
+                r1 = (int)((int64_t)rows * (sl + 1) / kReduceSlices);
+            }
+            const double x = (double)v[j];
+            const int w = (r - r0) & 3;
+            if (w == 0) b0 += x;
+            else if (w == 1) b1 += x;
+            else if (w == 2) b2 += x;
+            else b3 += x;
+        }
+    }
+    for (; sl < kReduceSlices; ++sl) {
+        t += ((b0 + b1) + b2) + b3;
+        b0 = b1 = b2 = b3 = 0.0;
+    }
+    return t;
+}
+#ifdef SDMM_REDUCE_MLP
+constexpr bool kReduceMlp = true;
+#else
+constexpr bool kReduceMlp = false;   // batched_col's one load per iteration
+#endif
+
 // One workgroup per leaf.  Phase 1: one thread per stats column (consecutive
 // threads read consecutive partial columns of a row: coalesced), each column
 // reduced exactly as batched_col / the single-mixture path orders it (16 row
@@ -1326,7 +1375,8 @@ reduce_finalize_batched_kernel(const float* __restrict__ partials, int pstride, 
     if (L.n <= 0) return;             // uniform over the workgroup
     const int ncols = 2 + 21 * K;
     for (int o = threadIdx.x; o < ncols; o += blockDim.x)
-        red[o] = batched_col(partials, pstride, L.row0, L.rows, partial_col(o, Kp, K));
+        red[o] = kReduceMlp ? batched_col_mlp(partials, pstride, L.row0, L.rows, partial_col(o, Kp, K))
+                            : batched_col(partials, pstride, L.row0, L.rows, partial_col(o, Kp, K));
     __syncthreads();
     double* stats = L.stats;
     if (threadIdx.x < 2) stats[threadIdx.x] = red[threadIdx.x];
