@@ -627,8 +627,7 @@ estep_resp_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s
                 const float4 b = blk_lds[tb + t][1];
                 V c;
                 q[t] = pair_q_tile<false>(P, a.x, a.y, a.z, a.w, b.x, b.y, c);
-                cbits = __builtin_elementwise_max(cbits, __builtin_elementwise_max(__builtin_bit_cast(uint32_t, c.x),
-                                                                                   __builtin_bit_cast(uint32_t, c.y)));
+                cbits = __builtin_elementwise_max(cbits, __builtin_elementwise_max(fbits(c.x), fbits(c.y)));
                 // keep the scheduler from hoisting every sample's LDS reads
                 // (and their registers) to the top of the tile
                 if (t % SB == SB - 1) __builtin_amdgcn_sched_barrier(0);

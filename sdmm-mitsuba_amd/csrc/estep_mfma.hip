@@ -203,7 +203,7 @@ estep_resp_mfma_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s
             const float dp = dipi_lds[16 * r + col];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                cbits = __builtin_elementwise_max(cbits, __builtin_bit_cast(uint32_t, C[j]));
+                cbits = __builtin_elementwise_max(cbits, fbits(C[j]));
                 pdf[r][j] = pair_pdf_m(C[j], AD[j], BD[j], U0[j], U1[j], U2[j], S3[j], S4[j], dp, rare);
                 acc[j] += pdf[r][j];
             }

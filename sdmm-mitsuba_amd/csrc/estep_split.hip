@@ -57,16 +57,9 @@ template <bool B> struct Tag { static constexpr bool value = B; };
 constexpr float kLog2Norm5S = -6.628740082514092f;   // log2((float)pow(0.39894228f, 5)), mvtn.h:351-352
 
 __device__ __forceinline__ f2 spl(float x) { return (f2)(x); }
-#ifdef SDMM_SPLIT_SCALAR
-// A/B build: the pair math as plain VOP3 f32 (no packed f32 beside the MFMAs)
-__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return f2{fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y)}; }
-__device__ __forceinline__ f2 pmul(f2 a, f2 b) { return f2{a.x * b.x, a.y * b.y}; }
-__device__ __forceinline__ f2 padd(f2 a, f2 b) { return f2{a.x + b.x, a.y + b.y}; }
-#else
 __device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 pmul(f2 a, f2 b) { return a * b; }
 __device__ __forceinline__ f2 padd(f2 a, f2 b) { return a + b; }
-#endif
 
 // two floats -> one dword of two bf16 (round to nearest even): element 0 (lo)
 // in bits 0..15, element 1 (hi) in bits 16..31 (v_cvt_pk_bf16_f32)
@@ -112,49 +105,11 @@ __device__ __forceinline__ void split3(float c, unsigned& h, unsigned& m, unsign
 // sqrt(log2(e) / 2): the rows of u (spatial forms, ad, bd) are pre-scaled by
 // it, so that the exponent 2^(log2 NORM5 - |u'|^2) = NORM5 exp(-q/2) is one
 // FMA chain from the constant (no separate q and scaling step)
-#ifdef SDMM_SPLIT_NOROWSCALE
-constexpr bool kFoldScale = false;
-constexpr double kRowScale = 1.0;
-#else
 constexpr bool kFoldScale = true;
 constexpr double kRowScale = 0.84932180028801904272;
-#endif
 
 // row start of L^-1 row m in the packed lower triangle (EP_L00 ...)
 __device__ __forceinline__ int lrow(int m) { return EP_L00 + m * (m + 1) / 2; }
-
-// Spatial origin of block r (components 16 r .. 16 r + 15): the mean of the
-// block's finite component means (kOrigin if none).  The spatial forms are
-// u_m = sum_j L_mj (p_j - o_r) + NC_m(o_r); with o_r near the block's
-// components the two terms stay small for the samples whose pdfs matter (the
-// MFMA accumulation error scales with them; a single scene-centre origin left
-// the heuristic row sums at 1.2e-5 of the fp64 evaluation instead of 4e-6).
-#ifdef SDMM_SPLIT_BLOCKORIGIN
-#ifdef SDMM_SPLIT_PIPE
-#error "SDMM_SPLIT_PIPE uses the one scene-centre origin"
-#endif
-constexpr bool kBlockOrigin = true;
-#else
-constexpr bool kBlockOrigin = false;
-#endif
-__device__ __forceinline__ void block_origin(const float* __restrict__ ep, int Kp, int r, float* o) {
-    if (!kBlockOrigin) {
-        o[0] = o[1] = o[2] = kOrigin;
-        return;
-    }
-    double acc[3] = {0.0, 0.0, 0.0};
-    int cnt = 0;
-    for (int i = 0; i < 16; ++i) {
-        const int k = 16 * r + i;
-        const float m0 = ep[EP_MU0 * Kp + k], m1 = ep[EP_MU1 * Kp + k], m2 = ep[EP_MU2 * Kp + k];
-        if (!(fabsf(m0) < 1e6f && fabsf(m1) < 1e6f && fabsf(m2) < 1e6f)) continue;
-        acc[0] += m0;
-        acc[1] += m1;
-        acc[2] += m2;
-        ++cnt;
-    }
-    for (int j = 0; j < 3; ++j) o[j] = cnt ? (float)(acc[j] / cnt) : kOrigin;
-}
 
 // Coefficient fragment of block r, form f, lane l (the A operand of the
 // MFMA; K layout in the header): lane group g < 3 pairs feature g's small
@@ -291,65 +246,128 @@ __device__ __forceinline__ void pdf_quad(const f4& C, const f4& AD, const f4& BD
 
 }  // namespace
 
-// LDS rows (K = 128): each block's unnormalised pdfs go to the
-// wave's LDS row stage as soon as they are formed (whole rows, 8 KB per wave)
-// instead of living in 32 VGPRs until the tile's normaliser is known; the
-// flush scales them on the way out.  The freed registers allow 3 waves per
-// SIMD (12-wave workgroups: 96 KB of stage + the 64 KB coefficient image fill
-// the 160 KB LDS, so detInv pi is then read from the E-step record instead).
-// (an option, SDMM_SPLIT_LDSROWS; round 4, four processes each on one box:
-// 177.5-180.6 us per launch against 175.7-176.9 us with the pdfs in registers
-// until the flush at the same 12-wave / 3-per-SIMD configuration, the default)
-#ifdef SDMM_SPLIT_LDSROWS
-constexpr bool kLdsRowsOn = true;
-#else
-constexpr bool kLdsRowsOn = false;
-#endif
+// ---------------------------------------------------------------------------
+// Sample features through LDS by DMA, with counted waits (round 5).
+//
+// vmcnt counts loads and stores together, in issue order, and the compiler
+// waits vmcnt(0) before the first use of a VGPR load whenever stores are
+// pending beside it.  With the features loaded into VGPRs every tile, each
+// wave therefore waited for ALL of its row stores before it could start the
+// next tile: compute and the write stream took turns instead of overlapping
+// (store-only shape 135 us against the 88-105 us write stream, the math then
+// +45 us on top).  Here the features of tile t + kFeatAhead go by
+// global_load_lds_dword (inline asm: the compiler does not track them, so it
+// never drains vmcnt for them) into a per-wave LDS ring, and the wave waits
+// with an explicit vmcnt(N) that leaves every store younger than that DMA in
+// flight: N = 2 kFeatAhead + R k, the two DMA pieces of each tile issued after
+// it plus the R row stores of each of the k = min(i, kFeatAhead + 1) flushes
+// issued after it (every one of them a full flush of exactly R stores; any
+// other flush in that window and the wait is vmcnt(0)).
+constexpr int kFeatAhead = 2;
+constexpr int kFeatSlots = kFeatAhead + 1;
+constexpr int kFeatSlotU4 = 32;   // two 256-B DMA pieces (64 lanes x 4 B)
 
-// the default block loop's scheduling fences (SDMM_SPLIT_NOFENCE, A/B: the
-// compiler schedules the MFMAs, the fragment reads and the pair math freely)
-#ifdef SDMM_SPLIT_NOFENCE
-#define SPLIT_FENCE() ((void)0)
+// vmcnt(N), then this lane's two 16-B feature records from the ring, in ONE
+// statement: the compiler sees neither the DMA that wrote the ring nor its
+// wait, so a plain read of the ring would be a read of memory it believes
+// unwritten (undef: it did fold one of them to an unrelated register).
+// lgkmcnt(0) inside: the outputs are complete when the statement ends.
+template <int N>
+__device__ __forceinline__ void read_feat(unsigned addr, f4& a, f4& b) {
+    static_assert(N >= 0 && N <= 63, "gfx950 vmcnt is six bits");
+    asm volatile(
+        "s_waitcnt vmcnt(%3)\n\t"
+        "ds_read_b128 %0, %2\n\t"
+        "ds_read_b128 %1, %2 offset:256\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(a), "=&v"(b)
+        : "v"(addr), "n"(N)
+        : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N <= 63, "gfx950 vmcnt is six bits");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// (diagnostic SDMM_SPLIT_DIAG_NOSTORE: every row computed, none stored -- the
+// compute-only time of the kernel; then only the DMAs are in flight)
+#ifdef SDMM_SPLIT_DIAG_NOSTORE
+constexpr bool kDiagNoStore = true;
 #else
-#define SPLIT_FENCE() __builtin_amdgcn_sched_barrier(0)
+constexpr bool kDiagNoStore = false;
 #endif
+template <int R>
+__device__ __forceinline__ void read_feat_counted(int k, bool window_full, unsigned addr, f4& a, f4& b) {
+    if (kDiagNoStore) {
+        read_feat<2 * kFeatAhead>(addr, a, b);
+        return;
+    }
+    if (!window_full) {
+        read_feat<0>(addr, a, b);
+        return;
+    }
+    switch (k) {   // wave-uniform
+        case 0: read_feat<2 * kFeatAhead>(addr, a, b); break;
+        case 1: read_feat<2 * kFeatAhead + R>(addr, a, b); break;
+        case 2: read_feat<2 * kFeatAhead + 2 * R>(addr, a, b); break;
+        default: read_feat<2 * kFeatAhead + 3 * R>(addr, a, b); break;
+    }
+    static_assert(kFeatAhead == 2, "read_feat_counted enumerates k = 0 .. kFeatAhead + 1");
+}
+
+// two LDS-DMA pieces: lane L's dword of a0 to lds[L], of a1 to lds[64 + L]
+// (M0 = the wave-uniform LDS byte address of the piece)
+__device__ __forceinline__ void dma_pair(uintptr_t a0, uintptr_t a1, unsigned lds0) {
+    unsigned keep;   // M0 is reserved by the compiler: saved and restored around the pieces
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dword %1, off\n\t"
+        "s_mov_b32 m0, %4\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dword %2, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(a0), "v"(a1), "s"(lds0), "s"(lds0 + 256u)
+        : "memory");
+}
+
 template <int R, int WPB, int OCC>
 __global__ void __launch_bounds__(64 * WPB, OCC)
 estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, int64_t n, int64_t nwaves,
                         float* __restrict__ resp) {
-    constexpr bool LR = kLdsRowsOn && R == 8;
-    constexpr bool DIMG = !LR || (WPB * 16 * 32 * 16 + R * 8 * 64 * 16 + R * 4 * 16 <= 163840);
-    // coefficient fragments (R blocks x 8 forms x 64 lanes) and detInv pi of
-    // components 16 r + 4 g .. +3 (the D rows of lane group g)
-    // one LDS block carved into the coefficient image, the per-wave row
-    // stages (16 rows x 512 B with LR, else 256-B half rows), detInv pi and
-    // the block origins (only the parts the configuration uses)
-    constexpr int NC = R * 8 * 64, NS = LR ? 16 * 32 : 16 * 16, ND = DIMG ? R * 4 : 0, NB = kBlockOrigin ? R : 0;
-    __shared__ u4 smem[NC + WPB * NS + ND + NB];
-    u4* const cimg = smem;
-    f4* const stage0 = (f4*)(smem + NC);
-    f4* const dimg = (f4*)(smem + NC + WPB * NS);
-    float (*const borig)[4] = (float (*)[4])(smem + NC + WPB * NS + ND);
-    if (kBlockOrigin && threadIdx.x < R) block_origin(ep, Kp, threadIdx.x, borig[threadIdx.x]);
-    __syncthreads();
-    // (without per-block origins every block's spatial forms use the one
-    // scene-centre origin kOrigin; borig then has no storage)
+    // one LDS block carved into: per wave the feature ring (kFeatSlots x 512 B;
+    // first, so every LDS-DMA destination lies below 64 KB), the coefficient
+    // image (R blocks x 8 forms x 64 lanes), detInv pi of components 16 r + 4 g
+    // .. + 3 (the D rows of lane group g), and per wave the 256-B half-row
+    // stage (R = 8: 16 rows)
+    constexpr int NC = R * 8 * 64, ND = R * 4, NS = R == 8 ? 16 * 16 : 0, NF = kFeatSlots * kFeatSlotU4;
+    constexpr int NTOT = WPB * NF + NC + ND + WPB * NS;
+    static_assert(NTOT * 16 <= 163840, "the carved LDS block exceeds the 160 KB of a CU");
+    static_assert(WPB * NF * 16 <= 65536, "LDS-DMA destinations stay below 64 KB");
+    __shared__ u4 smem[NTOT];
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    u4* const ring = smem + wid * NF;
+    u4* const cimg = smem + WPB * NF;
+    f4* const dimg = (f4*)(cimg + NC);
+    f4* const st = (f4*)(cimg + NC + ND + wid * NS);
+    static_assert(WPB * NF + NC + ND + WPB * NS == NTOT && (R != 8 || NS == 256), "LDS carve: every region has storage");
+
     const float o_scene[3] = {kOrigin, kOrigin, kOrigin};
 #ifdef SDMM_SPLIT_DIAG_NOIMAGE   // (diagnostic: a zero coefficient image -- results are not responsibilities)
-    for (int idx = threadIdx.x; idx < NC + WPB * NS + ND; idx += 64 * WPB) smem[idx] = u4{0u, 0u, 0u, 0u};
+    for (int idx = threadIdx.x; idx < NC + ND; idx += 64 * WPB) cimg[idx] = u4{0u, 0u, 0u, 0u};
 #else
-    for (int idx = threadIdx.x; idx < R * 8 * 64; idx += 64 * WPB)
-        cimg[idx] = coef_frag(ep, Kp, idx >> 9, (idx >> 6) & 7, idx & 63, kBlockOrigin ? borig[idx >> 9] : o_scene);
-    if constexpr (DIMG)
-        for (int i = threadIdx.x; i < R * 4; i += 64 * WPB) {
-            const float* d = ep + EP_DIPI * Kp + 4 * i;
-            dimg[i] = f4{d[0], d[1], d[2], d[3]};
-        }
+    for (int idx = threadIdx.x; idx < NC; idx += 64 * WPB)
+        cimg[idx] = coef_frag(ep, Kp, idx >> 9, (idx >> 6) & 7, idx & 63, o_scene);
+    for (int i = threadIdx.x; i < ND; i += 64 * WPB) {
+        const float* d = ep + EP_DIPI * Kp + 4 * i;
+        dimg[i] = f4{d[0], d[1], d[2], d[3]};
+    }
 #endif
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t wave = (int64_t)blockIdx.x * WPB + wid;
     // the launch's 16-sample tiles dealt round robin over its waves (one round
     // of resident waves: each workgroup builds the coefficient image once):
@@ -369,46 +387,36 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
     const int col = lane & 15;
     const bool has_h = s.hpdf != nullptr, has_d = s.isDiffuse != nullptr;
 
-    // sample col of tile t: position and direction coordinate g (lane group 3
-    // loads coordinate 0 and gathers all three from groups 0..2 when the
-    // fragments are built) and, when present, the heuristic pdf and the
-    // diffuse flag (its dword)
-    const int gf = g < 3 ? g : 0;
-    struct Feat {
-        float p, d, hp;
-        int dw;
+    // DMA sources of this lane: sample sl = lane >> 2 of the tile, plane pl =
+    // lane & 3 of piece 0 (x0 x1 x2 x3) and of piece 1 (x4 x5 hpdf isDiffuse;
+    // an absent optional plane re-reads x0).  The diffuse flag comes as the
+    // dword that holds its byte (the plane's dword-aligned word).
+    const int pl = lane & 3, sl = lane >> 2;
+    const uintptr_t src0 = (uintptr_t)(pl == 0 ? s.x[0] : pl == 1 ? s.x[1] : pl == 2 ? s.x[2] : s.x[3]);
+    const bool byteplane = pl == 3 && has_d;
+    const uintptr_t src1 = (uintptr_t)(pl == 0   ? s.x[4]
+                                       : pl == 1 ? s.x[5]
+                                       : pl == 2 ? (has_h ? s.hpdf : s.x[0])
+                                                 : (has_d ? (const float*)s.isDiffuse : s.x[0]));
+    const int sh1 = byteplane ? 0 : 2;
+    const unsigned ring_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) u4*)ring;
+    auto dma = [&](int64_t t, int slot) __attribute__((always_inline)) {
+        int64_t i = t + sl;
+        i = (i < s1) ? i : s1 - 1;   // past the end: a valid sample, never stored
+        const uintptr_t a0 = src0 + ((uintptr_t)i << 2);
+        const uintptr_t a1 = (src1 + ((uintptr_t)i << sh1)) & ~(uintptr_t)3;
+        dma_pair(a0, a1, ring_lds + (unsigned)slot * (kFeatSlotU4 * 16u));
     };
-    auto load_feat = [&](int64_t t) {
-        int64_t i = t + col;
-        i = (i < s1) ? i : s1 - 1;
-        Feat f;
-        f.p = __builtin_nontemporal_load(s.x[gf] + i);
-        f.d = __builtin_nontemporal_load(s.x[3 + gf] + i);
-        // optional planes: loaded only when present (a wave-uniform branch)
-        f.hp = 0.0f;
-        f.dw = 0;
-        if (has_h) f.hp = __builtin_nontemporal_load(s.hpdf + i);
-        if (has_d) f.dw = *(const __attribute__((address_space(1))) int*)((uintptr_t)(s.isDiffuse + i) & ~(uintptr_t)3);
-        return f;
-    };
-    // the three coordinates of sample col from lane groups 0..2
-    auto gather3 = [&](float v, float (&x)[3]) __attribute__((always_inline)) {
-        x[0] = __shfl(v, col);
-        x[1] = __shfl(v, 16 + col);
-        x[2] = __shfl(v, 32 + col);
-    };
-    auto pfrag = [&](const float (&p3)[3], const float* o) __attribute__((always_inline)) {
-        const float x[3] = {p3[0] - o[0], p3[1] - o[1], p3[2] - o[2]};
+
+    auto pfrag = [&](const float (&p3)[3]) __attribute__((always_inline)) {
+        const float x[3] = {p3[0] - kOrigin, p3[1] - kOrigin, p3[2] - kOrigin};
         return a_frag(x, g, true);
     };
     // block r's coefficient fragments and detInv pi of the lane's four components
     auto frags = [&](int r, bf8 (&F)[8], f4& dp) __attribute__((always_inline)) {
 #pragma unroll
         for (int f = 0; f < 8; ++f) F[f] = __builtin_bit_cast(bf8, cimg[(r * 8 + f) * 64 + lane]);
-        if constexpr (DIMG)
-            dp = dimg[r * 4 + g];
-        else
-            dp = *(const f4*)(ep + EP_DIPI * Kp + 16 * r + 4 * g);
+        dp = dimg[r * 4 + g];
     };
     auto forms = [&](const bf8 (&F)[8], bf8 bs, bf8 bd, f4 (&D)[8]) __attribute__((always_inline)) {
         const f4 z = f4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -416,48 +424,17 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
         for (int f = 0; f < 8; ++f) D[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F[f], f < 3 ? bd : bs, z, 0, 0, 0);
     };
 
-    // The stores of tile t are issued at the top of tile t + 1, BEFORE the
-    // loads of tile t + 2: vmcnt counts stores too, and a wait on loads that
-    // were issued before pending stores is a wait for those stores (the
-    // compiler emits vmcnt(0) on mixed pending events).  In this order the
-    // wait for tile t + 1's loads only covers stores issued a tile earlier.
-    float pdf[LR ? 1 : R][4];
-    f4* const st = stage0 + wid * NS;
+    // The rows of tile t are stored at the top of the next tile (flush), after
+    // the DMA of the features kFeatAhead tiles ahead; a full flush is exactly
+    // R store instructions (the count read_feat_counted relies on).
+    float pdf[R][4];
     float gsc_p = 0.0f;
     bool full_p = false;
     int64_t tp = -1;
     auto flush = [&]() __attribute__((always_inline)) {
         if (tp < 0) return;
+        if (kDiagNoStore && gsc_p != -1.0f) return;   // (never -1: the rows stay live)
         float* row = resp + (tp + col) * (int64_t)K + 4 * g;
-        if constexpr (LR) {
-            if (full_p) {
-                // whole unnormalised rows in the stage: lane (g, col) scales and
-                // stores 16-B chunk 16 h + col of rows g + 4 i (four contiguous
-                // 256-B half rows per store instruction)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int rw = g + 4 * i;
-                    const float sc = __shfl(gsc_p, rw);   // row rw's normaliser (lane rw holds it)
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const int ch = 16 * h + col;
-                        const f4 v = st[rw * 32 + (ch ^ rw)];
-                        __builtin_nontemporal_store(v * sc, (f4*)(resp + (tp + rw) * (int64_t)K + 4 * ch));
-                    }
-                }
-            } else if (tp + col < s1) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const f4 v = st[col * 32 + ((4 * r + g) ^ col)];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const float o = gsc_p != 0.0f ? v[j] * gsc_p : 0.0f;
-                        if (16 * r + 4 * g + j < K) __builtin_nontemporal_store(o, row + 16 * r + j);
-                    }
-                }
-            }
-            return;
-        }
         if (full_p && R != 8) {
             // one 16-B store per block: a sample's 64-B row segment per 4 lanes
 #pragma unroll
@@ -502,24 +479,30 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
         }
     };
 
-    Feat nf = load_feat(s0);
-    for (int64_t t = s0; t < s1; t += step) {
-        const Feat cf = nf;
-        float P3[3], D3[3];
-        gather3(cf.p, P3);
-        gather3(cf.d, D3);
+    // prologue: the first kFeatAhead tiles' features in flight
+#pragma unroll
+    for (int a = 0; a < kFeatAhead; ++a) dma(s0 + a * step, a);
+    unsigned hist = 0;   // bit j: the flush j iterations back was full
+    int it = 0;
+    for (int64_t t = s0; t < s1; t += step, ++it) {
+        const int slot = it % kFeatSlots;
+        dma(t + kFeatAhead * step, (it + kFeatAhead) % kFeatSlots);   // clamped past the end
+        if (tp >= 0) hist = (hist << 1) | (full_p ? 1u : 0u);
+        flush();                                                       // tile t - step's rows
+        const int k = it < kFeatAhead + 1 ? it : kFeatAhead + 1;
+        const unsigned need = (1u << k) - 1u;
+        f4 fa, fb;   // x0 x1 x2 x3 and x4 x5 hpdf flags of sample col
+        read_feat_counted<R>(k, (hist & need) == need, ring_lds + (unsigned)slot * (kFeatSlotU4 * 16u) + 16u * col,
+                             fa, fb);
+        const float P3[3] = {fa.x, fa.y, fa.z};
+        const float D3[3] = {fa.w, fb.x, fb.y};
         // d == 0 fails every log map (mvtn.h:152-154)
         const bool dzero = D3[0] == 0.0f && D3[1] == 0.0f && D3[2] == 0.0f;
-        const bool dif = has_d && ((cf.dw >> (8 * (int)((uintptr_t)(s.isDiffuse + ((t + col < s1) ? t + col : s1 - 1)) & 3))) & 0xff) != 0;
-        const float hp = has_h ? cf.hp : 0.0f;
+        const int64_t ic = (t + col < s1) ? t + col : s1 - 1;
+        const bool dif = has_d && ((fbits(fb.w) >> (8 * (int)((uintptr_t)(s.isDiffuse + ic) & 3))) & 0xffu) != 0u;
+        const float hp = has_h ? fb.z : 0.0f;
         const bf8 Bd = a_frag(D3, g, false);
-        const float o0[3] = {kOrigin, kOrigin, kOrigin};
-        const bf8 Bs0 = pfrag(P3, o0);   // one origin for every block unless kBlockOrigin
-        __builtin_amdgcn_sched_barrier(0);
-        flush();                          // tile t - 16's rows
-        __builtin_amdgcn_sched_barrier(0);
-        nf = load_feat(t + step);         // next tile in flight (clamped past the end)
-        __builtin_amdgcn_sched_barrier(0);
+        const bf8 Bs = pfrag(P3);
 
         f2 acc = f2{0.0f, 0.0f};
         uint32_t cbits = 0;
@@ -527,147 +510,42 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
             constexpr bool RARE = decltype(rare)::value;
             if constexpr (!RARE)
                 cbits = __builtin_elementwise_max(
-                    cbits, __builtin_elementwise_max(
-                               __builtin_elementwise_max(__builtin_bit_cast(uint32_t, D[0][0]), __builtin_bit_cast(uint32_t, D[0][1])),
-                               __builtin_elementwise_max(__builtin_bit_cast(uint32_t, D[0][2]), __builtin_bit_cast(uint32_t, D[0][3]))));
+                    cbits, __builtin_elementwise_max(__builtin_elementwise_max(fbits(D[0][0]), fbits(D[0][1])),
+                                                     __builtin_elementwise_max(fbits(D[0][2]), fbits(D[0][3]))));
             f2 p[2];
-#ifdef SDMM_SPLIT_DIAG_NOMATH
-            p[0] = f2{D[0][0] + D[1][0] + D[2][0] + D[3][0], D[4][1] + D[5][1] + D[6][1] + D[7][1]};
-            p[1] = f2{D[0][2] + D[1][2] + D[2][2] + D[3][2], D[4][3] + D[5][3] + D[6][3] + D[7][3]};
-#else
             pdf_quad<RARE>(D[0], D[1], D[2], D[3], D[4], D[5], D[6], D[7], dp, p);
-#endif
-            if constexpr (LR) {
-                st[col * 32 + ((4 * r + g) ^ col)] = f4{p[0].x, p[0].y, p[1].x, p[1].y};   // row col, chunk 4 r + g
-            } else {
-                pdf[r][0] = p[0].x;
-                pdf[r][1] = p[0].y;
-                pdf[r][2] = p[1].x;
-                pdf[r][3] = p[1].y;
-            }
+            pdf[r][0] = p[0].x;
+            pdf[r][1] = p[0].y;
+            pdf[r][2] = p[1].x;
+            pdf[r][3] = p[1].y;
             acc = padd(acc, padd(p[0], p[1]));
         };
 #if defined(SDMM_SPLIT_DIAG_STOREONLY)
-        // diagnostic ceiling (tools/build_variant.sh): the same loads, row
-        // staging and stores with no matrix or pair math; the rows are not
-        // responsibilities
+        // diagnostic ceiling (tools/build_variant.sh "-DSDMM_SPLIT_DIAG_STOREONLY"):
+        // the same DMA, row staging and stores with no matrix or pair math; the
+        // rows are not responsibilities
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            f4 v;
+        for (int r = 0; r < R; ++r)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                v[j] = P3[j & 1] + D3[j >> 1] + (float)(16 * r + j);
-                acc.x += v[j];
+                pdf[r][j] = P3[j & 1] + D3[j >> 1] + (float)(16 * r + j);
+                acc.x += pdf[r][j];
             }
-            if constexpr (LR)
-                st[col * 32 + ((4 * r + g) ^ col)] = v;
-            else
-#pragma unroll
-                for (int j = 0; j < 4; ++j) pdf[r][j] = v[j];
-        }
-#elif defined(SDMM_SPLIT_PAIR2)
-        {
-            // two blocks per step: their 16 MFMAs back to back, then both
-            // blocks' pair math with no fence between them, so the scheduler
-            // interleaves four independent packed chains (the pair math is
-            // dependency-bound at two); the next pair's fragments are read
-            // from LDS meanwhile
-          if constexpr (R % 2 != 0) {
-            bf8 F[8];
-            f4 dp, D[8];
-            frags(0, F, dp);
-            forms(F, Bs0, Bd, D);
-            pair_math(0, Tag<false>{}, D, dp);
-          } else {
-            bf8 F[2][8], G[2][8];
-            f4 dp[2], dq[2];
-            frags(0, F[0], dp[0]);
-            frags(1, G[0], dq[0]);
-#pragma unroll
-            for (int r = 0; r < R; r += 2) {
-                const int b = (r >> 1) & 1;
-                f4 D0[8], D1[8];
-                forms(F[b], Bs0, Bd, D0);
-                forms(G[b], Bs0, Bd, D1);
-                __builtin_amdgcn_sched_barrier(0);
-                if (r + 2 < R) {
-                    frags(r + 2, F[b ^ 1], dp[b ^ 1]);
-                    frags(r + 3, G[b ^ 1], dq[b ^ 1]);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                pair_math(r, Tag<false>{}, D0, dp[b]);
-                pair_math(r + 1, Tag<false>{}, D1, dq[b]);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-          }
-        }
-#elif defined(SDMM_SPLIT_PIPE)
-        {
-            // software-pipelined over the blocks: block r + 1's eight MFMAs are
-            // issued before block r's pair math and interleaved with it
-            // (sched_group_barrier), block r + 2's fragments are read from LDS
-            // meanwhile; the matrix pipe works while the VALU does
-            bf8 F[R][8];
-            f4 dp[R], D[R][8];
-            frags(0, F[0], dp[0]);
-            forms(F[0], Bs0, Bd, D[0]);
-            if (R > 1) frags(1, F[1], dp[1]);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                if (r + 1 < R) forms(F[r + 1], Bs0, Bd, D[r + 1]);
-                if (r + 2 < R) frags(r + 2, F[r + 2], dp[r + 2]);
-                pair_math(r, Tag<false>{}, D[r], dp[r]);
-                if (r + 1 < R) {
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);              // one MFMA
-                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);              // one LDS read
-                        __builtin_amdgcn_sched_group_barrier(0x002, SDMM_SPLIT_PIPE, 0);  // VALU
-                    }
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
 #else
         {
             // pipelined over the blocks: block r + 1's fragments are read from
             // LDS while block r's pair math runs
-            bf8 F[2][8], BS[2];
+            bf8 F[2][8];
             f4 dp[2];
             frags(0, F[0], dp[0]);
-            BS[0] = kBlockOrigin ? pfrag(P3, borig[0]) : Bs0;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 f4 D[8];
-                forms(F[r & 1], BS[r & 1], Bd, D);
-                SPLIT_FENCE();
-#ifndef SDMM_SPLIT_PREFETCH
-#define SDMM_SPLIT_PREFETCH 0
-#endif
-                // SDMM_SPLIT_PREFETCH = n (A/B): block r + 1's first n fragments
-                // are read while block r's pair math runs, the rest after it
-                // (default 0: 32 VGPRs fewer, 3 waves per SIMD fit, and the
-                // other waves cover the reads)
-                if (r + 1 < R && SDMM_SPLIT_PREFETCH > 0) {
-#pragma unroll
-                    for (int f = 0; f < SDMM_SPLIT_PREFETCH; ++f)
-                        F[(r + 1) & 1][f] = __builtin_bit_cast(bf8, cimg[((r + 1) * 8 + f) * 64 + lane]);
-                }
-                SPLIT_FENCE();
+                forms(F[r & 1], Bs, Bd, D);
+                __builtin_amdgcn_sched_barrier(0);
                 pair_math(r, Tag<false>{}, D, dp[r & 1]);
-                if (r + 1 < R) {
-#pragma unroll
-                    for (int f = SDMM_SPLIT_PREFETCH; f < 8; ++f)
-                        F[(r + 1) & 1][f] = __builtin_bit_cast(bf8, cimg[((r + 1) * 8 + f) * 64 + lane]);
-                    if constexpr (DIMG)
-                        dp[(r + 1) & 1] = dimg[(r + 1) * 4 + g];
-                    else
-                        dp[(r + 1) & 1] = *(const f4*)(ep + EP_DIPI * Kp + 16 * (r + 1) + 4 * g);
-                }
-                // the next block's spatial sample fragment, off the MFMA issue path
-                if (r + 1 < R) BS[(r + 1) & 1] = kBlockOrigin ? pfrag(P3, borig[r + 1]) : Bs0;
-                SPLIT_FENCE();
+                if (r + 1 < R) frags(r + 1, F[(r + 1) & 1], dp[(r + 1) & 1]);
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
 #endif
@@ -675,14 +553,8 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
         // unsigned, exceed those of -0.9999995f) or a NaN: redo the tile with
         // the reference's quirks (wave-uniform, a few tiles per launch)
         const bool odd = cbits > __builtin_bit_cast(uint32_t, -0.9999995f) || !(acc.x + acc.y >= 0.0f);
-#if defined(SDMM_SPLIT_DIAG_NOREDO)
-        if (false) {
-#elif defined(SDMM_SPLIT_DIAG_ALWAYSREDO)
-        if (__builtin_amdgcn_ballot_w64(odd) != 0 || true) {
-#else
         if (__builtin_amdgcn_ballot_w64(odd) != 0) {
-#endif
-            bf8 bd2 = Bd, bs2 = Bs0;
+            bf8 bd2 = Bd, bs2 = Bs;
             asm volatile("" : "+v"(bd2), "+v"(bs2));
             acc = f2{0.0f, 0.0f};
 #pragma unroll
@@ -690,7 +562,7 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
                 bf8 F[8];
                 f4 dp, D[8];
                 frags(r, F, dp);
-                forms(F, kBlockOrigin ? pfrag(P3, borig[r]) : bs2, bd2, D);
+                forms(F, bs2, bd2, D);
                 pair_math(r, Tag<true>{}, D, dp);
             }
         }
@@ -709,28 +581,27 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
         tp = t;
     }
     flush();
+    // the ring's last DMAs (clamped tiles past the end) land before the
+    // workgroup's LDS is released
+    wait_vm<0>();
 }
 
 // ---------------------------------------------------------------------------
 // Configurations (R = Kp / 16 blocks, waves per workgroup, waves per SIMD).
 // The B image takes R x 8 KB of LDS per workgroup.
-#define SDMM_SPLIT_CONFIGS(X) X(1, 4, 4) X(2, 4, 4) X(4, 4, 4) X(8, 4, 2) X(8, 8, 2) X(8, 12, 3)
+#define SDMM_SPLIT_CONFIGS(X) X(1, 4, 4) X(2, 4, 4) X(4, 4, 4) X(8, 12, 3)
 
-// R = 8 (K = 128): variants 0 and 2 = one 12-wave workgroup per CU at 3 waves
-// per SIMD (the 96-KB row stage + the 64-KB coefficient image fill the LDS),
-// 1 = two 4-wave workgroups at 2 per SIMD, 3 = one 8-wave workgroup at 2 per
-// SIMD (round 3's default)
-static void split_cfg(int R, int variant, int* wpb, int* occ) {
+// R = 8 (K = 128): one 12-wave workgroup per CU at 3 waves per SIMD (the
+// 64-KB coefficient image, the 48 KB of half-row stages and the 18 KB of
+// feature rings share the LDS).  Round 4 measured 4-wave / 2-per-SIMD and
+// 8-wave / 2-per-SIMD workgroups slower; the variant
+// argument is kept for the ABI's A/B hook and ignored.
+static void split_cfg(int R, int /*variant*/, int* wpb, int* occ) {
     *wpb = 4;
     *occ = 4;
     if (R == 8) {
-        // default: 12-wave workgroups at 3 waves per SIMD (round 4: 176 us
-        // per launch against 180-188 us for the round-3 configuration,
-        // variant 3, which also ran 340-370 us in some processes -- see
-        // DESIGN.md section 4)
-        *wpb = 12; *occ = 3;
-        if (variant == 1) { *wpb = 4; *occ = 2; }
-        if (variant == 3) { *wpb = 8; *occ = 2; }
+        *wpb = 12;
+        *occ = 3;
     }
 }
 

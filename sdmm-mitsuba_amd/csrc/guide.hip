@@ -25,6 +25,7 @@
 // direction and the mixture pdf (tolerances 1e-5 / 1e-4) use the float
 // transcendentals.
 #include "sdmm_device.h"
+#include "fastexp.h"
 #include <cstdlib>
 
 #include <hipcub/hipcub.hpp>
@@ -36,6 +37,18 @@ namespace sdmm {
 struct GuideConsts {
     float norm2, norm3;
 };
+
+// The 2^(j/64) table of norm_exp (fastexp.h), one copy per workgroup in LDS:
+// every kernel of this file that reaches a Gaussian weight fills it first
+// (exp_tbl_init, before any early exit).
+__constant__ double kExp2JDev[64] = {SDMM_EXP2J_TABLE};
+__shared__ double g_exp2j[64];
+__device__ __forceinline__ void exp_tbl_init() {
+    if (threadIdx.x < 64) g_exp2j[threadIdx.x] = kExp2JDev[threadIdx.x];
+    __syncthreads();
+}
+// (float)((double)norm * exp(-0.5 * (double)q)), bit for bit (fastexp.h)
+__device__ __forceinline__ float gauss_w(float norm, float q) { return norm_exp(norm, q, g_exp2j); }
 
 __device__ __forceinline__ float gp_ld(const float* gp, int Kp, int f, int k) {
     return ((cfloat_p)gp)[k * GP_STRIDE + f];   // AoS record (sdmm_device.h)
@@ -126,7 +139,7 @@ __device__ __forceinline__ float marginal_q(const float* gp, int Kp, int k, cons
 }
 __device__ __forceinline__ float marginal_pdf_q(const float* gp, int Kp, int k, float q, float norm3) {
     if (q > kMarginalZeroQ) return 0.0f;   // flushes to 0 in the reference (FTZ)
-    float pdf = (float)((double)norm3 * exp(-0.5 * (double)q));
+    float pdf = gauss_w(norm3, q);
     return pdf * gp_ld(gp, Kp, GP_MDI, k);
 }
 __device__ __forceinline__ float marginal_pdf(const float* gp, int Kp, int k, const float c[3], float norm3) {
@@ -167,7 +180,7 @@ __device__ __forceinline__ float marginal_weight_rec(const MargRec& m, const flo
     float s2 = (float)((double)r2 * marg_rcp(m, 2));   // r2 / ML22
     const float q = s0 * s0 + s1 * s1 + s2 * s2;
     float pdf = 0.0f;
-    if (!(q > kMarginalZeroQ)) pdf = (float)((double)norm3 * exp(-0.5 * (double)q)) * m.mdi;
+    if (!(q > kMarginalZeroQ)) pdf = gauss_w(norm3, q) * m.mdi;
     return m.w * pdf;
 }
 
@@ -217,6 +230,18 @@ __device__ __forceinline__ bool cond_valid(const float* gp, int Kp, int k, const
     float t1 = gp_ld(gp, Kp, GP_P10, k) * d0 + gp_ld(gp, Kp, GP_P11, k) * d1 + gp_ld(gp, Kp, GP_P12, k) * d2;
     float length = sqrtf(t0 * t0 + t1 * t1);
     return !((double)length >= kPi);
+}
+
+// test hook (sdmm_test_norm_exp): the device norm_exp over an array of q
+__global__ void __launch_bounds__(256) norm_exp_test_kernel(const float* __restrict__ q, int64_t n, float norm,
+                                                           float* __restrict__ out, int32_t* __restrict__ fast) {
+    exp_tbl_init();
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    int ok;
+    const float f = norm_exp_try(norm, q[i], g_exp2j, &ok);
+    out[i] = ok ? f : norm_exp_ref(norm, q[i]);
+    if (fast) fast[i] = ok;
 }
 
 // ---------------------------------------------------------------------------
@@ -708,6 +733,7 @@ template <bool PDF_ONLY, int LCAP>
 __global__ void __launch_bounds__(64)
 guide_cand_kernel(const float* __restrict__ gp, int Kp, int K, int64_t nq, GuideIO io, GuideConsts gc, int cap,
                   int* __restrict__ fb_count, int32_t* __restrict__ fb_list, const int32_t* __restrict__ perm) {
+    exp_tbl_init();
     __shared__ float cw[LCAP * 64];
     __shared__ unsigned short ck[LCAP * 64];
     const int tid = threadIdx.x;
@@ -732,6 +758,7 @@ guide_tree_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __re
                        GuideIO io, GuideConsts gc, int cap, int* __restrict__ fb_count,
                        int32_t* __restrict__ fb_list, const int32_t* __restrict__ perm,
                        int32_t* __restrict__ node_out, NodeRoute rt, const uint32_t* __restrict__ skeys, int mb) {
+    exp_tbl_init();
     __shared__ float cw[LCAP * 64];
     __shared__ unsigned short ck[LCAP * 64];
     const int tid = threadIdx.x;
@@ -1153,6 +1180,7 @@ template <bool PDF_ONLY>
 __global__ void __launch_bounds__(64)
 guide_fallback_kernel(const float* __restrict__ gp, int Kp, int K, GuideIO io, GuideConsts gc,
                       const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list) {
+    exp_tbl_init();
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x;
     const int count = *fb_count;
@@ -1171,6 +1199,7 @@ __global__ void __launch_bounds__(64)
 guide_tree_fallback_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __restrict__ tab, int kmax,
                            GuideIO io, GuideConsts gc, const int* __restrict__ fb_count,
                            const int32_t* __restrict__ fb_list, const int32_t* __restrict__ node_of) {
+    exp_tbl_init();
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x;
     const int count = *fb_count;
@@ -1613,6 +1642,7 @@ guide_group_fallback_kernel(const float* __restrict__ gp1, int Kp1, int K1, cons
                             const GuideMix* __restrict__ tab, GuideIO io, GuideConsts gc,
                             const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list,
                             int* __restrict__ fb2, const int32_t* __restrict__ node_of) {
+    exp_tbl_init();
     constexpr int G = kGroupLanes, GPW = 64 / G;
     const int lane = threadIdx.x;
     const int count = *fb_count;
@@ -1959,7 +1989,7 @@ __device__ __forceinline__ float mvtn_multiply(const float e[3], const float to_
     const float invDet = 1.0f / (Ls[0] * Ls[3]);
     const float s0 = om0 / Ls[0];
     const float s1 = (om1 - Ls[2] * s0) / Ls[3];
-    float w = (float)((double)norm2 * exp(-0.5 * (double)(s0 * s0 + s1 * s1)));
+    float w = gauss_w(norm2, s0 * s0 + s1 * s1);
     w = w * (invDet * jac);
     if (lazy && w == 0.0f) return 0.0f;
     // ts_exp_x(to_i, mt) and expJacobian(mt) share |mt|, its sinc and cos
@@ -2101,7 +2131,7 @@ __device__ __forceinline__ float prod_comp_pdf(const ProdComp& pc, const float d
     if (!ts_log_x(to, d, t0, t1, jac)) return 0.0f;
     const float s0 = pc.Linv[0] * t0 + pc.Linv[1] * t1;
     const float s1 = pc.Linv[2] * t0 + pc.Linv[3] * t1;
-    float v = (float)((double)norm2 * exp(-0.5 * (double)(s0 * s0 + s1 * s1)));
+    float v = gauss_w(norm2, s0 * s0 + s1 * s1);
     v *= pc.detInv * jac;
     return v;
 }
@@ -2290,6 +2320,7 @@ guide_product_cand_kernel(const float* __restrict__ gp, int Kp, int K, const flo
                           int64_t nq, GuideIO io, ProductIO pio, BsdfTab bt, GuideConsts gc, int cap,
                           int* __restrict__ fb_count, int32_t* __restrict__ fb_list,
                           const int32_t* __restrict__ perm) {
+    exp_tbl_init();
     __shared__ float cw[LCAP * 64];
     __shared__ unsigned short ck[LCAP * 64];
     const int tid = threadIdx.x;
@@ -2538,6 +2569,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDMM_PR
 guide_product_wave_kernel(const float* __restrict__ gp, int Kp, int K, const float* __restrict__ condCov,
                           GuideIO io, ProductIO pio, BsdfTab bt, GuideConsts gc, float* __restrict__ pscratch,
                           int pcap, const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list) {
+    exp_tbl_init();
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x;
     const WaveLds L = wave_lds(lds, K, pscratch, pcap, bt.M);
@@ -2588,6 +2620,7 @@ guide_tree_product_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideM
                                int32_t* __restrict__ fb_list, const int32_t* __restrict__ perm,
                                int32_t* __restrict__ node_out, NodeRoute rt, const uint32_t* __restrict__ skeys,
                                int mb) {
+    exp_tbl_init();
     __shared__ float cw[LCAP * 64];
     __shared__ unsigned short ck[LCAP * 64];
     const int tid = threadIdx.x;
@@ -2639,6 +2672,7 @@ guide_tree_product_wave_kernel(const STNodeDev* __restrict__ nodes, const GuideM
                                BsdfTab bt, GuideConsts gc, float* __restrict__ pscratch, int pcap,
                                const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list,
                                const int32_t* __restrict__ node_of) {
+    exp_tbl_init();
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x;
     const WaveLds L = wave_lds(lds, kmax, pscratch, pcap, bt.M);
@@ -3196,6 +3230,21 @@ hipError_t launch_sample_cdf(const float* cdf, int n, const float* u, int64_t nq
     hipLaunchKernelGGL(sample_cdf_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, cdf, n, u,
                        nq, out);
     return hipGetLastError();
+}
+
+hipError_t launch_norm_exp_test(const float* q, int64_t n, float norm, float* out, int32_t* fast, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(norm_exp_test_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, q, n, norm, out, fast);
+    return hipGetLastError();
+}
+void norm_exp_test_host(const float* q, int64_t n, float norm, float* out, int32_t* fast) {
+    static const double tbl[64] = {SDMM_EXP2J_TABLE};
+    for (int64_t i = 0; i < n; ++i) {
+        int ok;
+        const float f = norm_exp_try(norm, q[i], tbl, &ok);
+        out[i] = ok ? f : norm_exp_ref(norm, q[i]);
+        if (fast) fast[i] = ok;
+    }
 }
 
 }  // namespace sdmm

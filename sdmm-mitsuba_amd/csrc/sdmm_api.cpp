@@ -89,6 +89,8 @@ hipError_t launch_stree_route(const void* nodes, int num_nodes, int key_bits, co
                               uint32_t* keys0, uint32_t* keys1, int32_t* idx0, int32_t* idx1, void* temp,
                               size_t temp_bytes, int64_t* seg_dev, float* const out_x[6], float* out_w,
                               float* out_h, uint8_t* out_d, hipStream_t st);
+hipError_t launch_norm_exp_test(const float* q, int64_t n, float norm, float* out, int32_t* fast, hipStream_t st);
+void norm_exp_test_host(const float* q, int64_t n, float norm, float* out, int32_t* fast);
 hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float* const c[3],
                         const float* const u[3], const float* const dgiven[3], float* const d[3], float* pdf,
                         int32_t* comp, float norm2, float norm3, int cap, int* fb_count, int32_t* fb_list,
@@ -605,6 +607,18 @@ extern "C" {
 
 const char* sdmm_last_error(void) { return g_err.c_str(); }
 int sdmm_abi_version(void) { return SDMM_ABI_VERSION; }
+
+int sdmm_test_norm_exp(const float* q, int64_t n, float norm, int on_device, int device, float* out, int32_t* fast) {
+    if (n < 0 || (n > 0 && (!q || !out)) || !(norm > 0.0f)) return fail(SDMM_E_INVALID, "invalid argument");
+    if (!on_device) {
+        norm_exp_test_host(q, n, norm, out, fast);
+        return SDMM_OK;
+    }
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(launch_norm_exp_test(q, n, norm, out, fast, nullptr));
+    HIP_TRY(hipDeviceSynchronize());
+    return SDMM_OK;
+}
 
 void sdmm_em_params_default(sdmm_em_params* p) {
     if (!p) return;

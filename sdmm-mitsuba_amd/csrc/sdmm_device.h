@@ -111,6 +111,12 @@ enum : int {
     SC_HTW = 0, SC_SGH, SC_NORM, SC_IT, SC_ALPHA, SC_NI, SC_DECP, SC_CUT, SC_STATUS, SC_COUNT
 };
 
+// The bits of a float VALUE.  Never write __builtin_bit_cast(T, v.y) or
+// (T, v[j]) on an ext_vector element: hipcc (ROCm 7.2, clang) lowers a bit
+// cast of a vector-element lvalue as a read of element 0 (checked in the IR;
+// tests/test_gpu_parity.py test_rare_angle_every_lane_slot is the regression).
+__device__ __forceinline__ uint32_t fbits(float x) { return __builtin_bit_cast(uint32_t, x); }
+
 struct SamplesDev {
     const float* x[6];
     const float* w;

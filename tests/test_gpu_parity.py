@@ -361,6 +361,48 @@ def test_rare_angle_cases(pkg, oracle, synth, gpu, plog, K):
     _check_resp(got[keep], ref[keep], mix.get_params(), x[:, keep], plog, min_frac=0.3)
 
 
+@pytest.mark.parametrize("kernel,K", [("split", 128), ("split", 16), ("tile", 128), ("mfma", 128),
+                                      ("legacy", 128)])
+def test_rare_angle_every_lane_slot(pkg, oracle, synth, gpu, plog, monkeypatch, kernel, K):
+    """The reference's far-side quirk (mvtn.h:157-164: sin < 1e-3 with cos < 0
+    gives J = 1, so a direction 4e-4..9e-4 rad from ANTIPODAL to component k's
+    mean direction, at k's spatial mean, is explained by k) for every
+    component k, i.e. at every (lane, slot) position of the kernels' pair
+    layouts, on an unfitted mixture (wide directional covariances, so the
+    quirk changes the posteriors by O(1)), with no NaN row to force the tile
+    redo.  Regression: a bit cast of a vector element read element 0 only
+    (sdmm_device.h fbits), so the rare-angle detector saw one slot in four."""
+    import torch
+    monkeypatch.setenv("SDMM_RESP_KERNEL", kernel)
+    N = 8 * K
+    b, mix, om, ost, ds, os_ = _setup(pkg, oracle, synth, K, N, guards=False)
+    p = mix.get_params()
+    mu = p["mean"].astype(np.float64)
+    x = b["x"].copy()
+    rng = np.random.default_rng(11)
+    for i in range(N):
+        k = i % K
+        n = mu[k, 3:6] / np.linalg.norm(mu[k, 3:6])
+        t = np.cross(n, [0.0, 0.0, 1.0] if abs(n[2]) < 0.9 else [1.0, 0.0, 0.0])
+        t /= np.linalg.norm(t)
+        dl = rng.uniform(4e-4, 9e-4)
+        x[0:3, i] = mu[k, 0:3].astype(np.float32)
+        x[3:6, i] = (-np.cos(dl) * n + np.sin(dl) * t).astype(np.float32)
+    xt = [torch.from_numpy(x[i].copy()).to(gpu) for i in range(6)]
+    resp = torch.full((N, K), -1.0, device=gpu)
+    mix.posterior(pkg.DeviceSamples(xt, ds.w), resp)
+    got = resp.cpu().numpy()
+    ref = oracle.responsibilities(om, oracle.Samples(x, b["w"]))
+    exact = posterior_f64(p, x)
+    # the quirk matters: the targeted component holds a large share
+    tgt = exact[np.arange(N), np.arange(N) % K]
+    assert np.median(tgt) > 0.05
+    err = np.abs(got[np.arange(N), np.arange(N) % K] - tgt).max()
+    plog(f"rare_slot_{kernel}_{K}_target_err", err, 2e-5)
+    assert err <= 2e-5, err
+    _check_resp(got, ref, p, x, plog, min_frac=0.3)
+
+
 def _em_model(pkg, oracle, synth, K, N, iters):
     b, mix, om, ost, ds, os_ = _setup(pkg, oracle, synth, K, N)
     for _ in range(iters):
