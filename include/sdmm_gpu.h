@@ -564,6 +564,10 @@ typedef struct {
      * (sdmm_proc.cpp:297, :383-409, :764). */
     const float* bsdf_params;
 } sdmm_scene_desc;
+/* The descriptor has grown across ABI revisions (bsdf_params was appended):
+ * zero-initialise it (`sdmm_scene_desc d = {0};` / `memset`) before filling
+ * the fields you use, so an older caller's unset trailing pointer is NULL --
+ * sdmm_scene_create reads every field. */
 typedef struct {
     int spp;
     int max_depth;            /* maxDepth (:649, :684), -1 = unbounded (capped by the vertex slots) */
@@ -702,16 +706,6 @@ int sdmm_guiding_iteration(sdmm_guiding* g, sdmm_scene* scene, const sdmm_li_par
  * rgb[3][height][width].  The plugin writes iteration%05i.exr (the pass's
  * mean) and iteration_sqr%05i.exr (its mean of squares) per render pass. */
 int sdmm_write_exr(const char* path, int width, int height, const float* rgb, int spp, int iteration, float time);
-
-/* Test hook (no reference counterpart): out[i] = NORM exp(-q[i]/2) as the
- * guide kernels evaluate every Gaussian weight -- the reference expression
- * (float)((double)norm * exp(-0.5 * (double)q)) of multivariate_normal.h:126
- * through the table-driven fast path and its Ziv rounding test
- * (sdmm-mitsuba_amd/csrc/fastexp.h).  on_device = 0: host code, q / out /
- * fast are host arrays; 1: the device path on `device`, q / out / fast are
- * device pointers.  fast[i] (nullable) = 1 when the fast path decided the
- * float, 0 when the reference expression was evaluated. */
-int sdmm_test_norm_exp(const float* q, int64_t n, float norm, int on_device, int device, float* out, int32_t* fast);
 
 const char* sdmm_last_error(void);
 int sdmm_abi_version(void);

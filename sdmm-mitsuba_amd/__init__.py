@@ -86,9 +86,6 @@ def lib():
         L.sdmm_stats_len.argtypes = [C.c_int]
         L.sdmm_get_stream.restype = C.c_void_p
         L.sdmm_get_stream.argtypes = [C.c_void_p]
-        if hasattr(L, "sdmm_test_norm_exp"):   # (absent from A/B builds of older sources)
-            L.sdmm_test_norm_exp.argtypes = [C.c_void_p, C.c_int64, C.c_float, C.c_int, C.c_int, C.c_void_p,
-                                             C.c_void_p]
         L.sdmm_create.argtypes = [C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
         L.sdmm_destroy.argtypes = [C.c_void_p]
         L.sdmm_layout.argtypes = [C.c_void_p] + [C.POINTER(C.c_int)] * 4
@@ -192,32 +189,11 @@ def _check(rc: int):
         raise SDMMError(f"sdmm error {rc}: {lib().sdmm_last_error().decode()}")
 
 
-def norm_exp(q, norm: float, device=None):
-    """NORM exp(-q/2) per element as the guide kernels evaluate their Gaussian
-    weights (fastexp.h: table-driven double + Ziv rounding test, else the
-    reference expression).  q: float32 numpy array (host path) or a CUDA
-    tensor (device path).  Returns (values, fast-path flags)."""
-    if device is None:
-        qa = np.ascontiguousarray(q, dtype=np.float32)
-        out = np.empty_like(qa)
-        fast = np.empty(qa.shape, dtype=np.int32)
-        _check(lib().sdmm_test_norm_exp(qa.ctypes.data, qa.size, norm, 0, 0, out.ctypes.data, fast.ctypes.data))
-        return out, fast
-    import torch
-    qt = q.contiguous()
-    out = torch.empty_like(qt)
-    fast = torch.empty(qt.shape, dtype=torch.int32, device=qt.device)
-    _check(lib().sdmm_test_norm_exp(qt.data_ptr(), qt.numel(), norm, 1, qt.device.index or 0, out.data_ptr(),
-                                    fast.data_ptr()))
-    return out, fast
-
-
 def stats_len(K: int) -> int:
     return 2 + 21 * K
 
 
 EXPORTED_SYMBOLS = [
-    "sdmm_test_norm_exp",
     "sdmm_em_params_default", "sdmm_create", "sdmm_destroy", "sdmm_num_components", "sdmm_layout",
     "sdmm_kernel_name",
     "sdmm_set_guide_capacity", "sdmm_set_guide_order", "sdmm_guide_fallback_count",

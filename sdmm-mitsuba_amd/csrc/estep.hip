@@ -782,7 +782,7 @@ estep_stats_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, in
         const float thr = nm.fin ? 1e-10f : __builtin_inff();
         // Spatial statistics are accumulated centred on the component's mean
         // position (tp = p - mu_k) and un-centred in fp64 by
-        // uncenter_stats_kernel: the M-step's C/W - mu mu^T then does not
+        // sum_uncenter_kernel: the M-step's C/W - mu mu^T then does not
         // amplify fp32 accumulation error by |p|^2 / sigma^2.
 #pragma unroll
         for (int c = 0; c < NP; ++c) {
@@ -1149,7 +1149,7 @@ estep_stats_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
 // vector [H, wsum, W(K), M(5K), Clow(15K)], in two launches so the whole chip
 // takes part: stage 1 = (64-column block) x (row slice) workgroups, each
 // summing its slice in a fixed order into slice[s][col]; stage 2 (inside
-// sum_slices_kernel) sums the kReduceSlices slices of each column in order.
+// sum_uncenter_kernel) sums the kReduceSlices slices of each column in order.
 constexpr int kReduceSlices = 16;
 
 __device__ __forceinline__ int partial_col(int o, int Kp, int K) {
@@ -1189,17 +1189,6 @@ reduce_partials_slices_kernel(const float* __restrict__ partials, int rows, int 
 // statistics (fp64):
 //   M_p = M'_p + W mu,  C_pp = C'_pp + M'_p mu^T + mu M'_p^T + W mu mu^T,
 //   C_tp = C'_tp + M_t mu^T   (mu = the float mean the E-step subtracted).
-// Stage 2 of the reduction, one thread per stats column (coalesced): the
-// slices of column o summed in slice order, into stats[o].
-__global__ void __launch_bounds__(256)
-sum_slices_kernel(int ncols, const double* __restrict__ slices, double* __restrict__ stats) {
-    const int o = blockIdx.x * blockDim.x + threadIdx.x;
-    if (o >= ncols) return;
-    double t = 0.0;
-#pragma unroll
-    for (int sl = 0; sl < kReduceSlices; ++sl) t += slices[(int64_t)sl * ncols + o];
-    stats[o] = t;
-}
 // The un-centring of one component's spatial statistics (fp64, in place).
 __device__ __forceinline__ void uncenter_component(const double mu[3], double w, double M[5], double C[15]) {
     // C_pp (entries 0..5: (0,0) (1,0) (1,1) (2,0) (2,1) (2,2))
@@ -1214,26 +1203,9 @@ __device__ __forceinline__ void uncenter_component(const double mu[3], double w,
     }
     for (int i = 0; i < 3; ++i) M[i] = M[i] + w * mu[i];
 }
-// Then one thread per component un-centres its own columns in place (the
-// statistics were accumulated about mu_k).  Together: the former one-thread-
-// per-component kernel operation for operation (bitwise), which read its 21 x
-// 16 strided values on 128 threads (19 us of a 0.4 ms K = 128 EM step).
-__global__ void uncenter_stats_kernel(const float* __restrict__ ep, int Kp, int K, double* __restrict__ stats) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= K) return;
-    const double mu[3] = {(double)ep[EP_MU0 * Kp + k], (double)ep[EP_MU1 * Kp + k],
-                          (double)ep[EP_MU2 * Kp + k]};
-    const double w = stats[2 + k];
-    double M[5], C[15];   // C: lower triangle, row-major
-    for (int i = 0; i < 5; ++i) M[i] = stats[2 + K + 5 * k + i];
-    for (int i = 0; i < 15; ++i) C[i] = stats[2 + 6 * K + 15 * k + i];
-    uncenter_component(mu, w, M, C);
-    for (int i = 0; i < 5; ++i) stats[2 + K + 5 * k + i] = M[i];
-    for (int i = 0; i < 15; ++i) stats[2 + 6 * K + 15 * k + i] = C[i];
-}
-
-// sum_slices_kernel + uncenter_stats_kernel in ONE launch (the default;
-// SDMM_REDUCE_SPLIT=1 keeps the two launches): workgroup b owns components
+// Stage 2: the slices summed and the statistics un-centred in ONE launch
+// (round 4: two launches, a per-column slice sum then a per-component
+// un-centring, bitwise the same and slower): workgroup b owns components
 // kSumCB b .. kSumCB b + kSumCB - 1, one thread per column of theirs (their W,
 // M and C columns are three contiguous runs of the compact vector) sums the
 // slices in slice order into LDS, then one thread per component un-centres
@@ -1287,7 +1259,7 @@ sum_uncenter_kernel(int ncols, const double* __restrict__ slices, const float* _
 // Batched reduction + finalisation: thread (leaf blockIdx.y, component k)
 // reproduces, operation for operation, reduce_partials_slices_kernel (slices
 // of the leaf's rows, four row-interleaved fp64 partials per slice combined as
-// ((b0 + b1) + b2) + b3) followed by sum_slices_kernel + uncenter_stats_kernel (slices summed in
+// ((b0 + b1) + b2) + b3) followed by sum_uncenter_kernel (slices summed in
 // order, then the un-centring), so a batched leaf's stats are bitwise those of
 // its single-mixture E-step.
 __device__ __forceinline__ double batched_col(const float* __restrict__ partials, int pstride, int row0, int rows,
@@ -1307,61 +1279,13 @@ __device__ __forceinline__ double batched_col(const float* __restrict__ partials
     return t;
 }
 
-// batched_col with the column's rows fetched eight at a time as independent
-// loads (batched_col's loops of data-dependent trip count issue one load per
-// iteration, so a thread waits out one memory latency per row), then summed in
-// row order into the same per-slice sums: row r of slice sl adds to
-// b[(r - r0(sl)) & 3]; every slice, an empty one too, adds its
-// ((b0 + b1) + b2) + b3 to t in slice order.  The same additions in the same
-// order: bitwise equal.  (A b only ever starts at +0.0, so the selects below
-// never need to add a zero.)
-__device__ __forceinline__ double batched_col_mlp(const float* __restrict__ partials, int pstride, int row0,
-                                                  int rows, int col) {
-    constexpr int B = 8;
-    double t = 0.0, b0 = 0.0, b1 = 0.0, b2 = 0.0, b3 = 0.0;
-    int sl = 0, r0 = 0, r1 = (int)((int64_t)rows / kReduceSlices);
-    const float* p = partials + (int64_t)row0 * pstride + col;
-    for (int base = 0; base < rows; base += B) {
-        float v[B];
-#pragma unroll
-        for (int j = 0; j < B; ++j) v[j] = (base + j < rows) ? p[(int64_t)(base + j) * pstride] : 0.0f;
-#pragma unroll
-        for (int j = 0; j < B; ++j) {
-            const int r = base + j;
-            if (r >= rows) break;
-            while (r >= r1) {   // close slice sl (and any empty ones after it)
-                t += ((b0 + b1) + b2) + b3;
-                b0 = b1 = b2 = b3 = 0.0;
-                ++sl;
-                r0 = r1;
-                r1 = (int)((int64_t)rows * (sl + 1) / kReduceSlices);
-            }
-            const double x = (double)v[j];
-            const int w = (r - r0) & 3;
-            if (w == 0) b0 += x;
-            else if (w == 1) b1 += x;
-            else if (w == 2) b2 += x;
-            else b3 += x;
-        }
-    }
-    for (; sl < kReduceSlices; ++sl) {
-        t += ((b0 + b1) + b2) + b3;
-        b0 = b1 = b2 = b3 = 0.0;
-    }
-    return t;
-}
-#ifdef SDMM_REDUCE_MLP
-constexpr bool kReduceMlp = true;
-#else
-constexpr bool kReduceMlp = false;   // batched_col's one load per iteration
-#endif
 
 // One workgroup per leaf.  Phase 1: one thread per stats column (consecutive
 // threads read consecutive partial columns of a row: coalesced), each column
 // reduced exactly as batched_col / the single-mixture path orders it (16 row
 // slices, four row-interleaved fp64 sums per slice combined as
 // ((b0 + b1) + b2) + b3, slices summed in order) into LDS.  Phase 2: the
-// un-centring of the spatial moments per component, as uncenter_stats_kernel.
+// un-centring of the spatial moments per component, as sum_uncenter_kernel.
 // Bitwise equal to the previous thread-per-component form, with 21x more
 // threads in flight (it was latency-bound: 16 busy lanes per leaf): 257 ->
 // ~50 us per 256-leaf K=16 step (a (column, slice) split measured no faster).
@@ -1374,8 +1298,7 @@ reduce_finalize_batched_kernel(const float* __restrict__ partials, int pstride, 
     if (L.n <= 0) return;             // uniform over the workgroup
     const int ncols = 2 + 21 * K;
     for (int o = threadIdx.x; o < ncols; o += blockDim.x)
-        red[o] = kReduceMlp ? batched_col_mlp(partials, pstride, L.row0, L.rows, partial_col(o, Kp, K))
-                            : batched_col(partials, pstride, L.row0, L.rows, partial_col(o, Kp, K));
+        red[o] = batched_col(partials, pstride, L.row0, L.rows, partial_col(o, Kp, K));
     __syncthreads();
     double* stats = L.stats;
     if (threadIdx.x < 2) stats[threadIdx.x] = red[threadIdx.x];
@@ -1553,19 +1476,8 @@ hipError_t launch_reduce_partials(const float* partials, int rows, int pstride, 
                        partials, rows, pstride, Kp, K, scratch);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    static const bool split = [] {
-        const char* v = std::getenv("SDMM_REDUCE_SPLIT");
-        return v && v[0] == '1';
-    }();
-    if (!split) {
-        hipLaunchKernelGGL(sum_uncenter_kernel, dim3((K + kSumCB - 1) / kSumCB), dim3(256), 0, st, ncols, scratch,
-                           ep_for_finalize, Kp, K, stats);
-        return hipGetLastError();
-    }
-    hipLaunchKernelGGL(sum_slices_kernel, dim3((ncols + 255) / 256), dim3(256), 0, st, ncols, scratch, stats);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(uncenter_stats_kernel, dim3((K + 63) / 64), dim3(64), 0, st, ep_for_finalize, Kp, K, stats);
+    hipLaunchKernelGGL(sum_uncenter_kernel, dim3((K + kSumCB - 1) / kSumCB), dim3(256), 0, st, ncols, scratch,
+                       ep_for_finalize, Kp, K, stats);
     return hipGetLastError();
 }
 

@@ -25,7 +25,6 @@
 // direction and the mixture pdf (tolerances 1e-5 / 1e-4) use the float
 // transcendentals.
 #include "sdmm_device.h"
-#include "fastexp.h"
 #include <cstdlib>
 
 #include <hipcub/hipcub.hpp>
@@ -38,17 +37,15 @@ struct GuideConsts {
     float norm2, norm3;
 };
 
-// The 2^(j/64) table of norm_exp (fastexp.h), one copy per workgroup in LDS:
-// every kernel of this file that reaches a Gaussian weight fills it first
-// (exp_tbl_init, before any early exit).
-__constant__ double kExp2JDev[64] = {SDMM_EXP2J_TABLE};
-__shared__ double g_exp2j[64];
-__device__ __forceinline__ void exp_tbl_init() {
-    if (threadIdx.x < 64) g_exp2j[threadIdx.x] = kExp2JDev[threadIdx.x];
-    __syncthreads();
+// A Gaussian weight as the reference forms it: (float)((double)norm *
+// exp(-0.5 * (double)q)) (multivariate_normal.h:126, mvtn.h:359).  Round 5
+// measured a table-driven double exp decided by a Ziv rounding test in its
+// place: no faster (the device double exp is ~30 instructions, 14 of them
+// DFMA, about what the table path costs) and the LDS table cost occupancy --
+// Cornell K = 128 guided pass 12.0 vs 11.3 ms, K = 512 product 91 vs 86 ms.
+__device__ __forceinline__ float gauss_w(float norm, float q) {
+    return (float)((double)norm * exp(-0.5 * (double)q));
 }
-// (float)((double)norm * exp(-0.5 * (double)q)), bit for bit (fastexp.h)
-__device__ __forceinline__ float gauss_w(float norm, float q) { return norm_exp(norm, q, g_exp2j); }
 
 __device__ __forceinline__ float gp_ld(const float* gp, int Kp, int f, int k) {
     return ((cfloat_p)gp)[k * GP_STRIDE + f];   // AoS record (sdmm_device.h)
@@ -230,18 +227,6 @@ __device__ __forceinline__ bool cond_valid(const float* gp, int Kp, int k, const
     float t1 = gp_ld(gp, Kp, GP_P10, k) * d0 + gp_ld(gp, Kp, GP_P11, k) * d1 + gp_ld(gp, Kp, GP_P12, k) * d2;
     float length = sqrtf(t0 * t0 + t1 * t1);
     return !((double)length >= kPi);
-}
-
-// test hook (sdmm_test_norm_exp): the device norm_exp over an array of q
-__global__ void __launch_bounds__(256) norm_exp_test_kernel(const float* __restrict__ q, int64_t n, float norm,
-                                                           float* __restrict__ out, int32_t* __restrict__ fast) {
-    exp_tbl_init();
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    int ok;
-    const float f = norm_exp_try(norm, q[i], g_exp2j, &ok);
-    out[i] = ok ? f : norm_exp_ref(norm, q[i]);
-    if (fast) fast[i] = ok;
 }
 
 // ---------------------------------------------------------------------------
@@ -444,74 +429,15 @@ __device__ __forceinline__ int build_candidates(const float* gp, int Kp, int K, 
     return (ncand == K) ? K : -1;
 }
 
-// The same list built in REGISTERS (LCAP entries, static indices): a live
-// weight ripples through the sorted list by compare-and-swap (strictly
-// greater moves ahead: ties keep the earlier, lower index), the entry pushed
-// past slot cap - 1 is the dropped one.  No LDS latency chain per shift; the
-// finished list goes to the LDS slots once for the walk and finish.  Same
-// list, same results.  Measured (A/B, one box): the tree wavefront over
-// K = 128 leaves (wide, long lists) 21.1 -> 17.6 ms per guided pass; the
-// K = 16 leaves and the single trained K = 128 mixture (short lists, where
-// the ripple's fixed LCAP-step cost and its registers outweigh the LDS
-// shifts) 466 -> 489 us and 618 -> 692 us -- so only the tree kernel's
-// LCAP = 40 instance uses it.
-template <int LCAP>
-__device__ __forceinline__ int build_candidates_cas(const float* gp, int Kp, int K, const float c[3], float* cw,
-                                                    unsigned short* ck, int T, int tid, float norm3, int cap,
-                                                    float& accum) {
-    float rw[LCAP];
-    int rk[LCAP];
-#pragma unroll
-    for (int i = 0; i < LCAP; ++i) { rw[i] = -1.0f; rk[i] = 0; }
-    float total = 0.0f;
-    int cnt = 0;
-    const float skip_f = 0.0089f / (float)K;
-    MargRec nx = load_marg(gp, 0);
-    for (int k = 0; k < K; ++k) {
-        const MargRec rec = nx;
-        if (k + 1 < K) nx = load_marg(gp, k + 1);
-        const float w = marginal_weight_rec(rec, c, norm3);
-        total += w;
-        if (!(w > 0.0f) || w < total * skip_f) continue;
-        float x = w;
-        int xk = k;
-#pragma unroll
-        for (int i = 0; i < LCAP; ++i) {
-            const bool sw = (i < cap) && (x > rw[i]);
-            const float tw = rw[i];
-            const int tk = rk[i];
-            rw[i] = sw ? x : tw;
-            rk[i] = sw ? xk : tk;
-            x = sw ? tw : x;
-            xk = sw ? tk : xk;
-        }
-        cnt = min(cnt + 1, cap);
-    }
-#pragma unroll
-    for (int i = 0; i < LCAP; ++i)
-        if (i < cnt) {
-            cw[i * T + tid] = rw[i];
-            ck[i * T + tid] = (unsigned short)rk[i];
-        }
-    if (!__builtin_isfinite(total)) return -1;
-    if (total == 0.0f) return kNoMass;   // every marginal weight zero: BSDF only (below)
-    const float cutoff = (float)(0.99 * (double)total);
-    const double tau = ((double)total - (double)cutoff) / (double)K * 0.999;
-    if (!(tau > 0.0)) return -1;
-    int ncand = 0;
-    while (ncand < cnt && (double)cw[ncand * T + tid] >= tau) ++ncand;
-    accum = 0.0f;
-    for (int i = 0; i < ncand; ++i) {
-        const int k = ck[i * T + tid];
-        const bool ok = cond_valid(gp, Kp, k, c);
-        ck[i * T + tid] = (unsigned short)(k | (ok ? 0x8000 : 0));
-        accum += ok ? cw[i * T + tid] : 0.0f;
-        if (accum >= cutoff) return i + 1;
-    }
-    return (ncand == K) ? K : -1;
-}
-
-// The register list again, with each (weight, index) entry one orderable
+// The same list built in REGISTERS (LCAP entries, static indices), the
+// finished list written to the LDS slots once for the walk and finish.
+// Measured (A/B, one box): the tree wavefront over K = 128 leaves (wide,
+// long lists) 21.1 -> 17.6 ms per guided pass as a (weight, index)
+// compare-and-swap ripple; the K = 16 leaves and the single trained K = 128
+// mixture (short lists, where the ripple's fixed LCAP-step cost and its
+// registers outweigh the LDS shifts) 466 -> 489 us and 618 -> 692 us -- so
+// only the LCAP = 40 instances use it.
+// Each (weight, index) entry is one orderable
 // 64-bit key held as a double: bits 63..32 = the weight's bits + 1 (weights
 // here are positive normal floats, so the pattern is a positive normal double
 // and the doubles order as the keys), bits 31..0 = 2^32 - 1 - index (a larger
@@ -535,10 +461,7 @@ template <int LCAP>
 __device__ __forceinline__ int build_candidates_key(const float* gp, int Kp, int K, const float c[3], float* cw,
                                                     unsigned short* ck, int T, int tid, float norm3, int cap,
                                                     float& accum) {
-#ifndef SDMM_RIPPLE_CHUNK
-#define SDMM_RIPPLE_CHUNK 8   // slots per skippable chunk (A/B)
-#endif
-    constexpr int CH = (LCAP % SDMM_RIPPLE_CHUNK == 0) ? SDMM_RIPPLE_CHUNK : 8;
+    constexpr int CH = 8;   // slots per skippable chunk (round 4: chunks of 4 / 20 measured the same)
     static_assert(LCAP % CH == 0, "whole chunks");
     double L[LCAP];
 #pragma unroll
@@ -596,11 +519,7 @@ template <int LCAP>
 __device__ __forceinline__ int build_candidates_reg(const float* gp, int Kp, int K, const float c[3], float* cw,
                                                     unsigned short* ck, int T, int tid, float norm3, int cap,
                                                     float& accum) {
-#ifdef SDMM_GUIDE_RIPPLE_CAS
-    return build_candidates_cas<LCAP>(gp, Kp, K, c, cw, ck, T, tid, norm3, cap, accum);
-#else
     return build_candidates_key<LCAP>(gp, Kp, K, c, cw, ck, T, tid, norm3, cap, accum);
-#endif
 }
 
 // Plane pointers of one guided batch (inputs c, u or given directions e;
@@ -683,57 +602,12 @@ __device__ __forceinline__ bool serve_cand(const float* gp, int Kp, int K, const
     return false;
 }
 
-// Per-node routing of the tree wavefronts.  stats[3 n] counts the queries of
-// node n the candidate kernel served (uniform-leaf waves), stats[3 n + 1] how
-// many of them still needed the full-K path, and stats[3 n + 2] = 1 sends
-// node n's queries straight to the full-K path: guide_route_kernel sets it
-// before each candidate launch once more than two thirds of a node's served
-// queries fell back (routing pays when the fallback fraction p exceeds
-// 1 - c / F, c and F the per-query costs of the candidate and full-K paths:
-// 1.2 / 3.2 ns at K = 128, 10 / 32 ns for the K = 512 product).  A routed
-// query is served by the full-K path, whose result is the candidate path's
-// bit for bit, so routing changes the cost of a query, never its result.  The
-// counts start from zero whenever a different mixture table is bound.
-struct NodeRoute {
-    uint32_t* stats;   // 3 x nodes, or null: no routing
-    int nn;
-};
-constexpr uint32_t kRouteMinQueries = 256;
-__global__ void guide_route_kernel(uint32_t* __restrict__ stats, int nn) {
-    const int n = blockIdx.x * blockDim.x + threadIdx.x;
-    if (n >= nn) return;
-    uint32_t q = stats[3 * n], f = stats[3 * n + 1];
-    if (q >= (1u << 31)) {   // keep the counts far from wrapping
-        q >>= 1;
-        f >>= 1;
-        stats[3 * n] = q;
-        stats[3 * n + 1] = f;
-    }
-    stats[3 * n + 2] = (q >= kRouteMinQueries && (uint64_t)f * 3 > (uint64_t)q * 2) ? 1u : 0u;
-}
-static hipError_t launch_route(const NodeRoute& rt, hipStream_t st) {
-    if (!rt.stats || rt.nn <= 0) return hipSuccess;
-    hipLaunchKernelGGL(guide_route_kernel, dim3((unsigned)((rt.nn + 255) / 256)), dim3(256), 0, st, rt.stats, rt.nn);
-    return hipGetLastError();
-}
-// a uniform-leaf wave's counts: its queries and those that fell back
-__device__ __forceinline__ void route_count(const NodeRoute& rt, int n, bool fell) {
-    const uint64_t act = __builtin_amdgcn_ballot_w64(true);
-    const uint64_t fb = __builtin_amdgcn_ballot_w64(fell);
-    const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-    if (below == 0) {
-        atomicAdd(&rt.stats[3 * n], (uint32_t)__builtin_popcountll(act));
-        if (fb) atomicAdd(&rt.stats[3 * n + 1], (uint32_t)__builtin_popcountll(fb));
-    }
-}
-
 // LDS list capacity LCAP (24 or 40): the lists are 6 B per entry per thread,
 // so the capacity sets the workgroups per CU (LDS-limited occupancy).
 template <bool PDF_ONLY, int LCAP>
 __global__ void __launch_bounds__(64)
 guide_cand_kernel(const float* __restrict__ gp, int Kp, int K, int64_t nq, GuideIO io, GuideConsts gc, int cap,
                   int* __restrict__ fb_count, int32_t* __restrict__ fb_list, const int32_t* __restrict__ perm) {
-    exp_tbl_init();
     __shared__ float cw[LCAP * 64];
     __shared__ unsigned short ck[LCAP * 64];
     const int tid = threadIdx.x;
@@ -757,8 +631,7 @@ __global__ void __launch_bounds__(64)
 guide_tree_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __restrict__ tab, int64_t nq,
                        GuideIO io, GuideConsts gc, int cap, int* __restrict__ fb_count,
                        int32_t* __restrict__ fb_list, const int32_t* __restrict__ perm,
-                       int32_t* __restrict__ node_out, NodeRoute rt, const uint32_t* __restrict__ skeys, int mb) {
-    exp_tbl_init();
+                       int32_t* __restrict__ node_out, const uint32_t* __restrict__ skeys, int mb) {
     __shared__ float cw[LCAP * 64];
     __shared__ unsigned short ck[LCAP * 64];
     const int tid = threadIdx.x;
@@ -781,12 +654,9 @@ guide_tree_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __re
             const GuideMix mx = uniform_mix((n0 >= 0) ? tab[n0] : GuideMix{nullptr, 0, 0});
             if (mx.K <= 0) {
                 write_invalid<PDF_ONLY>(io, q);
-            } else if (rt.stats && rt.stats[3 * n0 + 2]) {
-                fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;   // routed: the full-K path serves it
             } else {
-                const bool fell = serve_cand<PDF_ONLY, LCAP, (LCAP >= kGuideRegCap)>(
-                    mx.gp, mx.Kp, mx.K, io, q, c, cw, ck, tid, cap, gc, fb_count, fb_list);
-                if (rt.stats) route_count(rt, n0, fell);
+                serve_cand<PDF_ONLY, LCAP, (LCAP >= kGuideRegCap)>(mx.gp, mx.Kp, mx.K, io, q, c, cw, ck, tid, cap, gc,
+                                                                 fb_count, fb_list);
             }
             return;
         }
@@ -1180,7 +1050,6 @@ template <bool PDF_ONLY>
 __global__ void __launch_bounds__(64)
 guide_fallback_kernel(const float* __restrict__ gp, int Kp, int K, GuideIO io, GuideConsts gc,
                       const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list) {
-    exp_tbl_init();
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x;
     const int count = *fb_count;
@@ -1199,7 +1068,6 @@ __global__ void __launch_bounds__(64)
 guide_tree_fallback_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __restrict__ tab, int kmax,
                            GuideIO io, GuideConsts gc, const int* __restrict__ fb_count,
                            const int32_t* __restrict__ fb_list, const int32_t* __restrict__ node_of) {
-    exp_tbl_init();
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x;
     const int count = *fb_count;
@@ -1628,21 +1496,17 @@ __device__ __forceinline__ bool serve_full_group_g(const float* gp, int Kp, int 
 // 16 (default) or 4 lanes per query.  Round 4 A/B, Cornell K=128 tree
 // wavefront: 12.4 ms per guided pass with 16-lane groups, 13.1 ms with 4-lane
 // groups (32 slots per lane: 256 VGPRs with a spill, 2 waves per SIMD)
-#ifndef SDMM_GROUP_LANES
-#define SDMM_GROUP_LANES 16
-#endif
-constexpr int kGroupLanes = SDMM_GROUP_LANES;
-#ifndef SDMM_GROUP_WPE
-#define SDMM_GROUP_WPE 4   // 16-lane groups: 128 VGPRs, no spill; K=128 guided pass 17.6 -> 15.2 ms (2: 189 VGPRs)
-#endif
+// 16-lane groups (round 4: 4-lane groups, 16 queries per wave, spilled and
+// lost: 13.1 against 12.0 ms per K = 128 guided pass)
+constexpr int kGroupLanes = 16;
+constexpr int kGroupWpe = 4;   // 128 VGPRs, no spill; K=128 guided pass 17.6 -> 15.2 ms (2: 189 VGPRs)
 // (4-lane groups with 16 or 32 slots: 256 VGPRs, 2 waves per SIMD, no spill)
 template <bool PDF_ONLY, bool TREE, int S>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(S >= 16 ? 2 : SDMM_GROUP_WPE)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(S >= 16 ? 2 : kGroupWpe)))
 guide_group_fallback_kernel(const float* __restrict__ gp1, int Kp1, int K1, const STNodeDev* __restrict__ nodes,
                             const GuideMix* __restrict__ tab, GuideIO io, GuideConsts gc,
                             const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list,
                             int* __restrict__ fb2, const int32_t* __restrict__ node_of) {
-    exp_tbl_init();
     constexpr int G = kGroupLanes, GPW = 64 / G;
     const int lane = threadIdx.x;
     const int count = *fb_count;
@@ -1652,11 +1516,7 @@ guide_group_fallback_kernel(const float* __restrict__ gp1, int Kp1, int K1, cons
     // record of a query is fetched in a three-stage pipeline across this
     // group's iterations (entry three ahead, node two ahead, record one
     // ahead), so no iteration starts by waiting on three dependent loads.
-#ifdef SDMM_GROUP_NOPIPE   // (A/B: the chain fetched at the top of every iteration)
-    const bool piped = false;
-#else
     const bool piped = TREE && node_of != nullptr;
-#endif
     int64_t qa = 0, qb = 0, qc = 0;   // entries of iterations i + 1, i + 2 (and i + 3 in flight)
     int nb = 0;                       // node of iteration i + 1
     GuideMix mc{gp1, Kp1, K1};        // record of iteration i
@@ -1718,16 +1578,8 @@ static void launch_group_fallback(int kmax, int blocks, hipStream_t st, const fl
     else if (kmax <= 8 * G)
         hipLaunchKernelGGL((guide_group_fallback_kernel<PDF_ONLY, TREE, 8>), dim3(blocks), dim3(64), 0, st, gp, Kp,
                            K, nd, tb, io, gc, fb_count, fb_list, fb2, node_of);
-    else if constexpr (G < 16) {
-        if (kmax <= 16 * G)
-            hipLaunchKernelGGL((guide_group_fallback_kernel<PDF_ONLY, TREE, 16>), dim3(blocks), dim3(64), 0, st, gp,
-                               Kp, K, nd, tb, io, gc, fb_count, fb_list, fb2, node_of);
-        else
-            hipLaunchKernelGGL((guide_group_fallback_kernel<PDF_ONLY, TREE, 32>), dim3(blocks), dim3(64), 0, st, gp,
-                               Kp, K, nd, tb, io, gc, fb_count, fb_list, fb2, node_of);
-    }
 }
-static_assert(kGroupKMax <= 32 * kGroupLanes || kGroupLanes == 16, "group slots");
+static_assert(kGroupKMax <= 8 * kGroupLanes, "group slots");
 
 // ---------------------------------------------------------------------------
 // Product with a learned BSDF (the plugin's sampleProduct path,
@@ -1750,10 +1602,7 @@ static_assert(kGroupKMax <= 32 * kGroupLanes || kGroupLanes == 16, "group slots"
 // Linv 4, detInv) at base[(p * kPairFields + f) * stride + col] -- coalesced
 // across a wave's queries.  A query with more than cap pairs re-forms them.
 constexpr int kPairFields = 10;
-#ifndef SDMM_PAIR_CACHE
-#define SDMM_PAIR_CACHE 16
-#endif
-constexpr int kPairCacheCap = SDMM_PAIR_CACHE;
+constexpr int kPairCacheCap = 16;
 struct PairCacheDev {
     float* base;
     int64_t stride;
@@ -2320,7 +2169,6 @@ guide_product_cand_kernel(const float* __restrict__ gp, int Kp, int K, const flo
                           int64_t nq, GuideIO io, ProductIO pio, BsdfTab bt, GuideConsts gc, int cap,
                           int* __restrict__ fb_count, int32_t* __restrict__ fb_list,
                           const int32_t* __restrict__ perm) {
-    exp_tbl_init();
     __shared__ float cw[LCAP * 64];
     __shared__ unsigned short ck[LCAP * 64];
     const int tid = threadIdx.x;
@@ -2561,15 +2409,12 @@ __device__ void product_tail_wave(const float* gp, int Kp, const float* condCov,
 
 // The product path's full-K queries (listed by guide_product_cand_kernel):
 // one wave per query, grid-stride.
-#ifndef SDMM_PRODUCT_WPE
-#define SDMM_PRODUCT_WPE 3   // waves per SIMD the register budget is sized for (A/B: 2: 10.57, 3: 9.93, 4 (spills): 13.4 ms)
-#endif
+constexpr int kProductWpe = 3;   // waves per SIMD the register budget is sized for (A/B: 2: 10.57, 3: 9.93, 4 (spills): 13.4 ms)
 template <bool PDF_ONLY>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDMM_PRODUCT_WPE)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kProductWpe)))
 guide_product_wave_kernel(const float* __restrict__ gp, int Kp, int K, const float* __restrict__ condCov,
                           GuideIO io, ProductIO pio, BsdfTab bt, GuideConsts gc, float* __restrict__ pscratch,
                           int pcap, const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list) {
-    exp_tbl_init();
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x;
     const WaveLds L = wave_lds(lds, K, pscratch, pcap, bt.M);
@@ -2618,9 +2463,8 @@ guide_tree_product_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideM
                                const float* const* __restrict__ cctab, int64_t nq, GuideIO io, ProductIO pio,
                                BsdfTab bt, GuideConsts gc, int cap, int* __restrict__ fb_count,
                                int32_t* __restrict__ fb_list, const int32_t* __restrict__ perm,
-                               int32_t* __restrict__ node_out, NodeRoute rt, const uint32_t* __restrict__ skeys,
+                               int32_t* __restrict__ node_out, const uint32_t* __restrict__ skeys,
                                int mb) {
-    exp_tbl_init();
     __shared__ float cw[LCAP * 64];
     __shared__ unsigned short ck[LCAP * 64];
     const int tid = threadIdx.x;
@@ -2636,17 +2480,13 @@ guide_tree_product_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideM
     const int n0 = __builtin_amdgcn_readfirstlane(node);
     const bool uniform = __builtin_amdgcn_ballot_w64(node != n0) == 0;
     if (uniform) {
-        // uniform-leaf wave: the record in SGPRs (scalar record loads); with
-        // routing, routed to the full-K path or served here and counted
+        // uniform-leaf wave: the record in SGPRs (scalar record loads)
         const GuideMix mx = uniform_mix((n0 >= 0) ? tab[n0] : GuideMix{nullptr, 0, 0});
         if (mx.K <= 0) {
             product_invalid<PDF_ONLY>(io, pio, q);
-        } else if (rt.stats && rt.stats[3 * n0 + 2]) {
-            fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
         } else {
-            const bool fell = serve_product_cand<PDF_ONLY, LCAP>(mx.gp, mx.Kp, mx.K, cctab[n0], io, pio, bt, q, c, cw,
-                                                                 ck, tid, cap, gc, fb_count, fb_list, t);
-            if (rt.stats) route_count(rt, n0, fell);
+            serve_product_cand<PDF_ONLY, LCAP>(mx.gp, mx.Kp, mx.K, cctab[n0], io, pio, bt, q, c, cw, ck, tid, cap,
+                                               gc, fb_count, fb_list, t);
         }
         return;
     }
@@ -2666,13 +2506,12 @@ guide_tree_product_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideM
 // the tree product path's full-K queries, one wave per query (grid-stride);
 // kmax sizes the LDS
 template <bool PDF_ONLY>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDMM_PRODUCT_WPE)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kProductWpe)))
 guide_tree_product_wave_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __restrict__ tab,
                                const float* const* __restrict__ cctab, int kmax, GuideIO io, ProductIO pio,
                                BsdfTab bt, GuideConsts gc, float* __restrict__ pscratch, int pcap,
                                const int* __restrict__ fb_count, const int32_t* __restrict__ fb_list,
                                const int32_t* __restrict__ node_of) {
-    exp_tbl_init();
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x;
     const WaveLds L = wave_lds(lds, kmax, pscratch, pcap, bt.M);
@@ -2744,15 +2583,9 @@ __global__ void morton_keys_kernel(const float* __restrict__ c0, const float* __
     idx[q] = q;
 }
 
-// SDMM_MORTON_BITS (A/B): bits per axis of the coherent order's key
-static int morton_bits() {
-    static const int b = [] {
-        const char* e = std::getenv("SDMM_MORTON_BITS");
-        const int v = e ? std::atoi(e) : 10;
-        return v < 1 ? 1 : (v > 10 ? 10 : v);
-    }();
-    return b;
-}
+// bits per axis of the coherent order's key (round 4: 8 bits, one radix
+// pass fewer, measured the same)
+static int morton_bits() { return 10; }
 
 size_t guide_sort_temp_bytes(int n) {
     size_t bytes = 0;
@@ -2780,17 +2613,9 @@ static hipError_t coherent_order(const float* const c[3], int n, uint32_t* keys_
 // Morton runs cross leaf boxes, whose planes sit at sample means, wherever
 // the Z-curve does).  The sorted keys then carry every query's node: the
 // candidate kernel reads node = (key >> mb) - 1 instead of walking the tree.
-// A/B: total key bits of the leaf-major order (0: 32, the Morton code at
-// (32 - node bits) / 3 bits per axis) and, when set, which 30-bit Morton
-// levels fill the low bits
-#ifndef SDMM_LEAF_KEY_BITS
-#define SDMM_LEAF_KEY_BITS 0
-#endif
-#ifndef SDMM_LEAF_MORTON_SHIFT
-#define SDMM_LEAF_MORTON_SHIFT -1
-#endif
-constexpr int kLeafKeyBits = SDMM_LEAF_KEY_BITS;
-constexpr int kLeafMortonShift = SDMM_LEAF_MORTON_SHIFT;
+// The key is 32 bits: the Morton code at (32 - node bits) / 3 bits per axis
+// (round 4: 24 / 28-bit keys over the Morton levels that vary inside a leaf
+// measured within noise, K = 16 slower).
 __global__ void tree_keys_kernel(const STNodeDev* __restrict__ nodes, const float* __restrict__ c0,
                                  const float* __restrict__ c1, const float* __restrict__ c2, int n, int mb,
                                  uint32_t* __restrict__ keys, int32_t* __restrict__ idx) {
@@ -2798,16 +2623,8 @@ __global__ void tree_keys_kernel(const STNodeDev* __restrict__ nodes, const floa
     if (q >= n) return;
     const float x = c0[q], y = c1[q], z = c2[q];
     const int node = stree_find_point(nodes, x, y, z);
-    uint32_t m;
-    if (kLeafMortonShift >= 0) {
-        // mb bits of the 30-bit Morton code starting at kLeafMortonShift: the
-        // levels that vary inside a leaf (the top ones are constant there)
-        const uint32_t m30 = spread3(quantb(x, 10)) | (spread3(quantb(y, 10)) << 1) | (spread3(quantb(z, 10)) << 2);
-        m = (m30 >> (kLeafMortonShift >= 0 ? kLeafMortonShift : 0)) & ((1u << mb) - 1u);
-    } else {
-        const int b = mb / 3;
-        m = spread3(quantb(x, b)) | (spread3(quantb(y, b)) << 1) | (spread3(quantb(z, b)) << 2);
-    }
+    const int b = mb / 3;
+    const uint32_t m = spread3(quantb(x, b)) | (spread3(quantb(y, b)) << 1) | (spread3(quantb(z, b)) << 2);
     keys[q] = ((uint32_t)(node + 1) << mb) | m;
     idx[q] = q;
 }
@@ -2821,7 +2638,7 @@ static hipError_t leaf_order(const STNodeDev* nodes, int nn, const float* const 
                              uint32_t* keys_out, int32_t* idx_in, int32_t* idx_out, void* temp, size_t temp_bytes,
                              hipStream_t st, int* mb_out) {
     const int nb = leaf_key_bits(nn);
-    const int mb = kLeafKeyBits > nb ? kLeafKeyBits - nb : 32 - nb;
+    const int mb = 32 - nb;
     *mb_out = mb;
     hipLaunchKernelGGL(tree_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nodes, c[0], c[1], c[2],
                        n, mb, keys_in, idx_in);
@@ -2830,14 +2647,9 @@ static hipError_t leaf_order(const STNodeDev* nodes, int nn, const float* const 
     return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, idx_in, idx_out, n, 0, nb + mb,
                                               st);
 }
-// SDMM_LEAF_ORDER=0 (A/B): the tree wavefronts keep the plain Morton order
-static bool leaf_order_on() {
-    static const bool on = [] {
-        const char* e = std::getenv("SDMM_LEAF_ORDER");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
+// (round 4: the plain Morton order instead: K = 128 guided pass 11.95
+// against 11.37 ms, K = 512 product 88.6 against 85.6)
+static bool leaf_order_on() { return true; }
 
 static GuideIO make_io(const float* const c[3], const float* const u[3], const float* const dgiven[3],
                        float* const d[3], float* pdf, int32_t* comp, const uint8_t* pmode = nullptr) {
@@ -2884,20 +2696,19 @@ static hipError_t launch_cand(int cap, dim3 grid, hipStream_t st, const float* g
 template <bool PDF_ONLY>
 static hipError_t launch_tree_cand(int cap, dim3 grid, hipStream_t st, const STNodeDev* nd, const GuideMix* tb,
                                    int64_t nq, const GuideIO& io, GuideConsts gc, int* fb_count, int32_t* fb_list,
-                                   const int32_t* perm, int32_t* node_out, const NodeRoute& rt,
-                                   const uint32_t* skeys, int mb) {
+                                   const int32_t* perm, int32_t* node_out, const uint32_t* skeys, int mb) {
     if (cap <= 16)
         hipLaunchKernelGGL((guide_tree_cand_kernel<PDF_ONLY, 16>), grid, dim3(64), 0, st, nd, tb, nq, io, gc, cap,
-                           fb_count, fb_list, perm, node_out, rt, skeys, mb);
+                           fb_count, fb_list, perm, node_out, skeys, mb);
     else if (cap <= 24)
         hipLaunchKernelGGL((guide_tree_cand_kernel<PDF_ONLY, 24>), grid, dim3(64), 0, st, nd, tb, nq, io, gc, cap,
-                           fb_count, fb_list, perm, node_out, rt, skeys, mb);
+                           fb_count, fb_list, perm, node_out, skeys, mb);
     else if (cap <= 40)
         hipLaunchKernelGGL((guide_tree_cand_kernel<PDF_ONLY, 40>), grid, dim3(64), 0, st, nd, tb, nq, io, gc, cap,
-                           fb_count, fb_list, perm, node_out, rt, skeys, mb);
+                           fb_count, fb_list, perm, node_out, skeys, mb);
     else
         hipLaunchKernelGGL((guide_tree_cand_kernel<PDF_ONLY, kGuideCap>), grid, dim3(64), 0, st, nd, tb, nq, io,
-                           gc, cap, fb_count, fb_list, perm, node_out, rt, skeys, mb);
+                           gc, cap, fb_count, fb_list, perm, node_out, skeys, mb);
     return hipGetLastError();
 }
 
@@ -2964,8 +2775,7 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
                              const float* const u[3], const float* const dgiven[3], float* const d[3],
                              float* pdf, int32_t* comp, int32_t* node_out, float norm2, float norm3, int cap,
                              int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
-                             const GuideSortScratch* sort, const uint8_t* pmode, int* fb2, uint32_t* route,
-                             int nn) {
+                             const GuideSortScratch* sort, const uint8_t* pmode, int* fb2, int nn) {
     if (nq <= 0) return hipSuccess;
     cap = (cap < 0) ? 0 : (cap > kGuideCap ? kGuideCap : cap);
     if (nq > INT32_MAX) return hipErrorInvalidValue;
@@ -2999,19 +2809,16 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
     const GuideIO io = make_io(c, u, dgiven, d, pdf, comp, pmode);
     if (pmode) dgiven = nullptr;   // mixed: the sampling kernels, pdf queries per pmode
     cap = cap < kmax ? cap : kmax;
-    const NodeRoute rt{route, nn};
-    e = launch_route(rt, st);
-    if (e != hipSuccess) return e;
     // every query's node as the candidate kernel finds it (the caller's
     // node_out, else a sort buffer free once the order is built: the sorted
     // keys with the plain Morton order, the sort's index input with the
     // leaf-major one): the fallback kernels read it instead of walking the tree
     int32_t* const node_of = node_out ? node_out
                                       : (sort ? (skeys ? sort->idx[0] : (int32_t*)sort->keys[1]) : nullptr);
-    e = dgiven ? launch_tree_cand<true>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_of, rt,
-                                        skeys, mb)
-               : launch_tree_cand<false>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_of, rt,
-                                         skeys, mb);
+    e = dgiven ? launch_tree_cand<true>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_of, skeys,
+                                        mb)
+               : launch_tree_cand<false>(cap, grid, st, nd, tb, nq, io, gc, fb_count, fb_list, perm, node_of, skeys,
+                                         mb);
     if (e != hipSuccess) return e;
     if (fb2 && kmax <= kGroupKMax) {
         e = hipMemsetAsync(fb2, 0, sizeof(int), st);
@@ -3037,17 +2844,22 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
 }
 
 // The product launches' scratch in the handle's grow-only buffer: the thread
-// path's pair cache for `threads` query columns, then the wave kernel's pair
-// slices (fblocks workgroups).  Regrowth frees the old buffer in stream order
-// (every earlier use is on the same stream) and allocates the larger one; an
-// allocation failure is an error (no silent uncached path).
+// path's pair cache for `threads` query columns (640 B per column), then the
+// wave kernel's pair slices (fblocks workgroups, mandatory).  Regrowth frees
+// the old buffer in stream order (every earlier use is on the same stream)
+// and allocates the larger one.  The cache is optional: when the buffer with
+// it cannot be allocated, the slices alone are, and the thread path
+// recomputes its pairs (the same values; pc->base = null), so a wavefront too
+// large for a cache still runs.  sdmm_destroy (or the tree's destruction)
+// releases the buffer.
 static hipError_t product_scratch(ProductScratch* ps, int64_t threads, unsigned fblocks, hipStream_t st,
                                   PairCacheDev* pc, float** pairs) {
+    if (!ps) return hipErrorInvalidValue;
     const size_t cb = kPairCacheCap > 0 ? sizeof(float) * kPairFields * (size_t)kPairCacheCap * (size_t)threads : 0;
     const size_t ca = (cb + 255) / 256 * 256;
-    const size_t need = ca + sizeof(float) * kPcStride * (size_t)kProductPairCap * fblocks;
-    if (!ps) return hipErrorInvalidValue;
-    if (ps->bytes < need) {
+    const size_t slices = sizeof(float) * kPcStride * (size_t)kProductPairCap * fblocks;
+    auto grow = [&](size_t need) -> hipError_t {
+        if (ps->bytes >= need) return hipSuccess;
         if (ps->base) {
             const hipError_t f = hipFreeAsync(ps->base, st);
             if (f != hipSuccess) return f;
@@ -3055,12 +2867,30 @@ static hipError_t product_scratch(ProductScratch* ps, int64_t threads, unsigned 
         ps->base = nullptr;
         ps->bytes = 0;
         const size_t grown = need + need / 4;
-        const hipError_t e = hipMallocAsync((void**)&ps->base, grown, st);
-        if (e != hipSuccess) return e;
+        hipError_t e = hipMallocAsync((void**)&ps->base, grown, st);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();   // clear the sticky allocation error; try the exact size
+            e = hipMallocAsync((void**)&ps->base, need, st);
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                ps->base = nullptr;
+                return e;
+            }
+            ps->bytes = need;
+            return hipSuccess;
+        }
         ps->bytes = grown;
+        return hipSuccess;
+    };
+    if (ca > 0 && grow(ca + slices) == hipSuccess) {
+        *pc = PairCacheDev{ps->base, threads, kPairCacheCap};
+        *pairs = (float*)((char*)ps->base + ca);
+        return hipSuccess;
     }
-    *pc = PairCacheDev{kPairCacheCap > 0 ? ps->base : nullptr, threads, kPairCacheCap};
-    *pairs = (float*)((char*)ps->base + ca);
+    const hipError_t e = grow(slices);   // no room for the cache: the slices alone
+    if (e != hipSuccess) return e;
+    *pc = PairCacheDev{nullptr, threads, kPairCacheCap};
+    *pairs = ps->base;
     return hipSuccess;
 }
 
@@ -3098,7 +2928,7 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
     const dim3 grid((unsigned)((nq + 63) / 64));
     // the full-K queries' product pairs (up to kProductPairCap per query): one
     // scratch slice per workgroup of the wave kernel
-    const unsigned fblocks = (unsigned)(cus * 4 * SDMM_PRODUCT_WPE);
+    const unsigned fblocks = (unsigned)(cus * 4 * kProductWpe);
     float* pscratch = nullptr;
     e = product_scratch(scratch, (int64_t)grid.x * 64, fblocks, st, &pio.cache, &pscratch);
     if (e != hipSuccess) return e;
@@ -3139,8 +2969,7 @@ hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const v
                                      float* h, const float* bw, const float* bmean, const float* bcov,
                                      const uint8_t* diffuse, int B, int M, float norm2, float norm3, int cap,
                                      int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
-                                     const GuideSortScratch* sort, ProductScratch* scratch, uint32_t* route,
-                                     int nn) {
+                                     const GuideSortScratch* sort, ProductScratch* scratch, int nn) {
     if (nq <= 0) return hipSuccess;
     if (nq > INT32_MAX) return hipErrorInvalidValue;
     if (kmax < 1) kmax = 1;
@@ -3188,19 +3017,16 @@ hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const v
     const GuideMix* tb = (const GuideMix*)tab;
     const float* const* cc = (const float* const*)cctab;
     const dim3 grid((unsigned)((nq + 63) / 64));
-    const unsigned fblocks = (unsigned)(cus * 4 * SDMM_PRODUCT_WPE);
+    const unsigned fblocks = (unsigned)(cus * 4 * kProductWpe);
     float* pscratch = nullptr;
     e = product_scratch(scratch, (int64_t)grid.x * 64, fblocks, st, &pio.cache, &pscratch);
-    if (e != hipSuccess) return e;
-    const NodeRoute rt{route, nn};
-    e = launch_route(rt, st);
     if (e != hipSuccess) return e;
     // every query's node from the candidate kernel (see launch_guide_tree)
     int32_t* const node_of = node_out ? node_out
                                       : (sort ? (skeys ? sort->idx[0] : (int32_t*)sort->keys[1]) : nullptr);
 #define SDMM_TREE_PRODUCT_CAND(P, L)                                                                         \
     hipLaunchKernelGGL((guide_tree_product_cand_kernel<P, L>), grid, dim3(64), 0, st, nd, tb, cc, nq, iox, pio, \
-                       bt, gc, cap, fb_count, fb_list, perm, node_of, rt, skeys, mb)
+                       bt, gc, cap, fb_count, fb_list, perm, node_of, skeys, mb)
     if (pdf_only) {
         if (cap <= 16) SDMM_TREE_PRODUCT_CAND(true, 16);
         else if (cap <= 24) SDMM_TREE_PRODUCT_CAND(true, 24);
@@ -3230,21 +3056,6 @@ hipError_t launch_sample_cdf(const float* cdf, int n, const float* u, int64_t nq
     hipLaunchKernelGGL(sample_cdf_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, cdf, n, u,
                        nq, out);
     return hipGetLastError();
-}
-
-hipError_t launch_norm_exp_test(const float* q, int64_t n, float norm, float* out, int32_t* fast, hipStream_t st) {
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(norm_exp_test_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, q, n, norm, out, fast);
-    return hipGetLastError();
-}
-void norm_exp_test_host(const float* q, int64_t n, float norm, float* out, int32_t* fast) {
-    static const double tbl[64] = {SDMM_EXP2J_TABLE};
-    for (int64_t i = 0; i < n; ++i) {
-        int ok;
-        const float f = norm_exp_try(norm, q[i], tbl, &ok);
-        out[i] = ok ? f : norm_exp_ref(norm, q[i]);
-        if (fast) fast[i] = ok;
-    }
 }
 
 }  // namespace sdmm

@@ -474,77 +474,7 @@ __device__ __forceinline__ void mstep_component(int k, int K, const double* __re
     for (int i = 0; i < 25; ++i) S.sgC[25 * k + i] = gC[i];
 }
 
-// Wave 0: the fp64 weight normalisation, the float weights and createCdf
-// (weights_cdf's float operations, in its order) with every sequential sum a
-// chain of v_readlane broadcasts and adds over registers -- lane l holds
-// components l, l + 64, ... -- and each prefix captured by the lane that owns
-// the element.  (Thread 0 alone walking C.weights / C.cdf in global memory,
-// which may alias, waited a round trip per element: a K = 128 M-step took
-// 73 us, 40 us once these loops ran on LDS; the rest is the per-component
-// fp64 work of mstep_component.)  Results in wl / cl (LDS); the caller copies
-// them out in parallel.  K <= 512.
-__device__ __forceinline__ double rl_f64(double x, int l) {
-    const uint64_t u = __builtin_bit_cast(uint64_t, x);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
-    return __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
-}
-__device__ __forceinline__ float rl_f32(float x, int l) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
-}
-__device__ __forceinline__ void mstep_finish_wave(int K, const EmStateDev& S, const double* newW, float* wl,
-                                                  float* cl, int lane) {
-    constexpr int SL = 8;   // 512 / 64
-    double nw[SL];
-    float w[SL], cdf[SL];
-#pragma unroll
-    for (int i = 0; i < SL; ++i) nw[i] = (64 * i + lane < K) ? newW[64 * i + lane] : 0.0;
-    double sum = 0.0;
-#pragma unroll
-    for (int i = 0; i < SL; ++i)
-        if (64 * i < K)
-            for (int l = 0; l < 64 && 64 * i + l < K; ++l) sum += rl_f64(nw[i], l);
-    if (sum != 0.0)
-#pragma unroll
-        for (int i = 0; i < SL; ++i) nw[i] = nw[i] / sum;
-#pragma unroll
-    for (int i = 0; i < SL; ++i) { w[i] = (float)nw[i]; cdf[i] = 0.0f; }
-    // createCdf(false): the unnormalised prefix (kept if the sum below is 0)
-    float acc = 0.0f;
-#pragma unroll
-    for (int i = 0; i < SL; ++i)
-        if (64 * i < K)
-            for (int l = 0; l < 64 && 64 * i + l < K; ++l) {
-                acc += rl_f32(w[i], l);
-                cdf[i] = (lane == l) ? acc : cdf[i];
-            }
-    float fs = 0.0f;
-#pragma unroll
-    for (int i = 0; i < SL; ++i)
-        if (64 * i < K)
-            for (int l = 0; l < 64 && 64 * i + l < K; ++l) fs += rl_f32(w[i], l);
-    if (fs != 0.0f) {
-#pragma unroll
-        for (int i = 0; i < SL; ++i) w[i] = w[i] / fs;
-        acc = 0.0f;
-#pragma unroll
-        for (int i = 0; i < SL; ++i)
-            if (64 * i < K)
-                for (int l = 0; l < 64 && 64 * i + l < K; ++l) {
-                    acc += rl_f32(w[i], l);
-                    cdf[i] = (lane == l) ? acc : cdf[i];
-                }
-    }
-#pragma unroll
-    for (int i = 0; i < SL; ++i)
-        if (64 * i + lane < K) {
-            wl[64 * i + lane] = w[i];
-            cl[64 * i + lane] = cdf[i];
-        }
-    if (lane == 0) S.scalars[SC_IT] = S.scalars[SC_IT] + 1.0;
-}
-
-// The same results as mstep_finish_wave from the whole workgroup: the three
+// The finish from the whole workgroup: the three
 // order-dependent sums (the fp64 total of newW, the float prefix of the
 // weights -- whose last value is also their float total --, the float prefix
 // of the normalised weights) are each ONE thread's sequential chain over LDS
@@ -635,11 +565,7 @@ __device__ __forceinline__ void mstep_body(int K, int Kp, const double* __restri
     // dynamic LDS: newW (8K bytes), setk (4K) -- reused as wl --, cl (4K)
     float* wl = (float*)setk;
     float* cl = wl + K;
-#ifdef SDMM_MSTEP_FINISH_WAVE
-    if (t < 64) mstep_finish_wave(K, S, newW, wl, cl, t);
-#else
     mstep_finish_block(K, S, newW, wl, cl, sh2);
-#endif
     __syncthreads();
     if (SDMM_MSTEP_STOP <= 4) return;
     for (int k = t; k < K; k += blockDim.x) {

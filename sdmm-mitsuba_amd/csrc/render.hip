@@ -121,7 +121,11 @@ __device__ __forceinline__ float fresnel_dielectric(float cos_i, float eta) {
 
 // SmoothPlastic's specular sampling probability (plastic.cpp:339-342)
 __device__ __forceinline__ float plastic_prob_specular(float Fi, float ssw) {
-    return (Fi * ssw) / (Fi * ssw + (1.0f - Fi) * (1.0f - ssw));
+    // 0 / 0 (no specular weight at a total reflection, or weight 1 with Fi =
+    // 0) is 0 here, NaN in plastic.cpp:339-342: both lobes then carry no
+    // energy along that direction, and a NaN would only poison the sample
+    const float num = Fi * ssw, den = num + (1.0f - Fi) * (1.0f - ssw);
+    return den == 0.0f ? 0.0f : num / den;
 }
 
 __device__ __forceinline__ float& vrec(const PathsDev& P, int f, int v, int64_t p) {
@@ -343,7 +347,7 @@ li_shade_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, i
                 // (bsdfWeight * bsdfPdf) / pdfSurface (:407, :531-534, :587-589)
                 const float bsdf_pdf = Q.bpdf[i];
                 mis_pdf = bsdf_pdf > 0.0f ? h * bsdf_pdf + (1.0f - h) * Q.pdf[j] : 0.0f;
-                for (int ch = 0; ch < 3; ++ch) weight[ch] = mis_pdf == 0.0f ? 0.0f : (bw[ch] * bsdf_pdf) / mis_pdf;
+                for (int ch = 0; ch < 3; ++ch) weight[ch] = mis_pdf == 0.0f ? 0.0f : (bw[ch] * bsdf_pdf) * (1.0f / mis_pdf);
             }
         } else {
             // the guide's direction: bsdf->eval (smooth lobe, ESolidAngle) / pdfSurface (:456-507)
@@ -359,7 +363,7 @@ li_shade_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, i
             const float k = cpdf * bp[5] * (1.0f - Fi) * (1.0f - Fo);
             for (int ch = 0; ch < 3; ++ch) {
                 const float f = up ? S.refl[3 * QD.bsdf + ch] * rd * k : 0.0f;
-                weight[ch] = mis_pdf == 0.0f ? 0.0f : f / mis_pdf;
+                weight[ch] = mis_pdf == 0.0f ? 0.0f : f * (1.0f / mis_pdf);
             }
         }
     } else if (!valid) {
@@ -373,7 +377,7 @@ li_shade_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, i
         wo[0] = Q.b0[i]; wo[1] = Q.b1[i]; wo[2] = Q.b2[i];
         const float bsdf_pdf = kInvPi * dot3(wo, n);
         mis_pdf = bsdf_pdf > 0.0f ? h * bsdf_pdf + (1.0f - h) * Q.pdf[j] : 0.0f;   // pdfSurface (:531-534)
-        for (int ch = 0; ch < 3; ++ch) weight[ch] = mis_pdf == 0.0f ? 0.0f : (rho[ch] * bsdf_pdf) / mis_pdf;
+        for (int ch = 0; ch < 3; ++ch) weight[ch] = mis_pdf == 0.0f ? 0.0f : (rho[ch] * bsdf_pdf) * (1.0f / mis_pdf);
     } else {
         // guide sample: bsdf->eval / pdf (:456-463, :504-507)
         wo[0] = Q.d0[j]; wo[1] = Q.d1[j]; wo[2] = Q.d2[j];
@@ -381,7 +385,7 @@ li_shade_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, i
         const bool zero = (wo[0] == 0.0f && wo[1] == 0.0f && wo[2] == 0.0f) || !__builtin_isfinite(cos_o);
         const float bsdf_pdf = (!zero && cos_o > 0.0f) ? kInvPi * cos_o : 0.0f;
         mis_pdf = bsdf_pdf > 0.0f ? h * bsdf_pdf + (1.0f - h) * Q.pdf[j] : 0.0f;   // pdfSurface (:531-534)
-        for (int ch = 0; ch < 3; ++ch) weight[ch] = mis_pdf == 0.0f ? 0.0f : (rho[ch] * (kInvPi * cos_o)) / mis_pdf;
+        for (int ch = 0; ch < 3; ++ch) weight[ch] = mis_pdf == 0.0f ? 0.0f : (rho[ch] * (kInvPi * cos_o)) * (1.0f / mis_pdf);
     }
     const float cos_o = dot3(wo, n);
     // zero weight, or strict normals (wo . n_geo * cos(wo) <= 0, :777-780): the path ends

@@ -155,7 +155,7 @@ int sdmm_scene_create(const sdmm_scene_desc* d, int device, sdmm_scene** out) {
             const float* bp = d->bsdf_params + kBsdfParams * b;
             const bool ok = bp[0] == (float)kBsdfDiffuse ||
                             (bp[0] == (float)kBsdfPlastic && bp[4] > 0.0f && bp[5] > 0.0f && bp[6] < 1.0f &&
-                             bp[7] >= 0.0f && bp[7] < 1.0f);
+                             bp[7] >= 0.0f && bp[7] <= 1.0f);
             if (!ok) return fail(SDMM_E_INVALID, "sdmm_scene_create: invalid bsdf_params");
         }
     *out = nullptr;

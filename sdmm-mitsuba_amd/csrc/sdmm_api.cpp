@@ -89,8 +89,6 @@ hipError_t launch_stree_route(const void* nodes, int num_nodes, int key_bits, co
                               uint32_t* keys0, uint32_t* keys1, int32_t* idx0, int32_t* idx1, void* temp,
                               size_t temp_bytes, int64_t* seg_dev, float* const out_x[6], float* out_w,
                               float* out_h, uint8_t* out_d, hipStream_t st);
-hipError_t launch_norm_exp_test(const float* q, int64_t n, float norm, float* out, int32_t* fast, hipStream_t st);
-void norm_exp_test_host(const float* q, int64_t n, float norm, float* out, int32_t* fast);
 hipError_t launch_guide(const float* gp, int Kp, int K, int64_t nq, const float* const c[3],
                         const float* const u[3], const float* const dgiven[3], float* const d[3], float* pdf,
                         int32_t* comp, float norm2, float norm3, int cap, int* fb_count, int32_t* fb_list,
@@ -100,7 +98,7 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
                              float* pdf, int32_t* comp, int32_t* node_out, float norm2, float norm3, int cap,
                              int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
                              const GuideSortScratch* sort, const uint8_t* pmode = nullptr, int* fb2 = nullptr,
-                             uint32_t* route = nullptr, int nn = 0);
+                             int nn = 0);
 hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* condCov, int64_t nq,
                                 const float* const c[3], const float* const u[3], const float* const dgiven[3],
                                 float* const d[3], float* pdf, int32_t* comp, const int32_t* material,
@@ -115,8 +113,7 @@ hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const v
                                      float* h, const float* bw, const float* bmean, const float* bcov,
                                      const uint8_t* diffuse, int B, int M, float norm2, float norm3, int cap,
                                      int* fb_count, int32_t* fb_list, int cus, hipStream_t st,
-                                     const GuideSortScratch* sort, ProductScratch* scratch, uint32_t* route = nullptr,
-                                     int nn = 0);
+                                     const GuideSortScratch* sort, ProductScratch* scratch, int nn = 0);
 #ifndef SDMM_GUIDE_CAP_MAX
 #define SDMM_GUIDE_CAP_MAX 64
 #endif
@@ -324,10 +321,10 @@ struct sdmm_mix {
     int rtile = 0;                           // 1: estep_resp_tile_kernel (64 < K <= 128)
                                              // 2: estep_resp_mfma_kernel (every K)
                                              // 3: estep_resp_split_kernel (bf16x3 MFMA forms, Kp <= 128)
-    int rvariant = 4;                        // tile kernel variant (SDMM_RESP_VARIANT): KT=8, 3 waves/SIMD
+    int rvariant = 4;                        // tile / mfma kernel variant: KT=8, 3 waves/SIMD
     int stile = 0;                           // 1: estep_stats_tile_kernel (64 < K <= 128)
                                              // 2: its GROUP form (128 < K <= 512: Kp / 128 waves per chunk)
-    int svariant = 0;                        // its occupancy variant (SDMM_STATS_VARIANT)
+    int svariant = 0;                        // its occupancy variant
     int device = 0;
     int cus = 256;
     int resp_blocks = 2, stats_blocks = 2;   // resident 256-thread WGs per CU
@@ -608,18 +605,6 @@ extern "C" {
 const char* sdmm_last_error(void) { return g_err.c_str(); }
 int sdmm_abi_version(void) { return SDMM_ABI_VERSION; }
 
-int sdmm_test_norm_exp(const float* q, int64_t n, float norm, int on_device, int device, float* out, int32_t* fast) {
-    if (n < 0 || (n > 0 && (!q || !out)) || !(norm > 0.0f)) return fail(SDMM_E_INVALID, "invalid argument");
-    if (!on_device) {
-        norm_exp_test_host(q, n, norm, out, fast);
-        return SDMM_OK;
-    }
-    HIP_TRY(hipSetDevice(device));
-    HIP_TRY(launch_norm_exp_test(q, n, norm, out, fast, nullptr));
-    HIP_TRY(hipDeviceSynchronize());
-    return SDMM_OK;
-}
-
 void sdmm_em_params_default(sdmm_em_params* p) {
     if (!p) return;
     p->alpha = 0.9f;
@@ -767,14 +752,10 @@ int create_impl(int K, const sdmm_em_params* params, int device, hipStream_t ord
         }
         if (mfma) m->rtile = 2;
         if (split && estep_resp_split_supported(m->Kp)) m->rtile = 3;
-        const char* vv = std::getenv("SDMM_RESP_VARIANT");
-        if (vv) m->rvariant = std::atoi(vv);
-        if (m->rtile == 3) m->rvariant = vv ? std::atoi(vv) : 0;
-        const char* sv = std::getenv("SDMM_STATS_KERNEL");
-        if (K > 64 && K <= 128 && !(sv && std::strcmp(sv, "legacy") == 0)) m->stile = 1;
-        if (K > 128 && K <= 512 && !(sv && std::strcmp(sv, "legacy") == 0)) m->stile = 2;
-        const char* svv = std::getenv("SDMM_STATS_VARIANT");
-        if (svv) m->svariant = std::atoi(svv);
+        // statistics: the tile kernel for 64 < K <= 128, its GROUP form for
+        // 128 < K <= 512 (estep.hip), estep_stats_kernel otherwise
+        if (K > 64 && K <= 128) m->stile = 1;
+        if (K > 128 && K <= 512) m->stile = 2;
     }
     static thread_local OccCache occ[8];
     OccCache& oc = occ[(K * 7 + device) & 7];
@@ -2154,8 +2135,6 @@ struct sdmm_stree {
     size_t dtab_cap = 0;
     int tab_kmax = 0;
     int tab_cap = kGuideCapDefault; // candidate capacity: the smallest of the bound mixtures' (sdmm_set_guide_capacity)
-    uint32_t* droute = nullptr;     // [3 nn] per-node routing counts of the wavefronts (guide.hip NodeRoute)
-    size_t droute_cap = 0;          // entries allocated
     bool tab_valid = false;     // bound table matches the current nodes
     int* guide_fb = nullptr;
     int64_t guide_fb_cap = 0;
@@ -2446,7 +2425,6 @@ void sdmm_stree_destroy(sdmm_stree* t) {
     if (t->dnodes) (void)hipFree(t->dnodes);
     if (t->scratch) (void)hipFree(t->scratch);
     if (t->dtab) (void)hipFree(t->dtab);
-    if (t->droute) (void)hipFree(t->droute);
     if (t->split_mem) (void)hipFree(t->split_mem);
     if (t->split_small) (void)hipFree(t->split_small);
     if (t->guide_fb) (void)hipFree(t->guide_fb);
@@ -2999,15 +2977,6 @@ int st_upload_table(sdmm_stree* t, const sdmm_mix* const* node_mix) {
     t->tab_cap = cap;
     t->tab_valid = true;
     if (same && t->dtab) return SDMM_OK;
-    // a different table: the routing counts start again (grow-only buffer)
-    if (3 * nn > t->droute_cap) {
-        release_dev(t->droute);
-        t->droute = nullptr;
-        t->droute_cap = 0;
-        HIP_TRY(hipMalloc(&t->droute, sizeof(uint32_t) * 3 * nn));
-        t->droute_cap = 3 * nn;
-    }
-    if (nn) HIP_TRY(hipMemsetAsync(t->droute, 0, sizeof(uint32_t) * 3 * nn, t->stream));
     HIP_TRY(hipStreamSynchronize(t->stream));   // the previous copy may still read tab_host
     const size_t nb = nn ? nn : 1;
     const size_t bytes = (sizeof(GuideMixHost) + sizeof(const float*)) * nb;
@@ -3052,38 +3021,12 @@ int st_prepare(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, int* 
     return SDMM_OK;
 }
 
-// smallest tree wavefront served in Morton order (SDMM_TREE_ORDER_MIN, A/B):
-// below it the batch is served as given -- the sort's ~10 launches cost more
-// than the coherence they buy on a small batch
-int64_t tree_order_min() {
-    static const int64_t v = [] {
-        const char* e = std::getenv("SDMM_TREE_ORDER_MIN");
-        return e ? (int64_t)std::atoll(e) : (int64_t)(1 << 14);
-    }();
-    return v;
-}
-
-// SDMM_TREE_ORDER=0 (A/B): the tree wavefronts serve queries in the given
-// order (no Morton sort of the batch)
-bool tree_order_on() {
-    static const bool on = [] {
-        const char* e = std::getenv("SDMM_TREE_ORDER");
-        return !(e && std::strcmp(e, "0") == 0);
-    }();
-    return on;
-}
-
-// SDMM_GUIDE_ROUTE=1 (A/B, off by default): per-node routing of the
-// wavefronts (guide.hip NodeRoute).  Measured round 4 on the Cornell K=128 and
-// K=512 product lines: no gain -- the fallback queries are spread over the
-// leaves (hardly any node passes the two-thirds threshold).
-uint32_t* route_stats(sdmm_stree* t) {
-    static const bool on = [] {
-        const char* e = std::getenv("SDMM_GUIDE_ROUTE");
-        return e && std::strcmp(e, "1") == 0;
-    }();
-    return (on && t->droute && t->droute_cap >= 3 * t->nodes.size()) ? t->droute : nullptr;
-}
+// smallest tree wavefront served in coherent order: below it the batch is
+// served as given -- the sort's ~10 launches cost more than the coherence
+// they buy on a small batch (round 4: a minimum of 64 K / 256 K or no sort at
+// all measured 11.9 / 13.6 / 20.5 ms per Cornell K = 128 guided pass against
+// 11.4 ms at 16 K)
+constexpr int64_t kTreeOrderMin = 1 << 14;
 
 int st_guide(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
              const float* const u[3], const float* const dgiven[3], float* const d[3], float* pdf, int32_t* comp,
@@ -3091,13 +3034,13 @@ int st_guide(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const f
     int cus = 256;
     const int r = st_prepare(t, node_mix, nq, &cus);
     if (r) return r;
-    const GuideSortScratch* sort = (nq >= tree_order_min() && tree_order_on()) ? &t->guide_sort : nullptr;
+    const GuideSortScratch* sort = (nq >= kTreeOrderMin) ? &t->guide_sort : nullptr;
     HIP_TRY(launch_guide_tree(t->dnodes, t->dtab, t->tab_kmax, nq, c, u, dgiven, d, pdf, comp, node_out,
                               norm_const(2), norm_const(3), t->tab_cap, t->guide_fb, t->guide_fb + 1,
                               cus, t->stream, sort, pmode,
                               // the NaN hand-off list of the group fallback: the
                               // Morton keys' input buffer, free once the order is built
-                              (int*)t->guide_sort.keys[0], route_stats(t), (int)t->nodes.size()));
+                              (int*)t->guide_sort.keys[0], (int)t->nodes.size()));
     return SDMM_OK;
 }
 
@@ -3108,12 +3051,12 @@ int st_guide_product(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq,
     int cus = 256;
     const int r = st_prepare(t, node_mix, nq, &cus);
     if (r) return r;
-    const GuideSortScratch* sort = (nq >= tree_order_min() && tree_order_on()) ? &t->guide_sort : nullptr;
+    const GuideSortScratch* sort = (nq >= kTreeOrderMin) ? &t->guide_sort : nullptr;
     HIP_TRY(launch_guide_product_tree(t->dnodes, t->dtab, t->dcctab, t->tab_kmax, nq, c, u, choice, dgiven, d, pdf,
                                       comp, node_out, material, frame, heuristic, bsdf->weights, bsdf->means,
                                       bsdf->covs, bsdf->diffuse, bsdf->B, bsdf->M, norm_const(2), norm_const(3),
                                       t->tab_cap, t->guide_fb, t->guide_fb + 1, cus, t->stream, sort,
-                                      &t->product_scratch, route_stats(t), (int)t->nodes.size()));
+                                      &t->product_scratch, (int)t->nodes.size()));
     return SDMM_OK;
 }
 

@@ -113,6 +113,31 @@ def test_product_li_matches_oracle(pkg, oracle, scenes, gpu, plog):
 PLASTIC = ("TallBox", "ShortBox", "Floor")
 
 
+def test_black_base_plastic_unguided_bitwise(pkg, oracle, scenes, gpu, plog):
+    """A smooth plastic with a black diffuse base (specular sampling weight
+    exactly 1: sdmm_scene_create accepts the closed end of [0, 1]) on the
+    floor: the device Li equals the CPU Li bit for bit, unguided."""
+    desc = scenes.cornell_box(128, 72, plastic=("Floor",))
+    names = list(scenes._BSDFS)
+    f = names.index("Floor")
+    bp = desc["bsdf_params"].reshape(-1, 8).copy()
+    bp[f] = scenes.plastic_params((0.0, 0.0, 0.0))
+    assert bp[f, 7] == 1.0
+    desc["bsdf_params"] = bp.reshape(-1)
+    refl = desc["reflectance"].reshape(-1, 3).copy()
+    refl[f] = 0.0
+    desc["reflectance"] = refl.reshape(-1)
+    sc = pkg.Scene(desc)
+    tree = _tree(pkg, sc)
+    img, rec, nv, _ = _device(sc, tree, None, False)
+    aabb, child, _ = tree.nodes()
+    r = oracle.li_render(desc, aabb, child, spp=SPP, seed=SEED, threads=8)
+    np.testing.assert_array_equal(nv, r["nv"])
+    sel = np.arange(rec.shape[1])[:, None] < nv[None, :]
+    np.testing.assert_array_equal(rec[:, sel], r["rec"][:, sel])
+    np.testing.assert_array_equal(img, r["image"])
+
+
 def test_plastic_li_matches_oracle(pkg, oracle, scenes, gpu, plog):
     """A delta + smooth BSDF (smooth plastic on the boxes and the floor, the
     Kitchen's `plastic`) through the device Li and the CPU Li: unguided

@@ -365,13 +365,17 @@ def test_rare_angle_cases(pkg, oracle, synth, gpu, plog, K):
                                       ("legacy", 128)])
 def test_rare_angle_every_lane_slot(pkg, oracle, synth, gpu, plog, monkeypatch, kernel, K):
     """The reference's far-side quirk (mvtn.h:157-164: sin < 1e-3 with cos < 0
-    gives J = 1, so a direction 4e-4..9e-4 rad from ANTIPODAL to component k's
-    mean direction, at k's spatial mean, is explained by k) for every
-    component k, i.e. at every (lane, slot) position of the kernels' pair
-    layouts, on an unfitted mixture (wide directional covariances, so the
-    quirk changes the posteriors by O(1)), with no NaN row to force the tile
-    redo.  Regression: a bit cast of a vector element read element 0 only
-    (sdmm_device.h fbits), so the rare-angle detector saw one slot in four."""
+    gives J = 1): a direction 7.5e-4..8.5e-4 rad from ANTIPODAL to component
+    k's mean direction, at k's spatial mean, is explained by k.  In that band
+    the float and double evaluations agree on the quirk (cos stays >= 3 float
+    ulps above -1 after the inputs' rounding, so no fp32 path lands on the
+    failed log map at cos = -1; sin stays below 1e-3).  Every targeted k is
+    3 mod 4, i.e. never slot 0 of a lane's components (split: 16 r + 4 g + j,
+    tile: the odd one of a pair, mfma: C[j]), and no NaN row forces the tile
+    redo, so only a detector that sees every slot takes the quirk path.  An
+    unfitted mixture (wide directional covariances: the quirk changes the
+    posteriors by O(1)).  Regression: a bit cast of a vector element read
+    element 0 only (sdmm_device.h fbits), so the detector saw one slot in four."""
     import torch
     monkeypatch.setenv("SDMM_RESP_KERNEL", kernel)
     N = 8 * K
@@ -380,12 +384,13 @@ def test_rare_angle_every_lane_slot(pkg, oracle, synth, gpu, plog, monkeypatch, 
     mu = p["mean"].astype(np.float64)
     x = b["x"].copy()
     rng = np.random.default_rng(11)
+    tgt_k = 4 * (np.arange(N) % (K // 4)) + 3
     for i in range(N):
-        k = i % K
+        k = tgt_k[i]
         n = mu[k, 3:6] / np.linalg.norm(mu[k, 3:6])
         t = np.cross(n, [0.0, 0.0, 1.0] if abs(n[2]) < 0.9 else [1.0, 0.0, 0.0])
         t /= np.linalg.norm(t)
-        dl = rng.uniform(4e-4, 9e-4)
+        dl = rng.uniform(7.5e-4, 8.5e-4)
         x[0:3, i] = mu[k, 0:3].astype(np.float32)
         x[3:6, i] = (-np.cos(dl) * n + np.sin(dl) * t).astype(np.float32)
     xt = [torch.from_numpy(x[i].copy()).to(gpu) for i in range(6)]
@@ -395,12 +400,15 @@ def test_rare_angle_every_lane_slot(pkg, oracle, synth, gpu, plog, monkeypatch, 
     ref = oracle.responsibilities(om, oracle.Samples(x, b["w"]))
     exact = posterior_f64(p, x)
     # the quirk matters: the targeted component holds a large share
-    tgt = exact[np.arange(N), np.arange(N) % K]
-    assert np.median(tgt) > 0.05
-    err = np.abs(got[np.arange(N), np.arange(N) % K] - tgt).max()
+    rows = np.arange(N)
+    assert np.median(exact[rows, tgt_k]) > 0.05
+    err = np.abs(got[rows, tgt_k] - exact[rows, tgt_k]).max()
     plog(f"rare_slot_{kernel}_{K}_target_err", err, 2e-5)
     assert err <= 2e-5, err
-    _check_resp(got, ref, p, x, plog, min_frac=0.3)
+    eg = np.abs(got - exact).max()
+    eo = np.abs(ref - exact).max()
+    plog(f"rare_slot_{kernel}_{K}_err", eg, 4 * eo + 1e-5, oracle_fp32_err=eo)
+    assert eg <= 4 * eo + 1e-5, (eg, eo)
 
 
 def _em_model(pkg, oracle, synth, K, N, iters):

@@ -96,15 +96,17 @@ def _plastic_albedo(cos_i, bp, rho):
     return fi * float(bp[1]) + (1 - fi) * inv_eta2 * rho / (1 - fdr_int) * (1 - fdr_ext)
 
 
-def test_plastic_albedo_known_answer(oracle, scenes):
+@pytest.mark.parametrize("rho", [0.6, 0.0])
+def test_plastic_albedo_known_answer(oracle, scenes, rho):
     """The plastic bounce (delta specular lobe + Fresnel-weighted diffuse
     base) against its closed-form directional albedo: a box whose far face is
     plastic and whose other faces are black emitters (Le = 1); with one
     scatter (maxDepth 2) a pixel's expected radiance is the albedo at its
     camera ray's incidence angle -- both lobes are exercised (the delta lobe
-    saves no vertex, the diffuse one does)."""
+    saves no vertex, the diffuse one does).  rho = 0: a black base, whose
+    specular sampling weight sAvg / (0 + sAvg) is exactly 1 -- only the delta
+    lobe is ever sampled and the albedo is Fi."""
     d = _furnace(0.0, 1.0, w=24, h=16)
-    rho = 0.6
     bp = scenes.plastic_params((rho, rho, rho))
     far = 5                                           # axis 2, sgn +1: the face the camera looks at
     d["bsdf"] = np.zeros(6, np.int32)
@@ -133,4 +135,7 @@ def test_plastic_albedo_known_answer(oracle, scenes):
     print("plastic albedo", img.mean(), want.mean(), sig)
     assert err <= 4 * sig + 2e-4, (img.mean(), want.mean(), sig)
     # both lobes taken: vertices saved for the diffuse lobe only
-    assert 0 < (r["nv"] == 1).mean() < 1
+    if rho > 0:
+        assert 0 < (r["nv"] == 1).mean() < 1
+    else:
+        assert bp[7] == 1.0 and (r["nv"] == 0).all()
