@@ -561,24 +561,38 @@ def main():
                               "kernel_us": st_kern * 1e6, "flops_per_pair": 113,
                               "fp32_frac": n_local * K * 113.0 / st_kern / FP32_PEAK}
         # ---- guided queries (replicas: each rank serves Q/world queries) ----
+        # two query sets against the fitted K = 128 mixture: SURVEY 8(d)'s
+        # stated workload (c uniform in [0,1]^3, 3 uniforms, seed 0x6A1D:
+        # synth.queries) -- the primary line -- and queries at sample
+        # positions, where guiding happens (the round-4 line, harder: the
+        # fitted components are live there and the lists are longer)
         q_local = args.Q // world
-        c, u = synth.sample_queries_near(batch, q_local, seed=synth.SEED_QUERIES + rank)
-        ct = [torch.from_numpy(c[i].copy()).to(dev) for i in range(3)]
-        ut = [torch.from_numpy(u[i].copy()).to(dev) for i in range(3)]
         gout = ([torch.empty(q_local, device=dev) for _ in range(3)], torch.empty(q_local, device=dev),
                 torch.empty(q_local, device=dev, dtype=torch.int32))
-        mix.guide(ct, ut, gout)
         g_steps = max(3, args.steps // 4)
-        g_wall, g_kern = timed(lambda: mix.guide(ct, ut, gout), g_steps)
-        # FP32 fraction of the guided queries, counted from below: the K
-        # marginal weights every query forms (3x3 triangular solve, squared
-        # norm, scaling: ~22 flops per component; the exp and the kept
-        # components' conditional / sample / pdf work not counted)
-        out["guide"] = {"queries_per_s": q_local * world / (g_wall / g_steps), "Q": q_local * world,
-                        "ms_per_step": g_wall / g_steps * 1e3, "bytes_per_query": 48,
-                        "kernel_us": g_kern * 1e6, "flops_per_query_lower_bound": 22 * K,
-                        "fp32_frac": q_local * 22.0 * K / g_kern / FP32_PEAK,
-                        "hbm_frac": q_local * 48.0 / g_kern / HBM_PEAK}
+
+        def guide_line(c, u):
+            ct = [torch.from_numpy(c[i].copy()).to(dev) for i in range(3)]
+            ut = [torch.from_numpy(u[i].copy()).to(dev) for i in range(3)]
+            mix.guide(ct, ut, gout)
+            g_wall, g_kern = timed(lambda: mix.guide(ct, ut, gout), g_steps)
+            # FP32 fraction of the guided queries, counted from below: the K
+            # marginal weights every query forms (3x3 triangular solve, squared
+            # norm, scaling: ~22 flops per component; the exp and the kept
+            # components' conditional / sample / pdf work not counted)
+            return {"queries_per_s": q_local * world / (g_wall / g_steps), "Q": q_local * world,
+                    "ms_per_step": g_wall / g_steps * 1e3, "bytes_per_query": 48,
+                    "kernel_us": g_kern * 1e6, "flops_per_query_lower_bound": 22 * K,
+                    "fp32_frac": q_local * 22.0 * K / g_kern / FP32_PEAK,
+                    "hbm_frac": q_local * 48.0 / g_kern / HBM_PEAK,
+                    "guided_frac": float((gout[2] >= 0).float().mean())}, ct, ut
+
+        c, u = synth.queries(q_local, seed=synth.SEED_QUERIES + rank)
+        out["guide"], _, _ = guide_line(c, u)
+        out["guide"]["queries"] = "uniform c in [0,1]^3 (SURVEY 8(d), seed 0x6A1D)"
+        c, u = synth.sample_queries_near(batch, q_local, seed=synth.SEED_QUERIES + rank)
+        out["guide_near"], ct, ut = guide_line(c, u)
+        out["guide_near"]["queries"] = "c at sample positions of the batch"
         # ---- batched per-leaf EM: the plugin's tree leaves,
         # each its own K=16 mixture over its own samples (volpath_sdmm.cpp:287-311);
         # leaves shard across ranks with no exchange (weak scaling per rank) ----

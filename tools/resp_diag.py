@@ -28,8 +28,15 @@ def main():
     for _ in range(5):
         mix.optimize(ds)
     resp = torch.empty((N, K), device=dev)
+    import os
+    import time
+    gap = float(os.environ.get("RESP_GAP_MS", "0"))   # idle time between launches (DVFS probe)
+    reps = int(os.environ.get("RESP_REPS", "40"))
     ts = []
-    for i in range(40):
+    for i in range(reps):
+        if gap > 0:
+            torch.cuda.synchronize()
+            time.sleep(gap * 1e-3)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         mix.posterior(ds, resp)
