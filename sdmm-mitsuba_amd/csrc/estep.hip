@@ -717,7 +717,8 @@ __device__ __forceinline__ SamplesDev shift_samples(SamplesDev s, int64_t s0) {
 
 // ---------------------------------------------------------------------------
 // Fused E-step + sufficient statistics (calculateStats + sumWeights).
-// partial row layout: [f*Kp + k] for f < ST_FIELDS, then [21Kp] = H, [21Kp+1] = wsum.
+// partial row layout (component-major): [ST_FIELDS k + f] for f < ST_FIELDS
+// (W, M0..M4, C00..C44: the compact order), then [21Kp] = H, [21Kp+1] = wsum.
 template <int CPL, int LPS>
 __global__ void __launch_bounds__(256)
 estep_stats_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, int64_t n,
@@ -782,7 +783,7 @@ estep_stats_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, in
         const float thr = nm.fin ? 1e-10f : __builtin_inff();
         // Spatial statistics are accumulated centred on the component's mean
         // position (tp = p - mu_k) and un-centred in fp64 by
-        // sum_uncenter_kernel: the M-step's C/W - mu mu^T then does not
+        // reduce_uncenter_kernel: the M-step's C/W - mu mu^T then does not
         // amplify fp32 accumulation error by |p|^2 / sigma^2.
 #pragma unroll
         for (int c = 0; c < NP; ++c) {
@@ -848,8 +849,10 @@ estep_stats_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev s, in
             for (int c = 0; c < NP; ++c)
 #pragma unroll
                 for (int f = 0; f < ST_FIELDS; ++f) {
-                    V* dst = (V*)&red[f * Kp + kbase + 2 * c];
-                    *dst = (w == 0) ? acc[c][f] : *dst + acc[c][f];
+                    float* d0 = &red[ST_FIELDS * (kbase + 2 * c) + f];
+                    float* d1 = d0 + ST_FIELDS;
+                    *d0 = (w == 0) ? acc[c][f].x : *d0 + acc[c][f].x;
+                    *d1 = (w == 0) ? acc[c][f].y : *d1 + acc[c][f].y;
                 }
             if (lane == 0) {
                 red[ST_FIELDS * Kp] = (w == 0) ? accH : red[ST_FIELDS * Kp] + accH;
@@ -1124,73 +1127,71 @@ estep_stats_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
         accH += __shfl_xor(accH, off);
         accWs += __shfl_xor(accWs, off);
     }
-    // fold the workgroup's waves in a fixed order through LDS (GROUP: the
-    // waves' component ranges are disjoint, each writes its own)
+    // fold the workgroup's waves in a fixed order: every wave parks its row in
+    // its own LDS slot, one barrier, then each column is summed over the slots
+    // in wave order ((a0 + a1) + a2) + a3 -- the order of a wave-by-wave fold,
+    // with one barrier instead of WPB (GROUP: the waves' component ranges are
+    // disjoint, one slot, each wave writes its own columns)
     const int rowlen = ST_FIELDS * Kp + 2;
-    for (int w = 0; w < WPB; ++w) {
-        if (wid == w) {
+    constexpr int NSLOT = GROUP ? 1 : WPB;
+    float* mine = red + (GROUP ? 0 : wid * rowlen);
 #pragma unroll
-            for (int f = 0; f < ST_FIELDS; ++f) {
-                V* dst = (V*)&red[f * Kp + kbase];
-                *dst = (w == 0 || GROUP) ? acc[f] : *dst + acc[f];
-            }
-            if (lane == 0) {
-                red[ST_FIELDS * Kp] = (w == 0) ? accH : red[ST_FIELDS * Kp] + accH;
-                red[ST_FIELDS * Kp + 1] = (w == 0) ? accWs : red[ST_FIELDS * Kp + 1] + accWs;
-            }
-        }
-        __syncthreads();
+    for (int f = 0; f < ST_FIELDS; ++f) {
+        mine[ST_FIELDS * kbase + f] = acc[f].x;
+        mine[ST_FIELDS * (kbase + 1) + f] = acc[f].y;
     }
-    for (int idx = threadIdx.x; idx < rowlen; idx += blockDim.x) prow[idx] = red[idx];
+    if (lane == 0 && (!GROUP || wid == 0)) {
+        mine[ST_FIELDS * Kp] = accH;
+        mine[ST_FIELDS * Kp + 1] = accWs;
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < rowlen; idx += blockDim.x) {
+        float v = red[idx];
+#pragma unroll
+        for (int w = 1; w < NSLOT; ++w) v += red[w * rowlen + idx];
+        prow[idx] = v;
+    }
 }
 
 // ---------------------------------------------------------------------------
 // Deterministic fp64 reduction of the partial rows into the compact stats
-// vector [H, wsum, W(K), M(5K), Clow(15K)], in two launches so the whole chip
-// takes part: stage 1 = (64-column block) x (row slice) workgroups, each
-// summing its slice in a fixed order into slice[s][col]; stage 2 (inside
-// sum_uncenter_kernel) sums the kReduceSlices slices of each column in order.
+// vector [H, wsum, W(K), M(5K), Clow(15K)].  The fixed summation order: the
+// rows split into kReduceSlices slices; within slice s four row-interleaved
+// fp64 sums (rows r0 + j, r0 + j + 4, ...; j < 4) combined as ((b0 + b1) + b2)
+// + b3; the slices summed in order from 0.0.  The batched per-leaf reduction
+// (batched_col) uses the same order, so a leaf's stats are bitwise those of
+// its single-mixture E-step.
 constexpr int kReduceSlices = 16;
 
+// Partial-row column of compact index o (component-major rows).
 __device__ __forceinline__ int partial_col(int o, int Kp, int K) {
     if (o == 0) return ST_FIELDS * Kp;
     if (o == 1) return ST_FIELDS * Kp + 1;
     const int r = o - 2;
-    if (r < K) return ST_W * Kp + r;
-    if (r < 6 * K) { const int q = r - K; return (ST_M0 + q % 5) * Kp + q / 5; }
+    if (r < K) return ST_FIELDS * r + ST_W;
+    if (r < 6 * K) { const int q = r - K; return ST_FIELDS * (q / 5) + ST_M0 + q % 5; }
     const int q = r - 6 * K;
-    return (ST_C00 + q % 15) * Kp + q / 15;
+    return ST_FIELDS * (q / 15) + ST_C00 + q % 15;
+}
+// ... and its inverse: the compact index of partial column c, or -1 (padding)
+__device__ __forceinline__ int compact_of(int c, int Kp, int K) {
+    if (c == ST_FIELDS * Kp) return 0;
+    if (c == ST_FIELDS * Kp + 1) return 1;
+    const int k = c / ST_FIELDS, f = c % ST_FIELDS;
+    if (k >= K) return -1;
+    if (f == ST_W) return 2 + k;
+    if (f < ST_C00) return 2 + K + 5 * k + (f - ST_M0);
+    return 2 + 6 * K + 15 * k + (f - ST_C00);
 }
 
-__global__ void __launch_bounds__(256)
-reduce_partials_slices_kernel(const float* __restrict__ partials, int rows, int pstride, int Kp, int K,
-                              double* __restrict__ slices) {
-    __shared__ double buf[4][64];
-    const int lane = threadIdx.x & 63;
-    const int wid = threadIdx.x >> 6;
-    const int ncols = 2 + ST_FIELDS * K;
-    const int o = blockIdx.x * 64 + lane;
-    const int sl = blockIdx.y;
-    const int r0 = (int)((int64_t)rows * sl / kReduceSlices);
-    const int r1 = (int)((int64_t)rows * (sl + 1) / kReduceSlices);
-    double sum = 0.0;
-    if (o < ncols) {
-        const int col = partial_col(o, Kp, K);
-        for (int r = r0 + wid; r < r1; r += 4) sum += (double)partials[(int64_t)r * pstride + col];
-    }
-    buf[wid][lane] = sum;
-    __syncthreads();
-    if (wid == 0 && o < ncols)
-        slices[(int64_t)sl * ncols + o] = ((buf[0][lane] + buf[1][lane]) + buf[2][lane]) + buf[3][lane];
-}
-
-
-// Sum the row slices of component k's columns, then un-centre its spatial
-// statistics (fp64):
+// The un-centring of one component's spatial statistics (fp64, in place):
 //   M_p = M'_p + W mu,  C_pp = C'_pp + M'_p mu^T + mu M'_p^T + W mu mu^T,
 //   C_tp = C'_tp + M_t mu^T   (mu = the float mean the E-step subtracted).
-// The un-centring of one component's spatial statistics (fp64, in place).
 __device__ __forceinline__ void uncenter_component(const double mu[3], double w, double M[5], double C[15]) {
+    // no FMA contraction: the single-mixture and the batched reduction inline
+    // this into different code, and a contraction the backend picks per
+    // context would part their bits
+#pragma clang fp contract(off)
     // C_pp (entries 0..5: (0,0) (1,0) (1,1) (2,0) (2,1) (2,2))
     int e = 0;
     for (int i = 0; i < 3; ++i)
@@ -1203,52 +1204,70 @@ __device__ __forceinline__ void uncenter_component(const double mu[3], double w,
     }
     for (int i = 0; i < 3; ++i) M[i] = M[i] + w * mu[i];
 }
-// Stage 2: the slices summed and the statistics un-centred in ONE launch
-// (round 4: two launches, a per-column slice sum then a per-component
-// un-centring, bitwise the same and slower): workgroup b owns components
-// kSumCB b .. kSumCB b + kSumCB - 1, one thread per column of theirs (their W,
-// M and C columns are three contiguous runs of the compact vector) sums the
-// slices in slice order into LDS, then one thread per component un-centres
-// from LDS and writes the final columns.  Workgroup 0 also sums H and wsum.
-// The same operations in the same order as the two kernels: bitwise equal.
-constexpr int kSumCB = 8;
-__global__ void __launch_bounds__(256)
-sum_uncenter_kernel(int ncols, const double* __restrict__ slices, const float* __restrict__ ep, int Kp, int K,
-                    double* __restrict__ stats) {
-    __shared__ double col[21 * kSumCB];
-    const int k0 = blockIdx.x * kSumCB;
-    const int t = threadIdx.x;
-    auto column = [&](int i) {   // compact index of this workgroup's column i (< 21 kSumCB), or -1
-        int k, o;
-        if (i < kSumCB) { k = k0 + i; o = 2 + k; }
-        else if (i < 6 * kSumCB) { k = k0 + (i - kSumCB) / 5; o = 2 + K + 5 * k0 + (i - kSumCB); }
-        else { k = k0 + (i - 6 * kSumCB) / 15; o = 2 + 6 * K + 15 * k0 + (i - 6 * kSumCB); }
-        return k < K ? o : -1;
-    };
-    if (t < 21 * kSumCB) {
-        const int o = column(t);
-        if (o >= 0) {
-            double v = 0.0;
-#pragma unroll
-            for (int sl = 0; sl < kReduceSlices; ++sl) v += slices[(int64_t)sl * ncols + o];
-            col[t] = v;
-        }
-    } else if (blockIdx.x == 0 && t < 21 * kSumCB + 2) {
-        const int o = t - 21 * kSumCB;   // H, wsum
-        double v = 0.0;
-#pragma unroll
-        for (int sl = 0; sl < kReduceSlices; ++sl) v += slices[(int64_t)sl * ncols + o];
-        stats[o] = v;
+
+// The whole reduction and the un-centring in ONE launch (round 4: two, a
+// (64-column block x slice) pass through an fp64 scratch then a per-component
+// slice sum + un-centring; 6.6 + 5.3 us at 512 rows, K = 128, both mostly
+// launch and latency): workgroup b owns components kRedCB b .. kRedCB b + 2,
+// whose 63 partial columns are contiguous in the component-major rows (one
+// lane each; the extra last workgroup owns H and wsum); wave s sums row slice
+// s (its four interleaved sums in registers, every load independent), wave 0
+// then sums the slices in order and lanes < kRedCB un-centre their component.
+// The same operations in the same order as the two-launch form: bitwise equal.
+constexpr int kRedCB = 3;
+static_assert(ST_FIELDS * kRedCB <= 64, "a workgroup's columns fit one wave");
+__global__ void __launch_bounds__(64 * kReduceSlices)
+reduce_uncenter_kernel(const float* __restrict__ partials, int rows, int pstride, const float* __restrict__ ep,
+                       int Kp, int K, double* __restrict__ stats) {
+    __shared__ double sv[kReduceSlices][64];
+    const int lane = threadIdx.x & 63;
+    const int sl = threadIdx.x >> 6;
+    const int nb = (K + kRedCB - 1) / kRedCB;
+    const int k0 = blockIdx.x * kRedCB;
+    int col = -1;
+    if (blockIdx.x == nb) {
+        if (lane < 2) col = ST_FIELDS * Kp + lane;
+    } else if (lane < ST_FIELDS * kRedCB && k0 + lane / ST_FIELDS < K) {
+        col = ST_FIELDS * k0 + lane;
     }
+    const int r0 = (int)((int64_t)rows * sl / kReduceSlices);
+    const int r1 = (int)((int64_t)rows * (sl + 1) / kReduceSlices);
+    double b[4] = {0.0, 0.0, 0.0, 0.0};
+    if (col >= 0) {
+        const float* p = partials + col;
+        int r = r0;
+        for (; r + 16 <= r1; r += 16) {
+            float v[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] = p[(int64_t)(r + i) * pstride];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) b[i & 3] += (double)v[i];
+        }
+        for (; r < r1; ++r) b[(r - r0) & 3] += (double)p[(int64_t)r * pstride];
+    }
+    sv[sl][lane] = ((b[0] + b[1]) + b[2]) + b[3];
     __syncthreads();
-    if (t < kSumCB && k0 + t < K) {
-        const int k = k0 + t;
+    if (sl != 0) return;
+    double v = 0.0;
+#pragma unroll
+    for (int s2 = 0; s2 < kReduceSlices; ++s2) v += sv[s2][lane];
+    if (blockIdx.x == nb) {
+        if (lane < 2) stats[lane] = v;
+        return;
+    }
+    // lane l < kRedCB gathers its component's 21 columns from lanes 21 l + f
+    const int cl = lane < kRedCB ? ST_FIELDS * lane : 0;
+    double c[ST_FIELDS];
+#pragma unroll
+    for (int f = 0; f < ST_FIELDS; ++f) c[f] = __shfl(v, cl + f);
+    const int k = k0 + lane;
+    if (lane < kRedCB && k < K) {
         const double mu[3] = {(double)ep[EP_MU0 * Kp + k], (double)ep[EP_MU1 * Kp + k],
                               (double)ep[EP_MU2 * Kp + k]};
-        const double w = col[t];
+        const double w = c[ST_W];
         double M[5], C[15];
-        for (int i = 0; i < 5; ++i) M[i] = col[kSumCB + 5 * t + i];
-        for (int i = 0; i < 15; ++i) C[i] = col[6 * kSumCB + 15 * t + i];
+        for (int i = 0; i < 5; ++i) M[i] = c[ST_M0 + i];
+        for (int i = 0; i < 15; ++i) C[i] = c[ST_C00 + i];
         uncenter_component(mu, w, M, C);
         stats[2 + k] = w;
         for (int i = 0; i < 5; ++i) stats[2 + K + 5 * k + i] = M[i];
@@ -1256,12 +1275,11 @@ sum_uncenter_kernel(int ncols, const double* __restrict__ slices, const float* _
     }
 }
 
-// Batched reduction + finalisation: thread (leaf blockIdx.y, component k)
-// reproduces, operation for operation, reduce_partials_slices_kernel (slices
-// of the leaf's rows, four row-interleaved fp64 partials per slice combined as
-// ((b0 + b1) + b2) + b3) followed by sum_uncenter_kernel (slices summed in
-// order, then the un-centring), so a batched leaf's stats are bitwise those of
-// its single-mixture E-step.
+// Batched reduction + finalisation: one column of a leaf's rows reduced in
+// reduce_uncenter_kernel's order (slices of the leaf's rows, four
+// row-interleaved fp64 partials per slice combined as ((b0 + b1) + b2) + b3,
+// slices summed in order), so a batched leaf's stats are bitwise those of its
+// single-mixture E-step.
 __device__ __forceinline__ double batched_col(const float* __restrict__ partials, int pstride, int row0, int rows,
                                               int col) {
     double t = 0.0;
@@ -1285,7 +1303,7 @@ __device__ __forceinline__ double batched_col(const float* __restrict__ partials
 // reduced exactly as batched_col / the single-mixture path orders it (16 row
 // slices, four row-interleaved fp64 sums per slice combined as
 // ((b0 + b1) + b2) + b3, slices summed in order) into LDS.  Phase 2: the
-// un-centring of the spatial moments per component, as sum_uncenter_kernel.
+// un-centring of the spatial moments per component, as reduce_uncenter_kernel.
 // Bitwise equal to the previous thread-per-component form, with 21x more
 // threads in flight (it was latency-bound: 16 busy lanes per leaf): 257 ->
 // ~50 us per 256-leaf K=16 step (a (column, slice) split measured no faster).
@@ -1297,8 +1315,12 @@ reduce_finalize_batched_kernel(const float* __restrict__ partials, int pstride, 
     const LeafDesc& L = leaves[blockIdx.x];
     if (L.n <= 0) return;             // uniform over the workgroup
     const int ncols = 2 + 21 * K;
-    for (int o = threadIdx.x; o < ncols; o += blockDim.x)
-        red[o] = batched_col(partials, pstride, L.row0, L.rows, partial_col(o, Kp, K));
+    // one thread per partial column (consecutive threads, consecutive
+    // addresses), stored at its compact index
+    for (int c = threadIdx.x; c < ST_FIELDS * Kp + 2; c += blockDim.x) {
+        const int o = compact_of(c, Kp, K);
+        if (o >= 0) red[o] = batched_col(partials, pstride, L.row0, L.rows, c);
+    }
     __syncthreads();
     double* stats = L.stats;
     if (threadIdx.x < 2) stats[threadIdx.x] = red[threadIdx.x];
@@ -1406,7 +1428,9 @@ const char* estep_resp_tile_name(int variant) {
 hipError_t launch_estep_stats_tile(int variant, const float* ep, int Kp, int K, const SamplesDev& s, int64_t n,
                                    int64_t chunk, int blocks, float* partials, int pstride, hipStream_t st,
                                    const LeafDesc* leaves, const int2* items) {
-    const size_t lds = sizeof(float) * (size_t)(ST_FIELDS * Kp + 2);
+    // one row slot per wave (GROUP: one shared slot)
+    const size_t row = sizeof(float) * (size_t)(ST_FIELDS * Kp + 2);
+    const size_t lds = (Kp == 128) ? 4 * row : row;
     if (Kp == 128 && K > 64 && K <= 128) {
         if (variant == 1)
             hipLaunchKernelGGL((estep_stats_tile_kernel<4, 3>), dim3(blocks), dim3(256), lds, st, ep, Kp, K, s, n,
@@ -1427,7 +1451,8 @@ hipError_t launch_estep_stats_tile(int variant, const float* ep, int Kp, int K, 
 }
 // resident workgroups per CU; *waves_per_wg: the waves of one (GROUP: one chunk)
 hipError_t estep_stats_tile_occupancy(int variant, int Kp, int* blocks_per_cu) {
-    const size_t lds = sizeof(float) * (size_t)(ST_FIELDS * Kp + 2);
+    const size_t row = sizeof(float) * (size_t)(ST_FIELDS * Kp + 2);
+    const size_t lds = (Kp == 128) ? 4 * row : row;
     if (Kp == 256)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(
             blocks_per_cu, reinterpret_cast<const void*>(&estep_stats_tile_kernel<2, 2, true>), 128, lds);
@@ -1470,13 +1495,9 @@ hipError_t estep_occupancy(int cpl, int lps, int Kp, int* resp_blocks, int* stat
 }
 
 hipError_t launch_reduce_partials(const float* partials, int rows, int pstride, const float* ep_for_finalize,
-                                  int Kp, int K, double* stats, double* scratch, hipStream_t st) {
-    const int ncols = 2 + ST_FIELDS * K;
-    hipLaunchKernelGGL(reduce_partials_slices_kernel, dim3((ncols + 63) / 64, kReduceSlices), dim3(256), 0, st,
-                       partials, rows, pstride, Kp, K, scratch);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(sum_uncenter_kernel, dim3((K + kSumCB - 1) / kSumCB), dim3(256), 0, st, ncols, scratch,
+                                  int Kp, int K, double* stats, hipStream_t st) {
+    const int nb = (K + kRedCB - 1) / kRedCB + 1;
+    hipLaunchKernelGGL(reduce_uncenter_kernel, dim3(nb), dim3(64 * kReduceSlices), 0, st, partials, rows, pstride,
                        ep_for_finalize, Kp, K, stats);
     return hipGetLastError();
 }

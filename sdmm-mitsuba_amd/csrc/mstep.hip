@@ -91,7 +91,11 @@ __device__ static void inv3_d(const double* m, double* r) {
 }
 
 // MVTN::set(mean, cov) in fp64, results rounded to float (oracle mode 1).
-__device__ static void set_component(int k, const double* mean, const double* cov, const CanonDev& C) {
+// have >= 0: the fp64 Cholesky of this cov was already attempted (the PD
+// test's own, pd_test_keep) -- have = its success, Lk / Lik its L and L^-1 --
+// and is not repeated (the same operations on the same doubles).
+__device__ static void set_component(int k, const double* mean, const double* cov, const CanonDev& C,
+                                     int have = -1, const double* Lk = nullptr, const double* Lik = nullptr) {
     float fm[6];
     for (int i = 0; i < 6; ++i) { fm[i] = (float)mean[i]; C.mean[6 * k + i] = fm[i]; }
     for (int i = 0; i < 25; ++i) C.cov[25 * k + i] = (float)cov[i];
@@ -123,10 +127,20 @@ __device__ static void set_component(int k, const double* mean, const double* co
         }
     for (int i = 0; i < 6; ++i) C.muPremult[6 * k + i] = (float)P[i];
     for (int i = 0; i < 4; ++i) C.condCov[4 * k + i] = (float)S[i];
-    double L[25], Li[25];
+    double Lb[25], Lib[25];
+    const double* L = Lk;
+    const double* Li = Lik;
     int ok = 1;
-    if (llt_d<5>(cov, L)) {
-        tri_inv_d<5>(L, Li);
+    bool chol;
+    if (have < 0) {
+        chol = llt_d<5>(cov, Lb);
+        if (chol) tri_inv_d<5>(Lb, Lib);
+        L = Lb;
+        Li = Lib;
+    } else {
+        chol = have != 0;
+    }
+    if (chol) {
         double det = 1.0;
         for (int i = 0; i < 5; ++i) det *= L[6 * i];
         for (int i = 0; i < 25; ++i) {
@@ -159,8 +173,10 @@ __device__ static void set_component(int k, const double* mean, const double* co
 }
 
 // Packed E-step and guide records of component k (k < Kp; k >= K is padding).
+// weights == false: every field but the weight ones (EP_PI, EP_DIPI, GP_W:
+// pack_weights writes them once the weights are final).
 __device__ static void pack_component(int k, int K, int Kp, const CanonDev& C, float* ep, float* gp,
-                                      float norm5) {
+                                      float norm5, bool weights = true) {
     float e[EP_FIELDS];
     float g[GP_FIELDS];
     for (int f = 0; f < EP_FIELDS; ++f) e[f] = 0.0f;
@@ -213,8 +229,22 @@ __device__ static void pack_component(int k, int K, int Kp, const CanonDev& C, f
             g[rml[i] + 1] = __builtin_bit_cast(float, (uint32_t)(bits >> 32));
         }
     }
-    for (int f = 0; f < EP_FIELDS; ++f) ep[f * Kp + k] = e[f];
-    for (int f = 0; f < GP_FIELDS; ++f) gp[k * GP_STRIDE + f] = g[f];
+    for (int f = 0; f < EP_FIELDS; ++f)
+        if (weights || (f != EP_PI && f != EP_DIPI)) ep[f * Kp + k] = e[f];
+    for (int f = 0; f < GP_FIELDS; ++f)
+        if (weights || f != GP_W) gp[k * GP_STRIDE + f] = g[f];
+}
+// The weight fields of record k, as pack_component forms them.
+__device__ static void pack_weights(int k, int K, int Kp, const CanonDev& C, float* ep, float* gp) {
+    float pi = 0.0f, dipi = 0.0f, w = 0.0f;
+    if (k < K) {
+        w = C.weights[k];
+        pi = C.valid[k] ? w : 0.0f;
+        dipi = ep[EP_DI * Kp + k] * pi;
+    }
+    ep[EP_PI * Kp + k] = pi;
+    ep[EP_DIPI * Kp + k] = dipi;
+    gp[k * GP_STRIDE + GP_W] = w;
 }
 
 // createCdf(false) then configure()'s createCdf(true) (float, sequential);
@@ -304,10 +334,9 @@ __device__ static bool pd_jacobi_d(const double* A) {
 // would report positive definite too; every other case (a failed or
 // near-singular factorisation) runs the Jacobi test itself.  Same decisions as
 // pd_jacobi_d alone, at the cost of a Cholesky for the common component.
-__device__ static bool pd_test_d(const double* A) {
-    double L[25];
-    if (llt_d<5>(A, L)) {
-        double Li[25];
+__device__ static bool pd_test_keep(const double* A, double* L, double* Li, bool* have) {
+    *have = llt_d<5>(A, L);
+    if (*have) {
         tri_inv_d<5>(L, Li);
         double fro = 0.0, an = 0.0;
         for (int i = 0; i < 25; ++i) {
@@ -319,6 +348,11 @@ __device__ static bool pd_test_d(const double* A) {
         if (isfinite(fro) && 1.0 / fro > 1e-9 * sqrt(an)) return true;
     }
     return pd_jacobi_d(A);
+}
+__device__ static bool pd_test_d(const double* A) {
+    double L[25], Li[25];
+    bool have;
+    return pd_test_keep(A, L, Li, &have);
 }
 
 // ---------------------------------------------------------------------------
@@ -336,8 +370,10 @@ __device__ static bool pd_test_d(const double* A) {
 //   4. pack      the E-step / guide records of every component
 // sh: [status, eta, weightSum, 1/hTW, invGlobal, invMix]; status 0: weightSum
 // == 0, optimize() returns early (nothing changes).
-__device__ __forceinline__ void mstep_scalars(const double* __restrict__ stats, int64_t nSamples, int K,
-                                              const EmStateDev& S, double* sh) {
+// sh as above; upd: the blended [heuristicTotalWeight, sgH, normalization]
+// the scalars take (written by mstep_scalars_store, after every reader).
+__device__ __forceinline__ void mstep_scalars_compute(const double* __restrict__ stats, int64_t nSamples, int K,
+                                                      const EmStateDev& S, double* sh, double* upd) {
     if (nSamples < 0) nSamples = (int64_t)stats[2 + ST_FIELDS * K];   // sharded: the all-reduced count
     const double weightSum = stats[1];
     sh[0] = (weightSum == 0.0) ? 0.0 : 1.0;
@@ -349,12 +385,12 @@ __device__ __forceinline__ void mstep_scalars(const double* __restrict__ stats, 
         double hTW = S.scalars[SC_HTW];
         hTW *= (1.0 - eta);
         hTW += eta * weightSum;
-        S.scalars[SC_HTW] = hTW;
+        upd[0] = hTW;
         double gH = S.scalars[SC_SGH] * (1.0 - eta);
         gH = eta * stats[0] + gH;
-        S.scalars[SC_SGH] = gH;
+        upd[1] = gH;
         const double norm = (double)(float)S.scalars[SC_NORM];
-        S.scalars[SC_NORM] = (double)(float)((1.0 - eta) * norm + eta * weightSum / (double)nSamples);
+        upd[2] = (double)(float)((1.0 - eta) * norm + eta * weightSum / (double)nSamples);
         const int cutoff = (int)S.scalars[SC_CUT];
         const int cut = (cutoff < it) ? cutoff : it;
         // 3^cut and 2^cut are exact in fp64 for cut <= 33 (the trainingCutoff
@@ -371,35 +407,77 @@ __device__ __forceinline__ void mstep_scalars(const double* __restrict__ stats, 
         sh[4] = invGlobal;
         sh[5] = invMix;
     }
+}
+__device__ __forceinline__ void mstep_scalars_store(const EmStateDev& S, const double* sh, const double* upd) {
+    if (sh[0] != 0.0) {
+        S.scalars[SC_HTW] = upd[0];
+        S.scalars[SC_SGH] = upd[1];
+        S.scalars[SC_NORM] = upd[2];
+    }
     S.scalars[SC_STATUS] = sh[0];
 }
+__device__ __forceinline__ void mstep_scalars(const double* __restrict__ stats, int64_t nSamples, int K,
+                                              const EmStateDev& S, double* sh) {
+    double upd[3];
+    mstep_scalars_compute(stats, nSamples, K, S, sh, upd);
+    mstep_scalars_store(S, sh, upd);
+}
 
-__device__ __forceinline__ void mstep_component(int k, int K, const double* __restrict__ stats, const CanonDev& C,
-                                                const EmStateDev& S, const double* sh, double* newW, int* setk,
-                                                double* __restrict__ wmean, double* __restrict__ wcov) {
+// Component k's inputs to the M-step (its stats, stepwise state, priors,
+// weight and frame), loaded ahead of the scalars so that the loads overlap
+// them (mstep_spread_kernel).
+struct CompIn {
+    double st[ST_FIELDS];   // W, M0..M4, Clow (the compact order)
+    double T, sgW, sgM[5], sgC[25], ni;
+    float bP[25], bD[9], to[9], w;
+    bool decp;
+};
+__device__ __forceinline__ void load_comp_in(int k, int K, const double* __restrict__ stats, const CanonDev& C,
+                                             const EmStateDev& S, CompIn& in) {
+    in.st[0] = stats[2 + k];
+    for (int i = 0; i < 5; ++i) in.st[1 + i] = stats[2 + K + 5 * k + i];
+    for (int i = 0; i < 15; ++i) in.st[6 + i] = stats[2 + 6 * K + 15 * k + i];
+    in.T = S.T[k];
+    in.sgW = S.sgW[k];
+    for (int i = 0; i < 5; ++i) in.sgM[i] = S.sgM[5 * k + i];
+    for (int i = 0; i < 25; ++i) in.sgC[i] = S.sgC[25 * k + i];
+    in.ni = S.scalars[SC_NI];
+    in.decp = S.scalars[SC_DECP] != 0.0;
+    for (int i = 0; i < 25; ++i) in.bP[i] = S.bPriors[25 * k + i];
+    for (int i = 0; i < 9; ++i) in.bD[i] = S.bDepth[9 * k + i];
+    for (int i = 0; i < 9; ++i) in.to[i] = C.to[9 * k + i];
+    in.w = C.weights[k];
+}
+
+// wm, wc: component k's accepted (mean, cov) slots; L5 / Li5 / have (or
+// nullptr): keep the PD test's fp64 factorisation for set_component.
+__device__ __forceinline__ void mstep_component(int k, int K, const CompIn& in, const EmStateDev& S,
+                                                const double* sh, double* newW, int* setk,
+                                                double* __restrict__ wm, double* __restrict__ wc,
+                                                double* L5 = nullptr, double* Li5 = nullptr, bool* have = nullptr) {
     const double eta = sh[1], weightSum = sh[2], invTotalWeight = sh[3];
     const double invGlobal = sh[4], invMix = sh[5];
-    const double ni = S.scalars[SC_NI];
-    const bool decreasePrior = S.scalars[SC_DECP] != 0.0;
+    const double ni = in.ni;
+    const bool decreasePrior = in.decp;
     setk[k] = 0;
-    double T = S.T[k];
+    double T = in.T;
     T *= (1.0 - eta);
     T += eta * weightSum;
     S.T[k] = T;
     // statsGlobal *= (1 - eta); stats.sumProductInto(statsGlobal, eta)
     const double oneMinus = 1.0 - eta;
-    double gW = S.sgW[k] * oneMinus;
-    gW = eta * stats[2 + k] + gW;
+    double gW = in.sgW * oneMinus;
+    gW = eta * in.st[0] + gW;
     double gM[5], gC[25];
     for (int i = 0; i < 5; ++i) {
-        double v = S.sgM[5 * k + i] * oneMinus;
-        gM[i] = eta * stats[2 + K + 5 * k + i] + v;
+        double v = in.sgM[i] * oneMinus;
+        gM[i] = eta * in.st[1 + i] + v;
     }
     for (int i = 0; i < 5; ++i)
         for (int j = 0; j < 5; ++j) {
             const int a = i > j ? i : j, b = i > j ? j : i;
-            const double sc = stats[2 + 6 * K + 15 * k + a * (a + 1) / 2 + b];
-            double v = S.sgC[25 * k + 5 * i + j] * oneMinus;
+            const double sc = in.st[6 + a * (a + 1) / 2 + b];
+            double v = in.sgC[5 * i + j] * oneMinus;
             gC[5 * i + j] = eta * sc + v;
         }
     // statsGlobalNormalized
@@ -411,7 +489,7 @@ __device__ __forceinline__ void mstep_component(int k, int K, const double* __re
     double decNi = ni;
     double decA = 100.0 / (double)K;
     double decB[25];
-    for (int i = 0; i < 25; ++i) decB[i] = decA * (double)S.bPriors[25 * k + i];
+    for (int i = 0; i < 25; ++i) decB[i] = decA * (double)in.bP[i];
     if (decreasePrior) {
         for (int i = 0; i < 25; ++i) decB[i] = decB[i] * invMix;
         decA = decA * invMix;
@@ -420,7 +498,7 @@ __device__ __forceinline__ void mstep_component(int k, int K, const double* __re
     const double invW = 1.0 / nW;
     const double invMatNorm = 1.0 / (0.05 * decA + nW);
     double w_new;
-    if (C.weights[k] == 0.0f) {
+    if (in.w == 0.0f) {
         w_new = 0.0;                       // dead stays dead (:785)
     } else if (!isfinite(invW)) {
         w_new = decNi + nW;                // weak component (:791)
@@ -433,10 +511,10 @@ __device__ __forceinline__ void mstep_component(int k, int K, const double* __re
         for (int i = 0; i < 25; ++i) cov[i] += decB[i];
         for (int i = 0; i < 25; ++i) cov[i] *= invMatNorm;
         for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) cov[5 * i + j] += (double)S.bDepth[9 * k + 3 * i + j];
+            for (int j = 0; j < 3; ++j) cov[5 * i + j] += (double)in.bD[3 * i + j];
         // exp of the new tangent mean in the OLD frame (:845-852)
         double to[9], emb[6];
-        for (int i = 0; i < 9; ++i) to[i] = (double)C.to[9 * k + i];
+        for (int i = 0; i < 9; ++i) to[i] = (double)in.to[i];
         {
             const double t0 = mean5[3], t1 = mean5[4];
             const double length = sqrt(t0 * t0 + t1 * t1);
@@ -451,11 +529,11 @@ __device__ __forceinline__ void mstep_component(int k, int K, const double* __re
                 emb[5] = to[2] * rel0 + to[5] * rel1 + to[8] * rel2;
             }
         }
-        if (!pd_test_d(cov)) {
+        if (!(L5 ? pd_test_keep(cov, L5, Li5, have) : pd_test_d(cov))) {
             w_new = 0.0;                   // not positive definite: kill (:945-960)
         } else {
-            for (int i = 0; i < 6; ++i) wmean[6 * k + i] = emb[i];
-            for (int i = 0; i < 25; ++i) wcov[25 * k + i] = cov[i];
+            for (int i = 0; i < 6; ++i) wm[i] = emb[i];
+            for (int i = 0; i < 25; ++i) wc[i] = cov[i];
             setk[k] = 1;
             for (int i = 0; i < 5; ++i)
                 for (int j = 0; j < 5; ++j) nC[5 * i + j] -= nM[i] * mean5[j];
@@ -474,17 +552,18 @@ __device__ __forceinline__ void mstep_component(int k, int K, const double* __re
     for (int i = 0; i < 25; ++i) S.sgC[25 * k + i] = gC[i];
 }
 
-// The finish from the whole workgroup: the three
-// order-dependent sums (the fp64 total of newW, the float prefix of the
-// weights -- whose last value is also their float total --, the float prefix
-// of the normalised weights) are each ONE thread's sequential chain over LDS
-// (loads batched ahead of the adds), the elementwise divisions and roundings
-// run on every thread between them.  The readlane chains above took ~16 us of
-// a K = 128 M-step (tools/em_phases.py with SDMM_MSTEP_STOP builds).
-// wl, cl: LDS, K floats each; sh2: 2 doubles of LDS.
-__device__ __forceinline__ void mstep_finish_block(int K, const EmStateDev& S, const double* newW, float* wl,
-                                                   float* cl, double* sh2) {
-    const int t = threadIdx.x;
+// The finish: the three order-dependent sums (the fp64 total of newW, the
+// float prefix of the weights -- whose last value is also their float total
+// --, the float prefix of the normalised weights) are each ONE thread's
+// sequential chain over LDS (loads batched ahead of the adds), the
+// elementwise divisions and roundings run on every thread (t of nt) between
+// them; sync() orders the LDS traffic (a workgroup barrier, or within one
+// wave).  The readlane chains before took ~16 us of a K = 128 M-step
+// (tools/em_phases.py with SDMM_MSTEP_STOP builds).
+// newW, wl, cl: LDS, K doubles / floats; sh2: 2 doubles of LDS.
+template <class Sync>
+__device__ __forceinline__ void mstep_finish(int K, const EmStateDev& S, const double* newW, float* wl, float* cl,
+                                             double* sh2, int t, int nt, Sync sync) {
     if (t == 0) {
         double sum = 0.0;
         int k = 0;
@@ -498,14 +577,14 @@ __device__ __forceinline__ void mstep_finish_block(int K, const EmStateDev& S, c
         for (; k < K; ++k) sum += newW[k];
         sh2[0] = sum;
     }
-    __syncthreads();
+    sync();
     const double sum = sh2[0];
-    for (int k = t; k < K; k += blockDim.x) {
+    for (int k = t; k < K; k += nt) {
         double nw = newW[k];
         if (sum != 0.0) nw = nw / sum;
         wl[k] = (float)nw;
     }
-    __syncthreads();
+    sync();
     // createCdf(false): the unnormalised prefix (kept if the total is 0); its
     // last value is the float total fs
     auto prefix = [&]() {
@@ -528,14 +607,18 @@ __device__ __forceinline__ void mstep_finish_block(int K, const EmStateDev& S, c
         return acc;
     };
     if (t == 0) sh2[1] = (double)prefix();
-    __syncthreads();
+    sync();
     const float fs = (float)sh2[1];
     if (fs != 0.0f) {
-        for (int k = t; k < K; k += blockDim.x) wl[k] = wl[k] / fs;
-        __syncthreads();
+        for (int k = t; k < K; k += nt) wl[k] = wl[k] / fs;
+        sync();
         if (t == 0) (void)prefix();
     }
     if (t == 0) S.scalars[SC_IT] = S.scalars[SC_IT] + 1.0;
+}
+__device__ __forceinline__ void mstep_finish_block(int K, const EmStateDev& S, const double* newW, float* wl,
+                                                   float* cl, double* sh2) {
+    mstep_finish(K, S, newW, wl, cl, sh2, (int)threadIdx.x, (int)blockDim.x, [] { __syncthreads(); });
 }
 
 // The four phases in one workgroup (the batched per-leaf M-step).
@@ -555,7 +638,11 @@ __device__ __forceinline__ void mstep_body(int K, int Kp, const double* __restri
     if (t == 0) mstep_scalars(stats, nSamples, K, S, sh);
     __syncthreads();
     if (sh[0] == 0.0 || SDMM_MSTEP_STOP <= 1) return;  // optimize() returns early when weightSum == 0
-    for (int k = t; k < K; k += blockDim.x) mstep_component(k, K, stats, C, S, sh, newW, setk, wmean, wcov);
+    for (int k = t; k < K; k += blockDim.x) {
+        CompIn in;
+        load_comp_in(k, K, stats, C, S, in);
+        mstep_component(k, K, in, S, sh, newW, setk, wmean + 6 * k, wcov + 25 * k);
+    }
     __syncthreads();
     if (SDMM_MSTEP_STOP <= 2) return;
     for (int k = t; k < K; k += blockDim.x)
@@ -585,11 +672,81 @@ mstep_batched_kernel(int K, int Kp, const MixDesc* __restrict__ mixes, float nor
     mstep_body(K, Kp, d.stats, n, d.C, d.S, d.ep, d.gp, norm5, d.wmean, d.wcov);
 }
 
-// The single-mixture M-step in one workgroup.
-__global__ void __launch_bounds__(512)
-mstep_single_kernel(int K, int Kp, const double* __restrict__ stats, int64_t nSamples, CanonDev C, EmStateDev S,
-                    float* ep, float* gp, float norm5, double* __restrict__ wmean, double* __restrict__ wcov) {
-    mstep_body(K, Kp, stats, nSamples, C, S, ep, gp, norm5, wmean, wcov);
+// The single-mixture M-step spread over ceil(Kp / 64) workgroups of two
+// waves (round 4: one workgroup, 20 us at K = 128 -- a latency chain per
+// component, with 88 VGPRs spilled at its 512-thread bound).  Wave 0 of
+// workgroup b owns components 64 b + lane: the blend / MAP / PD test, then
+// MVTN::set from the PD test's own fp64 factorisation and every record field
+// but the weight ones, all in one thread (nothing goes through memory).  The
+// workgroup whose blends complete last (device-scope counter count[0]) runs
+// the order-dependent finish on its wave 1 while its wave 0 sets: the weights
+// normalised, both CDF prefixes, the scalars.  The last of the nb set waves
+// and the finish to complete (count[1]) writes every record's weight fields
+// and re-arms both counters.  The operations are mstep_body's, so the
+// results are bitwise those of the batched per-leaf form.
+__global__ void __launch_bounds__(128)
+mstep_spread_kernel(int K, int Kp, const double* __restrict__ stats, int64_t nSamples, CanonDev C, EmStateDev S,
+                    float* ep, float* gp, float norm5, double* newW, unsigned* count) {
+    __shared__ double sh[8];
+    __shared__ double upd[3];
+    __shared__ double sh2[2];
+    __shared__ double nwl[512];
+    __shared__ float wl[512], cl[512];
+    __shared__ int role;   // bit 0: this workgroup runs the finish
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const unsigned nb = gridDim.x;
+    const int k = (int)blockIdx.x * 64 + lane;
+    // wave 1 forms the scalars while wave 0 loads its components' inputs
+    CompIn in;
+    if (wv == 0 && k < K) load_comp_in(k, K, stats, C, S, in);
+    if (t == 64) mstep_scalars_compute(stats, nSamples, K, S, sh, upd);
+    __syncthreads();
+    if (sh[0] == 0.0) {   // optimize() returns early when weightSum == 0
+        if (blockIdx.x == 0 && t == 0) S.scalars[SC_STATUS] = 0.0;
+        return;
+    }
+    __shared__ int setk[512];
+    double emb[6], cov[25], L[25], Li[25];
+    bool have = false;
+    if (wv == 0) {
+        if (k < K) mstep_component(k, K, in, S, sh, newW, setk, emb, cov, L, Li, &have);
+        __threadfence();
+        if (lane == 0) role = (atomicAdd(&count[0], 1u) == nb - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (wv == 0) {
+        if (k < K && setk[k]) set_component(k, emb, cov, C, have ? 1 : 0, L, Li);
+        if (k < Kp) pack_component(k, K, Kp, C, ep, gp, norm5, false);
+    } else {
+        if (!role) return;
+        __threadfence();
+        for (int i = lane; i < K; i += 64) nwl[i] = newW[i];
+        auto wave_sync = [] {
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+        };
+        wave_sync();
+        mstep_finish(K, S, nwl, wl, cl, sh2, lane, 64, wave_sync);
+        wave_sync();
+        for (int i = lane; i < K; i += 64) {
+            C.weights[i] = wl[i];
+            C.cdf[i] = cl[i];
+        }
+        if (lane == 0) mstep_scalars_store(S, sh, upd);
+    }
+    // the last of the nb set waves and the finish writes the weight fields
+    __threadfence();
+    __shared__ int fin[2];   // per wave
+    if (lane == 0) fin[wv] = (atomicAdd(&count[1], 1u) == nb) ? 1 : 0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    if (!fin[wv]) return;
+    __threadfence();
+    for (int i = lane; i < Kp; i += 64) pack_weights(i, K, Kp, C, ep, gp);
+    if (lane == 0) {
+        count[0] = 0u;
+        count[1] = 0u;
+    }
 }
 
 __global__ void set_f64_kernel(double* p, double v) { *p = v; }
@@ -880,15 +1037,14 @@ hipError_t launch_pack_all(int K, int Kp, const CanonDev& C, float* ep, float* g
     return hipGetLastError();
 }
 
+// newW: K doubles of scratch; count: two zeroed counters (re-armed by the
+// kernel itself).
 hipError_t launch_mstep(int K, int Kp, const double* stats, int64_t nSamples, const CanonDev& C,
-                        const EmStateDev& S, float* ep, float* gp, float norm5, double* wmean, double* wcov,
+                        const EmStateDev& S, float* ep, float* gp, float norm5, double* newW, unsigned* count,
                         hipStream_t st) {
-    // One workgroup: measured faster than spreading the components over the
-    // chip in separate launches (K = 128: 0.41 vs 0.46 ms per EM step; K = 512:
-    // 1.49 vs 1.62 ms) -- the M-step is launch/latency bound, not throughput bound.
-    const int threads = Kp < 64 ? 64 : (Kp > 512 ? 512 : Kp);
-    hipLaunchKernelGGL(mstep_single_kernel, dim3(1), dim3(threads), (sizeof(double) + sizeof(int) + sizeof(float)) * (size_t)K,
-                       st, K, Kp, stats, nSamples, C, S, ep, gp, norm5, wmean, wcov);
+    if (Kp > 512 || K > Kp) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(mstep_spread_kernel, dim3((unsigned)((Kp + 63) / 64)), dim3(128), 0, st, K, Kp, stats,
+                       nSamples, C, S, ep, gp, norm5, newW, count);
     return hipGetLastError();
 }
 

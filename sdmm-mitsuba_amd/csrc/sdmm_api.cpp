@@ -56,7 +56,7 @@ hipError_t launch_estep_stats_tile(int variant, const float* ep, int Kp, int K, 
                                    const LeafDesc* leaves = nullptr, const int2* items = nullptr);
 hipError_t estep_stats_tile_occupancy(int variant, int Kp, int* blocks_per_cu);
 hipError_t launch_reduce_partials(const float* partials, int rows, int pstride, const float* ep_for_finalize,
-                                  int Kp, int K, double* stats, double* scratch, hipStream_t st);
+                                  int Kp, int K, double* stats, hipStream_t st);
 hipError_t launch_set_all(int K, int Kp, const double* mean, const double* cov, const CanonDev& C,
                           float* ep, float* gp, float norm5, hipStream_t st);
 hipError_t launch_pack_all(int K, int Kp, const CanonDev& C, float* ep, float* gp, float norm5,
@@ -79,7 +79,7 @@ hipError_t launch_init_pack_many(int n, int K, int Kp, const double* scal, const
                                  double* sc, float* bp, float* bd, const CanonDev& C, float* ep, float* gp,
                                  float norm5, size_t stride, hipStream_t st);
 hipError_t launch_mstep(int K, int Kp, const double* stats, int64_t nSamples, const CanonDev& C,
-                        const EmStateDev& S, float* ep, float* gp, float norm5, double* wmean, double* wcov,
+                        const EmStateDev& S, float* ep, float* gp, float norm5, double* newW, unsigned* count,
                         hipStream_t st);
 size_t guide_sort_temp_bytes(int n);
 hipError_t launch_stree_find(const void* nodes, int64_t n, const float* p0, const float* p1, const float* p2,
@@ -350,9 +350,9 @@ struct sdmm_mix {
     float* ep = nullptr;
     float* gp = nullptr;
     double* stats = nullptr;     // compact stats (2 + 21K)
-    double* rscratch = nullptr;  // 16 x (2 + 21K) fp64 row-slice sums of the stats reduction
     double* tmp_mean = nullptr;  // K*6 (set_params / init)
     double* tmp_cov = nullptr;   // K*25
+    unsigned* mcount = nullptr;  // the spread M-step's two counters (zero between launches)
     float* partials = nullptr;
     int partial_rows = 0;
     int pstride = 0;
@@ -592,8 +592,7 @@ int run_estep_stats(sdmm_mix* m, const sdmm_samples* s, double* stats_out) {
     int r = ensure_partials(m, p.blocks);
     if (r) return r;
     HIP_TRY(launch_stats_kernel(m, d, s->n, p, p.blocks, m->partials, m->stream, nullptr, nullptr));
-    HIP_TRY(launch_reduce_partials(m->partials, p.blocks, m->pstride, m->ep, m->Kp, m->K, stats_out, m->rscratch,
-                                   m->stream));
+    HIP_TRY(launch_reduce_partials(m->partials, p.blocks, m->pstride, m->ep, m->Kp, m->K, stats_out, m->stream));
     return SDMM_OK;
 }
 
@@ -672,18 +671,18 @@ size_t layout_block(sdmm_mix* m, char* base) {
     float* ep = (float*)take(4 * (size_t)EP_FIELDS * m->Kp);
     float* gp = (float*)take(4 * (size_t)GP_STRIDE * m->Kp);
     double* stats = (double*)take(8 * (sdmm_stats_len(m->K) + 1));   // + the sample count of a sharded step
-    double* rscratch = (double*)take(8 * 16 * sdmm_stats_len(m->K));
     double* tmean = (double*)take(48 * Kc);
     double* tcov = (double*)take(200 * Kc);
+    unsigned* mcount = (unsigned*)take(8);
     if (base) {
         m->C = CanonDev{w, cdf, mean, cov, to, cl, cli, di, mp, cc, ml, mdi, cdl, cdli, cdi, valid};
         m->S = EmStateDev{sc, T, sgW, sgM, sgC, bp, bd};
         m->ep = ep;
         m->gp = gp;
         m->stats = stats;
-        m->rscratch = rscratch;
         m->tmp_mean = tmean;
         m->tmp_cov = tcov;
+        m->mcount = mcount;
     }
     return (off + 255) / 256 * 256;
 }
@@ -1393,7 +1392,7 @@ int sdmm_mstep(sdmm_mix* m, const double* stats, int64_t n_total) {
     if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
     HIP_TRY(hipSetDevice(m->device));
     HIP_TRY(launch_mstep(m->K, m->Kp, stats, n_total, m->C, m->S, m->ep, m->gp, m->norm5, m->tmp_mean,
-                         m->tmp_cov, m->stream));
+                         m->mcount, m->stream));
     return SDMM_OK;
 }
 
@@ -1480,7 +1479,7 @@ int sdmm_em_step_sharded(sdmm_mix* m, sdmm_comm* c, const sdmm_samples* shard, i
         // SUM over ranks, then the same M-step everywhere (n from the summed count)
         if ((r = comm_allreduce(c, m->stats, len + 1, m->stream))) return r;
         HIP_TRY(launch_mstep(m->K, m->Kp, m->stats, -1, m->C, m->S, m->ep, m->gp, m->norm5, m->tmp_mean,
-                             m->tmp_cov, m->stream));
+                             m->mcount, m->stream));
     }
     return SDMM_OK;
 }
@@ -1555,7 +1554,7 @@ int sdmm_em_step(sdmm_mix* m, const sdmm_samples* s, int iterations) {
         r = run_estep_stats(m, s, m->stats);
         if (r) return r;
         HIP_TRY(launch_mstep(m->K, m->Kp, m->stats, s->n, m->C, m->S, m->ep, m->gp, m->norm5, m->tmp_mean,
-                             m->tmp_cov, m->stream));
+                             m->mcount, m->stream));
     }
     return SDMM_OK;
 }

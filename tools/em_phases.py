@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--K", type=int, default=128)
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--no-rccl", action="store_true")
+    ap.add_argument("--worlds", default="1,8", help="shard counts to time (comma list)")
     a = ap.parse_args()
     import torch
     from conftest import load_pkg
@@ -56,7 +57,7 @@ def main():
         return e0.elapsed_time(e1) * 1000 / reps
 
     out = []
-    for world in (1, 8):
+    for world in [int(w) for w in a.worlds.split(",")]:
         n = N // world
         mix = pkg.SDMM(a.K)
         mix.init_hemisphere(pos, nrm, synth.DEPTH_PRIOR, synth.SPATIAL_DISTANCE, synth.SEED_MODEL)

@@ -14,6 +14,7 @@ def main():
     ap.add_argument("--grid", action="store_true")
     ap.add_argument("--filter", default="")
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--timeline", type=int, default=0, help="also print the last N dispatches: start gap, duration")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     names = {r[0]: r[1] for r in c.execute("select id, display_name from rocpd_info_kernel_symbol")}
@@ -25,6 +26,12 @@ def main():
             key = f"[grid {gx}/{wx}] {key}"
         if a.filter in key:
             agg[key].append(e - s)
+    if a.timeline:
+        prev = None
+        for kid, s, e, gx, wx in sorted(rows, key=lambda r: r[1])[-a.timeline:]:
+            gap = (s - prev) / 1e3 if prev is not None else 0.0
+            print(f"gap {gap:8.2f} us  dur {(e - s) / 1e3:8.2f} us  grid {gx}/{wx}  {names.get(kid, kid)[:70]}")
+            prev = e
     total = sum(sum(v) for v in agg.values())
     print(f"{'kernel':90s} {'calls':>6s} {'avg_us':>9s} {'total_us':>10s} {'%':>5s}")
     for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1]))[:a.top]:
