@@ -174,7 +174,7 @@ __device__ static void set_component(int k, const double* mean, const double* co
 
 // Packed E-step and guide records of component k (k < Kp; k >= K is padding).
 // weights == false: every field but the weight ones (EP_PI, EP_DIPI, GP_W:
-// pack_weights writes them once the weights are final).
+// mstep_spread_kernel's finish writes them once the weights are final).
 __device__ static void pack_component(int k, int K, int Kp, const CanonDev& C, float* ep, float* gp,
                                       float norm5, bool weights = true) {
     float e[EP_FIELDS];
@@ -233,18 +233,6 @@ __device__ static void pack_component(int k, int K, int Kp, const CanonDev& C, f
         if (weights || (f != EP_PI && f != EP_DIPI)) ep[f * Kp + k] = e[f];
     for (int f = 0; f < GP_FIELDS; ++f)
         if (weights || f != GP_W) gp[k * GP_STRIDE + f] = g[f];
-}
-// The weight fields of record k, as pack_component forms them.
-__device__ static void pack_weights(int k, int K, int Kp, const CanonDev& C, float* ep, float* gp) {
-    float pi = 0.0f, dipi = 0.0f, w = 0.0f;
-    if (k < K) {
-        w = C.weights[k];
-        pi = C.valid[k] ? w : 0.0f;
-        dipi = ep[EP_DI * Kp + k] * pi;
-    }
-    ep[EP_PI * Kp + k] = pi;
-    ep[EP_DIPI * Kp + k] = dipi;
-    gp[k * GP_STRIDE + GP_W] = w;
 }
 
 // createCdf(false) then configure()'s createCdf(true) (float, sequential);
@@ -429,7 +417,8 @@ __device__ __forceinline__ void mstep_scalars(const double* __restrict__ stats, 
 struct CompIn {
     double st[ST_FIELDS];   // W, M0..M4, Clow (the compact order)
     double T, sgW, sgM[5], sgC[25], ni;
-    float bP[25], bD[9], to[9], w;
+    float bP[25], bD[9], to[9], w, di;
+    int valid;
     bool decp;
 };
 __device__ __forceinline__ void load_comp_in(int k, int K, const double* __restrict__ stats, const CanonDev& C,
@@ -447,6 +436,8 @@ __device__ __forceinline__ void load_comp_in(int k, int K, const double* __restr
     for (int i = 0; i < 9; ++i) in.bD[i] = S.bDepth[9 * k + i];
     for (int i = 0; i < 9; ++i) in.to[i] = C.to[9 * k + i];
     in.w = C.weights[k];
+    in.di = C.detInv[k];
+    in.valid = C.valid[k];
 }
 
 // wm, wc: component k's accepted (mean, cov) slots; L5 / Li5 / have (or
@@ -680,13 +671,18 @@ mstep_batched_kernel(int K, int Kp, const MixDesc* __restrict__ mixes, float nor
 // but the weight ones, all in one thread (nothing goes through memory).  The
 // workgroup whose blends complete last (device-scope counter count[0]) runs
 // the order-dependent finish on its wave 1 while its wave 0 sets: the weights
-// normalised, both CDF prefixes, the scalars.  The last of the nb set waves
-// and the finish to complete (count[1]) writes every record's weight fields
-// and re-arms both counters.  The operations are mstep_body's, so the
-// results are bitwise those of the batched per-leaf form.
+// normalised, both CDF prefixes, the scalars, and every record's weight
+// fields -- from the valid flag and detInv each blend publishes beside its
+// weight (what its set will leave) -- then re-arms the counter.  The
+// operations are mstep_body's, so the results are bitwise those of the
+// batched per-leaf form.
 __global__ void __launch_bounds__(128)
 mstep_spread_kernel(int K, int Kp, const double* __restrict__ stats, int64_t nSamples, CanonDev C, EmStateDev S,
-                    float* ep, float* gp, float norm5, double* newW, unsigned* count) {
+                    float* ep, float* gp, float norm5, double* scratch, unsigned* count) {
+    // scratch: newW (K doubles), the valid flags and detInv after the set
+    double* newW = scratch;
+    float* dinew = (float*)(scratch + K);
+    int* vnew = (int*)(scratch + 2 * K);
     __shared__ double sh[8];
     __shared__ double upd[3];
     __shared__ double sh2[2];
@@ -705,18 +701,45 @@ mstep_spread_kernel(int K, int Kp, const double* __restrict__ stats, int64_t nSa
         if (blockIdx.x == 0 && t == 0) S.scalars[SC_STATUS] = 0.0;
         return;
     }
+    // SDMM_MSTEP_STOP=n (diagnostic builds): return after stage n -- 1 the
+    // loads + scalars, 2 the blends, 3 the first counter, 4 set / finish,
+    // 5 the records -- for a breakdown by subtraction (not results)
+    if (SDMM_MSTEP_STOP <= 1) return;
     __shared__ int setk[512];
     double emb[6], cov[25], L[25], Li[25];
     bool have = false;
     if (wv == 0) {
-        if (k < K) mstep_component(k, K, in, S, sh, newW, setk, emb, cov, L, Li, &have);
+        if (k < K) {
+            mstep_component(k, K, in, S, sh, newW, setk, emb, cov, L, Li, &have);
+            // the valid flag and detInv the set below leaves (set_component:
+            // 1 / det of the Cholesky when it succeeds, else unchanged), so
+            // that the finish can form the weight fields without waiting
+            int v = in.valid;
+            float di = in.di;
+            if (setk[k]) {
+                v = have ? 1 : 0;
+                if (have) {
+                    double det = 1.0;
+                    for (int i = 0; i < 5; ++i) det *= L[6 * i];
+                    di = (float)(1.0 / det);
+                }
+            }
+            vnew[k] = v;
+            dinew[k] = di;
+        }
+        if (SDMM_MSTEP_STOP <= 2) return;
         __threadfence();
         if (lane == 0) role = (atomicAdd(&count[0], 1u) == nb - 1) ? 1 : 0;
     }
+    if (SDMM_MSTEP_STOP <= 2) return;
     __syncthreads();
+    if (SDMM_MSTEP_STOP <= 5 && role && t == 0) count[0] = 0u;   // (diagnostic builds)
+    if (SDMM_MSTEP_STOP <= 3) return;
     if (wv == 0) {
         if (k < K && setk[k]) set_component(k, emb, cov, C, have ? 1 : 0, L, Li);
+        if (SDMM_MSTEP_STOP <= 4) return;
         if (k < Kp) pack_component(k, K, Kp, C, ep, gp, norm5, false);
+        if (SDMM_MSTEP_STOP <= 5) return;
     } else {
         if (!role) return;
         __threadfence();
@@ -727,25 +750,28 @@ mstep_spread_kernel(int K, int Kp, const double* __restrict__ stats, int64_t nSa
         };
         wave_sync();
         mstep_finish(K, S, nwl, wl, cl, sh2, lane, 64, wave_sync);
+        if (SDMM_MSTEP_STOP <= 4) return;
         wave_sync();
         for (int i = lane; i < K; i += 64) {
             C.weights[i] = wl[i];
             C.cdf[i] = cl[i];
         }
         if (lane == 0) mstep_scalars_store(S, sh, upd);
-    }
-    // the last of the nb set waves and the finish writes the weight fields
-    __threadfence();
-    __shared__ int fin[2];   // per wave
-    if (lane == 0) fin[wv] = (atomicAdd(&count[1], 1u) == nb) ? 1 : 0;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    if (!fin[wv]) return;
-    __threadfence();
-    for (int i = lane; i < Kp; i += 64) pack_weights(i, K, Kp, C, ep, gp);
-    if (lane == 0) {
-        count[0] = 0u;
-        count[1] = 0u;
+        if (SDMM_MSTEP_STOP <= 5) return;
+        // every record's weight fields (pack_component's, from the valid
+        // flags and detInv the blends published), and the counter re-armed
+        for (int i = lane; i < Kp; i += 64) {
+            float pi = 0.0f, dipi = 0.0f, w = 0.0f;
+            if (i < K) {
+                w = wl[i];
+                pi = vnew[i] ? w : 0.0f;
+                dipi = dinew[i] * pi;
+            }
+            ep[EP_PI * Kp + i] = pi;
+            ep[EP_DIPI * Kp + i] = dipi;
+            gp[i * GP_STRIDE + GP_W] = w;
+        }
+        if (lane == 0) count[0] = 0u;
     }
 }
 
@@ -1037,8 +1063,7 @@ hipError_t launch_pack_all(int K, int Kp, const CanonDev& C, float* ep, float* g
     return hipGetLastError();
 }
 
-// newW: K doubles of scratch; count: two zeroed counters (re-armed by the
-// kernel itself).
+// scratch: 3K doubles; count: a zeroed counter (re-armed by the kernel).
 hipError_t launch_mstep(int K, int Kp, const double* stats, int64_t nSamples, const CanonDev& C,
                         const EmStateDev& S, float* ep, float* gp, float norm5, double* newW, unsigned* count,
                         hipStream_t st) {
