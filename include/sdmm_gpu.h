@@ -561,7 +561,10 @@ typedef struct {
      * sAvg / (dAvg + sAvg) (plastic.cpp:188-196).  A plastic bounce queries
      * the guide like any BSDF with a smooth lobe; a delta lobe chosen by the
      * BSDF sample returns weight / h with pdf * h and saves no vertex
-     * (sdmm_proc.cpp:297, :383-409, :764). */
+     * (sdmm_proc.cpp:297, :383-409, :764).  Kind 2, rough conductor
+     * (bsdfs/roughconductor.cpp; `reflectance` unused): [1..3]
+     * specularReflectance, [4] eta, [5] k (a gray conductor), [6] the
+     * Beckmann alpha (isotropic, sampleVisible = false), [7] unused. */
     const float* bsdf_params;
 } sdmm_scene_desc;
 /* The descriptor has grown across ABI revisions (bsdf_params was appended):
@@ -579,10 +582,15 @@ typedef struct {
     int64_t pixel_begin, pixel_end;
     /* sampleProduct (volpath_sdmm.cpp:60, sdmm_proc.cpp:327-392): guided
      * bounces sample the product of the leaf's conditional with the hit
-     * material's learned BSDF (learned_bsdf row = the quad's bsdf index; every
-     * BSDF here is diffuse: set diffuse[b], the plugin's slice-0 rule) through
+     * material's learned BSDF (learned_bsdf row = the quad's bsdf index; for
+     * a diffuse BSDF set diffuse[b], the plugin's slice-0 rule) through
      * sdmm_guide_product_wavefront, with h = 0.3 (0.5 when the product is
-     * unusable) and the BSDF/guide choice taken against that h.  0: the plain
+     * unusable) and the BSDF/guide choice taken against that h.  A rough
+     * conductor's row is not read: each bounce forms its own lobes (getDMM
+     * conditioned on theta_i and alpha -- a synthetic 4-lobe stand-in for the
+     * suite's learned files, render.hip glossy_lobes -- then rotate_to_wo(wi)
+     * and the shading frame to world, sdmm_proc.cpp:340-355); the component
+     * index is then k * max(M, 4) + j.  0: the plain
      * conditional with bsdf_fraction.  (bsdfOnly never trains, :416, so it
      * is the guided = 0 render; its learned-BSDF branch, :331/:384/:410, is
      * unreachable in the reference.) */

@@ -55,15 +55,6 @@ __device__ __forceinline__ float gp_ld(const float* gp, int Kp, int f, int k) {
 // (2 (126 ln 2 + ln NORM3) = 169.16, with margin)
 constexpr float kMarginalZeroQ = 170.0f;
 
-__device__ __forceinline__ void coordinates_f(const float n[3], float to[9]) {
-    float sign = copysignf(1.0f, n[2]);
-    const float a = -1.0f / (sign + n[2]);
-    const float b = n[0] * n[1] * a;
-    to[0] = 1.0f + sign * n[0] * n[0] * a; to[1] = sign * b; to[2] = -sign * n[0];
-    to[3] = b; to[4] = sign + n[1] * n[1] * a; to[5] = -n[1];
-    to[6] = n[0]; to[7] = n[1]; to[8] = n[2];
-}
-
 __device__ __forceinline__ float sinc_pi_f(float x) {
     const float taylor_0_bound = 1.1920928955078125e-07f;
     const float taylor_2_bound = 3.4526698300124393e-04f;  // sqrtf(eps)

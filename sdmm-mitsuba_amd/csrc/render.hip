@@ -128,6 +128,160 @@ __device__ __forceinline__ float plastic_prob_specular(float Fi, float ssw) {
     return den == 0.0f ? 0.0f : num / den;
 }
 
+// ---------------------------------------------------------------------------
+// Rough conductor (bsdfs/roughconductor.cpp:296-470 over microfacet.h): the
+// Beckmann distribution with isotropic alpha, sampleVisible = false (sampleAll
+// / pdfAll, microfacet.h:287-407 -- a documented choice of the plugin), a gray
+// conductor (eta, k equal over the channels; fresnelConductorExact's Spectrum
+// form, libcore/util.cpp:739-761) times the specular reflectance.  exp / log /
+// sin / cos as (float)f((double)x): math::fastexp / fastlog on Linux x86_64
+// (math.h:185-197) and the library's sincos convention.
+constexpr float kPiF = 3.14159265358979323846f;
+
+__device__ __forceinline__ float fresnel_conductor(float ci, float eta, float k) {
+    const float ci2 = ci * ci, si2 = 1.0f - ci2, si4 = si2 * si2;
+    const float t1 = eta * eta - k * k - si2;
+    const float a2pb2 = sqrtf(fmaxf(0.0f, t1 * t1 + k * k * eta * eta * 4.0f));
+    const float a = sqrtf(fmaxf(0.0f, (a2pb2 + t1) * 0.5f));
+    const float term1 = a2pb2 + ci2, term2 = a * (2.0f * ci);
+    const float rs2 = (term1 - term2) / (term1 + term2);
+    const float term3 = a2pb2 * ci2 + si4, term4 = term2 * si2;
+    const float rp2 = rs2 * (term3 - term4) / (term3 + term4);
+    return 0.5f * (rp2 + rs2);
+}
+
+// MicrofacetDistribution::eval (microfacet.h:191-233), Beckmann
+__device__ __forceinline__ float beckmann_d(const float m[3], float alpha) {
+    if (m[2] <= 0.0f) return 0.0f;
+    const float ct2 = m[2] * m[2];
+    const float ex = ((m[0] * m[0]) / (alpha * alpha) + (m[1] * m[1]) / (alpha * alpha)) / ct2;
+    float r = (float)exp((double)-ex) / (kPiF * alpha * alpha * ct2 * ct2);
+    if (r * m[2] < 1e-20f) r = 0.0f;
+    return r;
+}
+
+// smithG1 (microfacet.h:477-518), Beckmann's rational approximation
+__device__ __forceinline__ float beckmann_g1(const float v[3], const float m[3], float alpha) {
+    if (dot3(v, m) * v[2] <= 0.0f) return 0.0f;
+    const float tmp = 1.0f - v[2] * v[2];
+    const float tan_t = tmp <= 0.0f ? 0.0f : fabsf(sqrtf(tmp) / v[2]);
+    if (tan_t == 0.0f) return 1.0f;
+    const float a = 1.0f / (alpha * tan_t);
+    if (a >= 1.6f) return 1.0f;
+    const float a2 = a * a;
+    return (3.535f * a + 2.181f * a2) / (1.0f + 2.276f * a + 2.577f * a2);
+}
+
+// Vector3 normalize (v * (1 / |v|), vector.h:625-627)
+__device__ __forceinline__ void normalize3(const float v[3], float r[3]) {
+    const float rc = 1.0f / sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    r[0] = v[0] * rc; r[1] = v[1] * rc; r[2] = v[2] * rc;
+}
+
+// RoughConductor::sample(bRec, pdf, sample) (roughconductor.cpp:414-462) in the
+// local frame, wi.z > 0: wo, the weight F * (D G (wi.m) / (pdf cos)) and the
+// solid-angle pdf; false: the sample is void (weight 0)
+__device__ __forceinline__ bool conductor_sample(const float wi[3], const float* bp, float u0, float u1,
+                                                 float wo[3], float bw[3], float* pdf) {
+    const float alpha = bp[6];
+    // sampleAll (microfacet.h:287-395), isotropic Beckmann
+    const float phi = (2.0f * kPiF) * u1;
+    double sd, cd;
+    sincos((double)phi, &sd, &cd);
+    const float sp = (float)sd, cp = (float)cd;
+    const float a2 = alpha * alpha;
+    const float tan2 = a2 * -(float)log((double)(1.0f - u0));
+    const float ct = 1.0f / sqrtf(1.0f + tan2);
+    float mpdf = (1.0f - u0) / (kPiF * alpha * alpha * ct * ct * ct);
+    if (mpdf < 1e-20f) mpdf = 0.0f;
+    const float st = sqrtf(fmaxf(0.0f, 1.0f - ct * ct));
+    const float m[3] = {st * cp, st * sp, ct};
+    *pdf = 0.0f;
+    bw[0] = bw[1] = bw[2] = 0.0f;
+    wo[0] = 0.0f; wo[1] = 0.0f; wo[2] = 1.0f;
+    if (mpdf == 0.0f) return false;
+    const float dm = dot3(wi, m);
+    for (int a = 0; a < 3; ++a) wo[a] = 2.0f * dm * m[a] - wi[a];   // reflect
+    if (wo[2] <= 0.0f) return false;
+    const float fr = fresnel_conductor(dm, bp[4], bp[5]);
+    const float g = beckmann_g1(wi, m, alpha) * beckmann_g1(wo, m, alpha);
+    const float weight = beckmann_d(m, alpha) * g * dm / (mpdf * wi[2]);
+    for (int ch = 0; ch < 3; ++ch) bw[ch] = fr * bp[1 + ch] * weight;
+    *pdf = mpdf / (4.0f * dot3(wo, m));
+    return true;
+}
+
+// RoughConductor::eval (ESolidAngle, :302-339) and pdf (:341-366) in the local
+// frame
+__device__ __forceinline__ float conductor_eval_pdf(const float wi[3], const float wo[3], const float* bp,
+                                                    float f[3]) {
+    f[0] = f[1] = f[2] = 0.0f;
+    if (wi[2] <= 0.0f || wo[2] <= 0.0f) return 0.0f;
+    const float alpha = bp[6];
+    const float hs[3] = {wo[0] + wi[0], wo[1] + wi[1], wo[2] + wi[2]};
+    float H[3];
+    normalize3(hs, H);
+    const float D = beckmann_d(H, alpha);
+    if (D != 0.0f) {
+        const float fr = fresnel_conductor(dot3(wi, H), bp[4], bp[5]);
+        const float G = beckmann_g1(wi, H, alpha) * beckmann_g1(wo, H, alpha);
+        const float model = D * G / (4.0f * wi[2]);
+        for (int ch = 0; ch < 3; ++ch) f[ch] = fr * bp[1 + ch] * model;
+    }
+    return D * H[2] / (4.0f * fabsf(dot3(wo, H)));
+}
+
+// The conductor's learned BSDF (RoughConductor::getDMM, roughconductor.cpp:
+// 182-196: the material's SDMM4 conditioned on (theta_i, alpha), sdmm-lib's
+// create_conditional_pruned) -- the suite's learned files are LFS pointers,
+// so a synthetic 4-lobe fit stands in: lobes in the canonical frame where wi
+// lies at azimuth 0, means at elevation theta_j on the mirror side (azimuth
+// pi), diagonal 2x2 covariances in each lobe's Coordinates(mean) frame:
+//   j   weight  theta_j                  sigma_1                  sigma_2
+//   0   0.55    theta                    1.5 alpha (1 + sin/2)    1.5 alpha
+//   1   0.20    0.6 theta                2.5 alpha                2.5 alpha
+//   2   0.15    min(theta + 0.35, 1.45)  3 alpha                  2 alpha
+//   3   0.10    0 (the normal)           0.5                      0.5
+// then sdmm_proc.cpp:340-355's rotate_to_wo(wi): the lobes rotated about the
+// normal onto wi's azimuth, each covariance re-expressed in the rotated mean's
+// Coordinates frame (the product kernels' convention, sdmm_bsdf_table).
+// Output: kGlossyLobes rows (weights, local means, covariances).
+__device__ __forceinline__ void glossy_lobes(const float wi[3], float alpha, float* w, float* mean, float* cov) {
+    const float theta = (float)acos((double)fminf(1.0f, wi[2]));
+    const float sth = (float)sin((double)theta);
+    const float th[kGlossyLobes] = {theta, 0.6f * theta, fminf(theta + 0.35f, 1.45f), 0.0f};
+    const float s1[kGlossyLobes] = {1.5f * alpha * (1.0f + 0.5f * sth), 2.5f * alpha, 3.0f * alpha, 0.5f};
+    const float s2[kGlossyLobes] = {1.5f * alpha, 2.5f * alpha, 2.0f * alpha, 0.5f};
+    const float wt[kGlossyLobes] = {0.55f, 0.2f, 0.15f, 0.1f};
+    // rotate_to_wo: R = Rz(phi_i), cos / sin from wi's azimuth (1, 0 at the pole)
+    const float sp2 = wi[0] * wi[0] + wi[1] * wi[1];
+    float c = 1.0f, s = 0.0f;
+    if (sp2 > 0.0f) {
+        const float rs = 1.0f / sqrtf(sp2);
+        c = wi[0] * rs;
+        s = wi[1] * rs;
+    }
+    for (int j = 0; j < kGlossyLobes; ++j) {
+        const float mc[3] = {-(float)sin((double)th[j]), 0.0f, (float)cos((double)th[j])};
+        float tc[9], tr[9];
+        coordinates_f(mc, tc);
+        const float m[3] = {c * mc[0] - s * mc[1], s * mc[0] + c * mc[1], mc[2]};
+        coordinates_f(m, tr);
+        // the canonical tangent axes rotated: R t1, R t2
+        const float r1[3] = {c * tc[0] - s * tc[1], s * tc[0] + c * tc[1], tc[2]};
+        const float r2[3] = {c * tc[3] - s * tc[4], s * tc[3] + c * tc[4], tc[5]};
+        // B = [f_i . (R t_j)], cov = B diag(s1^2, s2^2) B^T
+        const float b00 = dot3(tr, r1), b01 = dot3(tr, r2), b10 = dot3(tr + 3, r1), b11 = dot3(tr + 3, r2);
+        const float va = s1[j] * s1[j], vb = s2[j] * s2[j];
+        const float c00 = b00 * b00 * va + b01 * b01 * vb;
+        const float c01 = b00 * b10 * va + b01 * b11 * vb;
+        const float c11 = b10 * b10 * va + b11 * b11 * vb;
+        w[j] = wt[j];
+        mean[3 * j] = m[0]; mean[3 * j + 1] = m[1]; mean[3 * j + 2] = m[2];
+        cov[4 * j] = c00; cov[4 * j + 1] = c01; cov[4 * j + 2] = c01; cov[4 * j + 3] = c11;
+    }
+}
+
 __device__ __forceinline__ float& vrec(const PathsDev& P, int f, int v, int64_t p) {
     return P.rec[((int64_t)f * P.V + v) * P.P + p];
 }
@@ -204,10 +358,12 @@ li_query_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, i
         wi[0] = -P.dx[i]; wi[1] = -P.dy[i]; wi[2] = -P.dz[i];
         const float* rho = S.refl + 3 * QD.bsdf;
         const float* bp = S.bpar ? S.bpar + kBsdfParams * QD.bsdf : nullptr;
-        const bool zero_spec = !bp || bp[0] != (float)kBsdfPlastic || (bp[1] == 0.0f && bp[2] == 0.0f && bp[3] == 0.0f);
+        const int kind = bp ? (int)bp[0] : kBsdfDiffuse;
+        const bool zero_spec = kind == kBsdfDiffuse || (bp[1] == 0.0f && bp[2] == 0.0f && bp[3] == 0.0f);
+        const bool zero_diff = kind == kBsdfConductor || (rho[0] == 0.0f && rho[1] == 0.0f && rho[2] == 0.0f);
         // no reflection from the back side or with zero reflectances (the
         // light's BSDF): sample and eval are 0, the path ends (:772-774)
-        if (!(dot3(wi, n) > 0.0f) || (rho[0] == 0.0f && rho[1] == 0.0f && rho[2] == 0.0f && zero_spec)) live = false;
+        if (!(dot3(wi, n) > 0.0f) || (zero_diff && zero_spec)) live = false;
     }
     Q.live[i] = (uint8_t)((live && guided) ? 1 : 0);
     Q.slot[i] = -1;
@@ -253,6 +409,14 @@ li_query_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, i
             Q.bw2[i] = rho[2] * rd * k;
             Q.bpdf[i] = (1.0f - ps) * (kInvPi * w[2]);
         }
+    } else if (bp && bp[0] == (float)kBsdfConductor) {
+        // RoughConductor::sample (roughconductor.cpp:414-462); a void sample
+        // has weight 0 (the path ends if the BSDF direction is taken)
+        const float wl[3] = {dot3(wi, s), dot3(wi, t), dot3(wi, n)};
+        float bw[3], bpdf;
+        conductor_sample(wl, bp, rng_uniform(seed, gp, stream, 0), rng_uniform(seed, gp, stream, 1), w, bw, &bpdf);
+        Q.bw0[i] = bw[0]; Q.bw1[i] = bw[1]; Q.bw2[i] = bw[2];
+        Q.bpdf[i] = bpdf;
     } else {
         cosine_hemisphere(rng_uniform(seed, gp, stream, 0), rng_uniform(seed, gp, stream, 1), w);
     }
@@ -294,6 +458,17 @@ li_compact_kernel(SceneDev S, PathsDev P, QueryDev Q, const int32_t* __restrict_
         }
         Q.k_mat[j] = QD.bsdf;
         Q.k_ch[j] = Q.ch[i];
+        const float* bp = S.bpar ? S.bpar + kBsdfParams * QD.bsdf : nullptr;
+        if (Q.lw && bp && bp[0] == (float)kBsdfConductor) {
+            // getDMM + rotate_to_wo (sdmm_proc.cpp:327-355): the query's own
+            // lobes, local frame, in its row of the extended table
+            const float wi[3] = {-P.dx[i], -P.dy[i], -P.dz[i]};
+            const float wl[3] = {dot3(wi, s), dot3(wi, t), dot3(wi, QD.n)};
+            const int64_t row = (int64_t)Q.lrow0 + j;
+            glossy_lobes(wl, bp[6], Q.lw + row * Q.lM, Q.lm + row * Q.lM * 3, Q.lc + row * Q.lM * 4);
+            for (int l = kGlossyLobes; l < Q.lM; ++l) Q.lw[row * Q.lM + l] = 0.0f;   // (skipped lobes)
+            Q.k_mat[j] = (int32_t)row;
+        }
     }
 }
 
@@ -365,6 +540,33 @@ li_shade_kernel(SceneDev S, PathsDev P, QueryDev Q, int64_t path0, int bounce, i
                 const float f = up ? S.refl[3 * QD.bsdf + ch] * rd * k : 0.0f;
                 weight[ch] = mis_pdf == 0.0f ? 0.0f : f * (1.0f / mis_pdf);
             }
+        }
+    } else if (bp && bp[0] == (float)kBsdfConductor) {
+        // rough conductor: the loop head's sample (weight, pdf) or the guide's
+        // direction under eval / pdf (:392-407, :456-507)
+        const float bw[3] = {Q.bw0[i], Q.bw1[i], Q.bw2[i]};
+        if (!valid || comp == -2) {
+            wo[0] = Q.b0[i]; wo[1] = Q.b1[i]; wo[2] = Q.b2[i];
+            const float bsdf_pdf = Q.bpdf[i];
+            if (!valid) {
+                mis_pdf = bsdf_pdf;
+                for (int ch = 0; ch < 3; ++ch) weight[ch] = bw[ch];
+            } else {
+                mis_pdf = bsdf_pdf > 0.0f ? h * bsdf_pdf + (1.0f - h) * Q.pdf[j] : 0.0f;
+                for (int ch = 0; ch < 3; ++ch) weight[ch] = mis_pdf == 0.0f ? 0.0f : (bw[ch] * bsdf_pdf) * (1.0f / mis_pdf);
+            }
+        } else {
+            wo[0] = Q.d0[j]; wo[1] = Q.d1[j]; wo[2] = Q.d2[j];
+            float s[3], t[3];
+            frame_of(n, s, t);
+            const float wi[3] = {-P.dx[i], -P.dy[i], -P.dz[i]};
+            const float wil[3] = {dot3(wi, s), dot3(wi, t), dot3(wi, n)};
+            const float wol[3] = {dot3(wo, s), dot3(wo, t), dot3(wo, n)};
+            const bool zero = (wo[0] == 0.0f && wo[1] == 0.0f && wo[2] == 0.0f) || !__builtin_isfinite(wol[2]);
+            float f[3] = {0.0f, 0.0f, 0.0f};
+            const float bsdf_pdf = zero ? 0.0f : conductor_eval_pdf(wil, wol, bp, f);
+            mis_pdf = bsdf_pdf > 0.0f ? h * bsdf_pdf + (1.0f - h) * Q.pdf[j] : 0.0f;
+            for (int ch = 0; ch < 3; ++ch) weight[ch] = mis_pdf == 0.0f ? 0.0f : f[ch] * (1.0f / mis_pdf);
         }
     } else if (!valid) {
         // BSDF only, h = 1 (:316-323, :392-405): weight = rho, pdf = bsdfPdf

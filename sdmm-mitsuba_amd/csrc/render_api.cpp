@@ -63,6 +63,12 @@ struct sdmm_scene {
     int hfb_cap = 0;
     void* temp = nullptr;
     size_t temp_bytes = 0;
+    // rough conductors with product sampling: the extended learned-BSDF
+    // table -- the caller's B rows re-strided to lM >= kGlossyLobes lobes, then
+    // one row per compact query for the conductor's per-bounce lobes
+    bool has_conductor = false;
+    void* lt = nullptr;
+    size_t lt_bytes = 0;
 };
 
 namespace {
@@ -140,6 +146,50 @@ int grow(sdmm_scene* s, int64_t P, int V, hipStream_t st) {
     return SDMM_OK;
 }
 
+// The extended learned-BSDF table of a render with rough conductors: rows
+// 0 .. B-1 the caller's (device arrays, re-strided to lM = max(M,
+// kGlossyLobes) lobes, the extra lobes weight 0 -- skipped by the product),
+// rows B .. B + cap - 1 the compact queries' own conductor lobes (written by
+// li_compact_kernel).  *tab describes it; s->Q points at the query rows.
+int extend_learned(sdmm_scene* s, const sdmm_bsdf_table& user, int64_t cap, hipStream_t st, sdmm_bsdf_table* tab) {
+    const int M = user.M, lM = std::max(M, kGlossyLobes), B = user.B;
+    const int64_t rows = (int64_t)B + cap;
+    auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+    const size_t wb = al(sizeof(float) * (size_t)rows * lM), mb = 3 * wb, cb = 4 * wb, db = al((size_t)rows);
+    const size_t need = wb + mb + cb + db;
+    if (need > s->lt_bytes) {
+        HIP_TRY(hipStreamSynchronize(st));
+        if (s->lt) HIP_TRY(hipFree(s->lt));
+        s->lt = nullptr;
+        s->lt_bytes = 0;
+        HIP_TRY(hipMalloc(&s->lt, need));
+        s->lt_bytes = need;
+    }
+    char* b = (char*)s->lt;
+    float* w = (float*)b;
+    float* m = (float*)(b + wb);
+    float* c = (float*)(b + wb + mb);
+    uint8_t* dflag = (uint8_t*)(b + wb + mb + cb);
+    HIP_TRY(hipMemsetAsync(w, 0, sizeof(float) * (size_t)B * lM, st));
+    HIP_TRY(hipMemcpy2DAsync(w, sizeof(float) * lM, user.weights, sizeof(float) * M, sizeof(float) * M, B,
+                             hipMemcpyDeviceToDevice, st));
+    HIP_TRY(hipMemsetAsync(m, 0, sizeof(float) * 3 * (size_t)B * lM, st));
+    HIP_TRY(hipMemcpy2DAsync(m, sizeof(float) * 3 * lM, user.means, sizeof(float) * 3 * M, sizeof(float) * 3 * M, B,
+                             hipMemcpyDeviceToDevice, st));
+    HIP_TRY(hipMemsetAsync(c, 0, sizeof(float) * 4 * (size_t)B * lM, st));
+    HIP_TRY(hipMemcpy2DAsync(c, sizeof(float) * 4 * lM, user.covs, sizeof(float) * 4 * M, sizeof(float) * 4 * M, B,
+                             hipMemcpyDeviceToDevice, st));
+    HIP_TRY(hipMemsetAsync(dflag, 0, (size_t)rows, st));
+    if (user.diffuse) HIP_TRY(hipMemcpyAsync(dflag, user.diffuse, (size_t)B, hipMemcpyDeviceToDevice, st));
+    *tab = sdmm_bsdf_table{w, m, c, (int)std::min<int64_t>(rows, INT32_MAX), lM, dflag};
+    s->Q.lw = w;
+    s->Q.lm = m;
+    s->Q.lc = c;
+    s->Q.lrow0 = B;
+    s->Q.lM = lM;
+    return SDMM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -155,7 +205,10 @@ int sdmm_scene_create(const sdmm_scene_desc* d, int device, sdmm_scene** out) {
             const float* bp = d->bsdf_params + kBsdfParams * b;
             const bool ok = bp[0] == (float)kBsdfDiffuse ||
                             (bp[0] == (float)kBsdfPlastic && bp[4] > 0.0f && bp[5] > 0.0f && bp[6] < 1.0f &&
-                             bp[7] >= 0.0f && bp[7] <= 1.0f);
+                             bp[7] >= 0.0f && bp[7] <= 1.0f) ||
+                            (bp[0] == (float)kBsdfConductor && bp[1] >= 0.0f && bp[2] >= 0.0f && bp[3] >= 0.0f &&
+                             std::isfinite(bp[1] + bp[2] + bp[3]) && bp[4] > 0.0f && std::isfinite(bp[4]) &&
+                             bp[5] >= 0.0f && std::isfinite(bp[5]) && bp[6] > 0.0f && bp[6] <= 2.0f);
             if (!ok) return fail(SDMM_E_INVALID, "sdmm_scene_create: invalid bsdf_params");
         }
     *out = nullptr;
@@ -192,6 +245,10 @@ int sdmm_scene_create(const sdmm_scene_desc* d, int device, sdmm_scene** out) {
     sdmm_scene* s = new (std::nothrow) sdmm_scene();
     if (!s) return fail(SDMM_E_NOMEM, "out of host memory");
     s->device = device;
+    // (a conductor some quad uses: the CPU restatement's rule)
+    if (d->bsdf_params)
+        for (int q = 0; q < d->n_quads; ++q)
+            if (d->bsdf_params[kBsdfParams * d->bsdf[q]] == (float)kBsdfConductor) s->has_conductor = true;
     // render() (volpath_sdmm.cpp:375-393): spatialNormalization = the largest
     // extent; the tree box getAABB (:314-332)
     float ext[3], norm = 0.0f;
@@ -248,6 +305,7 @@ void sdmm_scene_destroy(sdmm_scene* s) {
     if (s->dbpar) (void)hipFree(s->dbpar);
     if (s->drad) (void)hipFree(s->drad);
     if (s->buf) (void)hipFree(s->buf);
+    if (s->lt) (void)hipFree(s->lt);
     if (s->hcount) (void)hipHostFree(s->hcount);
     if (s->hfb) (void)hipHostFree(s->hfb);
     delete s;
@@ -294,6 +352,12 @@ int sdmm_li_render(sdmm_scene* s, sdmm_stree* t, const sdmm_mix* const* node_mix
     if (r) return r;
     s->P.V = V;
     s->P.P = P;
+    sdmm_bsdf_table ltab{};
+    s->Q.lw = s->Q.lm = s->Q.lc = nullptr;
+    if (product && p->guided && s->has_conductor) {
+        r = extend_learned(s, p->learned_bsdf, s->cap_paths, st, &ltab);
+        if (r) return r;
+    }
     const int64_t path0 = p->pixel_begin * p->spp;
     HIP_TRY(launch_li_camera(s->S, s->P, path0, p->spp, p->seed, st));
     // bounces: rRec.depth 1 .. maxDepth - 1 scatter (:649, :684); unbounded
@@ -333,8 +397,9 @@ int sdmm_li_render(sdmm_scene* s, sdmm_stree* t, const sdmm_mix* const* node_mix
                     // guide choice taken against the query's own h
                     const float* F[9];
                     for (int i = 0; i < 9; ++i) F[i] = s->Q.k_F[i];
-                    r = sdmm_guide_product_wavefront(t, node_mix, nlive, c, u, s->Q.k_ch, bd, &p->learned_bsdf,
-                                                     s->Q.k_mat, F, d, s->Q.pdf, s->Q.comp, s->Q.hq, nullptr);
+                    r = sdmm_guide_product_wavefront(t, node_mix, nlive, c, u, s->Q.k_ch, bd,
+                                                     s->Q.lw ? &ltab : &p->learned_bsdf, s->Q.k_mat, F, d,
+                                                     s->Q.pdf, s->Q.comp, s->Q.hq, nullptr);
                 } else {
                     r = sdmm_guide_pdf_wavefront(t, node_mix, nlive, c, u, bd, s->Q.k_mode, d, s->Q.pdf,
                                                  s->Q.comp, nullptr);

@@ -32,13 +32,18 @@ struct QuadDev {
 };
 
 // Per-BSDF parameters beside the diffuse reflectance (kBsdfParams floats per
-// BSDF): [0] kind (0 diffuse, 1 smooth plastic), [1..3] specular reflectance,
-// [4] eta = intIOR / extIOR, [5] 1 / eta^2, [6] the internal diffuse Fresnel
-// reflectance fdrInt, [7] the specular sampling weight sAvg / (dAvg + sAvg)
-// (bsdfs/plastic.cpp:159-200)
+// BSDF): [0] kind (0 diffuse, 1 smooth plastic, 2 rough conductor).
+// Plastic: [1..3] specular reflectance, [4] eta = intIOR / extIOR, [5] 1 /
+// eta^2, [6] the internal diffuse Fresnel reflectance fdrInt, [7] the
+// specular sampling weight sAvg / (dAvg + sAvg) (bsdfs/plastic.cpp:159-200).
+// Rough conductor: [1..3] specular reflectance, [4] eta, [5] k (a gray
+// conductor), [6] the Beckmann alpha, [7] unused (bsdfs/roughconductor.cpp).
 constexpr int kBsdfParams = 8;
 constexpr int kBsdfDiffuse = 0;
 constexpr int kBsdfPlastic = 1;
+constexpr int kBsdfConductor = 2;
+// lobes of a rough conductor's (synthetic) learned BSDF (render.hip glossy_lobes)
+constexpr int kGlossyLobes = 4;
 
 struct SceneDev {
     const QuadDev* quads;
@@ -93,6 +98,11 @@ struct QueryDev {
     // sampled lobe delta (1) or smooth (0), its weight (RGB) and pdf
     uint8_t* bdelta;
     float *bw0, *bw1, *bw2, *bpdf;
+    // product with a rough conductor's learned BSDF: compact query j's lobes
+    // (weights, local means, covariances) at row lrow0 + j of the render's
+    // extended learned-BSDF table (lM lobes a row); lw null: no such material
+    float *lw, *lm, *lc;
+    int lrow0, lM;
 };
 
 }  // namespace sdmm

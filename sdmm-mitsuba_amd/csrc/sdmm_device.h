@@ -117,6 +117,18 @@ enum : int {
 // tests/test_gpu_parity.py test_rare_angle_every_lane_slot is the regression).
 __device__ __forceinline__ uint32_t fbits(float x) { return __builtin_bit_cast(uint32_t, x); }
 
+// jmm Coordinates (utils.h:32-48) in float: rows t1, t2, n of the tangent
+// frame of the unit vector n
+__device__ __forceinline__ void coordinates_f(const float n[3], float to[9]) {
+#pragma clang fp contract(off)   // (the header precedes the sources' own pragma)
+    float sign = copysignf(1.0f, n[2]);
+    const float a = -1.0f / (sign + n[2]);
+    const float b = n[0] * n[1] * a;
+    to[0] = 1.0f + sign * n[0] * n[0] * a; to[1] = sign * b; to[2] = -sign * n[0];
+    to[3] = b; to[4] = sign + n[1] * n[1] * a; to[5] = -n[1];
+    to[6] = n[0]; to[7] = n[1]; to[8] = n[2];
+}
+
 struct SamplesDev {
     const float* x[6];
     const float* w;

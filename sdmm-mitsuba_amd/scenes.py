@@ -143,11 +143,21 @@ def plastic_params(diffuse_rgb, specular_rgb=(1.0, 1.0, 1.0), int_ior=1.49, ext_
     return np.array([1.0, *specular_rgb, eta, inv_eta2, fdr_int, ssw], np.float32)
 
 
-def cornell_box(width=640, height=360, plastic=()):
+def conductor_params(specular_rgb=(1.0, 1.0, 1.0), eta=1.2, k=7.0, alpha=0.2):
+    """The 8 bsdf_params floats of a rough conductor (bsdfs/roughconductor.cpp;
+    include/sdmm_gpu.h sdmm_scene_desc): kind 2, specularReflectance, a gray
+    eta / k (default: aluminium-like, |n + ik| of Al over the visible), the
+    isotropic Beckmann alpha (sampleVisible = false)."""
+    return np.array([2.0, *specular_rgb, eta, k, alpha, 0.0], np.float32)
+
+
+def cornell_box(width=640, height=360, plastic=(), conductor=(), alpha=0.2):
     """sdmm_scene_desc fields for the Cornell Box (numpy arrays).  plastic:
     names of BSDFs (e.g. "TallBox", "ShortBox", "Floor") rendered as smooth
     plastic over their diffuse reflectance (a delta specular lobe beside a
-    smooth one, like the Kitchen's `plastic` materials, kitchen.xml)."""
+    smooth one, like the Kitchen's `plastic` materials, kitchen.xml);
+    conductor: names rendered as rough conductors (the Kitchen's glossy
+    `roughconductor` materials) tinted by their reflectance, Beckmann alpha."""
     names = list(_BSDFS)
     quads, bsdf, flip, emitter = [], [], [], []
     for m, name, fl in _RECTS:
@@ -161,14 +171,16 @@ def cornell_box(width=640, height=360, plastic=()):
     bsdf.append(names.index("Light")); flip.append(0); emitter.append(0)
     cam = np.array([float(x) for x in _CAMERA.split()], np.float32)
     extra = {}
-    if plastic:
-        unknown = set(plastic) - set(names)
-        if unknown:
-            raise ValueError(f"unknown BSDFs {sorted(unknown)}")
+    if plastic or conductor:
+        unknown = (set(plastic) | set(conductor)) - set(names)
+        if unknown or set(plastic) & set(conductor):
+            raise ValueError(f"unknown or doubly assigned BSDFs {sorted(unknown | (set(plastic) & set(conductor)))}")
         bp = np.zeros((len(names), 8), np.float32)
         for i, nm in enumerate(names):
             if nm in plastic:
                 bp[i] = plastic_params(_BSDFS[nm])
+            elif nm in conductor:
+                bp[i] = conductor_params(tuple(min(1.0, 1.25 * c) for c in _BSDFS[nm]), alpha=alpha)
         extra["bsdf_params"] = bp.reshape(-1)
     return {**extra,
         "quads": np.asarray(quads, np.float32).reshape(-1),

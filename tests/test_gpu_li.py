@@ -457,3 +457,31 @@ def test_native_guiding_model_async_equals_host_loop(pkg, scenes, gpu, plog):
     se = np.sqrt(a.var() / a.size + u.var() / u.size)
     plog("li_async_guided_vs_unguided_mean_sigma", float(abs(a.mean() - u.mean()) / se), 4.0)
     assert abs(a.mean() - u.mean()) < 4.0 * se
+
+
+@pytest.mark.parametrize("K", [16, 512])
+def test_glossy_product_render_unbiased(pkg, oracle, scenes, gpu, plog, K):
+    """sampleProduct through rough conductors (the non-diffuse learned-BSDF
+    branch: getDMM on (theta_i, alpha), rotate_to_wo, the shading frame to
+    world, sdmm_proc.cpp:327-355) beside diffuse materials: the product render
+    is unbiased against BSDF-only sampling of the same glossy scene (4 sigma
+    over the pixel means), and its training records still equal the
+    host-routed oracle bitwise."""
+    desc = scenes.cornell_box(160, 90, conductor=("TallBox", "Floor"))
+    sc = pkg.Scene(desc)
+    tree = _tree(pkg, sc)
+    node_mix = _train(pkg, sc, tree, 6, 8, K=K)
+    w, m, cov, dif = scenes.diffuse_learned_bsdf(len(desc["reflectance"]) // 3)
+    table = pkg.BsdfTable(w, m, cov, device=gpu, diffuse=dif)
+    img, verts, st = sc.render(tree, node_mix, spp=4, guided=True, seed=77, learned_bsdf=table)
+    assert np.isfinite(img.cpu().numpy()).all() and st["guided_queries"] > 0
+    _check_producer(pkg, oracle, tree, verts, 8, 0xABE, plog, "glossy_product")
+    spp = 64
+    lum = lambda im: im.cpu().numpy().mean(0).reshape(-1)
+    g = lum(sc.render(tree, node_mix, spp=spp, guided=True, seed=2346, learned_bsdf=table)[0])
+    u = lum(sc.render(tree, None, spp=spp, guided=False, seed=4322)[0])
+    mg, mu = g.mean(), u.mean()
+    se = np.sqrt(g.var() / g.size + u.var() / u.size)
+    plog(f"li_glossy_product_K{K}_vs_unguided_mean_sigma", float(abs(mg - mu) / se), 4.0, product=float(mg),
+         unguided=float(mu))
+    assert abs(mg - mu) < 4.0 * se, (mg, mu, se)

@@ -164,3 +164,50 @@ def test_plastic_li_matches_oracle(pkg, oracle, scenes, gpu, plog):
     r = oracle.li_render(desc, aabb, child, node_mix=_oracle_mixes(oracle, node_mix), guided=True, spp=SPP,
                          seed=SEED, threads=16)
     _compare_guided(oracle, plog, "li_plastic_guided", img, rec, nv, r)
+
+
+GLOSSY = ("TallBox", "Floor")
+
+
+def test_conductor_li_unguided_bitwise(pkg, oracle, scenes, gpu, plog):
+    """Rough conductors (Beckmann, roughconductor.cpp) on the tall box and the
+    floor: the device Li equals the CPU Li bit for bit, unguided -- records,
+    vertex counts, image -- at two roughnesses."""
+    for alpha in (0.2, 0.05):
+        desc = scenes.cornell_box(128, 72, conductor=GLOSSY, alpha=alpha)
+        sc = pkg.Scene(desc)
+        tree = _tree(pkg, sc)
+        img, rec, nv, _ = _device(sc, tree, None, False)
+        aabb, child, _ = tree.nodes()
+        r = oracle.li_render(desc, aabb, child, spp=SPP, seed=SEED, threads=8)
+        np.testing.assert_array_equal(nv, r["nv"])
+        sel = np.arange(rec.shape[1])[:, None] < nv[None, :]
+        plog(f"li_conductor_a{alpha}_unguided_rec_max_abs_diff", float(np.abs(rec - r["rec"])[:, sel].max()), 0.0)
+        np.testing.assert_array_equal(rec[:, sel], r["rec"][:, sel])
+        np.testing.assert_array_equal(img, r["image"])
+
+
+@pytest.mark.parametrize("K", [16, 512])
+def test_glossy_product_li_matches_oracle(pkg, oracle, scenes, gpu, plog, K):
+    """sampleProduct with a NON-diffuse learned BSDF inside the render: each
+    rough-conductor bounce conditions its learned lobes on (theta_i, alpha),
+    rotates them to wi (rotate_to_wo) and takes them to world through the
+    shading frame (sdmm_proc.cpp:340-355) -- the product's non-diffuse
+    branch, the Kitchen's (configs[4], K = 512) glossy materials -- beside the
+    diffuse materials' slice-0 rule.  >= 99 % of the paths match the CPU Li."""
+    desc = scenes.cornell_box(128, 72, conductor=GLOSSY)
+    sc = pkg.Scene(desc)
+    tree = _tree(pkg, sc)
+    node_mix = _train(pkg, sc, tree, 4, 8, K=K)
+    assert any(m is not None and m.K == K for m in node_mix)
+    learned = scenes.diffuse_learned_bsdf(len(desc["reflectance"]) // 3)
+    table = pkg.BsdfTable(*learned[:3], device=gpu, diffuse=learned[3])
+    img, rec, nv, _ = _device(sc, tree, node_mix, True, table=table)
+    aabb, child, _ = tree.nodes()
+    r = oracle.li_render(desc, aabb, child, node_mix=_oracle_mixes(oracle, node_mix), guided=True, spp=SPP,
+                         seed=SEED, learned=learned, threads=16)
+    _compare_guided(oracle, plog, f"li_glossy_product_K{K}", img, rec, nv, r)
+    # the conductor's bounces used the product (k * max(M, 4) + j indices of
+    # its own rows): some guided samples come from its lobes 1..3
+    comps = r["comps"]
+    assert ((comps >= 0) & (comps % 4 != 0)).sum() > 0
