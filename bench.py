@@ -271,17 +271,19 @@ def cornell_cpu_baseline(pkg, g, desc, spp, seed, threads, learned=None, budget_
 
 
 def cornell_bench(pkg, dev, args, world, optimize_async=0, K=16, product=False, cpu=False, cpu_probe_px=512,
-                  cpu_budget_s=6.0):
+                  cpu_budget_s=6.0, glossy=()):
     """configs[0] on the device: the test suite's Cornell Box (640x360), K=16
     per leaf (K=128: the Torus line's K, configs[2], over the one scene whose
     geometry the snapshot holds), 64 spp rendered 8 spp per iteration, training (push + optimize)
     while samplesRendered < sampleCount / 4 (volpath_sdmm.cpp:411-507), the
     native guiding model (sdmm_guiding_iteration) with the device Li.  Replicas
     only (each rank renders the whole image; no exchange).  "guided rays/s" =
-    bounce rays traced per second in the guided passes."""
+    bounce rays traced per second in the guided passes.  glossy: BSDFs made
+    rough conductors (with product sampling: the non-diffuse learned-BSDF
+    branch, per-bounce lobes rotated to wi)."""
     import torch
     scenes = importlib.import_module("sdmm_mitsuba_amd.scenes")
-    desc = scenes.cornell_box(640, 360)
+    desc = scenes.cornell_box(640, 360, conductor=glossy)
     sc = pkg.Scene(desc, device=dev.index)
     _, _, tmin, tmax = sc.normalization()
     table = learned = None
@@ -313,7 +315,8 @@ def cornell_bench(pkg, dev, args, world, optimize_async=0, K=16, product=False, 
     guided = [x for x in its if not x["train"]]
     seg = sum(x["segments"] for x in guided)
     gms = sum(x["ms"] for x in guided)
-    res = {"workload": f"Cornell Box 640x360, K={K} per leaf, 64 spp (8 per iteration, training for the first 16)",
+    res = {"workload": f"Cornell Box 640x360{' with rough conductors ' + '/'.join(glossy) if glossy else ''}, "
+                       f"K={K} per leaf, 64 spp (8 per iteration, training for the first 16)",
             "total_ms": total * 1e3, "guided_rays_per_s": seg / (gms * 1e-3),
             "guided_paths_per_s": sum(x["paths"] for x in guided) / (gms * 1e-3),
             "trained_leaves": its[-1]["trained"], "iterations": its,
@@ -647,6 +650,12 @@ def main():
         cpu = rank == 0 and world == 1 and not args.no_cpu
         out["cornell_k512_product"] = cornell_bench(pkg, dev, args, world, K=512, product=True, cpu=cpu,
                                                     cpu_probe_px=16, cpu_budget_s=10.0)
+        # ... and with the Kitchen's glossy materials' branch: the tall box and
+        # the floor rough conductors, whose per-bounce learned lobes take
+        # rotate_to_wo + the shading frame into the product (sdmm_proc.cpp:340-355)
+        out["cornell_k512_glossy_product"] = cornell_bench(pkg, dev, args, world, K=512, product=True, cpu=cpu,
+                                                           cpu_probe_px=16, cpu_budget_s=10.0,
+                                                           glossy=("TallBox", "Floor"))
 
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
