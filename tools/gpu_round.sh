@@ -22,6 +22,6 @@ rc=$?; echo "bench rc=$rc"; cat "$OUT/bench_$TAG.json"
 [ $rc -eq 0 ] || { tail -20 "$OUT/bench_$TAG.err"; exit $rc; }
 
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof_$TAG" -o run \
-    --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu --steps 20 --warmup 5 > "$GRAFT_REPO_ROOT/$OUT/prof_$TAG.log" 2>&1
+    --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu > "$GRAFT_REPO_ROOT/$OUT/prof_$TAG.log" 2>&1
 rc=$?; echo "rocprof rc=$rc"
 exit $rc
