@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""The drop-in plugin's per-tile guided bounce, timed.
+
+plugin/volpath_sdmm_amd.cpp (guideWavefront) serves each render tile's
+bounce with ONE sdmm_guide_pdf_wavefront call under a global mutex: upload the
+tile's query planes from pinned host staging (9 float planes + the mode
+byte), the call, download 4 float planes + the component index, synchronise.
+The mutex serialises the render threads' calls, so the pattern's throughput
+is that of back-to-back calls of the tile size.  This tool trains the Cornell
+Box guiding model (K = 128 leaves, as the bench's cornell_k128 line), takes
+real queries -- the saved vertices of one guided render (condition c, the
+sampled world direction as the BSDF direction), uniforms from a fixed
+generator, half of them pdf queries -- and times, per tile size:
+  * the plugin pattern: pinned H2D + wavefront + D2H + stream synchronise;
+  * the wavefront alone on device-resident planes (the device Li's path);
+and reports queries/s for each beside the full-frame wavefront.
+
+    python tools/plugin_pattern_bench.py [--reps 20]
+"""
+import argparse
+import importlib
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    import torch
+    from conftest import load_pkg
+    pkg = load_pkg()
+    scenes = importlib.import_module("sdmm_mitsuba_amd.scenes")
+    dev = torch.device("cuda:0")
+    desc = scenes.cornell_box(640, 360)
+    sc = pkg.Scene(desc)
+    _, _, tmin, tmax = sc.normalization()
+    g = pkg.Guiding(tmin, tmax, device=0, K=128)
+    img = torch.zeros(3, 360, 640, device=dev)
+    for it in range(3):                       # train for 16 spp, then one guided pass
+        g.iteration(sc, 8, seed=1 + it, push_seed=1001 + it, train=it < 2, image=img)
+    tree = g.tree
+    node_mix = g.node_mixtures()
+    _, verts, _ = sc.render(tree, node_mix, spp=8, guided=True, seed=99)
+    rec, nv = verts.to_numpy()
+    V = verts.s.max_vertices
+    r = rec.reshape(16, V, -1)
+    sel = np.arange(V)[:, None] < nv[None, :]
+    c = np.stack([r[7][sel], r[8][sel], r[9][sel]]).astype(np.float32)
+    dg = np.stack([r[10][sel], r[11][sel], r[12][sel]]).astype(np.float32)
+    n_all = c.shape[1]
+    rng = np.random.default_rng(5)
+    u = rng.uniform(0, 1, size=(3, n_all)).astype(np.float32)
+    mode = (rng.uniform(0, 1, size=n_all) < 0.5).astype(np.uint8)
+    tree.bind(node_mix)
+    ts = torch.cuda.ExternalStream(tree.stream_ptr) if tree.stream_ptr else torch.cuda.current_stream()
+    out = {"queries_available": int(n_all), "K": 128, "scene": "Cornell Box 640x360, trained 16 spp",
+           "pattern": "pinned H2D of 9 planes + mode, sdmm_guide_pdf_wavefront, D2H of 4 planes + comp, sync"}
+    for T in (4096, 32768, 262144, min(n_all, 1 << 21)):
+        if T > n_all:
+            continue
+        h_in = torch.from_numpy(np.concatenate([c[:, :T], u[:, :T], dg[:, :T]]).copy()).pin_memory()
+        h_mode = torch.from_numpy(mode[:T].copy()).pin_memory()
+        d_in = torch.empty((9, T), device=dev)
+        d_mode = torch.empty(T, dtype=torch.uint8, device=dev)
+        h_out = torch.empty((4, T)).pin_memory()
+        h_comp = torch.empty(T, dtype=torch.int32).pin_memory()
+
+        def device_call():
+            cc = [d_in[i] for i in range(3)]
+            uu = [d_in[3 + i] for i in range(3)]
+            gg = [d_in[6 + i] for i in range(3)]
+            return tree.guide_pdf(None, cc, uu, gg, d_mode)
+
+        def plugin_call():
+            with torch.cuda.stream(ts):
+                d_in.copy_(h_in, non_blocking=True)
+                d_mode.copy_(h_mode, non_blocking=True)
+                d, pdf, comp = device_call()
+                h_out[0:3].copy_(torch.stack(d), non_blocking=True)
+                h_out[3].copy_(pdf, non_blocking=True)
+                h_comp.copy_(comp, non_blocking=True)
+            ts.synchronize()
+
+        with torch.cuda.stream(ts):
+            d_in.copy_(h_in)
+            d_mode.copy_(h_mode)
+        torch.cuda.synchronize()
+        for fn in (plugin_call, device_call):
+            fn()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(a.reps):
+            plugin_call()
+        tp = (time.perf_counter() - t) / a.reps
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(a.reps):
+            device_call()
+        torch.cuda.synchronize()
+        td = (time.perf_counter() - t) / a.reps
+        out[f"tile_{T}"] = {"plugin_pattern_ms": tp * 1e3, "plugin_pattern_queries_per_s": T / tp,
+                            "device_resident_ms": td * 1e3, "device_resident_queries_per_s": T / td,
+                            "transfer_bytes_per_call": T * (9 * 4 + 1 + 4 * 4 + 4)}
+        print(json.dumps({f"tile_{T}": out[f"tile_{T}"]}), flush=True)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
