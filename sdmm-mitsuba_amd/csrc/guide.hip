@@ -2448,8 +2448,12 @@ __device__ __forceinline__ bool serve_product_cand(const float* gp, int Kp, int 
 }
 
 
+// Two waves per SIMD: left free the sampling form took 256 VGPRs + 10 AGPRs,
+// ONE wave per SIMD for a latency-bound thread-per-query kernel; bounded to
+// 256 registers it spills 11 (32 B of scratch) and the K = 512 product pass
+// runs 85.5 -> 71.1 ms (first guided pass 111 -> 95 ms; round 5)
 template <bool PDF_ONLY, int LCAP>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 guide_tree_product_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __restrict__ tab,
                                const float* const* __restrict__ cctab, int64_t nq, GuideIO io, ProductIO pio,
                                BsdfTab bt, GuideConsts gc, int cap, int* __restrict__ fb_count,
