@@ -715,7 +715,8 @@ struct WaveLds {
     int* sl;         // K   kept slot -> component | (conditional valid) << 31
     float* fw;       // K   slot weights: raw, then slot_w(i)
     float* se;       // 3K  conditional mean direction of each kept slot (product)
-    float* lobe;     // 20M world-frame learned-BSDF lobes of the query's material (product)
+    float* lobe;     // 20M world-frame learned-BSDF lobes of the query's material (product),
+                     // then M ints: the nonzero-weight lobes' indices in order
     float* pc;       // this workgroup's global scratch: kPcStride x pcap floats, the product
                      // pairs of pass 1 {w, included, mean, Linv, detInv} (when they fit)
     int pcap;
@@ -734,7 +735,7 @@ __device__ __forceinline__ WaveLds wave_lds(float* lds, int K, float* pscratch =
     L.pcap = pscratch ? pcap : 0;
     return L;
 }
-static size_t wave_lds_bytes(int K, int M = 0) { return sizeof(float) * (5 * (size_t)K + 20 * (size_t)M) + 16; }
+static size_t wave_lds_bytes(int K, int M = 0) { return sizeof(float) * (5 * (size_t)K + 21 * (size_t)M) + 16; }
 
 // lane ^ J of a wave-uniform compile-time J (DPP inside rows, ds_bpermute across)
 template <int J>
@@ -1928,9 +1929,9 @@ __device__ __forceinline__ void for_each_pair(const float* gp, int Kp, const flo
         coordinates_f(e, to_i);
         for (int l = 0; l < 4; ++l) ci[l] = condCov[4 * k + l];
         for (int j = 0; j < bt.M; ++j) {
+            if (bt.w[b * bt.M + j] == 0.0f) continue;   // (a skipped lobe: no world transform)
             float mw[3], tw[9], cj[4], wj;
             bsdf_world(F, bt, b, j, mw, tw, cj, wj);
-            if (wj == 0.0f) continue;
             if (e[0] * mw[0] + e[1] * mw[1] + e[2] * mw[2] < 0.0f) continue;
             ProdComp pc;
             const float nw = mvtn_multiply(e, to_i, ci, mw, tw, cj, norm2, pc, lazy);
@@ -2202,6 +2203,14 @@ __device__ __forceinline__ void wave_prepare_product(const float* gp, int Kp, co
         float* lb = L.lobe + 20 * j;
         bsdf_world(F, bt, b, j, lb, lb + 3, lb + 12, lb[16]);
     }
+    // the nonzero-weight lobes in order (M <= 64: one lane each): the pair
+    // walk skips the others, so it runs over kept x nonzero pairs only (a
+    // table padded to a common lobe count costs no chunks)
+    {
+        const bool nzl = lane < bt.M && bt.w[b * bt.M + lane] != 0.0f;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(nzl);
+        if (nzl) ((int*)(L.lobe + 20 * bt.M))[__builtin_popcountll(m & ((1ull << lane) - 1ull))] = lane;
+    }
     __syncthreads();
 }
 
@@ -2236,10 +2245,13 @@ template <bool PDF_ONLY>
 __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCov, const float c[3], int lastIdx,
                                     const WaveLds& L, const BsdfTab& bt, int b, const float F[9], const float* u,
                                     const float* dir_in, float choice, int lane, GuideConsts gc, QueryOut& o) {
-    const int M = bt.M;
+    wave_prepare_product(gp, Kp, c, lastIdx, L, bt, b, F, lane);
+    // pair f = (kept slot f / M, nonzero lobe nzj[f % M]) -- the reference's
+    // walk order with the zero-weight lobes (which it skips) left out
+    const int M = __builtin_popcountll(__builtin_amdgcn_ballot_w64(lane < bt.M && bt.w[b * bt.M + lane] != 0.0f));
+    const int* nzj = (const int*)(L.lobe + 20 * bt.M);
     const int NP = lastIdx * M;
     const bool keep = NP <= L.pcap;
-    wave_prepare_product(gp, Kp, c, lastIdx, L, bt, b, F, lane);
     // pass 1: the product mass (createCdf(true)'s sum) and the pair count
     float total = 0.0f;
     int P = 0;
@@ -2250,7 +2262,7 @@ __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCo
         if (f < NP) {
             ProdComp pc{};
             int k;
-            inc = pair_eval(condCov, L, f / M, f % M, gc.norm2, w, pc, k);
+            inc = pair_eval(condCov, L, f / M, nzj[f % M], gc.norm2, w, pc, k);
             if (keep) {
                 float* r = L.pc + kPcStride * f;
                 r[0] = w;
@@ -2283,7 +2295,7 @@ __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCo
                 } else {
                     ProdComp pc{};
                     int k;
-                    inc = pair_eval(condCov, L, f / M, f % M, gc.norm2, w, pc, k);
+                    inc = pair_eval(condCov, L, f / M, nzj[f % M], gc.norm2, w, pc, k);
                 }
                 if (inc) x = w / total;
             }
@@ -2303,7 +2315,7 @@ __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCo
         ProdComp pcs{};
         int ksel = 0;
         float wsel = 0.0f;
-        (void)pair_eval(condCov, L, sel_f / M, sel_f % M, gc.norm2, wsel, pcs, ksel, false);
+        (void)pair_eval(condCov, L, sel_f / M, nzj[sel_f % M], gc.norm2, wsel, pcs, ksel, false);
         const float radius = sqrtf(-2.0f * log_x(1.0f - u[1]));
         const float theta = (float)(2.0 * kPi * (double)u[2]);
         const float z0 = radius * sin_x(theta), z1 = radius * cos_x(theta);
@@ -2312,7 +2324,7 @@ __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCo
         float to[9];
         coordinates_f(pcs.mean, to);
         if (!ts_exp_x(to, v0, v1, dir)) dir[0] = dir[1] = dir[2] = 0.0f;
-        o.comp = ksel * M + sel_f % M;
+        o.comp = ksel * bt.M + nzj[sel_f % M];
     } else {
         dir[0] = dir_in[0]; dir[1] = dir_in[1]; dir[2] = dir_in[2];
     }
@@ -2338,7 +2350,7 @@ __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCo
                 ProdComp pc{};
                 int k;
                 float w = 0.0f;
-                if (pair_eval(condCov, L, f / M, f % M, gc.norm2, w, pc, k)) {
+                if (pair_eval(condCov, L, f / M, nzj[f % M], gc.norm2, w, pc, k)) {
                     const float wn = w / total;
                     if (wn != 0.0f) term = wn * prod_comp_pdf(pc, dir, gc.norm2);
                 }
