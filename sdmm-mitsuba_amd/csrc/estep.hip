@@ -1159,7 +1159,7 @@ estep_stats_tile_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
 // rows split into kReduceSlices slices; within slice s four row-interleaved
 // fp64 sums (rows r0 + j, r0 + j + 4, ...; j < 4) combined as ((b0 + b1) + b2)
 // + b3; the slices summed in order from 0.0.  The batched per-leaf reduction
-// (batched_col) uses the same order, so a leaf's stats are bitwise those of
+// (reduce_uncenter_batched_kernel) uses the same order, so a leaf's stats are bitwise those of
 // its single-mixture E-step.
 constexpr int kReduceSlices = 16;
 
@@ -1216,42 +1216,37 @@ __device__ __forceinline__ void uncenter_component(const double mu[3], double w,
 // The same operations in the same order as the two-launch form: bitwise equal.
 constexpr int kRedCB = 3;
 static_assert(ST_FIELDS * kRedCB <= 64, "a workgroup's columns fit one wave");
-__global__ void __launch_bounds__(64 * kReduceSlices)
-reduce_uncenter_kernel(const float* __restrict__ partials, int rows, int pstride, const float* __restrict__ ep,
-                       int Kp, int K, double* __restrict__ stats) {
-    __shared__ double sv[kReduceSlices][64];
-    const int lane = threadIdx.x & 63;
-    const int sl = threadIdx.x >> 6;
-    const int nb = (K + kRedCB - 1) / kRedCB;
-    const int k0 = blockIdx.x * kRedCB;
-    int col = -1;
-    if (blockIdx.x == nb) {
-        if (lane < 2) col = ST_FIELDS * Kp + lane;
-    } else if (lane < ST_FIELDS * kRedCB && k0 + lane / ST_FIELDS < K) {
-        col = ST_FIELDS * k0 + lane;
-    }
-    const int r0 = (int)((int64_t)rows * sl / kReduceSlices);
-    const int r1 = (int)((int64_t)rows * (sl + 1) / kReduceSlices);
+// Partial column of lane `lane` in component group g (components kRedCB g
+// ...; the extra group g == nb holds H and wsum), or -1.
+__device__ __forceinline__ int group_col(int lane, int g, int nb, int K, int Kp) {
+    if (g == nb) return lane < 2 ? ST_FIELDS * Kp + lane : -1;
+    const int k0 = g * kRedCB;
+    return (lane < ST_FIELDS * kRedCB && k0 + lane / ST_FIELDS < K) ? ST_FIELDS * k0 + lane : -1;
+}
+
+// One slice's sum of a column (rows [r0, r1) of p, stride pstride): four
+// row-interleaved fp64 partials, every load of a 16-row batch independent,
+// combined as ((b0 + b1) + b2) + b3.
+__device__ __forceinline__ double slice_sum(const float* __restrict__ p, int pstride, int r0, int r1) {
     double b[4] = {0.0, 0.0, 0.0, 0.0};
-    if (col >= 0) {
-        const float* p = partials + col;
-        int r = r0;
-        for (; r + 16 <= r1; r += 16) {
-            float v[16];
+    int r = r0;
+    for (; r + 16 <= r1; r += 16) {
+        float v[16];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) v[i] = p[(int64_t)(r + i) * pstride];
+        for (int i = 0; i < 16; ++i) v[i] = p[(int64_t)(r + i) * pstride];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) b[i & 3] += (double)v[i];
-        }
-        for (; r < r1; ++r) b[(r - r0) & 3] += (double)p[(int64_t)r * pstride];
+        for (int i = 0; i < 16; ++i) b[i & 3] += (double)v[i];
     }
-    sv[sl][lane] = ((b[0] + b[1]) + b[2]) + b[3];
-    __syncthreads();
-    if (sl != 0) return;
-    double v = 0.0;
-#pragma unroll
-    for (int s2 = 0; s2 < kReduceSlices; ++s2) v += sv[s2][lane];
-    if (blockIdx.x == nb) {
+    for (; r < r1; ++r) b[(r - r0) & 3] += (double)p[(int64_t)r * pstride];
+    return ((b[0] + b[1]) + b[2]) + b[3];
+}
+
+// Group g's column totals (lane = column, as group_col) into the compact
+// stats: H and wsum, or lanes < kRedCB un-centre their component.  Every lane
+// of the wave takes part (the shuffles).
+__device__ __forceinline__ void group_store(double v, int lane, int g, int nb, int K, int Kp,
+                                            const float* __restrict__ ep, double* __restrict__ stats) {
+    if (g == nb) {
         if (lane < 2) stats[lane] = v;
         return;
     }
@@ -1260,7 +1255,7 @@ reduce_uncenter_kernel(const float* __restrict__ partials, int rows, int pstride
     double c[ST_FIELDS];
 #pragma unroll
     for (int f = 0; f < ST_FIELDS; ++f) c[f] = __shfl(v, cl + f);
-    const int k = k0 + lane;
+    const int k = g * kRedCB + lane;
     if (lane < kRedCB && k < K) {
         const double mu[3] = {(double)ep[EP_MU0 * Kp + k], (double)ep[EP_MU1 * Kp + k],
                               (double)ep[EP_MU2 * Kp + k]};
@@ -1275,76 +1270,62 @@ reduce_uncenter_kernel(const float* __restrict__ partials, int rows, int pstride
     }
 }
 
-// Batched reduction + finalisation: one column of a leaf's rows reduced in
-// reduce_uncenter_kernel's order (slices of the leaf's rows, four
-// row-interleaved fp64 partials per slice combined as ((b0 + b1) + b2) + b3,
-// slices summed in order), so a batched leaf's stats are bitwise those of its
-// single-mixture E-step.
-__device__ __forceinline__ double batched_col(const float* __restrict__ partials, int pstride, int row0, int rows,
-                                              int col) {
-    double t = 0.0;
-    for (int sl = 0; sl < kReduceSlices; ++sl) {
-        const int r0 = (int)((int64_t)rows * sl / kReduceSlices);
-        const int r1 = (int)((int64_t)rows * (sl + 1) / kReduceSlices);
-        double b[4];
-        for (int w = 0; w < 4; ++w) {
-            double sum = 0.0;
-            for (int r = r0 + w; r < r1; r += 4) sum += (double)partials[(int64_t)(row0 + r) * pstride + col];
-            b[w] = sum;
-        }
-        t += ((b[0] + b[1]) + b[2]) + b[3];
-    }
-    return t;
+__global__ void __launch_bounds__(64 * kReduceSlices)
+reduce_uncenter_kernel(const float* __restrict__ partials, int rows, int pstride, const float* __restrict__ ep,
+                       int Kp, int K, double* __restrict__ stats) {
+    __shared__ double sv[kReduceSlices][64];
+    const int lane = threadIdx.x & 63;
+    const int sl = threadIdx.x >> 6;
+    const int nb = (K + kRedCB - 1) / kRedCB;
+    const int col = group_col(lane, blockIdx.x, nb, K, Kp);
+    const int r0 = (int)((int64_t)rows * sl / kReduceSlices);
+    const int r1 = (int)((int64_t)rows * (sl + 1) / kReduceSlices);
+    sv[sl][lane] = col >= 0 ? slice_sum(partials + col, pstride, r0, r1) : 0.0;
+    __syncthreads();
+    if (sl != 0) return;
+    double v = 0.0;
+#pragma unroll
+    for (int s2 = 0; s2 < kReduceSlices; ++s2) v += sv[s2][lane];
+    group_store(v, lane, blockIdx.x, nb, K, Kp, ep, stats);
 }
 
-
-// One workgroup per leaf.  Phase 1: one thread per stats column (consecutive
-// threads read consecutive partial columns of a row: coalesced), each column
-// reduced exactly as batched_col / the single-mixture path orders it (16 row
-// slices, four row-interleaved fp64 sums per slice combined as
-// ((b0 + b1) + b2) + b3, slices summed in order) into LDS.  Phase 2: the
-// un-centring of the spatial moments per component, as reduce_uncenter_kernel.
-// Bitwise equal to the previous thread-per-component form, with 21x more
-// threads in flight (it was latency-bound: 16 busy lanes per leaf): 257 ->
-// ~50 us per 256-leaf K=16 step (a (column, slice) split measured no faster).
+// The training pass's batched per-leaf reduction (round 5): ONE wave per
+// (leaf, component group), the 16 slices of the leaf's rows summed in order
+// by the same wave -- the single-mixture kernel's operations in its order, so
+// a batched leaf's stats stay bitwise those of its single-mixture E-step.  A
+// training pass's leaves hold a few rows each, so the single-mixture shape
+// (16 waves a group, one per slice) would mostly launch idle waves.  Grid
+// (leaves, ceil((groups + 1) / 4)), four waves a workgroup.  Round 4 ran one
+// workgroup per leaf with a thread per column (~40 columns per thread in
+// series at K = 512: 5.4 ms per launch).
 __global__ void __launch_bounds__(256)
-reduce_finalize_batched_kernel(const float* __restrict__ partials, int pstride, int Kp, int K,
+reduce_uncenter_batched_kernel(const float* __restrict__ partials, int pstride, int Kp, int K,
                                const LeafDesc* __restrict__ leaves) {
-    extern __shared__ double leaf_cols[];   // 2 + 21 K column sums of this leaf
-    double* red = leaf_cols;
     const LeafDesc& L = leaves[blockIdx.x];
     if (L.n <= 0) return;             // uniform over the workgroup
-    const int ncols = 2 + 21 * K;
-    // one thread per partial column (consecutive threads, consecutive
-    // addresses), stored at its compact index
-    for (int c = threadIdx.x; c < ST_FIELDS * Kp + 2; c += blockDim.x) {
-        const int o = compact_of(c, Kp, K);
-        if (o >= 0) red[o] = batched_col(partials, pstride, L.row0, L.rows, c);
+    const int lane = threadIdx.x & 63;
+    const int nb = (K + kRedCB - 1) / kRedCB;
+    const int g = (int)blockIdx.y * 4 + (int)(threadIdx.x >> 6);
+    if (g > nb) return;               // uniform over the wave
+    const int col = group_col(lane, g, nb, K, Kp);
+    double v = 0.0;
+    if (col >= 0) {
+        const float* p = partials + (int64_t)L.row0 * pstride + col;
+        for (int sl = 0; sl < kReduceSlices; ++sl) {
+            const int r0 = (int)((int64_t)L.rows * sl / kReduceSlices);
+            const int r1 = (int)((int64_t)L.rows * (sl + 1) / kReduceSlices);
+            v += slice_sum(p, pstride, r0, r1);
+        }
     }
-    __syncthreads();
-    double* stats = L.stats;
-    if (threadIdx.x < 2) stats[threadIdx.x] = red[threadIdx.x];
-    for (int k = threadIdx.x; k < K; k += blockDim.x) {
-        const float* ep = L.ep;
-        const double mu[3] = {(double)ep[EP_MU0 * Kp + k], (double)ep[EP_MU1 * Kp + k],
-                              (double)ep[EP_MU2 * Kp + k]};
-        const double w = red[2 + k];
-        double M[5], C[15];
-        for (int i = 0; i < 5; ++i) M[i] = red[2 + K + 5 * k + i];
-        for (int i = 0; i < 15; ++i) C[i] = red[2 + 6 * K + 15 * k + i];
-        uncenter_component(mu, w, M, C);
-        stats[2 + k] = w;
-        for (int i = 0; i < 5; ++i) stats[2 + K + 5 * k + i] = M[i];
-        for (int i = 0; i < 15; ++i) stats[2 + 6 * K + 15 * k + i] = C[i];
-    }
+    group_store(v, lane, g, nb, K, Kp, L.ep, L.stats);
 }
 
 hipError_t launch_reduce_finalize_batched(const float* partials, int pstride, int Kp, int K,
                                           const LeafDesc* leaves, int n_leaves, hipStream_t st) {
     if (n_leaves <= 0) return hipSuccess;
-    const size_t lds = sizeof(double) * (size_t)(2 + 21 * K);   // K <= 512: 86 KB
-    hipLaunchKernelGGL(reduce_finalize_batched_kernel, dim3(n_leaves), dim3(256), lds, st, partials, pstride, Kp,
-                       K, leaves);
+    const int nb = (K + kRedCB - 1) / kRedCB;
+    hipLaunchKernelGGL(reduce_uncenter_batched_kernel, dim3(n_leaves, (nb + 1 + 3) / 4), dim3(256), 0, st, partials,
+                       pstride, Kp, K, leaves);
     return hipGetLastError();
 }
 

@@ -55,6 +55,7 @@ def _device_samples(pkg, x, w):
     (16, [64] * 40 + [3000] * 3, 1),
     (32, [1000, 1500, 0, 2200], 2),
     (128, [5000, 300, 9000], 2),
+    (512, [3000, 40, 7000], 1),
 ])
 def test_batched_equals_sequential_bitwise(pkg, synth, gpu, K, sizes, iters):
     import torch
