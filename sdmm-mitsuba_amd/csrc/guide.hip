@@ -2852,9 +2852,10 @@ hipError_t launch_guide_tree(const void* nodes, const void* tab, int kmax, int64
 
 // The product launches' scratch in the handle's grow-only buffer: the thread
 // path's pair cache for `threads` query columns (640 B per column), then the
-// wave kernel's pair slices (fblocks workgroups, mandatory).  Regrowth frees
-// the old buffer in stream order (every earlier use is on the same stream)
-// and allocates the larger one.  The cache is optional: when the buffer with
+// wave kernel's pair slices (fblocks workgroups, mandatory).  Regrowth (rare:
+// grow-only) syncs the stream, frees the old buffer and allocates the larger
+// one with hipMalloc -- not from the stream-ordered pool: plugin threads call
+// this on many handles at once (sdmm_api.cpp copy_prefix_many).  The cache is optional: when the buffer with
 // it cannot be allocated, the slices alone are, and the thread path
 // recomputes its pairs (the same values; pc->base = null), so a wavefront too
 // large for a cache still runs.  sdmm_destroy (or the tree's destruction)
@@ -2868,16 +2869,17 @@ static hipError_t product_scratch(ProductScratch* ps, int64_t threads, unsigned 
     auto grow = [&](size_t need) -> hipError_t {
         if (ps->bytes >= need) return hipSuccess;
         if (ps->base) {
-            const hipError_t f = hipFreeAsync(ps->base, st);
+            const hipError_t f = hipStreamSynchronize(st);   // every earlier use is on this stream
             if (f != hipSuccess) return f;
+            (void)hipFree(ps->base);
         }
         ps->base = nullptr;
         ps->bytes = 0;
         const size_t grown = need + need / 4;
-        hipError_t e = hipMallocAsync((void**)&ps->base, grown, st);
+        hipError_t e = hipMalloc((void**)&ps->base, grown);
         if (e != hipSuccess) {
             (void)hipGetLastError();   // clear the sticky allocation error; try the exact size
-            e = hipMallocAsync((void**)&ps->base, need, st);
+            e = hipMalloc((void**)&ps->base, need);
             if (e != hipSuccess) {
                 (void)hipGetLastError();
                 ps->base = nullptr;

@@ -22,6 +22,7 @@
 #include <cmath>
 #include <cstdint>
 #include <string>
+#include <mutex>
 #include <vector>
 
 #include "../../include/sdmm_gpu.h"
@@ -230,8 +231,28 @@ int sdmm_kmeanspp_select(const sdmm_samples* s, const float* const normals[3], c
     const size_t o_idx = o_pdf + sizeof(double) * (size_t)ntot;
     const size_t o_pn = o_idx + ((sizeof(int64_t) * nu + 255) / 256) * 256;
     const size_t total = o_pn + sizeof(float) * 6 * nu;
-    char* d = nullptr;
-    if (e == hipSuccess) e = hipMallocAsync((void**)&d, total, st);
+    // the scratch: a per-device block grown with hipMalloc, held under a lock
+    // until the stream sync below (no stream-ordered pool allocation on an
+    // entry point host threads may call at once; sdmm_api.cpp copy_prefix_many)
+    struct Scratch {
+        std::mutex mu;
+        char* p = nullptr;
+        size_t cap = 0;
+    };
+    static Scratch scratch[64];
+    if (device < 0 || device >= 64) return kfail(SDMM_E_INVALID, "sdmm_kmeanspp_select: device index out of range");
+    Scratch& sc = scratch[device];
+    std::lock_guard<std::mutex> hold(sc.mu);
+    if (e == hipSuccess && total > sc.cap) {
+        if (sc.p) (void)hipFree(sc.p);   // idle: every holder synced its stream
+        sc.p = nullptr;
+        sc.cap = 0;
+        const size_t cap = total + total / 2;
+        e = hipMalloc((void**)&sc.p, cap);
+        if (e == hipSuccess) sc.cap = cap;
+        else sc.p = nullptr;
+    }
+    char* d = sc.p;
     if (e == hipSuccess) e = hipMemcpyAsync(d, lv.data(), sizeof(KmppLeaf) * lv.size(), hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemcpyAsync(d + o_u, uniforms, sizeof(float) * nu, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) {
@@ -245,8 +266,10 @@ int sdmm_kmeanspp_select(const sdmm_samples* s, const float* const normals[3], c
     if (e == hipSuccess) e = hipMemcpyAsync(out_index, d + o_idx, sizeof(int64_t) * nu, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess && (out_positions || out_normals))
         e = hipMemcpyAsync(pn.data(), d + o_pn, sizeof(float) * 6 * nu, hipMemcpyDeviceToHost, st);
-    if (d) (void)hipFreeAsync(d, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    {   // always: the scratch is released to the next holder only when idle
+        const hipError_t es = hipStreamSynchronize(st);
+        if (e == hipSuccess) e = es;
+    }
     if (e != hipSuccess) return kfail(SDMM_E_HIP, std::string("sdmm_kmeanspp_select: ") + hipGetErrorString(e));
     for (size_t i = 0; i < nu; ++i)
         for (int a = 0; a < 3; ++a) {

@@ -919,9 +919,9 @@ void sdmm_detail::destroy_impl(sdmm_mix* m, bool sync) {
     }
     if (m->partials) (void)hipFree(m->partials);
     if (m->guide_fb) (void)hipFree(m->guide_fb);
-    // stream ordered after the handle's last product launch (allocated on
-    // its stream; streams are synchronised above or by destroy_many)
-    if (m->product_scratch.base) (void)hipFreeAsync(m->product_scratch.base, m->stream);
+    // after the handle's last product launch (streams are synchronised above
+    // or by destroy_many)
+    if (m->product_scratch.base) (void)hipFree(m->product_scratch.base);
     if (m->staging) (void)hipFree(m->staging);
     if (m->batch_dev) (void)hipFree(m->batch_dev);
     if (m->batch_host) (void)hipHostFree(m->batch_host);
@@ -978,12 +978,40 @@ int copy_prefix_many(const sdmm_mix* const* src, sdmm_mix* const* dst, int n, hi
         ptrs[(size_t)i] = src[i]->C.weights;
         ptrs[(size_t)n + i] = dst[i]->C.weights;
     }
-    void* dtab = nullptr;
-    hipError_t e = hipMallocAsync(&dtab, sizeof(void*) * ptrs.size(), st);
-    if (e == hipSuccess) e = hipMemcpyAsync(dtab, ptrs.data(), sizeof(void*) * ptrs.size(), hipMemcpyHostToDevice, st);
+    // the pointer table in a per-device block grown with hipMalloc under a
+    // lock held until the stream sync below.  (Round 5: a stream-ordered
+    // pool allocation here and in the init, with the pool's default release
+    // threshold of 0, is the pattern round 2's hang had -- pool allocations
+    // on many streams beside other host threads' synchronisations -- and the
+    // C++ plugin harness's thread-per-leaf run faulted once this round.)
+    struct TabScratch {
+        std::mutex mu;
+        void* p = nullptr;
+        size_t cap = 0;
+    };
+    static TabScratch tabs[64];
+    const int dev_i = src[0]->device;
+    if (dev_i < 0 || dev_i >= 64) return fail(SDMM_E_INVALID, "device index out of range");
+    TabScratch& ts = tabs[dev_i];
+    std::lock_guard<std::mutex> hold(ts.mu);
+    hipError_t e = hipSuccess;
+    const size_t tb = sizeof(void*) * ptrs.size();
+    if (tb > ts.cap) {
+        if (ts.p) (void)hipFree(ts.p);   // idle: every holder synced its stream
+        ts.p = nullptr;
+        ts.cap = 0;
+        const size_t cap = std::max<size_t>(tb + tb / 2, 64 << 10);
+        e = hipMalloc(&ts.p, cap);
+        if (e == hipSuccess) ts.cap = cap;
+        else ts.p = nullptr;
+    }
+    void* dtab = ts.p;
+    if (e == hipSuccess) e = hipMemcpyAsync(dtab, ptrs.data(), tb, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = launch_copy_many(n, dtab, (void**)dtab + n, bytes, st);
-    if (dtab) (void)hipFreeAsync(dtab, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);   // ptrs is a host temporary
+    {   // always: ptrs is a host temporary and the table goes to the next holder
+        const hipError_t es = hipStreamSynchronize(st);
+        if (e == hipSuccess) e = es;
+    }
     if (e != hipSuccess) return fail(SDMM_E_HIP, std::string("mixture copy: ") + hipGetErrorString(e));
     return SDMM_OK;
 }
@@ -1212,10 +1240,15 @@ static int init_hemisphere_batched_impl(sdmm_mix* const* mixes, int n, const flo
     const size_t per = 4 * Kz + 4 * 6 * Kz + 4 * 25 * Kz + 4 * 25 * Kz + 4 * 9 * Kz;
     // pinned staging: one grow-only buffer per device, held for the call (a
     // fresh hipHostMalloc of ~10 MB per training pass pinned pages each time)
+    // (and the device block of the call, grown with hipMalloc under the same
+    // lock: no stream-ordered pool allocation on a path many host threads
+    // call at once -- see copy_prefix_many)
     struct Staging {
         std::mutex mu;
         char* p = nullptr;
         size_t cap = 0;
+        char* d = nullptr;
+        size_t dcap = 0;
     };
     static Staging staging[64];
     const int dev_i = mixes[0]->device;
@@ -1293,10 +1326,20 @@ static int init_hemisphere_batched_impl(sdmm_mix* const* mixes, int n, const flo
     // one upload, then (device generation) one kernel filling the staging
     // block and one kernel (a workgroup per mixture: copy in, MVTN::set, CDF,
     // pack)
-    void* dev = nullptr;
     const size_t total = stage_bytes + tab_bytes + in_bytes;
-    hipError_t e0 = r ? hipSuccess : hipMallocAsync(&dev, total, st);
-    char* d = (char*)dev;
+    hipError_t e0 = hipSuccess;
+    if (!r && total > sg.dcap) {
+        // the previous block is idle: every call syncs its stream before it
+        // releases the lock
+        if (sg.d) (void)hipFree(sg.d);
+        sg.d = nullptr;
+        sg.dcap = 0;
+        const size_t cap = std::max<size_t>(total + total / 2, 1 << 20);
+        e0 = hipMalloc((void**)&sg.d, cap);
+        if (e0 == hipSuccess) sg.dcap = cap;
+        else sg.d = nullptr;
+    }
+    char* d = sg.d;
     if (!r && e0 == hipSuccess) e0 = hipMemcpyAsync(d + up_off, pin, total - up_off, hipMemcpyHostToDevice, st);
     if (!r && e0 == hipSuccess && !host_gen)
         e0 = launch_hemi_gen_batched(n, K, (const float*)(d + in_off), (const float*)(d + in_off + pn_bytes),
@@ -1304,7 +1347,6 @@ static int init_hemisphere_batched_impl(sdmm_mix* const* mixes, int n, const flo
                                      d, per, st);
     if (!r && e0 == hipSuccess)
         e0 = launch_set_all_batched(n, K, mixes[0]->Kp, d + stage_bytes, d, per, mixes[0]->norm5, st);
-    if (dev) (void)hipFreeAsync(dev, st);
     if (!r && e0 != hipSuccess) r = fail(SDMM_E_HIP, std::string("init_hemisphere_batched: ") + hipGetErrorString(e0));
     const hipError_t e = hipStreamSynchronize(st);   // the pinned staging is reused by the next call
     if (r) return r;
@@ -2427,10 +2469,7 @@ void sdmm_stree_destroy(sdmm_stree* t) {
     if (t->split_mem) (void)hipFree(t->split_mem);
     if (t->split_small) (void)hipFree(t->split_small);
     if (t->guide_fb) (void)hipFree(t->guide_fb);
-    if (t->product_scratch.base) {
-        (void)hipFreeAsync(t->product_scratch.base, t->stream);
-        (void)hipStreamSynchronize(t->stream);
-    }
+    if (t->product_scratch.base) (void)hipFree(t->product_scratch.base);   // stream synced above
     for (hipEvent_t e : t->mix_events) (void)hipEventDestroy(e);
     if (t->stream && t->own_stream) (void)hipStreamDestroy(t->stream);
     delete t;
