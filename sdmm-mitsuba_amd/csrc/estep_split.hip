@@ -199,7 +199,18 @@ __device__ __forceinline__ void pdf_quad(const f4& C, const f4& AD, const f4& BD
     for (int i = 0; i < 2; ++i) {
         const f2 r = f2{__builtin_amdgcn_rsqf(s2[i].x), __builtin_amdgcn_rsqf(s2[i].y)};
         const f2 fneg = pfma(spl(3.14159265358979f), r, -h[i]);
-        a[i] = f2{c[i].x < 0.0f ? fneg.x : h[i].x, c[i].y < 0.0f ? fneg.y : h[i].y};
+        if constexpr (!RARE) {
+            // c < 0 ? fneg : h as one median: fneg > h on both sides (pi / s >
+            // 2 acos|c| / s), and -2^100 c is +huge for c < 0 and -huge for
+            // c > 0, so med3(h, fneg, -2^100 c) picks fneg or h (one packed
+            // product + one med3 per pair instead of a compare + a select).
+            // Only |c| < 2^-90 lands between (the result then h within
+            // ~1e-7: pi / s - 2 h ~ 0 there), NaN pairs go to the RARE redo.
+            const f2 t = pmul(c[i], spl(-0x1p100f));
+            a[i] = f2{__builtin_amdgcn_fmed3f(h[i].x, fneg.x, t.x), __builtin_amdgcn_fmed3f(h[i].y, fneg.y, t.y)};
+        } else {
+            a[i] = f2{c[i].x < 0.0f ? fneg.x : h[i].x, c[i].y < 0.0f ? fneg.y : h[i].y};
+        }
         if constexpr (RARE) {
             const float o0 = __builtin_amdgcn_fmed3f(1073741824.0f * (c[i].x + 1.0f), 0.0f, 1.0f);
             const float o1 = __builtin_amdgcn_fmed3f(1073741824.0f * (c[i].y + 1.0f), 0.0f, 1.0f);
@@ -207,6 +218,11 @@ __device__ __forceinline__ void pdf_quad(const f4& C, const f4& AD, const f4& BD
             a[i].y = (c[i].y < 0.0f && s2[i].y < 1e-6f) ? o1 : a[i].y;
         }
     }
+    // detInv pi_k * jacobian (mvtn.h:361, mixture_model.h:164) ahead of the
+    // exponent chain: the tail after the exp is one product per pair
+    f2 da[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) da[i] = pmul(f2{dipi[2 * i], dipi[2 * i + 1]}, a[i]);
     f2 arg[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -240,7 +256,7 @@ __device__ __forceinline__ void pdf_quad(const f4& C, const f4& AD, const f4& BD
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const f2 e = f2{__builtin_amdgcn_exp2f(arg[i].x), __builtin_amdgcn_exp2f(arg[i].y)};
-        p[i] = pmul(e, pmul(f2{dipi[2 * i], dipi[2 * i + 1]}, a[i]));   // * detInv * pi_k * jacobian (mvtn.h:361, mixture_model.h:164)
+        p[i] = pmul(e, da[i]);
     }
 }
 
@@ -504,7 +520,9 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
         const bf8 Bd = a_frag(D3, g, false);
         const bf8 Bs = pfrag(P3);
 
-        f2 acc = f2{0.0f, 0.0f};
+        // the normaliser's lane partials: two independent packed chains (rows
+        // j, j + 1 and j + 2, j + 3), so no product waits on the previous add
+        f2 acc = f2{0.0f, 0.0f}, acc2 = f2{0.0f, 0.0f};
         uint32_t cbits = 0;
         auto pair_math = [&](int r, auto rare, const f4 (&D)[8], const f4& dp) __attribute__((always_inline)) {
             constexpr bool RARE = decltype(rare)::value;
@@ -518,7 +536,8 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
             pdf[r][1] = p[0].y;
             pdf[r][2] = p[1].x;
             pdf[r][3] = p[1].y;
-            acc = padd(acc, padd(p[0], p[1]));
+            acc = padd(acc, p[0]);
+            acc2 = padd(acc2, p[1]);
         };
 #if defined(SDMM_SPLIT_DIAG_STOREONLY)
         // diagnostic ceiling (tools/build_variant.sh "-DSDMM_SPLIT_DIAG_STOREONLY"):
@@ -552,11 +571,12 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
         // rare angle case anywhere in the tile (c < -0.9999995; its bits,
         // unsigned, exceed those of -0.9999995f) or a NaN: redo the tile with
         // the reference's quirks (wave-uniform, a few tiles per launch)
-        const bool odd = cbits > __builtin_bit_cast(uint32_t, -0.9999995f) || !(acc.x + acc.y >= 0.0f);
+        const bool odd = cbits > __builtin_bit_cast(uint32_t, -0.9999995f) || !((acc.x + acc.y) + (acc2.x + acc2.y) >= 0.0f);
         if (__builtin_amdgcn_ballot_w64(odd) != 0) {
             bf8 bd2 = Bd, bs2 = Bs;
             asm volatile("" : "+v"(bd2), "+v"(bs2));
             acc = f2{0.0f, 0.0f};
+            acc2 = f2{0.0f, 0.0f};
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 bf8 F[8];
@@ -568,7 +588,7 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
         }
         // posterior normalisation of sample col (mixture_model.h:170-191): the
         // lane's 4 R components, then the four lane groups of the sample
-        float S = acc.x + acc.y;
+        float S = (acc.x + acc.y) + (acc2.x + acc2.y);
         S += __shfl_xor(S, 16);
         S += __shfl_xor(S, 32);
         const float S2 = dif ? fmaf(1.0f - kHeuristicWeight, S, kHeuristicWeight * hp) : S;
