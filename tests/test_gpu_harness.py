@@ -67,11 +67,14 @@ def test_plugin_pattern_harness(pkg, oracle, synth, gpu, tmp_path):
         assert rel(p["weights"]) <= 1e-4, (rel(p["weights"]), rel(runs["accurate"]))
 
 
-def test_plugin_pattern_batched_equals_threaded(pkg, synth, gpu, tmp_path):
+@pytest.mark.parametrize("L", [6, 16])
+def test_plugin_pattern_batched_equals_threaded(pkg, synth, gpu, tmp_path, L):
     """The harness in batched mode (one sdmm_em_step_batched_host per plugin
     call over all leaves, sdmm_amd::em_step_leaves) gives bitwise the same
-    per-leaf mixtures as the thread-per-leaf sdmm_em_step_host pattern."""
-    K, L, N = 16, 6, 6 * 2500
+    per-leaf mixtures as the thread-per-leaf sdmm_em_step_host pattern (L
+    host threads at once, each creating, initialising, stepping and
+    destroying its own handle)."""
+    K, N = 16, L * 2500
     b = synth.em_batch(N, 128)
     with open(tmp_path / "in.bin", "wb") as f:
         np.array([N], np.int64).tofile(f)
