@@ -39,6 +39,12 @@
  * against other handles; calls on one handle must be serialised by the
  * caller.  Work is enqueued on the handle's HIP stream (sdmm_set_stream);
  * functions that return data to host memory synchronise that stream.
+ * Host threads may call the library at once on distinct handles (the
+ * reference's per-leaf worker threads, volpath_sdmm.cpp:287-311, and render
+ * threads, sdmm_proc.cpp:1086-1106): host data moves through the calling
+ * thread's pinned bounce buffer (never a DMA from caller memory), per-call
+ * device scratch is pooled per (device, stream), and no buffer is freed
+ * before the stream that used it has been synchronised.
  */
 #ifndef SDMM_GPU_H
 #define SDMM_GPU_H
@@ -717,6 +723,12 @@ int sdmm_write_exr(const char* path, int width, int height, const float* rgb, in
 
 const char* sdmm_last_error(void);
 int sdmm_abi_version(void);
+
+/* Library teardown (no reference counterpart: sdmm-lib holds no device state
+ * outside its contexts).  Frees the per-(device, stream) scratch pool that
+ * init / clone / k-means++ calls keep between calls.  Call only when no other
+ * thread is inside the library; later calls regrow the pool on demand. */
+int sdmm_release_cached_scratch(void);
 
 #ifdef __cplusplus
 }

@@ -194,6 +194,7 @@ def stats_len(K: int) -> int:
 
 
 EXPORTED_SYMBOLS = [
+    "sdmm_release_cached_scratch",
     "sdmm_em_params_default", "sdmm_create", "sdmm_destroy", "sdmm_num_components", "sdmm_layout",
     "sdmm_kernel_name",
     "sdmm_set_guide_capacity", "sdmm_set_guide_order", "sdmm_guide_fallback_count",

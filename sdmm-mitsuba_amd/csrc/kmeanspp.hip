@@ -21,11 +21,13 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 #include <string>
 #include <mutex>
 #include <vector>
 
 #include "../../include/sdmm_gpu.h"
+#include "host_xfer.h"
 
 #pragma clang fp contract(off)
 
@@ -231,30 +233,25 @@ int sdmm_kmeanspp_select(const sdmm_samples* s, const float* const normals[3], c
     const size_t o_idx = o_pdf + sizeof(double) * (size_t)ntot;
     const size_t o_pn = o_idx + ((sizeof(int64_t) * nu + 255) / 256) * 256;
     const size_t total = o_pn + sizeof(float) * 6 * nu;
-    // the scratch: a per-device block grown with hipMalloc, held under a lock
-    // until the stream sync below (no stream-ordered pool allocation on an
-    // entry point host threads may call at once; sdmm_api.cpp copy_prefix_many)
-    struct Scratch {
-        std::mutex mu;
-        char* p = nullptr;
-        size_t cap = 0;
-    };
-    static Scratch scratch[64];
-    if (device < 0 || device >= 64) return kfail(SDMM_E_INVALID, "sdmm_kmeanspp_select: device index out of range");
-    Scratch& sc = scratch[device];
-    std::lock_guard<std::mutex> hold(sc.mu);
-    if (e == hipSuccess && total > sc.cap) {
-        if (sc.p) (void)hipFree(sc.p);   // idle: every holder synced its stream
-        sc.p = nullptr;
-        sc.cap = 0;
-        const size_t cap = total + total / 2;
-        e = hipMalloc((void**)&sc.p, cap);
-        if (e == hipSuccess) sc.cap = cap;
-        else sc.p = nullptr;
+    // the scratch: the (device, stream) pool entry, held until the stream sync
+    // below; host data moves through the thread's pinned bounce buffer (host
+    // transfer rules, sdmm_api.cpp)
+    if (device < 0) return kfail(SDMM_E_INVALID, "sdmm_kmeanspp_select: device index out of range");
+    sdmm_detail::StreamScratch* sc = nullptr;
+    std::unique_lock<std::mutex> hold = sdmm_detail::stream_scratch(device, st, &sc);
+    if (e == hipSuccess) e = sdmm_detail::scratch_reserve(*sc, total);
+    char* d = sc->p;
+    const size_t o_hu = ((sizeof(KmppLeaf) * lv.size() + 15) / 16) * 16;   // pinned: leaves, draws
+    const size_t o_hi = o_hu + ((sizeof(float) * nu + 15) / 16) * 16;       // then the results back
+    const size_t o_hp = o_hi + ((sizeof(int64_t) * nu + 15) / 16) * 16;
+    char* pin = nullptr;
+    if (e == hipSuccess) e = sdmm_detail::bounce_buf(o_hp + sizeof(float) * 6 * nu, &pin);
+    if (e == hipSuccess) {
+        std::memcpy(pin, lv.data(), sizeof(KmppLeaf) * lv.size());
+        std::memcpy(pin + o_hu, uniforms, sizeof(float) * nu);
+        e = hipMemcpyAsync(d, pin, sizeof(KmppLeaf) * lv.size(), hipMemcpyHostToDevice, st);
     }
-    char* d = sc.p;
-    if (e == hipSuccess) e = hipMemcpyAsync(d, lv.data(), sizeof(KmppLeaf) * lv.size(), hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(d + o_u, uniforms, sizeof(float) * nu, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(d + o_u, pin + o_hu, sizeof(float) * nu, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(kmeanspp_kernel, dim3((unsigned)n_leaves), dim3(KB), 0, st, s->x[0], s->x[1], s->x[2],
                            normals[0], normals[1], normals[2], s->w, (const KmppLeaf*)d, n_pos,
@@ -262,15 +259,16 @@ int sdmm_kmeanspp_select(const sdmm_samples* s, const float* const normals[3], c
                            (int64_t*)(d + o_idx), (float*)(d + o_pn));
         e = hipGetLastError();
     }
-    std::vector<float> pn(6 * nu);
-    if (e == hipSuccess) e = hipMemcpyAsync(out_index, d + o_idx, sizeof(int64_t) * nu, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(pin + o_hi, d + o_idx, sizeof(int64_t) * nu, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess && (out_positions || out_normals))
-        e = hipMemcpyAsync(pn.data(), d + o_pn, sizeof(float) * 6 * nu, hipMemcpyDeviceToHost, st);
-    {   // always: the scratch is released to the next holder only when idle
+        e = hipMemcpyAsync(pin + o_hp, d + o_pn, sizeof(float) * 6 * nu, hipMemcpyDeviceToHost, st);
+    {   // always: the scratch and the bounce buffer are reused only when idle
         const hipError_t es = hipStreamSynchronize(st);
         if (e == hipSuccess) e = es;
     }
     if (e != hipSuccess) return kfail(SDMM_E_HIP, std::string("sdmm_kmeanspp_select: ") + hipGetErrorString(e));
+    std::memcpy(out_index, pin + o_hi, sizeof(int64_t) * nu);
+    const float* pn = (const float*)(pin + o_hp);
     for (size_t i = 0; i < nu; ++i)
         for (int a = 0; a < 3; ++a) {
             if (out_positions) out_positions[3 * i + a] = pn[6 * i + a];

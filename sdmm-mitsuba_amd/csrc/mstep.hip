@@ -669,11 +669,12 @@ mstep_batched_kernel(int K, int Kp, const MixDesc* __restrict__ mixes, float nor
 // workgroup b owns components 64 b + lane: the blend / MAP / PD test, then
 // MVTN::set from the PD test's own fp64 factorisation and every record field
 // but the weight ones, all in one thread (nothing goes through memory).  The
-// workgroup whose blends complete last (device-scope counter count[0]) runs
-// the order-dependent finish on its wave 1 while its wave 0 sets: the weights
-// normalised, both CDF prefixes, the scalars, and every record's weight
-// fields -- from the valid flag and detInv each blend publishes beside its
-// weight (what its set will leave) -- then re-arms the counter.  The
+// workgroup whose blends complete last (device-scope counter count[0],
+// wrapped back to 0 by that arrival's atomicInc) runs the order-dependent
+// finish on its wave 1 while its wave 0 sets: the weights normalised, both CDF
+// prefixes, the scalars, and every record's weight fields -- from the valid
+// flag and detInv each blend publishes beside its weight (what its set will
+// leave).  The
 // operations are mstep_body's, so the results are bitwise those of the
 // batched per-leaf form.
 __global__ void __launch_bounds__(128)
@@ -729,11 +730,13 @@ mstep_spread_kernel(int K, int Kp, const double* __restrict__ stats, int64_t nSa
         }
         if (SDMM_MSTEP_STOP <= 2) return;
         __threadfence();
-        if (lane == 0) role = (atomicAdd(&count[0], 1u) == nb - 1) ? 1 : 0;
+        // atomicInc wraps to 0 on the last arrival: the counter is re-armed by
+        // the same atomic that elects the finish, so no launch depends on a
+        // later store of an earlier one (an aborted launch cannot leave it set)
+        if (lane == 0) role = (atomicInc(&count[0], nb - 1) == nb - 1) ? 1 : 0;
     }
     if (SDMM_MSTEP_STOP <= 2) return;
     __syncthreads();
-    if (SDMM_MSTEP_STOP <= 5 && role && t == 0) count[0] = 0u;   // (diagnostic builds)
     if (SDMM_MSTEP_STOP <= 3) return;
     if (wv == 0) {
         if (k < K && setk[k]) set_component(k, emb, cov, C, have ? 1 : 0, L, Li);
@@ -759,7 +762,7 @@ mstep_spread_kernel(int K, int Kp, const double* __restrict__ stats, int64_t nSa
         if (lane == 0) mstep_scalars_store(S, sh, upd);
         if (SDMM_MSTEP_STOP <= 5) return;
         // every record's weight fields (pack_component's, from the valid
-        // flags and detInv the blends published), and the counter re-armed
+        // flags and detInv the blends published)
         for (int i = lane; i < Kp; i += 64) {
             float pi = 0.0f, dipi = 0.0f, w = 0.0f;
             if (i < K) {
@@ -771,7 +774,6 @@ mstep_spread_kernel(int K, int Kp, const double* __restrict__ stats, int64_t nSa
             ep[EP_DIPI * Kp + i] = dipi;
             gp[i * GP_STRIDE + GP_W] = w;
         }
-        if (lane == 0) count[0] = 0u;
     }
 }
 
@@ -1063,7 +1065,7 @@ hipError_t launch_pack_all(int K, int Kp, const CanonDev& C, float* ep, float* g
     return hipGetLastError();
 }
 
-// scratch: 3K doubles; count: a zeroed counter (re-armed by the kernel).
+// scratch: 3K doubles; count: a zeroed counter (self-re-arming: atomicInc wraps).
 hipError_t launch_mstep(int K, int Kp, const double* stats, int64_t nSamples, const CanonDev& C,
                         const EmStateDev& S, float* ep, float* gp, float norm5, double* newW, unsigned* count,
                         hipStream_t st) {

@@ -23,6 +23,7 @@
 #include "../../include/sdmm_gpu.h"
 #include "sdmm_device.h"
 #include "render_device.h"
+#include "host_xfer.h"
 
 #pragma clang fp contract(off)
 
@@ -198,6 +199,157 @@ void release_host(T*& p) {
     if (q) (void)hipHostFree(q);
 }
 
+}  // namespace
+
+// ==========================================================================
+// Host transfer and scratch rules for entry points that host threads call at
+// once (round 6; DESIGN.md section 2 "Concurrency"):
+//   * no DMA from or to caller (pageable) memory: caller data is copied on the
+//     host into the calling thread's pinned bounce buffer and moves by one
+//     pinned copy (the runtime's pageable path pins user pages on the fly;
+//     two threads' buffers can share a page, and one thread's unpin under the
+//     other's transfer is a fault the GPU reports, or a transfer that never
+//     completes);
+//   * per-call device scratch comes from a pool keyed by (device, stream),
+//     held until the call has synchronised that stream: threads on distinct
+//     streams never wait for each other, and nothing is freed under a kernel;
+//   * a buffer is only ever freed or regrown after the stream that used it
+//     has been synchronised.
+namespace sdmm_detail {
+
+namespace {
+struct PinnedBounce {
+    char* p = nullptr;
+    size_t cap = 0;
+    ~PinnedBounce() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+thread_local PinnedBounce t_bounce;
+
+struct ScratchEntry {
+    int device = -1;
+    hipStream_t st = nullptr;
+    std::mutex mu;
+    StreamScratch s;
+};
+std::mutex g_scratch_mu;
+std::vector<ScratchEntry*> g_scratch;
+}  // namespace
+
+hipError_t bounce_buf(size_t bytes, char** out) {
+    if (bytes > t_bounce.cap) {
+        if (t_bounce.p) (void)hipHostFree(t_bounce.p);   // idle: its last user synchronised
+        t_bounce.p = nullptr;
+        t_bounce.cap = 0;
+        const size_t cap = std::max<size_t>(bytes + bytes / 4, (size_t)64 << 10);
+        const hipError_t e = hipHostMalloc((void**)&t_bounce.p, cap, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            t_bounce.p = nullptr;
+            return e;
+        }
+        t_bounce.cap = cap;
+    }
+    *out = t_bounce.p;
+    return hipSuccess;
+}
+
+std::unique_lock<std::mutex> stream_scratch(int device, hipStream_t st, StreamScratch** out) {
+    ScratchEntry* e = nullptr;
+    {
+        std::lock_guard<std::mutex> g(g_scratch_mu);
+        for (ScratchEntry* x : g_scratch)
+            if (x->device == device && x->st == st) { e = x; break; }
+        if (!e) {
+            e = new ScratchEntry();
+            e->device = device;
+            e->st = st;
+            g_scratch.push_back(e);
+        }
+    }
+    *out = &e->s;
+    return std::unique_lock<std::mutex>(e->mu);
+}
+
+hipError_t scratch_reserve(StreamScratch& s, size_t bytes) {
+    if (bytes <= s.cap) return hipSuccess;
+    if (s.p) (void)hipFree(s.p);   // idle: every holder synchronised its stream before unlocking
+    s.p = nullptr;
+    s.cap = 0;
+    const size_t cap = std::max<size_t>(bytes + bytes / 2, (size_t)64 << 10);
+    const hipError_t e = hipMalloc((void**)&s.p, cap);
+    if (e == hipSuccess) s.cap = cap;
+    else s.p = nullptr;
+    return e;
+}
+
+void release_stream_scratch() {
+    std::lock_guard<std::mutex> g(g_scratch_mu);
+    for (ScratchEntry* x : g_scratch) {
+        {
+            std::lock_guard<std::mutex> h(x->mu);
+            if (x->s.p) {
+                (void)hipSetDevice(x->device);
+                (void)hipFree(x->s.p);
+            }
+        }
+        delete x;
+    }
+    g_scratch.clear();
+}
+
+}  // namespace sdmm_detail
+
+using sdmm_detail::bounce_buf;
+using sdmm_detail::scratch_reserve;
+using sdmm_detail::stream_scratch;
+using sdmm_detail::StreamScratch;
+
+namespace {
+
+// Copies between caller host memory and device memory as pinned DMAs through
+// the thread's bounce buffer, synchronised on st before return.  Items with a
+// NULL host pointer are skipped.
+struct XferItem {
+    void* host;
+    void* dev;
+    size_t bytes;
+};
+int xfer(const XferItem* items, int n, bool to_device, hipStream_t st) {
+    size_t total = 0;
+    for (int i = 0; i < n; ++i)
+        if (items[i].host) total += (items[i].bytes + 15) / 16 * 16;
+    if (total == 0) return SDMM_OK;
+    char* pin = nullptr;
+    HIP_TRY(bounce_buf(total, &pin));
+    size_t off = 0;
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < n && e == hipSuccess; ++i) {
+        const XferItem& it = items[i];
+        if (!it.host) continue;
+        if (to_device) {
+            std::memcpy(pin + off, it.host, it.bytes);
+            e = hipMemcpyAsync(it.dev, pin + off, it.bytes, hipMemcpyHostToDevice, st);
+        } else {
+            e = hipMemcpyAsync(pin + off, it.dev, it.bytes, hipMemcpyDeviceToHost, st);
+        }
+        off += (it.bytes + 15) / 16 * 16;
+    }
+    const hipError_t es = hipStreamSynchronize(st);   // always: the bounce buffer is reused
+    if (e == hipSuccess) e = es;
+    if (e != hipSuccess) return fail(SDMM_E_HIP, std::string("host transfer: ") + hipGetErrorString(e));
+    if (!to_device) {
+        off = 0;
+        for (int i = 0; i < n; ++i) {
+            const XferItem& it = items[i];
+            if (!it.host) continue;
+            std::memcpy(it.host, pin + off, it.bytes);
+            off += (it.bytes + 15) / 16 * 16;
+        }
+    }
+    return SDMM_OK;
+}
+
 // (float) pow((double)(float)INV_SQRT_TWO_PI, d) -- mvtn.h:351-352
 float norm_const(int d) {
     return (float)std::pow((double)(float)0.39894228040143267793994605993438186847585863116492, (double)d);
@@ -311,7 +463,7 @@ void hemisphere_init(const float* positions, const float* normals, int nPosition
 // with its last mixture
 struct Slab {
     void* p = nullptr;
-    int refs = 0;
+    std::atomic<int> refs{0};   // members may be destroyed from different host threads
     hipStream_t st = nullptr;
 };
 
@@ -343,7 +495,6 @@ struct sdmm_mix {
 
     // device memory
     void* block = nullptr;       // canonical + state + packed records
-    bool block_async = false;    // stream-ordered allocation (sdmm_create_on_stream)
     struct Slab* slab = nullptr; // block carved from a shared slab (sdmm_create_many_on_stream)
     CanonDev C{};
     EmStateDev S{};
@@ -502,6 +653,8 @@ int check_samples(const sdmm_samples* s) {
 
 int ensure_partials(sdmm_mix* m, int rows) {
     if (rows <= m->partial_rows) return SDMM_OK;
+    // the handle's earlier launches may still read or write the old rows
+    if (m->partials) HIP_TRY(hipStreamSynchronize(m->stream));
     release_dev(m->partials);
     m->partials = nullptr;
     int cap = rows < 1024 ? 1024 : rows;
@@ -602,6 +755,11 @@ int run_estep_stats(sdmm_mix* m, const sdmm_samples* s, double* stats_out) {
 extern "C" {
 
 const char* sdmm_last_error(void) { return g_err.c_str(); }
+
+int sdmm_release_cached_scratch(void) {
+    sdmm_detail::release_stream_scratch();
+    return SDMM_OK;
+}
 int sdmm_abi_version(void) { return SDMM_ABI_VERSION; }
 
 void sdmm_em_params_default(sdmm_em_params* p) {
@@ -786,7 +944,6 @@ int create_impl(int K, const sdmm_em_params* params, int device, hipStream_t ord
     }
     if (on_stream) {
         m->stream = ordered;
-        m->block_async = true;
     } else {
         if (hipStreamCreateWithFlags(&m->own_stream, hipStreamNonBlocking) != hipSuccess)
             return cleanup(fail(SDMM_E_HIP, "hipStreamCreate failed"));
@@ -800,19 +957,15 @@ int create_impl(int K, const sdmm_em_params* params, int device, hipStream_t ord
     }
     // one allocation for every fixed-size array (all 16-byte aligned)
     const size_t total = layout_block(m, nullptr);
-    if (on_stream) {
-        if (hipMallocAsync(&m->block, total, m->stream) != hipSuccess)
-            return cleanup(fail(SDMM_E_HIP, "hipMallocAsync failed"));
-        if (hipMemsetAsync(m->block, 0, total, m->stream) != hipSuccess)
-            return cleanup(fail(SDMM_E_HIP, "hipMemsetAsync failed"));
-    } else {
-        if (hipMalloc(&m->block, total) != hipSuccess) return cleanup(fail(SDMM_E_HIP, "hipMalloc failed"));
-        // on the handle's own stream: ordered before the init kernels below (a
-        // plain hipMemset runs on the null stream, which a non-blocking stream
-        // does not wait for -- it could land after them and zero the state)
-        if (hipMemsetAsync(m->block, 0, total, m->stream) != hipSuccess)
-            return cleanup(fail(SDMM_E_HIP, "hipMemsetAsync failed"));
-    }
+    // hipMalloc also for a handle created on a caller's stream (sdmm_clone,
+    // sdmm_create_on_stream): no stream-ordered pool allocation on an entry
+    // point host threads may call at once (host transfer rules above).  The
+    // memset goes on the handle's stream, ordered before the init kernels
+    // below (a plain hipMemset runs on the null stream, which a non-blocking
+    // stream does not wait for -- it could land after them and zero the state).
+    if (hipMalloc(&m->block, total) != hipSuccess) return cleanup(fail(SDMM_E_HIP, "hipMalloc failed"));
+    if (hipMemsetAsync(m->block, 0, total, m->stream) != hipSuccess)
+        return cleanup(fail(SDMM_E_HIP, "hipMemsetAsync failed"));
     layout_block(m, (char*)m->block);
     const size_t Kc = (size_t)K;
     double* sc = m->S.scalars;
@@ -870,7 +1023,7 @@ int create_many(int K, const sdmm_em_params* params, int device, hipStream_t st,
     for (int i = 0; i < n && !r; ++i) {
         if (i == fail_at) { r = fail(SDMM_E_HIP, "create_many: injected failure"); break; }
         r = create_impl(K, params, device, st, true, &out[i], (char*)slab->p + stride * (size_t)i);
-        if (!r) { out[i]->slab = slab; ++slab->refs; out[i]->block_async = false; }
+        if (!r) { out[i]->slab = slab; ++slab->refs; }
     }
     hipError_t e = r ? hipSuccess : hipMemsetAsync(slab->p, 0, stride * (size_t)n, st);
     if (!r && e == hipSuccess) {
@@ -914,8 +1067,7 @@ void sdmm_detail::destroy_impl(sdmm_mix* m, bool sync) {
             delete m->slab;
         }
     } else if (m->block) {
-        if (m->block_async) (void)hipFreeAsync(m->block, m->stream);
-        else (void)hipFree(m->block);
+        (void)hipFree(m->block);
     }
     if (m->partials) (void)hipFree(m->partials);
     if (m->guide_fb) (void)hipFree(m->guide_fb);
@@ -969,7 +1121,13 @@ int copy_prefix_many(const sdmm_mix* const* src, sdmm_mix* const* dst, int n, hi
     for (int i = 0; i < n; ++i)
         if (src[i]->stream != st) HIP_TRY(hipStreamSynchronize(src[i]->stream));
     const size_t bytes = (size_t)((char*)src[0]->stats - (char*)src[0]->C.weights);   // 16-aligned pieces
-    std::vector<void*> ptrs(2 * (size_t)n);
+    // the pointer table: built in the thread's pinned bounce buffer, uploaded
+    // into the (device, stream) scratch entry held until the sync below (host
+    // transfer rules at the top of this file)
+    const size_t tb = sizeof(void*) * 2 * (size_t)n;
+    char* pin = nullptr;
+    HIP_TRY(bounce_buf(tb, &pin));
+    void** ptrs = (void**)pin;
     for (int i = 0; i < n; ++i) {
         dst[i]->params = src[i]->params;
         dst[i]->guide_cap = src[i]->guide_cap;
@@ -978,37 +1136,13 @@ int copy_prefix_many(const sdmm_mix* const* src, sdmm_mix* const* dst, int n, hi
         ptrs[(size_t)i] = src[i]->C.weights;
         ptrs[(size_t)n + i] = dst[i]->C.weights;
     }
-    // the pointer table in a per-device block grown with hipMalloc under a
-    // lock held until the stream sync below.  (Round 5: a stream-ordered
-    // pool allocation here and in the init, with the pool's default release
-    // threshold of 0, is the pattern round 2's hang had -- pool allocations
-    // on many streams beside other host threads' synchronisations -- and the
-    // C++ plugin harness's thread-per-leaf run faulted once this round.)
-    struct TabScratch {
-        std::mutex mu;
-        void* p = nullptr;
-        size_t cap = 0;
-    };
-    static TabScratch tabs[64];
-    const int dev_i = src[0]->device;
-    if (dev_i < 0 || dev_i >= 64) return fail(SDMM_E_INVALID, "device index out of range");
-    TabScratch& ts = tabs[dev_i];
-    std::lock_guard<std::mutex> hold(ts.mu);
-    hipError_t e = hipSuccess;
-    const size_t tb = sizeof(void*) * ptrs.size();
-    if (tb > ts.cap) {
-        if (ts.p) (void)hipFree(ts.p);   // idle: every holder synced its stream
-        ts.p = nullptr;
-        ts.cap = 0;
-        const size_t cap = std::max<size_t>(tb + tb / 2, 64 << 10);
-        e = hipMalloc(&ts.p, cap);
-        if (e == hipSuccess) ts.cap = cap;
-        else ts.p = nullptr;
-    }
-    void* dtab = ts.p;
-    if (e == hipSuccess) e = hipMemcpyAsync(dtab, ptrs.data(), tb, hipMemcpyHostToDevice, st);
+    StreamScratch* ss = nullptr;
+    std::unique_lock<std::mutex> hold = stream_scratch(src[0]->device, st, &ss);
+    hipError_t e = scratch_reserve(*ss, tb);
+    void* dtab = ss->p;
+    if (e == hipSuccess) e = hipMemcpyAsync(dtab, ptrs, tb, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = launch_copy_many(n, dtab, (void**)dtab + n, bytes, st);
-    {   // always: ptrs is a host temporary and the table goes to the next holder
+    {   // always: the bounce buffer and the table go to the next user
         const hipError_t es = hipStreamSynchronize(st);
         if (e == hipSuccess) e = es;
     }
@@ -1157,14 +1291,20 @@ int sdmm_hemisphere_init_host(const float* positions, const float* normals, int 
 
 static int upload_and_set(sdmm_mix* m, const float* weights, const float* means, const float* covs) {
     const size_t K = (size_t)m->K;
-    std::vector<double> md(6 * K), cd(25 * K);
+    // fp64-widened means and covariances, then the weights, in the thread's
+    // pinned bounce buffer (no pageable DMA)
+    char* pin = nullptr;
+    HIP_TRY(bounce_buf(8 * 31 * K + 4 * K, &pin));
+    double* md = (double*)pin;
+    double* cd = md + 6 * K;
     for (size_t i = 0; i < 6 * K; ++i) md[i] = (double)means[i];
     for (size_t i = 0; i < 25 * K; ++i) cd[i] = (double)covs[i];
-    HIP_TRY(hipMemcpyAsync(m->tmp_mean, md.data(), 8 * 6 * K, hipMemcpyHostToDevice, m->stream));
-    HIP_TRY(hipMemcpyAsync(m->tmp_cov, cd.data(), 8 * 25 * K, hipMemcpyHostToDevice, m->stream));
-    HIP_TRY(hipMemcpyAsync(m->C.weights, weights, 4 * K, hipMemcpyHostToDevice, m->stream));
+    std::memcpy(cd + 25 * K, weights, 4 * K);
+    HIP_TRY(hipMemcpyAsync(m->tmp_mean, md, 8 * 6 * K, hipMemcpyHostToDevice, m->stream));
+    HIP_TRY(hipMemcpyAsync(m->tmp_cov, cd, 8 * 25 * K, hipMemcpyHostToDevice, m->stream));
+    HIP_TRY(hipMemcpyAsync(m->C.weights, cd + 25 * K, 4 * K, hipMemcpyHostToDevice, m->stream));
     HIP_TRY(launch_set_all(m->K, m->Kp, m->tmp_mean, m->tmp_cov, m->C, m->ep, m->gp, m->norm5, m->stream));
-    HIP_TRY(hipStreamSynchronize(m->stream));  // host vectors go out of scope
+    HIP_TRY(hipStreamSynchronize(m->stream));  // the bounce buffer is reused by the thread's next call
     m->initialised = true;
     return SDMM_OK;
 }
@@ -1238,23 +1378,11 @@ static int init_hemisphere_batched_impl(sdmm_mix* const* mixes, int n, const flo
     // widens them to the fp64 MVTN::set takes)
     const size_t Kz = (size_t)K;
     const size_t per = 4 * Kz + 4 * 6 * Kz + 4 * 25 * Kz + 4 * 25 * Kz + 4 * 9 * Kz;
-    // pinned staging: one grow-only buffer per device, held for the call (a
-    // fresh hipHostMalloc of ~10 MB per training pass pinned pages each time)
-    // (and the device block of the call, grown with hipMalloc under the same
-    // lock: no stream-ordered pool allocation on a path many host threads
-    // call at once -- see copy_prefix_many)
-    struct Staging {
-        std::mutex mu;
-        char* p = nullptr;
-        size_t cap = 0;
-        char* d = nullptr;
-        size_t dcap = 0;
-    };
-    static Staging staging[64];
-    const int dev_i = mixes[0]->device;
-    if (dev_i < 0 || dev_i >= 64) return fail(SDMM_E_INVALID, "device index out of range");
-    Staging& sg = staging[dev_i];
-    std::lock_guard<std::mutex> hold(sg.mu);
+    // pinned staging: the calling thread's bounce buffer; the device block of
+    // the call: the (device, stream) scratch pool entry, held until the
+    // stream sync below (host transfer rules at the top of this file)
+    StreamScratch* ss = nullptr;
+    std::unique_lock<std::mutex> hold = stream_scratch(mixes[0]->device, st, &ss);
     // the staging block is generated on the device (hemi_gen_batched_kernel):
     // only the inputs and the pointer table travel.  SDMM_HEMI_HOST=1 runs the
     // host generator into pinned memory and uploads the whole block instead.
@@ -1268,15 +1396,8 @@ static int init_hemisphere_batched_impl(sdmm_mix* const* mixes, int n, const flo
     const size_t in_bytes = host_gen ? 0 : 2 * pn_bytes + sizeof(float) * (size_t)n + sizeof(uint64_t) * (size_t)n + 16;
     const size_t up_off = host_gen ? 0 : stage_bytes;   // device offset of what is uploaded
     const size_t want = (host_gen ? stage_bytes : 0) + tab_bytes + in_bytes;
-    if (want > sg.cap) {
-        release_host(sg.p);
-        sg.p = nullptr;
-        sg.cap = 0;
-        const size_t cap = std::max<size_t>(want + want / 2, 1 << 20);
-        HIP_TRY(hipHostMalloc((void**)&sg.p, cap, hipHostMallocDefault));
-        sg.cap = cap;
-    }
-    char* pin = sg.p;   // pinned image of device bytes [up_off, stage_bytes + tab_bytes + in_bytes)
+    char* pin = nullptr;   // pinned image of device bytes [up_off, stage_bytes + tab_bytes + in_bytes)
+    HIP_TRY(bounce_buf(want, &pin));
     int r = SDMM_OK;
     if (host_gen) {
         // the host fp64 initialisations, in parallel over the mixtures (each is
@@ -1327,19 +1448,8 @@ static int init_hemisphere_batched_impl(sdmm_mix* const* mixes, int n, const flo
     // block and one kernel (a workgroup per mixture: copy in, MVTN::set, CDF,
     // pack)
     const size_t total = stage_bytes + tab_bytes + in_bytes;
-    hipError_t e0 = hipSuccess;
-    if (!r && total > sg.dcap) {
-        // the previous block is idle: every call syncs its stream before it
-        // releases the lock
-        if (sg.d) (void)hipFree(sg.d);
-        sg.d = nullptr;
-        sg.dcap = 0;
-        const size_t cap = std::max<size_t>(total + total / 2, 1 << 20);
-        e0 = hipMalloc((void**)&sg.d, cap);
-        if (e0 == hipSuccess) sg.dcap = cap;
-        else sg.d = nullptr;
-    }
-    char* d = sg.d;
+    hipError_t e0 = r ? hipSuccess : scratch_reserve(*ss, total);
+    char* d = ss->p;
     if (!r && e0 == hipSuccess) e0 = hipMemcpyAsync(d + up_off, pin, total - up_off, hipMemcpyHostToDevice, st);
     if (!r && e0 == hipSuccess && !host_gen)
         e0 = launch_hemi_gen_batched(n, K, (const float*)(d + in_off), (const float*)(d + in_off + pn_bytes),
@@ -1802,31 +1912,41 @@ int batched_iteration(sdmm_mix* const* mixes, int n_mix, const sdmm_samples* s, 
 
 extern "C" {
 
-// Stage host sample planes into m's staging buffer (device SoA view in *d).
+// Stage host sample planes into m's staging buffer (device SoA view in *d):
+// the planes are gathered on the host into the thread's pinned bounce buffer
+// and move as ONE pinned copy (no pageable DMA; host transfer rules at the top
+// of this file).  The caller synchronises m's stream before it returns.
 static int stage_host_samples(sdmm_mix* m, const sdmm_samples* s, sdmm_samples* d) {
     const size_t n = (size_t)s->n;
+    const size_t planes = 7 + (s->hpdf ? 1 : 0);
+    const size_t bytes = 4 * n * planes + (s->is_diffuse ? n : 0);
     const size_t need = n * (7 * 4 + 4 + 1) + 64;
     if (need > m->staging_bytes) {
-        HIP_TRY(hipStreamSynchronize(m->stream));
+        HIP_TRY(hipStreamSynchronize(m->stream));   // the old block may still be read
         release_dev(m->staging);
-        m->staging = nullptr;
+        m->staging_bytes = 0;
         HIP_TRY(hipMalloc(&m->staging, need));
         m->staging_bytes = need;
     }
+    char* pin = nullptr;
+    HIP_TRY(bounce_buf(bytes, &pin));
+    float* hp = (float*)pin;
     float* f = (float*)m->staging;
     *d = sdmm_samples{};
     for (int i = 0; i < 6; ++i) {
-        HIP_TRY(hipMemcpyAsync(f + i * n, s->x[i], 4 * n, hipMemcpyHostToDevice, m->stream));
+        std::memcpy(hp + i * n, s->x[i], 4 * n);
         d->x[i] = f + i * n;
     }
-    HIP_TRY(hipMemcpyAsync(f + 6 * n, s->w, 4 * n, hipMemcpyHostToDevice, m->stream));
+    std::memcpy(hp + 6 * n, s->w, 4 * n);
     d->w = f + 6 * n;
     if (s->hpdf) {
-        HIP_TRY(hipMemcpyAsync(f + 7 * n, s->hpdf, 4 * n, hipMemcpyHostToDevice, m->stream));
+        std::memcpy(hp + 7 * n, s->hpdf, 4 * n);
         d->hpdf = f + 7 * n;
     }
+    HIP_TRY(hipMemcpyAsync(f, hp, 4 * n * planes, hipMemcpyHostToDevice, m->stream));
     if (s->is_diffuse) {
-        HIP_TRY(hipMemcpyAsync(f + 8 * n, s->is_diffuse, n, hipMemcpyHostToDevice, m->stream));
+        std::memcpy(pin + 4 * n * planes, s->is_diffuse, n);
+        HIP_TRY(hipMemcpyAsync(f + 8 * n, pin + 4 * n * planes, n, hipMemcpyHostToDevice, m->stream));
         d->is_diffuse = (const uint8_t*)(f + 8 * n);
     }
     d->n = s->n;
@@ -1846,8 +1966,10 @@ int sdmm_em_step_batched_host(sdmm_mix* const* mixes, int n_mix, const sdmm_samp
     r = stage_host_samples(m0, s, &d);
     if (r) return r;
     r = sdmm_em_step_batched(mixes, n_mix, &d, seg, iterations);
+    // always: the bounce buffer is reused by the thread's next call
+    const hipError_t e = hipStreamSynchronize(m0->stream);
     if (r) return r;
-    HIP_TRY(hipStreamSynchronize(m0->stream));  // the host planes may be reused on return
+    if (e != hipSuccess) return fail(SDMM_E_HIP, std::string("sdmm_em_step_batched_host: ") + hipGetErrorString(e));
     return SDMM_OK;
 }
 
@@ -1864,8 +1986,10 @@ int sdmm_em_step_batched_host_iters(sdmm_mix* const* mixes, int n_mix, const sdm
     r = stage_host_samples(m0, s, &d);
     if (r) return r;
     r = sdmm_em_step_batched_iters(mixes, n_mix, &d, seg, iterations);
+    // always: the bounce buffer is reused by the thread's next call
+    const hipError_t e = hipStreamSynchronize(m0->stream);
     if (r) return r;
-    HIP_TRY(hipStreamSynchronize(m0->stream));  // the host planes may be reused on return
+    if (e != hipSuccess) return fail(SDMM_E_HIP, std::string("sdmm_em_step_batched_host: ") + hipGetErrorString(e));
     return SDMM_OK;
 }
 
@@ -1875,34 +1999,15 @@ int sdmm_em_step_host(sdmm_mix* m, const sdmm_samples* s, int iterations) {
     int r = check_samples(s);
     if (r) return r;
     if (s->n == 0) return SDMM_OK;
-    const size_t n = (size_t)s->n;
-    const size_t need = n * (7 * 4 + 4 + 1) + 64;
-    if (need > m->staging_bytes) {
-        release_dev(m->staging);
-        m->staging = nullptr;
-        HIP_TRY(hipMalloc(&m->staging, need));
-        m->staging_bytes = need;
-    }
-    float* f = (float*)m->staging;
-    sdmm_samples d{};
-    for (int i = 0; i < 6; ++i) {
-        HIP_TRY(hipMemcpyAsync(f + i * n, s->x[i], 4 * n, hipMemcpyHostToDevice, m->stream));
-        d.x[i] = f + i * n;
-    }
-    HIP_TRY(hipMemcpyAsync(f + 6 * n, s->w, 4 * n, hipMemcpyHostToDevice, m->stream));
-    d.w = f + 6 * n;
-    if (s->hpdf) {
-        HIP_TRY(hipMemcpyAsync(f + 7 * n, s->hpdf, 4 * n, hipMemcpyHostToDevice, m->stream));
-        d.hpdf = f + 7 * n;
-    }
-    if (s->is_diffuse) {
-        HIP_TRY(hipMemcpyAsync(f + 8 * n, s->is_diffuse, n, hipMemcpyHostToDevice, m->stream));
-        d.is_diffuse = (const uint8_t*)(f + 8 * n);
-    }
-    d.n = s->n;
-    r = sdmm_em_step(m, &d, iterations);
+    if (!m->initialised) return fail(SDMM_E_STATE, "mixture not initialised");
+    sdmm_samples d;
+    r = stage_host_samples(m, s, &d);
     if (r) return r;
-    HIP_TRY(hipStreamSynchronize(m->stream));  // the host planes may be reused on return
+    r = sdmm_em_step(m, &d, iterations);
+    // always: the bounce buffer is reused by the thread's next call
+    const hipError_t e = hipStreamSynchronize(m->stream);
+    if (r) return r;
+    if (e != hipSuccess) return fail(SDMM_E_HIP, std::string("sdmm_em_step_host: ") + hipGetErrorString(e));
     return SDMM_OK;
 }
 
@@ -2028,9 +2133,8 @@ int sdmm_get_params(const sdmm_mix* m, const sdmm_params_out* o) {
     if (!m || !o) return fail(SDMM_E_INVALID, "invalid argument");
     HIP_TRY(hipSetDevice(m->device));
     const size_t K = (size_t)m->K;
-    hipStream_t st = m->stream;
-    struct Item { void* dst; const void* src; size_t bytes; };
-    const Item items[] = {
+    double sc[SC_COUNT];
+    const XferItem items[] = {
         {o->weights, m->C.weights, 4 * K}, {o->cdf, m->C.cdf, 4 * K}, {o->mean, m->C.mean, 24 * K},
         {o->cov, m->C.cov, 100 * K}, {o->to, m->C.to, 36 * K}, {o->cholL, m->C.cholL, 100 * K},
         {o->cholLInv, m->C.cholLInv, 100 * K}, {o->detInv, m->C.detInv, 4 * K},
@@ -2038,12 +2142,10 @@ int sdmm_get_params(const sdmm_mix* m, const sdmm_params_out* o) {
         {o->margL, m->C.margL, 36 * K}, {o->margDetInv, m->C.margDetInv, 4 * K},
         {o->condL, m->C.condL, 16 * K}, {o->condLInv, m->C.condLInv, 16 * K},
         {o->condDetInv, m->C.condDetInv, 4 * K}, {o->valid, m->C.valid, 4 * K},
+        {sc, m->S.scalars, sizeof(sc)},
     };
-    for (const Item& it : items)
-        if (it.dst) HIP_TRY(hipMemcpyAsync(it.dst, it.src, it.bytes, hipMemcpyDeviceToHost, st));
-    double sc[SC_COUNT];
-    HIP_TRY(hipMemcpyAsync(sc, m->S.scalars, sizeof(sc), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    const int r = xfer(items, (int)(sizeof(items) / sizeof(items[0])), false, m->stream);
+    if (r) return r;
     if (o->normalization) *o->normalization = (float)sc[SC_NORM];
     return SDMM_OK;
 }
@@ -2053,15 +2155,13 @@ int sdmm_get_state(const sdmm_mix* m, double* scalars, double* T, double* sgW, d
     if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
     HIP_TRY(hipSetDevice(m->device));
     const size_t K = (size_t)m->K;
-    hipStream_t st = m->stream;
-    if (scalars) HIP_TRY(hipMemcpyAsync(scalars, m->S.scalars, 8 * SC_COUNT, hipMemcpyDeviceToHost, st));
-    if (T) HIP_TRY(hipMemcpyAsync(T, m->S.T, 8 * K, hipMemcpyDeviceToHost, st));
-    if (sgW) HIP_TRY(hipMemcpyAsync(sgW, m->S.sgW, 8 * K, hipMemcpyDeviceToHost, st));
-    if (sgM) HIP_TRY(hipMemcpyAsync(sgM, m->S.sgM, 40 * K, hipMemcpyDeviceToHost, st));
-    if (sgC) HIP_TRY(hipMemcpyAsync(sgC, m->S.sgC, 200 * K, hipMemcpyDeviceToHost, st));
-    if (bpriors) HIP_TRY(hipMemcpyAsync(bpriors, m->S.bPriors, 100 * K, hipMemcpyDeviceToHost, st));
-    if (bdepth) HIP_TRY(hipMemcpyAsync(bdepth, m->S.bDepth, 36 * K, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    const XferItem items[] = {
+        {scalars, m->S.scalars, 8 * SC_COUNT}, {T, m->S.T, 8 * K}, {sgW, m->S.sgW, 8 * K},
+        {sgM, m->S.sgM, 40 * K}, {sgC, m->S.sgC, 200 * K}, {bpriors, m->S.bPriors, 100 * K},
+        {bdepth, m->S.bDepth, 36 * K},
+    };
+    const int r = xfer(items, (int)(sizeof(items) / sizeof(items[0])), false, m->stream);
+    if (r) return r;
     return SDMM_OK;
 }
 
@@ -2070,15 +2170,13 @@ int sdmm_set_state(sdmm_mix* m, const double* scalars, const double* T, const do
     if (!m) return fail(SDMM_E_INVALID, "handle is NULL");
     HIP_TRY(hipSetDevice(m->device));
     const size_t K = (size_t)m->K;
-    hipStream_t st = m->stream;
-    if (scalars) HIP_TRY(hipMemcpyAsync(m->S.scalars, scalars, 8 * SC_COUNT, hipMemcpyHostToDevice, st));
-    if (T) HIP_TRY(hipMemcpyAsync(m->S.T, T, 8 * K, hipMemcpyHostToDevice, st));
-    if (sgW) HIP_TRY(hipMemcpyAsync(m->S.sgW, sgW, 8 * K, hipMemcpyHostToDevice, st));
-    if (sgM) HIP_TRY(hipMemcpyAsync(m->S.sgM, sgM, 40 * K, hipMemcpyHostToDevice, st));
-    if (sgC) HIP_TRY(hipMemcpyAsync(m->S.sgC, sgC, 200 * K, hipMemcpyHostToDevice, st));
-    if (bpriors) HIP_TRY(hipMemcpyAsync(m->S.bPriors, bpriors, 100 * K, hipMemcpyHostToDevice, st));
-    if (bdepth) HIP_TRY(hipMemcpyAsync(m->S.bDepth, bdepth, 36 * K, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    const XferItem items[] = {
+        {(void*)scalars, m->S.scalars, 8 * SC_COUNT}, {(void*)T, m->S.T, 8 * K}, {(void*)sgW, m->S.sgW, 8 * K},
+        {(void*)sgM, m->S.sgM, 40 * K}, {(void*)sgC, m->S.sgC, 200 * K}, {(void*)bpriors, m->S.bPriors, 100 * K},
+        {(void*)bdepth, m->S.bDepth, 36 * K},
+    };
+    const int r = xfer(items, (int)(sizeof(items) / sizeof(items[0])), true, m->stream);
+    if (r) return r;
     return SDMM_OK;
 }
 
@@ -2095,20 +2193,20 @@ int sdmm_restore_params(sdmm_mix* m, const sdmm_params_out* in) {
     if (!m || !in) return fail(SDMM_E_INVALID, "invalid argument");
     const size_t K = (size_t)m->K;
     hipStream_t st = m->stream;
-    struct Item { void* dst; const void* src; size_t bytes; };
-    const Item items[] = {
-        {m->C.weights, in->weights, 4 * K}, {m->C.cdf, in->cdf, 4 * K}, {m->C.mean, in->mean, 24 * K},
-        {m->C.cov, in->cov, 100 * K}, {m->C.to, in->to, 36 * K}, {m->C.cholL, in->cholL, 100 * K},
-        {m->C.cholLInv, in->cholLInv, 100 * K}, {m->C.detInv, in->detInv, 4 * K},
-        {m->C.muPremult, in->muPremult, 24 * K}, {m->C.condCov, in->condCov, 16 * K},
-        {m->C.margL, in->margL, 36 * K}, {m->C.margDetInv, in->margDetInv, 4 * K},
-        {m->C.condL, in->condL, 16 * K}, {m->C.condLInv, in->condLInv, 16 * K},
-        {m->C.condDetInv, in->condDetInv, 4 * K}, {m->C.valid, in->valid, 4 * K},
+    const XferItem items[] = {
+        {in->weights, m->C.weights, 4 * K}, {in->cdf, m->C.cdf, 4 * K}, {in->mean, m->C.mean, 24 * K},
+        {in->cov, m->C.cov, 100 * K}, {in->to, m->C.to, 36 * K}, {in->cholL, m->C.cholL, 100 * K},
+        {in->cholLInv, m->C.cholLInv, 100 * K}, {in->detInv, m->C.detInv, 4 * K},
+        {in->muPremult, m->C.muPremult, 24 * K}, {in->condCov, m->C.condCov, 16 * K},
+        {in->margL, m->C.margL, 36 * K}, {in->margDetInv, m->C.margDetInv, 4 * K},
+        {in->condL, m->C.condL, 16 * K}, {in->condLInv, m->C.condLInv, 16 * K},
+        {in->condDetInv, m->C.condDetInv, 4 * K}, {(void*)in->valid, m->C.valid, 4 * K},
     };
-    for (const Item& it : items)
-        if (!it.src) return fail(SDMM_E_INVALID, "sdmm_restore_params: every array is required");
+    for (const XferItem& it : items)
+        if (!it.host) return fail(SDMM_E_INVALID, "sdmm_restore_params: every array is required");
     HIP_TRY(hipSetDevice(m->device));
-    for (const Item& it : items) HIP_TRY(hipMemcpyAsync(it.dst, it.src, it.bytes, hipMemcpyHostToDevice, st));
+    const int r = xfer(items, (int)(sizeof(items) / sizeof(items[0])), true, st);
+    if (r) return r;
     HIP_TRY(launch_pack_all(m->K, m->Kp, m->C, m->ep, m->gp, m->norm5, st));
     HIP_TRY(hipStreamSynchronize(st));
     m->initialised = true;

@@ -22,9 +22,12 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <fstream>
 #include <memory>
 #include <mutex>
+#include <sstream>
+#include <thread>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -38,8 +41,38 @@ struct Error : std::runtime_error {
     Error(int c, const std::string& what) : std::runtime_error(what), code(c) {}
 };
 
+// The calling thread, for error reports (several render / optimisation
+// threads call the library at once).
+inline std::string thread_tag() {
+    std::ostringstream o;
+    o << std::this_thread::get_id();
+    return o.str();
+}
+
+// SDMM_AMD_DEBUG_SYNC=1: every mixture call is followed by a synchronisation
+// of the handle's stream, so an asynchronous fault (a kernel or copy the call
+// enqueued) is reported by the call and the thread that caused it instead of
+// by a later, unrelated call.  Debugging aid only (it serialises the stream).
+inline bool debug_sync() {
+    static const bool on = [] {
+        const char* e = std::getenv("SDMM_AMD_DEBUG_SYNC");
+        return e && *e && *e != '0';
+    }();
+    return on;
+}
+
 inline void check(int rc, const char* where) {
-    if (rc != SDMM_OK) throw Error(rc, std::string(where) + ": " + sdmm_last_error());
+    if (rc != SDMM_OK) throw Error(rc, std::string(where) + " [thread " + thread_tag() + "]: " + sdmm_last_error());
+}
+// ... for a call on handle h: with SDMM_AMD_DEBUG_SYNC the enqueued work is
+// checked before returning
+inline void check(int rc, const char* where, sdmm_mix* h) {
+    check(rc, where);
+    if (h && debug_sync()) {
+        const int r = sdmm_synchronize(h);
+        if (r != SDMM_OK)
+            throw Error(r, std::string(where) + " [debug sync, thread " + thread_tag() + "]: " + sdmm_last_error());
+    }
 }
 
 // jmm::Samples / sdmm::Data: SoA training data, appended from many render
@@ -94,7 +127,7 @@ class Mixture {
 
 public:
     explicit Mixture(int K, int device = 0, const sdmm_em_params* params = nullptr) {
-        check(sdmm_create(K, params, device, &h_), "sdmm_create");
+        check(sdmm_create(K, params, device, &h_), "sdmm_create", h_);
     }
     ~Mixture() { sdmm_destroy(h_); }
     // take ownership of a handle (checkpoint loading)
@@ -112,7 +145,7 @@ public:
 
     int components() const { return sdmm_num_components(h_); }
     sdmm_mix* handle() { return h_; }
-    void set_stream(void* hip_stream) { check(sdmm_set_stream(h_, hip_stream), "sdmm_set_stream"); }
+    void set_stream(void* hip_stream) { check(sdmm_set_stream(h_, hip_stream), "sdmm_set_stream", h_); }
     void synchronize() { check(sdmm_synchronize(h_), "sdmm_synchronize"); }
 
     // sdmm::initialize: seed positions = the first K/8 training points
@@ -124,24 +157,24 @@ public:
         for (int i = 0; i < n_pos; ++i)
             for (int d = 0; d < 3; ++d) pos[3 * i + d] = data.plane(d)[i];
         check(sdmm_init_hemisphere(h_, pos.data(), data.normals(), n_pos, depth_prior, spatial_distance, seed),
-              "sdmm_init_hemisphere");
+              "sdmm_init_hemisphere", h_);
     }
 
     // sdmm::em_step + sdmm::prepare on host-resident training data.
     void em_step(const TrainingData& data, int iterations = 1) {
         sdmm_samples s = data.view();
-        check(sdmm_em_step_host(h_, &s, iterations), "sdmm_em_step_host");
+        check(sdmm_em_step_host(h_, &s, iterations), "sdmm_em_step_host", h_);
     }
     // ... or on device-resident SoA planes (no PCIe copy).
     void em_step_device(const sdmm_samples& device_samples, int iterations = 1) {
-        check(sdmm_em_step(h_, &device_samples, iterations), "sdmm_em_step");
+        check(sdmm_em_step(h_, &device_samples, iterations), "sdmm_em_step", h_);
     }
 
     // em.iterations_run (the plugin's 2-while-below-4 schedule, volpath_sdmm.cpp:299-302)
     int iterations_run() const {
         const sdmm_mix* h = h_;
         int it = 0;
-        check(sdmm_iterations_run(&h, 1, &it), "sdmm_iterations_run");
+        check(sdmm_iterations_run(&h, 1, &it), "sdmm_iterations_run", h_);
         return it;
     }
 
@@ -155,7 +188,7 @@ public:
         o.weights = weights.data();
         o.mean = means.data();
         o.cov = covs.data();
-        check(sdmm_get_params(h_, &o), "sdmm_get_params");
+        check(sdmm_get_params(h_, &o), "sdmm_get_params", h_);
     }
 
 private:

@@ -67,13 +67,17 @@ def test_plugin_pattern_harness(pkg, oracle, synth, gpu, tmp_path):
         assert rel(p["weights"]) <= 1e-4, (rel(p["weights"]), rel(runs["accurate"]))
 
 
-@pytest.mark.parametrize("L", [6, 16])
-def test_plugin_pattern_batched_equals_threaded(pkg, synth, gpu, tmp_path, L):
+@pytest.mark.parametrize("L,debug", [(6, 0), (16, 0), (6, 1)])
+def test_plugin_pattern_batched_equals_threaded(pkg, synth, gpu, tmp_path, L, debug):
     """The harness in batched mode (one sdmm_em_step_batched_host per plugin
     call over all leaves, sdmm_amd::em_step_leaves) gives bitwise the same
     per-leaf mixtures as the thread-per-leaf sdmm_em_step_host pattern (L
     host threads at once, each creating, initialising, stepping and
-    destroying its own handle)."""
+    destroying its own handle).  debug: SDMM_AMD_DEBUG_SYNC=1, every mixture
+    call checked by a stream synchronisation (a fault names its call and
+    thread)."""
+    import os
+    env = dict(os.environ, SDMM_AMD_DEBUG_SYNC=str(debug))
     K, N = 16, L * 2500
     b = synth.em_batch(N, 128)
     with open(tmp_path / "in.bin", "wb") as f:
@@ -83,9 +87,10 @@ def test_plugin_pattern_batched_equals_threaded(pkg, synth, gpu, tmp_path, L):
         b["w"].astype(np.float32).tofile(f)
         b["normals"].astype(np.float32).tofile(f)
     exe = _build(tmp_path)
-    subprocess.run([str(exe), str(tmp_path / "in.bin"), str(tmp_path / "threads.bin")], check=True, timeout=120)
+    subprocess.run([str(exe), str(tmp_path / "in.bin"), str(tmp_path / "threads.bin")], check=True, timeout=120,
+                   env=env)
     subprocess.run([str(exe), str(tmp_path / "in.bin"), str(tmp_path / "batched.bin"), "batched"], check=True,
-                   timeout=120)
+                   timeout=120, env=env)
     a = np.fromfile(tmp_path / "threads.bin", np.float32)
     c = np.fromfile(tmp_path / "batched.bin", np.float32)
     assert a.size == L * K * 32
