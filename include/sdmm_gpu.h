@@ -466,6 +466,41 @@ int sdmm_guide_product_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix,
 int sdmm_pdf_product_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],
                                const float* const d[3], const sdmm_bsdf_table* bsdf, const int32_t* material,
                                const float* const frame[9], float* pdf, float* heuristic);
+
+/* Concurrent guided bounces from many render threads -- the reference's
+ * render workers call create_conditional / sample / pdf at once, each with
+ * thread_local scratch (sdmm_proc.cpp:1086-1106, volpath_sdmm.cpp:411-507).
+ *   sdmm_stree_publish   make the tree's current state readable from guide
+ *                        contexts: uploads the nodes and the mixture table
+ *                        (node_mix, or the bound one when NULL) and waits for
+ *                        the bound mixtures' pending work.  Call it from one
+ *                        thread after any change to the tree, the binding or
+ *                        the bound mixtures (once per render pass); a later
+ *                        change un-publishes the tree (context calls then fail
+ *                        with SDMM_E_STATE).
+ *   sdmm_guide_ctx_*     one render worker's context: its own HIP stream
+ *                        (hip_stream NULL: a new non-blocking stream the
+ *                        context owns) and its own guided-batch / product
+ *                        scratch.  Contexts of one tree run at once from
+ *                        different host threads with no lock; calls on ONE
+ *                        context must be serialised by the caller.
+ *   sdmm_ctx_guide_pdf_wavefront / sdmm_ctx_guide_product_wavefront
+ *                        sdmm_guide_pdf_wavefront / sdmm_guide_product_wavefront
+ *                        against the published tree on the context's stream
+ *                        (outputs bitwise equal; asynchronous -- synchronise
+ *                        the context's stream before reading them). */
+typedef struct sdmm_guide_ctx sdmm_guide_ctx;
+int sdmm_stree_publish(sdmm_stree* t, const sdmm_mix* const* node_mix);
+int sdmm_guide_ctx_create(sdmm_stree* t, void* hip_stream, sdmm_guide_ctx** out);
+void sdmm_guide_ctx_destroy(sdmm_guide_ctx* g);
+void* sdmm_guide_ctx_stream(const sdmm_guide_ctx* g);
+int sdmm_ctx_guide_pdf_wavefront(sdmm_guide_ctx* g, int64_t nq, const float* const c[3], const float* const u[3],
+                                 const float* const dgiven[3], const uint8_t* pdf_mode, float* const d[3], float* pdf,
+                                 int32_t* comp, int32_t* node_out);
+int sdmm_ctx_guide_product_wavefront(sdmm_guide_ctx* g, int64_t nq, const float* const c[3], const float* const u[3],
+                                     const float* choice, const float* const dgiven[3], const sdmm_bsdf_table* bsdf,
+                                     const int32_t* material, const float* const frame[9], float* const d[3],
+                                     float* pdf, int32_t* comp, float* heuristic, int32_t* node_out);
 /* Checkpoints (.asdmm, JSON; schema in DESIGN.md section 9).
  *   sdmm_save_json      the accelerator: sdmm::save_json(m_accelerator, path),
  *                       volpath_sdmm.cpp:117-126 (model_%05i.asdmm, once per

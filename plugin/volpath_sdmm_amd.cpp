@@ -50,8 +50,11 @@
  *     lives on the GPU: one sdmm_guiding handle;
  *   - Li runs bounce-synchronously over a tile of paths (a wavefront): the
  *     CPU threads intersect and evaluate Mitsuba's BSDFs, and ONE
- *     sdmm_guide_pdf_wavefront call per bounce and tile builds every
- *     vertex's conditional once and samples it or evaluates its pdf;
+ *     sdmm_ctx_guide_pdf_wavefront call per bounce and tile builds every
+ *     vertex's conditional once and samples it or evaluates its pdf; each
+ *     worker thread has its own guide context (stream + scratch) on the tree
+ *     published once per pass, so the workers' bounces run concurrently with
+ *     no lock, as the reference's per-thread calls do (sdmm_proc.cpp:1086-1106);
  *   - push_back_data (:876-965) is one sdmm_guiding_push per tile.
  */
 #include <algorithm>
@@ -123,6 +126,10 @@ struct Staging {
     int32_t* h_nv = nullptr;
     float* d_rec = nullptr;
     int32_t* d_nv = nullptr;
+    // the worker's guide context (its own stream and scratch on the published
+    // tree: sdmm_guide_ctx_*), NULL on unguided passes
+    sdmm_guide_ctx* ctx = nullptr;
+    hipStream_t stream = nullptr;
 
     void allocate(int64_t n, int vslots, bool product) {
         release();
@@ -171,7 +178,10 @@ struct Staging {
         h_comp = d_comp = h_nv = d_nv = nullptr;
         cap = 0;
     }
-    ~Staging() { release(); }
+    ~Staging() {
+        release();
+        if (ctx) sdmm_guide_ctx_destroy(ctx);
+    }
     float& rec(int f, int v, int64_t p, int64_t n) { return h_rec[((int64_t)f * V + v) * n + p]; }
 };
 
@@ -372,11 +382,20 @@ private:
         std::atomic<int> next{0};
         std::atomic<int64_t> len{0}, cnt{0};
         const bool guided = sdmm_guiding_trained(m_guiding) > 0;   // m_iteration != 0 (:311-316)
+        // the render phase reads the tree and its leaves' conditionals from
+        // every worker at once (sdmm_proc.cpp:1086-1106): publish them once,
+        // then each worker guides through its own context, with no lock
+        if (guided) check_sdmm(sdmm_stree_publish(sdmm_guiding_tree(m_guiding), nullptr), "sdmm_stree_publish");
         auto worker = [&](int wid) {
             ref<Sampler> sampler = static_cast<Sampler*>(scene->getSampler()->clone().get());
             Staging st;
             const int V = std::max(1, m_maxDepth > 0 ? std::min(m_maxDepth - 1, 10) : 10);
             st.allocate((int64_t)T * T * m_samplesPerIteration, V, m_sampleProduct && !m_bsdfOnly);
+            if (guided) {
+                check_sdmm(sdmm_guide_ctx_create(sdmm_guiding_tree(m_guiding), nullptr, &st.ctx),
+                           "sdmm_guide_ctx_create");
+                st.stream = (hipStream_t)sdmm_guide_ctx_stream(st.ctx);
+            }
             for (int t = next++; t < tx * ty && !m_cancelled; t = next++) {
                 const int x0 = (t % tx) * T, y0 = (t / tx) * T;
                 const int w = std::min(T, size.x - x0), h = std::min(T, size.y - y0);
@@ -728,13 +747,15 @@ private:
     }
 
     // One guided bounce of a tile's wavefront: sampleSurface / pdfSurface for
-    // nq queries (query planes of stride n) in one call on the model's stream.
+    // nq queries (query planes of stride n) in one call on the worker's own
+    // guide context and stream -- the workers run at once, as the reference's
+    // render threads do (sdmm_proc.cpp:1086-1106).
     void guideWavefront(Staging& st, int64_t n, int64_t nq) {
-        std::lock_guard<std::mutex> lock(m_gpuMutex);
+        const hipStream_t wst = st.stream;   // the worker's context stream
         for (int f = 0; f < 9; ++f)
             check_hip(hipMemcpyAsync(st.d_in + f * n, st.h_in + f * n, sizeof(float) * nq, hipMemcpyHostToDevice,
-                                     m_stream), "upload queries");
-        check_hip(hipMemcpyAsync(st.d_mode, st.h_mode, nq, hipMemcpyHostToDevice, m_stream), "upload modes");
+                                     wst), "upload queries");
+        check_hip(hipMemcpyAsync(st.d_mode, st.h_mode, nq, hipMemcpyHostToDevice, wst), "upload modes");
         const float* c[3] = {st.d_in, st.d_in + n, st.d_in + 2 * n};
         const float* u[3] = {st.d_in + 3 * n, st.d_in + 4 * n, st.d_in + 5 * n};
         const float* dg[3] = {st.d_in + 6 * n, st.d_in + 7 * n, st.d_in + 8 * n};
@@ -742,37 +763,36 @@ private:
         if (st.h_mat) {
             // sampleProduct: the per-query table rows, frames and draws
             const size_t L = (size_t)nq * kMaxLobes;
-            check_hip(hipMemcpyAsync(st.d_bw, st.h_bw, sizeof(float) * L, hipMemcpyHostToDevice, m_stream), "upload");
-            check_hip(hipMemcpyAsync(st.d_bmean, st.h_bmean, sizeof(float) * 3 * L, hipMemcpyHostToDevice, m_stream),
+            check_hip(hipMemcpyAsync(st.d_bw, st.h_bw, sizeof(float) * L, hipMemcpyHostToDevice, wst), "upload");
+            check_hip(hipMemcpyAsync(st.d_bmean, st.h_bmean, sizeof(float) * 3 * L, hipMemcpyHostToDevice, wst),
                       "upload");
-            check_hip(hipMemcpyAsync(st.d_bcov, st.h_bcov, sizeof(float) * 4 * L, hipMemcpyHostToDevice, m_stream),
+            check_hip(hipMemcpyAsync(st.d_bcov, st.h_bcov, sizeof(float) * 4 * L, hipMemcpyHostToDevice, wst),
                       "upload");
-            check_hip(hipMemcpyAsync(st.d_bdiff, st.h_bdiff, nq, hipMemcpyHostToDevice, m_stream), "upload");
-            check_hip(hipMemcpyAsync(st.d_mat, st.h_mat, sizeof(int32_t) * nq, hipMemcpyHostToDevice, m_stream),
+            check_hip(hipMemcpyAsync(st.d_bdiff, st.h_bdiff, nq, hipMemcpyHostToDevice, wst), "upload");
+            check_hip(hipMemcpyAsync(st.d_mat, st.h_mat, sizeof(int32_t) * nq, hipMemcpyHostToDevice, wst),
                       "upload");
             for (int f = 0; f < 10; ++f)
                 check_hip(hipMemcpyAsync(st.d_pf + f * n, st.h_pf + f * n, sizeof(float) * nq, hipMemcpyHostToDevice,
-                                         m_stream), "upload");
+                                         wst), "upload");
             const sdmm_bsdf_table tab{st.d_bw, st.d_bmean, st.d_bcov, (int)nq, kMaxLobes, st.d_bdiff};
             const float* F[9];
             for (int f = 0; f < 9; ++f) F[f] = st.d_pf + f * n;
-            check_sdmm(sdmm_guide_product_wavefront(sdmm_guiding_tree(m_guiding), nullptr, nq, c, u, st.d_pf + 9 * n,
-                                                    dg, &tab, st.d_mat, F, d, st.d_out + 3 * n, st.d_comp,
-                                                    st.d_pf + 10 * n, nullptr),
-                       "sdmm_guide_product_wavefront");
+            check_sdmm(sdmm_ctx_guide_product_wavefront(st.ctx, nq, c, u, st.d_pf + 9 * n, dg, &tab, st.d_mat, F, d,
+                                                        st.d_out + 3 * n, st.d_comp, st.d_pf + 10 * n, nullptr),
+                       "sdmm_ctx_guide_product_wavefront");
             check_hip(hipMemcpyAsync(st.h_pf + 10 * n, st.d_pf + 10 * n, sizeof(float) * nq, hipMemcpyDeviceToHost,
-                                     m_stream), "download h");
+                                     wst), "download h");
         } else {
-            check_sdmm(sdmm_guide_pdf_wavefront(sdmm_guiding_tree(m_guiding), nullptr, nq, c, u, dg, st.d_mode, d,
-                                                st.d_out + 3 * n, st.d_comp, nullptr),
-                       "sdmm_guide_pdf_wavefront");
+            check_sdmm(sdmm_ctx_guide_pdf_wavefront(st.ctx, nq, c, u, dg, st.d_mode, d, st.d_out + 3 * n, st.d_comp,
+                                                    nullptr),
+                       "sdmm_ctx_guide_pdf_wavefront");
         }
         for (int f = 0; f < 4; ++f)
             check_hip(hipMemcpyAsync(st.h_out + f * n, st.d_out + f * n, sizeof(float) * nq, hipMemcpyDeviceToHost,
-                                     m_stream), "download directions");
-        check_hip(hipMemcpyAsync(st.h_comp, st.d_comp, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, m_stream),
+                                     wst), "download directions");
+        check_hip(hipMemcpyAsync(st.h_comp, st.d_comp, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, wst),
                   "download components");
-        check_hip(hipStreamSynchronize(m_stream), "hipStreamSynchronize");
+        check_hip(hipStreamSynchronize(wst), "hipStreamSynchronize");
     }
 
     bool m_strictNormals = true;
@@ -782,7 +802,7 @@ private:
     Point m_sceneMin;
     Float m_spatialNorm = 1;
     sdmm_guiding* m_guiding = nullptr;
-    hipStream_t m_stream = nullptr;
+    hipStream_t m_stream = nullptr;   // the model's (training-data pushes, under m_gpuMutex)
     std::mutex m_gpuMutex;
     std::atomic<bool> m_cancelled{false};
 };

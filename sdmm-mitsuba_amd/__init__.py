@@ -180,6 +180,19 @@ def lib():
                                            C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.sdmm_init_hemisphere_kmeanspp_batched.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p * 3,
                                                             C.c_void_p, C.c_float, C.c_void_p, C.c_void_p]
+        L.sdmm_stree_publish.argtypes = [C.c_void_p, C.c_void_p]
+        L.sdmm_guide_ctx_create.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]
+        L.sdmm_guide_ctx_destroy.argtypes = [C.c_void_p]
+        L.sdmm_guide_ctx_destroy.restype = None
+        L.sdmm_guide_ctx_stream.argtypes = [C.c_void_p]
+        L.sdmm_guide_ctx_stream.restype = C.c_void_p
+        L.sdmm_ctx_guide_pdf_wavefront.argtypes = [C.c_void_p, C.c_int64, C.c_void_p * 3, C.c_void_p * 3,
+                                                   C.c_void_p * 3, C.c_void_p, C.c_void_p * 3, C.c_void_p,
+                                                   C.c_void_p, C.c_void_p]
+        L.sdmm_ctx_guide_product_wavefront.argtypes = [C.c_void_p, C.c_int64, C.c_void_p * 3, C.c_void_p * 3,
+                                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                       C.c_void_p * 9, C.c_void_p * 3, C.c_void_p, C.c_void_p,
+                                                       C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -224,6 +237,8 @@ EXPORTED_SYMBOLS = [
     "sdmm_em_step_batched_host_iters", "sdmm_write_exr", "sdmm_clone_many_on_stream", "sdmm_copy_many",
     "sdmm_guiding_update", "sdmm_kmeanspp_select", "sdmm_init_hemisphere_kmeanspp_batched",
     "sdmm_guide_product_wavefront", "sdmm_pdf_product_wavefront", "sdmm_stree_split_leaf_recurse_device",
+    "sdmm_stree_publish", "sdmm_guide_ctx_create", "sdmm_guide_ctx_destroy", "sdmm_guide_ctx_stream",
+    "sdmm_ctx_guide_pdf_wavefront", "sdmm_ctx_guide_product_wavefront",
 ]
 
 
@@ -1003,6 +1018,12 @@ class STree:
                                               comp.data_ptr(), None if node_out is None else node_out.data_ptr()))
         return d, pdf, comp
 
+    def publish(self, node_mix=None):
+        """sdmm_stree_publish: nodes + mixture table (node_mix, or the bound
+        one) uploaded and the mixtures' pending work done; GuideContext calls
+        may then run from any thread until the tree or binding changes."""
+        _check(lib().sdmm_stree_publish(self.h, self._node_table(node_mix)))
+
     def guide_product(self, node_mix, c, u, bsdf, material, frame, choice=None, dgiven=None, node_out=None):
         """Product sampling over the leaves (sdmm_guide_product_wavefront):
         per query the leaf's conditional times its material's learned-BSDF
@@ -1203,6 +1224,81 @@ class _LiStats(C.Structure):
 
 def _hip():
     return C.CDLL("libamdhip64.so")
+
+
+class GuideContext:
+    """One render worker's guiding context on a published STree
+    (sdmm_guide_ctx_*): its own HIP stream and scratch, so contexts run
+    guided bounces from different host threads at once, as the reference's
+    render workers call the conditional concurrently (sdmm_proc.cpp:1086-1106).
+    Calls are asynchronous on the context's stream; the output planes are the
+    caller's (device tensors) and valid after synchronize()."""
+
+    def __init__(self, tree, stream=None):
+        self.tree = tree
+        h = C.c_void_p()
+        ptr = None if stream is None else int(getattr(stream, "cuda_stream", stream))
+        _check(lib().sdmm_guide_ctx_create(tree.h, C.c_void_p(ptr or None), C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().sdmm_guide_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream_ptr(self) -> int:
+        return int(lib().sdmm_guide_ctx_stream(self.h) or 0)
+
+    def synchronize(self):
+        h = _hip()
+        h.hipStreamSynchronize.argtypes = [C.c_void_p]
+        assert h.hipStreamSynchronize(C.c_void_p(self.stream_ptr or None)) == 0
+
+    def guide_pdf_into(self, nq, c, u, dgiven, pdf_mode, d, pdf, comp):
+        """sdmm_ctx_guide_pdf_wavefront on raw device pointers (plane
+        pointers as int sequences): the thread-friendly form (no tensor
+        allocation; the GIL is released for the call)."""
+        P3 = C.c_void_p * 3
+        _check(lib().sdmm_ctx_guide_pdf_wavefront(self.h, nq, P3(*c), P3(*u), P3(*dgiven), C.c_void_p(pdf_mode),
+                                                  P3(*d), C.c_void_p(pdf), C.c_void_p(comp), None))
+
+    def guide_pdf(self, c, u, dgiven, pdf_mode):
+        import torch
+        nq = c[0].numel()
+        dev = c[0].device
+        d = [torch.empty(nq, device=dev) for _ in range(3)]
+        pdf = torch.empty(nq, device=dev)
+        comp = torch.empty(nq, device=dev, dtype=torch.int32)
+        self.guide_pdf_into(nq, [t.data_ptr() for t in c], [t.data_ptr() for t in u], [t.data_ptr() for t in dgiven],
+                            pdf_mode.data_ptr(), [t.data_ptr() for t in d], pdf.data_ptr(), comp.data_ptr())
+        return d, pdf, comp
+
+    def guide_product(self, c, u, bsdf, material, frame, choice=None, dgiven=None):
+        """sdmm_ctx_guide_product_wavefront (see STree.guide_product)."""
+        import torch
+        nq = c[0].numel()
+        dev = c[0].device
+        d = [torch.empty(nq, device=dev) for _ in range(3)]
+        pdf = torch.empty(nq, device=dev)
+        comp = torch.empty(nq, device=dev, dtype=torch.int32)
+        h = torch.empty(nq, device=dev)
+        P3 = C.c_void_p * 3
+        gg = None if dgiven is None else P3(*[t.data_ptr() for t in dgiven])   # kept alive over the call
+        _check(lib().sdmm_ctx_guide_product_wavefront(
+            self.h, nq, P3(*[t.data_ptr() for t in c]), P3(*[t.data_ptr() for t in u]),
+            None if choice is None else C.c_void_p(choice.data_ptr()),
+            None if gg is None else C.cast(gg, C.c_void_p),
+            C.byref(bsdf.c), C.c_void_p(material.data_ptr()), (C.c_void_p * 9)(*[t.data_ptr() for t in frame]),
+            P3(*[t.data_ptr() for t in d]), C.c_void_p(pdf.data_ptr()), C.c_void_p(comp.data_ptr()),
+            C.c_void_p(h.data_ptr()), None))
+        return d, pdf, comp, h
 
 
 class PathVertices:

@@ -2290,6 +2290,10 @@ struct sdmm_stree {
     int64_t split_cap = 0;
     void* split_small = nullptr;
     size_t split_small_cap = 0;
+    // sdmm_stree_publish: nodes, mixture table and the bound mixtures' pending
+    // work complete; guide contexts may read them from any thread until the
+    // next change (an upload of either clears it)
+    bool published = false;
 };
 
 namespace {
@@ -2512,6 +2516,7 @@ int st_find_host(const sdmm_stree* t, const float p[3]) {
 int st_upload(sdmm_stree* t) {
     if (!t->stream && !t->stream_set) HIP_TRY(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
     if (!t->dirty) return SDMM_OK;
+    t->published = false;
     const size_t bytes = 32 * t->nodes.size();
     if (bytes > t->dnodes_cap) {
         HIP_TRY(hipStreamSynchronize(t->stream));
@@ -3113,6 +3118,7 @@ int st_upload_table(sdmm_stree* t, const sdmm_mix* const* node_mix) {
     t->tab_cap = cap;
     t->tab_valid = true;
     if (same && t->dtab) return SDMM_OK;
+    t->published = false;
     HIP_TRY(hipStreamSynchronize(t->stream));   // the previous copy may still read tab_host
     const size_t nb = nn ? nn : 1;
     const size_t bytes = (sizeof(GuideMixHost) + sizeof(const float*)) * nb;
@@ -3196,6 +3202,38 @@ int st_guide_product(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq,
     return SDMM_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Guide contexts (round 6): the reference's render workers
+// call create_conditional / sample / pdf concurrently, each with thread_local
+// scratch (sdmm_proc.cpp:1086-1106).  A context is one worker's: its own
+// stream and guided-batch / product scratch.  Its wavefront calls read the
+// tree's device nodes and bound mixture table -- immutable once the tree is
+// published -- and write only the context's scratch and the caller's planes,
+// so contexts run at once from different host threads without a lock.
+}  // namespace
+
+struct sdmm_guide_ctx {
+    sdmm_stree* t = nullptr;
+    int device = 0;
+    int cus = 256;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int* guide_fb = nullptr;
+    int64_t guide_fb_cap = 0;
+    GuideSortScratch guide_sort{};
+    ProductScratch product_scratch{};
+};
+
+namespace {
+
+int ctx_prepare(sdmm_guide_ctx* g, int64_t nq) {
+    const sdmm_stree* t = g->t;
+    if (!t->published || t->dirty || !t->tab_valid)
+        return fail(SDMM_E_STATE, "guide context: the tree changed since sdmm_stree_publish (publish it again)");
+    HIP_TRY(hipSetDevice(g->device));
+    return grow_guide_scratch(g->guide_fb, g->guide_fb_cap, g->guide_sort, g->stream, nq);
+}
+
 }  // namespace
 
 extern "C" {
@@ -3206,6 +3244,97 @@ int sdmm_stree_bind_mixtures(sdmm_stree* t, const sdmm_mix* const* node_mix) {
     int r = st_upload(t);
     if (r) return r;
     return st_upload_table(t, node_mix);
+}
+
+int sdmm_stree_publish(sdmm_stree* t, const sdmm_mix* const* node_mix) {
+    if (!t) return fail(SDMM_E_INVALID, "invalid argument");
+    HIP_TRY(hipSetDevice(t->device));
+    int r = st_upload(t);
+    if (r) return r;
+    if (node_mix) {
+        r = st_upload_table(t, node_mix);
+        if (r) return r;
+    } else if (!t->tab_valid) {
+        return fail(SDMM_E_STATE, "sdmm_stree_publish: no mixtures bound to the current tree");
+    }
+    // the bound mixtures' pending work (EM steps, copies) and the uploads
+    for (hipStream_t st : t->mix_streams) HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipStreamSynchronize(t->stream));
+    t->published = true;
+    return SDMM_OK;
+}
+
+int sdmm_guide_ctx_create(sdmm_stree* t, void* hip_stream, sdmm_guide_ctx** out) {
+    if (!t || !out) return fail(SDMM_E_INVALID, "invalid argument");
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(t->device));
+    sdmm_guide_ctx* g = new (std::nothrow) sdmm_guide_ctx();
+    if (!g) return fail(SDMM_E_NOMEM, "out of host memory");
+    g->t = t;
+    g->device = t->device;
+    (void)hipDeviceGetAttribute(&g->cus, hipDeviceAttributeMultiprocessorCount, t->device);
+    if (g->cus <= 0) g->cus = 256;
+    if (hip_stream) {
+        g->stream = (hipStream_t)hip_stream;
+    } else {
+        const hipError_t e = hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            delete g;
+            return fail(SDMM_E_HIP, std::string("sdmm_guide_ctx_create: ") + hipGetErrorString(e));
+        }
+        g->own_stream = true;
+    }
+    *out = g;
+    return SDMM_OK;
+}
+
+void sdmm_guide_ctx_destroy(sdmm_guide_ctx* g) {
+    if (!g) return;
+    (void)hipSetDevice(g->device);
+    (void)hipStreamSynchronize(g->stream);
+    if (g->guide_fb) (void)hipFree(g->guide_fb);
+    if (g->product_scratch.base) (void)hipFree(g->product_scratch.base);
+    if (g->own_stream) (void)hipStreamDestroy(g->stream);
+    delete g;
+}
+
+void* sdmm_guide_ctx_stream(const sdmm_guide_ctx* g) { return g ? (void*)g->stream : nullptr; }
+
+int sdmm_ctx_guide_pdf_wavefront(sdmm_guide_ctx* g, int64_t nq, const float* const c[3], const float* const u[3],
+                                 const float* const dgiven[3], const uint8_t* pdf_mode, float* const d[3], float* pdf,
+                                 int32_t* comp, int32_t* node_out) {
+    if (!g || nq < 0) return fail(SDMM_E_INVALID, "invalid argument");
+    if (nq == 0) return SDMM_OK;
+    if (!c || !u || !dgiven || !pdf_mode || !d || !pdf || !comp) return fail(SDMM_E_INVALID, "invalid argument");
+    const int r = ctx_prepare(g, nq);
+    if (r) return r;
+    const sdmm_stree* t = g->t;
+    const GuideSortScratch* sort = (nq >= kTreeOrderMin) ? &g->guide_sort : nullptr;
+    HIP_TRY(launch_guide_tree(t->dnodes, t->dtab, t->tab_kmax, nq, c, u, dgiven, d, pdf, comp, node_out,
+                              norm_const(2), norm_const(3), t->tab_cap, g->guide_fb, g->guide_fb + 1, g->cus,
+                              g->stream, sort, pdf_mode, (int*)g->guide_sort.keys[0], (int)t->nodes.size()));
+    return SDMM_OK;
+}
+
+int sdmm_ctx_guide_product_wavefront(sdmm_guide_ctx* g, int64_t nq, const float* const c[3], const float* const u[3],
+                                     const float* choice, const float* const dgiven[3], const sdmm_bsdf_table* bsdf,
+                                     const int32_t* material, const float* const frame[9], float* const d[3],
+                                     float* pdf, int32_t* comp, float* heuristic, int32_t* node_out) {
+    if (!g || nq < 0) return fail(SDMM_E_INVALID, "invalid argument");
+    if (nq == 0) return SDMM_OK;
+    if (!c || !u || !d || !pdf || !comp || (choice && !dgiven)) return fail(SDMM_E_INVALID, "invalid argument");
+    int r = check_bsdf(bsdf, material, frame);
+    if (r) return r;
+    r = ctx_prepare(g, nq);
+    if (r) return r;
+    const sdmm_stree* t = g->t;
+    const GuideSortScratch* sort = (nq >= kTreeOrderMin) ? &g->guide_sort : nullptr;
+    HIP_TRY(launch_guide_product_tree(t->dnodes, t->dtab, t->dcctab, t->tab_kmax, nq, c, u, choice,
+                                      choice ? dgiven : nullptr, d, pdf, comp, node_out, material, frame, heuristic,
+                                      bsdf->weights, bsdf->means, bsdf->covs, bsdf->diffuse, bsdf->B, bsdf->M,
+                                      norm_const(2), norm_const(3), t->tab_cap, g->guide_fb, g->guide_fb + 1, g->cus,
+                                      g->stream, sort, &g->product_scratch, (int)t->nodes.size()));
+    return SDMM_OK;
 }
 
 int sdmm_guide_wavefront(sdmm_stree* t, const sdmm_mix* const* node_mix, int64_t nq, const float* const c[3],

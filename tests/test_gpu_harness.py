@@ -154,3 +154,57 @@ def test_guiding_model_cpp_driver_equals_python(pkg, gpu, tmp_path, async_):
         sqr, _ = read_exr(tmp_path / "exr" / f"iteration_sqr{it:05d}.exr")
         assert np.all(sqr >= exr * exr * (1 - 1e-5) - 1e-30)
     assert g.trained > 0
+
+
+def _build_guide_pattern(tmp_path):
+    exe = tmp_path / "guide_pattern_harness"
+    lib = ROOT / "sdmm-mitsuba_amd" / "lib"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                    f"-I{ROOT / 'include'}", str(ROOT / "tests" / "cpp" / "guide_pattern_harness.cpp"),
+                    f"-L{lib}", "-lsdmm_amd", "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{lib}",
+                    "-Wl,-rpath,/opt/rocm/lib", "-pthread", "-o", str(exe)], check=True)
+    return exe
+
+
+def write_guide_queries(path, c, u, dg, mode):
+    with open(path, "wb") as f:
+        np.array([c.shape[1]], np.int64).tofile(f)
+        for a in (c, u, dg):
+            a.astype(np.float32).tofile(f)
+        mode.astype(np.uint8).tofile(f)
+
+
+@pytest.mark.parametrize("K", [16, 128])
+def test_guide_pattern_threads_equal_single_thread(pkg, synth, gpu, tmp_path, K):
+    """The plugin's guided bounce from C++ worker threads, each with its own
+    guide context on the published tree (tests/cpp/guide_pattern_harness.cpp,
+    the pattern of plugin/volpath_sdmm_amd.cpp guideWavefront): 8 threads x
+    4096-query tiles == 1 thread, bitwise, and both == one
+    sdmm_guide_pdf_wavefront over the whole batch on the original mixtures
+    (the harness guides on the checkpoint's restored ones)."""
+    import torch
+    from test_gpu_wavefront import _queries, _tree_and_leaf_mixtures
+    b, t, mixes, leaves = _tree_and_leaf_mixtures(pkg, synth, K)
+    nq = 40000
+    c, u, d, ct, ut, dt = _queries(gpu, nq, 51, 0.0, 1.0)
+    mode = (np.random.default_rng(6).uniform(size=nq) < 0.5).astype(np.uint8)
+    dr, pr, cr = t.guide_pdf(mixes, ct, ut, dt, torch.from_numpy(mode).to(gpu))
+    torch.cuda.synchronize()
+    t.save_json(tmp_path / "model.asdmm", mixes)
+    write_guide_queries(tmp_path / "q.bin", c, u, d, mode)
+    exe = _build_guide_pattern(tmp_path)
+    outs = []
+    for threads in (1, 8):
+        r = subprocess.run([str(exe), str(tmp_path / "model.asdmm"), str(tmp_path / "q.bin"),
+                            str(tmp_path / f"o{threads}.bin"), str(threads), "4096", "2"],
+                           check=True, timeout=120, capture_output=True, text=True)
+        assert '"queries_per_s"' in r.stdout
+        outs.append(np.fromfile(tmp_path / f"o{threads}.bin", np.uint8))
+    np.testing.assert_array_equal(outs[0], outs[1])
+    o = outs[1]
+    dd = o[:12 * nq].view(np.float32).reshape(3, nq)
+    pp = o[12 * nq:16 * nq].view(np.float32)
+    cc = o[16 * nq:].view(np.int32)
+    np.testing.assert_array_equal(cc, cr.cpu().numpy())
+    np.testing.assert_array_equal(pp, pr.cpu().numpy())
+    np.testing.assert_array_equal(dd, np.stack([x.cpu().numpy() for x in dr]))

@@ -2,11 +2,12 @@
 """The drop-in plugin's per-tile guided bounce, timed.
 
 plugin/volpath_sdmm_amd.cpp (guideWavefront) serves each render tile's
-bounce with ONE sdmm_guide_pdf_wavefront call under a global mutex: upload the
-tile's query planes from pinned host staging (9 float planes + the mode
-byte), the call, download 4 float planes + the component index, synchronise.
-The mutex serialises the render threads' calls, so the pattern's throughput
-is that of back-to-back calls of the tile size.  This tool trains the Cornell
+bounce with ONE guided-wavefront call: upload the tile's query planes from
+pinned host staging (9 float planes + the mode byte), the call, download 4
+float planes + the component index, synchronise.  Round 5 ran it under a
+global mutex on the model's stream (back-to-back calls of the tile size);
+round 6 gives each render worker its own guide context (stream + scratch) on
+the published tree, so the workers' calls overlap -- the "threads_*" rows.  This tool trains the Cornell
 Box guiding model (K = 128 leaves, as the bench's cornell_k128 line), takes
 real queries -- the saved vertices of one guided render (condition c, the
 sampled world direction as the BSDF direction), uniforms from a fixed
@@ -111,6 +112,33 @@ def main():
                             "device_resident_ms": td * 1e3, "device_resident_queries_per_s": T / td,
                             "transfer_bytes_per_call": T * (9 * 4 + 1 + 4 * 4 + 4)}
         print(json.dumps({f"tile_{T}": out[f"tile_{T}"]}), flush=True)
+    # the reference's threading (sdmm_proc.cpp:1086-1106) through guide
+    # contexts: C++ worker threads, each its own context / stream / pinned
+    # staging on the published tree (tests/cpp/guide_pattern_harness.cpp)
+    import subprocess
+    import tempfile
+    from test_gpu_harness import write_guide_queries
+    tmp = Path(tempfile.mkdtemp(prefix="gpb_"))
+    tree.save_json(tmp / "model.asdmm", node_mix)
+    n_mt = min(n_all, 1 << 21)
+    write_guide_queries(tmp / "q.bin", c[:, :n_mt], u[:, :n_mt], dg[:, :n_mt], mode[:n_mt])
+    exe = tmp / "guide_pattern_harness"
+    lib = ROOT / "sdmm-mitsuba_amd" / "lib"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                    f"-I{ROOT / 'include'}", str(ROOT / "tests" / "cpp" / "guide_pattern_harness.cpp"),
+                    f"-L{lib}", "-lsdmm_amd", "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{lib}",
+                    "-Wl,-rpath,/opt/rocm/lib", "-pthread", "-o", str(exe)], check=True)
+    ref = None
+    for threads, T in ((1, 32768), (16, 32768), (16, 4096), (32, 32768)):
+        r = subprocess.run([str(exe), str(tmp / "model.asdmm"), str(tmp / "q.bin"), str(tmp / "o.bin"), str(threads),
+                            str(T), str(max(2, a.reps // 4))], check=True, timeout=300, capture_output=True, text=True)
+        row = json.loads(r.stdout.strip().splitlines()[-1])
+        got = np.fromfile(tmp / "o.bin", np.uint8)
+        if ref is None:
+            ref = got
+        row["bitwise_equal_to_1_thread"] = bool(np.array_equal(got, ref))
+        out[f"threads_{threads}_tile_{T}"] = row
+        print(json.dumps({f"threads_{threads}_tile_{T}": row}), flush=True)
     print(json.dumps(out), flush=True)
 
 
