@@ -580,6 +580,48 @@ int sdmm_stree_set_nodes(sdmm_stree* t, int n, const float* aabb, const int32_t*
  * Random numbers are counter based: sample (path, stream, dimension) of a
  * path are fixed, whatever runs beside it (render_device.h). */
 typedef struct sdmm_scene sdmm_scene;
+/* A glossy material's learned BSDF: the reference's BSDF::SDMM4
+ * (include/mitsuba/render/bsdf.h:310-314), a mixture over (theta_i, alpha) x
+ * direction loaded per material by sdmm::load_json (roughconductor.cpp:
+ * 230-245).  M <= 8 components; host arrays
+ *   weights[M]
+ *   means[M][5]  (theta, alpha, x, y, z): the condition's mean and the unit
+ *                direction in the canonical local frame (z = normal, wi at
+ *                azimuth 0)
+ *   covs[M][16]  row major over the tangent coordinates (theta, alpha, t1,
+ *                t2), t at the component's direction in its
+ *                Coordinates(mean) frame (sdmm_bsdf_table's convention).
+ * getDMM (roughconductor.cpp:182-194) conditions it on (theta_i =
+ * acos(min(1, cos theta_i)), alpha) with create_conditional_pruned(..., 2):
+ * this library's reading of that sdmm-lib call (absent from the snapshot) is
+ * in sdmm-mitsuba_amd/csrc/learned_bsdf.h and DESIGN.md section 10. */
+typedef struct sdmm_learned_bsdf4 {
+    int M;
+    const float* weights;
+    const float* means;
+    const float* covs;
+} sdmm_learned_bsdf4;
+/* getDMM + rotate_to_wo on the host for the local incident direction
+ * wi_local (wi_local[2] > 0; the plugin's learnedRow): *n_out (<= keep)
+ * lobes weights[n], means[n][3] (local, unit), covs[n][4] (2x2 in each
+ * mean's Coordinates frame); *n_out = 0: no valid conditional.  The device
+ * render forms the same lobes bitwise. */
+int sdmm_learned4_conditional(const sdmm_learned_bsdf4* m, float alpha, const float wi_local[3], int keep,
+                              int* n_out, float* weights, float* means, float* covs);
+/* The same for nq local incident directions on the device (wi_local: 3
+ * device planes; outputs device: weights[nq][keep], means[nq][keep][3],
+ * covs[nq][keep][4], n_out[nq] the lobes per query, unused lobes weight 0),
+ * asynchronous on hip_stream -- a plugin's whole wavefront of getDMM calls
+ * in one launch. */
+int sdmm_learned4_conditional_device(const sdmm_learned_bsdf4* m, float alpha, int64_t nq,
+                                     const float* const wi_local[3], int keep, float* weights, float* means,
+                                     float* covs, int32_t* n_out, void* hip_stream);
+/* sdmm::load_json / save_json of a learned BSDF (the material's .sdmm file,
+ * roughconductor.cpp:230-245) in this library's JSON form (DESIGN.md section
+ * 9): load with cap 0 is a size query (*M_out only); otherwise the arrays
+ * hold cap components. */
+int sdmm_learned4_save_json(const sdmm_learned_bsdf4* m, const char* path);
+int sdmm_learned4_load_json(const char* path, int cap, int* M_out, float* weights, float* means, float* covs);
 typedef struct {
     int n_quads;
     const float* quads;
@@ -607,6 +649,12 @@ typedef struct {
      * specularReflectance, [4] eta, [5] k (a gray conductor), [6] the
      * Beckmann alpha (isotropic, sampleVisible = false), [7] unused. */
     const float* bsdf_params;
+    /* nullable: n_bsdfs entries (appended in round 6) -- a rough conductor's
+     * learned BSDF, the material's SDMM4 (roughconductor.cpp:182-194,
+     * :230-245); M = 0 (or the array NULL): none, so getDMM fails and the
+     * product falls back to the plain conditional (sdmm_proc.cpp:327-392).
+     * Only rough conductors read theirs. */
+    const struct sdmm_learned_bsdf4* learned_models;
 } sdmm_scene_desc;
 /* The descriptor has grown across ABI revisions (bsdf_params was appended):
  * zero-initialise it (`sdmm_scene_desc d = {0};` / `memset`) before filling
@@ -627,11 +675,12 @@ typedef struct {
      * a diffuse BSDF set diffuse[b], the plugin's slice-0 rule) through
      * sdmm_guide_product_wavefront, with h = 0.3 (0.5 when the product is
      * unusable) and the BSDF/guide choice taken against that h.  A rough
-     * conductor's row is not read: each bounce forms its own lobes (getDMM
-     * conditioned on theta_i and alpha -- a synthetic 4-lobe stand-in for the
-     * suite's learned files, render.hip glossy_lobes -- then rotate_to_wo(wi)
-     * and the shading frame to world, sdmm_proc.cpp:340-355); the component
-     * index is then k * max(M, 4) + j.  0: the plain
+     * conductor's row is not read: each bounce conditions the conductor's
+     * learned model (sdmm_scene_desc.learned_models: getDMM on theta_i and
+     * alpha, pruned to 2 lobes -- none or no valid conditional: the plain
+     * conditional) then rotate_to_wo(wi) and the shading frame to world,
+     * sdmm_proc.cpp:340-355; the component index is then k * max(M, 2) + j
+     * with a conductor in the scene.  0: the plain
      * conditional with bsdf_fraction.  (bsdfOnly never trains, :416, so it
      * is the guided = 0 render; its learned-BSDF branch, :331/:384/:410, is
      * unreachable in the reference.) */

@@ -457,6 +457,46 @@ def push_training(aabb, child, rec, nv, V, path0, saved, seed):
             "lost": int(lost.value)}
 
 
+L4_MAX, L4_REC = 8, 22
+L4_STRIDE = 1 + L4_MAX * L4_REC
+
+
+def pack_learned_models(models, n_bsdfs):
+    """desc["learned_models"] (per BSDF None or (weights[M], means[M][5],
+    covs[M][16])) as the oracle's packed table: L4_STRIDE floats per BSDF,
+    [M, M records of (w, mean 5, cov 16)]; None when there are none."""
+    if not models:
+        return None
+    out = np.zeros((n_bsdfs, L4_STRIDE), np.float32)
+    for b, m in enumerate(models):
+        if m is None:
+            continue
+        w, mu, cv = (np.asarray(x, np.float32) for x in m)
+        M = len(w)
+        out[b, 0] = M
+        rec = np.concatenate([w.reshape(M, 1), mu.reshape(M, 5), cv.reshape(M, 16)], axis=1)
+        out[b, 1:1 + M * L4_REC] = rec.reshape(-1)
+    return np.ascontiguousarray(out)
+
+
+def learned4_conditional(model, alpha, wl, keep=2):
+    """or_learned4_conditional: the conductor's lobes (weights, local means,
+    2x2 covariances) of one SDMM4 at local incident direction wl."""
+    w, mu, cv = (np.asarray(x, np.float32) for x in model)
+    M = len(w)
+    rec = np.ascontiguousarray(np.concatenate([w.reshape(M, 1), mu.reshape(M, 5), cv.reshape(M, 16)], axis=1),
+                               np.float32)
+    ow = np.zeros(L4_MAX, np.float32)
+    om = np.zeros((L4_MAX, 3), np.float32)
+    oc = np.zeros((L4_MAX, 4), np.float32)
+    wl = np.ascontiguousarray(wl, np.float32)
+    f = lib().or_learned4_conditional
+    f.restype = C.c_int
+    vp = lambda a: a.ctypes.data_as(C.c_void_p)
+    n = f(vp(rec), C.c_int(M), C.c_float(alpha), vp(wl), C.c_int(keep), vp(ow), vp(om), vp(oc))
+    return ow[:n], om[:n], oc[:n]
+
+
 def li_render(desc: dict, aabb, child, node_mix=None, guided=False, spp=1, max_depth=10, rr_depth=10, h=0.5,
               V=9, seed=0, pixels=None, learned=None, threads=1):
     """SDMMRenderer::Li restated on the CPU (sdmm_oracle_li.inc) for a
@@ -501,12 +541,13 @@ def li_render(desc: dict, aabb, child, node_mix=None, guided=False, spp=1, max_d
     f.restype = C.c_int
     vp = lambda a: a.ctypes.data_as(C.c_void_p)
     bpar = f32(desc["bsdf_params"]) if "bsdf_params" in desc else None
+    lmod = pack_learned_models(desc.get("learned_models"), len(refl) // 3)
     rc = f(vp(quads), vp(flip), vp(bsdf), C.c_int(len(bsdf)), vp(refl), vp(bpar) if bpar is not None else None,
            vp(em), vp(rad), vp(cam),
            C.c_float(desc["fov_x_deg"]), C.c_float(desc["near_clip"]), C.c_int(W), C.c_int(H), vp(mn), vp(mx),
            vp(ch), tab, C.c_int(int(guided)), C.c_int(spp), C.c_int(max_depth), C.c_int(rr_depth), C.c_float(h),
            C.c_int(V), C.c_uint64(seed), C.c_int64(lo), C.c_int64(hi), C.c_int(1 if learned is not None else 0),
            vp(bw), vp(bm), vp(bc), vp(bd), C.c_int(M), C.c_int(kmax), vp(image), vp(image_sqr), vp(rec), vp(nv),
-           vp(comps), C.c_int(threads))
+           vp(comps), C.c_int(threads), vp(lmod) if lmod is not None else None)
     assert rc == 0, "or_li_render failed"
     return {"image": image, "image_sqr": image_sqr, "rec": rec, "nv": nv, "comps": comps}

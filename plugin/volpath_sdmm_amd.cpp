@@ -52,9 +52,10 @@
  *     CPU threads intersect and evaluate Mitsuba's BSDFs, and ONE
  *     sdmm_ctx_guide_pdf_wavefront call per bounce and tile builds every
  *     vertex's conditional once and samples it or evaluates its pdf; each
- *     worker thread has its own guide context (stream + scratch) on the tree
- *     published once per pass, so the workers' bounces run concurrently with
- *     no lock, as the reference's per-thread calls do (sdmm_proc.cpp:1086-1106);
+ *     bounce leases a guide context (stream + scratch) on the tree published
+ *     once per pass, from a pool shared by the workers (property
+ *     guideContexts, 4), so the workers' bounces run concurrently, as the
+ *     reference's per-thread calls do (sdmm_proc.cpp:1086-1106);
  *   - push_back_data (:876-965) is one sdmm_guiding_push per tile.
  */
 #include <algorithm>
@@ -76,6 +77,7 @@
 #include <hip/hip_runtime.h>
 
 #include "sdmm_gpu.h"
+#include "sdmm_amd.hpp"   // GuideContextPool (sdmm-mitsuba_amd/host)
 
 MTS_NAMESPACE_BEGIN
 
@@ -126,11 +128,6 @@ struct Staging {
     int32_t* h_nv = nullptr;
     float* d_rec = nullptr;
     int32_t* d_nv = nullptr;
-    // the worker's guide context (its own stream and scratch on the published
-    // tree: sdmm_guide_ctx_*), NULL on unguided passes
-    sdmm_guide_ctx* ctx = nullptr;
-    hipStream_t stream = nullptr;
-
     void allocate(int64_t n, int vslots, bool product) {
         release();
         cap = n;
@@ -178,10 +175,7 @@ struct Staging {
         h_comp = d_comp = h_nv = d_nv = nullptr;
         cap = 0;
     }
-    ~Staging() {
-        release();
-        if (ctx) sdmm_guide_ctx_destroy(ctx);
-    }
+    ~Staging() { release(); }
     float& rec(int f, int v, int64_t p, int64_t n) { return h_rec[((int64_t)f * V + v) * n + p]; }
 };
 
@@ -221,6 +215,7 @@ public:
         // this port's own
         m_device = props.getInteger("hipDevice", 0);
         m_tileSize = props.getInteger("wavefrontTile", 64);
+        m_guideContexts = props.getInteger("guideContexts", 4);
         if (m_rrDepth <= 0) Log(EError, "'rrDepth' must be set to a value greater than zero!");
         if (m_maxDepth <= 0 && m_maxDepth != -1)
             Log(EError, "'maxDepth' must be set to -1 (infinite) or a value greater than zero!");
@@ -238,6 +233,7 @@ public:
         m_optimizeAsync = stream->readBool();
         m_device = stream->readInt();
         m_tileSize = stream->readInt();
+        m_guideContexts = stream->readInt();
     }
 
     ~SDMMAmdPathTracer() {
@@ -256,6 +252,7 @@ public:
         stream->writeBool(m_optimizeAsync);
         stream->writeInt(m_device);
         stream->writeInt(m_tileSize);
+        stream->writeInt(m_guideContexts);
     }
 
     bool preprocess(const Scene* scene, RenderQueue* queue, const RenderJob* job, int sceneResID, int sensorResID,
@@ -385,17 +382,19 @@ private:
         // the render phase reads the tree and its leaves' conditionals from
         // every worker at once (sdmm_proc.cpp:1086-1106): publish them once,
         // then each worker guides through its own context, with no lock
-        if (guided) check_sdmm(sdmm_stree_publish(sdmm_guiding_tree(m_guiding), nullptr), "sdmm_stree_publish");
+        // then each bounce leases a guide context (stream + scratch) from a
+        // pool shared by the workers (sdmm_amd::GuideContextPool)
+        std::unique_ptr<sdmm_amd::GuideContextPool> pool;
+        if (guided) {
+            check_sdmm(sdmm_stree_publish(sdmm_guiding_tree(m_guiding), nullptr), "sdmm_stree_publish");
+            pool.reset(new sdmm_amd::GuideContextPool(sdmm_guiding_tree(m_guiding), m_guideContexts));
+        }
+        m_ctxPool = pool.get();
         auto worker = [&](int wid) {
             ref<Sampler> sampler = static_cast<Sampler*>(scene->getSampler()->clone().get());
             Staging st;
             const int V = std::max(1, m_maxDepth > 0 ? std::min(m_maxDepth - 1, 10) : 10);
             st.allocate((int64_t)T * T * m_samplesPerIteration, V, m_sampleProduct && !m_bsdfOnly);
-            if (guided) {
-                check_sdmm(sdmm_guide_ctx_create(sdmm_guiding_tree(m_guiding), nullptr, &st.ctx),
-                           "sdmm_guide_ctx_create");
-                st.stream = (hipStream_t)sdmm_guide_ctx_stream(st.ctx);
-            }
             for (int t = next++; t < tx * ty && !m_cancelled; t = next++) {
                 const int x0 = (t % tx) * T, y0 = (t / tx) * T;
                 const int w = std::min(T, size.x - x0), h = std::min(T, size.y - y0);
@@ -406,9 +405,10 @@ private:
                 cnt += c;
             }
         };
-        std::vector<std::thread> pool;
-        for (int i = 0; i < nCores; ++i) pool.emplace_back(worker, i);
-        for (auto& th : pool) th.join();
+        std::vector<std::thread> workers;
+        for (int i = 0; i < nCores; ++i) workers.emplace_back(worker, i);
+        for (auto& th : workers) th.join();
+        m_ctxPool = nullptr;
         pathLength = len;
         paths = cnt;
         return !m_cancelled;
@@ -747,11 +747,12 @@ private:
     }
 
     // One guided bounce of a tile's wavefront: sampleSurface / pdfSurface for
-    // nq queries (query planes of stride n) in one call on the worker's own
-    // guide context and stream -- the workers run at once, as the reference's
+    // nq queries (query planes of stride n) in one call on a leased guide
+    // context and its stream -- the workers run at once, as the reference's
     // render threads do (sdmm_proc.cpp:1086-1106).
     void guideWavefront(Staging& st, int64_t n, int64_t nq) {
-        const hipStream_t wst = st.stream;   // the worker's context stream
+        const sdmm_amd::GuideContextPool::Lease lease = m_ctxPool->acquire();
+        const hipStream_t wst = (hipStream_t)lease.stream();
         for (int f = 0; f < 9; ++f)
             check_hip(hipMemcpyAsync(st.d_in + f * n, st.h_in + f * n, sizeof(float) * nq, hipMemcpyHostToDevice,
                                      wst), "upload queries");
@@ -777,13 +778,13 @@ private:
             const sdmm_bsdf_table tab{st.d_bw, st.d_bmean, st.d_bcov, (int)nq, kMaxLobes, st.d_bdiff};
             const float* F[9];
             for (int f = 0; f < 9; ++f) F[f] = st.d_pf + f * n;
-            check_sdmm(sdmm_ctx_guide_product_wavefront(st.ctx, nq, c, u, st.d_pf + 9 * n, dg, &tab, st.d_mat, F, d,
+            check_sdmm(sdmm_ctx_guide_product_wavefront(lease.get(), nq, c, u, st.d_pf + 9 * n, dg, &tab, st.d_mat, F, d,
                                                         st.d_out + 3 * n, st.d_comp, st.d_pf + 10 * n, nullptr),
                        "sdmm_ctx_guide_product_wavefront");
             check_hip(hipMemcpyAsync(st.h_pf + 10 * n, st.d_pf + 10 * n, sizeof(float) * nq, hipMemcpyDeviceToHost,
                                      wst), "download h");
         } else {
-            check_sdmm(sdmm_ctx_guide_pdf_wavefront(st.ctx, nq, c, u, dg, st.d_mode, d, st.d_out + 3 * n, st.d_comp,
+            check_sdmm(sdmm_ctx_guide_pdf_wavefront(lease.get(), nq, c, u, dg, st.d_mode, d, st.d_out + 3 * n, st.d_comp,
                                                     nullptr),
                        "sdmm_ctx_guide_pdf_wavefront");
         }
@@ -803,6 +804,8 @@ private:
     Float m_spatialNorm = 1;
     sdmm_guiding* m_guiding = nullptr;
     hipStream_t m_stream = nullptr;   // the model's (training-data pushes, under m_gpuMutex)
+    int m_guideContexts = 4;          // guide contexts shared by the workers (one per hardware queue)
+    sdmm_amd::GuideContextPool* m_ctxPool = nullptr;   // the pass's (renderPass)
     std::mutex m_gpuMutex;
     std::atomic<bool> m_cancelled{false};
 };

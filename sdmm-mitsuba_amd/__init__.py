@@ -180,6 +180,13 @@ def lib():
                                            C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.sdmm_init_hemisphere_kmeanspp_batched.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p * 3,
                                                             C.c_void_p, C.c_float, C.c_void_p, C.c_void_p]
+        L.sdmm_learned4_conditional.argtypes = [C.c_void_p, C.c_float, C.c_void_p, C.c_int, C.POINTER(C.c_int),
+                                                C.c_void_p, C.c_void_p, C.c_void_p]
+        L.sdmm_learned4_save_json.argtypes = [C.c_void_p, C.c_char_p]
+        L.sdmm_learned4_conditional_device.argtypes = [C.c_void_p, C.c_float, C.c_int64, C.c_void_p * 3, C.c_int,
+                                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.sdmm_learned4_load_json.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_int), C.c_void_p, C.c_void_p,
+                                              C.c_void_p]
         L.sdmm_stree_publish.argtypes = [C.c_void_p, C.c_void_p]
         L.sdmm_guide_ctx_create.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]
         L.sdmm_guide_ctx_destroy.argtypes = [C.c_void_p]
@@ -239,6 +246,8 @@ EXPORTED_SYMBOLS = [
     "sdmm_guide_product_wavefront", "sdmm_pdf_product_wavefront", "sdmm_stree_split_leaf_recurse_device",
     "sdmm_stree_publish", "sdmm_guide_ctx_create", "sdmm_guide_ctx_destroy", "sdmm_guide_ctx_stream",
     "sdmm_ctx_guide_pdf_wavefront", "sdmm_ctx_guide_product_wavefront",
+    "sdmm_learned4_conditional", "sdmm_learned4_save_json", "sdmm_learned4_load_json",
+    "sdmm_learned4_conditional_device",
 ]
 
 
@@ -1202,7 +1211,75 @@ class _SceneDesc(C.Structure):
                 ("n_bsdfs", C.c_int), ("reflectance", C.c_void_p), ("emitter", C.c_void_p),
                 ("n_emitters", C.c_int), ("radiance", C.c_void_p), ("camera_to_world", C.c_float * 16),
                 ("fov_x_deg", C.c_float), ("near_clip", C.c_float), ("width", C.c_int), ("height", C.c_int),
-                ("bsdf_params", C.c_void_p)]
+                ("bsdf_params", C.c_void_p), ("learned_models", C.c_void_p)]
+
+
+class _Learned4(C.Structure):
+    _fields_ = [("M", C.c_int), ("weights", C.c_void_p), ("means", C.c_void_p), ("covs", C.c_void_p)]
+
+
+class LearnedBSDF:
+    """A glossy material's learned BSDF (sdmm_learned_bsdf4): the reference's
+    BSDF::SDMM4 over (theta_i, alpha) x direction (bsdf.h:310-314) --
+    weights[M], means[M][5] (theta, alpha, unit direction in the canonical
+    local frame), covs[M][16] over the tangent (theta, alpha, t1, t2)."""
+
+    def __init__(self, weights, means, covs):
+        self.weights = np.ascontiguousarray(weights, np.float32).reshape(-1)
+        M = self.weights.size
+        self.means = np.ascontiguousarray(means, np.float32).reshape(M, 5)
+        self.covs = np.ascontiguousarray(covs, np.float32).reshape(M, 16)
+        self.c = _Learned4(M, self.weights.ctypes.data, self.means.ctypes.data, self.covs.ctypes.data)
+
+    @property
+    def M(self):
+        return self.weights.size
+
+    def arrays(self):
+        return self.weights, self.means, self.covs
+
+    def save_json(self, path):
+        _check(lib().sdmm_learned4_save_json(C.byref(self.c), os.fsencode(path)))
+
+    @classmethod
+    def load_json(cls, path):
+        M = C.c_int()
+        _check(lib().sdmm_learned4_load_json(os.fsencode(path), 0, C.byref(M), None, None, None))
+        w = np.zeros(M.value, np.float32)
+        mu = np.zeros((M.value, 5), np.float32)
+        cv = np.zeros((M.value, 16), np.float32)
+        _check(lib().sdmm_learned4_load_json(os.fsencode(path), M.value, C.byref(M), w.ctypes.data, mu.ctypes.data,
+                                             cv.ctypes.data))
+        return cls(w, mu, cv)
+
+    def conditional_device(self, alpha, wl, keep=2, stream=None):
+        """sdmm_learned4_conditional_device over local directions wl (3
+        device tensors): (weights (nq, keep), means (nq, keep, 3), covs (nq,
+        keep, 4), n (nq,)) on the device."""
+        import torch
+        nq = wl[0].numel()
+        dev = wl[0].device
+        w = torch.empty((nq, keep), device=dev)
+        m = torch.empty((nq, keep, 3), device=dev)
+        c = torch.empty((nq, keep, 4), device=dev)
+        n = torch.empty(nq, dtype=torch.int32, device=dev)
+        st = torch.cuda.current_stream(dev) if stream is None else stream
+        _check(lib().sdmm_learned4_conditional_device(
+            C.byref(self.c), C.c_float(alpha), nq, (C.c_void_p * 3)(*[t.data_ptr() for t in wl]), keep,
+            w.data_ptr(), m.data_ptr(), c.data_ptr(), n.data_ptr(), C.c_void_p(int(st.cuda_stream) or None)))
+        return w, m, c, n
+
+    def conditional(self, alpha, wi_local, keep=2):
+        """getDMM + rotate_to_wo on the host (sdmm_learned4_conditional):
+        (weights[n], means[n][3], covs[n][4]), n = 0 without a valid one."""
+        wl = np.ascontiguousarray(wi_local, np.float32)
+        n = C.c_int()
+        w = np.zeros(8, np.float32)
+        m = np.zeros((8, 3), np.float32)
+        c = np.zeros((8, 4), np.float32)
+        _check(lib().sdmm_learned4_conditional(C.byref(self.c), C.c_float(alpha), wl.ctypes.data, keep, C.byref(n),
+                                               w.ctypes.data, m.ctypes.data, c.ctypes.data))
+        return w[:n.value], m[:n.value], c[:n.value]
 
 
 class _LiParams(C.Structure):
@@ -1346,6 +1423,15 @@ class Scene:
         if "bsdf_params" in self._keep:
             self._keep["bsdf_params"] = np.ascontiguousarray(self._keep["bsdf_params"], np.float32)
             d.bsdf_params = self._keep["bsdf_params"].ctypes.data
+        if desc.get("learned_models"):
+            # per BSDF: None or (weights, means, covs) / a LearnedBSDF
+            self._models = [None if m is None else (m if isinstance(m, LearnedBSDF) else LearnedBSDF(*m))
+                            for m in desc["learned_models"]]
+            self._model_tab = (_Learned4 * d.n_bsdfs)()
+            for b, m in enumerate(self._models):
+                if m is not None:
+                    self._model_tab[b] = m.c
+            d.learned_models = C.cast(self._model_tab, C.c_void_p)
         self.width, self.height, self.device = d.width, d.height, device
         h = C.c_void_p()
         _check(lib().sdmm_scene_create(C.byref(d), int(device), C.byref(h)))

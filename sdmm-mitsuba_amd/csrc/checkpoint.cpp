@@ -35,6 +35,7 @@ int set_error(int code, const char* msg);   // sdmm_api.cpp
 namespace {
 
 constexpr const char* kFormat = "sdmm-amd.asdmm";
+constexpr const char* kFormat4 = "sdmm-amd.sdmm4";   // a learned BSDF (sdmm_learned4_*)
 constexpr int kVersion = 1;
 constexpr int kScalars = 9;
 
@@ -355,7 +356,7 @@ bool iarr(const Value& o, const char* k, std::vector<int32_t>& out, size_t n) {
     });
 }
 
-int read_file(const char* path, std::string& s, Value& root) {
+int read_file(const char* path, std::string& s, Value& root, const char* format = kFormat) {
     FILE* fp = std::fopen(path, "rb");
     if (!fp) return err(SDMM_E_INVALID, std::string("cannot open ") + path);
     char buf[1 << 16];
@@ -369,8 +370,8 @@ int read_file(const char* path, std::string& s, Value& root) {
     const Value* f = root.get("format");
     const Value* ver = root.get("version");
     long long vv = 0;
-    if (!f || f->kind != Value::Str || f->text != kFormat || !ver || !num_int(*ver, vv) || vv != kVersion)
-        return err(SDMM_E_INVALID, std::string(path) + ": not an sdmm-amd checkpoint (format/version)");
+    if (!f || f->kind != Value::Str || f->text != format || !ver || !num_int(*ver, vv) || vv != kVersion)
+        return err(SDMM_E_INVALID, std::string(path) + ": not an " + format + " file (format/version)");
     return SDMM_OK;
 }
 
@@ -557,6 +558,55 @@ int sdmm_load_json(const char* path, int device, sdmm_stree** tree_out, sdmm_mix
 // ---------------------------------------------------------------------------
 // OpenEXR (scanline, NO_COMPRESSION, FLOAT channels B G R) -- the per-pass
 // image dumps of SDMMWorkResult::dumpIndividual (sdmm_wr.cpp:115-146).
+// A learned BSDF (sdmm_learned_bsdf4): {"format": "sdmm-amd.sdmm4",
+// "version": 1, "M": M, "weights": [M], "means": [5M], "covs": [16M]} --
+// floats written with 9 significant digits (exact round trip).
+int sdmm_learned4_save_json(const sdmm_learned_bsdf4* m, const char* path) {
+    if (!m || !path || m->M < 1 || m->M > 8 || !m->weights || !m->means || !m->covs)
+        return err(SDMM_E_INVALID, "sdmm_learned4_save_json: invalid argument");
+    Writer w;
+    w.raw("{\"format\":\"");
+    w.raw(kFormat4);
+    w.raw("\",\"version\":");
+    w.i64(kVersion);
+    w.raw(",\"M\":");
+    w.i64(m->M);
+    w.raw(",");
+    w.farr("weights", m->weights, (size_t)m->M);
+    w.farr("means", m->means, 5 * (size_t)m->M);
+    w.farr("covs", m->covs, 16 * (size_t)m->M);
+    w.close_obj();
+    w.raw("\n");
+    FILE* fp = std::fopen(path, "wb");
+    if (!fp) return err(SDMM_E_INVALID, std::string("cannot write ") + path);
+    const bool ok = std::fwrite(w.s.data(), 1, w.s.size(), fp) == w.s.size();
+    if (std::fclose(fp) != 0 || !ok) return err(SDMM_E_INVALID, std::string("write failed: ") + path);
+    return SDMM_OK;
+}
+
+int sdmm_learned4_load_json(const char* path, int cap, int* M_out, float* weights, float* means, float* covs) {
+    if (!path || !M_out || cap < 0 || (cap > 0 && (!weights || !means || !covs)))
+        return err(SDMM_E_INVALID, "sdmm_learned4_load_json: invalid argument");
+    std::string text;
+    Value root;
+    int r = read_file(path, text, root, kFormat4);
+    if (r) return r;
+    const Value* mv = root.get("M");
+    long long M = 0;
+    if (!mv || !num_int(*mv, M) || M < 1 || M > 8) return err(SDMM_E_INVALID, std::string(path) + ": bad M");
+    std::vector<float> w, mu, c;
+    if (!farr(root, "weights", w, (size_t)M) || !farr(root, "means", mu, 5 * (size_t)M) ||
+        !farr(root, "covs", c, 16 * (size_t)M))
+        return err(SDMM_E_INVALID, std::string(path) + ": weights / means / covs missing or of the wrong size");
+    *M_out = (int)M;
+    if (cap == 0) return SDMM_OK;
+    if (cap < M) return err(SDMM_E_INVALID, std::string(path) + ": cap smaller than M");
+    std::memcpy(weights, w.data(), sizeof(float) * w.size());
+    std::memcpy(means, mu.data(), sizeof(float) * mu.size());
+    std::memcpy(covs, c.data(), sizeof(float) * c.size());
+    return SDMM_OK;
+}
+
 int sdmm_write_exr(const char* path, int width, int height, const float* rgb, int spp, int iteration, float time) {
     if (!path || !rgb || width < 1 || height < 1) return err(SDMM_E_INVALID, "sdmm_write_exr: invalid argument");
     std::string h;

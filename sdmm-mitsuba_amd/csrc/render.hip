@@ -32,6 +32,7 @@
 // the reference's Mitsuba sampler itself is not reproducible here.
 #include "sdmm_device.h"
 #include "render_device.h"
+#include "learned_bsdf.h"
 
 #include <hipcub/hipcub.hpp>
 
@@ -231,57 +232,6 @@ __device__ __forceinline__ float conductor_eval_pdf(const float wi[3], const flo
     return D * H[2] / (4.0f * fabsf(dot3(wo, H)));
 }
 
-// The conductor's learned BSDF (RoughConductor::getDMM, roughconductor.cpp:
-// 182-196: the material's SDMM4 conditioned on (theta_i, alpha), sdmm-lib's
-// create_conditional_pruned) -- the suite's learned files are LFS pointers,
-// so a synthetic 4-lobe fit stands in: lobes in the canonical frame where wi
-// lies at azimuth 0, means at elevation theta_j on the mirror side (azimuth
-// pi), diagonal 2x2 covariances in each lobe's Coordinates(mean) frame:
-//   j   weight  theta_j                  sigma_1                  sigma_2
-//   0   0.55    theta                    1.5 alpha (1 + sin/2)    1.5 alpha
-//   1   0.20    0.6 theta                2.5 alpha                2.5 alpha
-//   2   0.15    min(theta + 0.35, 1.45)  3 alpha                  2 alpha
-//   3   0.10    0 (the normal)           0.5                      0.5
-// then sdmm_proc.cpp:340-355's rotate_to_wo(wi): the lobes rotated about the
-// normal onto wi's azimuth, each covariance re-expressed in the rotated mean's
-// Coordinates frame (the product kernels' convention, sdmm_bsdf_table).
-// Output: kGlossyLobes rows (weights, local means, covariances).
-__device__ __forceinline__ void glossy_lobes(const float wi[3], float alpha, float* w, float* mean, float* cov) {
-    const float theta = (float)acos((double)fminf(1.0f, wi[2]));
-    const float sth = (float)sin((double)theta);
-    const float th[kGlossyLobes] = {theta, 0.6f * theta, fminf(theta + 0.35f, 1.45f), 0.0f};
-    const float s1[kGlossyLobes] = {1.5f * alpha * (1.0f + 0.5f * sth), 2.5f * alpha, 3.0f * alpha, 0.5f};
-    const float s2[kGlossyLobes] = {1.5f * alpha, 2.5f * alpha, 2.0f * alpha, 0.5f};
-    const float wt[kGlossyLobes] = {0.55f, 0.2f, 0.15f, 0.1f};
-    // rotate_to_wo: R = Rz(phi_i), cos / sin from wi's azimuth (1, 0 at the pole)
-    const float sp2 = wi[0] * wi[0] + wi[1] * wi[1];
-    float c = 1.0f, s = 0.0f;
-    if (sp2 > 0.0f) {
-        const float rs = 1.0f / sqrtf(sp2);
-        c = wi[0] * rs;
-        s = wi[1] * rs;
-    }
-    for (int j = 0; j < kGlossyLobes; ++j) {
-        const float mc[3] = {-(float)sin((double)th[j]), 0.0f, (float)cos((double)th[j])};
-        float tc[9], tr[9];
-        coordinates_f(mc, tc);
-        const float m[3] = {c * mc[0] - s * mc[1], s * mc[0] + c * mc[1], mc[2]};
-        coordinates_f(m, tr);
-        // the canonical tangent axes rotated: R t1, R t2
-        const float r1[3] = {c * tc[0] - s * tc[1], s * tc[0] + c * tc[1], tc[2]};
-        const float r2[3] = {c * tc[3] - s * tc[4], s * tc[3] + c * tc[4], tc[5]};
-        // B = [f_i . (R t_j)], cov = B diag(s1^2, s2^2) B^T
-        const float b00 = dot3(tr, r1), b01 = dot3(tr, r2), b10 = dot3(tr + 3, r1), b11 = dot3(tr + 3, r2);
-        const float va = s1[j] * s1[j], vb = s2[j] * s2[j];
-        const float c00 = b00 * b00 * va + b01 * b01 * vb;
-        const float c01 = b00 * b10 * va + b01 * b11 * vb;
-        const float c11 = b10 * b10 * va + b11 * b11 * vb;
-        w[j] = wt[j];
-        mean[3 * j] = m[0]; mean[3 * j + 1] = m[1]; mean[3 * j + 2] = m[2];
-        cov[4 * j] = c00; cov[4 * j + 1] = c01; cov[4 * j + 2] = c01; cov[4 * j + 3] = c11;
-    }
-}
-
 __device__ __forceinline__ float& vrec(const PathsDev& P, int f, int v, int64_t p) {
     return P.rec[((int64_t)f * P.V + v) * P.P + p];
 }
@@ -460,14 +410,24 @@ li_compact_kernel(SceneDev S, PathsDev P, QueryDev Q, const int32_t* __restrict_
         Q.k_ch[j] = Q.ch[i];
         const float* bp = S.bpar ? S.bpar + kBsdfParams * QD.bsdf : nullptr;
         if (Q.lw && bp && bp[0] == (float)kBsdfConductor) {
-            // getDMM + rotate_to_wo (sdmm_proc.cpp:327-355): the query's own
-            // lobes, local frame, in its row of the extended table
+            // getDMM (roughconductor.cpp:182-194: the material's SDMM4
+            // conditioned on (theta_i, alpha), pruned to 2) + rotate_to_wo
+            // (sdmm_proc.cpp:340-355): the query's own lobes, local frame, in
+            // its row of the extended table; no model or no valid conditional:
+            // no learned BSDF (the plain conditional, h 0.5)
             const float wi[3] = {-P.dx[i], -P.dy[i], -P.dz[i]};
             const float wl[3] = {dot3(wi, s), dot3(wi, t), dot3(wi, QD.n)};
             const int64_t row = (int64_t)Q.lrow0 + j;
-            glossy_lobes(wl, bp[6], Q.lw + row * Q.lM, Q.lm + row * Q.lM * 3, Q.lc + row * Q.lM * 4);
-            for (int l = kGlossyLobes; l < Q.lM; ++l) Q.lw[row * Q.lM + l] = 0.0f;   // (skipped lobes)
-            Q.k_mat[j] = (int32_t)row;
+            const float* lm = S.lmodel ? S.lmodel + (size_t)kLearnedStride * QD.bsdf : nullptr;
+            const int M = lm ? (int)lm[0] : 0;
+            int kept = 0;
+            if (M > 0) {
+                const float theta = (float)acos((double)fminf(1.0f, wl[2]));
+                kept = learned4_conditional(lm + 1, M, theta, bp[6], wl, kLearnedKeep, Q.lw + row * Q.lM,
+                                            Q.lm + row * Q.lM * 3, Q.lc + row * Q.lM * 4);
+            }
+            for (int l = kept; l < Q.lM; ++l) Q.lw[row * Q.lM + l] = 0.0f;   // (skipped lobes)
+            Q.k_mat[j] = kept > 0 ? (int32_t)row : -1;
         }
     }
 }
@@ -842,6 +802,45 @@ hipError_t launch_li_shade(const SceneDev& S, const PathsDev& P, const QueryDev&
                        product);
     return hipGetLastError();
 }
+// getDMM + rotate_to_wo for a batch of local incident directions against one
+// learned model (sdmm_learned4_conditional_device): query q's lobes at
+// w[q * keep ..], mean[(q * keep + j) * 3 ..], cov[(q * keep + j) * 4 ..],
+// its lobe count n[q] (0: no valid conditional, or cos theta_i <= 0)
+struct Learned4Rec {
+    float r[kLearnedMaxComp * kLearnedRec];
+};
+__global__ void __launch_bounds__(256)
+learned4_kernel(Learned4Rec model, int M, float alpha, int64_t nq, const float* __restrict__ w0,
+                const float* __restrict__ w1, const float* __restrict__ w2, int keep, float* __restrict__ w,
+                float* __restrict__ mean, float* __restrict__ cov, int32_t* __restrict__ n) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    const float wl[3] = {w0[q], w1[q], w2[q]};
+    int kept = 0;
+    if (wl[2] > 0.0f) {
+        const float theta = (float)acos((double)fminf(1.0f, wl[2]));
+        float lw[kLearnedMaxComp], lm[3 * kLearnedMaxComp], lc[4 * kLearnedMaxComp];
+        kept = learned4_conditional(model.r, M, theta, alpha, wl, keep, lw, lm, lc);
+        for (int j = 0; j < kept; ++j) {
+            w[q * keep + j] = lw[j];
+            for (int i = 0; i < 3; ++i) mean[(q * keep + j) * 3 + i] = lm[3 * j + i];
+            for (int i = 0; i < 4; ++i) cov[(q * keep + j) * 4 + i] = lc[4 * j + i];
+        }
+    }
+    for (int j = kept; j < keep; ++j) w[q * keep + j] = 0.0f;
+    n[q] = kept;
+}
+hipError_t launch_learned4(const float* rec, int M, float alpha, int64_t nq, const float* const wl[3], int keep,
+                           float* w, float* mean, float* cov, int32_t* n, hipStream_t st) {
+    if (M < 0 || M > kLearnedMaxComp || keep < 1 || keep > kLearnedMaxComp) return hipErrorInvalidValue;
+    if (nq <= 0) return hipSuccess;
+    Learned4Rec m{};
+    for (int i = 0; i < M * kLearnedRec; ++i) m.r[i] = rec[i];
+    hipLaunchKernelGGL(learned4_kernel, grid_for(nq), dim3(256), 0, st, m, M, alpha, nq, wl[0], wl[1], wl[2], keep, w,
+                       mean, cov, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_li_film(const PathsDev& P, int64_t pix0, int64_t npix, int spp, int64_t plane, float* image,
                           float* image_sqr, hipStream_t st) {
     hipLaunchKernelGGL(li_film_kernel, grid_for(npix), dim3(256), 0, st, P, pix0, npix, spp, plane, image, image_sqr);

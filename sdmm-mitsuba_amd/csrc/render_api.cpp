@@ -3,6 +3,7 @@
 // (camera -> [query -> guided wavefront -> shade] x bounces -> film) and the
 // path / query / vertex buffers, grown on demand and reused across renders.
 #include <hip/hip_runtime.h>
+#include <xmmintrin.h>
 
 #include <hipcub/hipcub.hpp>
 
@@ -14,6 +15,7 @@
 
 #include "../../include/sdmm_gpu.h"
 #include "render_device.h"
+#include "learned_bsdf.h"
 
 // the scene's derived quad data in plain IEEE float (no FMA contraction), as
 // the CPU restatement of Li forms it (oracle/sdmm_oracle_li.inc)
@@ -31,6 +33,8 @@ hipError_t launch_li_compact(const SceneDev& S, const PathsDev& P, const QueryDe
                              void* temp, size_t temp_bytes, int product, hipStream_t st);
 hipError_t launch_li_film(const PathsDev& P, int64_t pix0, int64_t npix, int spp, int64_t plane, float* image,
                           float* image_sqr, hipStream_t st);
+hipError_t launch_learned4(const float* rec, int M, float alpha, int64_t nq, const float* const wl[3], int keep,
+                           float* w, float* mean, float* cov, int32_t* n, hipStream_t st);
 }  // namespace sdmm
 
 namespace sdmm_detail {
@@ -47,6 +51,7 @@ struct sdmm_scene {
     QuadDev* dquads = nullptr;
     float* drefl = nullptr;
     float* dbpar = nullptr;
+    float* dlmod = nullptr;   // kLearnedStride per BSDF (learned_models), null: none
     float* drad = nullptr;
     float smin[3] = {0, 0, 0}, snorm = 1.0f, tmin[3] = {0, 0, 0}, tmax[3] = {0, 0, 0};
     // per-render buffers (grown)
@@ -64,7 +69,7 @@ struct sdmm_scene {
     void* temp = nullptr;
     size_t temp_bytes = 0;
     // rough conductors with product sampling: the extended learned-BSDF
-    // table -- the caller's B rows re-strided to lM >= kGlossyLobes lobes, then
+    // table -- the caller's B rows re-strided to lM >= kLearnedKeep lobes, then
     // one row per compact query for the conductor's per-bounce lobes
     bool has_conductor = false;
     void* lt = nullptr;
@@ -148,11 +153,11 @@ int grow(sdmm_scene* s, int64_t P, int V, hipStream_t st) {
 
 // The extended learned-BSDF table of a render with rough conductors: rows
 // 0 .. B-1 the caller's (device arrays, re-strided to lM = max(M,
-// kGlossyLobes) lobes, the extra lobes weight 0 -- skipped by the product),
+// kLearnedKeep) lobes, the extra lobes weight 0 -- skipped by the product),
 // rows B .. B + cap - 1 the compact queries' own conductor lobes (written by
 // li_compact_kernel).  *tab describes it; s->Q points at the query rows.
 int extend_learned(sdmm_scene* s, const sdmm_bsdf_table& user, int64_t cap, hipStream_t st, sdmm_bsdf_table* tab) {
-    const int M = user.M, lM = std::max(M, kGlossyLobes), B = user.B;
+    const int M = user.M, lM = std::max(M, kLearnedKeep), B = user.B;
     const int64_t rows = (int64_t)B + cap;
     auto al = [](size_t b) { return (b + 255) / 256 * 256; };
     const size_t wb = al(sizeof(float) * (size_t)rows * lM), mb = 3 * wb, cb = 4 * wb, db = al((size_t)rows);
@@ -211,6 +216,31 @@ int sdmm_scene_create(const sdmm_scene_desc* d, int device, sdmm_scene** out) {
                              bp[5] >= 0.0f && std::isfinite(bp[5]) && bp[6] > 0.0f && bp[6] <= 2.0f);
             if (!ok) return fail(SDMM_E_INVALID, "sdmm_scene_create: invalid bsdf_params");
         }
+    // learned models: at most kLearnedMaxComp components, finite, unit directions
+    std::vector<float> lmod;
+    if (d->learned_models) {
+        lmod.assign((size_t)kLearnedStride * (size_t)d->n_bsdfs, 0.0f);
+        for (int b = 0; b < d->n_bsdfs; ++b) {
+            const sdmm_learned_bsdf4& L = d->learned_models[b];
+            if (L.M == 0) continue;
+            if (L.M < 0 || L.M > kLearnedMaxComp || !L.weights || !L.means || !L.covs)
+                return fail(SDMM_E_INVALID, "sdmm_scene_create: invalid learned model (1 <= M <= 8, arrays)");
+            float* o = lmod.data() + (size_t)kLearnedStride * b;
+            o[0] = (float)L.M;
+            for (int k = 0; k < L.M; ++k) {
+                float* r = o + 1 + kLearnedRec * k;
+                r[0] = L.weights[k];
+                for (int i = 0; i < 5; ++i) r[1 + i] = L.means[5 * k + i];
+                for (int i = 0; i < 16; ++i) r[6 + i] = L.covs[16 * k + i];
+                bool ok = r[0] >= 0.0f;
+                for (int i = 0; i < kLearnedRec; ++i) ok = ok && std::isfinite(r[i]);
+                const double n2 = (double)r[3] * r[3] + (double)r[4] * r[4] + (double)r[5] * r[5];
+                if (!ok || std::fabs(n2 - 1.0) > 1e-5)
+                    return fail(SDMM_E_INVALID, "sdmm_scene_create: learned model with a non-finite value, a "
+                                                "negative weight or a non-unit direction");
+            }
+        }
+    }
     *out = nullptr;
     std::vector<QuadDev> qs((size_t)d->n_quads);
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -268,6 +298,9 @@ int sdmm_scene_create(const sdmm_scene_desc* d, int device, sdmm_scene** out) {
     if (e == hipSuccess && d->bsdf_params)
         e = hipMemcpy(s->dbpar, d->bsdf_params, sizeof(float) * kBsdfParams * (size_t)d->n_bsdfs,
                       hipMemcpyHostToDevice);
+    if (e == hipSuccess && !lmod.empty()) e = hipMalloc(&s->dlmod, sizeof(float) * lmod.size());
+    if (e == hipSuccess && !lmod.empty())
+        e = hipMemcpy(s->dlmod, lmod.data(), sizeof(float) * lmod.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(s->dquads, qs.data(), sizeof(QuadDev) * qs.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipMemcpy(s->drefl, d->reflectance, sizeof(float) * 3 * (size_t)d->n_bsdfs, hipMemcpyHostToDevice);
@@ -282,6 +315,7 @@ int sdmm_scene_create(const sdmm_scene_desc* d, int device, sdmm_scene** out) {
     S.n_quads = d->n_quads;
     S.refl = s->drefl;
     S.bpar = s->dbpar;
+    S.lmodel = s->dlmod;
     S.rad = s->drad;
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 4; ++c) S.cam[4 * r + c] = d->camera_to_world[4 * r + c];
@@ -296,6 +330,57 @@ int sdmm_scene_create(const sdmm_scene_desc* d, int device, sdmm_scene** out) {
     return SDMM_OK;
 }
 
+int sdmm_learned4_conditional(const sdmm_learned_bsdf4* m, float alpha, const float wi_local[3], int keep,
+                              int* n_out, float* weights, float* means, float* covs) {
+    if (!m || !wi_local || !n_out || keep < 1 || m->M < 0 || m->M > kLearnedMaxComp ||
+        (m->M > 0 && (!m->weights || !m->means || !m->covs)) || !weights || !means || !covs)
+        return fail(SDMM_E_INVALID, "sdmm_learned4_conditional: invalid argument");
+    *n_out = 0;
+    if (m->M == 0 || !(wi_local[2] > 0.0f)) return SDMM_OK;   // getDMM: no model, or cosTheta(wi) <= 0
+    float rec[kLearnedMaxComp * kLearnedRec];
+    for (int k = 0; k < m->M; ++k) {
+        float* r = rec + kLearnedRec * k;
+        r[0] = m->weights[k];
+        for (int i = 0; i < 5; ++i) r[1 + i] = m->means[5 * k + i];
+        for (int i = 0; i < 16; ++i) r[6 + i] = m->covs[16 * k + i];
+    }
+    // the device's float environment: denormals flushed (-fgpu-flush-denormals-to-zero)
+    const unsigned csr = _mm_getcsr();
+    _mm_setcsr(csr | 0x8040u);
+    const float theta = (float)std::acos((double)std::fmin(1.0f, wi_local[2]));
+    float w[kLearnedMaxComp], mm[3 * kLearnedMaxComp], cc[4 * kLearnedMaxComp];
+    const int n = learned4_conditional(rec, m->M, theta, alpha, wi_local, keep, w, mm, cc);
+    _mm_setcsr(csr);
+    for (int j = 0; j < n; ++j) {
+        weights[j] = w[j];
+        for (int i = 0; i < 3; ++i) means[3 * j + i] = mm[3 * j + i];
+        for (int i = 0; i < 4; ++i) covs[4 * j + i] = cc[4 * j + i];
+    }
+    *n_out = n;
+    return SDMM_OK;
+}
+
+int sdmm_learned4_conditional_device(const sdmm_learned_bsdf4* m, float alpha, int64_t nq, const float* const wi_local[3],
+                                     int keep, float* weights, float* means, float* covs, int32_t* n_out,
+                                     void* hip_stream) {
+    if (!m || nq < 0 || keep < 1 || keep > kLearnedMaxComp || m->M < 0 || m->M > kLearnedMaxComp ||
+        (m->M > 0 && (!m->weights || !m->means || !m->covs)))
+        return fail(SDMM_E_INVALID, "sdmm_learned4_conditional_device: invalid argument");
+    if (nq == 0) return SDMM_OK;
+    if (!wi_local || !wi_local[0] || !wi_local[1] || !wi_local[2] || !weights || !means || !covs || !n_out)
+        return fail(SDMM_E_INVALID, "sdmm_learned4_conditional_device: invalid argument");
+    float rec[kLearnedMaxComp * kLearnedRec];
+    for (int k = 0; k < m->M; ++k) {
+        float* r = rec + kLearnedRec * k;
+        r[0] = m->weights[k];
+        for (int i = 0; i < 5; ++i) r[1 + i] = m->means[5 * k + i];
+        for (int i = 0; i < 16; ++i) r[6 + i] = m->covs[16 * k + i];
+    }
+    HIP_TRY(launch_learned4(rec, m->M, alpha, nq, wi_local, keep, weights, means, covs, n_out,
+                            (hipStream_t)hip_stream));
+    return SDMM_OK;
+}
+
 void sdmm_scene_destroy(sdmm_scene* s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
@@ -303,6 +388,7 @@ void sdmm_scene_destroy(sdmm_scene* s) {
     if (s->dquads) (void)hipFree(s->dquads);
     if (s->drefl) (void)hipFree(s->drefl);
     if (s->dbpar) (void)hipFree(s->dbpar);
+    if (s->dlmod) (void)hipFree(s->dlmod);
     if (s->drad) (void)hipFree(s->drad);
     if (s->buf) (void)hipFree(s->buf);
     if (s->lt) (void)hipFree(s->lt);

@@ -42,14 +42,13 @@ constexpr int kBsdfParams = 8;
 constexpr int kBsdfDiffuse = 0;
 constexpr int kBsdfPlastic = 1;
 constexpr int kBsdfConductor = 2;
-// lobes of a rough conductor's (synthetic) learned BSDF (render.hip glossy_lobes)
-constexpr int kGlossyLobes = 4;
 
 struct SceneDev {
     const QuadDev* quads;
     int n_quads;
     const float* refl;    // 3 per BSDF (plastic: its diffuseReflectance)
     const float* bpar;    // kBsdfParams per BSDF; null: every BSDF diffuse
+    const float* lmodel;  // kLearnedStride per BSDF: [M, M SDMM4 records] (learned_bsdf.h); null: none
     const float* rad;     // 3 per emitter
     float cam[12];        // camera-to-world 3x4 (row major)
     float tanx, aspect, near_clip;

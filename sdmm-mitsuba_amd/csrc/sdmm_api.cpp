@@ -3222,6 +3222,7 @@ struct sdmm_guide_ctx {
     int64_t guide_fb_cap = 0;
     GuideSortScratch guide_sort{};
     ProductScratch product_scratch{};
+    int64_t order_min = 0;   // smallest call served in leaf-major order
 };
 
 namespace {
@@ -3272,6 +3273,8 @@ int sdmm_guide_ctx_create(sdmm_stree* t, void* hip_stream, sdmm_guide_ctx** out)
     if (!g) return fail(SDMM_E_NOMEM, "out of host memory");
     g->t = t;
     g->device = t->device;
+    g->order_min = kTreeOrderMin;
+    if (const char* e = std::getenv("SDMM_CTX_ORDER_MIN")) g->order_min = std::atoll(e);   // (A/B switch)
     (void)hipDeviceGetAttribute(&g->cus, hipDeviceAttributeMultiprocessorCount, t->device);
     if (g->cus <= 0) g->cus = 256;
     if (hip_stream) {
@@ -3309,7 +3312,7 @@ int sdmm_ctx_guide_pdf_wavefront(sdmm_guide_ctx* g, int64_t nq, const float* con
     const int r = ctx_prepare(g, nq);
     if (r) return r;
     const sdmm_stree* t = g->t;
-    const GuideSortScratch* sort = (nq >= kTreeOrderMin) ? &g->guide_sort : nullptr;
+    const GuideSortScratch* sort = (nq >= g->order_min) ? &g->guide_sort : nullptr;
     HIP_TRY(launch_guide_tree(t->dnodes, t->dtab, t->tab_kmax, nq, c, u, dgiven, d, pdf, comp, node_out,
                               norm_const(2), norm_const(3), t->tab_cap, g->guide_fb, g->guide_fb + 1, g->cus,
                               g->stream, sort, pdf_mode, (int*)g->guide_sort.keys[0], (int)t->nodes.size()));
@@ -3328,7 +3331,7 @@ int sdmm_ctx_guide_product_wavefront(sdmm_guide_ctx* g, int64_t nq, const float*
     r = ctx_prepare(g, nq);
     if (r) return r;
     const sdmm_stree* t = g->t;
-    const GuideSortScratch* sort = (nq >= kTreeOrderMin) ? &g->guide_sort : nullptr;
+    const GuideSortScratch* sort = (nq >= g->order_min) ? &g->guide_sort : nullptr;
     HIP_TRY(launch_guide_product_tree(t->dnodes, t->dtab, t->dcctab, t->tab_kmax, nq, c, u, choice,
                                       choice ? dgiven : nullptr, d, pdf, comp, node_out, material, frame, heuristic,
                                       bsdf->weights, bsdf->means, bsdf->covs, bsdf->diffuse, bsdf->B, bsdf->M,

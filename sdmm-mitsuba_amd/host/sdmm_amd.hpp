@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <fstream>
 #include <memory>
+#include <condition_variable>
 #include <mutex>
 #include <sstream>
 #include <thread>
@@ -257,6 +258,71 @@ inline void em_step_leaves(const std::vector<Mixture*>& leaves, const std::vecto
     check(sdmm_em_step_batched_host_iters(h.data(), (int)h.size(), &s, seg.data(), iterations.data()),
           "sdmm_em_step_batched_host_iters");
 }
+
+// Guide contexts shared by a renderer's worker threads (sdmm_guide_ctx_*):
+// the reference's workers call the conditional concurrently
+// (sdmm_proc.cpp:1086-1106); here each guided bounce leases a free context
+// (its own stream and scratch on the published tree) for the duration of its
+// copies + wavefront + synchronisation.  A pool smaller than the worker count
+// keeps the device's hardware queues (GPU_MAX_HW_QUEUES, 4 by default) and
+// copy engines from being oversubscribed by many small streams
+// (tools/plugin_pattern_bench.py: 16 workers on 16 contexts ran slower than
+// on 4).  Contexts are created on first use.
+class GuideContextPool {
+public:
+    GuideContextPool(sdmm_stree* tree, int contexts) : tree_(tree), cap_(contexts > 0 ? contexts : 1) {}
+    ~GuideContextPool() {
+        for (sdmm_guide_ctx* c : all_) sdmm_guide_ctx_destroy(c);
+    }
+    GuideContextPool(const GuideContextPool&) = delete;
+    GuideContextPool& operator=(const GuideContextPool&) = delete;
+
+    class Lease {
+    public:
+        Lease(GuideContextPool* p, sdmm_guide_ctx* c) : pool_(p), ctx_(c) {}
+        Lease(Lease&& o) noexcept : pool_(o.pool_), ctx_(o.ctx_) { o.ctx_ = nullptr; }
+        Lease(const Lease&) = delete;
+        Lease& operator=(const Lease&) = delete;
+        ~Lease() {
+            if (ctx_) pool_->release(ctx_);
+        }
+        sdmm_guide_ctx* get() const { return ctx_; }
+        void* stream() const { return sdmm_guide_ctx_stream(ctx_); }
+
+    private:
+        GuideContextPool* pool_;
+        sdmm_guide_ctx* ctx_;
+    };
+
+    // a free context (blocks while all `contexts` are leased)
+    Lease acquire() {
+        std::unique_lock<std::mutex> lock(mu_);
+        cv_.wait(lock, [&] { return !free_.empty() || (int)all_.size() < cap_; });
+        sdmm_guide_ctx* c = nullptr;
+        if (!free_.empty()) {
+            c = free_.back();
+            free_.pop_back();
+        } else {
+            check(sdmm_guide_ctx_create(tree_, nullptr, &c), "sdmm_guide_ctx_create");
+            all_.push_back(c);
+        }
+        return Lease(this, c);
+    }
+
+private:
+    void release(sdmm_guide_ctx* c) {
+        {
+            std::lock_guard<std::mutex> lock(mu_);
+            free_.push_back(c);
+        }
+        cv_.notify_one();
+    }
+    sdmm_stree* tree_;
+    int cap_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::vector<sdmm_guide_ctx*> all_, free_;
+};
 
 // A wavefront of guided-bounce queries against one mixture: the batched form
 // of create_conditional + sample + posterior/hsum (sdmm_proc.cpp:368-545).

@@ -20,6 +20,9 @@ here (no Mitsuba); the image is therefore not compared with Mitsuba renders --
 the device Li is checked for unbiasedness and its training batches for
 parity with the host-routed reference instead (tests/test_gpu_li.py).
 """
+import json
+from pathlib import Path
+
 import numpy as np
 
 CORNELL_MAX_DEPTH = 10       # _integrators/sdmm.xml: maxDepth
@@ -151,13 +154,31 @@ def conductor_params(specular_rgb=(1.0, 1.0, 1.0), eta=1.2, k=7.0, alpha=0.2):
     return np.array([2.0, *specular_rgb, eta, k, alpha, 0.0], np.float32)
 
 
-def cornell_box(width=640, height=360, plastic=(), conductor=(), alpha=0.2):
+LEARNED_CONDUCTOR = Path(__file__).resolve().parent / "data" / "conductor_beckmann_4c.sdmm4.json"
+
+
+def load_learned(path=LEARNED_CONDUCTOR):
+    """A learned BSDF file (sdmm-amd.sdmm4 JSON, include/sdmm_gpu.h
+    sdmm_learned4_load_json) as (weights[M], means[M][5], covs[M][16])
+    float32 -- the numbers are written with 9 digits, so they round-trip."""
+    doc = json.loads(Path(path).read_text())
+    if doc.get("format") != "sdmm-amd.sdmm4" or doc.get("version") != 1:
+        raise ValueError(f"{path}: not an sdmm-amd.sdmm4 file")
+    M = int(doc["M"])
+    return (np.asarray(doc["weights"], np.float32).reshape(M), np.asarray(doc["means"], np.float32).reshape(M, 5),
+            np.asarray(doc["covs"], np.float32).reshape(M, 16))
+
+
+def cornell_box(width=640, height=360, plastic=(), conductor=(), alpha=0.2, learned=LEARNED_CONDUCTOR):
     """sdmm_scene_desc fields for the Cornell Box (numpy arrays).  plastic:
     names of BSDFs (e.g. "TallBox", "ShortBox", "Floor") rendered as smooth
     plastic over their diffuse reflectance (a delta specular lobe beside a
     smooth one, like the Kitchen's `plastic` materials, kitchen.xml);
     conductor: names rendered as rough conductors (the Kitchen's glossy
-    `roughconductor` materials) tinted by their reflectance, Beckmann alpha."""
+    `roughconductor` materials) tinted by their reflectance, Beckmann alpha,
+    each with the learned BSDF `learned` (an sdmm4 file; None: no learned
+    model, so product sampling falls back to the plain conditional there) --
+    the synthetic stand-in of tools/make_learned_conductor.py by default."""
     names = list(_BSDFS)
     quads, bsdf, flip, emitter = [], [], [], []
     for m, name, fl in _RECTS:
@@ -182,6 +203,9 @@ def cornell_box(width=640, height=360, plastic=(), conductor=(), alpha=0.2):
             elif nm in conductor:
                 bp[i] = conductor_params(tuple(min(1.0, 1.25 * c) for c in _BSDFS[nm]), alpha=alpha)
         extra["bsdf_params"] = bp.reshape(-1)
+        if conductor and learned is not None:
+            model = load_learned(learned)
+            extra["learned_models"] = [model if nm in conductor else None for nm in names]
     return {**extra,
         "quads": np.asarray(quads, np.float32).reshape(-1),
         "flip_normals": np.asarray(flip, np.int32),

@@ -5,7 +5,11 @@
 // published tree -- pinned H2D of the tile's query planes, one
 // sdmm_ctx_guide_pdf_wavefront, D2H of the outputs, a stream synchronise.
 //
-// usage: guide_pattern_harness model.asdmm queries.bin out.bin threads tile reps
+// usage: guide_pattern_harness model.asdmm queries.bin out.bin threads tile reps [contexts] [resident]
+//   contexts: guide contexts shared by the threads through
+//             sdmm_amd::GuideContextPool (0 or absent: one per thread)
+//   resident: the tiles' queries stay in device memory (no copies: the
+//             device-resident rate of the same calls, for comparison)
 //   queries.bin: int64 n, float c[3][n], u[3][n], dgiven[3][n], uint8 mode[n]
 //   out.bin    : float d[3][n], pdf[n], int32 comp[n] (the last repetition)
 //   stdout     : one JSON line {threads, tile, reps, queries, seconds, queries_per_s}
@@ -24,7 +28,7 @@
 #include <thread>
 #include <vector>
 
-#include "sdmm_gpu.h"
+#include "sdmm_amd.hpp"
 
 namespace {
 
@@ -39,25 +43,24 @@ void hk(hipError_t e, const char* what) {
     if (e != hipSuccess) die(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// The staging of one tile, as the plugin lays it out (Staging): the 9 query
+// planes (stride `tile`) then the mode bytes in ONE block, and the 4 output
+// planes then the component indices in one block, so that a bounce is one
+// H2D and one D2H copy.
 struct Worker {
-    sdmm_guide_ctx* ctx = nullptr;
-    hipStream_t st = nullptr;
     std::vector<int64_t> tiles;   // first query of each of this worker's tiles
-    // pinned: per tile 9 float planes + mode in, 4 float planes + comp out
-    float* h_in = nullptr;
-    uint8_t* h_mode = nullptr;
-    float* h_out = nullptr;
-    int32_t* h_comp = nullptr;
-    float* d_in = nullptr;
-    uint8_t* d_mode = nullptr;
-    float* d_out = nullptr;
-    int32_t* d_comp = nullptr;
+    char* h_in = nullptr;         // pinned, per tile: in block, then out block
+    char* d_in = nullptr;         // device: one tile's in block (resident: every tile's)
+    char* d_out = nullptr;        // device: one tile's out block
 };
 
 }  // namespace
 
 int main(int argc, char** argv) {
-    if (argc != 7) die("usage: guide_pattern_harness model.asdmm queries.bin out.bin threads tile reps");
+    if (argc < 7 || argc > 9)
+        die("usage: guide_pattern_harness model.asdmm queries.bin out.bin threads tile reps [contexts] [resident]");
+    const int contexts_arg = argc >= 8 ? std::atoi(argv[7]) : 0;
+    const bool resident = argc == 9;
     const int T = std::atoi(argv[4]);
     const int64_t tile = std::atoll(argv[5]);
     const int reps = std::atoi(argv[6]);
@@ -82,32 +85,29 @@ int main(int argc, char** argv) {
     ck(sdmm_stree_publish(tree, cmix.data()), "sdmm_stree_publish");
 
     const int64_t ntiles = (n + tile - 1) / tile;
+    const size_t in_bytes = (36 + 1) * (size_t)tile, out_bytes = (16 + 4) * (size_t)tile;
     std::vector<Worker> W((size_t)T);
     for (int i = 0; i < T; ++i) {
         Worker& w = W[(size_t)i];
         for (int64_t t = i; t < ntiles; t += T) w.tiles.push_back(t * tile);
         const size_t k = w.tiles.size() ? w.tiles.size() : 1;
-        const size_t m = k * (size_t)tile;
-        ck(sdmm_guide_ctx_create(tree, nullptr, &w.ctx), "sdmm_guide_ctx_create");
-        w.st = (hipStream_t)sdmm_guide_ctx_stream(w.ctx);
-        hk(hipHostMalloc((void**)&w.h_in, 4 * 9 * m, hipHostMallocDefault), "hipHostMalloc");
-        hk(hipHostMalloc((void**)&w.h_mode, m, hipHostMallocDefault), "hipHostMalloc");
-        hk(hipHostMalloc((void**)&w.h_out, 4 * 4 * m, hipHostMallocDefault), "hipHostMalloc");
-        hk(hipHostMalloc((void**)&w.h_comp, 4 * m, hipHostMallocDefault), "hipHostMalloc");
-        hk(hipMalloc((void**)&w.d_in, 4 * 9 * (size_t)tile), "hipMalloc");
-        hk(hipMalloc((void**)&w.d_mode, (size_t)tile), "hipMalloc");
-        hk(hipMalloc((void**)&w.d_out, 4 * 4 * (size_t)tile), "hipMalloc");
-        hk(hipMalloc((void**)&w.d_comp, 4 * (size_t)tile), "hipMalloc");
+        hk(hipHostMalloc((void**)&w.h_in, (in_bytes + out_bytes) * k, hipHostMallocDefault), "hipHostMalloc");
+        hk(hipMalloc((void**)&w.d_in, in_bytes * (resident ? k : 1)), "hipMalloc");
+        hk(hipMalloc((void**)&w.d_out, out_bytes), "hipMalloc");
         // the worker's tiles in its pinned staging (what its path tracing
-        // would have written there), planes of stride `tile` per tile
+        // would have written there)
         for (size_t j = 0; j < w.tiles.size(); ++j) {
             const int64_t a = w.tiles[j], e = std::min(a + tile, n);
-            for (int p = 0; p < 9; ++p)
-                std::memcpy(w.h_in + (j * 9 + p) * tile, q.data() + p * n + a, 4 * (size_t)(e - a));
-            std::memcpy(w.h_mode + j * tile, mode.data() + a, (size_t)(e - a));
+            float* hi = (float*)(w.h_in + (in_bytes + out_bytes) * j);
+            for (int p = 0; p < 9; ++p) std::memcpy(hi + p * tile, q.data() + p * n + a, 4 * (size_t)(e - a));
+            std::memcpy((char*)(hi + 9 * tile), mode.data() + a, (size_t)(e - a));
+            if (resident)
+                hk(hipMemcpy(w.d_in + in_bytes * j, hi, in_bytes, hipMemcpyHostToDevice), "hipMemcpy");
         }
     }
 
+    const int contexts = contexts_arg > 0 ? contexts_arg : T;
+    sdmm_amd::GuideContextPool pool(tree, contexts);
     std::atomic<int> ready{0};
     std::atomic<bool> go{false};
     std::vector<std::string> err((size_t)T);
@@ -118,28 +118,30 @@ int main(int argc, char** argv) {
         for (int r = 0; r < reps && err[(size_t)i].empty(); ++r)
             for (size_t j = 0; j < w.tiles.size(); ++j) {
                 const int64_t a = w.tiles[j], nq = std::min(a + tile, n) - a;
-                float* hi = w.h_in + j * 9 * tile;
-                for (int p = 0; p < 9; ++p)
-                    if (hipMemcpyAsync(w.d_in + p * tile, hi + p * tile, 4 * (size_t)nq, hipMemcpyHostToDevice,
-                                       w.st) != hipSuccess) { err[(size_t)i] = "upload"; return; }
-                if (hipMemcpyAsync(w.d_mode, w.h_mode + j * tile, (size_t)nq, hipMemcpyHostToDevice, w.st) !=
-                    hipSuccess) { err[(size_t)i] = "upload"; return; }
-                const float* c[3] = {w.d_in, w.d_in + tile, w.d_in + 2 * tile};
-                const float* u[3] = {w.d_in + 3 * tile, w.d_in + 4 * tile, w.d_in + 5 * tile};
-                const float* dg[3] = {w.d_in + 6 * tile, w.d_in + 7 * tile, w.d_in + 8 * tile};
-                float* d[3] = {w.d_out, w.d_out + tile, w.d_out + 2 * tile};
-                if (sdmm_ctx_guide_pdf_wavefront(w.ctx, nq, c, u, dg, w.d_mode, d, w.d_out + 3 * tile, w.d_comp,
-                                                 nullptr) != SDMM_OK) {
+                char* hb = w.h_in + (in_bytes + out_bytes) * j;
+                const sdmm_amd::GuideContextPool::Lease lease = pool.acquire();
+                const hipStream_t st = (hipStream_t)lease.stream();
+                float* din = (float*)(resident ? w.d_in + in_bytes * j : w.d_in);
+                if (!resident && hipMemcpyAsync(din, hb, in_bytes, hipMemcpyHostToDevice, st) != hipSuccess) {
+                    err[(size_t)i] = "upload";
+                    return;
+                }
+                const float* c[3] = {din, din + tile, din + 2 * tile};
+                const float* u[3] = {din + 3 * tile, din + 4 * tile, din + 5 * tile};
+                const float* dg[3] = {din + 6 * tile, din + 7 * tile, din + 8 * tile};
+                float* dout = (float*)w.d_out;
+                float* d[3] = {dout, dout + tile, dout + 2 * tile};
+                if (sdmm_ctx_guide_pdf_wavefront(lease.get(), nq, c, u, dg, (const uint8_t*)(din + 9 * tile), d,
+                                                 dout + 3 * tile, (int32_t*)(dout + 4 * tile), nullptr) != SDMM_OK) {
                     err[(size_t)i] = std::string("sdmm_ctx_guide_pdf_wavefront: ") + sdmm_last_error();
                     return;
                 }
-                float* ho = w.h_out + j * 4 * tile;
-                for (int p = 0; p < 4; ++p)
-                    if (hipMemcpyAsync(ho + p * tile, w.d_out + p * tile, 4 * (size_t)nq, hipMemcpyDeviceToHost,
-                                       w.st) != hipSuccess) { err[(size_t)i] = "download"; return; }
-                if (hipMemcpyAsync(w.h_comp + j * tile, w.d_comp, 4 * (size_t)nq, hipMemcpyDeviceToHost, w.st) !=
-                    hipSuccess) { err[(size_t)i] = "download"; return; }
-                if (hipStreamSynchronize(w.st) != hipSuccess) { err[(size_t)i] = "hipStreamSynchronize"; return; }
+                if (!resident || r == reps - 1)
+                    if (hipMemcpyAsync(hb + in_bytes, w.d_out, out_bytes, hipMemcpyDeviceToHost, st) != hipSuccess) {
+                        err[(size_t)i] = "download";
+                        return;
+                    }
+                if (hipStreamSynchronize(st) != hipSuccess) { err[(size_t)i] = "hipStreamSynchronize"; return; }
             }
     };
     std::vector<std::thread> th;
@@ -158,10 +160,10 @@ int main(int argc, char** argv) {
     for (const Worker& w : W)
         for (size_t j = 0; j < w.tiles.size(); ++j) {
             const int64_t a = w.tiles[j], e = std::min(a + tile, n);
-            for (int p = 0; p < 3; ++p)
-                std::memcpy(d.data() + p * n + a, w.h_out + (j * 4 + p) * tile, 4 * (size_t)(e - a));
-            std::memcpy(pdf.data() + a, w.h_out + (j * 4 + 3) * tile, 4 * (size_t)(e - a));
-            std::memcpy(comp.data() + a, w.h_comp + j * tile, 4 * (size_t)(e - a));
+            const float* ho = (const float*)(w.h_in + (in_bytes + out_bytes) * j + in_bytes);
+            for (int p = 0; p < 3; ++p) std::memcpy(d.data() + p * n + a, ho + p * tile, 4 * (size_t)(e - a));
+            std::memcpy(pdf.data() + a, ho + 3 * tile, 4 * (size_t)(e - a));
+            std::memcpy(comp.data() + a, ho + 4 * tile, 4 * (size_t)(e - a));
         }
     FILE* o = std::fopen(argv[3], "wb");
     if (!o) die("cannot write output");
@@ -171,13 +173,13 @@ int main(int argc, char** argv) {
     std::fclose(o);
 
     const double total = (double)n * reps;
-    std::printf("{\"threads\": %d, \"tile\": %lld, \"reps\": %d, \"queries\": %lld, \"seconds\": %.6f, "
-                "\"queries_per_s\": %.1f}\n",
-                T, (long long)tile, reps, (long long)n, sec, total / sec);
+    std::printf("{\"threads\": %d, \"contexts\": %d, \"tile\": %lld, \"reps\": %d, \"queries\": %lld, "
+                "\"resident\": %s, \"seconds\": %.6f, \"queries_per_s\": %.1f}\n",
+                T, contexts, (long long)tile, reps, (long long)n, resident ? "true" : "false", sec, total / sec);
     for (Worker& w : W) {
-        sdmm_guide_ctx_destroy(w.ctx);
-        (void)hipHostFree(w.h_in); (void)hipHostFree(w.h_mode); (void)hipHostFree(w.h_out); (void)hipHostFree(w.h_comp);
-        (void)hipFree(w.d_in); (void)hipFree(w.d_mode); (void)hipFree(w.d_out); (void)hipFree(w.d_comp);
+        (void)hipHostFree(w.h_in);
+        (void)hipFree(w.d_in);
+        (void)hipFree(w.d_out);
     }
     for (sdmm_mix* m : mix) sdmm_destroy(m);
     sdmm_stree_destroy(tree);

@@ -160,7 +160,8 @@ def _build_guide_pattern(tmp_path):
     exe = tmp_path / "guide_pattern_harness"
     lib = ROOT / "sdmm-mitsuba_amd" / "lib"
     subprocess.run(["g++", "-O2", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
-                    f"-I{ROOT / 'include'}", str(ROOT / "tests" / "cpp" / "guide_pattern_harness.cpp"),
+                    f"-I{ROOT / 'include'}", f"-I{ROOT / 'sdmm-mitsuba_amd' / 'host'}",
+                    str(ROOT / "tests" / "cpp" / "guide_pattern_harness.cpp"),
                     f"-L{lib}", "-lsdmm_amd", "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{lib}",
                     "-Wl,-rpath,/opt/rocm/lib", "-pthread", "-o", str(exe)], check=True)
     return exe

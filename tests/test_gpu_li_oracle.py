@@ -190,12 +190,15 @@ def test_conductor_li_unguided_bitwise(pkg, oracle, scenes, gpu, plog):
 @pytest.mark.parametrize("K", [16, 512])
 def test_glossy_product_li_matches_oracle(pkg, oracle, scenes, gpu, plog, K):
     """sampleProduct with a NON-diffuse learned BSDF inside the render: each
-    rough-conductor bounce conditions its learned lobes on (theta_i, alpha),
-    rotates them to wi (rotate_to_wo) and takes them to world through the
-    shading frame (sdmm_proc.cpp:340-355) -- the product's non-diffuse
-    branch, the Kitchen's (configs[4], K = 512) glossy materials -- beside the
-    diffuse materials' slice-0 rule.  >= 99 % of the paths match the CPU Li."""
+    rough-conductor bounce conditions the material's learned SDMM4 on
+    (theta_i, alpha) and prunes it to 2 lobes (getDMM, roughconductor.cpp:
+    182-194; learned_bsdf.h), rotates them to wi (rotate_to_wo) and takes
+    them to world through the shading frame (sdmm_proc.cpp:340-355) -- the
+    product's non-diffuse branch, the Kitchen's (configs[4], K = 512) glossy
+    materials -- beside the diffuse materials' slice-0 rule.  >= 99 % of the
+    paths match the CPU Li, whose conditional is the oracle's restatement."""
     desc = scenes.cornell_box(128, 72, conductor=GLOSSY)
+    assert desc["learned_models"][list(scenes._BSDFS).index("Floor")] is not None
     sc = pkg.Scene(desc)
     tree = _tree(pkg, sc)
     node_mix = _train(pkg, sc, tree, 4, 8, K=K)
@@ -207,7 +210,29 @@ def test_glossy_product_li_matches_oracle(pkg, oracle, scenes, gpu, plog, K):
     r = oracle.li_render(desc, aabb, child, node_mix=_oracle_mixes(oracle, node_mix), guided=True, spp=SPP,
                          seed=SEED, learned=learned, threads=16)
     _compare_guided(oracle, plog, f"li_glossy_product_K{K}", img, rec, nv, r)
-    # the conductor's bounces used the product (k * max(M, 4) + j indices of
-    # its own rows): some guided samples come from its lobes 1..3
+    # the conductor's bounces used the product (k * max(M, 2) + j indices of
+    # its own rows; the diffuse rows hold one lobe): some guided samples come
+    # from the conditioned model's second lobe
     comps = r["comps"]
-    assert ((comps >= 0) & (comps % 4 != 0)).sum() > 0
+    assert ((comps >= 0) & (comps % 2 != 0)).sum() > 0
+
+
+def test_conductor_without_learned_model_plain_conditional(pkg, oracle, scenes, gpu, plog):
+    """A rough conductor with no learned model (m_sdmm == nullptr: getDMM
+    returns false, roughconductor.cpp:182-184): its product bounces fall back
+    to the plain conditional with h 0.5 (sdmm_proc.cpp:383) -- device == CPU
+    Li; no guided sample comes from a second lobe."""
+    desc = scenes.cornell_box(128, 72, conductor=GLOSSY, learned=None)
+    assert "learned_models" not in desc
+    sc = pkg.Scene(desc)
+    tree = _tree(pkg, sc)
+    node_mix = _train(pkg, sc, tree, 4, 8)
+    learned = scenes.diffuse_learned_bsdf(len(desc["reflectance"]) // 3)
+    table = pkg.BsdfTable(*learned[:3], device=gpu, diffuse=learned[3])
+    img, rec, nv, _ = _device(sc, tree, node_mix, True, table=table)
+    aabb, child, _ = tree.nodes()
+    r = oracle.li_render(desc, aabb, child, node_mix=_oracle_mixes(oracle, node_mix), guided=True, spp=SPP,
+                         seed=SEED, learned=learned, threads=16)
+    _compare_guided(oracle, plog, "li_conductor_no_model", img, rec, nv, r)
+    comps = r["comps"]
+    assert ((comps >= 0) & (comps % 2 != 0)).sum() == 0

@@ -3,18 +3,21 @@
 
 plugin/volpath_sdmm_amd.cpp (guideWavefront) serves each render tile's
 bounce with ONE guided-wavefront call: upload the tile's query planes from
-pinned host staging (9 float planes + the mode byte), the call, download 4
-float planes + the component index, synchronise.  Round 5 ran it under a
-global mutex on the model's stream (back-to-back calls of the tile size);
-round 6 gives each render worker its own guide context (stream + scratch) on
-the published tree, so the workers' calls overlap -- the "threads_*" rows.  This tool trains the Cornell
-Box guiding model (K = 128 leaves, as the bench's cornell_k128 line), takes
-real queries -- the saved vertices of one guided render (condition c, the
-sampled world direction as the BSDF direction), uniforms from a fixed
-generator, half of them pdf queries -- and times, per tile size:
-  * the plugin pattern: pinned H2D + wavefront + D2H + stream synchronise;
-  * the wavefront alone on device-resident planes (the device Li's path);
-and reports queries/s for each beside the full-frame wavefront.
+pinned host staging (9 float planes + the mode byte, one copy), the call,
+download 4 float planes + the component index (one copy), synchronise.
+Round 5 ran it under a global mutex on the model's stream (back-to-back calls
+of the tile size).  Round 6 runs it through guide contexts (stream + scratch)
+on the published tree, leased from a pool by the render workers, so the
+workers' calls overlap.  This tool trains the Cornell Box guiding model
+(K = 128 leaves, as the bench's cornell_k128 line), takes real queries -- the
+saved vertices of one guided render (condition c, the sampled world direction
+as the BSDF direction), uniforms from a fixed generator, half of them pdf
+queries -- and times:
+  * one thread, per tile size: the plugin pattern (pinned H2D + wavefront +
+    D2H + synchronise) and the wavefront alone on device-resident planes;
+  * the "threads_*" rows: C++ worker threads (tests/cpp/guide_pattern_harness.cpp)
+    sharing a pool of guide contexts, aggregate queries/s, outputs checked
+    bitwise against the one-thread run.
 
     python tools/plugin_pattern_bench.py [--reps 20]
 """
@@ -35,6 +38,7 @@ sys.path.insert(0, str(ROOT / "tests"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--keep", default=None, help="write the model / queries / harness here and keep them")
     a = ap.parse_args()
     import torch
     from conftest import load_pkg
@@ -118,27 +122,39 @@ def main():
     import subprocess
     import tempfile
     from test_gpu_harness import write_guide_queries
-    tmp = Path(tempfile.mkdtemp(prefix="gpb_"))
+    tmp = Path(a.keep) if a.keep else Path(tempfile.mkdtemp(prefix="gpb_"))
+    tmp.mkdir(parents=True, exist_ok=True)
     tree.save_json(tmp / "model.asdmm", node_mix)
     n_mt = min(n_all, 1 << 21)
     write_guide_queries(tmp / "q.bin", c[:, :n_mt], u[:, :n_mt], dg[:, :n_mt], mode[:n_mt])
     exe = tmp / "guide_pattern_harness"
     lib = ROOT / "sdmm-mitsuba_amd" / "lib"
     subprocess.run(["g++", "-O2", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
-                    f"-I{ROOT / 'include'}", str(ROOT / "tests" / "cpp" / "guide_pattern_harness.cpp"),
+                    f"-I{ROOT / 'include'}", f"-I{ROOT / 'sdmm-mitsuba_amd' / 'host'}",
+                    str(ROOT / "tests" / "cpp" / "guide_pattern_harness.cpp"),
                     f"-L{lib}", "-lsdmm_amd", "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{lib}",
                     "-Wl,-rpath,/opt/rocm/lib", "-pthread", "-o", str(exe)], check=True)
     ref = None
-    for threads, T in ((1, 32768), (16, 32768), (16, 4096), (32, 32768)):
+    import os
+    # (threads, tile, contexts (0: one per thread), resident, extra env)
+    rows = [(1, 32768, 0, 0, {}), (1, 32768, 0, 1, {}), (4, 32768, 0, 0, {}), (16, 32768, 0, 0, {}),
+            (16, 32768, 0, 1, {}), (16, 32768, 4, 0, {}), (16, 32768, 4, 1, {}), (16, 32768, 8, 0, {}),
+            (16, 32768, 2, 0, {}), (16, 4096, 4, 0, {}), (16, 262144, 4, 0, {}),
+            (16, 32768, 8, 0, {"GPU_MAX_HW_QUEUES": "8"})]
+    for threads, T, nctx, res, extra in rows:
         r = subprocess.run([str(exe), str(tmp / "model.asdmm"), str(tmp / "q.bin"), str(tmp / "o.bin"), str(threads),
-                            str(T), str(max(2, a.reps // 4))], check=True, timeout=300, capture_output=True, text=True)
+                            str(T), str(max(2, a.reps // 4)), str(nctx)] + (["resident"] if res else []),
+                           check=True, timeout=300, capture_output=True, text=True, env=dict(os.environ, **extra))
         row = json.loads(r.stdout.strip().splitlines()[-1])
         got = np.fromfile(tmp / "o.bin", np.uint8)
         if ref is None:
             ref = got
         row["bitwise_equal_to_1_thread"] = bool(np.array_equal(got, ref))
-        out[f"threads_{threads}_tile_{T}"] = row
-        print(json.dumps({f"threads_{threads}_tile_{T}": row}), flush=True)
+        key = f"threads_{threads}_ctx_{nctx or threads}_tile_{T}" + ("_resident" if res else "") + "".join(
+            f"_{k}={v}" for k, v in extra.items())
+        row["env"] = extra
+        out[key] = row
+        print(json.dumps({key: row}), flush=True)
     print(json.dumps(out), flush=True)
 
 
