@@ -246,17 +246,32 @@ def test_em_matches_oracle(pkg, oracle, synth, gpu, plog, K, N, iters, heuristic
     np.testing.assert_array_equal(p["weights"] > 0, om.weights > 0)
 
 
-def test_em_faithful_oracle_within_reference_noise(pkg, oracle, synth, gpu):
-    """Against the fp32 'faithful' oracle the agreement is the reference's own
-    fp32 noise (~1e-4 relative); reported, looser bound."""
+# realised GPU-vs-faithful-fp32-oracle distances after 3 EM steps (K = 128,
+# N = 16384), measured in round 6: weights 3.38e-4, covariances 1.30e-3
+# (profiles/round6_parity_errors_faithful.jsonl); the bounds are 2x those
+# 
+FAITHFUL_W_RTOL = 2 * 3.4e-4
+FAITHFUL_COV_RTOL = 2 * 1.31e-3
+
+
+def test_em_faithful_oracle_within_reference_noise(pkg, oracle, synth, gpu, plog):
+    """Against the fp32 'faithful' oracle (the literal jmm arithmetic) the
+    agreement is the reference's own fp32 noise: the E-step's summation order
+    differs, so the distance is logged and bounded at 2x its realised value
+    (the north-star 1e-4 is held against the exact oracle, above)."""
     K, N = 128, 16384
     b, mix, om, ost, ds, os_ = _setup(pkg, oracle, synth, K, N, mode=0)
     for _ in range(3):
         mix.optimize(ds)
         oracle.optimize(om, ost, os_, accurate=False)
     p = mix.get_params()
-    np.testing.assert_allclose(p["weights"], om.weights, rtol=2e-3, atol=1e-6)
-    assert _cov_close(p["cov"], om.cov, 1e-2) <= 1e-2
+    ow = np.asarray(om.weights, np.float64)
+    werr = float((np.abs(p["weights"] - ow) / np.maximum(np.abs(ow), 1e-4)).max())
+    cerr = _cov_close(p["cov"], om.cov, FAITHFUL_COV_RTOL)
+    plog("em_faithful_fp32_weights_rel_err", werr, FAITHFUL_W_RTOL)
+    plog("em_faithful_fp32_cov_rel_err", cerr, FAITHFUL_COV_RTOL)
+    assert werr <= FAITHFUL_W_RTOL
+    assert cerr <= FAITHFUL_COV_RTOL
 
 
 def test_em_split_phase_equals_fused(pkg, oracle, synth, gpu):
