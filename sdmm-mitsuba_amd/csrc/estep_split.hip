@@ -609,7 +609,11 @@ estep_resp_split_kernel(const float* __restrict__ ep, int Kp, int K, SamplesDev 
 // ---------------------------------------------------------------------------
 // Configurations (R = Kp / 16 blocks, waves per workgroup, waves per SIMD).
 // The B image takes R x 8 KB of LDS per workgroup.
-#define SDMM_SPLIT_CONFIGS(X) X(1, 4, 4) X(2, 4, 4) X(4, 4, 4) X(8, 12, 3)
+#ifndef SDMM_SPLIT_R8_WPB   // (overridable for tools/build_variant.sh A/B builds)
+#define SDMM_SPLIT_R8_WPB 12
+#define SDMM_SPLIT_R8_OCC 3
+#endif
+#define SDMM_SPLIT_CONFIGS(X) X(1, 4, 4) X(2, 4, 4) X(4, 4, 4) X(8, SDMM_SPLIT_R8_WPB, SDMM_SPLIT_R8_OCC)
 
 // R = 8 (K = 128): one 12-wave workgroup per CU at 3 waves per SIMD (the
 // 64-KB coefficient image, the 48 KB of half-row stages and the 18 KB of
@@ -620,8 +624,8 @@ static void split_cfg(int R, int /*variant*/, int* wpb, int* occ) {
     *wpb = 4;
     *occ = 4;
     if (R == 8) {
-        *wpb = 12;
-        *occ = 3;
+        *wpb = SDMM_SPLIT_R8_WPB;
+        *occ = SDMM_SPLIT_R8_OCC;
     }
 }
 

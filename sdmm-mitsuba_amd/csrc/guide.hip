@@ -33,6 +33,20 @@
 
 namespace sdmm {
 
+// (diagnostic SDMM_WAVE_CLOCK: per-phase shader clocks of the one-wave full-K
+// product path, summed by workgroups 0..3 and printed at their end)
+#ifdef SDMM_WAVE_CLOCK
+__shared__ unsigned long long g_wclk[12];
+__shared__ unsigned long long g_wlast;
+#define WCLK(i)                                                          \
+    do {                                                                 \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();   \
+        if (threadIdx.x == 0) { g_wclk[i] += now_ - g_wlast; g_wlast = now_; } \
+    } while (0)
+#else
+#define WCLK(i) do {} while (0)
+#endif
+
 struct GuideConsts {
     float norm2, norm3;
 };
@@ -701,9 +715,27 @@ guide_tree_cand_kernel(const STNodeDev* __restrict__ nodes, const GuideMix* __re
 __device__ __forceinline__ float rl(float x, int l) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
 }
-// acc += x of lanes 0 .. n-1, in lane order (uniform result)
-__device__ __forceinline__ float seq_sum(float acc, float x, int n) {
-    for (int l = 0; l < n; ++l) acc += rl(x, l);
+// acc += x of lanes 0 .. n-1, in lane order (uniform result).  The wave's
+// values go through a 64-float LDS stage (st, 16-B aligned, this wave's own)
+// and come back as 16 broadcast ds_read_b128, so each term is ONE dependent
+// VGPR add; lanes >= n stage -0.0f, an exact no-op (x + -0 == x for every x,
+// NaN included).  (Round 6; was a v_readlane + SALU-counted loop per term:
+// 5 instructions and a taken branch, ~37 wall cycles a term at 3 waves per
+// SIMD.)
+__device__ __forceinline__ void stage64(float* st, float x, bool live) {
+    st[__lane_id()] = live ? x : -0.0f;
+}
+__device__ __forceinline__ float seq_sum(float acc, float x, int n, float* st) {
+    stage64(st, x, __lane_id() < n);
+    const float4* s4 = (const float4*)st;
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+        const float4 v = s4[p];
+        acc += v.x;
+        acc += v.y;
+        acc += v.z;
+        acc += v.w;
+    }
     return acc;
 }
 template <int CTRL>
@@ -720,6 +752,7 @@ struct WaveLds {
     float* pc;       // this workgroup's global scratch: kPcStride x pcap floats, the product
                      // pairs of pass 1 {w, included, mean, Linv, detInv} (when they fit)
     int pcap;
+    float* st;       // 64  the serial sums' broadcast stage (seq_sum), 16-B aligned
 };
 constexpr int kPcStride = 10;
 constexpr int kProductPairCap = 1024;   // kept x lobes per full-K product query kept in scratch
@@ -733,9 +766,12 @@ __device__ __forceinline__ WaveLds wave_lds(float* lds, int K, float* pscratch =
     L.lobe = L.se + 3 * K;
     L.pc = pscratch ? pscratch + (size_t)blockIdx.x * kPcStride * pcap : nullptr;
     L.pcap = pscratch ? pcap : 0;
+    L.st = lds + ((5 * K + 21 * M + 3) & ~3);
     return L;
 }
-static size_t wave_lds_bytes(int K, int M = 0) { return sizeof(float) * (5 * (size_t)K + 21 * (size_t)M) + 16; }
+static size_t wave_lds_bytes(int K, int M = 0) {
+    return sizeof(float) * ((5 * (size_t)K + 21 * (size_t)M + 3) / 4 * 4 + 64) + 16;
+}
 
 // lane ^ J of a wave-uniform compile-time J (DPP inside rows, ds_bpermute across)
 template <int J>
@@ -835,10 +871,12 @@ __device__ __forceinline__ int build_full_wave_s(const float* gp, int Kp, int K,
         }
         nan_seen |= (wr[i] != wr[i]);
     }
+    WCLK(1);
     float total = 0.0f;   // component order
 #pragma unroll
     for (int i = 0; i < S; ++i)
-        if (64 * i < K) total = seq_sum(total, wr[i], min(64, K - 64 * i));
+        if (64 * i < K) total = seq_sum(total, wr[i], min(64, K - 64 * i), L.st);
+    WCLK(8);
     const float cutoff = (float)(0.99 * (double)total);
     accum = 0.0f;
     int lastIdx = K;   // the reference leaves it uninitialised if never reached
@@ -854,6 +892,7 @@ __device__ __forceinline__ int build_full_wave_s(const float* gp, int Kp, int K,
 #pragma unroll
             for (int i = 0; i < S; ++i) { key[i] = sel_wkey(v[i]); idx[i] = sel_idx(v[i]); }
         }
+        WCLK(9);
         // sorted element p = 64 i + lane: its slot record, written by its own
         // lane, and its term of the kept mass (0 for an invalid conditional)
         int n_live = 0;   // entries with a weight (sorted first)
@@ -879,12 +918,24 @@ __device__ __forceinline__ int build_full_wave_s(const float* gp, int Kp, int K,
         for (int i = 0; i < S; ++i) {
             if (done) break;
             const int n = min(64, n_live - 64 * i);
-            for (int l = 0; l < n; ++l) {
-                accum += rl(term[i], l);
-                if (accum >= cutoff) { lastIdx = 64 * i + l + 1; done = true; break; }
+            if (n <= 0) break;
+            // the terms through the broadcast stage (seq_sum); a padded
+            // lane's -0.0f cannot cross the cutoff (accum unchanged)
+            stage64(L.st, term[i], lane < n);
+            const float4* s4 = (const float4*)L.st;
+#pragma unroll 1
+            for (int p = 0; 4 * p < n && !done; ++p) {
+                const float4 v = s4[p];
+                const float e4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    accum += e4[e];
+                    if (accum >= cutoff) { lastIdx = 64 * i + 4 * p + e + 1; done = true; break; }
+                }
             }
         }
         __syncthreads();
+        WCLK(10);
         return lastIdx;
     }
     for (int it = 0; it < K; ++it) {
@@ -938,7 +989,7 @@ __device__ __forceinline__ float wave_slot_weights(int lastIdx, float accum, con
             if (scaled) wi = wi * invSum;
             L.fw[i] = wi;
         }
-        sum2 = seq_sum(sum2, wi, min(64, lastIdx - base));
+        sum2 = seq_sum(sum2, wi, min(64, lastIdx - base), L.st);
     }
     if (lastIdx > 0 && sum2 != 0.0f) {
         const DivBy by_sum2(sum2);
@@ -964,11 +1015,21 @@ __device__ QueryOut finish_query_wave(const float* gp, int Kp, const float c[3],
         for (int base = 0; base < lastIdx && slot < 0; base += 64) {
             const float x = (base + lane < lastIdx) ? L.fw[base + lane] : 0.0f;
             const int n = min(64, lastIdx - base);
-            for (int l = 0; l < n; ++l) {
-                cdf += rl(x, l);
-                if (base + l == 0 || cdf != prev) runStart = base + l;
-                prev = cdf;
-                if (cdf >= u[0]) { slot = base + l; break; }
+            stage64(L.st, x, true);   // (broadcast stage, as seq_sum)
+            const float4* s4 = (const float4*)L.st;
+#pragma unroll 1
+            for (int q4 = 0; 4 * q4 < n && slot < 0; ++q4) {
+                const float4 v = s4[q4];
+                const float e4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int l = 4 * q4 + e;
+                    if (l >= n) break;
+                    cdf += e4[e];
+                    if (base + l == 0 || cdf != prev) runStart = base + l;
+                    prev = cdf;
+                    if (cdf >= u[0]) { slot = base + l; break; }
+                }
             }
         }
         if (slot < 0) slot = runStart;
@@ -1006,7 +1067,7 @@ __device__ QueryOut finish_query_wave(const float* gp, int Kp, const float c[3],
                 term = f * cond_component_pdf(gp, Kp, k, e, dir, gc.norm2);
             }
         }
-        acc = seq_sum(acc, term, min(64, lastIdx - base));
+        acc = seq_sum(acc, term, min(64, lastIdx - base), L.st);
     }
     o.d[0] = dir[0]; o.d[1] = dir[1]; o.d[2] = dir[2];
     o.pdf = acc;
@@ -2246,6 +2307,7 @@ __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCo
                                     const WaveLds& L, const BsdfTab& bt, int b, const float F[9], const float* u,
                                     const float* dir_in, float choice, int lane, GuideConsts gc, QueryOut& o) {
     wave_prepare_product(gp, Kp, c, lastIdx, L, bt, b, F, lane);
+    WCLK(3);
     // pair f = (kept slot f / M, nonzero lobe nzj[f % M]) -- the reference's
     // walk order with the zero-weight lobes (which it skips) left out
     const int M = __builtin_popcountll(__builtin_amdgcn_ballot_w64(lane < bt.M && bt.w[b * bt.M + lane] != 0.0f));
@@ -2272,10 +2334,11 @@ __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCo
                 r[9] = pc.detInv;
             }
         }
-        total = seq_sum(total, inc ? w : -0.0f, min(64, NP - base));
+        total = seq_sum(total, inc ? w : -0.0f, min(64, NP - base), L.st);
         P += __builtin_popcountll(__builtin_amdgcn_ballot_w64(inc));
     }
     __syncthreads();
+    WCLK(4);
     if (P == 0 || total == 0.0f) return false;
     float dir[3];
     o.comp = kCompPdfValid;
@@ -2301,13 +2364,23 @@ __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCo
             }
             const uint64_t incm = __builtin_amdgcn_ballot_w64(inc);
             const int n = min(64, NP - base);
-            for (int l = 0; l < n; ++l) {
-                if (!((incm >> l) & 1)) continue;
-                cdf += rl(x, l);
-                if (p == 0 || cdf != prev) run_f = base + l;
-                prev = cdf;
-                ++p;
-                if (cdf >= u[0]) { sel_f = base + l; break; }
+            stage64(L.st, x, true);   // (broadcast stage, as seq_sum)
+            const float4* s4 = (const float4*)L.st;
+#pragma unroll 1
+            for (int q4 = 0; 4 * q4 < n && sel_f < 0; ++q4) {
+                const float4 v = s4[q4];
+                const float e4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int l = 4 * q4 + e;
+                    if (l >= n) break;
+                    if (!((incm >> l) & 1)) continue;
+                    cdf += e4[e];
+                    if (p == 0 || cdf != prev) run_f = base + l;
+                    prev = cdf;
+                    ++p;
+                    if (cdf >= u[0]) { sel_f = base + l; break; }
+                }
             }
         }
         if (sel_f < 0) sel_f = run_f;
@@ -2328,6 +2401,7 @@ __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCo
     } else {
         dir[0] = dir_in[0]; dir[1] = dir_in[1]; dir[2] = dir_in[2];
     }
+    WCLK(5);
     // pass 3: the product mixture pdf at dir
     float acc = 0.0f;
     for (int base = 0; base < NP; base += 64) {
@@ -2356,8 +2430,9 @@ __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCo
                 }
             }
         }
-        acc = seq_sum(acc, term, min(64, NP - base));
+        acc = seq_sum(acc, term, min(64, NP - base), L.st);
     }
+    WCLK(6);
     o.d[0] = dir[0]; o.d[1] = dir[1]; o.d[2] = dir[2];
     o.pdf = acc;
     return true;
@@ -2373,6 +2448,7 @@ __device__ void product_tail_wave(const float* gp, int Kp, const float* condCov,
     const bool mixed = !PDF_ONLY && pio.choice != nullptr;
     const float choice = mixed ? pio.choice[q] : 2.0f;
     const float sum2 = wave_slot_weights(lastIdx, accum, L, lane);
+    WCLK(2);
     const bool cvalid = lastIdx > 0 && sum2 != 0.0f;
     QueryOut o{{0.0f, 0.0f, 0.0f}, 0.0f, -1};
     float h = 1.0f;                       // no valid conditional: BSDF only
@@ -2523,17 +2599,36 @@ guide_tree_product_wave_kernel(const STNodeDev* __restrict__ nodes, const GuideM
     const int lane = threadIdx.x;
     const WaveLds L = wave_lds(lds, kmax, pscratch, pcap, bt.M);
     const int n = *fb_count;
+#ifdef SDMM_WAVE_CLOCK
+    if (lane < 12) g_wclk[lane] = 0;
+    if (lane == 0) g_wlast = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    unsigned nq = 0, npairs = 0, nkept = 0;
+#endif
     for (int idx = blockIdx.x; idx < n; idx += gridDim.x) {
         const int64_t q = fb_list[idx];
         const float c[3] = {io.c0[q], io.c1[q], io.c2[q]};
         // uniform: a listed query has a mixture; node_of: the candidate kernel's find
         const int node = node_of ? node_of[q] : stree_find_point(nodes, c[0], c[1], c[2]);
         const GuideMix mx = uniform_mix(tab[node]);   // (one query per wave: uniform)
+        WCLK(0);
         float accum = 0.0f;
         const int lastIdx = build_full_wave(mx.gp, mx.Kp, mx.K, c, L, lane, gc.norm3, accum);
+#ifdef SDMM_WAVE_CLOCK
+        ++nq;
+        nkept += lastIdx;
+#endif
         product_tail_wave<PDF_ONLY>(mx.gp, mx.Kp, cctab[node], c, lastIdx, accum, L, io, pio, bt, q, lane, gc);
         __syncthreads();   // the LDS is reused by the next query
+        WCLK(7);
     }
+#ifdef SDMM_WAVE_CLOCK
+    if (lane == 0 && blockIdx.x < 4)
+        printf("WCLK blk %d q %u kept %u fetch %llu weights %llu sum2 %llu prep %llu pass1 %llu pass2 %llu pass3 %llu "
+               "tail %llu total %llu sort %llu accum %llu\n",
+               blockIdx.x, nq, nkept, g_wclk[0], g_wclk[1], g_wclk[2], g_wclk[3], g_wclk[4], g_wclk[5], g_wclk[6],
+               g_wclk[7], g_wclk[8], g_wclk[9], g_wclk[10]);
+#endif
 }
 
 // lower_bound + tie walk on caller-provided CDFs (the bit-exact index KAT).

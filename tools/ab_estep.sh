@@ -17,10 +17,12 @@ done
 python3 - "$OUT" <<'PY'
 import json, sys, collections, statistics
 d = collections.defaultdict(list)
+h = collections.defaultdict(set)
 for line in open(sys.argv[1]):
     name, js = line.split(" ", 1)
     r = json.loads(js)
     d[name].append(statistics.median(r["us"][60:]))
+    h[name].add(r.get("sha256_16"))
 for k, v in d.items():
-    print(k, [round(x, 1) for x in v], "median", round(statistics.median(v), 1))
+    print(k, [round(x, 1) for x in v], "median", round(statistics.median(v), 1), "output", sorted(h[k]))
 PY
