@@ -755,6 +755,8 @@ struct WaveLds {
     float* st;       // 64  the serial sums' broadcast stage (seq_sum), 16-B aligned
 };
 constexpr int kPcStride = 10;
+// pair f = base + lane's record in the pair scratch: field j at r[64 j] (each
+// 64-pair chunk field-major, so a chunk's field is one coalesced 256-B access)
 constexpr int kProductPairCap = 1024;   // kept x lobes per full-K product query kept in scratch
 
 // LDS carve-up of a one-wave workgroup (+ its slice of the pair scratch).
@@ -768,6 +770,9 @@ __device__ __forceinline__ WaveLds wave_lds(float* lds, int K, float* pscratch =
     L.pcap = pscratch ? pcap : 0;
     L.st = lds + ((5 * K + 21 * M + 3) & ~3);
     return L;
+}
+__device__ __forceinline__ float* pc_rec(const WaveLds& L, int base, int lane) {
+    return L.pc + (size_t)base * kPcStride + lane;
 }
 static size_t wave_lds_bytes(int K, int M = 0) {
     return sizeof(float) * ((5 * (size_t)K + 21 * (size_t)M + 3) / 4 * 4 + 64) + 16;
@@ -2326,12 +2331,12 @@ __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCo
             int k;
             inc = pair_eval(condCov, L, f / M, nzj[f % M], gc.norm2, w, pc, k);
             if (keep) {
-                float* r = L.pc + kPcStride * f;
+                float* r = pc_rec(L, base, lane);
                 r[0] = w;
-                r[1] = inc ? 1.0f : 0.0f;
-                r[2] = pc.mean[0]; r[3] = pc.mean[1]; r[4] = pc.mean[2];
-                r[5] = pc.Linv[0]; r[6] = pc.Linv[1]; r[7] = pc.Linv[2]; r[8] = pc.Linv[3];
-                r[9] = pc.detInv;
+                r[64] = inc ? 1.0f : 0.0f;
+                r[2 * 64] = pc.mean[0]; r[3 * 64] = pc.mean[1]; r[4 * 64] = pc.mean[2];
+                r[5 * 64] = pc.Linv[0]; r[6 * 64] = pc.Linv[1]; r[7 * 64] = pc.Linv[2]; r[8 * 64] = pc.Linv[3];
+                r[9 * 64] = pc.detInv;
             }
         }
         total = seq_sum(total, inc ? w : -0.0f, min(64, NP - base), L.st);
@@ -2353,8 +2358,9 @@ __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCo
             if (f < NP) {
                 float w = 0.0f;
                 if (keep) {
-                    inc = L.pc[kPcStride * f + 1] != 0.0f;
-                    w = L.pc[kPcStride * f];
+                    const float* r = pc_rec(L, base, lane);
+                    inc = r[64] != 0.0f;
+                    w = r[0];
                 } else {
                     ProdComp pc{};
                     int k;
@@ -2402,14 +2408,21 @@ __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCo
         dir[0] = dir_in[0]; dir[1] = dir_in[1]; dir[2] = dir_in[2];
     }
     WCLK(5);
-    // pass 3: the product mixture pdf at dir
+    // pass 3: the product mixture pdf at dir (a cached chunk's ten fields
+    // loaded at once, coalesced; fetching the next chunk's ahead measured no
+    // gain and 18 more spilled VGPRs)
     float acc = 0.0f;
     for (int base = 0; base < NP; base += 64) {
         const int f = base + lane;
         float term = -0.0f;
+        float r[kPcStride];
+        if (keep && f < NP) {
+            const float* rr = pc_rec(L, base, lane);
+#pragma unroll
+            for (int j = 0; j < kPcStride; ++j) r[j] = rr[64 * j];
+        }
         if (f < NP) {
             if (keep) {
-                const float* r = L.pc + kPcStride * f;
                 if (r[1] != 0.0f) {
                     const float wn = r[0] / total;
                     if (wn != 0.0f) {
