@@ -501,6 +501,36 @@ int sdmm_ctx_guide_product_wavefront(sdmm_guide_ctx* g, int64_t nq, const float*
                                      const float* choice, const float* const dgiven[3], const sdmm_bsdf_table* bsdf,
                                      const int32_t* material, const float* const frame[9], float* const d[3],
                                      float* pdf, int32_t* comp, float* heuristic, int32_t* node_out);
+/* Several render workers' guided bounces served as ONE wavefront (round 6):
+ * the requests' queries, in request order, go through a single
+ * sdmm_ctx_guide_pdf_wavefront on the context -- each query's outputs are
+ * bitwise those of a call on its own request (queries are independent) --
+ * with the copies done here: per request one strided H2D of its nine query
+ * planes and one of its mode bytes, one strided D2H of its four output planes
+ * and one of its components.  Synchronous (the context's stream is
+ * synchronised before returning).  Host buffers must be pinned
+ * (hipHostMalloc / hipHostRegister): checked, SDMM_E_INVALID otherwise.  The
+ * C++ mirror's sdmm_amd::GuideBatcher gathers concurrent workers' requests
+ * into these calls.
+ *   in   : planes c0 c1 c2 u0 u1 u2 dgiven0 dgiven1 dgiven2 (as
+ *          sdmm_guide_pdf_wavefront), plane p at in + p * in_stride
+ *   mode : n bytes (pdf_mode)
+ *   out  : planes d0 d1 d2 pdf, plane p at out + p * out_stride
+ *   comp : n int32 */
+typedef struct sdmm_guide_host_req {
+    int64_t n;
+    const float* in;
+    int64_t in_stride;
+    const uint8_t* mode;
+    float* out;
+    int64_t out_stride;
+    int32_t* comp;
+} sdmm_guide_host_req;
+int sdmm_ctx_guide_pdf_host_batch(sdmm_guide_ctx* g, int nreq, const sdmm_guide_host_req* reqs);
+/* Page-locked host memory for such requests (hipHostMalloc / hipHostFree on
+ * the library's side, so that host code needs no HIP headers). */
+int sdmm_pinned_alloc(size_t bytes, void** out);
+void sdmm_pinned_free(void* p);
 /* Checkpoints (.asdmm, JSON; schema in DESIGN.md section 9).
  *   sdmm_save_json      the accelerator: sdmm::save_json(m_accelerator, path),
  *                       volpath_sdmm.cpp:117-126 (model_%05i.asdmm, once per

@@ -216,6 +216,7 @@ public:
         m_device = props.getInteger("hipDevice", 0);
         m_tileSize = props.getInteger("wavefrontTile", 64);
         m_guideContexts = props.getInteger("guideContexts", 4);
+        m_guideBatch = props.getInteger("guideBatch", 1 << 18);
         if (m_rrDepth <= 0) Log(EError, "'rrDepth' must be set to a value greater than zero!");
         if (m_maxDepth <= 0 && m_maxDepth != -1)
             Log(EError, "'maxDepth' must be set to -1 (infinite) or a value greater than zero!");
@@ -234,9 +235,12 @@ public:
         m_device = stream->readInt();
         m_tileSize = stream->readInt();
         m_guideContexts = stream->readInt();
+        m_guideBatch = stream->readInt();
     }
 
     ~SDMMAmdPathTracer() {
+        m_batch.reset();   // (their contexts read the model's tree)
+        m_pool.reset();
         if (m_guiding) sdmm_guiding_destroy(m_guiding);
     }
 
@@ -253,6 +257,7 @@ public:
         stream->writeInt(m_device);
         stream->writeInt(m_tileSize);
         stream->writeInt(m_guideContexts);
+        stream->writeInt(m_guideBatch);
     }
 
     bool preprocess(const Scene* scene, RenderQueue* queue, const RenderJob* job, int sceneResID, int sensorResID,
@@ -295,6 +300,12 @@ public:
         sdmm_guiding_config_default(&cfg);             // K 16, split_to_depth(2), 4000, 2048
         cfg.saved_per_path = m_savedSamplesPerPath;
         cfg.optimize_async = m_optimizeAsync ? 1 : 0;
+        m_batch.reset();   // (a previous render's model and its contexts)
+        m_pool.reset();
+        if (m_guiding) {
+            sdmm_guiding_destroy(m_guiding);
+            m_guiding = nullptr;
+        }
         check_sdmm(sdmm_guiding_create(tmin, tmax, &cfg, m_device, &m_guiding), "sdmm_guiding_create");
         m_stream = (hipStream_t)sdmm_stree_get_stream(sdmm_guiding_tree(m_guiding));
 
@@ -384,12 +395,20 @@ private:
         // then each worker guides through its own context, with no lock
         // then each bounce leases a guide context (stream + scratch) from a
         // pool shared by the workers (sdmm_amd::GuideContextPool)
-        std::unique_ptr<sdmm_amd::GuideContextPool> pool;
+        // -- or, for the plain (non-product) bounce with guideBatch > 0, the
+        // workers' bounces are gathered into shared wavefronts of up to
+        // guideBatch queries (sdmm_amd::GuideBatcher, two in flight)
+        // (both kept across passes: the tree object is the model's for its
+        // lifetime, a republished tree serves the same contexts, and their
+        // scratch stays allocated)
         if (guided) {
             check_sdmm(sdmm_stree_publish(sdmm_guiding_tree(m_guiding), nullptr), "sdmm_stree_publish");
-            pool.reset(new sdmm_amd::GuideContextPool(sdmm_guiding_tree(m_guiding), m_guideContexts));
+            if (!m_pool) m_pool.reset(new sdmm_amd::GuideContextPool(sdmm_guiding_tree(m_guiding), m_guideContexts));
+            if (!m_batch && m_guideBatch > 0 && !(m_sampleProduct && !m_bsdfOnly))
+                m_batch.reset(new sdmm_amd::GuideBatcher(sdmm_guiding_tree(m_guiding), 2, m_guideBatch));
         }
-        m_ctxPool = pool.get();
+        m_ctxPool = guided ? m_pool.get() : nullptr;
+        m_batcher = guided ? m_batch.get() : nullptr;
         auto worker = [&](int wid) {
             ref<Sampler> sampler = static_cast<Sampler*>(scene->getSampler()->clone().get());
             Staging st;
@@ -409,6 +428,7 @@ private:
         for (int i = 0; i < nCores; ++i) workers.emplace_back(worker, i);
         for (auto& th : workers) th.join();
         m_ctxPool = nullptr;
+        m_batcher = nullptr;
         pathLength = len;
         paths = cnt;
         return !m_cancelled;
@@ -751,6 +771,17 @@ private:
     // context and its stream -- the workers run at once, as the reference's
     // render threads do (sdmm_proc.cpp:1086-1106).
     void guideWavefront(Staging& st, int64_t n, int64_t nq) {
+        if (m_batcher && !st.h_mat) {
+            // the staging is the request (pinned planes of stride n); the
+            // batch's leader copies, launches and synchronises
+            const sdmm_guide_host_req rq{nq, st.h_in, n, st.h_mode, st.h_out, n, st.h_comp};
+            try {
+                m_batcher->serve(rq);
+            } catch (const sdmm_amd::Error& e) {
+                SLog(EError, "%s", e.what());
+            }
+            return;
+        }
         const sdmm_amd::GuideContextPool::Lease lease = m_ctxPool->acquire();
         const hipStream_t wst = (hipStream_t)lease.stream();
         for (int f = 0; f < 9; ++f)
@@ -806,6 +837,10 @@ private:
     hipStream_t m_stream = nullptr;   // the model's (training-data pushes, under m_gpuMutex)
     int m_guideContexts = 4;          // guide contexts shared by the workers (one per hardware queue)
     sdmm_amd::GuideContextPool* m_ctxPool = nullptr;   // the pass's (renderPass)
+    int m_guideBatch = 1 << 18;       // queries per gathered wavefront (0: each worker calls alone)
+    sdmm_amd::GuideBatcher* m_batcher = nullptr;       // the pass's (renderPass)
+    std::unique_ptr<sdmm_amd::GuideContextPool> m_pool;   // created at the first guided pass
+    std::unique_ptr<sdmm_amd::GuideBatcher> m_batch;
     std::mutex m_gpuMutex;
     std::atomic<bool> m_cancelled{false};
 };

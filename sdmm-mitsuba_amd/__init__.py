@@ -200,8 +200,15 @@ def lib():
                                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                                        C.c_void_p * 9, C.c_void_p * 3, C.c_void_p, C.c_void_p,
                                                        C.c_void_p, C.c_void_p]
+        L.sdmm_ctx_guide_pdf_host_batch.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
         _lib = L
     return _lib
+
+
+class _GuideHostReq(C.Structure):
+    """sdmm_guide_host_req (include/sdmm_gpu.h)."""
+    _fields_ = [("n", C.c_int64), ("inp", C.c_void_p), ("in_stride", C.c_int64), ("mode", C.c_void_p),
+                ("out", C.c_void_p), ("out_stride", C.c_int64), ("comp", C.c_void_p)]
 
 
 def _check(rc: int):
@@ -245,7 +252,8 @@ EXPORTED_SYMBOLS = [
     "sdmm_guiding_update", "sdmm_kmeanspp_select", "sdmm_init_hemisphere_kmeanspp_batched",
     "sdmm_guide_product_wavefront", "sdmm_pdf_product_wavefront", "sdmm_stree_split_leaf_recurse_device",
     "sdmm_stree_publish", "sdmm_guide_ctx_create", "sdmm_guide_ctx_destroy", "sdmm_guide_ctx_stream",
-    "sdmm_ctx_guide_pdf_wavefront", "sdmm_ctx_guide_product_wavefront",
+    "sdmm_ctx_guide_pdf_wavefront", "sdmm_ctx_guide_product_wavefront", "sdmm_ctx_guide_pdf_host_batch",
+    "sdmm_pinned_alloc", "sdmm_pinned_free",
     "sdmm_learned4_conditional", "sdmm_learned4_save_json", "sdmm_learned4_load_json",
     "sdmm_learned4_conditional_device",
 ]
@@ -1356,6 +1364,18 @@ class GuideContext:
         self.guide_pdf_into(nq, [t.data_ptr() for t in c], [t.data_ptr() for t in u], [t.data_ptr() for t in dgiven],
                             pdf_mode.data_ptr(), [t.data_ptr() for t in d], pdf.data_ptr(), comp.data_ptr())
         return d, pdf, comp
+
+    def guide_pdf_host(self, reqs):
+        """sdmm_ctx_guide_pdf_host_batch: reqs = [(inp, mode, out, comp)] host
+        tensors (pinned: inp (9, n) float32, mode (n,) uint8, out (4, n)
+        float32, comp (n,) int32), served as one wavefront; outputs written in
+        place, synchronously."""
+        arr = (_GuideHostReq * max(1, len(reqs)))()
+        for i, (inp, mode, out, comp) in enumerate(reqs):
+            n = int(mode.numel())
+            arr[i] = _GuideHostReq(n, inp.data_ptr(), inp.stride(0), mode.data_ptr(), out.data_ptr(), out.stride(0),
+                                   comp.data_ptr())
+        _check(lib().sdmm_ctx_guide_pdf_host_batch(self.h, len(reqs), C.cast(arr, C.c_void_p)))
 
     def guide_product(self, c, u, bsdf, material, frame, choice=None, dgiven=None):
         """sdmm_ctx_guide_product_wavefront (see STree.guide_product)."""

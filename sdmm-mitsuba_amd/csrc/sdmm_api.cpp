@@ -3223,6 +3223,8 @@ struct sdmm_guide_ctx {
     GuideSortScratch guide_sort{};
     ProductScratch product_scratch{};
     int64_t order_min = 0;   // smallest call served in leaf-major order
+    char* hbuf = nullptr;    // host-batch planes on the device (sdmm_ctx_guide_pdf_host_batch)
+    int64_t hbuf_cap = 0;    // queries it holds
 };
 
 namespace {
@@ -3297,6 +3299,7 @@ void sdmm_guide_ctx_destroy(sdmm_guide_ctx* g) {
     (void)hipStreamSynchronize(g->stream);
     if (g->guide_fb) (void)hipFree(g->guide_fb);
     if (g->product_scratch.base) (void)hipFree(g->product_scratch.base);
+    if (g->hbuf) (void)hipFree(g->hbuf);
     if (g->own_stream) (void)hipStreamDestroy(g->stream);
     delete g;
 }
@@ -3316,6 +3319,88 @@ int sdmm_ctx_guide_pdf_wavefront(sdmm_guide_ctx* g, int64_t nq, const float* con
     HIP_TRY(launch_guide_tree(t->dnodes, t->dtab, t->tab_kmax, nq, c, u, dgiven, d, pdf, comp, node_out,
                               norm_const(2), norm_const(3), t->tab_cap, g->guide_fb, g->guide_fb + 1, g->cus,
                               g->stream, sort, pdf_mode, (int*)g->guide_sort.keys[0], (int)t->nodes.size()));
+    return SDMM_OK;
+}
+
+int sdmm_pinned_alloc(size_t bytes, void** out) {
+    if (!out) return fail(SDMM_E_INVALID, "invalid argument");
+    *out = nullptr;
+    if (bytes == 0) return SDMM_OK;
+    HIP_TRY(hipHostMalloc(out, bytes, hipHostMallocDefault));
+    return SDMM_OK;
+}
+void sdmm_pinned_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
+// The requests' planes stacked on the device (plane p of the batch at
+// din + p * N, request r's queries at offset off_r), one wavefront, outputs
+// copied back per request; 2-D copies carry a request's planes in one call.
+int sdmm_ctx_guide_pdf_host_batch(sdmm_guide_ctx* g, int nreq, const sdmm_guide_host_req* reqs) {
+    if (!g || nreq < 0 || (nreq > 0 && !reqs)) return fail(SDMM_E_INVALID, "invalid argument");
+    int64_t N = 0;
+    auto pinned = [](const void* p) {
+        hipPointerAttribute_t a{};
+        return hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost;
+    };
+    for (int i = 0; i < nreq; ++i) {
+        const sdmm_guide_host_req& q = reqs[i];
+        if (q.n < 0) return fail(SDMM_E_INVALID, "sdmm_ctx_guide_pdf_host_batch: negative request size");
+        if (q.n == 0) continue;
+        if (!q.in || !q.mode || !q.out || !q.comp || q.in_stride < q.n || q.out_stride < q.n)
+            return fail(SDMM_E_INVALID, "sdmm_ctx_guide_pdf_host_batch: invalid request");
+        if (!pinned(q.in) || !pinned(q.mode) || !pinned(q.out) || !pinned(q.comp)) {
+            (void)hipGetLastError();   // (the query's own error on pageable memory)
+            return fail(SDMM_E_INVALID, "sdmm_ctx_guide_pdf_host_batch: host buffers must be pinned");
+        }
+        N += q.n;
+    }
+    if (N == 0) return SDMM_OK;
+    int r = ctx_prepare(g, N);
+    if (r) return r;
+    // planes: in 9 + out 4 floats, comp int32, mode u8 per query
+    const size_t per = 13 * sizeof(float) + sizeof(int32_t) + 1;
+    if (N > g->hbuf_cap) {
+        if (g->hbuf) {
+            HIP_TRY(hipStreamSynchronize(g->stream));
+            (void)hipFree(g->hbuf);
+            g->hbuf = nullptr;
+            g->hbuf_cap = 0;
+        }
+        const int64_t cap = N + N / 4;
+        HIP_TRY(hipMalloc((void**)&g->hbuf, per * (size_t)cap + 256));
+        g->hbuf_cap = cap;
+    }
+    float* din = (float*)g->hbuf;
+    float* dout = din + 9 * N;
+    int32_t* dcomp = (int32_t*)(dout + 4 * N);
+    uint8_t* dmode = (uint8_t*)(dcomp + N);
+    const size_t dp = sizeof(float) * (size_t)N;
+    int64_t off = 0;
+    for (int i = 0; i < nreq; ++i) {
+        const sdmm_guide_host_req& q = reqs[i];
+        if (q.n == 0) continue;
+        HIP_TRY(hipMemcpy2DAsync(din + off, dp, q.in, sizeof(float) * (size_t)q.in_stride, sizeof(float) * (size_t)q.n,
+                                 9, hipMemcpyHostToDevice, g->stream));
+        HIP_TRY(hipMemcpyAsync(dmode + off, q.mode, (size_t)q.n, hipMemcpyHostToDevice, g->stream));
+        off += q.n;
+    }
+    const float* c[3] = {din, din + N, din + 2 * N};
+    const float* u[3] = {din + 3 * N, din + 4 * N, din + 5 * N};
+    const float* dg[3] = {din + 6 * N, din + 7 * N, din + 8 * N};
+    float* d[3] = {dout, dout + N, dout + 2 * N};
+    r = sdmm_ctx_guide_pdf_wavefront(g, N, c, u, dg, dmode, d, dout + 3 * N, dcomp, nullptr);
+    if (r) return r;
+    off = 0;
+    for (int i = 0; i < nreq; ++i) {
+        const sdmm_guide_host_req& q = reqs[i];
+        if (q.n == 0) continue;
+        HIP_TRY(hipMemcpy2DAsync(q.out, sizeof(float) * (size_t)q.out_stride, dout + off, dp,
+                                 sizeof(float) * (size_t)q.n, 4, hipMemcpyDeviceToHost, g->stream));
+        HIP_TRY(hipMemcpyAsync(q.comp, dcomp + off, sizeof(int32_t) * (size_t)q.n, hipMemcpyDeviceToHost, g->stream));
+        off += q.n;
+    }
+    HIP_TRY(hipStreamSynchronize(g->stream));
     return SDMM_OK;
 }
 

@@ -18,17 +18,21 @@
 
 #include <sys/stat.h>
 
+#include <algorithm>
 #include <cerrno>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <fstream>
 #include <memory>
 #include <condition_variable>
 #include <mutex>
 #include <sstream>
 #include <thread>
+#include <unordered_set>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -322,6 +326,180 @@ private:
     std::mutex mu_;
     std::condition_variable cv_;
     std::vector<sdmm_guide_ctx*> all_, free_;
+};
+
+// Concurrent workers' guided bounces gathered into few large wavefronts
+// (round 6).  The per-call cost of a guided wavefront (the leaf-major sort,
+// the candidate and full-K kernels' tails, each copy's DMA set-up) is paid
+// per CALL, so 16 workers each calling with its own tile run well below one
+// call over their union (tools/plugin_pattern_bench.py).
+//
+// `slots` batches, each with its own guide context and pinned staging in
+// batch layout (planes of stride cap).  serve() joins the open batch at the
+// next free offset and copies its query planes into the batch's staging
+// (host memcpy, the workers in parallel).  The first worker of a batch leads
+// it: it waits until the batch holds `target` queries, or every thread that
+// ever called serve() is inside serve() (nobody left to wait for), or
+// `wait_us` passed; then it closes the batch (later arrivals take the next
+// free one), waits for the members' copies and runs ONE
+// sdmm_ctx_guide_pdf_host_batch over the staging -- one H2D, one wavefront,
+// one D2H -- and wakes the members, who copy their outputs out.  Outputs are
+// bitwise those of per-worker calls (every query is independent).
+class GuideBatcher {
+public:
+    GuideBatcher(sdmm_stree* tree, int slots = 2, int64_t target = 1 << 18, int wait_us = 200)
+        : tree_(tree), target_(target > 0 ? target : 1), wait_(wait_us > 0 ? wait_us : 0) {
+        const int n = slots > 0 ? slots : 1;
+        for (int i = 0; i < n; ++i) batches_.emplace_back(new Batch());
+        for (auto& b : batches_) free_.push_back(b.get());
+    }
+    ~GuideBatcher() {
+        for (auto& b : batches_) {
+            if (b->ctx) sdmm_guide_ctx_destroy(b->ctx);
+            sdmm_pinned_free(b->stage);
+        }
+    }
+    GuideBatcher(const GuideBatcher&) = delete;
+    GuideBatcher& operator=(const GuideBatcher&) = delete;
+
+    // Blocks until r's outputs are in its host buffers; throws Error on failure.
+    void serve(const sdmm_guide_host_req& r) {
+        if (r.n <= 0) return;
+        std::unique_lock<std::mutex> lock(mu_);
+        callers_.insert(std::this_thread::get_id());
+        ++inside_;
+        // the open batch, if r fits; else close it and take a free one
+        if (open_ && open_->n + r.n > open_->cap) close(open_);
+        while (!open_) {
+            if (free_.empty()) {
+                cv_.wait(lock);
+                continue;
+            }
+            Batch* b = free_.back();
+            free_.pop_back();
+            b->reset();
+            if (b->cap < std::max(target_, r.n)) {
+                // (idle batch: nothing reads its staging)
+                const int64_t cap = std::max(target_, r.n) + std::max<int64_t>(r.n, 1 << 15);
+                lock.unlock();
+                sdmm_pinned_free(b->stage);
+                b->stage = nullptr;
+                b->cap = 0;
+                void* p = nullptr;
+                const int rc = sdmm_pinned_alloc((size_t)cap * kBytesPerQuery, &p);
+                lock.lock();
+                if (rc != SDMM_OK) {
+                    free_.push_back(b);
+                    --inside_;
+                    cv_.notify_all();
+                    throw Error(rc, std::string("GuideBatcher staging: ") + sdmm_last_error());
+                }
+                b->stage = (char*)p;
+                b->cap = cap;
+            }
+            if (open_) {                      // (another thread opened one meanwhile)
+                free_.push_back(b);
+                if (open_->n + r.n > open_->cap) close(open_);
+                continue;
+            }
+            open_ = b;
+        }
+        Batch* b = open_;
+        const int64_t off = b->n;
+        b->n += r.n;
+        const bool leader = b->members++ == 0;
+        ++b->copying;
+        if (b->n >= target_ || inside_ >= callers_.size()) close(b);
+        lock.unlock();
+        copy_in(*b, off, r);
+        lock.lock();
+        if (--b->copying == 0) cv_.notify_all();
+        if (leader) {
+            const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(wait_);
+            cv_.wait_until(lock, deadline, [&] { return b->closed; });
+            if (!b->closed) close(b);
+            cv_.wait(lock, [&] { return b->copying == 0; });
+            const int64_t N = b->n;
+            lock.unlock();
+            int rc = SDMM_OK;
+            std::string err;
+            if (!b->ctx) rc = sdmm_guide_ctx_create(tree_, nullptr, &b->ctx);
+            if (rc == SDMM_OK) {
+                const sdmm_guide_host_req all{N, b->in(), b->cap, b->mode(), b->out(), b->cap, b->comp()};
+                rc = sdmm_ctx_guide_pdf_host_batch(b->ctx, 1, &all);
+            }
+            if (rc != SDMM_OK) err = sdmm_last_error();
+            lock.lock();
+            b->rc = rc;
+            b->err = err;
+            b->done = true;
+            cv_.notify_all();
+        } else {
+            cv_.wait(lock, [&] { return b->done; });
+        }
+        const int rc = b->rc;
+        const std::string err = b->err;
+        lock.unlock();
+        if (rc == SDMM_OK) copy_out(*b, off, r);
+        lock.lock();
+        if (--b->members == 0) {              // the last one out frees the batch
+            free_.push_back(b);
+            cv_.notify_all();
+        }
+        --inside_;
+        lock.unlock();
+        if (rc != SDMM_OK) throw Error(rc, "sdmm_ctx_guide_pdf_host_batch (thread " + thread_tag() + "): " + err);
+    }
+
+private:
+    // per query: 9 + 4 float planes, the int32 component, the mode byte
+    static constexpr size_t kBytesPerQuery = 13 * sizeof(float) + sizeof(int32_t) + 1;
+    struct Batch {
+        sdmm_guide_ctx* ctx = nullptr;
+        char* stage = nullptr;   // in 9 x cap floats | out 4 x cap floats | comp cap int32 | mode cap bytes
+        int64_t cap = 0;
+        int64_t n = 0;
+        int members = 0, copying = 0;
+        bool closed = false, done = false;
+        int rc = SDMM_OK;
+        std::string err;
+        float* in() const { return (float*)stage; }
+        float* out() const { return (float*)stage + 9 * cap; }
+        int32_t* comp() const { return (int32_t*)((float*)stage + 13 * cap); }
+        uint8_t* mode() const { return (uint8_t*)((float*)stage + 14 * cap); }
+        void reset() {
+            n = 0;
+            members = copying = 0;
+            closed = done = false;
+            rc = SDMM_OK;
+            err.clear();
+        }
+    };
+    void close(Batch* b) {   // (mu_ held)
+        b->closed = true;
+        if (open_ == b) open_ = nullptr;
+        cv_.notify_all();
+    }
+    static void copy_in(const Batch& b, int64_t off, const sdmm_guide_host_req& r) {
+        for (int p = 0; p < 9; ++p)
+            std::memcpy(b.in() + p * b.cap + off, r.in + p * r.in_stride, sizeof(float) * (size_t)r.n);
+        std::memcpy(b.mode() + off, r.mode, (size_t)r.n);
+    }
+    static void copy_out(const Batch& b, int64_t off, const sdmm_guide_host_req& r) {
+        for (int p = 0; p < 4; ++p)
+            std::memcpy(r.out + p * r.out_stride, b.out() + p * b.cap + off, sizeof(float) * (size_t)r.n);
+        std::memcpy(r.comp, b.comp() + off, sizeof(int32_t) * (size_t)r.n);
+    }
+    sdmm_stree* tree_;
+    int64_t target_;
+    int wait_;
+    std::vector<std::unique_ptr<Batch>> batches_;
+    std::vector<Batch*> free_;
+    Batch* open_ = nullptr;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::unordered_set<std::thread::id> callers_;   // threads that ever called serve
+    size_t inside_ = 0;                              // threads inside serve now
 };
 
 // A wavefront of guided-bounce queries against one mixture: the batched form

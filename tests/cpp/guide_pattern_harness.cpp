@@ -5,16 +5,21 @@
 // published tree -- pinned H2D of the tile's query planes, one
 // sdmm_ctx_guide_pdf_wavefront, D2H of the outputs, a stream synchronise.
 //
-// usage: guide_pattern_harness model.asdmm queries.bin out.bin threads tile reps [contexts] [resident]
+// usage: guide_pattern_harness model.asdmm queries.bin out.bin threads tile reps [contexts] [resident|batch[:T:W]]
 //   contexts: guide contexts shared by the threads through
 //             sdmm_amd::GuideContextPool (0 or absent: one per thread)
 //   resident: the tiles' queries stay in device memory (no copies: the
 //             device-resident rate of the same calls, for comparison)
+//   batch   : the workers' bounces gathered by sdmm_amd::GuideBatcher into
+//             wavefronts of up to T queries (default 262144), a batch's
+//             leader waiting at most W us (default 200) for more; contexts =
+//             the batches in flight
 //   queries.bin: int64 n, float c[3][n], u[3][n], dgiven[3][n], uint8 mode[n]
 //   out.bin    : float d[3][n], pdf[n], int32 comp[n] (the last repetition)
 //   stdout     : one JSON line {threads, tile, reps, queries, seconds, queries_per_s}
 // Threads take tiles t = i, i + threads, ... (a fixed assignment, so the
 // pinned staging of a thread's tiles is filled once, outside the timing).
+// One untimed pass over the tiles precedes the timed `reps` passes.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -58,9 +63,19 @@ struct Worker {
 
 int main(int argc, char** argv) {
     if (argc < 7 || argc > 9)
-        die("usage: guide_pattern_harness model.asdmm queries.bin out.bin threads tile reps [contexts] [resident]");
+        die("usage: guide_pattern_harness model.asdmm queries.bin out.bin threads tile reps [contexts] "
+            "[resident|batch[:T:W]]");
     const int contexts_arg = argc >= 8 ? std::atoi(argv[7]) : 0;
-    const bool resident = argc == 9;
+    const std::string mode_arg = argc == 9 ? argv[8] : "";
+    const bool resident = mode_arg == "resident";
+    const bool batch = mode_arg.rfind("batch", 0) == 0;
+    if (!mode_arg.empty() && !resident && !batch) die("mode: resident or batch[:T:W]");
+    int64_t batch_target = 1 << 18;
+    int batch_wait = 200;
+    if (batch && mode_arg.size() > 5) {
+        if (std::sscanf(mode_arg.c_str(), "batch:%lld:%d", (long long*)&batch_target, &batch_wait) != 2)
+            die("batch:T:W expects two integers");
+    }
     const int T = std::atoi(argv[4]);
     const int64_t tile = std::atoll(argv[5]);
     const int reps = std::atoi(argv[6]);
@@ -108,51 +123,75 @@ int main(int argc, char** argv) {
 
     const int contexts = contexts_arg > 0 ? contexts_arg : T;
     sdmm_amd::GuideContextPool pool(tree, contexts);
-    std::atomic<int> ready{0};
-    std::atomic<bool> go{false};
+    sdmm_amd::GuideBatcher batcher(tree, contexts, batch_target, batch_wait);
     std::vector<std::string> err((size_t)T);
-    auto body = [&](int i) {
-        Worker& w = W[(size_t)i];
-        ++ready;
-        while (!go.load()) std::this_thread::yield();
-        for (int r = 0; r < reps && err[(size_t)i].empty(); ++r)
-            for (size_t j = 0; j < w.tiles.size(); ++j) {
-                const int64_t a = w.tiles[j], nq = std::min(a + tile, n) - a;
-                char* hb = w.h_in + (in_bytes + out_bytes) * j;
-                const sdmm_amd::GuideContextPool::Lease lease = pool.acquire();
-                const hipStream_t st = (hipStream_t)lease.stream();
-                float* din = (float*)(resident ? w.d_in + in_bytes * j : w.d_in);
-                if (!resident && hipMemcpyAsync(din, hb, in_bytes, hipMemcpyHostToDevice, st) != hipSuccess) {
-                    err[(size_t)i] = "upload";
-                    return;
-                }
-                const float* c[3] = {din, din + tile, din + 2 * tile};
-                const float* u[3] = {din + 3 * tile, din + 4 * tile, din + 5 * tile};
-                const float* dg[3] = {din + 6 * tile, din + 7 * tile, din + 8 * tile};
-                float* dout = (float*)w.d_out;
-                float* d[3] = {dout, dout + tile, dout + 2 * tile};
-                if (sdmm_ctx_guide_pdf_wavefront(lease.get(), nq, c, u, dg, (const uint8_t*)(din + 9 * tile), d,
-                                                 dout + 3 * tile, (int32_t*)(dout + 4 * tile), nullptr) != SDMM_OK) {
-                    err[(size_t)i] = std::string("sdmm_ctx_guide_pdf_wavefront: ") + sdmm_last_error();
-                    return;
-                }
-                if (!resident || r == reps - 1)
-                    if (hipMemcpyAsync(hb + in_bytes, w.d_out, out_bytes, hipMemcpyDeviceToHost, st) != hipSuccess) {
-                        err[(size_t)i] = "download";
+    // one pass of every thread over its tiles, `nrep` times; returns seconds
+    auto run = [&](int nrep) {
+        std::atomic<int> ready{0};
+        std::atomic<bool> go{false};
+        auto body = [&](int i) {
+            Worker& w = W[(size_t)i];
+            ++ready;
+            while (!go.load()) std::this_thread::yield();
+            for (int r = 0; r < nrep && err[(size_t)i].empty(); ++r)
+                for (size_t j = 0; j < w.tiles.size(); ++j) {
+                    const int64_t a = w.tiles[j], nq = std::min(a + tile, n) - a;
+                    char* hb = w.h_in + (in_bytes + out_bytes) * j;
+                    if (batch) {
+                        // the staging as the request: 9 planes (stride tile) + modes
+                        // in, 4 planes + components out
+                        const sdmm_guide_host_req rq{nq, (const float*)hb, tile, (const uint8_t*)(hb + 36 * tile),
+                                                     (float*)(hb + in_bytes), tile,
+                                                     (int32_t*)(hb + in_bytes + 16 * tile)};
+                        try {
+                            batcher.serve(rq);
+                        } catch (const std::exception& e) {
+                            err[(size_t)i] = e.what();
+                            return;
+                        }
+                        continue;
+                    }
+                    const sdmm_amd::GuideContextPool::Lease lease = pool.acquire();
+                    const hipStream_t st = (hipStream_t)lease.stream();
+                    float* din = (float*)(resident ? w.d_in + in_bytes * j : w.d_in);
+                    if (!resident && hipMemcpyAsync(din, hb, in_bytes, hipMemcpyHostToDevice, st) != hipSuccess) {
+                        err[(size_t)i] = "upload";
                         return;
                     }
-                if (hipStreamSynchronize(st) != hipSuccess) { err[(size_t)i] = "hipStreamSynchronize"; return; }
-            }
+                    const float* c[3] = {din, din + tile, din + 2 * tile};
+                    const float* u[3] = {din + 3 * tile, din + 4 * tile, din + 5 * tile};
+                    const float* dg[3] = {din + 6 * tile, din + 7 * tile, din + 8 * tile};
+                    float* dout = (float*)w.d_out;
+                    float* d[3] = {dout, dout + tile, dout + 2 * tile};
+                    if (sdmm_ctx_guide_pdf_wavefront(lease.get(), nq, c, u, dg, (const uint8_t*)(din + 9 * tile), d,
+                                                     dout + 3 * tile, (int32_t*)(dout + 4 * tile), nullptr) != SDMM_OK) {
+                        err[(size_t)i] = std::string("sdmm_ctx_guide_pdf_wavefront: ") + sdmm_last_error();
+                        return;
+                    }
+                    if (!resident || r == nrep - 1)
+                        if (hipMemcpyAsync(hb + in_bytes, w.d_out, out_bytes, hipMemcpyDeviceToHost, st) != hipSuccess) {
+                            err[(size_t)i] = "download";
+                            return;
+                        }
+                    if (hipStreamSynchronize(st) != hipSuccess) { err[(size_t)i] = "hipStreamSynchronize"; return; }
+                }
+        };
+        std::vector<std::thread> th;
+        for (int i = 0; i < T; ++i) th.emplace_back(body, i);
+        while (ready.load() < T) std::this_thread::yield();
+        const auto t0 = std::chrono::steady_clock::now();
+        go = true;
+        for (auto& x : th) x.join();
+        const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        for (int i = 0; i < T; ++i)
+            if (!err[(size_t)i].empty()) die("worker " + std::to_string(i) + ": " + err[(size_t)i]);
+        return sec;
     };
-    std::vector<std::thread> th;
-    for (int i = 0; i < T; ++i) th.emplace_back(body, i);
-    while (ready.load() < T) std::this_thread::yield();
-    const auto t0 = std::chrono::steady_clock::now();
-    go = true;
-    for (auto& x : th) x.join();
-    const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    for (int i = 0; i < T; ++i)
-        if (!err[(size_t)i].empty()) die("worker " + std::to_string(i) + ": " + err[(size_t)i]);
+    // an untimed pass first: the pool's contexts are created on first use and
+    // a context's scratch grows on its first calls (once per render pass in
+    // the plugin, where a pass serves a whole frame of tiles)
+    (void)run(1);
+    const double sec = run(reps);
 
     // the outputs in query order
     std::vector<float> d(3 * (size_t)n), pdf((size_t)n);
@@ -174,8 +213,10 @@ int main(int argc, char** argv) {
 
     const double total = (double)n * reps;
     std::printf("{\"threads\": %d, \"contexts\": %d, \"tile\": %lld, \"reps\": %d, \"queries\": %lld, "
-                "\"resident\": %s, \"seconds\": %.6f, \"queries_per_s\": %.1f}\n",
-                T, contexts, (long long)tile, reps, (long long)n, resident ? "true" : "false", sec, total / sec);
+                "\"resident\": %s, \"batch\": %s, \"batch_target\": %lld, \"batch_wait_us\": %d, "
+                "\"seconds\": %.6f, \"queries_per_s\": %.1f}\n",
+                T, contexts, (long long)tile, reps, (long long)n, resident ? "true" : "false", batch ? "true" : "false",
+                (long long)batch_target, batch_wait, sec, total / sec);
     for (Worker& w : W) {
         (void)hipHostFree(w.h_in);
         (void)hipFree(w.d_in);

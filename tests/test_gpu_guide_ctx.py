@@ -144,3 +144,45 @@ def test_ctx_unpublished_after_change(pkg, synth, gpu):
     with pytest.raises(pkg.SDMMError):
         ctx.guide_pdf(ct, ut, dt, mode)
     ctx.close()
+
+
+def test_ctx_host_batch_equals_one_wavefront(pkg, synth, gpu):
+    """sdmm_ctx_guide_pdf_host_batch: several requests' pinned host planes
+    (strides larger than their sizes, one empty request, ragged sizes) served
+    as one wavefront == one device call over the concatenated queries,
+    bitwise; pageable host buffers are refused (SDMM_E_INVALID)."""
+    import torch
+    b, t, mixes, leaves = _tree_and_leaf_mixtures(pkg, synth, 128)
+    sizes = [5000, 0, 12345, 77, 30000]
+    nq = sum(sizes)
+    c, u, d, ct, ut, dt = _queries(gpu, nq, 41, 0.0, 1.0)
+    mode_np = (np.random.default_rng(9).uniform(size=nq) < 0.5).astype(np.uint8)
+    mode = torch.from_numpy(mode_np).to(gpu)
+    t.bind(mixes)
+    dr, pr, cr = t.guide_pdf(None, ct, ut, dt, mode)
+    torch.cuda.synchronize()
+    t.publish()
+    ctx = pkg.GuideContext(t)
+    planes = np.concatenate([c, u, d]).astype(np.float32)          # (9, nq)
+    reqs, outs, off = [], [], 0
+    for n in sizes:
+        stride = n + 64
+        inp = torch.zeros((9, stride), dtype=torch.float32).pin_memory()
+        inp[:, :n] = torch.from_numpy(planes[:, off:off + n])
+        md = torch.from_numpy(mode_np[off:off + n].copy()).pin_memory()
+        out = torch.full((4, stride + 3), -7.0, dtype=torch.float32).pin_memory()
+        cp = torch.full((n,), -9, dtype=torch.int32).pin_memory()
+        reqs.append((inp, md, out, cp))
+        outs.append((off, n, out, cp))
+        off += n
+    ctx.guide_pdf_host(reqs)
+    for off, n, out, cp in outs:
+        for k in range(3):
+            np.testing.assert_array_equal(out[k, :n].numpy(), dr[k][off:off + n].cpu().numpy())
+        np.testing.assert_array_equal(out[3, :n].numpy(), pr[off:off + n].cpu().numpy())
+        np.testing.assert_array_equal(cp.numpy(), cr[off:off + n].cpu().numpy())
+        assert (out[:, n:].numpy() == -7.0).all()                  # nothing past the request
+    inp, md, out, cp = reqs[0]
+    with pytest.raises(pkg.SDMMError):
+        ctx.guide_pdf_host([(inp.clone(), md, out, cp)])           # pageable input planes
+    ctx.close()

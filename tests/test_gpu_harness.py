@@ -195,13 +195,17 @@ def test_guide_pattern_threads_equal_single_thread(pkg, synth, gpu, tmp_path, K)
     write_guide_queries(tmp_path / "q.bin", c, u, d, mode)
     exe = _build_guide_pattern(tmp_path)
     outs = []
-    for threads in (1, 8):
+    # one thread; 8 threads on their own contexts; 8 threads gathered by
+    # sdmm_amd::GuideBatcher (batches of up to 12 K queries, 2 in flight: the
+    # 4096-query tiles straddle batch boundaries and a ragged last tile)
+    for i, (threads, extra) in enumerate(((1, []), (8, []), (8, ["2", "batch:12288:300"]))):
         r = subprocess.run([str(exe), str(tmp_path / "model.asdmm"), str(tmp_path / "q.bin"),
-                            str(tmp_path / f"o{threads}.bin"), str(threads), "4096", "2"],
+                            str(tmp_path / f"o{i}.bin"), str(threads), "4096", "2"] + extra,
                            check=True, timeout=120, capture_output=True, text=True)
         assert '"queries_per_s"' in r.stdout
-        outs.append(np.fromfile(tmp_path / f"o{threads}.bin", np.uint8))
+        outs.append(np.fromfile(tmp_path / f"o{i}.bin", np.uint8))
     np.testing.assert_array_equal(outs[0], outs[1])
+    np.testing.assert_array_equal(outs[0], outs[2])
     o = outs[1]
     dd = o[:12 * nq].view(np.float32).reshape(3, nq)
     pp = o[12 * nq:16 * nq].view(np.float32)

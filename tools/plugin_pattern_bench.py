@@ -16,8 +16,9 @@ queries -- and times:
   * one thread, per tile size: the plugin pattern (pinned H2D + wavefront +
     D2H + synchronise) and the wavefront alone on device-resident planes;
   * the "threads_*" rows: C++ worker threads (tests/cpp/guide_pattern_harness.cpp)
-    sharing a pool of guide contexts, aggregate queries/s, outputs checked
-    bitwise against the one-thread run.
+    sharing a pool of guide contexts -- or, "_batch" rows, gathered into large
+    wavefronts by sdmm_amd::GuideBatcher -- aggregate queries/s, outputs
+    checked bitwise against the one-thread run.
 
     python tools/plugin_pattern_bench.py [--reps 20]
 """
@@ -39,6 +40,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--keep", default=None, help="write the model / queries / harness here and keep them")
+    ap.add_argument("--rows", default=None, help="comma list of threaded-row indices to run (default: all)")
+    ap.add_argument("--no-tiles", action="store_true", help="skip the one-thread Python tile rows")
     a = ap.parse_args()
     import torch
     from conftest import load_pkg
@@ -70,7 +73,7 @@ def main():
     out = {"queries_available": int(n_all), "K": 128, "scene": "Cornell Box 640x360, trained 16 spp",
            "pattern": "pinned H2D of 9 planes + mode, sdmm_guide_pdf_wavefront, D2H of 4 planes + comp, sync"}
     for T in (4096, 32768, 262144, min(n_all, 1 << 21)):
-        if T > n_all:
+        if T > n_all or a.no_tiles:
             continue
         h_in = torch.from_numpy(np.concatenate([c[:, :T], u[:, :T], dg[:, :T]]).copy()).pin_memory()
         h_mode = torch.from_numpy(mode[:T].copy()).pin_memory()
@@ -136,21 +139,23 @@ def main():
                     "-Wl,-rpath,/opt/rocm/lib", "-pthread", "-o", str(exe)], check=True)
     ref = None
     import os
-    # (threads, tile, contexts (0: one per thread), resident, extra env)
-    rows = [(1, 32768, 0, 0, {}), (1, 32768, 0, 1, {}), (4, 32768, 0, 0, {}), (16, 32768, 0, 0, {}),
-            (16, 32768, 0, 1, {}), (16, 32768, 4, 0, {}), (16, 32768, 4, 1, {}), (16, 32768, 8, 0, {}),
-            (16, 32768, 2, 0, {}), (16, 4096, 4, 0, {}), (16, 262144, 4, 0, {}),
-            (16, 32768, 8, 0, {"GPU_MAX_HW_QUEUES": "8"})]
-    for threads, T, nctx, res, extra in rows:
+    # (threads, tile, contexts (0: one per thread), mode ("", "resident", "batch[:T:W]"), extra env)
+    rows = [(1, 32768, 0, "", {}), (1, 32768, 0, "resident", {}), (4, 32768, 0, "", {}), (16, 32768, 4, "", {}),
+            (16, 32768, 4, "resident", {}), (16, 32768, 2, "batch", {}), (16, 32768, 3, "batch", {}),
+            (16, 32768, 4, "batch", {}), (16, 32768, 3, "batch:131072:200", {}), (16, 32768, 3, "batch:524288:400", {}),
+            (16, 4096, 3, "batch", {}), (16, 262144, 3, "batch", {}), (16, 4096, 4, "", {}), (16, 262144, 4, "", {})]
+    if a.rows:
+        rows = [rows[int(i)] for i in a.rows.split(",")]
+    for threads, T, nctx, mode, extra in rows:
         r = subprocess.run([str(exe), str(tmp / "model.asdmm"), str(tmp / "q.bin"), str(tmp / "o.bin"), str(threads),
-                            str(T), str(max(2, a.reps // 4)), str(nctx)] + (["resident"] if res else []),
+                            str(T), str(max(2, a.reps // 4)), str(nctx)] + ([mode] if mode else []),
                            check=True, timeout=300, capture_output=True, text=True, env=dict(os.environ, **extra))
         row = json.loads(r.stdout.strip().splitlines()[-1])
         got = np.fromfile(tmp / "o.bin", np.uint8)
         if ref is None:
             ref = got
         row["bitwise_equal_to_1_thread"] = bool(np.array_equal(got, ref))
-        key = f"threads_{threads}_ctx_{nctx or threads}_tile_{T}" + ("_resident" if res else "") + "".join(
+        key = f"threads_{threads}_ctx_{nctx or threads}_tile_{T}" + (f"_{mode}" if mode else "") + "".join(
             f"_{k}={v}" for k, v in extra.items())
         row["env"] = extra
         out[key] = row
