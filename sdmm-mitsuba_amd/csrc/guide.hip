@@ -847,6 +847,57 @@ __device__ __forceinline__ void bsort(uint64_t (&v)[S], int gl) {
     if constexpr (KS < W * S) bsort<W, S, 2 * KS>(v, gl);
 }
 
+// The kept prefix from sorted entries (build_full_wave_s): sorted element
+// p = 64 i + lane, its slot record written by its own lane, its term of the
+// kept mass (0 for an invalid conditional); accum in the selection order up
+// to the first slot that reaches the cutoff.  Returns true with lastIdx =
+// that slot + 1; false when every live entry was taken without reaching it
+// (lastIdx = n_live: the scan finds nothing left, K when every weight is live).
+template <int S2>
+__device__ __forceinline__ bool kept_prefix(const uint32_t (&key)[S2], const uint32_t (&idx)[S2], unsigned vmask,
+                                            float cutoff, const WaveLds& L, int lane, float& accum, int& lastIdx) {
+    int n_live = 0;   // entries with a weight (sorted first)
+    float term[S2];
+#pragma unroll
+    for (int i = 0; i < S2; ++i) {
+        n_live += __builtin_popcountll(__builtin_amdgcn_ballot_w64(key[i] != 0u));
+        const unsigned vm = (unsigned)__shfl((int)vmask, (int)(idx[i] & 63u));
+        const bool ok = (vm >> (idx[i] >> 6)) & 1u;
+        const float w = __builtin_bit_cast(float, key[i] - 1u);
+        term[i] = ok ? w : 0.0f;
+        if (key[i] != 0u) {
+            L.sl[64 * i + lane] = (int)idx[i] | (ok ? (int)0x80000000 : 0);
+            L.fw[64 * i + lane] = w;
+        }
+    }
+    // accum in the selection order, up to the first slot that reaches the
+    // cutoff; all live entries taken without reaching it: lastIdx = n_live
+    // (the scan finds nothing left), which is K when every weight is live
+    lastIdx = n_live;
+    bool done = false;
+#pragma unroll
+    for (int i = 0; i < S2; ++i) {
+        if (done) break;
+        const int n = min(64, n_live - 64 * i);
+        if (n <= 0) break;
+        // the terms through the broadcast stage (seq_sum); a padded
+        // lane's -0.0f cannot cross the cutoff (accum unchanged)
+        stage64(L.st, term[i], lane < n);
+        const float4* s4 = (const float4*)L.st;
+#pragma unroll 1
+        for (int p = 0; 4 * p < n && !done; ++p) {
+            const float4 v = s4[p];
+            const float e4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                accum += e4[e];
+                if (accum >= cutoff) { lastIdx = 64 * i + 4 * p + e + 1; done = true; break; }
+            }
+        }
+    }
+    return done;
+}
+
 // The kept prefix of query c's full-K conditional (above): slots
 // i < lastIdx in L.sl / L.fw (raw weight); returns lastIdx and accum.
 //
@@ -886,6 +937,75 @@ __device__ __forceinline__ int build_full_wave_s(const float* gp, int Kp, int K,
     accum = 0.0f;
     int lastIdx = K;   // the reference leaves it uninitialised if never reached
     if (!__any(nan_seen)) {
+        if constexpr (S >= 4) {
+            // K > 128: the kept prefix is usually far shorter than K (~90 of
+            // 512 at the Cornell K = 512 leaves).  The entries with key >= T,
+            // T the smallest 16-bit-prefix threshold leaving at most 128 of
+            // them, are exactly the first entries of the full sorted order
+            // (every other key is smaller), so sorting only them (two per
+            // lane) gives the same prefix, slots and accum -- when the
+            // cutoff is reached inside them; otherwise the full sort below.
+            uint32_t wk[S];
+#pragma unroll
+            for (int i = 0; i < S; ++i)
+                wk[i] = __builtin_signbit(wr[i]) ? 0u : __builtin_bit_cast(uint32_t, wr[i]) + 1u;
+            auto count_ge = [&](uint32_t t) __attribute__((always_inline)) {
+                int cnt = 0;
+#pragma unroll
+                for (int i = 0; i < S; ++i) cnt += __builtin_popcountll(__builtin_amdgcn_ballot_w64(wk[i] >= t));
+                return cnt;
+            };
+            constexpr int kSub = 128;
+            uint32_t T = 1u;
+            if (count_ge(1u) > kSub) {
+                // keys are at most 0x7F800001 (+inf + 1): prefix 0x7F81 leaves none
+                uint32_t lo = 0u, hi = 0x7F81u;
+                while (hi - lo > 1u) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (count_ge(mid << 16) <= kSub) hi = mid;
+                    else lo = mid;
+                }
+                T = hi << 16;
+            }
+            // their valid mass (any order) against the cutoff: a cheap test
+            // that the prefix ends inside them (kept_prefix decides exactly)
+            float part = 0.0f;
+#pragma unroll
+            for (int i = 0; i < S; ++i)
+                if (wk[i] >= T && ((vmask >> i) & 1u)) part += wr[i];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o);
+            if (part >= cutoff) {
+                uint64_t* sc = (uint64_t*)(((uintptr_t)L.se + 7u) & ~(uintptr_t)7u);   // (se: unused until prep)
+                int base = 0;
+#pragma unroll
+                for (int i = 0; i < S; ++i) {
+                    const bool in = wk[i] >= T;
+                    const uint64_t m = __builtin_amdgcn_ballot_w64(in);
+                    const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    if (in) sc[pos] = sel_key(wk[i], (uint32_t)(lane + 64 * i));
+                    base += __builtin_popcountll(m);
+                }
+                __builtin_amdgcn_wave_barrier();
+                uint64_t v2[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int q = lane + 64 * j;
+                    v2[j] = q < base ? sc[q] : sel_key(0u, (uint32_t)lane);   // padding: absent
+                }
+                __builtin_amdgcn_wave_barrier();
+                bsort<64, 2>(v2, lane);
+                uint32_t key2[2], idx2[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) { key2[j] = sel_wkey(v2[j]); idx2[j] = sel_idx(v2[j]); }
+                if (kept_prefix<2>(key2, idx2, vmask, cutoff, L, lane, accum, lastIdx)) {
+                    __syncthreads();
+                    return lastIdx;
+                }
+                accum = 0.0f;   // (the cutoff lies past them: the full sort)
+            }
+        }
         uint32_t key[S], idx[S];
         {
             uint64_t v[S];
@@ -898,47 +1018,7 @@ __device__ __forceinline__ int build_full_wave_s(const float* gp, int Kp, int K,
             for (int i = 0; i < S; ++i) { key[i] = sel_wkey(v[i]); idx[i] = sel_idx(v[i]); }
         }
         WCLK(9);
-        // sorted element p = 64 i + lane: its slot record, written by its own
-        // lane, and its term of the kept mass (0 for an invalid conditional)
-        int n_live = 0;   // entries with a weight (sorted first)
-        float term[S];
-#pragma unroll
-        for (int i = 0; i < S; ++i) {
-            n_live += __builtin_popcountll(__builtin_amdgcn_ballot_w64(key[i] != 0u));
-            const unsigned vm = (unsigned)__shfl((int)vmask, (int)(idx[i] & 63u));
-            const bool ok = (vm >> (idx[i] >> 6)) & 1u;
-            const float w = __builtin_bit_cast(float, key[i] - 1u);
-            term[i] = ok ? w : 0.0f;
-            if (key[i] != 0u) {
-                L.sl[64 * i + lane] = (int)idx[i] | (ok ? (int)0x80000000 : 0);
-                L.fw[64 * i + lane] = w;
-            }
-        }
-        // accum in the selection order, up to the first slot that reaches the
-        // cutoff; all live entries taken without reaching it: lastIdx = n_live
-        // (the scan finds nothing left), which is K when every weight is live
-        lastIdx = n_live;
-        bool done = false;
-#pragma unroll
-        for (int i = 0; i < S; ++i) {
-            if (done) break;
-            const int n = min(64, n_live - 64 * i);
-            if (n <= 0) break;
-            // the terms through the broadcast stage (seq_sum); a padded
-            // lane's -0.0f cannot cross the cutoff (accum unchanged)
-            stage64(L.st, term[i], lane < n);
-            const float4* s4 = (const float4*)L.st;
-#pragma unroll 1
-            for (int p = 0; 4 * p < n && !done; ++p) {
-                const float4 v = s4[p];
-                const float e4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    accum += e4[e];
-                    if (accum >= cutoff) { lastIdx = 64 * i + 4 * p + e + 1; done = true; break; }
-                }
-            }
-        }
+        kept_prefix<S>(key, idx, vmask, cutoff, L, lane, accum, lastIdx);
         __syncthreads();
         WCLK(10);
         return lastIdx;
