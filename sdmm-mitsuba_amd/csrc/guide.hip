@@ -2387,11 +2387,19 @@ __device__ __forceinline__ bool pair_eval(const float* condCov, const WaveLds& L
 // workgroup's scratch (written and re-read by the same wave: L2-resident) and
 // the CDF walk and the pdf read them; otherwise they are recomputed.
 // Returns false when the product is unusable (no pair / zero mass).
+// (diagnostic SDMM_PW_STOP = 4 / 1 / 2 / 3: return after the slot weights /
+// the preparation / pass 1 / pass 2 -- stage costs by difference; the outputs
+// are not the product's)
+#ifndef SDMM_PW_STOP
+#define SDMM_PW_STOP 0
+#endif
 template <bool PDF_ONLY>
 __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCov, const float c[3], int lastIdx,
                                     const WaveLds& L, const BsdfTab& bt, int b, const float F[9], const float* u,
                                     const float* dir_in, float choice, int lane, GuideConsts gc, QueryOut& o) {
+    if (SDMM_PW_STOP == 4) return true;
     wave_prepare_product(gp, Kp, c, lastIdx, L, bt, b, F, lane);
+    if (SDMM_PW_STOP == 1) return true;
     WCLK(3);
     // pair f = (kept slot f / M, nonzero lobe nzj[f % M]) -- the reference's
     // walk order with the zero-weight lobes (which it skips) left out
@@ -2424,6 +2432,7 @@ __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCo
     }
     __syncthreads();
     WCLK(4);
+    if (SDMM_PW_STOP == 2) return true;
     if (P == 0 || total == 0.0f) return false;
     float dir[3];
     o.comp = kCompPdfValid;
@@ -2488,6 +2497,7 @@ __device__ bool finish_product_wave(const float* gp, int Kp, const float* condCo
         dir[0] = dir_in[0]; dir[1] = dir_in[1]; dir[2] = dir_in[2];
     }
     WCLK(5);
+    if (SDMM_PW_STOP == 3) return true;
     // pass 3: the product mixture pdf at dir (a cached chunk's ten fields
     // loaded at once, coalesced; fetching the next chunk's ahead measured no
     // gain and 18 more spilled VGPRs)
