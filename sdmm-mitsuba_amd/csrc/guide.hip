@@ -49,7 +49,21 @@ __shared__ unsigned long long g_wlast;
 
 struct GuideConsts {
     float norm2, norm3;
+    // product path: a candidate-served query with more than this many pairs
+    // (kept slots x table lobes) goes to the one-wave path instead (the
+    // same bits; its pairs then run 64 at a time)
+    int route_pairs = 0x7fffffff;
 };
+// The threshold above: 160 pairs (Kitchen product, 8 lobes, capacity 40:
+// 8.75 -> 8.32 ms a call, profiles/round6_ab_route.log; the Cornell products'
+// candidate queries stay below it).  SDMM_PRODUCT_ROUTE_PAIRS overrides.
+static int product_route_pairs() {
+    static const int v = [] {
+        const char* e = std::getenv("SDMM_PRODUCT_ROUTE_PAIRS");
+        return e && *e ? std::atoi(e) : 160;
+    }();
+    return v;
+}
 
 // A Gaussian weight as the reference forms it: (float)((double)norm *
 // exp(-0.5 * (double)q)) (multivariate_normal.h:126, mvtn.h:359).  Round 5
@@ -2298,6 +2312,15 @@ __device__ __forceinline__ void product_invalid(const GuideIO& io, const Product
     if (pio.h) pio.h[q] = 1.0f;
 }
 
+// A candidate-served product query whose pair walk (kept slots x lobes) is
+// long goes to the one-wave path (gc.route_pairs; the results are the same)
+__device__ __forceinline__ bool routed_to_wave(int lastIdx, const ProductIO& pio, const BsdfTab& bt, int64_t q,
+                                               const GuideConsts& gc) {
+    if (lastIdx * bt.M <= gc.route_pairs) return false;
+    const int b = pio.material ? pio.material[q] : -1;
+    return b >= 0 && b < bt.B;
+}
+
 // Candidate path (as guide_cand_kernel: the kept prefix from the per-query LDS
 // list, bit-identical to the full-K selection); queries the list cannot serve
 // exactly go to fb_list for guide_product_wave_kernel.  perm: coherent order.
@@ -2321,7 +2344,7 @@ guide_product_cand_kernel(const float* __restrict__ gp, int Kp, int K, const flo
         product_invalid<PDF_ONLY>(io, pio, q);
         return;
     }
-    if (lastIdx < 0) {
+    if (lastIdx < 0 || routed_to_wave(lastIdx, pio, bt, q, gc)) {
         fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
         return;
     }
@@ -2630,7 +2653,7 @@ __device__ __forceinline__ bool serve_product_cand(const float* gp, int Kp, int 
         product_invalid<PDF_ONLY>(io, pio, q);
         return false;
     }
-    if (lastIdx < 0) {
+    if (lastIdx < 0 || routed_to_wave(lastIdx, pio, bt, q, gc)) {
         fb_list[atomicAdd(fb_count, 1)] = (int32_t)q;
         return true;
     }
@@ -3117,6 +3140,7 @@ hipError_t launch_guide_product(const float* gp, int Kp, int K, const float* con
     cap = (cap < 0) ? 0 : (cap > kGuideCap ? kGuideCap : cap);
     cap = cap < K ? cap : K;
     GuideConsts gc{norm2, norm3};
+    gc.route_pairs = product_route_pairs();
     const GuideIO io = make_io(c, u, dgiven, d, pdf, comp);
     ProductIO pio{};
     pio.material = material;
@@ -3185,6 +3209,7 @@ hipError_t launch_guide_product_tree(const void* nodes, const void* tab, const v
     cap = (cap < 0) ? 0 : (cap > kGuideCap ? kGuideCap : cap);
     cap = cap < kmax ? cap : kmax;
     GuideConsts gc{norm2, norm3};
+    gc.route_pairs = product_route_pairs();
     const bool pdf_only = dgiven != nullptr && choice == nullptr;
     // mixed: the sampling kernels also read the given directions (io.e);
     // the per-query mode comes from pio.choice, not io.pmode
