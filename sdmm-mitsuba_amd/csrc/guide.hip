@@ -2614,7 +2614,16 @@ __device__ void product_tail_wave(const float* gp, int Kp, const float* condCov,
 
 // The product path's full-K queries (listed by guide_product_cand_kernel):
 // one wave per query, grid-stride.
-constexpr int kProductWpe = 3;   // waves per SIMD the register budget is sized for (A/B: 2: 10.57, 3: 9.93, 4 (spills): 13.4 ms)
+// Waves per SIMD the one-wave product kernels' register budget is sized for.
+// Round 5 (A/B: 2: 10.57, 3: 9.93, 4 (spills): 13.4 ms a Kitchen call) kept 3
+// with ~65 VGPRs spilled; after round 6's serial-sum and partial-sort changes
+// 2 (256 VGPRs, no spill) wins: Kitchen 8.33 -> 7.59 ms a call, K = 512
+// Cornell product pass 62.9 -> 60.5 ms (4: 13.7 ms / 92 ms;
+// profiles/round6_ab_product_wpe.log).
+#ifndef SDMM_PRODUCT_WPE   // (A/B: tools/build_variant.sh)
+#define SDMM_PRODUCT_WPE 2
+#endif
+constexpr int kProductWpe = SDMM_PRODUCT_WPE;
 template <bool PDF_ONLY>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kProductWpe)))
 guide_product_wave_kernel(const float* __restrict__ gp, int Kp, int K, const float* __restrict__ condCov,
