@@ -645,6 +645,10 @@ def main():
         # on the device): the Torus meshes are LFS pointers in the snapshot, so
         # the same guided renderer runs over the Cornell Box with K=128 leaves
         out["cornell_k128"] = cornell_bench(pkg, dev, args, world, K=128, cpu=cpu)
+        # ... with the reference's default optimizeAsync = true
+        # (volpath_sdmm.cpp:65, :446-507): a training pass's EM runs beside
+        # the next pass's render, which guides with the model it has
+        out["cornell_k128_async"] = cornell_bench(pkg, dev, args, world, K=128, optimize_async=1)
         # sampleProduct (configs[4]'s learned-BSDF product sampling, sdmm_proc.cpp:327-392)
         # inside the full guided render: the Cornell BSDFs' synthesised diffuse lobes
         out["cornell_product"] = cornell_bench(pkg, dev, args, world, product=True, cpu=cpu)
