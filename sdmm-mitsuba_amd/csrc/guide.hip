@@ -1651,7 +1651,10 @@ __device__ __forceinline__ bool serve_full_group_g(const float* gp, int Kp, int 
 // 16-lane groups (round 4: 4-lane groups, 16 queries per wave, spilled and
 // lost: 13.1 against 12.0 ms per K = 128 guided pass)
 constexpr int kGroupLanes = 16;
-constexpr int kGroupWpe = 4;   // 128 VGPRs, no spill; K=128 guided pass 17.6 -> 15.2 ms (2: 189 VGPRs)
+#ifndef SDMM_GROUP_WPE   // (A/B: tools/build_variant.sh)
+#define SDMM_GROUP_WPE 4
+#endif
+constexpr int kGroupWpe = SDMM_GROUP_WPE;   // 128 VGPRs, no spill; K=128 guided pass 17.6 -> 15.2 ms (2: 189 VGPRs)
 // (4-lane groups with 16 or 32 slots: 256 VGPRs, 2 waves per SIMD, no spill)
 template <bool PDF_ONLY, bool TREE, int S>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(S >= 16 ? 2 : kGroupWpe)))
