@@ -377,15 +377,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    # (60: the E-step's clock transient -- per-launch times rise from ~163 to
-    # ~190 us over launches 5-25 after the EM warm-up, then settle at ~157-160
-    # by launch ~60 (profiles/round5_resp_series.json); the default times the
-    # sustained rate.  The driver's own --warmup overrides it.)
+    # (the E-step's clock transient: per-launch times rise from ~163 to ~190 us
+    # over launches 5-25 after the EM warm-up, fall to ~157-161 by launches
+    # 50-100 and settle at ~149-155 from launch ~200 on
+    # (profiles/round5_resp_series.json, profiles/round6_resp_series600.json:
+    # 600 launches); the defaults time the sustained rate.  The driver's own
+    # --warmup overrides --warmup, not --settle.)
     ap.add_argument("--warmup", type=int, default=60)
     # untimed E-step launches before the timed ones, at least: a driver run
     # with a small --warmup would otherwise time the clock transient; the
     # extra launches beyond --warmup are reported as "settle_launches"
-    ap.add_argument("--settle", type=int, default=60)
+    # (200 launches: ~32 ms)
+    ap.add_argument("--settle", type=int, default=200)
     ap.add_argument("--K", type=int, default=128)
     ap.add_argument("--N", type=int, default=1 << 20)
     ap.add_argument("--Q", type=int, default=1 << 20)
