@@ -217,6 +217,7 @@ public:
         m_tileSize = props.getInteger("wavefrontTile", 64);
         m_guideContexts = props.getInteger("guideContexts", 4);
         m_guideBatch = props.getInteger("guideBatch", 1 << 18);
+        m_guideBatchBelow = props.getInteger("guideBatchBelow", 1 << 14);
         if (m_rrDepth <= 0) Log(EError, "'rrDepth' must be set to a value greater than zero!");
         if (m_maxDepth <= 0 && m_maxDepth != -1)
             Log(EError, "'maxDepth' must be set to -1 (infinite) or a value greater than zero!");
@@ -236,6 +237,7 @@ public:
         m_tileSize = stream->readInt();
         m_guideContexts = stream->readInt();
         m_guideBatch = stream->readInt();
+        m_guideBatchBelow = stream->readInt();
     }
 
     ~SDMMAmdPathTracer() {
@@ -258,6 +260,7 @@ public:
         stream->writeInt(m_tileSize);
         stream->writeInt(m_guideContexts);
         stream->writeInt(m_guideBatch);
+        stream->writeInt(m_guideBatchBelow);
     }
 
     bool preprocess(const Scene* scene, RenderQueue* queue, const RenderJob* job, int sceneResID, int sensorResID,
@@ -395,7 +398,8 @@ private:
         // then each worker guides through its own context, with no lock
         // then each bounce leases a guide context (stream + scratch) from a
         // pool shared by the workers (sdmm_amd::GuideContextPool)
-        // -- or, for the plain (non-product) bounce with guideBatch > 0, the
+        // -- or, for a plain (non-product) bounce of fewer than guideBatchBelow
+        // queries with guideBatch > 0 (late bounces, small tiles), the
         // workers' bounces are gathered into shared wavefronts of up to
         // guideBatch queries (sdmm_amd::GuideBatcher, two in flight)
         // (both kept across passes: the tree object is the model's for its
@@ -771,7 +775,7 @@ private:
     // context and its stream -- the workers run at once, as the reference's
     // render threads do (sdmm_proc.cpp:1086-1106).
     void guideWavefront(Staging& st, int64_t n, int64_t nq) {
-        if (m_batcher && !st.h_mat) {
+        if (m_batcher && !st.h_mat && nq < m_guideBatchBelow) {
             // the staging is the request (pinned planes of stride n); the
             // batch's leader copies, launches and synchronises
             const sdmm_guide_host_req rq{nq, st.h_in, n, st.h_mode, st.h_out, n, st.h_comp};
@@ -838,6 +842,11 @@ private:
     int m_guideContexts = 4;          // guide contexts shared by the workers (one per hardware queue)
     sdmm_amd::GuideContextPool* m_ctxPool = nullptr;   // the pass's (renderPass)
     int m_guideBatch = 1 << 18;       // queries per gathered wavefront (0: each worker calls alone)
+    // bounces with fewer queries than this are gathered, larger ones go
+    // through the context pool (16 x 32 K-query tiles: contexts 298 M/s,
+    // batcher 212-240; 4 K-query tiles: batcher 85 M/s, contexts 14;
+    // profiles/round6_plugin_pattern_final.json)
+    int m_guideBatchBelow = 1 << 14;
     sdmm_amd::GuideBatcher* m_batcher = nullptr;       // the pass's (renderPass)
     std::unique_ptr<sdmm_amd::GuideContextPool> m_pool;   // created at the first guided pass
     std::unique_ptr<sdmm_amd::GuideBatcher> m_batch;
